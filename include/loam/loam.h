@@ -1,0 +1,143 @@
+/* loam.h — C-ABI of the MI355X LOAM scan-matching engine (libloam_hip.so).
+ *
+ * Drop-in for the compute bodies of the four ROS nodes of the reference
+ * (/root/reference = Maofei/loam_velodyne-1).  Each entry point replaces one node callback:
+ *
+ *   loam_scan_registration  <- laserCloudHandler        src/scanRegistration.cpp:211-636
+ *   loam_imu                <- imuHandler               src/scanRegistration.cpp:638-660 (§8f, not yet)
+ *   loam_odometry           <- laserOdometry loop body  src/laserOdometry.cpp:413-931
+ *                              (inputs = what handlers :275-354 store)
+ *   loam_mapping            <- laserMapping loop body   src/laserMapping.cpp:411-1097
+ *                              (inputs = what handlers :274-321 store)
+ *   loam_maintenance        <- transformMaintenance     src/transformMaintenance.cpp:147-203
+ *   loam_batch_*            <- config 4 of BASELINE.json (independent problems, no reference
+ *                              equivalent: one problem = the bodies above composed)
+ *
+ * Conventions: no C++ types cross the boundary; all host storage is caller-owned and never
+ * retained after a call; a context owns its device memory, one HIP device and one stream; a
+ * context is not thread-safe, distinct contexts may run concurrently.  Every function returns
+ * LOAM_OK (0) or a negative LOAM_E_* code; loam_last_error() describes the last failure on the
+ * calling thread.  LOAM_E_CAPACITY writes the required size back into the cloud's `count`.
+ */
+#ifndef LOAM_LOAM_H
+#define LOAM_LOAM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LOAM_OK 0
+#define LOAM_E_INVAL (-1)
+#define LOAM_E_CAPACITY (-2)
+#define LOAM_E_HIP (-3)
+#define LOAM_E_NOT_READY (-4) /* scan registration inside systemDelay (Q1) */
+#define LOAM_E_NOMEM (-5)
+
+/* published-flag bits of loam_odometry (the topics laserOdometry publishes on this call) */
+#define LOAM_PUB_POSE 1   /* /laser_odom_to_init  (src/laserOdometry.cpp:858-873) */
+#define LOAM_PUB_CLOUDS 2 /* /laser_cloud_corner_last + /laser_cloud_surf_last (:439-449, :913-923) */
+#define LOAM_PUB_FULL 4   /* /velodyne_cloud_3    (:925-929) */
+
+/* ring-ID models for scan registration */
+#define LOAM_RING_VLP16 0  /* reference: round(angle) -> r>0 ? r : r+(N-1)  src/scanRegistration.cpp:248-260 */
+#define LOAM_RING_LINEAR 1 /* bk HDL-64E hint: int((angle-lo)/step + 0.5f), bk src/scanRegistration.cpp:268-275 */
+
+/* PCL PointXYZI payload in a 16-byte record (PCL's in-memory PointXYZI is 32 B with padding).
+ * intensity = ring + 0.1*relTime out of scan registration (src/scanRegistration.cpp:283-284),
+ * the integer ring after TransformToEnd (src/laserOdometry.cpp:193). */
+typedef struct { float x, y, z, intensity; } loam_point;
+
+/* the reference's float transform[6] layout: (rx, ry, rz, tx, ty, tz) in the camera frame
+ * (x left, y up, z forward), e.g. transformSum src/laserOdometry.cpp:94 */
+typedef struct { float rx, ry, rz, tx, ty, tz; } loam_pose6;
+
+/* caller-owned input cloud; x, y, z floats at byte offsets 0, 4, 8 of each record
+ * (accepts 16-B PointXYZ/loam_point and 32-B PointXYZI / velodyne XYZIR records) */
+typedef struct { const void *data; uint32_t count; uint32_t stride_bytes; } loam_cloud_in;
+
+/* caller-owned output storage; count = points written (or required, on LOAM_E_CAPACITY) */
+typedef struct { loam_point *pts; uint32_t count; uint32_t capacity; } loam_cloud_out;
+
+/* the six topics scanRegistration publishes (src/scanRegistration.cpp:584-635) */
+typedef struct {
+  loam_cloud_out full;       /* /velodyne_cloud_2 */
+  loam_cloud_out sharp;      /* /laser_cloud_sharp */
+  loam_cloud_out less_sharp; /* /laser_cloud_less_sharp */
+  loam_cloud_out flat;       /* /laser_cloud_flat */
+  loam_cloud_out less_flat;  /* /laser_cloud_less_flat */
+  float imu_trans[12];       /* /imu_trans: start RPY, cur RPY, shift, velo (zeros without IMU) */
+} loam_features;
+
+typedef struct {
+  uint32_t n_rings;        /* N_SCANS (16)                                  scanRegistration.cpp:61 */
+  uint32_t ring_model;     /* LOAM_RING_VLP16 | LOAM_RING_LINEAR */
+  float ring_lo_deg;       /* LOAM_RING_LINEAR lower bound (-24.8) */
+  float ring_hi_deg;       /* LOAM_RING_LINEAR upper bound (2.0) */
+  uint32_t system_delay;   /* 20                                            scanRegistration.cpp:57 */
+  uint32_t max_points;     /* per-sweep capacity (40000 in the reference)   scanRegistration.cpp:63 */
+  uint32_t od_max_iter;    /* 25                                            laserOdometry.cpp:470 */
+  uint32_t mp_max_iter;    /* 10                                            laserMapping.cpp:710 */
+  uint32_t skip_frame_num; /* 1                                             laserOdometry.cpp:51 */
+  uint32_t map_capacity;   /* device map-store capacity in points (per map instance) */
+} loam_config;
+
+/* per-call counters; feed the algorithmic-byte formula of SURVEY.md §8(d) */
+typedef struct {
+  uint64_t n_raw, n_ring;                       /* SR input points, ring-sorted points */
+  uint64_t n_sharp, n_less_sharp, n_flat, n_less_flat;
+  uint64_t od_iters, od_assoc_rounds, od_rows_sum, od_corner_last, od_surf_last, od_queries;
+  uint64_t mp_iters, mp_rows_sum, mp_stack, mp_map_points, mp_map_valid_points;
+  uint64_t bytes_sr, bytes_od, bytes_mp;        /* algorithmic bytes, SURVEY.md §8(d) */
+  double ms_sr, ms_od, ms_mp;                   /* device time per stage (HIP events) */
+} loam_stats;
+
+typedef struct loam_ctx loam_ctx;
+
+void loam_config_default(loam_config *cfg);               /* reference constants (VLP-16) */
+int loam_create(loam_ctx **out, const loam_config *cfg, int device);
+void loam_destroy(loam_ctx *ctx);
+const char *loam_last_error(void);
+
+/* = laserCloudHandler.  Returns LOAM_E_NOT_READY for the first system_delay sweeps (Q1). */
+int loam_scan_registration(loam_ctx *ctx, double stamp, loam_cloud_in raw, loam_features *out);
+
+/* = laserOdometry loop body for one synchronised set of the six scanRegistration topics.
+ * sum_out receives transformSum when LOAM_PUB_POSE is set; the three clouds are written when
+ * their flag is set in *published. */
+int loam_odometry(loam_ctx *ctx, double stamp, const loam_features *in, loam_pose6 *sum_out,
+                  loam_cloud_out *corner_last, loam_cloud_out *surf_last, loam_cloud_out *full_end,
+                  int *published);
+
+/* = laserMapping loop body for one synchronised (corner_last, surf_last, full, odometry) set.
+ * odom_sum goes through the reference's nav_msgs quaternion round trip.  aft / bef are
+ * transformAftMapped / transformBefMapped (the Bef pose the reference smuggles in the twist
+ * fields, src/laserMapping.cpp:1082-1087); registered = full cloud in the map frame. */
+int loam_mapping(loam_ctx *ctx, double stamp, const loam_pose6 *odom_sum,
+                 const loam_cloud_out *corner_last, const loam_cloud_out *surf_last,
+                 const loam_cloud_out *full_end, loam_pose6 *aft, loam_pose6 *bef,
+                 loam_cloud_out *registered);
+
+/* = transformMaintenance laserOdometryHandler with the last odomAftMappedHandler state.
+ * Pure host function (scalar pose algebra, no kernel). */
+int loam_maintenance(const loam_pose6 *odom_sum, const loam_pose6 *bef, const loam_pose6 *aft,
+                     loam_pose6 *integrated);
+
+/* ---- batched independent problems (config 4) ----
+ * problem i = scan registration of (prev_i, cur_i), odometry seeded from prev_i and solved on
+ * cur_i, mapping of prev_i into an empty map then solved for cur_i.
+ * upload copies the host sweeps into device memory; run executes every problem on the device
+ * with all inputs resident in HBM; download copies the poses back. */
+int loam_batch_upload(loam_ctx *ctx, uint32_t n, const loam_cloud_in *prev,
+                      const loam_cloud_in *cur);
+int loam_batch_run(loam_ctx *ctx);
+int loam_batch_download(loam_ctx *ctx, loam_pose6 *od_sum, loam_pose6 *aft, loam_stats *stats);
+
+/* last-call statistics of a context (stage device times, counts, algorithmic bytes) */
+int loam_get_stats(loam_ctx *ctx, loam_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LOAM_LOAM_H */
