@@ -1,0 +1,224 @@
+"""ctypes binding of libloam_hip.so, the MI355X LOAM scan-matching engine (C-ABI in
+include/loam/loam.h).  One `Engine` = one loam_ctx = the four reference ROS nodes' compute bodies
+on one GPU:
+
+    scan_registration(raw)          laserCloudHandler    src/scanRegistration.cpp:211-636
+    odometry(features)              laserOdometry body   src/laserOdometry.cpp:413-931
+    mapping(pose, corner, surf, full) laserMapping body  src/laserMapping.cpp:411-1097
+    maintenance(sum, bef, aft)      transformMaintenance src/transformMaintenance.cpp:147-203
+    batch_*                         config 4 (independent problems)
+
+There is no CPU path: without a GPU (or without the built library) every call raises.
+The package directory name contains '-', so import it with
+importlib.import_module("loam_velodyne-1_amd")."""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libloam_hip.so")
+_LIB = None
+
+LOAM_OK, LOAM_E_INVAL, LOAM_E_CAPACITY, LOAM_E_HIP, LOAM_E_NOT_READY, LOAM_E_NOMEM = 0, -1, -2, -3, -4, -5
+PUB_POSE, PUB_CLOUDS, PUB_FULL = 1, 2, 4
+RING_VLP16, RING_LINEAR = 0, 1
+
+
+class LoamError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"loam error {code}: {msg}")
+        self.code = code
+
+
+class CloudIn(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("count", ctypes.c_uint32), ("stride_bytes", ctypes.c_uint32)]
+
+
+class CloudOut(ctypes.Structure):
+    _fields_ = [("pts", ctypes.c_void_p), ("count", ctypes.c_uint32), ("capacity", ctypes.c_uint32)]
+
+
+class Features(ctypes.Structure):
+    _fields_ = [("full", CloudOut), ("sharp", CloudOut), ("less_sharp", CloudOut),
+                ("flat", CloudOut), ("less_flat", CloudOut), ("imu_trans", ctypes.c_float * 12)]
+
+
+class Pose6(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_float) for n in ("rx", "ry", "rz", "tx", "ty", "tz")]
+
+    def arr(self):
+        return np.array([self.rx, self.ry, self.rz, self.tx, self.ty, self.tz], np.float32)
+
+    @staticmethod
+    def of(a):
+        p = Pose6()
+        p.rx, p.ry, p.rz, p.tx, p.ty, p.tz = [float(v) for v in a]
+        return p
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("n_rings", ctypes.c_uint32), ("ring_model", ctypes.c_uint32),
+                ("ring_lo_deg", ctypes.c_float), ("ring_hi_deg", ctypes.c_float),
+                ("system_delay", ctypes.c_uint32), ("max_points", ctypes.c_uint32),
+                ("od_max_iter", ctypes.c_uint32), ("mp_max_iter", ctypes.c_uint32),
+                ("skip_frame_num", ctypes.c_uint32), ("map_capacity", ctypes.c_uint32)]
+
+
+STAT_U64 = ("n_raw", "n_ring", "n_sharp", "n_less_sharp", "n_flat", "n_less_flat",
+            "od_iters", "od_assoc_rounds", "od_rows_sum", "od_corner_last", "od_surf_last", "od_queries",
+            "mp_iters", "mp_rows_sum", "mp_stack", "mp_map_points", "mp_map_valid_points",
+            "bytes_sr", "bytes_od", "bytes_mp")
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in STAT_U64] + \
+               [(n, ctypes.c_double) for n in ("ms_sr", "ms_od", "ms_mp")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+EXPORTS = ("loam_config_default", "loam_create", "loam_destroy", "loam_last_error",
+           "loam_scan_registration", "loam_odometry", "loam_mapping", "loam_maintenance",
+           "loam_batch_upload", "loam_batch_run", "loam_batch_download", "loam_get_stats")
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is not built (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        P, PP = ctypes.POINTER, ctypes.c_void_p
+        L.loam_config_default.argtypes = [P(Config)]
+        L.loam_create.argtypes = [P(PP), P(Config), ctypes.c_int]
+        L.loam_destroy.argtypes = [PP]
+        L.loam_last_error.restype = ctypes.c_char_p
+        L.loam_scan_registration.argtypes = [PP, ctypes.c_double, CloudIn, P(Features)]
+        L.loam_odometry.argtypes = [PP, ctypes.c_double, P(Features), P(Pose6), P(CloudOut), P(CloudOut),
+                                    P(CloudOut), P(ctypes.c_int)]
+        L.loam_mapping.argtypes = [PP, ctypes.c_double, P(Pose6), P(CloudOut), P(CloudOut), P(CloudOut),
+                                   P(Pose6), P(Pose6), P(CloudOut)]
+        L.loam_maintenance.argtypes = [P(Pose6)] * 4
+        L.loam_batch_upload.argtypes = [PP, ctypes.c_uint32, P(CloudIn), P(CloudIn)]
+        L.loam_batch_run.argtypes = [PP]
+        L.loam_batch_download.argtypes = [PP, P(Pose6), P(Pose6), P(Stats)]
+        L.loam_get_stats.argtypes = [PP, P(Stats)]
+        _LIB = L
+    return _LIB
+
+
+def _check(rc):
+    if rc != LOAM_OK:
+        raise LoamError(rc, lib().loam_last_error().decode())
+    return rc
+
+
+def default_config(**kw):
+    c = Config()
+    lib().loam_config_default(ctypes.byref(c))
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def _cloud_in(a):
+    a = np.ascontiguousarray(a, np.float32)
+    return CloudIn(a.ctypes.data, a.shape[0], a.shape[1] * 4), a
+
+
+class _Out:
+    def __init__(self, cap):
+        self.arr = np.zeros((max(cap, 1), 4), np.float32)
+        self.c = CloudOut(self.arr.ctypes.data, 0, cap)
+
+    def get(self, count=None):
+        return self.arr[:self.c.count if count is None else count].copy()
+
+
+def _cloud_ref(a):
+    a = np.ascontiguousarray(a, np.float32).reshape(-1, 4)
+    return CloudOut(a.ctypes.data if a.shape[0] else None, a.shape[0], a.shape[0]), a
+
+
+class Engine:
+    def __init__(self, cfg=None, device=0, cap=None):
+        self.cfg = cfg or default_config()
+        self.h = ctypes.c_void_p()
+        _check(lib().loam_create(ctypes.byref(self.h), ctypes.byref(self.cfg), device))
+        self.cap = cap or int(self.cfg.max_points)
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().loam_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+    def stats(self):
+        s = Stats()
+        _check(lib().loam_get_stats(self.h, ctypes.byref(s)))
+        return s.as_dict()
+
+    # --- the four node bodies
+    def scan_registration(self, raw, stamp=0.0):
+        ci, keep = _cloud_in(raw)
+        outs = [_Out(self.cap) for _ in range(5)]
+        f = Features(*[o.c for o in outs])
+        rc = lib().loam_scan_registration(self.h, stamp, ci, ctypes.byref(f))
+        if rc == LOAM_E_NOT_READY:
+            return rc, None
+        _check(rc)
+        names = ["full", "sharp", "less_sharp", "flat", "less_flat"]
+        return 0, {n: o.get(getattr(f, n).count) for n, o in zip(names, outs)}
+
+    def odometry(self, feats, stamp=0.0):
+        refs = [_cloud_ref(feats[n]) for n in ("full", "sharp", "less_sharp", "flat", "less_flat")]
+        f = Features(*[r[0] for r in refs])
+        pose = Pose6()
+        outs = [_Out(self.cap) for _ in range(3)]
+        pub = ctypes.c_int(0)
+        _check(lib().loam_odometry(self.h, stamp, ctypes.byref(f), ctypes.byref(pose), ctypes.byref(outs[0].c),
+                                   ctypes.byref(outs[1].c), ctypes.byref(outs[2].c), ctypes.byref(pub)))
+        return pub.value, pose.arr(), outs[0].get(), outs[1].get(), outs[2].get()
+
+    def mapping(self, odom_sum, corner, surf, full, stamp=0.0):
+        refs = [_cloud_ref(a) for a in (corner, surf, full)]
+        aft, bef = Pose6(), Pose6()
+        reg = _Out(max(int(np.asarray(full).shape[0]), 1))
+        _check(lib().loam_mapping(self.h, stamp, ctypes.byref(Pose6.of(odom_sum)), ctypes.byref(refs[0][0]),
+                                  ctypes.byref(refs[1][0]), ctypes.byref(refs[2][0]), ctypes.byref(aft),
+                                  ctypes.byref(bef), ctypes.byref(reg.c)))
+        return aft.arr(), bef.arr(), reg.get()
+
+    # --- config 4
+    def batch_upload(self, prevs, curs):
+        n = len(prevs)
+        keep = []
+        a = (CloudIn * n)()
+        b = (CloudIn * n)()
+        for i in range(n):
+            a[i], k1 = _cloud_in(prevs[i])
+            b[i], k2 = _cloud_in(curs[i])
+            keep += [k1, k2]
+        _check(lib().loam_batch_upload(self.h, n, a, b))
+        self.n = n
+
+    def batch_run(self):
+        _check(lib().loam_batch_run(self.h))
+
+    def batch_download(self):
+        od = (Pose6 * self.n)()
+        aft = (Pose6 * self.n)()
+        st = Stats()
+        _check(lib().loam_batch_download(self.h, od, aft, ctypes.byref(st)))
+        return (np.array([p.arr() for p in od]), np.array([p.arr() for p in aft]), st.as_dict())
+
+
+def maintenance(odom_sum, bef, aft):
+    out = Pose6()
+    _check(lib().loam_maintenance(ctypes.byref(Pose6.of(odom_sum)), ctypes.byref(Pose6.of(bef)),
+                                  ctypes.byref(Pose6.of(aft)), ctypes.byref(out)))
+    return out.arr()

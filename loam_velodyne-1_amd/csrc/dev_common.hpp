@@ -1,0 +1,389 @@
+// Device-side building blocks shared by the SR / OD / MP kernels (gfx950, wave64).
+//
+// Numerics: every kernel is compiled with -ffp-contract=off so that float expressions round
+// exactly like the reference build (x86-64 SSE, no FMA).  The reference's unqualified libm calls
+// bind the C double functions (ROS Indigo toolchain, see oracle/oracle.cpp header), so the helpers
+// below evaluate trig in double and callers round once on assignment to float, mirroring
+// src/laserOdometry.cpp / src/laserMapping.cpp; scanRegistration's `using std::atan2` calls are
+// float (src/scanRegistration.cpp:51-53).
+#ifndef LOAM_DEV_COMMON_HPP
+#define LOAM_DEV_COMMON_HPP
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LOAM_HD __host__ __device__ __forceinline__
+#define LOAM_D __device__ __forceinline__
+
+namespace loamdev {
+
+constexpr int kWave = 64;
+
+LOAM_HD double D(float x) { return (double)x; }
+LOAM_HD double dsin(float x) { return sin((double)x); }
+LOAM_HD double dcos(float x) { return cos((double)x); }
+LOAM_HD double rad2deg(double r) { return r * 180.0 / M_PI; }
+
+// squared distance in the reference's float order (dx*dx + dy*dy) + dz*dz
+LOAM_HD float sqdist(float ax, float ay, float az, float bx, float by, float bz) {
+  float dx = ax - bx, dy = ay - by, dz = az - bz;
+  return dx * dx + dy * dy + dz * dz;
+}
+
+// ------------------------------------------------------------------ wave primitives
+LOAM_D int lane_id() { return __lane_id(); }
+LOAM_D uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+template <typename T>
+LOAM_D T wave_sum(T v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+LOAM_D int wave_min_i(int v) {
+  for (int o = 32; o > 0; o >>= 1) { int w = __shfl_xor(v, o, 64); v = w < v ? w : v; }
+  return v;
+}
+LOAM_D int wave_max_i(int v) {
+  for (int o = 32; o > 0; o >>= 1) { int w = __shfl_xor(v, o, 64); v = w > v ? w : v; }
+  return v;
+}
+LOAM_D uint64_t wave_min_u64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t w = __shfl_xor(v, o, 64);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+LOAM_D float wave_min_f(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+LOAM_D float wave_max_f(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// inclusive prefix sum across the wave
+LOAM_D int wave_incl_scan(int v) {
+  for (int o = 1; o < 64; o <<= 1) {
+    int w = __shfl_up(v, o, 64);
+    if (lane_id() >= o) v += w;
+  }
+  return v;
+}
+
+// ------------------------------------------------------------------ block primitives
+// exclusive scan of one int per thread over a block of NT threads; returns the block total.
+// scratch: at least NT/64 ints of LDS.
+template <int NT>
+LOAM_D int block_excl_scan(int v, int* scratch, int& total) {
+  const int nw = NT / 64, w = threadIdx.x >> 6, l = lane_id();
+  int incl = wave_incl_scan(v);
+  if (l == 63) scratch[w] = incl;
+  __syncthreads();
+  if (w == 0) {
+    int s = l < nw ? scratch[l] : 0;
+    int si = wave_incl_scan(s);
+    if (l < nw) scratch[l] = si - s;
+    if (l == nw - 1) scratch[nw] = si;
+  }
+  __syncthreads();
+  int r = incl - v + scratch[w];
+  total = scratch[nw];
+  __syncthreads();
+  return r;
+}
+
+template <int NT, typename T, typename Op>
+LOAM_D T block_reduce(T v, T* scratch, Op op) {
+  const int nw = NT / 64, w = threadIdx.x >> 6, l = lane_id();
+  for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o, 64));
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  T r = scratch[0];
+  for (int i = 1; i < nw; ++i) r = op(r, scratch[i]);
+  __syncthreads();
+  return r;
+}
+
+// ------------------------------------------------------------------ LDS bitonic sort (ascending)
+// sorts n64 = power of two 64-bit keys in LDS with the whole block; pad with ~0ull.
+template <int NT>
+LOAM_D void block_bitonic_sort(uint64_t* k, int n64) {
+  for (int size = 2; size <= n64; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < (n64 >> 1); t += NT) {
+        int lo = 2 * t - (t & (stride - 1));
+        int hi = lo + stride;
+        bool up = ((lo & size) == 0);
+        uint64_t a = k[lo], b = k[hi];
+        if ((a > b) == up) { k[lo] = b; k[hi] = a; }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+LOAM_HD int next_pow2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+// order-preserving float -> uint32 for non-negative floats (curvature, squared distances)
+LOAM_HD uint32_t fkey(float f) { return __float_as_uint(f); }
+
+// ------------------------------------------------------------------ spatial hash
+LOAM_HD uint32_t cell_hash(int ix, int iy, int iz) {
+  uint32_t h = (uint32_t)ix * 73856093u ^ (uint32_t)iy * 19349663u ^ (uint32_t)iz * 83492791u;
+  h ^= h >> 16;
+  h *= 0x7feb352du;
+  h ^= h >> 15;
+  return h;
+}
+LOAM_HD int cell_of(float v, float inv_h) { return (int)floorf(v * inv_h); }
+
+}  // namespace loamdev
+
+// ------------------------------------------------------------------ small dense solvers
+// Written for the engine from the published algorithms of the calls the reference makes
+// (cv::solve DECOMP_QR, cv::eigen Jacobi, cv::Mat::inv LU, float gemm with double accumulation;
+// SURVEY.md appendix A2).  Executed by one lane; float arithmetic in the documented order.
+namespace loamla {
+
+LOAM_HD float sgn1(float x) { return x >= 0.0f ? 1.0f : -1.0f; }
+
+// Householder least squares, m x n (m >= n <= 6), row-major A (m*n), b (m); A,b destroyed.
+// ws: >= 14 floats of scratch (registers for small per-lane solves, LDS for the 6x6 one)
+LOAM_HD bool qr_solve(float* A, float* b, int m, int n, float* x, float* ws) {
+  float* v = ws;
+  float* h = ws + 8;
+  const float eps = 1.1920928955078125e-07f * 10;
+  for (int l = 0; l < n; ++l) {
+    const int len = m - l;
+    float nrm = 0.0f;
+    for (int i = 0; i < len; ++i) { v[i] = A[(l + i) * n + l]; nrm += v[i] * v[i]; }
+    const float v0 = v[0];
+    v[0] = v[0] + sgn1(v[0]) * sqrtf(nrm);
+    nrm = sqrtf(nrm + v[0] * v[0] - v0 * v0);
+    for (int i = 0; i < len; ++i) v[i] /= nrm;
+    for (int j = l; j < n; ++j) {
+      float dot = 0.0f;
+      for (int i = l; i < m; ++i) dot += v[i - l] * A[i * n + j];
+      for (int i = l; i < m; ++i) A[i * n + j] -= 2 * v[i - l] * dot;
+    }
+    h[l] = v[0] * v[0];
+    for (int i = 1; i < len; ++i) A[(l + i) * n + l] = v[i] / v[0];
+  }
+  for (int l = 0; l < n; ++l) {
+    v[0] = 1.0f;
+    for (int j = 1; j < m - l; ++j) v[j] = A[(j + l) * n + l];
+    float dot = 0.0f;
+    for (int i = l; i < m; ++i) dot += v[i - l] * b[i];
+    for (int i = l; i < m; ++i) b[i] -= 2 * v[i - l] * dot * h[l];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    for (int j = n - 1; j > i; --j) b[i] -= b[j] * A[i * n + j];
+    if (fabsf(A[i * n + i]) < eps) {
+      for (int q = 0; q < n; ++q) x[q] = 0.0f;
+      return false;
+    }
+    b[i] /= A[i * n + i];
+  }
+  for (int i = 0; i < n; ++i) x[i] = b[i];
+  return true;
+}
+
+LOAM_HD float hypot_cv(float a, float b) {
+  a = fabsf(a);
+  b = fabsf(b);
+  if (a > b) { b /= a; return a * sqrtf(1 + b * b); }
+  if (b > 0) { a /= b; return b * sqrtf(1 + a * a); }
+  return 0;
+}
+
+template <int N>
+LOAM_HD void jacobi_rowmax(const float* A, int* indR, int k) {
+  int m = k + 1;
+  float mv = fabsf(A[k * N + m]);
+  for (int i = k + 2; i < N; ++i) {
+    float val = fabsf(A[k * N + i]);
+    if (mv < val) { mv = val; m = i; }
+  }
+  indR[k] = m;
+}
+template <int N>
+LOAM_HD void jacobi_colmax(const float* A, int* indC, int k) {
+  int m = 0;
+  float mv = fabsf(A[k]);
+  for (int i = 1; i < k; ++i) {
+    float val = fabsf(A[i * N + k]);
+    if (mv < val) { mv = val; m = i; }
+  }
+  indC[k] = m;
+}
+
+// symmetric N x N (A destroyed): W descending, V eigenvectors as rows
+template <int N>
+LOAM_HD void jacobi(float* A, float* W, float* V, int* iws) {
+  int* indR = iws;
+  int* indC = iws + N;
+  const float eps = 1.1920928955078125e-07f;
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) V[i * N + j] = (i == j) ? 1.0f : 0.0f;
+  for (int k = 0; k < N; ++k) {
+    W[k] = A[k * N + k];
+    indR[k] = 0;
+    indC[k] = 0;
+    if (k < N - 1) jacobi_rowmax<N>(A, indR, k);
+    if (k > 0) jacobi_colmax<N>(A, indC, k);
+  }
+  for (int iters = 0; iters < N * N * 30; ++iters) {
+    int k = 0;
+    float mv = fabsf(A[indR[0]]);
+    for (int i = 1; i < N - 1; ++i) {
+      float val = fabsf(A[i * N + indR[i]]);
+      if (mv < val) { mv = val; k = i; }
+    }
+    int l = indR[k];
+    for (int i = 1; i < N; ++i) {
+      float val = fabsf(A[indC[i] * N + i]);
+      if (mv < val) { mv = val; k = indC[i]; l = i; }
+    }
+    float p = A[k * N + l];
+    if (fabsf(p) <= eps) break;
+    float y = (float)((W[l] - W[k]) * 0.5);
+    float t = fabsf(y) + hypot_cv(p, y);
+    float s = hypot_cv(p, t);
+    float c = t / s;
+    s = p / s;
+    t = (p / t) * p;
+    if (y < 0) { s = -s; t = -t; }
+    A[k * N + l] = 0;
+    W[k] -= t;
+    W[l] += t;
+#define LOAM_ROT(v0, v1)            \
+  {                                 \
+    float a0 = v0, b0 = v1;         \
+    v0 = a0 * c - b0 * s;           \
+    v1 = a0 * s + b0 * c;           \
+  }
+    for (int i = 0; i < k; ++i) LOAM_ROT(A[i * N + k], A[i * N + l]);
+    for (int i = k + 1; i < l; ++i) LOAM_ROT(A[k * N + i], A[i * N + l]);
+    for (int i = l + 1; i < N; ++i) LOAM_ROT(A[k * N + i], A[l * N + i]);
+    for (int i = 0; i < N; ++i) LOAM_ROT(V[k * N + i], V[l * N + i]);
+#undef LOAM_ROT
+    for (int j = 0; j < 2; ++j) {
+      int idx = j == 0 ? k : l;
+      if (idx < N - 1) jacobi_rowmax<N>(A, indR, idx);
+      if (idx > 0) jacobi_colmax<N>(A, indC, idx);
+    }
+  }
+  for (int k = 0; k < N - 1; ++k) {
+    int m = k;
+    for (int i = k + 1; i < N; ++i)
+      if (W[m] < W[i]) m = i;
+    if (k != m) {
+      float t = W[m]; W[m] = W[k]; W[k] = t;
+      for (int i = 0; i < N; ++i) { float q = V[m * N + i]; V[m * N + i] = V[k * N + i]; V[k * N + i] = q; }
+    }
+  }
+}
+
+// 6 x 6 LU inverse with partial pivoting (A destroyed)
+LOAM_HD bool lu_inv6(float* A, float* Inv, float* b) {
+  const int n = 6;
+  for (int i = 0; i < 36; ++i) b[i] = 0.0f;
+  for (int i = 0; i < n; ++i) b[i * n + i] = 1.0f;
+  const float eps = 1.1920928955078125e-07f * 10;
+  for (int i = 0; i < n; ++i) {
+    int k = i;
+    for (int j = i + 1; j < n; ++j)
+      if (fabsf(A[j * n + i]) > fabsf(A[k * n + i])) k = j;
+    if (fabsf(A[k * n + i]) < eps) {
+      for (int q = 0; q < 36; ++q) Inv[q] = 0.0f;
+      return false;
+    }
+    if (k != i) {
+      for (int j = i; j < n; ++j) { float t = A[i * n + j]; A[i * n + j] = A[k * n + j]; A[k * n + j] = t; }
+      for (int j = 0; j < n; ++j) { float t = b[i * n + j]; b[i * n + j] = b[k * n + j]; b[k * n + j] = t; }
+    }
+    float d = -1 / A[i * n + i];
+    for (int j = i + 1; j < n; ++j) {
+      float alpha = A[j * n + i] * d;
+      for (int q = i + 1; q < n; ++q) A[j * n + q] += alpha * A[i * n + q];
+      for (int q = 0; q < n; ++q) b[j * n + q] += alpha * b[i * n + q];
+    }
+  }
+  for (int i = n - 1; i >= 0; --i)
+    for (int j = 0; j < n; ++j) {
+      float s = b[i * n + j];
+      for (int q = i + 1; q < n; ++q) s -= A[i * n + q] * b[q * n + j];
+      b[i * n + j] = s / A[i * n + i];
+    }
+  for (int q = 0; q < 36; ++q) Inv[q] = b[q];
+  return true;
+}
+
+// C[m x n] = A[m x k] B[k x n], products and sums in double, one rounding (OpenCV CV_32F gemm)
+LOAM_HD void gemm_d(const float* A, const float* B, int m, int k, int n, float* C) {
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < n; ++j) {
+      double s = 0.0;
+      for (int l = 0; l < k; ++l) s += (double)A[i * k + l] * (double)B[l * n + j];
+      C[i * n + j] = (float)s;
+    }
+}
+
+// The L-M step on a reduced normal system (shared by odometry :765-826 and mapping :922-974):
+// AtA (6x6 float), AtB (6), iteration-0 degeneracy analysis.  One lane.
+// ws: >= kLmWs floats of scratch (LDS when called from a kernel lane), iws: >= 12 ints
+constexpr int kLmWs = 36 * 6 + 6 + 14 + 6;
+LOAM_HD void lm_step(const float* AtA_in, const float* AtB_in, int iter, float eig_thresh,
+                     int* isDegenerate, float* matP, float* X, float* ws, int* iws) {
+  float* A = ws;            // 36
+  float* b = ws + 36;       // 6
+  float* A2 = ws + 42;      // 36
+  float* V = ws + 78;       // 36
+  float* V2 = ws + 114;     // 36
+  float* Vi = ws + 150;     // 36
+  float* E = ws + 186;      // 6
+  float* tmp = ws + 192;    // 36 (LU rhs) / 14 (QR) / 6 (X2)
+  for (int i = 0; i < 36; ++i) A[i] = AtA_in[i];
+  for (int i = 0; i < 6; ++i) b[i] = AtB_in[i];
+  qr_solve(A, b, 6, 6, X, tmp);
+  if (iter == 0) {
+    for (int i = 0; i < 36; ++i) A2[i] = AtA_in[i];
+    jacobi<6>(A2, E, V, iws);
+    for (int i = 0; i < 36; ++i) V2[i] = V[i];
+    int degen = 0;
+    for (int i = 5; i >= 0; --i) {
+      if (E[i] < eig_thresh) {
+        for (int j = 0; j < 6; ++j) V2[i * 6 + j] = 0;
+        degen = 1;
+      } else {
+        break;
+      }
+    }
+    *isDegenerate = degen;
+    lu_inv6(V, Vi, tmp);
+    gemm_d(Vi, V2, 6, 6, 6, matP);
+  }
+  if (*isDegenerate) {
+    for (int i = 0; i < 6; ++i) tmp[i] = X[i];
+    gemm_d(matP, tmp, 6, 6, 1, X);
+  }
+}
+
+LOAM_HD float delta_r(const float* X) {
+  double a = loamdev::rad2deg((double)X[0]), b = loamdev::rad2deg((double)X[1]),
+         c = loamdev::rad2deg((double)X[2]);
+  return (float)sqrt(a * a + b * b + c * c);
+}
+LOAM_HD float delta_t(const float* X) {
+  double a = (double)(X[3] * 100), b = (double)(X[4] * 100), c = (double)(X[5] * 100);
+  return (float)sqrt(a * a + b * b + c * c);
+}
+
+}  // namespace loamla
+
+#endif

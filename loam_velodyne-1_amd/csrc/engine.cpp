@@ -1,0 +1,509 @@
+// libloam_hip: host engine behind the C-ABI of include/loam/loam.h.
+//
+// A context owns one HIP device, one stream and the device-resident state the four reference
+// nodes keep in globals: the scan-registration delay counter, the odometry transform / Last
+// clouds / their voxel hashes, and the mapping cube store.  Every entry point uploads the
+// caller's host cloud(s), runs the kernels of sr.hip / od.hip / mp.hip on the context stream and
+// copies the results back; nothing here computes a point on the CPU (a missing GPU or kernel
+// image fails loudly with LOAM_E_HIP).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/loam/loam.h"
+#include "engine.hpp"
+#include "mp.hpp"
+#include "od.hpp"
+#include "pose_math.hpp"
+
+using namespace loam;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess)                                                          \
+      return fail(LOAM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));  \
+  } while (0)
+
+FeatView feat_view(const SrBuffers& b, int first, int step) {
+  FeatView v;
+  const size_t R = b.R;
+  v.sharp = b.sharp + (size_t)first * kSharpPerRing * R;
+  v.lsharp = b.lsharp + (size_t)first * kLessSharpPerRing * R;
+  v.flat = b.flat + (size_t)first * kFlatPerRing * R;
+  v.lflat = b.lflat + (size_t)first * b.cap;
+  v.full = b.full + (size_t)first * b.cap;
+  v.sharp_stride = (size_t)step * kSharpPerRing * R;
+  v.lsharp_stride = (size_t)step * kLessSharpPerRing * R;
+  v.flat_stride = (size_t)step * kFlatPerRing * R;
+  v.lflat_stride = (size_t)step * b.cap;
+  v.full_stride = (size_t)step * b.cap;
+  v.cnt = b.cnt + (size_t)first * 4;
+  v.cnt_stride = 4 * step;
+  v.nfull_p = b.n_full + first;
+  v.nfull_stride = step;
+  return v;
+}
+
+}  // namespace
+
+struct loam_ctx {
+  loam_config cfg;
+  int device = 0;
+  hipStream_t st = nullptr;
+  int R = 16, cap = 40000;
+  // scan registration (streaming)
+  int sr_init_count = 0;
+  bool sr_inited = false;
+  SrBuffers sr1;        // one sweep
+  SrBuffers odin;       // odometry input feature set (host topics uploaded here)
+  OdBuffers od1;        // one odometry problem
+  bool od_inited = false;
+  int od_last = 0, od_frame_count = 1;
+  MpBuffers mp1;        // streaming map
+  // batch (config 4)
+  int P = 0;
+  SrBuffers srb;
+  OdBuffers odb;
+  MpBuffers mpb;
+  std::vector<float4> stage;
+  loam_stats stats;
+  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+};
+
+namespace {
+
+int check_cloud_in(const loam_cloud_in& c, int cap) {
+  if (c.count > 0 && c.data == nullptr) return fail(LOAM_E_INVAL, "cloud data is null");
+  if (c.stride_bytes < 12 || c.stride_bytes % 4 != 0) return fail(LOAM_E_INVAL, "bad stride_bytes");
+  if ((int)c.count > cap) return fail(LOAM_E_CAPACITY, "cloud exceeds max_points");
+  return LOAM_OK;
+}
+
+void pack(const loam_cloud_in& c, float4* dst) {
+  const char* base = (const char*)c.data;
+  for (uint32_t i = 0; i < c.count; ++i) {
+    const float* q = (const float*)(base + (size_t)i * c.stride_bytes);
+    dst[i] = make_float4(q[0], q[1], q[2], 0.0f);
+  }
+}
+
+int copy_out(hipStream_t st, const float4* dev, int n, loam_cloud_out* o) {
+  if (o == nullptr) return LOAM_OK;
+  if ((uint32_t)n > o->capacity) {
+    o->count = (uint32_t)n;
+    return fail(LOAM_E_CAPACITY, "output cloud capacity too small");
+  }
+  o->count = (uint32_t)n;
+  if (n > 0) HIP_TRY(hipMemcpyAsync(o->pts, dev, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost, st));
+  return LOAM_OK;
+}
+
+int upload_cloud(hipStream_t st, const loam_cloud_out& c, float4* dev, int cap) {
+  if (c.count > (uint32_t)cap) return fail(LOAM_E_CAPACITY, "input feature cloud exceeds capacity");
+  if (c.count > 0) {
+    if (c.pts == nullptr) return fail(LOAM_E_INVAL, "feature cloud pts is null");
+    HIP_TRY(hipMemcpyAsync(dev, c.pts, (size_t)c.count * sizeof(float4), hipMemcpyHostToDevice, st));
+  }
+  return LOAM_OK;
+}
+
+int sr_errors(int e) {
+  if (e & ERR_EMPTY) return fail(LOAM_E_INVAL, "sweep has no finite point");
+  if (e & ERR_CAP_RING) return fail(LOAM_E_CAPACITY, "a ring span exceeds the per-ring capacity");
+  return LOAM_OK;
+}
+
+SrParams sr_params(const loam_ctx* c) {
+  SrParams p;
+  p.R = c->R;
+  p.ring_model = (int)c->cfg.ring_model;
+  p.ring_lo = c->cfg.ring_lo_deg;
+  p.ring_hi = c->cfg.ring_hi_deg;
+  return p;
+}
+
+void count_bytes(loam_stats& s) {
+  // algorithmic bytes, SURVEY.md §8(d)
+  s.bytes_sr = 16 * s.n_raw + 32 * s.n_ring + 16 * (s.n_sharp + s.n_less_sharp + s.n_flat + s.n_less_flat);
+  s.bytes_od = s.od_assoc_rounds * 16 * (s.od_corner_last + s.od_surf_last) + 16 * s.od_queries +
+               12 * s.od_queries + 32 * s.od_rows_sum;
+  s.bytes_mp = 16 * s.mp_map_points + 96 * s.mp_stack * (s.mp_iters ? 1 : 0) + 64 * s.mp_rows_sum +
+               32 * s.mp_stack + 32 * s.mp_map_valid_points;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* loam_last_error(void) { return g_err.c_str(); }
+
+void loam_config_default(loam_config* d) {
+  std::memset(d, 0, sizeof(*d));
+  d->n_rings = 16;
+  d->ring_model = LOAM_RING_VLP16;
+  d->ring_lo_deg = -24.8f;
+  d->ring_hi_deg = 2.0f;
+  d->system_delay = 20;
+  d->max_points = 40000;
+  d->od_max_iter = 25;
+  d->mp_max_iter = 10;
+  d->skip_frame_num = 1;
+  d->map_capacity = 1u << 21;
+}
+
+int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
+  if (out == nullptr) return fail(LOAM_E_INVAL, "out is null");
+  *out = nullptr;
+  loam_config c;
+  if (cfg) c = *cfg;
+  else loam_config_default(&c);
+  if (c.n_rings < 2 || c.n_rings > 64) return fail(LOAM_E_INVAL, "n_rings must be in [2, 64]");
+  if (c.max_points < 64 || c.max_points > (1u << 22)) return fail(LOAM_E_INVAL, "bad max_points");
+  if (c.od_max_iter < 1 || c.od_max_iter > 1000 || c.mp_max_iter < 1 || c.mp_max_iter > 1000)
+    return fail(LOAM_E_INVAL, "bad iteration limits");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(LOAM_E_HIP, "no HIP device available (the engine has no CPU fallback)");
+  if (device < 0 || device >= ndev) return fail(LOAM_E_INVAL, "bad device index");
+  HIP_TRY(hipSetDevice(device));
+  loam_ctx* x = new loam_ctx();
+  x->cfg = c;
+  x->device = device;
+  x->R = (int)c.n_rings;
+  x->cap = (int)c.max_points;
+  std::memset(&x->stats, 0, sizeof(x->stats));
+  if (hipStreamCreateWithFlags(&x->st, hipStreamNonBlocking) != hipSuccess) {
+    delete x;
+    return fail(LOAM_E_HIP, "hipStreamCreate failed");
+  }
+  for (auto& e : x->ev) (void)hipEventCreate(&e);
+  sr_alloc(x->sr1, 1, x->cap, x->R);
+  sr_alloc(x->odin, 1, x->cap, x->R);
+  od_alloc(x->od1, 1, x->R, x->cap, (int)c.od_max_iter);
+  mp_alloc(x->mp1, 1, x->R, x->cap, (int)c.map_capacity, (int)c.mp_max_iter);
+  if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess) {
+    loam_destroy(x);
+    return fail(LOAM_E_NOMEM, "device allocation failed");
+  }
+  *out = x;
+  return LOAM_OK;
+}
+
+void loam_destroy(loam_ctx* x) {
+  if (!x) return;
+  (void)hipSetDevice(x->device);
+  if (x->st) (void)hipStreamSynchronize(x->st);
+  sr_free(x->sr1);
+  sr_free(x->odin);
+  od_free(x->od1);
+  mp_free(x->mp1);
+  sr_free(x->srb);
+  od_free(x->odb);
+  mp_free(x->mpb);
+  for (auto& e : x->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (x->st) (void)hipStreamDestroy(x->st);
+  delete x;
+}
+
+int loam_get_stats(loam_ctx* x, loam_stats* s) {
+  if (!x || !s) return fail(LOAM_E_INVAL, "null argument");
+  *s = x->stats;
+  return LOAM_OK;
+}
+
+// ------------------------------------------------------------------ scanRegistration
+int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_features* out) {
+  (void)stamp;
+  if (!x || !out) return fail(LOAM_E_INVAL, "null argument");
+  if (!x->sr_inited) {  // src/scanRegistration.cpp:213-219 (Q1)
+    x->sr_init_count++;
+    if (x->sr_init_count >= (int)x->cfg.system_delay) x->sr_inited = true;
+    return fail(LOAM_E_NOT_READY, "inside systemDelay");
+  }
+  int rc = check_cloud_in(raw, x->cap);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(x->device));
+  x->stage.resize(raw.count);
+  pack(raw, x->stage.data());
+  SrBuffers& b = x->sr1;
+  const int n = (int)raw.count;
+  HIP_TRY(hipMemcpyAsync(b.raw, x->stage.data(), (size_t)n * sizeof(float4), hipMemcpyHostToDevice, x->st));
+  HIP_TRY(hipMemcpyAsync(b.raw_n, &n, sizeof(int), hipMemcpyHostToDevice, x->st));
+  HIP_TRY(hipEventRecord(x->ev[0], x->st));
+  sr_launch(b, sr_params(x), x->st);
+  HIP_TRY(hipEventRecord(x->ev[1], x->st));
+  HIP_TRY(hipGetLastError());
+  int cnt[4], nfull, err;
+  HIP_TRY(hipMemcpyAsync(cnt, b.cnt, sizeof(cnt), hipMemcpyDeviceToHost, x->st));
+  HIP_TRY(hipMemcpyAsync(&nfull, b.n_full, sizeof(int), hipMemcpyDeviceToHost, x->st));
+  HIP_TRY(hipMemcpyAsync(&err, b.err, sizeof(int), hipMemcpyDeviceToHost, x->st));
+  HIP_TRY(hipStreamSynchronize(x->st));
+  rc = sr_errors(err);
+  if (rc) return rc;
+  int e = 0;
+  e |= copy_out(x->st, b.full, nfull, &out->full);
+  e |= copy_out(x->st, b.sharp, cnt[0], &out->sharp);
+  e |= copy_out(x->st, b.lsharp, cnt[1], &out->less_sharp);
+  e |= copy_out(x->st, b.flat, cnt[2], &out->flat);
+  e |= copy_out(x->st, b.lflat, cnt[3], &out->less_flat);
+  std::memset(out->imu_trans, 0, sizeof(out->imu_trans));
+  HIP_TRY(hipStreamSynchronize(x->st));
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, x->ev[0], x->ev[1]);
+  std::memset(&x->stats, 0, sizeof(x->stats));
+  x->stats.n_raw = (uint64_t)n;
+  x->stats.n_ring = (uint64_t)nfull;
+  x->stats.n_sharp = cnt[0]; x->stats.n_less_sharp = cnt[1];
+  x->stats.n_flat = cnt[2]; x->stats.n_less_flat = cnt[3];
+  x->stats.ms_sr = ms;
+  count_bytes(x->stats);
+  return e ? LOAM_E_CAPACITY : LOAM_OK;
+}
+
+// ------------------------------------------------------------------ laserOdometry
+int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6* sum_out,
+                  loam_cloud_out* corner_last, loam_cloud_out* surf_last, loam_cloud_out* full_end,
+                  int* published) {
+  (void)stamp;
+  if (!x || !in || !published) return fail(LOAM_E_INVAL, "null argument");
+  HIP_TRY(hipSetDevice(x->device));
+  *published = 0;
+  SrBuffers& fi = x->odin;
+  OdBuffers& o = x->od1;
+  const int R = x->R;
+  if (in->sharp.count > (uint32_t)(kSharpPerRing * R) || in->flat.count > (uint32_t)(kFlatPerRing * R) ||
+      in->less_sharp.count > (uint32_t)(kLessSharpPerRing * R))
+    return fail(LOAM_E_CAPACITY, "feature cloud larger than scan registration can produce");
+  int rc = 0;
+  if ((rc = upload_cloud(x->st, in->sharp, fi.sharp, kSharpPerRing * R)) ||
+      (rc = upload_cloud(x->st, in->less_sharp, fi.lsharp, kLessSharpPerRing * R)) ||
+      (rc = upload_cloud(x->st, in->flat, fi.flat, kFlatPerRing * R)) ||
+      (rc = upload_cloud(x->st, in->less_flat, fi.lflat, x->cap)) ||
+      (rc = upload_cloud(x->st, in->full, fi.full, x->cap)))
+    return rc;
+  int cnt[5] = {(int)in->sharp.count, (int)in->less_sharp.count, (int)in->flat.count,
+                (int)in->less_flat.count, (int)in->full.count};
+  HIP_TRY(hipMemcpyAsync(fi.cnt, cnt, 4 * sizeof(int), hipMemcpyHostToDevice, x->st));
+  HIP_TRY(hipMemcpyAsync(fi.n_full, &cnt[4], sizeof(int), hipMemcpyHostToDevice, x->st));
+  const FeatView fv = feat_view(fi, 0, 1);
+  std::memset(&x->stats, 0, sizeof(x->stats));
+  if (!x->od_inited) {  // src/laserOdometry.cpp:427-456: Last = raw lessSharp / lessFlat, no L-M
+    hipLaunchKernelGGL(k_od_end, dim3(16, 1), dim3(256), 0, x->st, o, fv, 0, 0, 0);
+    od_build_hashes(o, 0, x->st);
+    HIP_TRY(hipGetLastError());
+    x->od_last = 0;
+    x->od_inited = true;
+    int nl[2];
+    HIP_TRY(hipMemcpyAsync(nl, o.nlast, 2 * sizeof(int), hipMemcpyDeviceToHost, x->st));
+    HIP_TRY(hipStreamSynchronize(x->st));
+    *published = LOAM_PUB_CLOUDS;
+    int e = copy_out(x->st, o.lastC, nl[0], corner_last) | copy_out(x->st, o.lastS, nl[1], surf_last);
+    HIP_TRY(hipStreamSynchronize(x->st));
+    return e ? LOAM_E_CAPACITY : LOAM_OK;
+  }
+  const int cur = x->od_last, nxt = 1 - cur;
+  HIP_TRY(hipEventRecord(x->ev[0], x->st));
+  hipLaunchKernelGGL(k_od_solve, dim3(1), dim3(256), 0, x->st, o, fv, cur);
+  x->od_frame_count++;
+  const bool pub = x->od_frame_count >= (int)x->cfg.skip_frame_num + 1;
+  hipLaunchKernelGGL(k_od_end, dim3(16, 1), dim3(256), 0, x->st, o, fv, nxt, 2, pub ? 1 : 0);
+  od_build_hashes(o, nxt, x->st);
+  HIP_TRY(hipEventRecord(x->ev[1], x->st));
+  HIP_TRY(hipGetLastError());
+  x->od_last = nxt;
+  float st[kOdStateFloats];
+  int ist[kOdStateInts], nl[4], nfe[2];
+  HIP_TRY(hipMemcpyAsync(st, o.state, sizeof(st), hipMemcpyDeviceToHost, x->st));
+  HIP_TRY(hipMemcpyAsync(ist, o.istate, sizeof(ist), hipMemcpyDeviceToHost, x->st));
+  HIP_TRY(hipMemcpyAsync(nl, o.nlast, sizeof(nl), hipMemcpyDeviceToHost, x->st));
+  HIP_TRY(hipMemcpyAsync(nfe, o.nfullEnd, sizeof(nfe), hipMemcpyDeviceToHost, x->st));
+  HIP_TRY(hipStreamSynchronize(x->st));
+  if (ist[kIsErr]) return fail(LOAM_E_CAPACITY, "odometry capacity exceeded");
+  if (sum_out) std::memcpy(sum_out, st + kOdSum, sizeof(loam_pose6));
+  *published = LOAM_PUB_POSE;
+  int e = 0;
+  if (pub) {
+    x->od_frame_count = 0;
+    *published |= LOAM_PUB_CLOUDS | LOAM_PUB_FULL;
+    e |= copy_out(x->st, o.lastC + (size_t)nxt * o.P * o.capC, nl[nxt * 2 + 0], corner_last);
+    e |= copy_out(x->st, o.lastS + (size_t)nxt * o.P * o.capS, nl[nxt * 2 + 1], surf_last);
+    e |= copy_out(x->st, o.fullEnd + (size_t)nxt * o.P * o.capS, nfe[nxt], full_end);
+    HIP_TRY(hipStreamSynchronize(x->st));
+  }
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, x->ev[0], x->ev[1]);
+  x->stats.ms_od = ms;
+  x->stats.od_iters = ist[kIsIters];
+  x->stats.od_assoc_rounds = ist[kIsAssoc];
+  x->stats.od_rows_sum = (uint64_t)ist[kIsRows];
+  x->stats.od_queries = ist[kIsQueries];
+  x->stats.od_corner_last = nl[cur * 2 + 0];
+  x->stats.od_surf_last = nl[cur * 2 + 1];
+  count_bytes(x->stats);
+  return e ? LOAM_E_CAPACITY : LOAM_OK;
+}
+
+// ------------------------------------------------------------------ laserMapping
+int loam_mapping(loam_ctx* x, double stamp, const loam_pose6* odom_sum, const loam_cloud_out* corner_last,
+                 const loam_cloud_out* surf_last, const loam_cloud_out* full_end, loam_pose6* aft,
+                 loam_pose6* bef, loam_cloud_out* registered) {
+  (void)stamp;
+  if (!x || !odom_sum || !corner_last || !surf_last || !full_end || !aft || !bef)
+    return fail(LOAM_E_INVAL, "null argument");
+  HIP_TRY(hipSetDevice(x->device));
+  return mp_stream_frame(x->mp1, x->st, *odom_sum, *corner_last, *surf_last, *full_end, aft, bef,
+                         registered, &x->stats, g_err);
+}
+
+// ------------------------------------------------------------------ transformMaintenance
+int loam_maintenance(const loam_pose6* odom_sum, const loam_pose6* bef, const loam_pose6* aft,
+                     loam_pose6* integrated) {
+  if (!odom_sum || !bef || !aft || !integrated) return fail(LOAM_E_INVAL, "null argument");
+  // src/transformMaintenance.cpp:147-203: Sum and Aft arrive as quaternion messages, Bef through
+  // the twist fields; then transformAssociateToMap (:60-145).  Scalar host algebra, no kernel.
+  float S[6], A[6], B[6], incre[6] = {0, 0, 0, 0, 0, 0}, T[6];
+  loampose::pose_through_msg((const float*)odom_sum, S);
+  loampose::pose_through_msg((const float*)aft, A);
+  std::memcpy(B, bef, sizeof(B));
+  loampose::associate_to_map(S, B, A, incre, T);
+  std::memcpy(integrated, T, sizeof(T));
+  return LOAM_OK;
+}
+
+// ------------------------------------------------------------------ batch (config 4)
+int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const loam_cloud_in* cur) {
+  if (!x || !prev || !cur || n == 0) return fail(LOAM_E_INVAL, "bad batch arguments");
+  HIP_TRY(hipSetDevice(x->device));
+  for (uint32_t i = 0; i < n; ++i) {
+    int rc = check_cloud_in(prev[i], x->cap);
+    if (!rc) rc = check_cloud_in(cur[i], x->cap);
+    if (rc) return rc;
+  }
+  if ((int)n != x->P) {
+    HIP_TRY(hipStreamSynchronize(x->st));
+    sr_free(x->srb);
+    od_free(x->odb);
+    mp_free(x->mpb);
+    x->P = (int)n;
+    sr_alloc(x->srb, 2 * x->P, x->cap, x->R);
+    od_alloc(x->odb, x->P, x->R, x->cap, (int)x->cfg.od_max_iter);
+    mp_alloc(x->mpb, x->P, x->R, x->cap, mp_batch_map_capacity(x->cap), (int)x->cfg.mp_max_iter);
+    HIP_TRY(hipDeviceSynchronize());
+    if (hipGetLastError() != hipSuccess) return fail(LOAM_E_NOMEM, "batch allocation failed");
+  }
+  std::vector<float4> h((size_t)x->cap);
+  std::vector<int> counts(2 * n);
+  for (uint32_t i = 0; i < n; ++i)
+    for (int k = 0; k < 2; ++k) {
+      const loam_cloud_in& c = k == 0 ? prev[i] : cur[i];
+      pack(c, h.data());
+      counts[2 * i + k] = (int)c.count;
+      HIP_TRY(hipMemcpy(x->srb.raw + (size_t)(2 * i + k) * x->cap, h.data(), (size_t)c.count * sizeof(float4),
+                        hipMemcpyHostToDevice));
+    }
+  HIP_TRY(hipMemcpy(x->srb.raw_n, counts.data(), counts.size() * sizeof(int), hipMemcpyHostToDevice));
+  return LOAM_OK;
+}
+
+int loam_batch_run(loam_ctx* x) {
+  if (!x || x->P == 0) return fail(LOAM_E_INVAL, "no batch uploaded");
+  HIP_TRY(hipSetDevice(x->device));
+  const int P = x->P;
+  OdBuffers& o = x->odb;
+  HIP_TRY(hipEventRecord(x->ev[0], x->st));
+  sr_launch(x->srb, sr_params(x), x->st);
+  HIP_TRY(hipEventRecord(x->ev[1], x->st));
+  HIP_TRY(hipMemsetAsync(o.state, 0, (size_t)P * kOdStateFloats * sizeof(float), x->st));
+  HIP_TRY(hipMemsetAsync(o.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st));
+  const FeatView fprev = feat_view(x->srb, 0, 2), fcur = feat_view(x->srb, 1, 2);
+  // odometry seeded from prev as a solved zero-increment frame, then one loop body on cur
+  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fprev, 0, 1, 1);
+  od_build_hashes(o, 0, x->st);
+  hipLaunchKernelGGL(k_od_solve, dim3(P), dim3(256), 0, x->st, o, fcur, 0);
+  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, 1, 2, 1);
+  HIP_TRY(hipEventRecord(x->ev[2], x->st));
+  // mapping: prev into an empty map at the origin, then cur with the odometry pose
+  mp_batch_run(x->mpb, o, x->st);
+  HIP_TRY(hipEventRecord(x->ev[3], x->st));
+  HIP_TRY(hipGetLastError());
+  return LOAM_OK;
+}
+
+int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_stats* stats) {
+  if (!x || x->P == 0) return fail(LOAM_E_INVAL, "no batch");
+  HIP_TRY(hipSetDevice(x->device));
+  const int P = x->P;
+  HIP_TRY(hipStreamSynchronize(x->st));
+  std::vector<float> st((size_t)P * kOdStateFloats);
+  std::vector<int> ist((size_t)P * kOdStateInts), srerr(2 * P), cnt(8 * P), nfull(2 * P), nl(4 * P);
+  HIP_TRY(hipMemcpy(st.data(), x->odb.state, st.size() * sizeof(float), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(ist.data(), x->odb.istate, ist.size() * sizeof(int), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(srerr.data(), x->srb.err, srerr.size() * sizeof(int), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(cnt.data(), x->srb.cnt, cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(nfull.data(), x->srb.n_full, nfull.size() * sizeof(int), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(nl.data(), x->odb.nlast, nl.size() * sizeof(int), hipMemcpyDeviceToHost));
+  for (int i = 0; i < 2 * P; ++i) {
+    int rc = sr_errors(srerr[i]);
+    if (rc) return rc;
+  }
+  if (od_sum)
+    for (int i = 0; i < P; ++i) std::memcpy(&od_sum[i], &st[(size_t)i * kOdStateFloats + kOdSum], sizeof(loam_pose6));
+  loam_stats s;
+  std::memset(&s, 0, sizeof(s));
+  int rc = mp_batch_download(x->mpb, x->st, aft, &s, g_err);
+  if (rc) return rc;
+  for (int i = 0; i < 2 * P; ++i) {
+    s.n_ring += nfull[i];
+    s.n_sharp += cnt[4 * i]; s.n_less_sharp += cnt[4 * i + 1];
+    s.n_flat += cnt[4 * i + 2]; s.n_less_flat += cnt[4 * i + 3];
+  }
+  int raw_n[2];
+  (void)raw_n;
+  std::vector<int> rn(2 * P);
+  HIP_TRY(hipMemcpy(rn.data(), x->srb.raw_n, rn.size() * sizeof(int), hipMemcpyDeviceToHost));
+  for (int i = 0; i < 2 * P; ++i) s.n_raw += rn[i];
+  for (int i = 0; i < P; ++i) {
+    const int* q = &ist[(size_t)i * kOdStateInts];
+    if (q[kIsErr]) return fail(LOAM_E_CAPACITY, "odometry capacity exceeded");
+    s.od_iters += q[kIsIters];
+    s.od_assoc_rounds += q[kIsAssoc];
+    s.od_rows_sum += (uint64_t)q[kIsRows];
+    s.od_queries += q[kIsQueries];
+    s.od_corner_last += nl[i * 4 + 0];
+    s.od_surf_last += nl[i * 4 + 1];
+  }
+  // per-problem association rounds multiply per-problem cloud sizes: use the mean
+  count_bytes(s);
+  if (P > 0 && s.od_assoc_rounds) {
+    uint64_t per = 0;
+    for (int i = 0; i < P; ++i)
+      per += (uint64_t)ist[(size_t)i * kOdStateInts + kIsAssoc] * 16 * (nl[i * 4 + 0] + nl[i * 4 + 1]);
+    s.bytes_od = per + 16 * s.od_queries + 12 * s.od_queries + 32 * s.od_rows_sum;
+  }
+  float ms_sr = 0, ms_od = 0, ms_mp = 0;
+  (void)hipEventElapsedTime(&ms_sr, x->ev[0], x->ev[1]);
+  (void)hipEventElapsedTime(&ms_od, x->ev[1], x->ev[2]);
+  (void)hipEventElapsedTime(&ms_mp, x->ev[2], x->ev[3]);
+  s.ms_sr = ms_sr;
+  s.ms_od = ms_od;
+  s.ms_mp = ms_mp;
+  x->stats = s;
+  if (stats) *stats = s;
+  return LOAM_OK;
+}
+
+}  // extern "C"

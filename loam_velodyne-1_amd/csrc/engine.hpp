@@ -1,0 +1,70 @@
+// Engine-internal declarations: device buffers of a batch of sweeps / problems and the kernel
+// launchers of sr.hip, od.hip, mp.hip.  Not part of the C-ABI (include/loam/loam.h).
+#ifndef LOAM_ENGINE_HPP
+#define LOAM_ENGINE_HPP
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/loam/loam.h"
+
+namespace loam {
+
+// error bits a kernel may raise (per sweep / problem); mapped to LOAM_E_* by the host
+enum : int {
+  ERR_CAP_RING = 1,     // a ring span / segment exceeds the per-ring LDS capacity
+  ERR_CAP_ROWS = 2,     // L-M row buffer overflow
+  ERR_EMPTY = 4,        // no finite input point
+  ERR_CAP_MAP = 8,      // map store overflow
+  ERR_CAP_STACK = 16,   // stack / FromMap capacity
+};
+
+constexpr int kSrThreads = 512;     // ring-sort workgroup (one per sweep)
+constexpr int kSelThreads = 256;    // per-ring selection workgroup
+constexpr int kRingCap = 4096;      // max ring span (points) handled in LDS by one workgroup
+constexpr int kSegCap = 2048;       // max segment length (LDS bitonic sort)
+constexpr int kSharpPerRing = 12, kLessSharpPerRing = 120, kFlatPerRing = 24;
+
+// Scan-registration buffers for S sweeps of capacity `cap` points each (index s*cap + i).
+struct SrBuffers {
+  int S = 0, cap = 0, R = 0;
+  float4* raw = nullptr;     // input (x, y, z, *) in sensor frame, per-sweep stride cap
+  int* raw_n = nullptr;
+  float* tmp_ori = nullptr;
+  uint8_t* tmp_sid = nullptr;
+  int* tilecnt = nullptr;    // [S][ntiles][R]
+  float4* full = nullptr;    // ring-sorted cloud (camera frame, intensity = ring + 0.1 relTime)
+  int* n_full = nullptr;
+  float* curv = nullptr;
+  uint8_t* picked = nullptr;
+  int* sortind = nullptr;
+  int8_t* label = nullptr;
+  int* ring_se = nullptr;    // [S][2R] scanStartInd / scanEndInd
+  int* st_sharp = nullptr;   // [S][R][12] point indices
+  int* st_lsharp = nullptr;  // [S][R][120]
+  int* st_flat = nullptr;    // [S][R][24]
+  float4* st_lflat = nullptr;  // [S][R][kRingCap] downsampled points
+  int* st_cnt = nullptr;     // [S][R][4]
+  float4* sharp = nullptr;   // [S][12R]
+  float4* lsharp = nullptr;  // [S][120R]
+  float4* flat = nullptr;    // [S][24R]
+  float4* lflat = nullptr;   // [S][cap]
+  int* cnt = nullptr;        // [S][4]: sharp, less_sharp, flat, less_flat
+  int* err = nullptr;        // [S]
+  __host__ __device__ int ntiles() const { return (cap + kSrThreads - 1) / kSrThreads; }
+};
+
+struct SrParams {
+  int R;
+  int ring_model;
+  float ring_lo, ring_hi;
+};
+
+void sr_alloc(SrBuffers& b, int S, int cap, int R);
+void sr_free(SrBuffers& b);
+// runs the whole scan registration for sweeps [0, S) already in b.raw / b.raw_n
+void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st);
+
+}  // namespace loam
+
+#endif

@@ -1,0 +1,592 @@
+// Laser odometry on gfx950: the laserOdometry loop body (/root/reference/src/laserOdometry.cpp:413-931)
+// for a batch of independent problems, one persistent workgroup per problem.
+//
+//  k_hash_build   voxel-hashed CSR index of a cloud (spatial hash of 1 m cells -> buckets, counting
+//                 sort).  Replaces kdtreeCornerLast / kdtreeSurfLast (:78-79, :436-437, :905-906).
+//  k_od_solve     the whole L-M loop (:465-828) in one workgroup of 256 threads:
+//                   TransformToStart of every query (lane per query),
+//                   every 5th iteration the association (wave per query): exact NN through the hash
+//                   (27 cells; exhaustive fallback when the best match is farther than one cell),
+//                   then the ring-window scans of :486-523 / :598-645 as 64-wide chunks with a
+//                   ballot for the break and a (distance, scan order) min-reduction = the
+//                   reference's sequential first-minimum,
+//                   residuals + weights (lane per query), rows appended in query order (Q12),
+//                   J of every accumulated row at the current transform and JᵀJ / Jᵀb accumulated in
+//                   fp64 with a fixed-order block reduction, the 6x6 QR solve / iteration-0
+//                   degeneracy analysis on one lane, NaN guard, convergence test;
+//                 then the pose accumulation (:830-856).
+//  k_od_end       TransformToEnd of lessSharp / lessFlat / full (:875-891) into the next Last clouds.
+#include "dev_common.hpp"
+#include "od.hpp"
+#include "pose_math.hpp"
+
+using namespace loamdev;
+
+namespace loam {
+
+namespace {
+
+constexpr int kOdThreads = 256;
+constexpr int kOdWaves = kOdThreads / 64;
+
+LOAM_D loampose::Imu load_imu(const float* st) {
+  loampose::Imu m;
+  const float* q = st + kOdImu;
+  m.pitchStart = q[0]; m.yawStart = q[1]; m.rollStart = q[2];
+  m.pitchLast = q[3]; m.yawLast = q[4]; m.rollLast = q[5];
+  m.shiftX = q[6]; m.shiftY = q[7]; m.shiftZ = q[8];
+  m.veloX = q[9]; m.veloY = q[10]; m.veloZ = q[11];
+  return m;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- voxel hash build
+// One workgroup per cloud: T = pow2 >= count (clamped to [64, tmax]) buckets, CSR start[T+1],
+// points re-ordered by bucket with their source index in .w (bit pattern).
+__global__ __launch_bounds__(256) void k_hash_build(HashJob j) {
+  const int p = blockIdx.x, tid = threadIdx.x;
+  const int n = *(const int*)((const char*)j.count + (size_t)p * j.count_stride_bytes);
+  const float4* pts = j.pts + (size_t)p * j.pts_stride;
+  int* start = j.start + (size_t)p * (j.tmax + 1);
+  int* fill = j.fill + (size_t)p * j.tmax;
+  float4* out = j.out + (size_t)p * j.pts_stride;
+  __shared__ int scratch[16];
+  __shared__ int sh_T;
+  if (tid == 0) {
+    int T = next_pow2(n > 64 ? n : 64);
+    if (T > j.tmax) T = j.tmax;
+    sh_T = T;
+    j.tsize[p] = T;
+  }
+  __syncthreads();
+  const int T = sh_T;
+  for (int b = tid; b < T; b += 256) fill[b] = 0;
+  __threadfence();
+  __syncthreads();
+  for (int i = tid; i < n; i += 256) {
+    const float4 a = pts[i];
+    uint32_t h = cell_hash(cell_of(a.x, j.inv_h), cell_of(a.y, j.inv_h), cell_of(a.z, j.inv_h)) & (T - 1);
+    atomicAdd(&fill[h], 1);
+  }
+  __threadfence();
+  __syncthreads();
+  // exclusive scan of fill[0..T) into start: contiguous chunk per thread
+  const int per = (T + 255) / 256;
+  const int b0 = tid * per, b1 = min(T, b0 + per);
+  int local = 0;
+  for (int b = b0; b < b1; ++b) local += __hip_atomic_load(&fill[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int tot;
+  int run = block_excl_scan<256>(local, scratch, tot);
+  for (int b = b0; b < b1; ++b) {
+    int c = __hip_atomic_load(&fill[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    start[b] = run;
+    __hip_atomic_store(&fill[b], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    run += c;
+  }
+  if (tid == 0) start[T] = tot;
+  __threadfence();
+  __syncthreads();
+  for (int i = tid; i < n; i += 256) {
+    const float4 a = pts[i];
+    uint32_t h = cell_hash(cell_of(a.x, j.inv_h), cell_of(a.y, j.inv_h), cell_of(a.z, j.inv_h)) & (T - 1);
+    int pos = atomicAdd(&fill[h], 1);
+    out[pos] = make_float4(a.x, a.y, a.z, __int_as_float(i));
+  }
+}
+
+namespace {
+
+// exact nearest neighbour of q among the hashed cloud (wave-cooperative); returns the packed
+// (float distance bits << 32 | index) minimum, ~0 if the cloud is empty.  `cells` = per-wave LDS
+// scratch of 64 ints.
+LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const float4* cloud, int n,
+                             float h, float inv_h, float qx, float qy, float qz, int* cells) {
+  const int lane = lane_id();
+  const int cx = cell_of(qx, inv_h), cy = cell_of(qy, inv_h), cz = cell_of(qz, inv_h);
+  int bucket = -1, b0 = 0, cnt = 0;
+  if (lane < 27) {
+    const int dx = lane % 3 - 1, dy = (lane / 3) % 3 - 1, dz = lane / 9 - 1;
+    bucket = (int)(cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1));
+    b0 = start[bucket];
+    cnt = start[bucket + 1] - b0;
+  }
+  // two of the 27 cells may share a bucket: count it once
+  for (int o = 0; o < 27; ++o) {
+    int bo = __shfl(bucket, o, 64);
+    if (o < lane && bo == bucket) cnt = 0;
+  }
+  const int incl = wave_incl_scan(cnt);
+  const int total = __shfl(incl, 63, 64);
+  if (lane < 27) { cells[lane] = incl - cnt; cells[32 + lane] = b0; }
+  __builtin_amdgcn_wave_barrier();
+  uint64_t best = ~0ull;
+  for (int t = lane; t < total; t += 64) {
+    int k = 0;
+    while (k < 26 && cells[k + 1] <= t) ++k;
+    const float4 a = hp[cells[32 + k] + (t - cells[k])];
+    const float d = sqdist(a.x, a.y, a.z, qx, qy, qz);
+    const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)__float_as_int(a.w);
+    best = key < best ? key : best;
+  }
+  best = wave_min_u64(best);
+  __builtin_amdgcn_wave_barrier();
+  // exact only if the best lies within one cell of q; otherwise scan the whole cloud
+  if (best == ~0ull || __uint_as_float((uint32_t)(best >> 32)) >= h * h) {
+    best = ~0ull;
+    for (int t = lane; t < n; t += 64) {
+      const float4 a = cloud[t];
+      const float d = sqdist(a.x, a.y, a.z, qx, qy, qz);
+      const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)t;
+      best = key < best ? key : best;
+    }
+    best = wave_min_u64(best);
+  }
+  return best;
+}
+
+// corner association (:478-527): closest (kd NN, sqDis < 25) and the best point of an adjacent
+// ring in the index window.  fwd_end = min(cornerPointsSharpNum, C) (Q11).
+LOAM_D void wave_assoc_corner(const float4* CL, int C, int fwd_end, uint64_t nn, float4 sel,
+                              int& ind1, int& ind2) {
+  const int lane = lane_id();
+  ind1 = -1;
+  ind2 = -1;
+  if (nn == ~0ull) return;
+  const float d0 = __uint_as_float((uint32_t)(nn >> 32));
+  if (!(D(d0) < 25)) return;
+  const int c = (int)(uint32_t)nn;
+  ind1 = c;
+  const int scan = (int)CL[c].w;
+  uint64_t best = ~0ull;
+  for (int base = c + 1; base < fwd_end; base += 64) {
+    const int j = base + lane;
+    const bool inr = j < fwd_end;
+    const float4 a = inr ? CL[j] : make_float4(0, 0, 0, 0);
+    const int r = (int)a.w;
+    const uint64_t mb = __ballot(inr && D(r) > scan + 2.5);
+    const int limit = mb ? __ffsll((unsigned long long)mb) - 1 : 64;
+    if (inr && lane < limit && r > scan) {
+      const float d = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
+      if (d < 25) {
+        const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)(j - c - 1);
+        best = key < best ? key : best;
+      }
+    }
+    if (mb) break;
+  }
+  for (int base = c - 1; base >= 0; base -= 64) {
+    const int j = base - lane;
+    const bool inr = j >= 0;
+    const float4 a = inr ? CL[j] : make_float4(0, 0, 0, 0);
+    const int r = (int)a.w;
+    const uint64_t mb = __ballot(inr && D(r) < scan - 2.5);
+    const int limit = mb ? __ffsll((unsigned long long)mb) - 1 : 64;
+    if (inr && lane < limit && r < scan) {
+      const float d = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
+      if (d < 25) {
+        const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)((1u << 30) + (c - 1 - j));
+        best = key < best ? key : best;
+      }
+    }
+    if (mb) break;
+  }
+  best = wave_min_u64(best);
+  if (best != ~0ull) {
+    const uint32_t o = (uint32_t)best;
+    ind2 = o >= (1u << 30) ? c - 1 - (int)(o - (1u << 30)) : c + 1 + (int)o;
+  }
+}
+
+// surface association (:590-650): closest, the best of the same / lower ring (min2) and of the
+// higher rings (min3) in the forward window; mirrored in the backward window.
+LOAM_D void wave_assoc_surf(const float4* SL, int S, int fwd_end, uint64_t nn, float4 sel, int& ind1,
+                            int& ind2, int& ind3) {
+  const int lane = lane_id();
+  ind1 = ind2 = ind3 = -1;
+  if (nn == ~0ull) return;
+  const float d0 = __uint_as_float((uint32_t)(nn >> 32));
+  if (!(D(d0) < 25)) return;
+  const int c = (int)(uint32_t)nn;
+  ind1 = c;
+  const int scan = (int)SL[c].w;
+  uint64_t best2 = ~0ull, best3 = ~0ull;
+  for (int base = c + 1; base < fwd_end; base += 64) {
+    const int j = base + lane;
+    const bool inr = j < fwd_end;
+    const float4 a = inr ? SL[j] : make_float4(0, 0, 0, 0);
+    const int r = (int)a.w;
+    const uint64_t mb = __ballot(inr && D(r) > scan + 2.5);
+    const int limit = mb ? __ffsll((unsigned long long)mb) - 1 : 64;
+    if (inr && lane < limit) {
+      const float d = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
+      if (d < 25) {
+        const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)(j - c - 1);
+        if (r <= scan) best2 = key < best2 ? key : best2;
+        else best3 = key < best3 ? key : best3;
+      }
+    }
+    if (mb) break;
+  }
+  for (int base = c - 1; base >= 0; base -= 64) {
+    const int j = base - lane;
+    const bool inr = j >= 0;
+    const float4 a = inr ? SL[j] : make_float4(0, 0, 0, 0);
+    const int r = (int)a.w;
+    const uint64_t mb = __ballot(inr && D(r) < scan - 2.5);
+    const int limit = mb ? __ffsll((unsigned long long)mb) - 1 : 64;
+    if (inr && lane < limit) {
+      const float d = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
+      if (d < 25) {
+        const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)((1u << 30) + (c - 1 - j));
+        if (r >= scan) best2 = key < best2 ? key : best2;
+        else best3 = key < best3 ? key : best3;
+      }
+    }
+    if (mb) break;
+  }
+  best2 = wave_min_u64(best2);
+  best3 = wave_min_u64(best3);
+  auto decode = [c](uint64_t k) {
+    const uint32_t o = (uint32_t)k;
+    return o >= (1u << 30) ? c - 1 - (int)(o - (1u << 30)) : c + 1 + (int)o;
+  };
+  if (best2 != ~0ull) ind2 = decode(best2);
+  if (best3 != ~0ull) ind3 = decode(best3);
+}
+
+struct OdShared {
+  float4 sel[kOdMaxQ];
+  int ind[3][kOdMaxQ];
+  double red[kOdWaves][27];
+  int cells[kOdWaves][64];
+  int scratch[16];
+  float trig[6];
+  float transform[6];
+  float lm_ws[loamla::kLmWs];
+  int lm_iws[12];
+  float AtA[36], AtB[6], X[6];
+  int nrows, stop;
+};
+
+}  // namespace
+
+__global__ __launch_bounds__(kOdThreads) void k_od_solve(OdBuffers b, FeatView f, int last_buf) {
+  const int p = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  __shared__ OdShared sh;
+  float* st = b.state + (size_t)p * kOdStateFloats;
+  int* ist = b.istate + (size_t)p * kOdStateInts;
+  const loampose::Imu imu = load_imu(st);
+  const int nc = f.count(p, 0), ns = f.count(p, 2);
+  const float4* sharp = f.sharp + (size_t)p * f.sharp_stride;
+  const float4* flat = f.flat + (size_t)p * f.flat_stride;
+  const int C = b.nlast[(p * 2 + last_buf) * 2 + 0], S = b.nlast[(p * 2 + last_buf) * 2 + 1];
+  const float4* CL = b.lastC + ((size_t)last_buf * b.P + p) * b.capC;
+  const float4* SL = b.lastS + ((size_t)last_buf * b.P + p) * b.capS;
+  const int* hcs = b.hC_start + ((size_t)last_buf * b.P + p) * (b.tC + 1);
+  const int* hss = b.hS_start + ((size_t)last_buf * b.P + p) * (b.tS + 1);
+  const float4* hcp = b.hC_pts + ((size_t)last_buf * b.P + p) * b.capC;
+  const float4* hsp = b.hS_pts + ((size_t)last_buf * b.P + p) * b.capS;
+  const int TC = b.hC_T[last_buf * b.P + p], TS = b.hS_T[last_buf * b.P + p];
+  float4* rows_pt = b.rows_pt + (size_t)p * b.cap_rows;
+  float4* rows_cf = b.rows_cf + (size_t)p * b.cap_rows;
+  const int nq = nc + ns;
+  if (tid == 0) {
+    // :461-463 constant-velocity IMU prior (zero without IMU)
+    const float scanPeriod = 0.1f;
+    st[3] -= imu.veloX * scanPeriod;
+    st[4] -= imu.veloY * scanPeriod;
+    st[5] -= imu.veloZ * scanPeriod;
+    for (int k = 0; k < 6; ++k) sh.transform[k] = st[k];
+    sh.nrows = 0;
+    sh.stop = 0;
+  }
+  __syncthreads();
+  int iters = 0, assoc = 0;
+  long rows_sum = 0;
+  const bool run_lm = ist[kIsCornerLastNum] > 10 && ist[kIsSurfLastNum] > 100;
+  if (run_lm && nq > kOdMaxQ) {
+    if (tid == 0) ist[kIsErr] |= ERR_CAP_ROWS;
+  } else if (run_lm) {
+    for (int iter = 0; iter < b.max_iter; ++iter) {
+      ++iters;
+      // TransformToStart of every query point (:472, :587)
+      for (int q = tid; q < nq; q += kOdThreads)
+        sh.sel[q] = loampose::transform_to_start(sh.transform, q < nc ? sharp[q] : flat[q - nc]);
+      __syncthreads();
+      if (iter % 5 == 0) {  // association (Q10)
+        ++assoc;
+        for (int q = w; q < nq; q += kOdWaves) {
+          const float4 s4 = sh.sel[q];
+          int i1, i2, i3 = -1;
+          if (q < nc) {
+            const uint64_t nn = wave_hash_nn(hcs, hcp, TC, CL, C, 1.0f, 1.0f, s4.x, s4.y, s4.z, sh.cells[w]);
+            wave_assoc_corner(CL, C, min(nc, C), nn, s4, i1, i2);
+          } else {
+            const uint64_t nn = wave_hash_nn(hss, hsp, TS, SL, S, 1.0f, 1.0f, s4.x, s4.y, s4.z, sh.cells[w]);
+            wave_assoc_surf(SL, S, min(ns, S), nn, s4, i1, i2, i3);
+          }
+          if (lane == 0) { sh.ind[0][q] = i1; sh.ind[1][q] = i2; sh.ind[2][q] = i3; }
+        }
+        __syncthreads();
+      }
+      // residuals + weights (:530-583, :653-694), rows appended in query order
+      for (int base = 0; base < nq; base += kOdThreads) {
+        const int q = base + tid;
+        int ok = 0;
+        float4 cf = make_float4(0, 0, 0, 0);
+        if (q < nq) {
+          const float4 s4 = sh.sel[q];
+          if (q < nc) {
+            if (sh.ind[1][q] >= 0) {
+              const float4 t1 = CL[sh.ind[0][q]], t2 = CL[sh.ind[1][q]];
+              const float x0 = s4.x, y0 = s4.y, z0 = s4.z;
+              const float x1 = t1.x, y1 = t1.y, z1 = t1.z, x2 = t2.x, y2 = t2.y, z2 = t2.z;
+              const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
+              const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
+              const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
+              const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
+              const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
+              const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
+              const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
+              const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
+              const float ld2 = a012 / l12;
+              float sw = 1;
+              if (iter >= 5) sw = (float)(1 - 1.8 * fabs(D(ld2)));
+              cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
+              ok = (D(sw) > 0.1 && ld2 != 0) ? 1 : 0;
+            }
+          } else if (sh.ind[1][q] >= 0 && sh.ind[2][q] >= 0) {
+            const float4 t1 = SL[sh.ind[0][q]], t2 = SL[sh.ind[1][q]], t3 = SL[sh.ind[2][q]];
+            float pa = (t2.y - t1.y) * (t3.z - t1.z) - (t3.y - t1.y) * (t2.z - t1.z);
+            float pb = (t2.z - t1.z) * (t3.x - t1.x) - (t3.z - t1.z) * (t2.x - t1.x);
+            float pc = (t2.x - t1.x) * (t3.y - t1.y) - (t3.x - t1.x) * (t2.y - t1.y);
+            float pd = -(pa * t1.x + pb * t1.y + pc * t1.z);
+            const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
+            pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+            const float pd2 = pa * s4.x + pb * s4.y + pc * s4.z + pd;
+            float sw = 1;
+            if (iter >= 5)
+              sw = (float)(1 - 1.8 * fabs(D(pd2)) / sqrt(sqrt(D(s4.x * s4.x + s4.y * s4.y + s4.z * s4.z))));
+            cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
+            ok = (D(sw) > 0.1 && pd2 != 0) ? 1 : 0;
+          }
+        }
+        int tot;
+        const int ex = block_excl_scan<kOdThreads>(ok, sh.scratch, tot);
+        const int r0 = sh.nrows;
+        if (ok && r0 + ex < b.cap_rows) {
+          rows_pt[r0 + ex] = q < nc ? sharp[q] : flat[q - nc];
+          rows_cf[r0 + ex] = cf;
+        }
+        __syncthreads();
+        if (tid == 0) sh.nrows = min(r0 + tot, b.cap_rows);
+        __syncthreads();
+      }
+      const int nrows = sh.nrows;
+      rows_sum += nrows;
+      if (nrows < 10) continue;  // :697-700
+      if (tid == 0) {
+        for (int k = 0; k < 3; ++k) {
+          sh.trig[2 * k] = (float)dsin(1 * sh.transform[k]);
+          sh.trig[2 * k + 1] = (float)dcos(1 * sh.transform[k]);
+        }
+      }
+      __syncthreads();
+      // J rows at the current transform (:708-764), JᵀJ / Jᵀb in fp64
+      const float srx = sh.trig[0], crx = sh.trig[1], sry = sh.trig[2], cry = sh.trig[3],
+                  srz = sh.trig[4], crz = sh.trig[5];
+      const float sw = 1;
+      const float tx = sw * sh.transform[3], ty = sw * sh.transform[4], tz = sw * sh.transform[5];
+      double acc[27];
+#pragma unroll
+      for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+      for (int r = tid; r < nrows; r += kOdThreads) {
+        const float4 po = rows_pt[r], c4 = rows_cf[r];
+        float a[6];
+        a[0] = (-sw * crx * sry * srz * po.x + sw * crx * crz * sry * po.y + sw * srx * sry * po.z +
+                sw * tx * crx * sry * srz - sw * ty * crx * crz * sry - sw * tz * srx * sry) * c4.x +
+               (sw * srx * srz * po.x - sw * crz * srx * po.y + sw * crx * po.z + sw * ty * crz * srx -
+                sw * tz * crx - sw * tx * srx * srz) * c4.y +
+               (sw * crx * cry * srz * po.x - sw * crx * cry * crz * po.y - sw * cry * srx * po.z +
+                sw * tz * cry * srx + sw * ty * crx * cry * crz - sw * tx * crx * cry * srz) * c4.z;
+        a[1] = ((-sw * crz * sry - sw * cry * srx * srz) * po.x + (sw * cry * crz * srx - sw * sry * srz) * po.y -
+                sw * crx * cry * po.z + tx * (sw * crz * sry + sw * cry * srx * srz) +
+                ty * (sw * sry * srz - sw * cry * crz * srx) + sw * tz * crx * cry) * c4.x +
+               ((sw * cry * crz - sw * srx * sry * srz) * po.x + (sw * cry * srz + sw * crz * srx * sry) * po.y -
+                sw * crx * sry * po.z + sw * tz * crx * sry - ty * (sw * cry * srz + sw * crz * srx * sry) -
+                tx * (sw * cry * crz - sw * srx * sry * srz)) * c4.z;
+        a[2] = ((-sw * cry * srz - sw * crz * srx * sry) * po.x + (sw * cry * crz - sw * srx * sry * srz) * po.y +
+                tx * (sw * cry * srz + sw * crz * srx * sry) - ty * (sw * cry * crz - sw * srx * sry * srz)) * c4.x +
+               (-sw * crx * crz * po.x - sw * crx * srz * po.y + sw * ty * crx * srz + sw * tx * crx * crz) * c4.y +
+               ((sw * cry * crz * srx - sw * sry * srz) * po.x + (sw * crz * sry + sw * cry * srx * srz) * po.y +
+                tx * (sw * sry * srz - sw * cry * crz * srx) - ty * (sw * crz * sry + sw * cry * srx * srz)) * c4.z;
+        a[3] = -sw * (cry * crz - srx * sry * srz) * c4.x + sw * crx * srz * c4.y -
+               sw * (crz * sry + cry * srx * srz) * c4.z;
+        a[4] = -sw * (cry * srz + crz * srx * sry) * c4.x - sw * crx * crz * c4.y -
+               sw * (sry * srz - cry * crz * srx) * c4.z;
+        a[5] = sw * crx * sry * c4.x - sw * srx * c4.y - sw * crx * cry * c4.z;
+        const float bb = (float)(-0.05 * D(c4.w));
+        int k = 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+          for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
+      }
+#pragma unroll
+      for (int k = 0; k < 27; ++k) {
+        double v = acc[k];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == 0) sh.red[w][k] = v;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        float* AtA = sh.AtA;
+        float* AtB = sh.AtB;
+        float* X = sh.X;
+        double tot[27];
+        for (int k = 0; k < 27; ++k) {
+          double v = sh.red[0][k];
+          for (int ww = 1; ww < kOdWaves; ++ww) v += sh.red[ww][k];
+          tot[k] = v;
+        }
+        int k = 0;
+        for (int i = 0; i < 6; ++i)
+          for (int jj = i; jj < 6; ++jj) {
+            AtA[i * 6 + jj] = (float)tot[k];
+            AtA[jj * 6 + i] = (float)tot[k];
+            ++k;
+          }
+        for (int i = 0; i < 6; ++i) AtB[i] = (float)tot[21 + i];
+        int degen = ist[kIsDegenerate];
+        loamla::lm_step(AtA, AtB, iter, 10.0f, &degen, st + kOdMatP, X, sh.lm_ws, sh.lm_iws);
+        ist[kIsDegenerate] = degen;
+        const bool nan = isnan(X[0]) || isnan(X[1]) || isnan(X[2]) || isnan(X[3]) || isnan(X[4]) || isnan(X[5]);
+        if (!nan)  // Q16
+          for (int q = 0; q < 6; ++q) sh.transform[q] += X[q];
+        const float dR = loamla::delta_r(X), dT = loamla::delta_t(X);
+        sh.stop = (D(dR) < 0.1 && D(dT) < 0.1) ? 1 : 0;
+      }
+      __syncthreads();
+      if (sh.stop) break;
+    }
+  }
+  if (tid == 0) {
+    for (int k = 0; k < 6; ++k) st[k] = sh.transform[k];
+    loampose::accumulate_pose(st, imu, st + kOdSum);  // :830-856
+    ist[kIsIters] = iters;
+    ist[kIsAssoc] = assoc;
+    ist[kIsRows] = (int)rows_sum;
+    ist[kIsQueries] = assoc * nq;
+  }
+}
+
+// TransformToEnd of lessSharp / lessFlat (and full) into Last[dst] / fullEnd[dst] (:875-891).
+// mode 0: copy raw (the init frame, :427-434); 1: zero transform (batch seeding); 2: solved transform
+__global__ __launch_bounds__(256) void k_od_end(OdBuffers b, FeatView f, int dst, int mode, int do_full) {
+  const int p = blockIdx.y;
+  const float* st = b.state + (size_t)p * kOdStateFloats;
+  float t[6] = {0, 0, 0, 0, 0, 0};
+  loampose::Imu imu = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if (mode == 2) {
+    for (int k = 0; k < 6; ++k) t[k] = st[k];
+    imu = load_imu(st);
+  }
+  const int nl = f.count(p, 1), nf = f.count(p, 3), nfull = do_full ? f.nfull(p) : 0;
+  const int cl = min(nl, b.capC), cf = min(nf, b.capS), cu = min(nfull, b.capS);
+  const int total = cl + cf + cu;
+  float4* oc = b.lastC + ((size_t)dst * b.P + p) * b.capC;
+  float4* os = b.lastS + ((size_t)dst * b.P + p) * b.capS;
+  float4* ofl = b.fullEnd + ((size_t)dst * b.P + p) * b.capS;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    float4 a;
+    float4* o;
+    if (i < cl) { a = f.lsharp[(size_t)p * f.lsharp_stride + i]; o = oc + i; }
+    else if (i < cl + cf) { a = f.lflat[(size_t)p * f.lflat_stride + (i - cl)]; o = os + (i - cl); }
+    else { a = f.full[(size_t)p * f.full_stride + (i - cl - cf)]; o = ofl + (i - cl - cf); }
+    *o = mode == 0 ? a : loampose::transform_to_end(t, imu, a);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    b.nlast[(p * 2 + dst) * 2 + 0] = cl;
+    b.nlast[(p * 2 + dst) * 2 + 1] = cf;
+    b.nfullEnd[p * 2 + dst] = cu;
+    if (mode != 0) {  // laserCloudCornerLastNum / SurfLastNum (:901-902); the init frame leaves 0 (Q8)
+      b.istate[(size_t)p * kOdStateInts + kIsCornerLastNum] = cl;
+      b.istate[(size_t)p * kOdStateInts + kIsSurfLastNum] = cf;
+    }
+    if (nl > b.capC || nf > b.capS || nfull > b.capS) b.istate[(size_t)p * kOdStateInts + kIsErr] |= ERR_CAP_ROWS;
+  }
+}
+
+// ---------------------------------------------------------------- host side
+void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
+  b.P = P;
+  b.capC = kLessSharpPerRing * R;
+  b.capS = cap_pts;
+  b.max_iter = max_iter;
+  b.cap_rows = max_iter * (kSharpPerRing + kFlatPerRing) * R;
+  b.tC = next_pow2(b.capC);
+  b.tS = next_pow2(b.capS) > 65536 ? 65536 : next_pow2(b.capS);
+  (void)hipMalloc(&b.state, (size_t)P * kOdStateFloats * sizeof(float));
+  (void)hipMalloc(&b.istate, (size_t)P * kOdStateInts * sizeof(int));
+  (void)hipMalloc(&b.lastC, (size_t)2 * P * b.capC * sizeof(float4));
+  (void)hipMalloc(&b.lastS, (size_t)2 * P * b.capS * sizeof(float4));
+  (void)hipMalloc(&b.fullEnd, (size_t)2 * P * b.capS * sizeof(float4));
+  (void)hipMalloc(&b.nlast, (size_t)P * 4 * sizeof(int));
+  (void)hipMalloc(&b.nfullEnd, (size_t)P * 2 * sizeof(int));
+  (void)hipMalloc(&b.hC_start, (size_t)2 * P * (b.tC + 1) * sizeof(int));
+  (void)hipMalloc(&b.hS_start, (size_t)2 * P * (b.tS + 1) * sizeof(int));
+  (void)hipMalloc(&b.hC_fill, (size_t)P * b.tC * sizeof(int));
+  (void)hipMalloc(&b.hS_fill, (size_t)P * b.tS * sizeof(int));
+  (void)hipMalloc(&b.hC_pts, (size_t)2 * P * b.capC * sizeof(float4));
+  (void)hipMalloc(&b.hS_pts, (size_t)2 * P * b.capS * sizeof(float4));
+  (void)hipMalloc(&b.hC_T, (size_t)2 * P * sizeof(int));
+  (void)hipMalloc(&b.hS_T, (size_t)2 * P * sizeof(int));
+  (void)hipMalloc(&b.rows_pt, (size_t)P * b.cap_rows * sizeof(float4));
+  (void)hipMalloc(&b.rows_cf, (size_t)P * b.cap_rows * sizeof(float4));
+  (void)hipMemset(b.state, 0, (size_t)P * kOdStateFloats * sizeof(float));
+  (void)hipMemset(b.istate, 0, (size_t)P * kOdStateInts * sizeof(int));
+  (void)hipMemset(b.nlast, 0, (size_t)P * 4 * sizeof(int));
+  (void)hipMemset(b.nfullEnd, 0, (size_t)P * 2 * sizeof(int));
+  (void)hipMemset(b.hC_T, 0, (size_t)2 * P * sizeof(int));
+  (void)hipMemset(b.hS_T, 0, (size_t)2 * P * sizeof(int));
+}
+
+void od_free(OdBuffers& b) {
+  void* ptrs[] = {b.state, b.istate, b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
+                  b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T,
+                  b.rows_pt, b.rows_cf};
+  for (void* q : ptrs)
+    if (q) (void)hipFree(q);
+  b = OdBuffers();
+}
+
+// voxel hashes of Last[buf] (corner and surf), 1 m cells
+void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
+  HashJob jc;
+  jc.pts = b.lastC + (size_t)buf * b.P * b.capC;
+  jc.pts_stride = b.capC;
+  jc.count = b.nlast + buf * 2 + 0;
+  jc.count_stride_bytes = 4 * sizeof(int);
+  jc.start = b.hC_start + (size_t)buf * b.P * (b.tC + 1);
+  jc.fill = b.hC_fill;
+  jc.out = b.hC_pts + (size_t)buf * b.P * b.capC;
+  jc.tsize = b.hC_T + buf * b.P;
+  jc.tmax = b.tC;
+  jc.inv_h = 1.0f;
+  hipLaunchKernelGGL(k_hash_build, dim3(b.P), dim3(256), 0, st, jc);
+  HashJob js = jc;
+  js.pts = b.lastS + (size_t)buf * b.P * b.capS;
+  js.pts_stride = b.capS;
+  js.count = b.nlast + buf * 2 + 1;
+  js.start = b.hS_start + (size_t)buf * b.P * (b.tS + 1);
+  js.fill = b.hS_fill;
+  js.out = b.hS_pts + (size_t)buf * b.P * b.capS;
+  js.tsize = b.hS_T + buf * b.P;
+  js.tmax = b.tS;
+  hipLaunchKernelGGL(k_hash_build, dim3(b.P), dim3(256), 0, st, js);
+}
+
+}  // namespace loam

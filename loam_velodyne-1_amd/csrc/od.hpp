@@ -1,0 +1,75 @@
+// Odometry / hash device buffers and kernel declarations (engine-internal).
+#ifndef LOAM_OD_HPP
+#define LOAM_OD_HPP
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "engine.hpp"
+
+namespace loam {
+
+// per-problem float state: transform[6] | transformSum[6] | matP[36] | imu_trans[12]
+constexpr int kOdSum = 6, kOdMatP = 12, kOdImu = 48, kOdStateFloats = 64;
+// per-problem int state
+enum { kIsDegenerate = 0, kIsCornerLastNum, kIsSurfLastNum, kIsIters, kIsAssoc, kIsRows, kIsQueries,
+       kIsErr, kOdStateInts = 16 };
+constexpr int kOdMaxQ = 2304;  // sharp + flat queries per problem (36 per ring x 64 rings)
+
+// read-only view of one feature set per problem (stride = elements between problems)
+struct FeatView {
+  const float4 *sharp, *lsharp, *flat, *lflat, *full;
+  size_t sharp_stride, lsharp_stride, flat_stride, lflat_stride, full_stride;
+  const int* cnt;       // 4 counts per problem at cnt[p * cnt_stride]
+  int cnt_stride;
+  const int* nfull_p;   // full-cloud count at nfull_p[p * nfull_stride]
+  int nfull_stride;
+  __device__ __forceinline__ int count(int p, int k) const { return cnt[p * cnt_stride + k]; }
+  __device__ __forceinline__ int nfull(int p) const { return nfull_p[p * nfull_stride]; }
+};
+
+struct HashJob {
+  const float4* pts;    // cloud of problem p at pts + p * pts_stride
+  size_t pts_stride;
+  const int* count;     // count of problem p at (char*)count + p * count_stride_bytes
+  size_t count_stride_bytes;
+  int* start;           // [P][tmax + 1]
+  int* fill;            // [P][tmax]
+  float4* out;          // [P][pts_stride]
+  int* tsize;           // [P] table size used
+  int tmax;
+  float inv_h;
+};
+
+struct OdBuffers {
+  int P = 0, capC = 0, capS = 0, cap_rows = 0, tC = 0, tS = 0, max_iter = 25;
+  float* state = nullptr;   // [P][kOdStateFloats]
+  int* istate = nullptr;    // [P][kOdStateInts]
+  float4* lastC = nullptr;  // [2][P][capC]
+  float4* lastS = nullptr;  // [2][P][capS]
+  float4* fullEnd = nullptr;  // [2][P][capS]
+  int* nlast = nullptr;     // [P][2][2]
+  int* nfullEnd = nullptr;  // [P][2]
+  int* hC_start = nullptr;  // [2][P][tC+1]
+  int* hS_start = nullptr;  // [2][P][tS+1]
+  int* hC_fill = nullptr;   // [P][tC]
+  int* hS_fill = nullptr;   // [P][tS]
+  float4* hC_pts = nullptr; // [2][P][capC]
+  float4* hS_pts = nullptr; // [2][P][capS]
+  int* hC_T = nullptr;      // [2][P]
+  int* hS_T = nullptr;      // [2][P]
+  float4* rows_pt = nullptr;  // [P][cap_rows]
+  float4* rows_cf = nullptr;
+};
+
+__global__ void k_hash_build(HashJob j);
+__global__ void k_od_solve(OdBuffers b, FeatView f, int last_buf);
+__global__ void k_od_end(OdBuffers b, FeatView f, int dst, int mode, int do_full);
+
+void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter);
+void od_free(OdBuffers& b);
+void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st);
+
+}  // namespace loam
+
+#endif

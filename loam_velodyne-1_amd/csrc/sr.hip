@@ -1,0 +1,664 @@
+// Scan registration on gfx950: laserCloudHandler (/root/reference/src/scanRegistration.cpp:211-636)
+// as four kernels over a batch of sweeps.
+//
+//  k_sr_ring_sort   one workgroup per sweep: NaN filter, axis swap, ring ID, orientation with the
+//                   sequential halfPassed flag (a block min-reduction finds the flip point), relTime,
+//                   intensity, stable ring bucketing (per-tile ring counts + wave ballot ranks).
+//                   src/scanRegistration.cpp:225-357
+//  k_sr_features    256-point tiles with a 6-point halo in LDS: 11-tap curvature, ring bounds
+//                   (last-write-wins transitions = atomicMax), occlusion / parallel-beam marks as a
+//                   gather over the 12 neighbouring events.  :358-452
+//  k_sr_select      one workgroup per (sweep, ring): the six segment sorts (LDS bitonic on
+//                   (curvature, position) = the reference's stable insertion sort), the greedy
+//                   sharp / flat picks by one wave with ballots, lessFlat candidates, PCL VoxelGrid
+//                   0.2 of the ring (LDS sort by (voxel, position), ordered per-voxel sums).  :460-581
+//                   Rings are independent whenever their spans are >5 points apart (always for
+//                   sweeps with no empty ring); otherwise one workgroup walks the rings in order.
+//  k_sr_compact     per sweep: ring-major concatenation of the picks and the downsampled lessFlat.
+//
+// HBM traffic per sweep (algorithmic): 16 B/pt raw read, 16 B/pt ring-sorted
+// write + read, 16 B per feature point written.
+#include "dev_common.hpp"
+#include "engine.hpp"
+
+using namespace loamdev;
+
+namespace loam {
+
+namespace {
+
+LOAM_D int ring_id(const SrParams& p, float angle) {
+  if (p.ring_model == LOAM_RING_LINEAR) {
+    const float step = (p.ring_hi - p.ring_lo) / (float)(p.R - 1);
+    const float angleID = (angle - p.ring_lo) / step;
+    return (int)(angleID + 0.5f);
+  }
+  int rounded = (int)(D(angle) + (D(angle) < 0.0 ? -0.5 : +0.5));
+  return rounded > 0 ? rounded : rounded + (p.R - 1);
+}
+
+LOAM_D float ori_first(float ori, float startOri) {  // :263-268
+  if (D(ori) < D(startOri) - M_PI / 2) ori = (float)(D(ori) + 2 * M_PI);
+  else if (D(ori) > D(startOri) + M_PI * 3 / 2) ori = (float)(D(ori) - 2 * M_PI);
+  return ori;
+}
+LOAM_D float ori_second(float ori, float endOri) {  // :274-280
+  ori = (float)(D(ori) + 2 * M_PI);
+  if (D(ori) < D(endOri) - M_PI * 3 / 2) ori = (float)(D(ori) + 2 * M_PI);
+  else if (D(ori) > D(endOri) + M_PI / 2) ori = (float)(D(ori) - 2 * M_PI);
+  return ori;
+}
+LOAM_D bool finite3(const float4& q) {
+  return isfinite(q.x) && isfinite(q.y) && isfinite(q.z);
+}
+
+// ---------------------------------------------------------------- ring sort
+__global__ __launch_bounds__(kSrThreads) void k_sr_ring_sort(SrBuffers b, SrParams p) {
+  const int s = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int n = b.raw_n[s];
+  const float4* raw = b.raw + (size_t)s * b.cap;
+  float* tori = b.tmp_ori + (size_t)s * b.cap;
+  uint8_t* tsid = b.tmp_sid + (size_t)s * b.cap;
+  const int R = p.R, ntiles = (n + kSrThreads - 1) / kSrThreads;
+  int* tc = b.tilecnt + (size_t)s * b.ntiles() * R;
+  __shared__ int sh_first, sh_last, sh_F, sh_total;
+  __shared__ float sh_start, sh_end;
+  __shared__ int sh_cnt[64];
+  __shared__ int sh_wcnt[kSrThreads / 64][64];
+  __shared__ int sh_base[64];
+  if (tid == 0) { sh_first = 0x7fffffff; sh_last = -1; sh_F = 0x7fffffff; }
+  __syncthreads();
+  int f = 0x7fffffff, l = -1;
+  for (int i = tid; i < n; i += kSrThreads) {
+    if (finite3(raw[i])) { f = min(f, i); l = max(l, i); }
+  }
+  f = wave_min_i(f);
+  l = wave_max_i(l);
+  if (lane == 0) { atomicMin(&sh_first, f); atomicMax(&sh_last, l); }
+  __syncthreads();
+  if (sh_last < 0) {
+    if (tid == 0) { b.n_full[s] = 0; b.err[s] |= ERR_EMPTY; }
+    return;
+  }
+  if (tid == 0) {  // :230-238
+    float4 a = raw[sh_first], z = raw[sh_last];
+    float startOri = -atan2f(a.y, a.x);
+    float endOri = (float)(D(-atan2f(z.y, z.x)) + 2 * M_PI);
+    if (D(endOri - startOri) > 3 * M_PI) endOri = (float)(D(endOri) - 2 * M_PI);
+    else if (D(endOri - startOri) < M_PI) endOri = (float)(D(endOri) + 2 * M_PI);
+    sh_start = startOri;
+    sh_end = endOri;
+  }
+  __syncthreads();
+  const float startOri = sh_start, endOri = sh_end;
+  // phase A: ring id + first-branch orientation; the halfPassed flip point F
+  int Floc = 0x7fffffff;
+  for (int t = 0; t < ntiles; ++t) {
+    if (tid < R) sh_cnt[tid] = 0;
+    __syncthreads();
+    const int i = t * kSrThreads + tid;
+    if (i < n) {
+      const float4 q = raw[i];
+      uint8_t sid = 255;
+      float ori = 0.0f;
+      if (finite3(q)) {
+        const float px = q.y, py = q.z, pz = q.x;
+        float angle = (float)(atan(D(py) / sqrt(D(px * px + pz * pz))) * 180 / M_PI);
+        int scanID = ring_id(p, angle);
+        if (scanID >= 0 && scanID <= R - 1) {
+          sid = (uint8_t)scanID;
+          ori = -atan2f(px, pz);
+          float o1 = ori_first(ori, startOri);
+          if (D(o1 - startOri) > M_PI) Floc = min(Floc, i);
+          atomicAdd(&sh_cnt[scanID], 1);
+        }
+      }
+      tori[i] = ori;
+      tsid[i] = sid;
+    }
+    __syncthreads();
+    if (tid < R) tc[t * R + tid] = sh_cnt[tid];
+    __syncthreads();
+  }
+  Floc = wave_min_i(Floc);
+  if (lane == 0) atomicMin(&sh_F, Floc);
+  __threadfence_block();
+  __syncthreads();
+  // phase B: per-ring exclusive scan over tiles, ring bases
+  if (tid < R) {
+    int run = 0;
+    for (int t = 0; t < ntiles; ++t) {
+      int c = tc[t * R + tid];
+      tc[t * R + tid] = run;
+      run += c;
+    }
+    sh_cnt[tid] = run;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int r = 0; r < R; ++r) { sh_base[r] = run; run += sh_cnt[r]; }
+    sh_total = run;
+  }
+  __syncthreads();
+  const int F = sh_F;
+  // phase C: stable scatter into ring order
+  for (int t = 0; t < ntiles; ++t) {
+    const int i = t * kSrThreads + tid;
+    int sid = 255;
+    if (i < n) sid = tsid[i];
+    const bool valid = (i < n) && sid != 255;
+    if (lane < R) sh_wcnt[w][lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    int rank = 0;
+    uint64_t mval = __ballot(valid);
+    while (mval) {
+      const int leader = __ffsll((unsigned long long)mval) - 1;
+      const int rl = __shfl(sid, leader, 64);
+      const uint64_t mm = __ballot(valid && sid == rl);
+      if (valid && sid == rl) rank = __popcll(mm & lanemask_lt());
+      if (lane == leader) sh_wcnt[w][rl] = __popcll(mm);
+      mval &= ~mm;
+    }
+    __syncthreads();
+    if (valid) {
+      int pos = sh_base[sid] + tc[t * R + sid] + rank;
+      for (int v = 0; v < w; ++v) pos += sh_wcnt[v][sid];
+      const float4 q = raw[i];
+      float ori = tori[i];
+      ori = (i <= F) ? ori_first(ori, startOri) : ori_second(ori, endOri);
+      float relTime = (ori - startOri) / (endOri - startOri);
+      float4 o;
+      o.x = q.y;
+      o.y = q.z;
+      o.z = q.x;
+      o.w = (float)(sid + 0.1 * D(relTime));
+      b.full[(size_t)s * b.cap + pos] = o;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) b.n_full[s] = sh_total;
+}
+
+// ---------------------------------------------------------------- curvature + marks
+constexpr int kFeatTile = 256;
+
+__global__ __launch_bounds__(kFeatTile) void k_sr_features(SrBuffers b, SrParams p) {
+  const int s = blockIdx.y, tid = threadIdx.x;
+  const int n = b.n_full[s];
+  const int i0 = blockIdx.x * kFeatTile;
+  if (i0 >= n) return;
+  const float4* pts = b.full + (size_t)s * b.cap;
+  __shared__ float4 sp[kFeatTile + 12];
+  __shared__ int8_t evt[kFeatTile + 12];
+  for (int t = tid; t < kFeatTile + 12; t += kFeatTile) {
+    int g = i0 - 6 + t;
+    if (g >= 0 && g < n) sp[t] = pts[g];
+  }
+  __syncthreads();
+  for (int t = tid; t < kFeatTile + 11; t += kFeatTile) {  // occlusion events (:395-438)
+    const int k = i0 - 6 + t;
+    int8_t e = 0;
+    if (k >= 5 && k <= n - 7) {
+      const float4 a = sp[t], c = sp[t + 1];
+      float dX = c.x - a.x, dY = c.y - a.y, dZ = c.z - a.z;
+      float diff = dX * dX + dY * dY + dZ * dZ;
+      if (D(diff) > 0.1) {
+        float depth1 = (float)sqrt(D(a.x * a.x + a.y * a.y + a.z * a.z));
+        float depth2 = (float)sqrt(D(c.x * c.x + c.y * c.y + c.z * c.z));
+        if (depth1 > depth2) {
+          dX = c.x - a.x * depth2 / depth1;
+          dY = c.y - a.y * depth2 / depth1;
+          dZ = c.z - a.z * depth2 / depth1;
+          if (sqrt(D(dX * dX + dY * dY + dZ * dZ)) / D(depth2) < 0.1) e = 1;
+        } else {
+          dX = c.x * depth1 / depth2 - a.x;
+          dY = c.y * depth1 / depth2 - a.y;
+          dZ = c.z * depth1 / depth2 - a.z;
+          if (sqrt(D(dX * dX + dY * dY + dZ * dZ)) / D(depth1) < 0.1) e = 2;
+        }
+      }
+    }
+    evt[t] = e;
+  }
+  __syncthreads();
+  const int i = i0 + tid;
+  if (i >= n) return;
+  const int li = tid + 6;
+  const size_t gi = (size_t)s * b.cap + i;
+  float cv = 0.0f;
+  if (i >= 5 && i < n - 5) {  // :359-378
+    const float4* q = sp + li;
+    float dX = q[-5].x + q[-4].x + q[-3].x + q[-2].x + q[-1].x - 10 * q[0].x + q[1].x + q[2].x +
+               q[3].x + q[4].x + q[5].x;
+    float dY = q[-5].y + q[-4].y + q[-3].y + q[-2].y + q[-1].y - 10 * q[0].y + q[1].y + q[2].y +
+               q[3].y + q[4].y + q[5].y;
+    float dZ = q[-5].z + q[-4].z + q[-3].z + q[-2].z + q[-1].z - 10 * q[0].z + q[1].z + q[2].z +
+               q[3].z + q[4].z + q[5].z;
+    cv = dX * dX + dY * dY + dZ * dZ;
+    // ring bounds (:383-390): the last transition into ring v wins
+    const int v = (int)q[0].w;
+    const int pv = (i == 5) ? -1 : (int)q[-1].w;
+    if (v != pv && v > 0 && v < p.R) {
+      atomicMax(&b.ring_se[s * 2 * p.R + v], i + 5);
+      atomicMax(&b.ring_se[s * 2 * p.R + p.R + v - 1], i - 5);
+    }
+  }
+  int pk = 0;
+  for (int k = 0; k <= 5; ++k) pk |= (evt[li + k] == 1);
+  for (int k = 1; k <= 6; ++k) pk |= (evt[li - k] == 2);
+  if (i >= 5 && i <= n - 7) {  // :440-451
+    const float4 a = sp[li - 1], c = sp[li], e = sp[li + 1];
+    float dX = e.x - c.x, dY = e.y - c.y, dZ = e.z - c.z;
+    float diff = dX * dX + dY * dY + dZ * dZ;
+    float dX2 = c.x - a.x, dY2 = c.y - a.y, dZ2 = c.z - a.z;
+    float diff2 = dX2 * dX2 + dY2 * dY2 + dZ2 * dZ2;
+    float dis = c.x * c.x + c.y * c.y + c.z * c.z;
+    if (D(diff) > 0.0002 * D(dis) && D(diff2) > 0.0002 * D(dis)) pk = 1;
+  }
+  b.curv[gi] = cv;
+  b.picked[gi] = (uint8_t)pk;
+  b.sortind[gi] = i;
+  b.label[gi] = 0;
+}
+
+// ---------------------------------------------------------------- per-ring selection
+struct SelShared {
+  uint64_t keys[kRingCap];
+  int sidx[kRingCap];
+  int tmp[kSegCap];     // segment permutation scratch
+  int cand[kRingCap];   // lessFlat candidate positions of the ring
+  uint8_t pk[kRingCap + 16];
+  int8_t lab[kRingCap + 16];
+  int se[128];
+  int picks[kSharpPerRing + kLessSharpPerRing + kFlatPerRing];
+  int scratch[16];
+  float red[6][kSelThreads / 64];
+  int nsharp, nlsharp, nflat, ncand, wf, wlo, whi, lo, hi;
+};
+
+LOAM_D void mark_neighbours(const float4* pts, int n, int ind, uint8_t* pk, int wlo) {
+  for (int l = 1; l <= 5; ++l) {  // :495-507
+    if (ind + l >= n) break;
+    const float4 a = pts[ind + l], c = pts[ind + l - 1];
+    float ex = a.x - c.x, ey = a.y - c.y, ez = a.z - c.z;
+    if (D(ex * ex + ey * ey + ez * ez) > 0.05) break;
+    pk[ind + l - wlo] = 1;
+  }
+  for (int l = -1; l >= -5; --l) {  // :508-520
+    if (ind + l < 0) break;
+    const float4 a = pts[ind + l], c = pts[ind + l + 1];
+    float ex = a.x - c.x, ey = a.y - c.y, ez = a.z - c.z;
+    if (D(ex * ex + ey * ey + ez * ez) > 0.05) break;
+    pk[ind + l - wlo] = 1;
+  }
+}
+
+// processes ring q of sweep s; `seq` = fallback mode (rings walked in order by one workgroup)
+LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq, SelShared& sh) {
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const float4* pts = b.full + (size_t)s * b.cap;
+  const float* curv = b.curv + (size_t)s * b.cap;
+  const int sq = sh.se[q], eq = sh.se[R + q];
+  const int lo = sq, hi = eq - 1;
+  if (tid == 0) { sh.nsharp = 0; sh.nlsharp = 0; sh.nflat = 0; sh.ncand = 0; }
+  int* st_cnt = b.st_cnt + (size_t)(s * R + q) * 4;
+  if (lo > hi) {  // every segment is empty
+    if (tid < 4) st_cnt[tid] = 0;
+    return;
+  }
+  if (hi - lo + 1 > kRingCap || lo < 0 || hi >= n) {
+    if (tid == 0) b.err[s] |= ERR_CAP_RING;
+    if (tid < 4) st_cnt[tid] = 0;
+    return;
+  }
+  // window of point indices this ring may touch: span and the indices its sortInd holds, +-5
+  int vmin = lo, vmax = hi;
+  if (seq) {
+    for (int k = lo + tid; k <= hi; k += kSelThreads) {
+      int v = b.sortind[(size_t)s * b.cap + k];
+      vmin = min(vmin, v);
+      vmax = max(vmax, v);
+    }
+    vmin = wave_min_i(vmin);
+    vmax = wave_max_i(vmax);
+    if (lane == 0) { sh.scratch[w] = vmin; sh.scratch[8 + w] = vmax; }
+    __syncthreads();
+    for (int v = 0; v < kSelThreads / 64; ++v) {
+      vmin = min(vmin, sh.scratch[v]);
+      vmax = max(vmax, sh.scratch[8 + v]);
+    }
+    __syncthreads();
+  }
+  const int wlo = max(0, vmin - 5), whi = min(n - 1, vmax + 5);
+  if (whi - wlo + 1 > kRingCap + 16) {
+    if (tid == 0) b.err[s] |= ERR_CAP_RING;
+    if (tid < 4) st_cnt[tid] = 0;
+    return;
+  }
+  for (int k = wlo + tid; k <= whi; k += kSelThreads) {
+    sh.pk[k - wlo] = b.picked[(size_t)s * b.cap + k];
+    sh.lab[k - wlo] = b.label[(size_t)s * b.cap + k];
+  }
+  for (int k = lo + tid; k <= hi; k += kSelThreads) sh.sidx[k - lo] = b.sortind[(size_t)s * b.cap + k];
+  __syncthreads();
+
+  for (int j = 0; j < 6; ++j) {
+    const int sp = (sq * (6 - j) + eq * j) / 6;
+    const int ep = (sq * (5 - j) + eq * (j + 1)) / 6 - 1;
+    if (sp < 0 || ep >= n) continue;
+    const int len = ep - sp + 1;
+    if (len <= 0) continue;
+    if (len > kSegCap) {
+      if (tid == 0) b.err[s] |= ERR_CAP_RING;
+      continue;
+    }
+    // (:466-474) stable ascending sort of sortInd[sp..ep] by curvature
+    const int P2 = next_pow2(len);
+    for (int t = tid; t < P2; t += kSelThreads)
+      sh.keys[t] = t < len ? (((uint64_t)fkey(curv[sh.sidx[sp - lo + t]]) << 32) | (uint32_t)t) : ~0ull;
+    __syncthreads();
+    block_bitonic_sort<kSelThreads>(sh.keys, P2);
+    for (int t = tid; t < len; t += kSelThreads) sh.tmp[t] = sh.sidx[sp - lo + (int)(sh.keys[t] & 0xffffffffu)];
+    __syncthreads();
+    for (int t = tid; t < len; t += kSelThreads) sh.sidx[sp - lo + t] = sh.tmp[t];
+    __syncthreads();
+    if (w == 0) {
+      // (:476-522) sharp / less sharp, walking from the largest curvature down
+      int largest = 0;
+      bool done = false;
+      for (int base = ep; base >= sp && !done; base -= 64) {
+        const int k = base - lane;
+        const bool inr = k >= sp;
+        const int ind = inr ? sh.sidx[k - lo] : 0;
+        const bool elig = inr && D(curv[ind]) > 0.1;
+        uint64_t remaining = __ballot(elig);
+        while (remaining) {
+          const bool cand = elig && ((remaining >> lane) & 1ull) && sh.pk[ind - wlo] == 0;
+          const uint64_t m = __ballot(cand);
+          if (!m) break;
+          const int f = __ffsll((unsigned long long)m) - 1;
+          largest++;
+          if (largest > 20) { done = true; break; }
+          if (lane == f) {
+            if (largest <= 2) {
+              sh.lab[ind - wlo] = 2;
+              sh.picks[sh.nsharp++] = ind;
+              sh.picks[kSharpPerRing + sh.nlsharp++] = ind;
+            } else {
+              sh.lab[ind - wlo] = 1;
+              sh.picks[kSharpPerRing + sh.nlsharp++] = ind;
+            }
+            sh.pk[ind - wlo] = 1;
+            mark_neighbours(pts, n, ind, sh.pk, wlo);
+          }
+          __threadfence_block();
+          __builtin_amdgcn_wave_barrier();
+          remaining &= ~((2ull << f) - 1ull);
+        }
+      }
+      // (:524-566) flat, walking from the smallest curvature up; break after the 4th push
+      int smallest = 0;
+      done = false;
+      for (int base = sp; base <= ep && !done; base += 64) {
+        const int k = base + lane;
+        const bool inr = k <= ep;
+        const int ind = inr ? sh.sidx[k - lo] : 0;
+        const bool elig = inr && D(curv[ind]) < 0.1;
+        uint64_t remaining = __ballot(elig);
+        while (remaining) {
+          const bool cand = elig && ((remaining >> lane) & 1ull) && sh.pk[ind - wlo] == 0;
+          const uint64_t m = __ballot(cand);
+          if (!m) break;
+          const int f = __ffsll((unsigned long long)m) - 1;
+          if (lane == f) {
+            sh.lab[ind - wlo] = -1;
+            sh.picks[kSharpPerRing + kLessSharpPerRing + sh.nflat++] = ind;
+          }
+          smallest++;
+          if (smallest >= 4) { done = true; break; }
+          if (lane == f) {
+            sh.pk[ind - wlo] = 1;
+            mark_neighbours(pts, n, ind, sh.pk, wlo);
+          }
+          __threadfence_block();
+          __builtin_amdgcn_wave_barrier();
+          remaining &= ~((2ull << f) - 1ull);
+        }
+      }
+    }
+    __syncthreads();
+    // (:568-572) lessFlat candidates of this segment, in position order
+    int run = sh.ncand;
+    for (int base = sp; base <= ep; base += kSelThreads) {
+      const int k = base + tid;
+      const int flag = (k <= ep && sh.lab[k - wlo] <= 0) ? 1 : 0;
+      int tot;
+      const int ex = block_excl_scan<kSelThreads>(flag, sh.scratch, tot);
+      if (flag) sh.cand[run + ex] = k;
+      run += tot;
+    }
+    __syncthreads();
+    if (tid == 0) sh.ncand = run;
+    __syncthreads();
+  }
+  // ---- PCL VoxelGrid 0.2 of the ring's lessFlat candidates (:575-579)
+  const int nc = sh.ncand;
+  float4* outp = b.st_lflat + (size_t)(s * R + q) * kRingCap;
+  float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+  for (int t = tid; t < nc; t += kSelThreads) {
+    const float4 a = pts[sh.cand[t]];
+    mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
+    mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
+  }
+  for (int d = 0; d < 3; ++d) {
+    mn[d] = wave_min_f(mn[d]);
+    mx[d] = wave_max_f(mx[d]);
+    if (lane == 0) { sh.red[d][w] = mn[d]; sh.red[3 + d][w] = mx[d]; }
+  }
+  __syncthreads();
+  for (int d = 0; d < 3; ++d)
+    for (int v = 0; v < kSelThreads / 64; ++v) {
+      mn[d] = fminf(mn[d], sh.red[d][v]);
+      mx[d] = fmaxf(mx[d], sh.red[3 + d][v]);
+    }
+  __syncthreads();
+  int nout = 0;
+  if (nc > 0) {
+    const float inv = 1.0f / 0.2f;
+    const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
+    const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
+    const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
+    if (dx * dy * dz > (int64_t)0x7fffffff) {  // "leaf size too small": output = input
+      for (int t = tid; t < nc; t += kSelThreads) outp[t] = pts[sh.cand[t]];
+      nout = nc;
+    } else {
+      int minb[3], maxb[3];
+      for (int d = 0; d < 3; ++d) {
+        minb[d] = (int)floorf(mn[d] * inv);
+        maxb[d] = (int)floorf(mx[d] * inv);
+      }
+      const int divx = maxb[0] - minb[0] + 1, divy = maxb[1] - minb[1] + 1;
+      const int mul1 = divx, mul2 = divx * divy;
+      const int P2 = next_pow2(nc);
+      for (int t = tid; t < P2; t += kSelThreads) {
+        uint64_t key = ~0ull;
+        if (t < nc) {
+          const float4 a = pts[sh.cand[t]];
+          int i0 = (int)(floorf(a.x * inv) - (float)minb[0]);
+          int i1 = (int)(floorf(a.y * inv) - (float)minb[1]);
+          int i2 = (int)(floorf(a.z * inv) - (float)minb[2]);
+          uint32_t idx = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
+          key = ((uint64_t)idx << 32) | (uint32_t)t;
+        }
+        sh.keys[t] = key;
+      }
+      __syncthreads();
+      block_bitonic_sort<kSelThreads>(sh.keys, P2);
+      int run = 0;
+      for (int base = 0; base < nc; base += kSelThreads) {
+        const int t = base + tid;
+        const int head = (t < nc && (t == 0 || (sh.keys[t] >> 32) != (sh.keys[t - 1] >> 32))) ? 1 : 0;
+        int tot;
+        const int ex = block_excl_scan<kSelThreads>(head, sh.scratch, tot);
+        if (head) {
+          const uint32_t vk = (uint32_t)(sh.keys[t] >> 32);
+          float sx = 0, sy = 0, sz = 0, si = 0;
+          int e = t;
+          while (e < nc && (uint32_t)(sh.keys[e] >> 32) == vk) {
+            const float4 a = pts[sh.cand[(int)(sh.keys[e] & 0xffffffffu)]];
+            sx += a.x; sy += a.y; sz += a.z; si += a.w;
+            ++e;
+          }
+          const float cnt = (float)(e - t);
+          outp[run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+        }
+        run += tot;
+      }
+      nout = run;
+    }
+  }
+  // pick lists -> staging
+  const int ns = sh.nsharp, nl = sh.nlsharp, nf = sh.nflat;
+  for (int t = tid; t < ns; t += kSelThreads) b.st_sharp[(size_t)(s * R + q) * kSharpPerRing + t] = sh.picks[t];
+  for (int t = tid; t < nl; t += kSelThreads)
+    b.st_lsharp[(size_t)(s * R + q) * kLessSharpPerRing + t] = sh.picks[kSharpPerRing + t];
+  for (int t = tid; t < nf; t += kSelThreads)
+    b.st_flat[(size_t)(s * R + q) * kFlatPerRing + t] = sh.picks[kSharpPerRing + kLessSharpPerRing + t];
+  if (tid == 0) { st_cnt[0] = ns; st_cnt[1] = nl; st_cnt[2] = nf; st_cnt[3] = nout; }
+  if (seq) {  // write the shared state back for the next ring (one workgroup, ordered)
+    for (int k = wlo + tid; k <= whi; k += kSelThreads) {
+      b.picked[(size_t)s * b.cap + k] = sh.pk[k - wlo];
+      b.label[(size_t)s * b.cap + k] = sh.lab[k - wlo];
+    }
+    for (int k = lo + tid; k <= hi; k += kSelThreads) b.sortind[(size_t)s * b.cap + k] = sh.sidx[k - lo];
+    __threadfence();
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kSelThreads) void k_sr_select(SrBuffers b, SrParams p) {
+  const int q = blockIdx.x, s = blockIdx.y, tid = threadIdx.x, R = p.R;
+  const int n = b.n_full[s];
+  __shared__ SelShared sh;
+  if (tid < R) {
+    int st = b.ring_se[s * 2 * R + tid], en = b.ring_se[s * 2 * R + R + tid];
+    if (tid == 0) st = 5;            // :392
+    if (tid == R - 1) en = n - 5;    // :393
+    sh.se[tid] = st;
+    sh.se[R + tid] = en;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    // rings are independent when their active spans [start, end-1] are more than 5 points apart
+    int wf = 1, prev_hi = -100000;
+    int order[64], na = 0;
+    for (int r = 0; r < R; ++r)
+      if (sh.se[r] <= sh.se[R + r] - 1) order[na++] = r;
+    for (int a = 1; a < na; ++a) {
+      int v = order[a], c = a;
+      while (c > 0 && sh.se[order[c - 1]] > sh.se[v]) { order[c] = order[c - 1]; --c; }
+      order[c] = v;
+    }
+    for (int a = 0; a < na; ++a) {
+      int lo = sh.se[order[a]], hi = sh.se[R + order[a]] - 1;
+      if (lo < 0 || hi >= n || lo - prev_hi <= 5) wf = 0;
+      prev_hi = hi;
+    }
+    sh.wf = wf;
+  }
+  __syncthreads();
+  if (n <= 0) {
+    if (tid < 4) b.st_cnt[(size_t)(s * R + q) * 4 + tid] = 0;
+    return;
+  }
+  if (sh.wf) {
+    select_ring(b, s, q, R, n, false, sh);
+  } else if (q == 0) {
+    for (int r = 0; r < R; ++r) select_ring(b, s, r, R, n, true, sh);
+  }
+}
+
+// ---------------------------------------------------------------- compaction
+__global__ __launch_bounds__(256) void k_sr_compact(SrBuffers b, SrParams p) {
+  const int s = blockIdx.x, tid = threadIdx.x, R = p.R;
+  __shared__ int off[4][65];
+  if (tid == 0) {
+    int run[4] = {0, 0, 0, 0};
+    for (int r = 0; r < R; ++r)
+      for (int k = 0; k < 4; ++k) {
+        off[k][r] = run[k];
+        run[k] += b.st_cnt[(size_t)(s * R + r) * 4 + k];
+      }
+    for (int k = 0; k < 4; ++k) { off[k][R] = run[k]; b.cnt[s * 4 + k] = run[k]; }
+  }
+  __syncthreads();
+  const float4* pts = b.full + (size_t)s * b.cap;
+  for (int r = 0; r < R; ++r) {
+    const int* c = b.st_cnt + (size_t)(s * R + r) * 4;
+    for (int t = tid; t < c[0]; t += 256)
+      b.sharp[(size_t)s * kSharpPerRing * R + off[0][r] + t] =
+          pts[b.st_sharp[(size_t)(s * R + r) * kSharpPerRing + t]];
+    for (int t = tid; t < c[1]; t += 256)
+      b.lsharp[(size_t)s * kLessSharpPerRing * R + off[1][r] + t] =
+          pts[b.st_lsharp[(size_t)(s * R + r) * kLessSharpPerRing + t]];
+    for (int t = tid; t < c[2]; t += 256)
+      b.flat[(size_t)s * kFlatPerRing * R + off[2][r] + t] =
+          pts[b.st_flat[(size_t)(s * R + r) * kFlatPerRing + t]];
+    for (int t = tid; t < c[3]; t += 256)
+      b.lflat[(size_t)s * b.cap + off[3][r] + t] = b.st_lflat[(size_t)(s * R + r) * kRingCap + t];
+  }
+}
+
+}  // namespace
+
+#define HIPCHK(x) (void)(x)
+
+void sr_alloc(SrBuffers& b, int S, int cap, int R) {
+  b.S = S; b.cap = cap; b.R = R;
+  const size_t n = (size_t)S * cap;
+  HIPCHK(hipMalloc(&b.raw, n * sizeof(float4)));
+  HIPCHK(hipMalloc(&b.raw_n, S * sizeof(int)));
+  HIPCHK(hipMalloc(&b.tmp_ori, n * sizeof(float)));
+  HIPCHK(hipMalloc(&b.tmp_sid, n));
+  HIPCHK(hipMalloc(&b.tilecnt, (size_t)S * b.ntiles() * R * sizeof(int)));
+  HIPCHK(hipMalloc(&b.full, n * sizeof(float4)));
+  HIPCHK(hipMalloc(&b.n_full, S * sizeof(int)));
+  HIPCHK(hipMalloc(&b.curv, n * sizeof(float)));
+  HIPCHK(hipMalloc(&b.picked, n));
+  HIPCHK(hipMalloc(&b.sortind, n * sizeof(int)));
+  HIPCHK(hipMalloc(&b.label, n));
+  HIPCHK(hipMalloc(&b.ring_se, (size_t)S * 2 * R * sizeof(int)));
+  HIPCHK(hipMalloc(&b.st_sharp, (size_t)S * R * kSharpPerRing * sizeof(int)));
+  HIPCHK(hipMalloc(&b.st_lsharp, (size_t)S * R * kLessSharpPerRing * sizeof(int)));
+  HIPCHK(hipMalloc(&b.st_flat, (size_t)S * R * kFlatPerRing * sizeof(int)));
+  HIPCHK(hipMalloc(&b.st_lflat, (size_t)S * R * kRingCap * sizeof(float4)));
+  HIPCHK(hipMalloc(&b.st_cnt, (size_t)S * R * 4 * sizeof(int)));
+  HIPCHK(hipMalloc(&b.sharp, (size_t)S * R * kSharpPerRing * sizeof(float4)));
+  HIPCHK(hipMalloc(&b.lsharp, (size_t)S * R * kLessSharpPerRing * sizeof(float4)));
+  HIPCHK(hipMalloc(&b.flat, (size_t)S * R * kFlatPerRing * sizeof(float4)));
+  HIPCHK(hipMalloc(&b.lflat, n * sizeof(float4)));
+  HIPCHK(hipMalloc(&b.cnt, (size_t)S * 4 * sizeof(int)));
+  HIPCHK(hipMalloc(&b.err, S * sizeof(int)));
+}
+
+void sr_free(SrBuffers& b) {
+  void* ptrs[] = {b.raw, b.raw_n, b.tmp_ori, b.tmp_sid, b.tilecnt, b.full, b.n_full, b.curv,
+                  b.picked, b.sortind, b.label, b.ring_se, b.st_sharp, b.st_lsharp, b.st_flat,
+                  b.st_lflat, b.st_cnt, b.sharp, b.lsharp, b.flat, b.lflat, b.cnt, b.err};
+  for (void* q : ptrs)
+    if (q) HIPCHK(hipFree(q));
+  b = SrBuffers();
+}
+
+void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st) {
+  HIPCHK(hipMemsetAsync(b.ring_se, 0, (size_t)b.S * 2 * b.R * sizeof(int), st));
+  HIPCHK(hipMemsetAsync(b.err, 0, (size_t)b.S * sizeof(int), st));
+  hipLaunchKernelGGL(k_sr_ring_sort, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
+  hipLaunchKernelGGL(k_sr_features, dim3((b.cap + kFeatTile - 1) / kFeatTile, b.S), dim3(kFeatTile), 0,
+                     st, b, p);
+  hipLaunchKernelGGL(k_sr_select, dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
+  hipLaunchKernelGGL(k_sr_compact, dim3(b.S), dim3(256), 0, st, b, p);
+}
+
+}  // namespace loam
