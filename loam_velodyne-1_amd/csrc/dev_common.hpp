@@ -130,7 +130,8 @@ LOAM_HD int next_pow2(int v) {
 }
 
 // order-preserving float -> uint32 for non-negative floats (curvature, squared distances)
-LOAM_HD uint32_t fkey(float f) { return __float_as_uint(f); }
+LOAM_HD uint32_t fkey(float f) { return __builtin_bit_cast(uint32_t, f); }
+LOAM_HD int32_t f2i(float f) { return __builtin_bit_cast(int32_t, f); }
 
 // ------------------------------------------------------------------ spatial hash
 LOAM_HD uint32_t cell_hash(int ix, int iy, int iz) {
@@ -141,6 +142,90 @@ LOAM_HD uint32_t cell_hash(int ix, int iy, int iz) {
   return h;
 }
 LOAM_HD int cell_of(float v, float inv_h) { return (int)floorf(v * inv_h); }
+
+
+// ------------------------------------------------------------------ glibc-identical atan2f
+// scanRegistration's float atan2 (`using std::atan2`, src/scanRegistration.cpp:53) resolves to
+// glibc's atan2f, the fdlibm single-precision algorithm (sysdeps/ieee754/flt-32/e_atan2f.c,
+// s_atanf.c).  Restated here so the device orientation / relTime / intensity are bit-identical
+// to the reference toolchain's (ocml's atan2f differs in the last bit for some inputs);
+// tests/test_atan2f.py checks it against the host glibc.
+LOAM_HD float atanf_fdlibm(float x) {
+  const float atanhi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
+  const float atanlo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
+  const float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f, aT2 = 1.4285714924e-01f,
+              aT3 = -1.1111110449e-01f, aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
+              aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f, aT8 = 4.9768779427e-02f,
+              aT9 = -3.6531571299e-02f, aT10 = 1.6285819933e-02f;
+  const int32_t hx = f2i(x), ix = hx & 0x7fffffff;
+  int id;
+  if (ix >= 0x4c800000) {  // |x| >= 2^26
+    if (ix > 0x7f800000) return x + x;
+    return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+  }
+  if (ix < 0x3ee00000) {   // |x| < 0.4375
+    if (ix < 0x39800000) return x;
+    id = -1;
+  } else {
+    x = fabsf(x);
+    if (ix < 0x3f980000) {
+      if (ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); }
+      else { id = 1; x = (x - 1.0f) / (x + 1.0f); }
+    } else {
+      if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); }
+      else { id = 3; x = -1.0f / x; }
+    }
+  }
+  const float z = x * x, w = z * z;
+  const float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+  const float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+  if (id < 0) return x - x * (s1 + s2);
+  const float r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+  return hx < 0 ? -r : r;
+}
+
+LOAM_HD float atan2f_fdlibm(float y, float x) {
+  const float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f,
+              pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
+  const int32_t hx = f2i(x), ix = hx & 0x7fffffff;
+  const int32_t hy = f2i(y), iy = hy & 0x7fffffff;
+  if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+  if (hx == 0x3f800000) return atanf_fdlibm(y);
+  int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+  if (iy == 0) {
+    if (m < 2) return y;
+    return m == 2 ? pi + tiny : -pi - tiny;
+  }
+  if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  if (ix == 0x7f800000) {
+    if (iy == 0x7f800000) {
+      switch (m) {
+        case 0: return pi_o_4 + tiny;
+        case 1: return -pi_o_4 - tiny;
+        case 2: return 3.0f * pi_o_4 + tiny;
+        default: return -3.0f * pi_o_4 - tiny;
+      }
+    }
+    switch (m) {
+      case 0: return 0.0f;
+      case 1: return -0.0f;
+      case 2: return pi + tiny;
+      default: return -pi - tiny;
+    }
+  }
+  if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  const int k = (iy - ix) >> 23;
+  float z;
+  if (k > 26) { z = pi_o_2 + 0.5f * pi_lo; m &= 1; }
+  else if (k < -26 && hx < 0) z = 0.0f;
+  else z = atanf_fdlibm(fabsf(y / x));
+  switch (m) {
+    case 0: return z;
+    case 1: return -z;
+    case 2: return pi - (z - pi_lo);
+    default: return (z - pi_lo) - pi;
+  }
+}
 
 }  // namespace loamdev
 

@@ -1,19 +1,1023 @@
-// Laser mapping on gfx950 (placeholder until the mapping kernels land).
+// Laser mapping on gfx950: the laserMapping loop body (/root/reference/src/laserMapping.cpp:411-1097)
+// for P independent map instances (the streaming map, or one per config-4 problem).
+//
+//  k_mp_prepare    pose prediction (transformAssociateToMap :110-197, fed through the nav_msgs
+//                  quaternion round trip :304-321), cube-grid recentring (:440-614) as slot-table
+//                  shifts, FOV cube selection (:616-672), FromMap prefix.
+//  k_mp_stack      stack to map frame and back (:424-434, :683-691, Q24)
+//  vg_run          segmented PCL VoxelGrid (hipCUB segmented radix sort by voxel index; equal keys
+//                  keep input order) for the stacks (:693-701) and the valid cubes (:1018-1036)
+//  k_mp_gather     FromMap = valid cubes concatenated (:674-681), then voxel-hashed (k_hash_build)
+//  k_mp_solve      the L-M loop (:706-978) in one workgroup per instance: lane per stack point,
+//                  exact 5-NN through the 1 m hash (any point within the 1 m acceptance radius lies
+//                  in the 27 cells), corner PCA with the 3x3 Jacobi, surface 5x3 QR plane, rows
+//                  (cleared every iteration), fp64 JᵀJ, 6x6 solve on one lane; transformUpdate.
+//  k_mp_insert     stack -> cubes in stack order (:980-1016)
+//  k_mp_vcopy      per valid cube: old content ++ appended points -> DS input
+//  k_mp_compact    new cube store (valid cubes downsampled, others appended) into the other pool
+//  k_mp_register   full cloud to the map frame (:1060-1063)
+#include <hipcub/hipcub.hpp>
+
+#include <cstring>
+#include <vector>
+
+#include "dev_common.hpp"
 #include "mp.hpp"
+#include "od.hpp"
+#include "pose_math.hpp"
+
+using namespace loamdev;
 
 namespace loam {
 
-void mp_alloc(MpBuffers& b, int P, int, int, int, int) { b.P = P; }
-void mp_free(MpBuffers& b) { b = MpBuffers(); }
-int mp_stream_frame(MpBuffers&, hipStream_t, const loam_pose6&, const loam_cloud_out&, const loam_cloud_out&,
-                    const loam_cloud_out&, loam_pose6*, loam_pose6*, loam_cloud_out*, loam_stats*, std::string& err) {
-  err = "mapping kernels not built yet";
-  return LOAM_E_INVAL;
+namespace {
+
+constexpr int kMpThreads = 256;
+constexpr int kMpWaves = kMpThreads / 64;
+
+LOAM_D int cube_of(float v, int cen) {  // :446-452, :983-989
+  int c = (int)((D(v) + 25.0) / 50.0) + cen;
+  if (D(v) + 25.0 < 0) c--;
+  return c;
 }
-void mp_batch_run(MpBuffers&, const OdBuffers&, hipStream_t) {}
-int mp_batch_download(MpBuffers& b, hipStream_t, loam_pose6* aft, loam_stats*, std::string&) {
-  if (aft)
-    for (int i = 0; i < b.P; ++i) aft[i] = loam_pose6{0, 0, 0, 0, 0, 0};
+LOAM_D int cube_index(int i, int j, int k) { return i + kCubeW * j + kCubeW * kCubeH * k; }
+
+LOAM_D int* slot_table(const MpBuffers& b, int pool, int p) {
+  return b.slots + ((size_t)pool * b.P + p) * kCubeNum * 4;
+}
+
+// ---------------------------------------------------------------- prepare
+__global__ __launch_bounds__(kMpThreads) void k_mp_prepare(MpBuffers b, MpInput in) {
+  const int p = blockIdx.x, tid = threadIdx.x;
+  float* st = b.state + (size_t)p * kMpStateFloats;
+  int* ist = b.istate + (size_t)p * kMpStateInts;
+  int* slots = slot_table(b, b.pool_cur, p);
+  __shared__ int sh_shift[256];
+  __shared__ int sh_nshift, sh_c[3];
+  if (tid == 0) {
+    float pose[6] = {0, 0, 0, 0, 0, 0};
+    if (in.pose)
+      for (int k = 0; k < 6; ++k) pose[k] = in.pose[(size_t)p * in.pose_stride + k];
+    loampose::pose_through_msg(pose, st + kMpSum);
+    loampose::associate_to_map(st + kMpSum, st + kMpBef, st + kMpAft, st + kMpIncre, st + kMpTobe);
+    const float* T = st + kMpTobe;
+    const loampose::MapRot r = loampose::map_rot(T);
+    const float4 onY = loampose::point_to_map(r, make_float4(0.0f, 10.0f, 0.0f, 0.0f));
+    st[kMpOnY] = onY.x; st[kMpOnY + 1] = onY.y; st[kMpOnY + 2] = onY.z;
+    int cW = ist[kMiCenW], cH = ist[kMiCenH], cD = ist[kMiCenD];
+    int cI = cube_of(T[3], cW), cJ = cube_of(T[4], cH), cK = cube_of(T[5], cD);
+    int n = 0;
+    // encoded shift: axis * 2 + (dir > 0); bounded to the table size
+    while (cI < 3 && n < 255) { sh_shift[n++] = 0 * 2 + 1; cI++; cW++; }
+    while (cI >= kCubeW - 3 && n < 255) { sh_shift[n++] = 0 * 2 + 0; cI--; cW--; }
+    while (cJ < 3 && n < 255) { sh_shift[n++] = 1 * 2 + 1; cJ++; cH++; }
+    while (cJ >= kCubeH - 3 && n < 255) { sh_shift[n++] = 1 * 2 + 0; cJ--; cH--; }
+    while (cK < 3 && n < 255) { sh_shift[n++] = 2 * 2 + 1; cK++; cD++; }
+    while (cK >= kCubeD - 3 && n < 255) { sh_shift[n++] = 2 * 2 + 0; cK--; cD--; }
+    sh_nshift = n;
+    sh_c[0] = cI; sh_c[1] = cJ; sh_c[2] = cK;
+    ist[kMiCenW] = cW; ist[kMiCenH] = cH; ist[kMiCenD] = cD;
+  }
+  __syncthreads();
+  for (int s = 0; s < sh_nshift; ++s) {  // slot-table shifts: the cleared cube wraps around
+    const int axis = sh_shift[s] >> 1, up = sh_shift[s] & 1;
+    const int nAx = axis == 0 ? kCubeW : (axis == 1 ? kCubeH : kCubeD);
+    const int na = axis == 0 ? kCubeH : kCubeW, nb = axis == 2 ? kCubeH : kCubeD;
+    for (int line = tid; line < na * nb; line += kMpThreads) {
+      const int a = line % na, bb = line / na;
+      auto at = [&](int c) {
+        if (axis == 0) return cube_index(c, a, bb);
+        if (axis == 1) return cube_index(a, c, bb);
+        return cube_index(a, bb, c);
+      };
+      int4* sl = (int4*)slots;
+      if (up) {
+        int4 keep = sl[at(nAx - 1)];
+        for (int c = nAx - 1; c >= 1; --c) sl[at(c)] = sl[at(c - 1)];
+        keep.y = 0; keep.w = 0;
+        sl[at(0)] = keep;
+      } else {
+        int4 keep = sl[at(0)];
+        for (int c = 0; c < nAx - 1; ++c) sl[at(c)] = sl[at(c + 1)];
+        keep.y = 0; keep.w = 0;
+        sl[at(nAx - 1)] = keep;
+      }
+    }
+    __threadfence();
+    __syncthreads();
+  }
+  if (tid == 0) {  // FOV selection (:616-672) and FromMap prefix
+    const float* T = st + kMpTobe;
+    const float ox = st[kMpOnY], oy = st[kMpOnY + 1], oz = st[kMpOnY + 2];
+    const int cI = sh_c[0], cJ = sh_c[1], cK = sh_c[2];
+    const int cW = ist[kMiCenW], cH = ist[kMiCenH], cD = ist[kMiCenD];
+    int nv = 0, accC = 0, accS = 0;
+    int* vp = b.vpre + (size_t)p * (kMaxValid + 1) * 2;
+    for (int i = cI - 2; i <= cI + 2; ++i)
+      for (int j = cJ - 2; j <= cJ + 2; ++j)
+        for (int k = cK - 2; k <= cK + 2; ++k) {
+          if (!(i >= 0 && i < kCubeW && j >= 0 && j < kCubeH && k >= 0 && k < kCubeD)) continue;
+          const float centerX = (float)(50.0 * (i - cW));
+          const float centerY = (float)(50.0 * (j - cH));
+          const float centerZ = (float)(50.0 * (k - cD));
+          bool inFOV = false;
+          for (int ii = -1; ii <= 1; ii += 2)
+            for (int jj = -1; jj <= 1; jj += 2)
+              for (int kk = -1; kk <= 1; kk += 2) {
+                const float cornerX = (float)(D(centerX) + 25.0 * ii);
+                const float cornerY = (float)(D(centerY) + 25.0 * jj);
+                const float cornerZ = (float)(D(centerZ) + 25.0 * kk);
+                const float sq1 = (T[3] - cornerX) * (T[3] - cornerX) + (T[4] - cornerY) * (T[4] - cornerY) +
+                                  (T[5] - cornerZ) * (T[5] - cornerZ);
+                const float sq2 = (ox - cornerX) * (ox - cornerX) + (oy - cornerY) * (oy - cornerY) +
+                                  (oz - cornerZ) * (oz - cornerZ);
+                const float check1 = (float)(100.0 + D(sq1) - D(sq2) - 10.0 * sqrt(3.0) * sqrt(D(sq1)));
+                const float check2 = (float)(100.0 + D(sq1) - D(sq2) + 10.0 * sqrt(3.0) * sqrt(D(sq1)));
+                if (check1 < 0 && check2 > 0) inFOV = true;
+              }
+          if (inFOV) {
+            const int ind = cube_index(i, j, k);
+            b.valid[(size_t)p * kMaxValid + nv] = ind;
+            vp[nv * 2 + 0] = accC;
+            vp[nv * 2 + 1] = accS;
+            accC += slots[ind * 4 + 1];
+            accS += slots[ind * 4 + 3];
+            ++nv;
+          }
+        }
+    vp[nv * 2 + 0] = accC;
+    vp[nv * 2 + 1] = accS;
+    ist[kMiNValid] = nv;
+    if (accC + accS > b.map_cap) {
+      ist[kMiErr] |= ERR_CAP_MAP;
+      accC = accS = 0;
+      ist[kMiNValid] = 0;
+    }
+    b.nfrom[p * 2 + 0] = accC;
+    b.nfrom[p * 2 + 1] = accS;
+  }
+}
+
+// ---------------------------------------------------------------- stacks
+__global__ __launch_bounds__(256) void k_mp_stack(MpBuffers b, MpInput in) {
+  const int p = blockIdx.y;
+  const float* st = b.state + (size_t)p * kMpStateFloats;
+  const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
+  const int nc = min(in.ncorner[p * in.ncorner_stride], b.capC);
+  const int ns = min(in.nsurf[p * in.nsurf_stride], b.capS);
+  float4* out = b.stack2 + (size_t)p * b.cap_stack;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < nc + ns; i += gridDim.x * 256) {
+    const float4 a = i < nc ? in.corner[(size_t)p * in.corner_stride + i]
+                            : in.surf[(size_t)p * in.surf_stride + (i - nc)];
+    const float4 m = loampose::point_to_map(r, a);
+    out[i < nc ? i : b.capC + (i - nc)] = loampose::point_to_tobe_mapped(r, m);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const size_t base = (size_t)p * b.cap_stack;
+    b.sseg_b[p * 2 + 0] = (int)base;
+    b.sseg_e[p * 2 + 0] = (int)base + nc;
+    b.sseg_b[p * 2 + 1] = (int)(base + b.capC);
+    b.sseg_e[p * 2 + 1] = (int)(base + b.capC) + ns;
+    b.sseg_leaf[p * 2 + 0] = 0.2f;
+    b.sseg_leaf[p * 2 + 1] = 0.4f;
+    if (in.ncorner[p * in.ncorner_stride] > b.capC || in.nsurf[p * in.nsurf_stride] > b.capS)
+      b.istate[(size_t)p * kMpStateInts + kMiErr] |= ERR_CAP_STACK;
+  }
+}
+
+// ---------------------------------------------------------------- segmented VoxelGrid
+__global__ __launch_bounds__(256) void k_vg_params(VgJob j) {
+  const int s = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int b0 = j.begin[s], b1 = j.end[s];
+  __shared__ float red[6][4];
+  float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+  for (int i = b0 + tid; i < b1; i += 256) {
+    const float4 a = j.in[i];
+    mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
+    mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
+  }
+  for (int d = 0; d < 3; ++d) {
+    mn[d] = wave_min_f(mn[d]);
+    mx[d] = wave_max_f(mx[d]);
+    if (lane == 0) { red[d][w] = mn[d]; red[3 + d][w] = mx[d]; }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int d = 0; d < 3; ++d)
+      for (int v = 1; v < 4; ++v) { red[d][0] = fminf(red[d][0], red[d][v]); red[3 + d][0] = fmaxf(red[3 + d][0], red[3 + d][v]); }
+    int* prm = j.params + (size_t)s * 8;
+    if (b1 <= b0) { prm[5] = 0; return; }
+    const float inv = 1.0f / j.leaf[s];
+    const int64_t dx = (int64_t)((red[3][0] - red[0][0]) * inv) + 1;
+    const int64_t dy = (int64_t)((red[4][0] - red[1][0]) * inv) + 1;
+    const int64_t dz = (int64_t)((red[5][0] - red[2][0]) * inv) + 1;
+    int minb[3], maxb[3];
+    for (int d = 0; d < 3; ++d) {
+      minb[d] = (int)floorf(red[d][0] * inv);
+      maxb[d] = (int)floorf(red[3 + d][0] * inv);
+    }
+    const int divx = maxb[0] - minb[0] + 1, divy = maxb[1] - minb[1] + 1;
+    prm[0] = minb[0]; prm[1] = minb[1]; prm[2] = minb[2];
+    prm[3] = divx; prm[4] = divx * divy;
+    prm[5] = (dx * dy * dz > (int64_t)0x7fffffff) ? 1 : 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_vg_keys(VgJob j) {
+  const int s = blockIdx.y;
+  const int b0 = j.begin[s], b1 = j.end[s];
+  const int* prm = j.params + (size_t)s * 8;
+  const float inv = 1.0f / j.leaf[s];
+  for (int i = b0 + blockIdx.x * 256 + threadIdx.x; i < b1; i += gridDim.x * 256) {
+    uint32_t key = 0;
+    if (!prm[5]) {
+      const float4 a = j.in[i];
+      const int i0 = (int)(floorf(a.x * inv) - (float)prm[0]);
+      const int i1 = (int)(floorf(a.y * inv) - (float)prm[1]);
+      const int i2 = (int)(floorf(a.z * inv) - (float)prm[2]);
+      key = (uint32_t)i0 + (uint32_t)i1 * (uint32_t)prm[3] + (uint32_t)i2 * (uint32_t)prm[4];
+    }
+    j.keys[i] = key;
+    j.vals[i] = (uint32_t)i;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_vg_reduce(VgJob j) {
+  const int s = blockIdx.x, tid = threadIdx.x;
+  const int b0 = j.begin[s], b1 = j.end[s];
+  const int* prm = j.params + (size_t)s * 8;
+  __shared__ int scratch[16];
+  if (b1 <= b0) {
+    if (tid == 0) j.out_count[s] = 0;
+    return;
+  }
+  if (prm[5]) {  // "leaf size too small": output = input
+    for (int i = b0 + tid; i < b1; i += 256) j.out[i] = j.in[i];
+    if (tid == 0) j.out_count[s] = b1 - b0;
+    return;
+  }
+  int run = 0;
+  for (int base = b0; base < b1; base += 256) {
+    const int t = base + tid;
+    const int head = (t < b1 && (t == b0 || j.keys_alt[t] != j.keys_alt[t - 1])) ? 1 : 0;
+    int tot;
+    const int ex = block_excl_scan<256>(head, scratch, tot);
+    if (head) {
+      const uint32_t k = j.keys_alt[t];
+      float sx = 0, sy = 0, sz = 0, si = 0;
+      int e = t;
+      while (e < b1 && j.keys_alt[e] == k) {
+        const float4 a = j.in[j.vals_alt[e]];
+        sx += a.x; sy += a.y; sz += a.z; si += a.w;
+        ++e;
+      }
+      const float cnt = (float)(e - t);
+      j.out[b0 + run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+    }
+    run += tot;
+  }
+  if (tid == 0) j.out_count[s] = run;
+}
+
+void vg_run(const VgJob& j, void* tmp, size_t tmp_bytes, hipStream_t st) {
+  if (j.nseg == 0) return;
+  hipLaunchKernelGGL(k_vg_params, dim3(j.nseg), dim3(256), 0, st, j);
+  hipLaunchKernelGGL(k_vg_keys, dim3(8, j.nseg), dim3(256), 0, st, j);
+  size_t bytes = tmp_bytes;
+  (void)hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
+                                                    j.nseg, j.begin, j.end, 0, 32, st);
+  hipLaunchKernelGGL(k_vg_reduce, dim3(j.nseg), dim3(256), 0, st, j);
+}
+
+size_t vg_tmp_bytes(int total, int nseg) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                    (uint32_t*)nullptr, (uint32_t*)nullptr, total, nseg,
+                                                    (int*)nullptr, (int*)nullptr, 0, 32);
+  return bytes;
+}
+
+// ---------------------------------------------------------------- FromMap gather
+__global__ __launch_bounds__(256) void k_mp_gather(MpBuffers b) {
+  const int p = blockIdx.y;
+  const int nv = b.istate[(size_t)p * kMpStateInts + kMiNValid];
+  const int* vp = b.vpre + (size_t)p * (kMaxValid + 1) * 2;
+  const int* slots = slot_table(b, b.pool_cur, p);
+  const float4* pool = b.pool + ((size_t)b.pool_cur * b.P + p) * b.map_cap;
+  const int totC = vp[nv * 2 + 0], totS = vp[nv * 2 + 1];
+  float4* out = b.from + (size_t)p * b.map_cap;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < totC + totS; i += gridDim.x * 256) {
+    const int kind = i < totC ? 0 : 1;
+    const int t = kind ? i - totC : i;
+    int lo = 0, hi = nv - 1;   // last valid cube with prefix <= t
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (vp[mid * 2 + kind] <= t) lo = mid; else hi = mid - 1;
+    }
+    const int ind = b.valid[(size_t)p * kMaxValid + lo];
+    out[i] = pool[slots[ind * 4 + 2 * kind] + (t - vp[lo * 2 + kind])];
+  }
+}
+
+// ---------------------------------------------------------------- L-M
+struct Top5 {
+  float d[5];
+  int i[5];
+};
+LOAM_D void top5_offer(Top5& t, float d, int idx) {
+  // ascending (distance, index); a point already held (duplicate bucket) is skipped
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    if (t.i[k] == idx) return;
+  if (d > t.d[4] || (d == t.d[4] && idx > t.i[4])) return;
+  t.d[4] = d;
+  t.i[4] = idx;
+#pragma unroll
+  for (int k = 4; k > 0; --k) {
+    const bool sw = t.d[k] < t.d[k - 1] || (t.d[k] == t.d[k - 1] && t.i[k] < t.i[k - 1]);
+    if (sw) {
+      float fd = t.d[k]; t.d[k] = t.d[k - 1]; t.d[k - 1] = fd;
+      int fi = t.i[k]; t.i[k] = t.i[k - 1]; t.i[k - 1] = fi;
+    }
+  }
+}
+
+LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t) {
+#pragma unroll
+  for (int k = 0; k < 5; ++k) { t.d[k] = 3.4e38f; t.i[k] = 0x7fffffff; }
+  if (T <= 0) return;
+  const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
+  for (int c = 0; c < 27; ++c) {
+    const uint32_t h = cell_hash(cx + c % 3 - 1, cy + (c / 3) % 3 - 1, cz + c / 9 - 1) & (uint32_t)(T - 1);
+    const int b0 = start[h], b1 = start[h + 1];
+    for (int k = b0; k < b1; ++k) {
+      const float4 a = hp[k];
+      top5_offer(t, sqdist(a.x, a.y, a.z, q.x, q.y, q.z), __builtin_bit_cast(int, a.w));
+    }
+  }
+}
+
+struct MpShared {
+  double red[kMpWaves][27];
+  int scratch[16];
+  float trig[6];
+  float T[6];
+  float lm_ws[loamla::kLmWs];
+  int lm_iws[12];
+  float AtA[36], AtB[6], X[6];
+  float jac[kMpThreads][33];   // per-lane 3x3 Jacobi scratch
+  int nrows, stop;
+};
+
+}  // namespace
+
+__global__ __launch_bounds__(kMpThreads) void k_mp_solve(MpBuffers b) {
+  const int p = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  __shared__ MpShared sh;
+  float* st = b.state + (size_t)p * kMpStateFloats;
+  int* ist = b.istate + (size_t)p * kMpStateInts;
+  const int nfc = b.nfrom[p * 2 + 0], nfs = b.nfrom[p * 2 + 1];
+  const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
+  const float4* stack = b.stack + (size_t)p * b.cap_stack;
+  const float4* fromC = b.from + (size_t)p * b.map_cap;
+  const float4* fromS = fromC + nfc;
+  const int* hcs = b.hC_start + (size_t)p * (b.tmax + 1);
+  const int* hss = b.hS_start + (size_t)p * (b.tmax + 1);
+  const float4* hcp = b.hC_pts + (size_t)p * b.map_cap;
+  const float4* hsp = b.hS_pts + (size_t)p * b.map_cap;
+  const int TC = b.hC_T[p], TS = b.hS_T[p];
+  float4* rows_pt = b.rows_pt + (size_t)p * b.cap_stack;
+  float4* rows_cf = b.rows_cf + (size_t)p * b.cap_stack;
+  const int nq = nsc + nss;
+  if (tid == 0) {
+    for (int k = 0; k < 6; ++k) sh.T[k] = st[kMpTobe + k];
+    ist[kMiStackC] = nsc;
+    ist[kMiStackS] = nss;
+    ist[kMiFromC] = nfc;
+    ist[kMiFromS] = nfs;
+    ist[kMiLmRan] = 0;
+    ist[kMiIters] = 0;
+    ist[kMiRows] = 0;
+  }
+  __syncthreads();
+  if (!(nfc > 10 && nfs > 100)) return;  // :706
+  int iters = 0;
+  long rows_sum = 0;
+  float* jw = sh.jac[tid];
+  for (int iter = 0; iter < b.max_iter; ++iter) {
+    ++iters;
+    const loampose::MapRot r = loampose::map_rot(sh.T);
+    if (tid == 0) sh.nrows = 0;
+    __syncthreads();
+    for (int base = 0; base < nq; base += kMpThreads) {
+      const int q = base + tid;
+      int ok = 0;
+      float4 cf = make_float4(0, 0, 0, 0), po = make_float4(0, 0, 0, 0);
+      if (q < nq) {
+        po = stack[q < nsc ? q : b.capC + (q - nsc)];
+        const float4 sel = loampose::point_to_map(r, po);
+        Top5 t;
+        if (q < nsc) {  // :714-819
+          knn5(hcs, hcp, TC, sel, t);
+          if (t.i[4] != 0x7fffffff && D(t.d[4]) < 1.0) {
+            float cx = 0, cy = 0, cz = 0;
+            for (int k = 0; k < 5; ++k) { const float4 a = fromC[t.i[k]]; cx += a.x; cy += a.y; cz += a.z; }
+            cx /= 5; cy /= 5; cz /= 5;
+            float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+            for (int k = 0; k < 5; ++k) {
+              const float4 a = fromC[t.i[k]];
+              const float ax = a.x - cx, ay = a.y - cy, az = a.z - cz;
+              a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
+              a22 += ay * ay; a23 += ay * az; a33 += az * az;
+            }
+            a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
+            float* A1 = jw;
+            float* D1 = jw + 9;
+            float* V1 = jw + 12;
+            int* iws = (int*)(jw + 21);
+            A1[0] = a11; A1[1] = a12; A1[2] = a13; A1[3] = a12; A1[4] = a22;
+            A1[5] = a23; A1[6] = a13; A1[7] = a23; A1[8] = a33;
+            loamla::jacobi<3>(A1, D1, V1, iws);
+            if (D1[0] > 3 * D1[1]) {
+              const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
+              const float x1 = (float)(D(cx) + 0.1 * D(V1[0])), y1 = (float)(D(cy) + 0.1 * D(V1[1])),
+                          z1 = (float)(D(cz) + 0.1 * D(V1[2]));
+              const float x2 = (float)(D(cx) - 0.1 * D(V1[0])), y2 = (float)(D(cy) - 0.1 * D(V1[1])),
+                          z2 = (float)(D(cz) - 0.1 * D(V1[2]));
+              const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
+              const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
+              const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
+              const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
+              const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
+              const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
+              const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
+              const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
+              const float ld2 = a012 / l12;
+              const float sw = (float)(1 - 0.9 * fabs(D(ld2)));
+              cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
+              ok = D(sw) > 0.1 ? 1 : 0;
+            }
+          }
+        } else {  // :821-877
+          knn5(hss, hsp, TS, sel, t);
+          if (t.i[4] != 0x7fffffff && D(t.d[4]) < 1.0) {
+            float A0[15], B0[5] = {-1, -1, -1, -1, -1}, X0[3], ws[14];
+            for (int k = 0; k < 5; ++k) {
+              const float4 a = fromS[t.i[k]];
+              A0[k * 3 + 0] = a.x; A0[k * 3 + 1] = a.y; A0[k * 3 + 2] = a.z;
+            }
+            loamla::qr_solve(A0, B0, 5, 3, X0, ws);
+            float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
+            const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
+            pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+            bool planeValid = true;
+            for (int k = 0; k < 5; ++k) {
+              const float4 a = fromS[t.i[k]];
+              if (fabs(D(pa * a.x + pb * a.y + pc * a.z + pd)) > 0.2) { planeValid = false; break; }
+            }
+            if (planeValid) {
+              const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
+              const float sw = (float)(1 - 0.9 * fabs(D(pd2)) /
+                                               sqrt(sqrt(D(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z))));
+              cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
+              ok = D(sw) > 0.1 ? 1 : 0;
+            }
+          }
+        }
+      }
+      int tot;
+      const int ex = block_excl_scan<kMpThreads>(ok, sh.scratch, tot);
+      const int r0 = sh.nrows;
+      if (ok) {
+        rows_pt[r0 + ex] = po;
+        rows_cf[r0 + ex] = cf;
+      }
+      __syncthreads();
+      if (tid == 0) sh.nrows = r0 + tot;
+      __syncthreads();
+    }
+    const int nrows = sh.nrows;
+    rows_sum += nrows;
+    if (tid == 0) {
+      for (int k = 0; k < 3; ++k) {
+        sh.trig[2 * k] = (float)dsin(sh.T[k]);
+        sh.trig[2 * k + 1] = (float)dcos(sh.T[k]);
+      }
+    }
+    __syncthreads();
+    if (nrows < 50) continue;  // :886-889
+    const float srx = sh.trig[0], crx = sh.trig[1], sry = sh.trig[2], cry = sh.trig[3], srz = sh.trig[4],
+                crz = sh.trig[5];
+    double acc[27];
+#pragma unroll
+    for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+    for (int rr = tid; rr < nrows; rr += kMpThreads) {  // :897-921
+      const float4 o = rows_pt[rr], c = rows_cf[rr];
+      float a[6];
+      a[0] = (crx * sry * srz * o.x + crx * crz * sry * o.y - srx * sry * o.z) * c.x +
+             (-srx * srz * o.x - crz * srx * o.y - crx * o.z) * c.y +
+             (crx * cry * srz * o.x + crx * cry * crz * o.y - cry * srx * o.z) * c.z;
+      a[1] = ((cry * srx * srz - crz * sry) * o.x + (sry * srz + cry * crz * srx) * o.y + crx * cry * o.z) * c.x +
+             ((-cry * crz - srx * sry * srz) * o.x + (cry * srz - crz * srx * sry) * o.y - crx * sry * o.z) * c.z;
+      a[2] = ((crz * srx * sry - cry * srz) * o.x + (-cry * crz - srx * sry * srz) * o.y) * c.x +
+             (crx * crz * o.x - crx * srz * o.y) * c.y +
+             ((sry * srz + cry * crz * srx) * o.x + (crz * sry - cry * srx * srz) * o.y) * c.z;
+      a[3] = c.x;
+      a[4] = c.y;
+      a[5] = c.z;
+      const float bb = -c.w;
+      int k = 0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
+    }
+#pragma unroll
+    for (int k = 0; k < 27; ++k) {
+      double v = acc[k];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0) sh.red[w][k] = v;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double tot[27];
+      for (int k = 0; k < 27; ++k) {
+        double v = sh.red[0][k];
+        for (int ww = 1; ww < kMpWaves; ++ww) v += sh.red[ww][k];
+        tot[k] = v;
+      }
+      int k = 0;
+      for (int i = 0; i < 6; ++i)
+        for (int jj = i; jj < 6; ++jj) {
+          sh.AtA[i * 6 + jj] = (float)tot[k];
+          sh.AtA[jj * 6 + i] = (float)tot[k];
+          ++k;
+        }
+      for (int i = 0; i < 6; ++i) sh.AtB[i] = (float)tot[21 + i];
+      int degen = ist[kMiDegen];
+      loamla::lm_step(sh.AtA, sh.AtB, iter, 100.0f, &degen, st + kMpMatP, sh.X, sh.lm_ws, sh.lm_iws);
+      ist[kMiDegen] = degen;
+      for (int q = 0; q < 6; ++q) sh.T[q] += sh.X[q];  // no NaN guard in mapping (:956-961)
+      const float dR = loamla::delta_r(sh.X), dT = loamla::delta_t(sh.X);
+      sh.stop = (D(dR) < 0.05 && D(dT) < 0.05) ? 1 : 0;
+    }
+    __syncthreads();
+    if (sh.stop) break;
+  }
+  if (tid == 0) {
+    for (int k = 0; k < 6; ++k) {
+      st[kMpTobe + k] = sh.T[k];
+      st[kMpBef + k] = st[kMpSum + k];  // transformUpdate (:199-232, no IMU)
+      st[kMpAft + k] = sh.T[k];
+    }
+    ist[kMiLmRan] = 1;
+    ist[kMiIters] = iters;
+    ist[kMiRows] = (int)rows_sum;
+  }
+}
+
+namespace {
+
+// ---------------------------------------------------------------- insertion (:980-1016)
+// one workgroup per instance: cube slot of every stack point (corner, then surf), stable ranks by
+// one wave walking the stack in order, per-cube prefix, scatter of the map-frame points.
+__global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot_of, int* rank_of) {
+  const int p = blockIdx.x, tid = threadIdx.x, lane = lane_id();
+  const float* st = b.state + (size_t)p * kMpStateFloats;
+  const int* ist = b.istate + (size_t)p * kMpStateInts;
+  const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
+  const float4* stack = b.stack + (size_t)p * b.cap_stack;
+  const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
+  const int cW = ist[kMiCenW], cH = ist[kMiCenH], cD = ist[kMiCenD];
+  int* so = slot_of + (size_t)p * b.cap_stack;
+  int* ro = rank_of + (size_t)p * b.cap_stack;
+  __shared__ int cnt[2][kCubeNum];
+  __shared__ int scratch[16];
+  for (int i = tid; i < 2 * kCubeNum; i += kMpThreads) cnt[i / kCubeNum][i % kCubeNum] = 0;
+  for (int q = tid; q < nsc + nss; q += kMpThreads) {
+    const float4 a = loampose::point_to_map(r, stack[q < nsc ? q : b.capC + (q - nsc)]);
+    const int ci = cube_of(a.x, cW), cj = cube_of(a.y, cH), ck = cube_of(a.z, cD);
+    const bool in = ci >= 0 && ci < kCubeW && cj >= 0 && cj < kCubeH && ck >= 0 && ck < kCubeD;
+    so[q] = in ? cube_index(ci, cj, ck) : -1;
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (tid < 64) {  // stable ranks: one wave, stack order
+    for (int base = 0; base < nsc + nss; base += 64) {
+      const int q = base + lane;
+      const bool v = q < nsc + nss;
+      const int kind = q < nsc ? 0 : 1;
+      const int s = v ? so[q] : -1;
+      const int key = s < 0 ? -1 : s * 2 + kind;
+      uint64_t m = __ballot(v && key >= 0);
+      int rank = 0;
+      while (m) {
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        const int kl = __shfl(key, leader, 64);
+        const uint64_t mm = __ballot(v && key == kl);
+        const int basecnt = cnt[kl & 1][kl >> 1];
+        if (v && key == kl) rank = basecnt + __popcll(mm & lanemask_lt());
+        __builtin_amdgcn_wave_barrier();
+        if (lane == leader) cnt[kl & 1][kl >> 1] = basecnt + __popcll(mm);
+        __builtin_amdgcn_wave_barrier();
+        m &= ~mm;
+      }
+      if (v) ro[q] = rank;
+    }
+  }
+  __syncthreads();
+  // per-kind exclusive prefix over the cube slots
+  int* ac = b.app_cnt + (size_t)p * kCubeNum * 2;
+  int* ao = b.app_off + (size_t)p * kCubeNum * 2;
+  int run = 0;
+  for (int kind = 0; kind < 2; ++kind)
+    for (int base = 0; base < kCubeNum; base += kMpThreads) {
+      const int s = base + tid;
+      const int c = s < kCubeNum ? cnt[kind][s] : 0;
+      int tot;
+      const int ex = block_excl_scan<kMpThreads>(c, scratch, tot);
+      if (s < kCubeNum) { ac[s * 2 + kind] = c; ao[s * 2 + kind] = run + ex; }
+      run += tot;
+    }
+  __threadfence_block();
+  __syncthreads();
+  float4* app = b.app + (size_t)p * b.cap_stack;
+  for (int q = tid; q < nsc + nss; q += kMpThreads) {
+    const int s = so[q];
+    if (s < 0) continue;
+    const int kind = q < nsc ? 0 : 1;
+    app[ao[s * 2 + kind] + ro[q]] = loampose::point_to_map(r, stack[q < nsc ? q : b.capC + (q - nsc)]);
+  }
+}
+
+// per valid cube: DS input = old cube content ++ appended points (corner region, then surf region)
+__global__ __launch_bounds__(kMpThreads) void k_mp_vseg(MpBuffers b) {
+  const int p = blockIdx.x, tid = threadIdx.x;
+  const int nv = b.istate[(size_t)p * kMpStateInts + kMiNValid];
+  const int* slots = slot_table(b, b.pool_cur, p);
+  const int* ac = b.app_cnt + (size_t)p * kCubeNum * 2;
+  if (tid == 0) {
+    int run = (int)((size_t)p * b.map_cap);
+    const int lim = (int)((size_t)(p + 1) * b.map_cap);
+    for (int kind = 0; kind < 2; ++kind)
+      for (int v = 0; v < kMaxValid; ++v) {
+        const int sidx = p * 2 * kMaxValid + kind * kMaxValid + v;
+        int n = 0;
+        if (v < nv) {
+          const int ind = b.valid[(size_t)p * kMaxValid + v];
+          n = slots[ind * 4 + 1 + 2 * kind] + ac[ind * 2 + kind];
+        }
+        if (run + n > lim) {
+          b.istate[(size_t)p * kMpStateInts + kMiErr] |= ERR_CAP_MAP;
+          n = 0;
+        }
+        b.vseg_b[sidx] = run;
+        b.vseg_e[sidx] = run + n;
+        b.vseg_leaf[sidx] = kind == 0 ? 0.2f : 0.4f;
+        run += n;
+      }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mp_vcopy(MpBuffers b) {
+  const int p = blockIdx.y;
+  const int nv = b.istate[(size_t)p * kMpStateInts + kMiNValid];
+  const int* slots = slot_table(b, b.pool_cur, p);
+  const float4* pool = b.pool + ((size_t)b.pool_cur * b.P + p) * b.map_cap;
+  const int* ac = b.app_cnt + (size_t)p * kCubeNum * 2;
+  const int* ao = b.app_off + (size_t)p * kCubeNum * 2;
+  const float4* app = b.app + (size_t)p * b.cap_stack;
+  for (int sg = blockIdx.x; sg < 2 * nv; sg += gridDim.x) {
+    const int kind = sg / nv, v = sg % nv;
+    const int sidx = p * 2 * kMaxValid + kind * kMaxValid + v;
+    const int ind = b.valid[(size_t)p * kMaxValid + v];
+    const int b0 = b.vseg_b[sidx], n = b.vseg_e[sidx] - b0;
+    const int nold = slots[ind * 4 + 1 + 2 * kind], off = slots[ind * 4 + 2 * kind];
+    for (int t = threadIdx.x; t < n; t += 256)
+      b.vin[b0 + t] = t < nold ? pool[off + t] : app[ao[ind * 2 + kind] + (t - nold)];
+    (void)ac;
+  }
+}
+
+// new cube store: valid cubes <- their DS output, every other cube <- old ++ appended
+__global__ __launch_bounds__(kMpThreads) void k_mp_compact_table(MpBuffers b) {
+  const int p = blockIdx.x, tid = threadIdx.x;
+  const int nv = b.istate[(size_t)p * kMpStateInts + kMiNValid];
+  const int* old = slot_table(b, b.pool_cur, p);
+  int* nw = slot_table(b, 1 - b.pool_cur, p);
+  const int* ac = b.app_cnt + (size_t)p * kCubeNum * 2;
+  __shared__ int vidx[kCubeNum];
+  __shared__ int scratch[16];
+  for (int s = tid; s < kCubeNum; s += kMpThreads) vidx[s] = -1;
+  __syncthreads();
+  if (tid < nv) vidx[b.valid[(size_t)p * kMaxValid + tid]] = tid;
+  __syncthreads();
+  int run = 0, vpts = 0;
+  for (int kind = 0; kind < 2; ++kind)
+    for (int base = 0; base < kCubeNum; base += kMpThreads) {
+      const int s = base + tid;
+      int n = 0;
+      if (s < kCubeNum) {
+        const int v = vidx[s];
+        n = v >= 0 ? b.vseg_cnt[p * 2 * kMaxValid + kind * kMaxValid + v] : old[s * 4 + 1 + 2 * kind] + ac[s * 2 + kind];
+        if (v >= 0) vpts += n;
+      }
+      int tot;
+      const int ex = block_excl_scan<kMpThreads>(n, scratch, tot);
+      if (s < kCubeNum) {
+        nw[s * 4 + 2 * kind] = run + ex;
+        nw[s * 4 + 1 + 2 * kind] = n;
+      }
+      run += tot;
+    }
+  vpts = block_reduce<kMpThreads>(vpts, scratch, [](int a, int c) { return a + c; });
+  if (tid == 0) {
+    b.istate[(size_t)p * kMpStateInts + kMiValidPts] = vpts;
+    if (run > b.map_cap) b.istate[(size_t)p * kMpStateInts + kMiErr] |= ERR_CAP_MAP;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mp_compact_copy(MpBuffers b) {
+  const int p = blockIdx.y;
+  const int err = b.istate[(size_t)p * kMpStateInts + kMiErr];
+  if (err & ERR_CAP_MAP) return;
+  const int* old = slot_table(b, b.pool_cur, p);
+  const int* nw = slot_table(b, 1 - b.pool_cur, p);
+  const float4* pool = b.pool + ((size_t)b.pool_cur * b.P + p) * b.map_cap;
+  float4* npool = b.pool + ((size_t)(1 - b.pool_cur) * b.P + p) * b.map_cap;
+  const int* ao = b.app_off + (size_t)p * kCubeNum * 2;
+  const float4* app = b.app + (size_t)p * b.cap_stack;
+  const int nv = b.istate[(size_t)p * kMpStateInts + kMiNValid];
+  for (int item = blockIdx.x; item < 2 * kCubeNum; item += gridDim.x) {
+    const int kind = item / kCubeNum, s = item % kCubeNum;
+    const int n = nw[s * 4 + 1 + 2 * kind];
+    if (n == 0) continue;
+    const int dst = nw[s * 4 + 2 * kind];
+    int v = -1;
+    for (int q = 0; q < nv; ++q)
+      if (b.valid[(size_t)p * kMaxValid + q] == s) v = q;
+    if (v >= 0) {
+      const int b0 = b.vseg_b[p * 2 * kMaxValid + kind * kMaxValid + v];
+      for (int t = threadIdx.x; t < n; t += 256) npool[dst + t] = b.vout[b0 + t];
+    } else {
+      const int nold = old[s * 4 + 1 + 2 * kind], off = old[s * 4 + 2 * kind];
+      for (int t = threadIdx.x; t < n; t += 256)
+        npool[dst + t] = t < nold ? pool[off + t] : app[ao[s * 2 + kind] + (t - nold)];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mp_register(MpBuffers b, MpInput in) {
+  const int p = blockIdx.y;
+  const loampose::MapRot r = loampose::map_rot(b.state + (size_t)p * kMpStateFloats + kMpTobe);
+  const int n = min(in.nfull[p * in.nfull_stride], b.capS);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+    b.reg[(size_t)p * b.capS + i] = loampose::point_to_map(r, in.full[(size_t)p * in.full_stride + i]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) b.nreg[p] = n;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host side
+void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter) {
+  b.P = P;
+  b.capC = kLessSharpPerRing * R;
+  b.capS = cap_pts;
+  b.cap_stack = b.capC + b.capS;
+  b.map_cap = map_cap;
+  b.max_iter = max_iter;
+  b.tmax = next_pow2(map_cap) > (1 << 20) ? (1 << 20) : next_pow2(map_cap);
+  b.pool_cur = 0;
+  const size_t Pm = (size_t)P * map_cap, Ps = (size_t)P * b.cap_stack;
+  (void)hipMalloc(&b.state, (size_t)P * kMpStateFloats * sizeof(float));
+  (void)hipMalloc(&b.istate, (size_t)P * kMpStateInts * sizeof(int));
+  (void)hipMalloc(&b.slots, (size_t)2 * P * kCubeNum * 4 * sizeof(int));
+  (void)hipMalloc(&b.pool, 2 * Pm * sizeof(float4));
+  (void)hipMalloc(&b.valid, (size_t)P * kMaxValid * sizeof(int));
+  (void)hipMalloc(&b.vpre, (size_t)P * (kMaxValid + 1) * 2 * sizeof(int));
+  (void)hipMalloc(&b.inC, (size_t)P * b.capC * sizeof(float4));
+  (void)hipMalloc(&b.inS, (size_t)P * b.capS * sizeof(float4));
+  (void)hipMalloc(&b.inF, (size_t)P * b.capS * sizeof(float4));
+  (void)hipMalloc(&b.in_n, (size_t)P * 3 * sizeof(int));
+  (void)hipMalloc(&b.in_pose, (size_t)P * 6 * sizeof(float));
+  (void)hipMalloc(&b.stack2, Ps * sizeof(float4));
+  (void)hipMalloc(&b.stack, Ps * sizeof(float4));
+  (void)hipMalloc(&b.nstack, (size_t)P * 2 * sizeof(int));
+  (void)hipMalloc(&b.from, Pm * sizeof(float4));
+  (void)hipMalloc(&b.hC_start, (size_t)P * (b.tmax + 1) * sizeof(int));
+  (void)hipMalloc(&b.hS_start, (size_t)P * (b.tmax + 1) * sizeof(int));
+  (void)hipMalloc(&b.h_fill, (size_t)P * b.tmax * sizeof(int));
+  (void)hipMalloc(&b.hC_T, (size_t)P * sizeof(int));
+  (void)hipMalloc(&b.hS_T, (size_t)P * sizeof(int));
+  (void)hipMalloc(&b.hC_pts, Pm * sizeof(float4));
+  (void)hipMalloc(&b.hS_pts, Pm * sizeof(float4));
+  (void)hipMalloc(&b.nfrom, (size_t)P * 2 * sizeof(int));
+  (void)hipMalloc(&b.rows_pt, Ps * sizeof(float4));
+  (void)hipMalloc(&b.rows_cf, Ps * sizeof(float4));
+  (void)hipMalloc(&b.app_cnt, (size_t)P * kCubeNum * 2 * sizeof(int));
+  (void)hipMalloc(&b.app_off, (size_t)P * kCubeNum * 2 * sizeof(int));
+  (void)hipMalloc(&b.app, Ps * sizeof(float4));
+  (void)hipMalloc(&b.vin, Pm * sizeof(float4));
+  (void)hipMalloc(&b.vout, Pm * sizeof(float4));
+  (void)hipMalloc(&b.vseg_b, (size_t)P * 2 * kMaxValid * sizeof(int));
+  (void)hipMalloc(&b.vseg_e, (size_t)P * 2 * kMaxValid * sizeof(int));
+  (void)hipMalloc(&b.vseg_cnt, (size_t)P * 2 * kMaxValid * sizeof(int));
+  (void)hipMalloc(&b.vseg_leaf, (size_t)P * 2 * kMaxValid * sizeof(float));
+  (void)hipMalloc(&b.sseg_b, (size_t)P * 2 * sizeof(int));
+  (void)hipMalloc(&b.sseg_e, (size_t)P * 2 * sizeof(int));
+  (void)hipMalloc(&b.sseg_cnt, (size_t)P * 2 * sizeof(int));
+  (void)hipMalloc(&b.sseg_leaf, (size_t)P * 2 * sizeof(float));
+  const size_t vgn = Pm > Ps ? Pm : Ps;
+  (void)hipMalloc(&b.vg_params, (size_t)P * 2 * kMaxValid * 8 * sizeof(int));
+  (void)hipMalloc(&b.vg_k, vgn * sizeof(uint32_t));
+  (void)hipMalloc(&b.vg_k2, vgn * sizeof(uint32_t));
+  (void)hipMalloc(&b.vg_v, vgn * sizeof(uint32_t));
+  (void)hipMalloc(&b.vg_v2, vgn * sizeof(uint32_t));
+  const size_t t1 = vg_tmp_bytes((int)vgn, P * 2 * kMaxValid), t2 = vg_tmp_bytes((int)Ps, P * 2);
+  b.cub_bytes = t1 > t2 ? t1 : t2;
+  (void)hipMalloc(&b.cub_tmp, b.cub_bytes);
+  (void)hipMalloc(&b.reg, (size_t)P * b.capS * sizeof(float4));
+  (void)hipMalloc(&b.nreg, (size_t)P * sizeof(int));
+  mp_reset(b, nullptr);
+  (void)hipDeviceSynchronize();
+}
+
+void mp_free(MpBuffers& b) {
+  void* ptrs[] = {b.state, b.istate, b.slots, b.pool, b.valid, b.vpre, b.inC, b.inS, b.inF, b.in_n, b.in_pose,
+                  b.stack2, b.stack, b.nstack, b.from, b.hC_start, b.hS_start, b.h_fill, b.hC_T, b.hS_T,
+                  b.hC_pts, b.hS_pts, b.nfrom, b.rows_pt, b.rows_cf, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
+                  b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
+                  b.vg_params, b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.cub_tmp, b.reg, b.nreg};
+  for (void* q : ptrs)
+    if (q) (void)hipFree(q);
+  b = MpBuffers();
+}
+
+__global__ void k_mp_reset(MpBuffers b) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= b.P) return;
+  int* ist = b.istate + (size_t)p * kMpStateInts;
+  ist[kMiCenW] = 10; ist[kMiCenH] = 5; ist[kMiCenD] = 10;  // :64-66
+}
+
+void mp_reset(MpBuffers& b, hipStream_t st) {
+  b.pool_cur = 0;
+  (void)hipMemsetAsync(b.state, 0, (size_t)b.P * kMpStateFloats * sizeof(float), st);
+  (void)hipMemsetAsync(b.istate, 0, (size_t)b.P * kMpStateInts * sizeof(int), st);
+  (void)hipMemsetAsync(b.slots, 0, (size_t)2 * b.P * kCubeNum * 4 * sizeof(int), st);
+  hipLaunchKernelGGL(k_mp_reset, dim3((b.P + 255) / 256), dim3(256), 0, st, b);
+}
+
+void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st) {
+  const int P = b.P;
+  hipLaunchKernelGGL(k_mp_prepare, dim3(P), dim3(kMpThreads), 0, st, b, in);
+  hipLaunchKernelGGL(k_mp_stack, dim3(16, P), dim3(256), 0, st, b, in);
+  VgJob js;
+  js.in = b.stack2; js.out = b.stack; js.begin = b.sseg_b; js.end = b.sseg_e; js.leaf = b.sseg_leaf;
+  js.out_count = b.sseg_cnt; js.params = b.vg_params; js.keys = b.vg_k; js.keys_alt = b.vg_k2;
+  js.vals = b.vg_v; js.vals_alt = b.vg_v2; js.nseg = 2 * P; js.total = P * b.cap_stack;
+  vg_run(js, b.cub_tmp, b.cub_bytes, st);
+  hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);
+  HashJob hc;
+  hc.pts = b.from; hc.pts_stride = b.map_cap; hc.pts_off = nullptr; hc.pts_off_stride = 0;
+  hc.count = b.nfrom; hc.count_stride_bytes = 2 * sizeof(int);
+  hc.start = b.hC_start; hc.fill = b.h_fill; hc.out = b.hC_pts; hc.tsize = b.hC_T; hc.tmax = b.tmax;
+  hc.inv_h = 1.0f;
+  hipLaunchKernelGGL(k_hash_build, dim3(P), dim3(256), 0, st, hc);
+  HashJob hs = hc;
+  hs.pts_off = b.nfrom; hs.pts_off_stride = 2;
+  hs.count = b.nfrom + 1; hs.start = b.hS_start; hs.out = b.hS_pts; hs.tsize = b.hS_T;
+  hipLaunchKernelGGL(k_hash_build, dim3(P), dim3(256), 0, st, hs);
+  hipLaunchKernelGGL(k_mp_solve, dim3(P), dim3(kMpThreads), 0, st, b);
+  // insertion + per-valid-cube downsampling into the other pool
+  hipLaunchKernelGGL(k_mp_insert, dim3(P), dim3(kMpThreads), 0, st, b, (int*)b.vg_k, (int*)b.vg_v);
+  hipLaunchKernelGGL(k_mp_vseg, dim3(P), dim3(kMpThreads), 0, st, b);
+  hipLaunchKernelGGL(k_mp_vcopy, dim3(32, P), dim3(256), 0, st, b);
+  VgJob jv;
+  jv.in = b.vin; jv.out = b.vout; jv.begin = b.vseg_b; jv.end = b.vseg_e; jv.leaf = b.vseg_leaf;
+  jv.out_count = b.vseg_cnt; jv.params = b.vg_params; jv.keys = b.vg_k; jv.keys_alt = b.vg_k2;
+  jv.vals = b.vg_v; jv.vals_alt = b.vg_v2; jv.nseg = 2 * kMaxValid * P; jv.total = P * b.map_cap;
+  vg_run(jv, b.cub_tmp, b.cub_bytes, st);
+  hipLaunchKernelGGL(k_mp_compact_table, dim3(P), dim3(kMpThreads), 0, st, b);
+  hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);
+  hipLaunchKernelGGL(k_mp_register, dim3(16, P), dim3(256), 0, st, b, in);
+  b.pool_cur = 1 - b.pool_cur;
+}
+
+int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
+                    const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
+                    loam_cloud_out* registered, loam_stats* stats, std::string& err) {
+  if (corner.count > (uint32_t)b.capC || surf.count > (uint32_t)b.capS || full.count > (uint32_t)b.capS) {
+    err = "mapping input cloud exceeds capacity";
+    return LOAM_E_CAPACITY;
+  }
+  if ((corner.count && !corner.pts) || (surf.count && !surf.pts) || (full.count && !full.pts)) {
+    err = "mapping input cloud pts is null";
+    return LOAM_E_INVAL;
+  }
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  int n[3] = {(int)corner.count, (int)surf.count, (int)full.count};
+  if (n[0]) (void)hipMemcpyAsync(b.inC, corner.pts, n[0] * sizeof(float4), hipMemcpyHostToDevice, st);
+  if (n[1]) (void)hipMemcpyAsync(b.inS, surf.pts, n[1] * sizeof(float4), hipMemcpyHostToDevice, st);
+  if (n[2]) (void)hipMemcpyAsync(b.inF, full.pts, n[2] * sizeof(float4), hipMemcpyHostToDevice, st);
+  (void)hipMemcpyAsync(b.in_n, n, sizeof(n), hipMemcpyHostToDevice, st);
+  (void)hipMemcpyAsync(b.in_pose, &odom_sum, 6 * sizeof(float), hipMemcpyHostToDevice, st);
+  MpInput in;
+  in.corner = b.inC; in.surf = b.inS; in.full = b.inF;
+  in.corner_stride = b.capC; in.surf_stride = b.capS; in.full_stride = b.capS;
+  in.ncorner = b.in_n; in.nsurf = b.in_n + 1; in.nfull = b.in_n + 2;
+  in.ncorner_stride = in.nsurf_stride = in.nfull_stride = 3;
+  in.pose = b.in_pose; in.pose_stride = 6;
+  (void)hipEventRecord(e0, st);
+  mp_frame(b, in, st);
+  (void)hipEventRecord(e1, st);
+  float sf[kMpStateFloats];
+  int si[kMpStateInts], nreg = 0;
+  (void)hipMemcpyAsync(sf, b.state, sizeof(sf), hipMemcpyDeviceToHost, st);
+  (void)hipMemcpyAsync(si, b.istate, sizeof(si), hipMemcpyDeviceToHost, st);
+  (void)hipMemcpyAsync(&nreg, b.nreg, sizeof(int), hipMemcpyDeviceToHost, st);
+  hipError_t he = hipStreamSynchronize(st);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (he != hipSuccess) {
+    err = std::string("mapping: ") + hipGetErrorString(he);
+    return LOAM_E_HIP;
+  }
+  if (si[kMiErr]) {
+    err = "mapping capacity exceeded (map store / stack)";
+    return LOAM_E_CAPACITY;
+  }
+  std::memcpy(aft, sf + kMpAft, sizeof(loam_pose6));
+  std::memcpy(bef, sf + kMpBef, sizeof(loam_pose6));
+  int rc = LOAM_OK;
+  if (registered) {
+    if ((uint32_t)nreg > registered->capacity) {
+      registered->count = (uint32_t)nreg;
+      err = "registered cloud capacity too small";
+      rc = LOAM_E_CAPACITY;
+    } else {
+      registered->count = (uint32_t)nreg;
+      if (nreg) (void)hipMemcpy(registered->pts, b.reg, (size_t)nreg * sizeof(float4), hipMemcpyDeviceToHost);
+    }
+  }
+  if (stats) {
+    std::memset(stats, 0, sizeof(*stats));
+    stats->mp_iters = si[kMiIters];
+    stats->mp_rows_sum = (uint64_t)si[kMiRows];
+    stats->mp_stack = (uint64_t)(si[kMiStackC] + si[kMiStackS]);
+    stats->mp_map_points = (uint64_t)(si[kMiFromC] + si[kMiFromS]);
+    stats->mp_map_valid_points = (uint64_t)si[kMiValidPts];
+    stats->ms_mp = ms;
+  }
+  return rc;
+}
+
+void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st) {
+  mp_reset(b, st);
+  MpInput in;
+  // frame 1: prev (Last[0], fullEnd[0]) at the zero pose
+  in.corner = od.lastC; in.surf = od.lastS; in.full = od.fullEnd;
+  in.corner_stride = od.capC; in.surf_stride = od.capS; in.full_stride = od.capS;
+  in.ncorner = od.nlast + 0; in.nsurf = od.nlast + 1; in.nfull = od.nfullEnd + 0;
+  in.ncorner_stride = 4; in.nsurf_stride = 4; in.nfull_stride = 2;
+  in.pose = nullptr; in.pose_stride = 0;
+  mp_frame(b, in, st);
+  // frame 2: cur (Last[1], fullEnd[1]) with the odometry transformSum
+  in.corner = od.lastC + (size_t)od.P * od.capC;
+  in.surf = od.lastS + (size_t)od.P * od.capS;
+  in.full = od.fullEnd + (size_t)od.P * od.capS;
+  in.ncorner = od.nlast + 2; in.nsurf = od.nlast + 3; in.nfull = od.nfullEnd + 1;
+  in.pose = od.state + kOdSum; in.pose_stride = kOdStateFloats;
+  mp_frame(b, in, st);
+}
+
+int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err) {
+  (void)hipStreamSynchronize(st);
+  std::vector<float> sf((size_t)b.P * kMpStateFloats);
+  std::vector<int> si((size_t)b.P * kMpStateInts);
+  (void)hipMemcpy(sf.data(), b.state, sf.size() * sizeof(float), hipMemcpyDeviceToHost);
+  (void)hipMemcpy(si.data(), b.istate, si.size() * sizeof(int), hipMemcpyDeviceToHost);
+  for (int p = 0; p < b.P; ++p) {
+    const int* q = &si[(size_t)p * kMpStateInts];
+    if (q[kMiErr]) {
+      err = "mapping capacity exceeded (map store / stack)";
+      return LOAM_E_CAPACITY;
+    }
+    if (aft) std::memcpy(&aft[p], &sf[(size_t)p * kMpStateFloats + kMpAft], sizeof(loam_pose6));
+    if (stats) {
+      stats->mp_iters += q[kMiIters];
+      stats->mp_rows_sum += (uint64_t)q[kMiRows];
+      stats->mp_stack += (uint64_t)(q[kMiStackC] + q[kMiStackS]);
+      stats->mp_map_points += (uint64_t)(q[kMiFromC] + q[kMiFromS]);
+      stats->mp_map_valid_points += (uint64_t)q[kMiValidPts];
+    }
+  }
   return LOAM_OK;
 }
 

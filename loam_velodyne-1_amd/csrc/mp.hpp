@@ -11,13 +11,87 @@
 
 namespace loam {
 
-struct MpBuffers {
-  int P = 0;
+// cube grid of src/laserMapping.cpp:64-70
+constexpr int kCubeW = 21, kCubeH = 11, kCubeD = 21, kCubeNum = kCubeW * kCubeH * kCubeD;
+constexpr int kMaxValid = 125;
+
+// per-instance float state: Sum | Incre | TobeMapped | Bef | Aft | matP[36] | pointOnYAxis[3]
+constexpr int kMpSum = 0, kMpIncre = 6, kMpTobe = 12, kMpBef = 18, kMpAft = 24, kMpMatP = 30, kMpOnY = 66,
+              kMpStateFloats = 72;
+enum { kMiCenW = 0, kMiCenH, kMiCenD, kMiDegen, kMiNValid, kMiIters, kMiRows, kMiStackC, kMiStackS, kMiFromC,
+       kMiFromS, kMiErr, kMiLmRan, kMiValidPts, kMpStateInts = 16 };
+
+// one mapping frame's inputs for every instance (device pointers)
+struct MpInput {
+  const float4 *corner, *surf, *full;
+  size_t corner_stride, surf_stride, full_stride;
+  const int *ncorner, *nsurf, *nfull;
+  int ncorner_stride, nsurf_stride, nfull_stride;
+  const float* pose;   // transformSum of the odometry message (nullptr = zero pose)
+  int pose_stride;
 };
 
-inline int mp_batch_map_capacity(int cap) { return 4 * cap; }
+// segmented PCL VoxelGrid job (segment s: input in[begin[s] .. end[s]), output out[begin[s] ..))
+struct VgJob {
+  const float4* in;
+  float4* out;
+  const int* begin;
+  const int* end;
+  const float* leaf;     // per segment
+  int* out_count;        // per segment
+  int* params;           // [nseg][8]: minb xyz, mul1, mul2, overflow
+  uint32_t *keys, *keys_alt, *vals, *vals_alt;
+  int nseg;
+  int total;             // size of in / out / keys arrays
+};
+
+struct MpBuffers {
+  int P = 0, capC = 0, capS = 0, cap_stack = 0, map_cap = 0, max_iter = 10, tmax = 0;
+  int pool_cur = 0;
+  float* state = nullptr;     // [P][kMpStateFloats]
+  int* istate = nullptr;      // [P][kMpStateInts]
+  int* slots = nullptr;       // [2][P][kCubeNum][4] (offC, cntC, offS, cntS) per pool
+  float4* pool = nullptr;     // [2][P][map_cap]
+  int* valid = nullptr;       // [P][kMaxValid]
+  int* vpre = nullptr;        // [P][kMaxValid + 1][2] FromMap prefix (corner, surf)
+  // streaming inputs
+  float4 *inC = nullptr, *inS = nullptr, *inF = nullptr;
+  int* in_n = nullptr;        // [P][3]
+  float* in_pose = nullptr;   // [P][6]
+  // stacks
+  float4* stack2 = nullptr;   // [P][cap_stack] corner at 0, surf at capC
+  float4* stack = nullptr;    // [P][cap_stack] voxel-grid output (same layout)
+  int* nstack = nullptr;      // [P][2]
+  // FromMap + hashes
+  float4* from = nullptr;     // [P][map_cap] corner then surf
+  int *hC_start = nullptr, *hS_start = nullptr, *h_fill = nullptr, *hC_T = nullptr, *hS_T = nullptr;
+  float4 *hC_pts = nullptr, *hS_pts = nullptr;   // [P][map_cap]
+  int* nfrom = nullptr;       // [P][2]
+  // rows
+  float4 *rows_pt = nullptr, *rows_cf = nullptr;  // [P][cap_stack]
+  // insertion / per-cube downsampling
+  int* app_cnt = nullptr;     // [P][kCubeNum][2] appended points per cube
+  int* app_off = nullptr;     // [P][kCubeNum][2]
+  float4* app = nullptr;      // [P][cap_stack] stack points grouped by cube (map frame)
+  float4* vin = nullptr;      // [P][map_cap] per-valid-cube DS input (old ++ appended)
+  float4* vout = nullptr;     // [P][map_cap]
+  int *vseg_b = nullptr, *vseg_e = nullptr, *vseg_cnt = nullptr;  // [P][2*kMaxValid]
+  float* vseg_leaf = nullptr;
+  int *sseg_b = nullptr, *sseg_e = nullptr, *sseg_cnt = nullptr;  // [P][2] stack segments
+  float* sseg_leaf = nullptr;
+  int* vg_params = nullptr;
+  uint32_t *vg_k = nullptr, *vg_k2 = nullptr, *vg_v = nullptr, *vg_v2 = nullptr;
+  void* cub_tmp = nullptr;
+  size_t cub_bytes = 0;
+  float4* reg = nullptr;      // [P][capS] registered full cloud
+  int* nreg = nullptr;
+};
+
+inline int mp_batch_map_capacity(int cap) { return 2 * cap; }
 void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter);
 void mp_free(MpBuffers& b);
+void mp_reset(MpBuffers& b, hipStream_t st);
+void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st);
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
                     const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
                     loam_cloud_out* registered, loam_stats* stats, std::string& err);

@@ -47,7 +47,7 @@ LOAM_D loampose::Imu load_imu(const float* st) {
 __global__ __launch_bounds__(256) void k_hash_build(HashJob j) {
   const int p = blockIdx.x, tid = threadIdx.x;
   const int n = *(const int*)((const char*)j.count + (size_t)p * j.count_stride_bytes);
-  const float4* pts = j.pts + (size_t)p * j.pts_stride;
+  const float4* pts = j.pts + (size_t)p * j.pts_stride + (j.pts_off ? j.pts_off[p * j.pts_off_stride] : 0);
   int* start = j.start + (size_t)p * (j.tmax + 1);
   int* fill = j.fill + (size_t)p * j.tmax;
   float4* out = j.out + (size_t)p * j.pts_stride;
@@ -568,6 +568,8 @@ void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
   HashJob jc;
   jc.pts = b.lastC + (size_t)buf * b.P * b.capC;
   jc.pts_stride = b.capC;
+  jc.pts_off = nullptr;
+  jc.pts_off_stride = 0;
   jc.count = b.nlast + buf * 2 + 0;
   jc.count_stride_bytes = 4 * sizeof(int);
   jc.start = b.hC_start + (size_t)buf * b.P * (b.tC + 1);

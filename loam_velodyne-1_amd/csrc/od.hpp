@@ -29,8 +29,10 @@ struct FeatView {
 };
 
 struct HashJob {
-  const float4* pts;    // cloud of problem p at pts + p * pts_stride
+  const float4* pts;    // cloud of problem p at pts + p * pts_stride (+ pts_off[p * pts_off_stride])
   size_t pts_stride;
+  const int* pts_off;   // optional per-problem element offset (nullptr = 0)
+  int pts_off_stride;
   const int* count;     // count of problem p at (char*)count + p * count_stride_bytes
   size_t count_stride_bytes;
   int* start;           // [P][tmax + 1]

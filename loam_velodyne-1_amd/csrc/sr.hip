@@ -82,8 +82,8 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_sort(SrBuffers b, SrPara
   }
   if (tid == 0) {  // :230-238
     float4 a = raw[sh_first], z = raw[sh_last];
-    float startOri = -atan2f(a.y, a.x);
-    float endOri = (float)(D(-atan2f(z.y, z.x)) + 2 * M_PI);
+    float startOri = -atan2f_fdlibm(a.y, a.x);
+    float endOri = (float)(D(-atan2f_fdlibm(z.y, z.x)) + 2 * M_PI);
     if (D(endOri - startOri) > 3 * M_PI) endOri = (float)(D(endOri) - 2 * M_PI);
     else if (D(endOri - startOri) < M_PI) endOri = (float)(D(endOri) + 2 * M_PI);
     sh_start = startOri;
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_sort(SrBuffers b, SrPara
         int scanID = ring_id(p, angle);
         if (scanID >= 0 && scanID <= R - 1) {
           sid = (uint8_t)scanID;
-          ori = -atan2f(px, pz);
+          ori = -atan2f_fdlibm(px, pz);
           float o1 = ori_first(ori, startOri);
           if (D(o1 - startOri) > M_PI) Floc = min(Floc, i);
           atomicAdd(&sh_cnt[scanID], 1);

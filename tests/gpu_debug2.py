@@ -1,0 +1,39 @@
+"""Diagnostic: mapping parity (streaming + batch) GPU vs oracle."""
+import importlib, os, sys, time
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "oracle"))
+loam = importlib.import_module("loam_velodyne-1_amd")
+sg = importlib.import_module("loam_velodyne-1_amd.synthgen")
+import oracle_ctypes as oc
+np.set_printoptions(precision=5, suppress=True, linewidth=200)
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+sweeps = sg.stream_sweeps(N, 1)
+def stream(impl):
+    out = []
+    for k, sw in enumerate(sweeps):
+        rc, f = impl.scan_registration(sw, stamp=0.1 * k)
+        if rc != 0: continue
+        pub, pose, cl, sl, full = impl.odometry(f)
+        if pub == 7:
+            t = time.time()
+            aft, bef, reg = impl.mapping(pose, cl, sl, full)
+            dt = time.time() - t
+            st = impl.stats()
+            out.append((pose, aft, bef, reg, st, dt))
+    return out
+e = loam.Engine(loam.default_config(system_delay=2)); o = oc.Oracle(oc.default_config(system_delay=2))
+a = stream(e); b = stream(o)
+for x, y in zip(a, b):
+    print("od", np.abs(x[0]-y[0]).max(), "aft", np.abs(x[1]-y[1]).max(), "bef", np.abs(x[2]-y[2]).max(),
+          "reg", np.abs(x[3][:, :3]-y[3][:, :3]).max() if x[3].shape == y[3].shape else (x[3].shape, y[3].shape),
+          "it", x[4]["mp_iters"], y[4]["mp_iters"], "rows", x[4]["mp_rows_sum"], y[4]["mp_rows_sum"],
+          "stack", x[4]["mp_stack"], y[4]["mp_stack"], "map", x[4]["mp_map_points"], y[4]["mp_map_points"],
+          "vp", x[4]["mp_map_valid_points"], y[4]["mp_map_valid_points"], "t", round(x[5], 4), round(y[5], 4))
+prevs, curs = sg.batch_problems(16)
+eb = loam.Engine(); eb.batch_upload(prevs, curs)
+eb.batch_run(); od, aft, st = eb.batch_download()
+t = time.time(); eb.batch_run(); od, aft, st = eb.batch_download(); print("batch16", time.time() - t, st)
+for i in range(16):
+    odo, afto, sto = oc.problem(prevs[i], curs[i])
+    print(i, np.abs(od[i] - odo).max(), np.abs(aft[i] - afto).max(), sto["mp_iters"], aft[i], afto)
