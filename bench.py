@@ -1,0 +1,189 @@
+"""Benchmark: scans/sec of the LOAM hot path (scan registration + odometry L-M + mapping L-M) on
+MI355X, BASELINE.json config 4 shape: independent synthetic VLP-16 problems, sharded across ranks.
+
+One step = one pass of the whole hot path over this rank's batch of problems, inputs resident in
+HBM: scan registration of both sweeps of every problem, odometry seeded from prev and solved on
+cur, mapping of prev into an empty map and solved for cur.  Weak scaling: every
+rank owns --batch problems (seeds 1000 + global index); the data path has no collective; one RCCL
+all-gather of the poses after the timed steps.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--cpu-seconds S]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "scans/sec (odometry+mapping L-M solve) VLP-16 sweep, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def kernel_bytes(st):
+    """Algorithmic HBM bytes per launch of each kernel over the whole batch."""
+    sr_in = 16 * st["n_raw"]
+    feats = 16 * (st["n_sharp"] + st["n_less_sharp"] + st["n_flat"] + st["n_less_flat"])
+    od_assoc = 16 * st["od_assoc_rounds"] * 0  # per-problem product accounted in bytes_od
+    return {
+        "k_sr_ring_sort": sr_in + 16 * st["n_ring"],
+        "k_sr_features": 16 * st["n_ring"],
+        "k_sr_select": 16 * st["n_ring"] + feats,
+        "k_od_solve": st["bytes_od"] - od_assoc,
+        "k_mp_solve": 16 * st["mp_stack"] + 80 * st["mp_stack"] + 64 * st["mp_rows_sum"],
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1024, help="problems per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--profile-steps", type=int, default=3)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    loam = importlib.import_module("loam_velodyne-1_amd")
+    sg = importlib.import_module("loam_velodyne-1_amd.synthgen")
+
+    B = args.batch
+    prevs, curs = sg.batch_problems(B, base_seed=1000 + rank * B)
+    eng = loam.Engine(device=local)
+    eng.batch_upload(prevs, curs)
+
+    def sync():
+        eng.sync()
+
+    for _ in range(args.warmup):
+        eng.batch_run()
+    sync()
+
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.batch_run()
+    sync()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+
+    od, aft, st = eng.batch_download()
+
+    # per-kernel device times of the same workload (HIP events on the engine stream), untimed
+    eng.set_profiling(True)
+    for _ in range(args.profile_steps):
+        eng.batch_run()
+    eng.batch_download()
+    ktimes = eng.kernel_times()
+    eng.set_profiling(False)
+
+    if dist:  # the one collective: gather every rank's poses (RCCL all-gather)
+        import torch
+        mine = torch.from_numpy(np.concatenate([od, aft], axis=1).astype(np.float32)).to(f"cuda:{local}")
+        allp = torch.empty((world * B, 12), dtype=torch.float32, device=f"cuda:{local}")
+        dist.all_gather_into_tensor(allp, mine)
+        torch.cuda.synchronize()
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * B * args.steps / elapsed
+
+    # roofline of the dominant kernel: algorithmic bytes per launch / average launch duration
+    kb = kernel_bytes(st)
+    dom = max(ktimes.items(), key=lambda kv: kv[1][0])[0] if ktimes else None
+    roof = None
+    if dom:
+        tot_ms, launches = ktimes[dom]
+        avg_ms = tot_ms / max(launches, 1)
+        nbytes = kb.get(dom)
+        launches_per_step = launches / max(args.profile_steps, 1)
+        per_launch = nbytes / launches_per_step if nbytes is not None else None
+        achieved = per_launch / (avg_ms * 1e-3) / 1e9 if per_launch is not None else None
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tpath):
+            try:
+                traffic = json.load(open(tpath)).get(dom)
+            except Exception:
+                traffic = None
+        roof = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved is not None else None,
+                "traffic": traffic, "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": per_launch}
+
+    # CPU baseline: the oracle (single-thread C++ restatement) on a bounded sample, N=1 only
+    cpu = None
+    parity = None
+    if world == 1 and args.cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_ctypes as oc
+        n_done, t_cpu, err_od, err_mp = 0, 0.0, 0.0, 0.0
+        while n_done < B and (t_cpu < args.cpu_seconds or n_done < 4):
+            a = time.perf_counter()
+            od_o, aft_o, _ = oc.problem(prevs[n_done], curs[n_done])
+            t_cpu += time.perf_counter() - a
+            err_od = max(err_od, float(np.abs(od[n_done] - od_o).max()))
+            err_mp = max(err_mp, float(np.abs(aft[n_done] - aft_o).max()))
+            n_done += 1
+        cpu = {"value": n_done / t_cpu, "unit": "scans/s", "cores": 1, "kind": "port",
+               "sample": f"first {n_done} problems of the batch (seeds 1000..{999 + n_done}), "
+                         f"oracle/liboracle.so -O3 single thread, {t_cpu:.1f} s"}
+        parity = {"problems_checked": n_done, "max_abs_err_odometry": err_od, "max_abs_err_mapping": err_mp}
+
+    stage_ms = {k: round(v[0] / max(args.profile_steps, 1), 4) for k, v in sorted(ktimes.items())}
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "scans/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32 (fp64 JtJ accumulation)",
+        "data": "synthetic (seeded VLP-16 ray-cast sweeps, random planes+edges scenes; bags unavailable offline)",
+        "config": {"workload": "config4: independent VLP-16 problems (SR prev+cur, odometry L-M, mapping L-M)",
+                   "problems_per_gpu": B, "global_batch": world * B, "points_per_sweep": 28800,
+                   "parallelism": f"shard{world}"},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "parity": parity,
+        "kernel_ms_per_step": stage_ms,
+    }
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -132,10 +132,16 @@ int loam_maintenance(const loam_pose6 *odom_sum, const loam_pose6 *bef, const lo
 int loam_batch_upload(loam_ctx *ctx, uint32_t n, const loam_cloud_in *prev,
                       const loam_cloud_in *cur);
 int loam_batch_run(loam_ctx *ctx);
+int loam_batch_sync(loam_ctx *ctx);   /* waits for the work enqueued by loam_batch_run */
 int loam_batch_download(loam_ctx *ctx, loam_pose6 *od_sum, loam_pose6 *aft, loam_stats *stats);
 
 /* last-call statistics of a context (stage device times, counts, algorithmic bytes) */
 int loam_get_stats(loam_ctx *ctx, loam_stats *stats);
+
+/* diagnostics (no reference equivalent): per-kernel device time of the batch path, measured with
+ * HIP events on the context stream.  loam_get_kernel_times writes "name total_ms launches\n" lines. */
+int loam_set_profiling(loam_ctx *ctx, int on);
+int loam_get_kernel_times(loam_ctx *ctx, char *buf, uint32_t cap);
 
 #ifdef __cplusplus
 }

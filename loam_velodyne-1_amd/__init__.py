@@ -81,7 +81,8 @@ class Stats(ctypes.Structure):
 
 EXPORTS = ("loam_config_default", "loam_create", "loam_destroy", "loam_last_error",
            "loam_scan_registration", "loam_odometry", "loam_mapping", "loam_maintenance",
-           "loam_batch_upload", "loam_batch_run", "loam_batch_download", "loam_get_stats")
+           "loam_batch_upload", "loam_batch_run", "loam_batch_sync", "loam_batch_download", "loam_get_stats",
+           "loam_set_profiling", "loam_get_kernel_times")
 
 
 def lib():
@@ -103,6 +104,9 @@ def lib():
         L.loam_maintenance.argtypes = [P(Pose6)] * 4
         L.loam_batch_upload.argtypes = [PP, ctypes.c_uint32, P(CloudIn), P(CloudIn)]
         L.loam_batch_run.argtypes = [PP]
+        L.loam_batch_sync.argtypes = [PP]
+        L.loam_set_profiling.argtypes = [PP, ctypes.c_int]
+        L.loam_get_kernel_times.argtypes = [PP, ctypes.c_char_p, ctypes.c_uint32]
         L.loam_batch_download.argtypes = [PP, P(Pose6), P(Pose6), P(Stats)]
         L.loam_get_stats.argtypes = [PP, P(Stats)]
         _LIB = L
@@ -208,6 +212,22 @@ class Engine:
 
     def batch_run(self):
         _check(lib().loam_batch_run(self.h))
+
+    def sync(self):
+        _check(lib().loam_batch_sync(self.h))
+
+    def set_profiling(self, on):
+        _check(lib().loam_set_profiling(self.h, 1 if on else 0))
+
+    def kernel_times(self):
+        """{kernel: (total_ms, launches)} accumulated since profiling was enabled"""
+        buf = ctypes.create_string_buffer(1 << 16)
+        _check(lib().loam_get_kernel_times(self.h, buf, len(buf)))
+        out = {}
+        for line in buf.value.decode().splitlines():
+            name, ms, n = line.split()
+            out[name] = (float(ms), int(n))
+        return out
 
     def batch_download(self):
         od = (Pose6 * self.n)()

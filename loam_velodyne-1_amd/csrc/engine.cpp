@@ -80,6 +80,7 @@ struct loam_ctx {
   MpBuffers mpb;
   std::vector<float4> stage;
   loam_stats stats;
+  Prof prof;
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -217,6 +218,26 @@ void loam_destroy(loam_ctx* x) {
     if (e) (void)hipEventDestroy(e);
   if (x->st) (void)hipStreamDestroy(x->st);
   delete x;
+}
+
+int loam_set_profiling(loam_ctx* x, int on) {
+  if (!x) return fail(LOAM_E_INVAL, "null argument");
+  x->prof.on = on != 0;
+  x->prof.acc.clear();
+  return LOAM_OK;
+}
+
+int loam_get_kernel_times(loam_ctx* x, char* buf, uint32_t cap) {
+  if (!x || !buf || cap == 0) return fail(LOAM_E_INVAL, "null argument");
+  std::string s;
+  for (auto& kv : x->prof.acc) {
+    char line[256];
+    std::snprintf(line, sizeof(line), "%s %.6f %ld\n", kv.first.c_str(), kv.second.first, kv.second.second);
+    s += line;
+  }
+  if (s.size() + 1 > cap) return fail(LOAM_E_CAPACITY, "buffer too small");
+  std::memcpy(buf, s.c_str(), s.size() + 1);
+  return LOAM_OK;
 }
 
 int loam_get_stats(loam_ctx* x, loam_stats* s) {
@@ -424,22 +445,35 @@ int loam_batch_run(loam_ctx* x) {
   HIP_TRY(hipSetDevice(x->device));
   const int P = x->P;
   OdBuffers& o = x->odb;
+  Prof* pf = x->prof.on ? &x->prof : nullptr;
   HIP_TRY(hipEventRecord(x->ev[0], x->st));
-  sr_launch(x->srb, sr_params(x), x->st);
+  x->prof.begin(x->st);
+  sr_launch(x->srb, sr_params(x), x->st, pf);
   HIP_TRY(hipEventRecord(x->ev[1], x->st));
   HIP_TRY(hipMemsetAsync(o.state, 0, (size_t)P * kOdStateFloats * sizeof(float), x->st));
   HIP_TRY(hipMemsetAsync(o.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st));
   const FeatView fprev = feat_view(x->srb, 0, 2), fcur = feat_view(x->srb, 1, 2);
   // odometry seeded from prev as a solved zero-increment frame, then one loop body on cur
   hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fprev, 0, 1, 1);
+  x->prof.mark("k_od_end_seed");
   od_build_hashes(o, 0, x->st);
+  x->prof.mark("k_hash_build_last");
   hipLaunchKernelGGL(k_od_solve, dim3(P), dim3(256), 0, x->st, o, fcur, 0);
+  x->prof.mark("k_od_solve");
   hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, 1, 2, 1);
+  x->prof.mark("k_od_end");
   HIP_TRY(hipEventRecord(x->ev[2], x->st));
   // mapping: prev into an empty map at the origin, then cur with the odometry pose
-  mp_batch_run(x->mpb, o, x->st);
+  mp_batch_run(x->mpb, o, x->st, pf);
   HIP_TRY(hipEventRecord(x->ev[3], x->st));
   HIP_TRY(hipGetLastError());
+  return LOAM_OK;
+}
+
+int loam_batch_sync(loam_ctx* x) {
+  if (!x) return fail(LOAM_E_INVAL, "null argument");
+  HIP_TRY(hipSetDevice(x->device));
+  HIP_TRY(hipStreamSynchronize(x->st));
   return LOAM_OK;
 }
 
@@ -494,6 +528,7 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
       per += (uint64_t)ist[(size_t)i * kOdStateInts + kIsAssoc] * 16 * (nl[i * 4 + 0] + nl[i * 4 + 1]);
     s.bytes_od = per + 16 * s.od_queries + 12 * s.od_queries + 32 * s.od_rows_sum;
   }
+  x->prof.collect();
   float ms_sr = 0, ms_od = 0, ms_mp = 0;
   (void)hipEventElapsedTime(&ms_sr, x->ev[0], x->ev[1]);
   (void)hipEventElapsedTime(&ms_od, x->ev[1], x->ev[2]);

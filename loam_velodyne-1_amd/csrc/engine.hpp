@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include "../../include/loam/loam.h"
+#include "prof.hpp"
 
 namespace loam {
 
@@ -63,7 +64,7 @@ struct SrParams {
 void sr_alloc(SrBuffers& b, int S, int cap, int R);
 void sr_free(SrBuffers& b);
 // runs the whole scan registration for sweeps [0, S) already in b.raw / b.raw_n
-void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st);
+void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof = nullptr);
 
 }  // namespace loam
 

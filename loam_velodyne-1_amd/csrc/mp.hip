@@ -870,16 +870,21 @@ void mp_reset(MpBuffers& b, hipStream_t st) {
   hipLaunchKernelGGL(k_mp_reset, dim3((b.P + 255) / 256), dim3(256), 0, st, b);
 }
 
-void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st) {
+void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
   const int P = b.P;
+  auto mark = [&](const char* n) { if (prof) prof->mark(n); };
   hipLaunchKernelGGL(k_mp_prepare, dim3(P), dim3(kMpThreads), 0, st, b, in);
+  mark("k_mp_prepare");
   hipLaunchKernelGGL(k_mp_stack, dim3(16, P), dim3(256), 0, st, b, in);
+  mark("k_mp_stack");
   VgJob js;
   js.in = b.stack2; js.out = b.stack; js.begin = b.sseg_b; js.end = b.sseg_e; js.leaf = b.sseg_leaf;
   js.out_count = b.sseg_cnt; js.params = b.vg_params; js.keys = b.vg_k; js.keys_alt = b.vg_k2;
   js.vals = b.vg_v; js.vals_alt = b.vg_v2; js.nseg = 2 * P; js.total = P * b.cap_stack;
   vg_run(js, b.cub_tmp, b.cub_bytes, st);
+  mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);
+  mark("k_mp_gather");
   HashJob hc;
   hc.pts = b.from; hc.pts_stride = b.map_cap; hc.pts_off = nullptr; hc.pts_off_stride = 0;
   hc.count = b.nfrom; hc.count_stride_bytes = 2 * sizeof(int);
@@ -890,19 +895,26 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st) {
   hs.pts_off = b.nfrom; hs.pts_off_stride = 2;
   hs.count = b.nfrom + 1; hs.start = b.hS_start; hs.out = b.hS_pts; hs.tsize = b.hS_T;
   hipLaunchKernelGGL(k_hash_build, dim3(P), dim3(256), 0, st, hs);
+  mark("k_hash_build_map");
   hipLaunchKernelGGL(k_mp_solve, dim3(P), dim3(kMpThreads), 0, st, b);
+  mark("k_mp_solve");
   // insertion + per-valid-cube downsampling into the other pool
   hipLaunchKernelGGL(k_mp_insert, dim3(P), dim3(kMpThreads), 0, st, b, (int*)b.vg_k, (int*)b.vg_v);
+  mark("k_mp_insert");
   hipLaunchKernelGGL(k_mp_vseg, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_vcopy, dim3(32, P), dim3(256), 0, st, b);
+  mark("k_mp_vseg_vcopy");
   VgJob jv;
   jv.in = b.vin; jv.out = b.vout; jv.begin = b.vseg_b; jv.end = b.vseg_e; jv.leaf = b.vseg_leaf;
   jv.out_count = b.vseg_cnt; jv.params = b.vg_params; jv.keys = b.vg_k; jv.keys_alt = b.vg_k2;
   jv.vals = b.vg_v; jv.vals_alt = b.vg_v2; jv.nseg = 2 * kMaxValid * P; jv.total = P * b.map_cap;
   vg_run(jv, b.cub_tmp, b.cub_bytes, st);
+  mark("vg_cubes");
   hipLaunchKernelGGL(k_mp_compact_table, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);
+  mark("k_mp_compact");
   hipLaunchKernelGGL(k_mp_register, dim3(16, P), dim3(256), 0, st, b, in);
+  mark("k_mp_register");
   b.pool_cur = 1 - b.pool_cur;
 }
 
@@ -978,8 +990,9 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   return rc;
 }
 
-void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st) {
+void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof) {
   mp_reset(b, st);
+  if (prof) prof->mark("mp_reset");
   MpInput in;
   // frame 1: prev (Last[0], fullEnd[0]) at the zero pose
   in.corner = od.lastC; in.surf = od.lastS; in.full = od.fullEnd;
@@ -987,14 +1000,14 @@ void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st) {
   in.ncorner = od.nlast + 0; in.nsurf = od.nlast + 1; in.nfull = od.nfullEnd + 0;
   in.ncorner_stride = 4; in.nsurf_stride = 4; in.nfull_stride = 2;
   in.pose = nullptr; in.pose_stride = 0;
-  mp_frame(b, in, st);
+  mp_frame(b, in, st, prof);
   // frame 2: cur (Last[1], fullEnd[1]) with the odometry transformSum
   in.corner = od.lastC + (size_t)od.P * od.capC;
   in.surf = od.lastS + (size_t)od.P * od.capS;
   in.full = od.fullEnd + (size_t)od.P * od.capS;
   in.ncorner = od.nlast + 2; in.nsurf = od.nlast + 3; in.nfull = od.nfullEnd + 1;
   in.pose = od.state + kOdSum; in.pose_stride = kOdStateFloats;
-  mp_frame(b, in, st);
+  mp_frame(b, in, st, prof);
 }
 
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err) {

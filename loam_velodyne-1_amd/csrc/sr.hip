@@ -651,14 +651,20 @@ void sr_free(SrBuffers& b) {
   b = SrBuffers();
 }
 
-void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st) {
+void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof) {
+  auto mark = [&](const char* n) { if (prof) prof->mark(n); };
   HIPCHK(hipMemsetAsync(b.ring_se, 0, (size_t)b.S * 2 * b.R * sizeof(int), st));
   HIPCHK(hipMemsetAsync(b.err, 0, (size_t)b.S * sizeof(int), st));
+  mark("sr_memset");
   hipLaunchKernelGGL(k_sr_ring_sort, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
+  mark("k_sr_ring_sort");
   hipLaunchKernelGGL(k_sr_features, dim3((b.cap + kFeatTile - 1) / kFeatTile, b.S), dim3(kFeatTile), 0,
                      st, b, p);
+  mark("k_sr_features");
   hipLaunchKernelGGL(k_sr_select, dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
+  mark("k_sr_select");
   hipLaunchKernelGGL(k_sr_compact, dim3(b.S), dim3(256), 0, st, b, p);
+  mark("k_sr_compact");
 }
 
 }  // namespace loam

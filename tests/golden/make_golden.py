@@ -1,0 +1,64 @@
+"""Regenerates tests/golden/oracle_golden.json: outputs of the CPU oracle (oracle/liboracle.so) on
+the seeded synthetic configs.  PARITY UNPINNED: the reference cannot be built or run here and
+ships no fixtures, so these vectors are regression pins of the oracle itself (they catch drift of
+the restatement and are the GPU engine's targets); see DESIGN.md §5.
+
+    python tests/golden/make_golden.py
+"""
+import hashlib
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+def digest(a):
+    return hashlib.sha256(np.ascontiguousarray(a, np.float32).tobytes()).hexdigest()
+
+
+def main():
+    import oracle_ctypes as oc
+    sg = importlib.import_module("loam_velodyne-1_amd.synthgen")
+    out = {"note": "oracle outputs on seeded synthetic inputs (regression pins; parity vs the reference unpinned)"}
+    prev, cur = sg.single_problem(0)
+    o = oc.Oracle(oc.default_config(system_delay=1))
+    o.scan_registration(cur)
+    rc, f = o.scan_registration(cur)
+    out["config2_sr_cur"] = {k: {"count": int(v.shape[0]), "sha256": digest(v)} for k, v in f.items()}
+    od, aft, st = oc.problem(prev, cur)
+    out["config2_problem"] = {"od_sum": od.tolist(), "aft": aft.tolist(),
+                              "od_iters": int(st["od_iters"]), "mp_iters": int(st["mp_iters"])}
+    prevs, curs = sg.batch_problems(8, base_seed=1000)
+    out["config4_first8"] = [dict(zip(("od_sum", "aft"), [x.tolist() for x in oc.problem(prevs[i], curs[i])[:2]]))
+                             for i in range(8)]
+    hp, hc = sg.single_problem(2, lidar=sg.HDL64)
+    hcfg = oc.default_config(n_rings=64, ring_model=1, max_points=160000)
+    od, aft, st = oc.problem(hp, hc, hcfg)
+    out["config5_problem"] = {"od_sum": od.tolist(), "aft": aft.tolist()}
+    sweeps = sg.stream_sweeps(30, 1)
+    o = oc.Oracle(oc.default_config(system_delay=2))
+    traj = []
+    for k, sw in enumerate(sweeps):
+        rc, f = o.scan_registration(sw)
+        if rc:
+            continue
+        pub, pose, cl, sl, full = o.odometry(f)
+        rec = {"pub": int(pub), "od_sum": pose.tolist() if pub & 1 else None}
+        if pub == 7:
+            a, b, reg = o.mapping(pose, cl, sl, full)
+            rec.update(aft=a.tolist(), bef=b.tolist(), registered_sha256=digest(reg))
+        traj.append(rec)
+    out["config3_first30"] = traj
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle_golden.json")
+    json.dump(out, open(path, "w"), indent=1)
+    print("wrote", path)
+
+
+if __name__ == "__main__":
+    main()

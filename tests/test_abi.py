@@ -1,0 +1,64 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every function declared in
+include/loam/loam.h, reports the reference defaults, refuses to run without a GPU (no CPU
+fallback), and its host-side pose algebra (transformMaintenance) matches the oracle bit for bit."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "loam", "loam.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(loam_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_exports_every_declared_symbol(loam):
+    lib = loam.lib()
+    names = header_functions()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(loam.EXPORTS)
+
+
+def test_config_defaults_are_reference_constants(loam):
+    c = loam.default_config()
+    assert (c.n_rings, c.system_delay, c.max_points, c.od_max_iter, c.mp_max_iter, c.skip_frame_num) == \
+        (16, 20, 40000, 25, 10, 1)   # scanRegistration.cpp:57-66, laserOdometry.cpp:51,470, laserMapping.cpp:710
+
+
+def test_no_cpu_fallback(loam):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(loam.LoamError) as ei:
+        loam.Engine()
+    assert ei.value.code == loam.LOAM_E_HIP
+
+
+def test_bad_config_rejected(loam):
+    h = ctypes.c_void_p()
+    cfg = loam.default_config(n_rings=0)
+    assert loam.lib().loam_create(ctypes.byref(h), ctypes.byref(cfg), 0) == loam.LOAM_E_INVAL
+
+
+def test_maintenance_matches_oracle(loam, oc):
+    rng = np.random.default_rng(7)
+    for _ in range(200):
+        s, b, a = (np.concatenate([rng.uniform(-0.6, 0.6, 3), rng.uniform(-50, 50, 3)]).astype(np.float32)
+                   for _ in range(3))
+        g = loam.maintenance(s, b, a)
+        o = oc.maintenance(s, b, a)
+        np.testing.assert_array_equal(g, o)
+
+
+def test_maintenance_identity(loam):
+    # with Bef == Sum the integrated pose is the mapped pose (transformMaintenance.cpp:60-145)
+    p = np.array([0.01, -0.2, 0.03, 1.0, -2.0, 3.0], np.float32)
+    out = loam.maintenance(p, p, p)
+    assert np.abs(out - p).max() < 1e-5

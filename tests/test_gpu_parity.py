@@ -120,3 +120,104 @@ def test_batch_single_problem_config2(loam, oc, sg):
     od_o, aft_o, st_o = oc.problem(prev, cur)
     assert np.abs(od[0] - od_o).max() <= POSE_TOL
     assert st["od_iters"] == st_o["od_iters"]
+
+
+def test_mapping_stream_parity(loam, oc, sg):
+    sweeps = sg.stream_sweeps(30, 1)
+    cfg = dict(system_delay=2)
+    pg, mg = _stream(loam.Engine(loam.default_config(**cfg)), sweeps, mapping=True)
+    po, mo = _stream(oc.Oracle(oc.default_config(**cfg)), sweeps, mapping=True)
+    assert len(mg) == len(mo) >= 10
+    for (ag, bg), (ao, bo) in zip(mg, mo):
+        assert np.abs(ag - ao).max() <= POSE_TOL
+        assert np.abs(bg - bo).max() <= POSE_TOL
+
+
+def test_golden_config3_stream(loam, sg):
+    import json, os, hashlib
+    G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "oracle_golden.json")))
+    sweeps = sg.stream_sweeps(30, 1)
+    e = loam.Engine(loam.default_config(system_delay=2))
+    traj = []
+    for k, sw in enumerate(sweeps):
+        rc, f = e.scan_registration(sw)
+        if rc:
+            continue
+        pub, pose, cl, sl, full = e.odometry(f)
+        rec = {"pub": pub, "od": pose}
+        if pub == 7:
+            a, b, reg = e.mapping(pose, cl, sl, full)
+            rec.update(aft=a, bef=b, reg=hashlib.sha256(np.ascontiguousarray(reg, np.float32).tobytes()).hexdigest())
+        traj.append(rec)
+    assert len(traj) == len(G["config3_first30"])
+    for r, g in zip(traj, G["config3_first30"]):
+        assert r["pub"] == g["pub"]
+        if g["od_sum"] is not None:
+            assert np.abs(r["od"] - np.float32(g["od_sum"])).max() <= POSE_TOL
+        if "aft" in g:
+            assert np.abs(r["aft"] - np.float32(g["aft"])).max() <= POSE_TOL
+
+
+def test_golden_config4(loam, sg):
+    import json, os
+    G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "oracle_golden.json")))
+    prevs, curs = sg.batch_problems(8, base_seed=1000)
+    e = loam.Engine()
+    e.batch_upload(prevs, curs)
+    e.batch_run()
+    od, aft, st = e.batch_download()
+    for i in range(8):
+        assert np.abs(od[i] - np.float32(G["config4_first8"][i]["od_sum"])).max() <= POSE_TOL
+        assert np.abs(aft[i] - np.float32(G["config4_first8"][i]["aft"])).max() <= POSE_TOL
+
+
+def test_batch_mapping_parity_64(loam, oc, sg):
+    prevs, curs = sg.batch_problems(64, base_seed=1100)
+    e = loam.Engine()
+    e.batch_upload(prevs, curs)
+    e.batch_run()
+    od, aft, st = e.batch_download()
+    errs = []
+    for i in range(64):
+        od_o, aft_o, _ = oc.problem(prevs[i], curs[i])
+        errs.append(max(np.abs(od[i] - od_o).max(), np.abs(aft[i] - aft_o).max()))
+    assert max(errs) <= POSE_TOL, errs
+    # the repeated run of the same batch is deterministic
+    e.batch_run()
+    od2, aft2, _ = e.batch_download()
+    np.testing.assert_array_equal(od, od2)
+    np.testing.assert_array_equal(aft, aft2)
+
+
+def test_hdl64_problem_config5(loam, oc, sg):
+    prev, cur = sg.single_problem(2, lidar=sg.HDL64)
+    kw = dict(n_rings=64, ring_model=loam.RING_LINEAR, max_points=160000)
+    e = loam.Engine(loam.default_config(**kw))
+    e.batch_upload([prev], [cur])
+    e.batch_run()
+    od, aft, st = e.batch_download()
+    od_o, aft_o, _ = oc.problem(prev, cur, oc.default_config(**kw))
+    assert np.abs(od[0] - od_o).max() <= POSE_TOL
+    assert np.abs(aft[0] - aft_o).max() <= POSE_TOL
+
+
+def test_capacity_and_empty_errors(loam, sg):
+    e = loam.Engine(loam.default_config(system_delay=0, max_points=20000))
+    _, cur = sg.single_problem(0)
+    e.scan_registration(cur[:100])                      # consumed by systemDelay
+    with pytest.raises(loam.LoamError) as ei:
+        e.scan_registration(cur)                        # 28800 > max_points
+    assert ei.value.code == loam.LOAM_E_CAPACITY
+    nan = np.full((50, 4), np.nan, np.float32)
+    with pytest.raises(loam.LoamError) as ei:
+        e.scan_registration(nan)
+    assert ei.value.code == loam.LOAM_E_INVAL
+
+
+def test_maintenance_chain(loam, oc, sg):
+    prev, cur = sg.single_problem(0)
+    e = loam.Engine()
+    e.batch_upload([prev], [cur])
+    e.batch_run()
+    od, aft, st = e.batch_download()
+    np.testing.assert_array_equal(loam.maintenance(od[0], od[0], aft[0]), oc.maintenance(od[0], od[0], aft[0]))
