@@ -27,16 +27,18 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
 def kernel_bytes(st):
-    """Algorithmic HBM bytes per launch of each kernel over the whole batch."""
-    sr_in = 16 * st["n_raw"]
+    """Algorithmic HBM bytes of each kernel over one step of the whole batch (SURVEY.md §8(d),
+    split by the kernel that moves them)."""
     feats = 16 * (st["n_sharp"] + st["n_less_sharp"] + st["n_flat"] + st["n_less_flat"])
-    od_assoc = 16 * st["od_assoc_rounds"] * 0  # per-problem product accounted in bytes_od
     return {
-        "k_sr_ring_sort": sr_in + 16 * st["n_ring"],
+        "k_sr_ring_sort": 16 * st["n_raw"] + 16 * st["n_ring"],
         "k_sr_features": 16 * st["n_ring"],
         "k_sr_select": 16 * st["n_ring"] + feats,
-        "k_od_solve": st["bytes_od"] - od_assoc,
-        "k_mp_solve": 16 * st["mp_stack"] + 80 * st["mp_stack"] + 64 * st["mp_rows_sum"],
+        "k_od_solve": st["bytes_od"],
+        # per iteration: stack point 16 B + 5 neighbours 80 B read, row (16 B point + 16 B coeff) written
+        "k_mp_query": 96 * st["mp_stack_iters"] + 32 * st["mp_rows_sum"],
+        # rows read back for JtJ
+        "k_mp_iter": 32 * st["mp_rows_sum"],
     }
 
 

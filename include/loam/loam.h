@@ -88,7 +88,9 @@ typedef struct {
   uint64_t n_raw, n_ring;                       /* SR input points, ring-sorted points */
   uint64_t n_sharp, n_less_sharp, n_flat, n_less_flat;
   uint64_t od_iters, od_assoc_rounds, od_rows_sum, od_corner_last, od_surf_last, od_queries;
+  uint64_t od_assoc_points;                     /* sum over problems of rounds x (C + S) */
   uint64_t mp_iters, mp_rows_sum, mp_stack, mp_map_points, mp_map_valid_points;
+  uint64_t mp_stack_iters;                      /* sum over problems of iterations x stack size */
   uint64_t bytes_sr, bytes_od, bytes_mp;        /* algorithmic bytes, SURVEY.md §8(d) */
   double ms_sr, ms_od, ms_mp;                   /* device time per stage (HIP events) */
 } loam_stats;

@@ -139,10 +139,9 @@ SrParams sr_params(const loam_ctx* c) {
 void count_bytes(loam_stats& s) {
   // algorithmic bytes, SURVEY.md §8(d)
   s.bytes_sr = 16 * s.n_raw + 32 * s.n_ring + 16 * (s.n_sharp + s.n_less_sharp + s.n_flat + s.n_less_flat);
-  s.bytes_od = s.od_assoc_rounds * 16 * (s.od_corner_last + s.od_surf_last) + 16 * s.od_queries +
-               12 * s.od_queries + 32 * s.od_rows_sum;
-  s.bytes_mp = 16 * s.mp_map_points + 96 * s.mp_stack * (s.mp_iters ? 1 : 0) + 64 * s.mp_rows_sum +
-               32 * s.mp_stack + 32 * s.mp_map_valid_points;
+  s.bytes_od = 16 * s.od_assoc_points + 16 * s.od_queries + 12 * s.od_queries + 32 * s.od_rows_sum;
+  s.bytes_mp = 16 * s.mp_map_points + 96 * s.mp_stack_iters + 64 * s.mp_rows_sum + 32 * s.mp_stack +
+               32 * s.mp_map_valid_points;
 }
 
 }  // namespace
@@ -374,6 +373,7 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
   x->stats.od_queries = ist[kIsQueries];
   x->stats.od_corner_last = nl[cur * 2 + 0];
   x->stats.od_surf_last = nl[cur * 2 + 1];
+  x->stats.od_assoc_points = (uint64_t)ist[kIsAssoc] * (nl[cur * 2 + 0] + nl[cur * 2 + 1]);
   count_bytes(x->stats);
   return e ? LOAM_E_CAPACITY : LOAM_OK;
 }
@@ -519,15 +519,9 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
     s.od_queries += q[kIsQueries];
     s.od_corner_last += nl[i * 4 + 0];
     s.od_surf_last += nl[i * 4 + 1];
+    s.od_assoc_points += (uint64_t)q[kIsAssoc] * (nl[i * 4 + 0] + nl[i * 4 + 1]);
   }
-  // per-problem association rounds multiply per-problem cloud sizes: use the mean
   count_bytes(s);
-  if (P > 0 && s.od_assoc_rounds) {
-    uint64_t per = 0;
-    for (int i = 0; i < P; ++i)
-      per += (uint64_t)ist[(size_t)i * kOdStateInts + kIsAssoc] * 16 * (nl[i * 4 + 0] + nl[i * 4 + 1]);
-    s.bytes_od = per + 16 * s.od_queries + 12 * s.od_queries + 32 * s.od_rows_sum;
-  }
   x->prof.collect();
   float ms_sr = 0, ms_od = 0, ms_mp = 0;
   (void)hipEventElapsedTime(&ms_sr, x->ev[0], x->ev[1]);

@@ -8,16 +8,20 @@
 //  vg_run          segmented PCL VoxelGrid (hipCUB segmented radix sort by voxel index; equal keys
 //                  keep input order) for the stacks (:693-701) and the valid cubes (:1018-1036)
 //  k_mp_gather     FromMap = valid cubes concatenated (:674-681), then voxel-hashed (k_hash_build)
-//  k_mp_solve      the L-M loop (:706-978) in one workgroup per instance: lane per stack point,
-//                  exact 5-NN through the 1 m hash (any point within the 1 m acceptance radius lies
-//                  in the 27 cells), corner PCA with the 3x3 Jacobi, surface 5x3 QR plane, rows
-//                  (cleared every iteration), fp64 JᵀJ, 6x6 solve on one lane; transformUpdate.
+//  k_mp_query      one L-M iteration's correspondences (:714-877) for every instance at once, lane
+//                  per stack point: exact 5-NN through the 1 m hash (any point within the 1 m
+//                  acceptance radius lies in the 27 cells), corner PCA with the 3x3 Jacobi, surface
+//                  5x3 QR plane, weight -> accepted flag + coefficients
+//  k_mp_iter       per instance: fp64 JᵀJ / Jᵀb of the accepted rows, the 6x6 solve and
+//                  degeneracy projection on one lane, update, convergence (:879-974)
+//  k_mp_lm_end     transformUpdate (:199-232)
 //  k_mp_insert     stack -> cubes in stack order (:980-1016)
 //  k_mp_vcopy      per valid cube: old content ++ appended points -> DS input
 //  k_mp_compact    new cube store (valid cubes downsampled, others appended) into the other pool
 //  k_mp_register   full cloud to the map frame (:1060-1063)
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -325,11 +329,11 @@ struct Top5 {
   int i[5];
 };
 LOAM_D void top5_offer(Top5& t, float d, int idx) {
-  // ascending (distance, index); a point already held (duplicate bucket) is skipped
+  // ascending (distance, index); a point already held (two cells in one bucket) is skipped
+  if (d > t.d[4] || (d == t.d[4] && idx > t.i[4])) return;
 #pragma unroll
   for (int k = 0; k < 5; ++k)
     if (t.i[k] == idx) return;
-  if (d > t.d[4] || (d == t.d[4] && idx > t.i[4])) return;
   t.d[4] = d;
   t.i[4] = idx;
 #pragma unroll
@@ -342,42 +346,58 @@ LOAM_D void top5_offer(Top5& t, float d, int idx) {
   }
 }
 
+// exact 5-NN within the 27 cells around q (1 m cells); every bucket range is fetched up front so
+// the 27 loads are in flight together
 LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t) {
 #pragma unroll
   for (int k = 0; k < 5; ++k) { t.d[k] = 3.4e38f; t.i[k] = 0x7fffffff; }
   if (T <= 0) return;
   const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
+  int b0[27], b1[27];
+#pragma unroll
   for (int c = 0; c < 27; ++c) {
     const uint32_t h = cell_hash(cx + c % 3 - 1, cy + (c / 3) % 3 - 1, cz + c / 9 - 1) & (uint32_t)(T - 1);
-    const int b0 = start[h], b1 = start[h + 1];
-    for (int k = b0; k < b1; ++k) {
+    b0[c] = start[h];
+    b1[c] = start[h + 1];
+  }
+#pragma unroll
+  for (int c = 0; c < 27; ++c) {
+    for (int k = b0[c]; k < b1[c]; ++k) {
       const float4 a = hp[k];
       top5_offer(t, sqdist(a.x, a.y, a.z, q.x, q.y, q.z), __builtin_bit_cast(int, a.w));
     }
   }
 }
 
-struct MpShared {
-  double red[kMpWaves][27];
-  int scratch[16];
-  float trig[6];
-  float T[6];
-  float lm_ws[loamla::kLmWs];
-  int lm_iws[12];
-  float AtA[36], AtB[6], X[6];
-  float jac[kMpThreads][33];   // per-lane 3x3 Jacobi scratch
-  int nrows, stop;
-};
+constexpr int kMpQueryThreads = 256;
 
 }  // namespace
 
-__global__ __launch_bounds__(kMpThreads) void k_mp_solve(MpBuffers b) {
-  const int p = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  __shared__ MpShared sh;
-  float* st = b.state + (size_t)p * kMpStateFloats;
+__global__ void k_mp_lm_begin(MpBuffers b) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= b.P) return;
   int* ist = b.istate + (size_t)p * kMpStateInts;
   const int nfc = b.nfrom[p * 2 + 0], nfs = b.nfrom[p * 2 + 1];
+  ist[kMiStackC] = b.sseg_cnt[p * 2 + 0];
+  ist[kMiStackS] = b.sseg_cnt[p * 2 + 1];
+  ist[kMiFromC] = nfc;
+  ist[kMiFromS] = nfs;
+  ist[kMiLmRan] = (nfc > 10 && nfs > 100) ? 1 : 0;  // :706
+  ist[kMiStop] = 0;
+  ist[kMiIters] = 0;
+  ist[kMiRows] = 0;
+}
+
+// one L-M iteration's correspondences (:714-877): lane per stack point (corner, then surf)
+__global__ __launch_bounds__(kMpQueryThreads) void k_mp_query(MpBuffers b) {
+  const int p = blockIdx.y, tid = threadIdx.x;
+  const int* ist = b.istate + (size_t)p * kMpStateInts;
+  if (!ist[kMiLmRan] || ist[kMiStop]) return;
+  const float* st = b.state + (size_t)p * kMpStateFloats;
+  __shared__ float jac[kMpQueryThreads][33];   // per-lane 3x3 Jacobi scratch
+  const int nfc = b.nfrom[p * 2 + 0];
   const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
+  const int nq = nsc + nss;
   const float4* stack = b.stack + (size_t)p * b.cap_stack;
   const float4* fromC = b.from + (size_t)p * b.map_cap;
   const float4* fromS = fromC + nfc;
@@ -386,168 +406,169 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_solve(MpBuffers b) {
   const float4* hcp = b.hC_pts + (size_t)p * b.map_cap;
   const float4* hsp = b.hS_pts + (size_t)p * b.map_cap;
   const int TC = b.hC_T[p], TS = b.hS_T[p];
-  float4* rows_pt = b.rows_pt + (size_t)p * b.cap_stack;
-  float4* rows_cf = b.rows_cf + (size_t)p * b.cap_stack;
-  const int nq = nsc + nss;
-  if (tid == 0) {
-    for (int k = 0; k < 6; ++k) sh.T[k] = st[kMpTobe + k];
-    ist[kMiStackC] = nsc;
-    ist[kMiStackS] = nss;
-    ist[kMiFromC] = nfc;
-    ist[kMiFromS] = nfs;
-    ist[kMiLmRan] = 0;
-    ist[kMiIters] = 0;
-    ist[kMiRows] = 0;
-  }
-  __syncthreads();
-  if (!(nfc > 10 && nfs > 100)) return;  // :706
-  int iters = 0;
-  long rows_sum = 0;
-  float* jw = sh.jac[tid];
-  for (int iter = 0; iter < b.max_iter; ++iter) {
-    ++iters;
-    const loampose::MapRot r = loampose::map_rot(sh.T);
-    if (tid == 0) sh.nrows = 0;
-    __syncthreads();
-    for (int base = 0; base < nq; base += kMpThreads) {
-      const int q = base + tid;
-      int ok = 0;
-      float4 cf = make_float4(0, 0, 0, 0), po = make_float4(0, 0, 0, 0);
-      if (q < nq) {
-        po = stack[q < nsc ? q : b.capC + (q - nsc)];
-        const float4 sel = loampose::point_to_map(r, po);
-        Top5 t;
-        if (q < nsc) {  // :714-819
-          knn5(hcs, hcp, TC, sel, t);
-          if (t.i[4] != 0x7fffffff && D(t.d[4]) < 1.0) {
-            float cx = 0, cy = 0, cz = 0;
-            for (int k = 0; k < 5; ++k) { const float4 a = fromC[t.i[k]]; cx += a.x; cy += a.y; cz += a.z; }
-            cx /= 5; cy /= 5; cz /= 5;
-            float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
-            for (int k = 0; k < 5; ++k) {
-              const float4 a = fromC[t.i[k]];
-              const float ax = a.x - cx, ay = a.y - cy, az = a.z - cz;
-              a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
-              a22 += ay * ay; a23 += ay * az; a33 += az * az;
-            }
-            a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
-            float* A1 = jw;
-            float* D1 = jw + 9;
-            float* V1 = jw + 12;
-            int* iws = (int*)(jw + 21);
-            A1[0] = a11; A1[1] = a12; A1[2] = a13; A1[3] = a12; A1[4] = a22;
-            A1[5] = a23; A1[6] = a13; A1[7] = a23; A1[8] = a33;
-            loamla::jacobi<3>(A1, D1, V1, iws);
-            if (D1[0] > 3 * D1[1]) {
-              const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
-              const float x1 = (float)(D(cx) + 0.1 * D(V1[0])), y1 = (float)(D(cy) + 0.1 * D(V1[1])),
-                          z1 = (float)(D(cz) + 0.1 * D(V1[2]));
-              const float x2 = (float)(D(cx) - 0.1 * D(V1[0])), y2 = (float)(D(cy) - 0.1 * D(V1[1])),
-                          z2 = (float)(D(cz) - 0.1 * D(V1[2]));
-              const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
-              const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
-              const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
-              const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
-              const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
-              const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
-              const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
-              const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
-              const float ld2 = a012 / l12;
-              const float sw = (float)(1 - 0.9 * fabs(D(ld2)));
-              cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
-              ok = D(sw) > 0.1 ? 1 : 0;
-            }
-          }
-        } else {  // :821-877
-          knn5(hss, hsp, TS, sel, t);
-          if (t.i[4] != 0x7fffffff && D(t.d[4]) < 1.0) {
-            float A0[15], B0[5] = {-1, -1, -1, -1, -1}, X0[3], ws[14];
-            for (int k = 0; k < 5; ++k) {
-              const float4 a = fromS[t.i[k]];
-              A0[k * 3 + 0] = a.x; A0[k * 3 + 1] = a.y; A0[k * 3 + 2] = a.z;
-            }
-            loamla::qr_solve(A0, B0, 5, 3, X0, ws);
-            float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
-            const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
-            pa /= ps; pb /= ps; pc /= ps; pd /= ps;
-            bool planeValid = true;
-            for (int k = 0; k < 5; ++k) {
-              const float4 a = fromS[t.i[k]];
-              if (fabs(D(pa * a.x + pb * a.y + pc * a.z + pd)) > 0.2) { planeValid = false; break; }
-            }
-            if (planeValid) {
-              const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
-              const float sw = (float)(1 - 0.9 * fabs(D(pd2)) /
-                                               sqrt(sqrt(D(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z))));
-              cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
-              ok = D(sw) > 0.1 ? 1 : 0;
-            }
-          }
+  int8_t* qok = b.q_ok + (size_t)p * b.cap_stack;
+  float4* qcf = b.q_cf + (size_t)p * b.cap_stack;
+  const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
+  float* jw = jac[tid];
+  for (int q = blockIdx.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
+    int ok = 0;
+    float4 cf = make_float4(0, 0, 0, 0);
+    const float4 po = stack[q < nsc ? q : b.capC + (q - nsc)];
+    const float4 sel = loampose::point_to_map(r, po);
+    Top5 t;
+    if (q < nsc) {  // :714-819
+      knn5(hcs, hcp, TC, sel, t);
+      if (t.i[4] != 0x7fffffff && D(t.d[4]) < 1.0) {
+        float4 nb[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) nb[k] = fromC[t.i[k]];
+        float cx = 0, cy = 0, cz = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { cx += nb[k].x; cy += nb[k].y; cz += nb[k].z; }
+        cx /= 5; cy /= 5; cz /= 5;
+        float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const float ax = nb[k].x - cx, ay = nb[k].y - cy, az = nb[k].z - cz;
+          a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
+          a22 += ay * ay; a23 += ay * az; a33 += az * az;
+        }
+        a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
+        float* A1 = jw;
+        float* D1 = jw + 9;
+        float* V1 = jw + 12;
+        int* iws = (int*)(jw + 21);
+        A1[0] = a11; A1[1] = a12; A1[2] = a13; A1[3] = a12; A1[4] = a22;
+        A1[5] = a23; A1[6] = a13; A1[7] = a23; A1[8] = a33;
+        loamla::jacobi<3>(A1, D1, V1, iws);
+        if (D1[0] > 3 * D1[1]) {
+          const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
+          const float x1 = (float)(D(cx) + 0.1 * D(V1[0])), y1 = (float)(D(cy) + 0.1 * D(V1[1])),
+                      z1 = (float)(D(cz) + 0.1 * D(V1[2]));
+          const float x2 = (float)(D(cx) - 0.1 * D(V1[0])), y2 = (float)(D(cy) - 0.1 * D(V1[1])),
+                      z2 = (float)(D(cz) - 0.1 * D(V1[2]));
+          const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
+          const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
+          const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
+          const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
+          const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
+          const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
+          const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
+          const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
+          const float ld2 = a012 / l12;
+          const float sw = (float)(1 - 0.9 * fabs(D(ld2)));
+          cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
+          ok = D(sw) > 0.1 ? 1 : 0;
         }
       }
-      int tot;
-      const int ex = block_excl_scan<kMpThreads>(ok, sh.scratch, tot);
-      const int r0 = sh.nrows;
-      if (ok) {
-        rows_pt[r0 + ex] = po;
-        rows_cf[r0 + ex] = cf;
+    } else {  // :821-877
+      knn5(hss, hsp, TS, sel, t);
+      if (t.i[4] != 0x7fffffff && D(t.d[4]) < 1.0) {
+        float4 nb[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) nb[k] = fromS[t.i[k]];
+        float A0[15], B0[5] = {-1, -1, -1, -1, -1}, X0[3], ws[14];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { A0[k * 3 + 0] = nb[k].x; A0[k * 3 + 1] = nb[k].y; A0[k * 3 + 2] = nb[k].z; }
+        loamla::qr_solve(A0, B0, 5, 3, X0, ws);
+        float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
+        const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
+        pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+        bool planeValid = true;
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+          if (fabs(D(pa * nb[k].x + pb * nb[k].y + pc * nb[k].z + pd)) > 0.2) planeValid = false;
+        if (planeValid) {
+          const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
+          const float sw = (float)(1 - 0.9 * fabs(D(pd2)) / sqrt(sqrt(D(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z))));
+          cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
+          ok = D(sw) > 0.1 ? 1 : 0;
+        }
       }
-      __syncthreads();
-      if (tid == 0) sh.nrows = r0 + tot;
-      __syncthreads();
     }
-    const int nrows = sh.nrows;
-    rows_sum += nrows;
-    if (tid == 0) {
-      for (int k = 0; k < 3; ++k) {
-        sh.trig[2 * k] = (float)dsin(sh.T[k]);
-        sh.trig[2 * k + 1] = (float)dcos(sh.T[k]);
-      }
+    qok[q] = (int8_t)ok;
+    qcf[q] = cf;
+  }
+}
+
+namespace {
+struct MpIterShared {
+  double red[kMpWaves][28];
+  float trig[6];
+  float lm_ws[loamla::kLmWs];
+  int lm_iws[12];
+  float AtA[36], AtB[6], X[6];
+};
+}  // namespace
+
+// the normal equations of the accepted rows (:879-974) and the 6x6 step, one workgroup per
+// instance; rows = the accepted correspondences of this iteration, in stack order
+__global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
+  const int p = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  int* ist = b.istate + (size_t)p * kMpStateInts;
+  if (!ist[kMiLmRan] || ist[kMiStop]) return;
+  float* st = b.state + (size_t)p * kMpStateFloats;
+  __shared__ MpIterShared sh;
+  const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
+  const int nq = nsc + nss;
+  const float4* stack = b.stack + (size_t)p * b.cap_stack;
+  const int8_t* qok = b.q_ok + (size_t)p * b.cap_stack;
+  const float4* qcf = b.q_cf + (size_t)p * b.cap_stack;
+  if (tid == 0)
+    for (int k = 0; k < 3; ++k) {
+      sh.trig[2 * k] = (float)dsin(st[kMpTobe + k]);
+      sh.trig[2 * k + 1] = (float)dcos(st[kMpTobe + k]);
     }
-    __syncthreads();
-    if (nrows < 50) continue;  // :886-889
-    const float srx = sh.trig[0], crx = sh.trig[1], sry = sh.trig[2], cry = sh.trig[3], srz = sh.trig[4],
-                crz = sh.trig[5];
-    double acc[27];
+  __syncthreads();
+  const float srx = sh.trig[0], crx = sh.trig[1], sry = sh.trig[2], cry = sh.trig[3], srz = sh.trig[4],
+              crz = sh.trig[5];
+  double acc[28];
 #pragma unroll
-    for (int k = 0; k < 27; ++k) acc[k] = 0.0;
-    for (int rr = tid; rr < nrows; rr += kMpThreads) {  // :897-921
-      const float4 o = rows_pt[rr], c = rows_cf[rr];
-      float a[6];
-      a[0] = (crx * sry * srz * o.x + crx * crz * sry * o.y - srx * sry * o.z) * c.x +
-             (-srx * srz * o.x - crz * srx * o.y - crx * o.z) * c.y +
-             (crx * cry * srz * o.x + crx * cry * crz * o.y - cry * srx * o.z) * c.z;
-      a[1] = ((cry * srx * srz - crz * sry) * o.x + (sry * srz + cry * crz * srx) * o.y + crx * cry * o.z) * c.x +
-             ((-cry * crz - srx * sry * srz) * o.x + (cry * srz - crz * srx * sry) * o.y - crx * sry * o.z) * c.z;
-      a[2] = ((crz * srx * sry - cry * srz) * o.x + (-cry * crz - srx * sry * srz) * o.y) * c.x +
-             (crx * crz * o.x - crx * srz * o.y) * c.y +
-             ((sry * srz + cry * crz * srx) * o.x + (crz * sry - cry * srx * srz) * o.y) * c.z;
-      a[3] = c.x;
-      a[4] = c.y;
-      a[5] = c.z;
-      const float bb = -c.w;
-      int k = 0;
+  for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+  for (int q = tid; q < nq; q += kMpThreads) {  // :897-921
+    if (!qok[q]) continue;
+    const float4 o = stack[q < nsc ? q : b.capC + (q - nsc)], c = qcf[q];
+    float a[6];
+    a[0] = (crx * sry * srz * o.x + crx * crz * sry * o.y - srx * sry * o.z) * c.x +
+           (-srx * srz * o.x - crz * srx * o.y - crx * o.z) * c.y +
+           (crx * cry * srz * o.x + crx * cry * crz * o.y - cry * srx * o.z) * c.z;
+    a[1] = ((cry * srx * srz - crz * sry) * o.x + (sry * srz + cry * crz * srx) * o.y + crx * cry * o.z) * c.x +
+           ((-cry * crz - srx * sry * srz) * o.x + (cry * srz - crz * srx * sry) * o.y - crx * sry * o.z) * c.z;
+    a[2] = ((crz * srx * sry - cry * srz) * o.x + (-cry * crz - srx * sry * srz) * o.y) * c.x +
+           (crx * crz * o.x - crx * srz * o.y) * c.y +
+           ((sry * srz + cry * crz * srx) * o.x + (crz * sry - cry * srx * srz) * o.y) * c.z;
+    a[3] = c.x;
+    a[4] = c.y;
+    a[5] = c.z;
+    const float bb = -c.w;
+    int k = 0;
 #pragma unroll
-      for (int i = 0; i < 6; ++i)
+    for (int i = 0; i < 6; ++i)
 #pragma unroll
-        for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
+      for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
 #pragma unroll
-      for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
+    for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
+    acc[27] += 1.0;
+  }
+#pragma unroll
+  for (int k = 0; k < 28; ++k) {
+    double v = acc[k];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) sh.red[w][k] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double tot[28];
+    for (int k = 0; k < 28; ++k) {
+      double v = sh.red[0][k];
+      for (int ww = 1; ww < kMpWaves; ++ww) v += sh.red[ww][k];
+      tot[k] = v;
     }
-#pragma unroll
-    for (int k = 0; k < 27; ++k) {
-      double v = acc[k];
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      if (lane == 0) sh.red[w][k] = v;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      double tot[27];
-      for (int k = 0; k < 27; ++k) {
-        double v = sh.red[0][k];
-        for (int ww = 1; ww < kMpWaves; ++ww) v += sh.red[ww][k];
-        tot[k] = v;
-      }
+    const int iter = ist[kMiIters];
+    const int nrows = (int)tot[27];
+    ist[kMiIters] = iter + 1;
+    ist[kMiRows] += nrows;
+    if (nrows >= 50) {  // :886-889
       int k = 0;
       for (int i = 0; i < 6; ++i)
         for (int jj = i; jj < 6; ++jj) {
@@ -559,22 +580,24 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_solve(MpBuffers b) {
       int degen = ist[kMiDegen];
       loamla::lm_step(sh.AtA, sh.AtB, iter, 100.0f, &degen, st + kMpMatP, sh.X, sh.lm_ws, sh.lm_iws);
       ist[kMiDegen] = degen;
-      for (int q = 0; q < 6; ++q) sh.T[q] += sh.X[q];  // no NaN guard in mapping (:956-961)
+      for (int q = 0; q < 6; ++q) st[kMpTobe + q] += sh.X[q];  // no NaN guard in mapping (:956-961)
       const float dR = loamla::delta_r(sh.X), dT = loamla::delta_t(sh.X);
-      sh.stop = (D(dR) < 0.05 && D(dT) < 0.05) ? 1 : 0;
+      if (D(dR) < 0.05 && D(dT) < 0.05) ist[kMiStop] = 1;
     }
-    __syncthreads();
-    if (sh.stop) break;
+    if (ist[kMiIters] >= b.max_iter) ist[kMiStop] = 1;
   }
-  if (tid == 0) {
-    for (int k = 0; k < 6; ++k) {
-      st[kMpTobe + k] = sh.T[k];
-      st[kMpBef + k] = st[kMpSum + k];  // transformUpdate (:199-232, no IMU)
-      st[kMpAft + k] = sh.T[k];
-    }
-    ist[kMiLmRan] = 1;
-    ist[kMiIters] = iters;
-    ist[kMiRows] = (int)rows_sum;
+}
+
+// transformUpdate (:199-232, no IMU) for the instances whose L-M ran
+__global__ void k_mp_lm_end(MpBuffers b) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= b.P) return;
+  const int* ist = b.istate + (size_t)p * kMpStateInts;
+  if (!ist[kMiLmRan]) return;
+  float* st = b.state + (size_t)p * kMpStateFloats;
+  for (int k = 0; k < 6; ++k) {
+    st[kMpBef + k] = st[kMpSum + k];
+    st[kMpAft + k] = st[kMpTobe + k];
   }
 }
 
@@ -814,8 +837,8 @@ void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter
   (void)hipMalloc(&b.hC_pts, Pm * sizeof(float4));
   (void)hipMalloc(&b.hS_pts, Pm * sizeof(float4));
   (void)hipMalloc(&b.nfrom, (size_t)P * 2 * sizeof(int));
-  (void)hipMalloc(&b.rows_pt, Ps * sizeof(float4));
-  (void)hipMalloc(&b.rows_cf, Ps * sizeof(float4));
+  (void)hipMalloc(&b.q_ok, Ps * sizeof(int8_t));
+  (void)hipMalloc(&b.q_cf, Ps * sizeof(float4));
   (void)hipMalloc(&b.app_cnt, (size_t)P * kCubeNum * 2 * sizeof(int));
   (void)hipMalloc(&b.app_off, (size_t)P * kCubeNum * 2 * sizeof(int));
   (void)hipMalloc(&b.app, Ps * sizeof(float4));
@@ -847,7 +870,7 @@ void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter
 void mp_free(MpBuffers& b) {
   void* ptrs[] = {b.state, b.istate, b.slots, b.pool, b.valid, b.vpre, b.inC, b.inS, b.inF, b.in_n, b.in_pose,
                   b.stack2, b.stack, b.nstack, b.from, b.hC_start, b.hS_start, b.h_fill, b.hC_T, b.hS_T,
-                  b.hC_pts, b.hS_pts, b.nfrom, b.rows_pt, b.rows_cf, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
+                  b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
                   b.vg_params, b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.cub_tmp, b.reg, b.nreg};
   for (void* q : ptrs)
@@ -896,8 +919,15 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
   hs.count = b.nfrom + 1; hs.start = b.hS_start; hs.out = b.hS_pts; hs.tsize = b.hS_T;
   hipLaunchKernelGGL(k_hash_build, dim3(P), dim3(256), 0, st, hs);
   mark("k_hash_build_map");
-  hipLaunchKernelGGL(k_mp_solve, dim3(P), dim3(kMpThreads), 0, st, b);
-  mark("k_mp_solve");
+  hipLaunchKernelGGL(k_mp_lm_begin, dim3((P + 255) / 256), dim3(256), 0, st, b);
+  const int gq = std::min(64, (b.cap_stack + kMpQueryThreads - 1) / kMpQueryThreads);
+  for (int it = 0; it < b.max_iter; ++it) {
+    hipLaunchKernelGGL(k_mp_query, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
+    mark("k_mp_query");
+    hipLaunchKernelGGL(k_mp_iter, dim3(P), dim3(kMpThreads), 0, st, b);
+    mark("k_mp_iter");
+  }
+  hipLaunchKernelGGL(k_mp_lm_end, dim3((P + 255) / 256), dim3(256), 0, st, b);
   // insertion + per-valid-cube downsampling into the other pool
   hipLaunchKernelGGL(k_mp_insert, dim3(P), dim3(kMpThreads), 0, st, b, (int*)b.vg_k, (int*)b.vg_v);
   mark("k_mp_insert");
@@ -983,6 +1013,7 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
     stats->mp_iters = si[kMiIters];
     stats->mp_rows_sum = (uint64_t)si[kMiRows];
     stats->mp_stack = (uint64_t)(si[kMiStackC] + si[kMiStackS]);
+    stats->mp_stack_iters = (uint64_t)si[kMiIters] * (si[kMiStackC] + si[kMiStackS]);
     stats->mp_map_points = (uint64_t)(si[kMiFromC] + si[kMiFromS]);
     stats->mp_map_valid_points = (uint64_t)si[kMiValidPts];
     stats->ms_mp = ms;
@@ -1027,6 +1058,7 @@ int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats*
       stats->mp_iters += q[kMiIters];
       stats->mp_rows_sum += (uint64_t)q[kMiRows];
       stats->mp_stack += (uint64_t)(q[kMiStackC] + q[kMiStackS]);
+      stats->mp_stack_iters += (uint64_t)q[kMiIters] * (q[kMiStackC] + q[kMiStackS]);
       stats->mp_map_points += (uint64_t)(q[kMiFromC] + q[kMiFromS]);
       stats->mp_map_valid_points += (uint64_t)q[kMiValidPts];
     }

@@ -19,7 +19,7 @@ constexpr int kMaxValid = 125;
 constexpr int kMpSum = 0, kMpIncre = 6, kMpTobe = 12, kMpBef = 18, kMpAft = 24, kMpMatP = 30, kMpOnY = 66,
               kMpStateFloats = 72;
 enum { kMiCenW = 0, kMiCenH, kMiCenD, kMiDegen, kMiNValid, kMiIters, kMiRows, kMiStackC, kMiStackS, kMiFromC,
-       kMiFromS, kMiErr, kMiLmRan, kMiValidPts, kMpStateInts = 16 };
+       kMiFromS, kMiErr, kMiLmRan, kMiValidPts, kMiStop, kMpStateInts = 16 };
 
 // one mapping frame's inputs for every instance (device pointers)
 struct MpInput {
@@ -67,8 +67,9 @@ struct MpBuffers {
   int *hC_start = nullptr, *hS_start = nullptr, *h_fill = nullptr, *hC_T = nullptr, *hS_T = nullptr;
   float4 *hC_pts = nullptr, *hS_pts = nullptr;   // [P][map_cap]
   int* nfrom = nullptr;       // [P][2]
-  // rows
-  float4 *rows_pt = nullptr, *rows_cf = nullptr;  // [P][cap_stack]
+  // per-query L-M outputs of the current iteration
+  int8_t* q_ok = nullptr;     // [P][cap_stack]
+  float4* q_cf = nullptr;     // [P][cap_stack]
   // insertion / per-cube downsampling
   int* app_cnt = nullptr;     // [P][kCubeNum][2] appended points per cube
   int* app_off = nullptr;     // [P][kCubeNum][2]
