@@ -337,7 +337,7 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
   }
   const int cur = x->od_last, nxt = 1 - cur;
   HIP_TRY(hipEventRecord(x->ev[0], x->st));
-  hipLaunchKernelGGL(k_od_solve, dim3(1), dim3(256), 0, x->st, o, fv, cur);
+  od_solve(o, fv, cur, x->st);
   x->od_frame_count++;
   const bool pub = x->od_frame_count >= (int)x->cfg.skip_frame_num + 1;
   hipLaunchKernelGGL(k_od_end, dim3(16, 1), dim3(256), 0, x->st, o, fv, nxt, 2, pub ? 1 : 0);
@@ -458,8 +458,7 @@ int loam_batch_run(loam_ctx* x) {
   x->prof.mark("k_od_end_seed");
   od_build_hashes(o, 0, x->st);
   x->prof.mark("k_hash_build_last");
-  hipLaunchKernelGGL(k_od_solve, dim3(P), dim3(256), 0, x->st, o, fcur, 0);
-  x->prof.mark("k_od_solve");
+  od_solve(o, fcur, 0, x->st, pf);
   hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, 1, 2, 1);
   x->prof.mark("k_od_end");
   HIP_TRY(hipEventRecord(x->ev[2], x->st));

@@ -1,20 +1,21 @@
 // Laser odometry on gfx950: the laserOdometry loop body (/root/reference/src/laserOdometry.cpp:413-931)
-// for a batch of independent problems, one persistent workgroup per problem.
+// for a batch of independent problems.
 //
 //  k_hash_build   voxel-hashed CSR index of a cloud (spatial hash of 1 m cells -> buckets, counting
 //                 sort).  Replaces kdtreeCornerLast / kdtreeSurfLast (:78-79, :436-437, :905-906).
-//  k_od_solve     the whole L-M loop (:465-828) in one workgroup of 256 threads:
-//                   TransformToStart of every query (lane per query),
-//                   every 5th iteration the association (wave per query): exact NN through the hash
-//                   (27 cells; exhaustive fallback when the best match is farther than one cell),
-//                   then the ring-window scans of :486-523 / :598-645 as 64-wide chunks with a
-//                   ballot for the break and a (distance, scan order) min-reduction = the
-//                   reference's sequential first-minimum,
-//                   residuals + weights (lane per query), rows appended in query order (Q12),
-//                   J of every accumulated row at the current transform and JᵀJ / Jᵀb accumulated in
-//                   fp64 with a fixed-order block reduction, the 6x6 QR solve / iteration-0
-//                   degeneracy analysis on one lane, NaN guard, convergence test;
-//                 then the pose accumulation (:830-856).
+//  the L-M loop (:465-828) as one launch sequence per iteration over every problem at once:
+//  k_od_begin     IMU prior, whether L-M runs (:461-465)
+//  k_od_assoc     every 5th iteration, one wave per query: TransformToStart, exact NN through the
+//                 hash (27 cells; exhaustive fallback when the best match is farther than one cell),
+//                 then the ring-window scans of :486-523 / :598-645 as 64-wide chunks with a
+//                 ballot for the break and a (distance, scan order) min-reduction = the
+//                 reference's sequential first-minimum
+//  k_od_rows      lane per query: residual + weight of this iteration stored per (iteration, query)
+//                 (the row order of the reference's append, Q12), J of every row accumulated so far
+//                 at the current transform, JᵀJ / Jᵀb partial sums in fp64
+//  k_od_step      wave per problem: fixed-order sum of the partials, 6x6 QR solve / iteration-0
+//                 degeneracy analysis on one lane, NaN guard, convergence test
+//  k_od_fini      pose accumulation (:830-856)
 //  k_od_end       TransformToEnd of lessSharp / lessFlat / full (:875-891) into the next Last clouds.
 #include "dev_common.hpp"
 #include "od.hpp"
@@ -255,232 +256,254 @@ LOAM_D void wave_assoc_surf(const float4* SL, int S, int fwd_end, uint64_t nn, f
   if (best3 != ~0ull) ind3 = decode(best3);
 }
 
-struct OdShared {
-  float4 sel[kOdMaxQ];
-  int ind[3][kOdMaxQ];
-  double red[kOdWaves][27];
-  int cells[kOdWaves][64];
-  int scratch[16];
-  float trig[6];
-  float transform[6];
-  float lm_ws[loamla::kLmWs];
-  int lm_iws[12];
-  float AtA[36], AtB[6], X[6];
-  int nrows, stop;
-};
-
 }  // namespace
 
-__global__ __launch_bounds__(kOdThreads) void k_od_solve(OdBuffers b, FeatView f, int last_buf) {
-  const int p = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  __shared__ OdShared sh;
+// ---------------------------------------------------------------- the L-M loop, split per iteration
+// Launch sequence per problem batch (od_solve): k_od_begin, then for iter = 0..max_iter-1
+// [k_od_assoc when iter % 5 == 0] k_od_rows k_od_step, then k_od_fini.  A problem that has
+// converged (or never runs L-M) makes every later launch return at once.
+
+__global__ void k_od_begin(OdBuffers b, FeatView f) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= b.P) return;
   float* st = b.state + (size_t)p * kOdStateFloats;
   int* ist = b.istate + (size_t)p * kOdStateInts;
   const loampose::Imu imu = load_imu(st);
-  const int nc = f.count(p, 0), ns = f.count(p, 2);
+  const float scanPeriod = 0.1f;  // :461-463 constant-velocity IMU prior (zero without IMU)
+  st[3] -= imu.veloX * scanPeriod;
+  st[4] -= imu.veloY * scanPeriod;
+  st[5] -= imu.veloZ * scanPeriod;
+  const int nq = f.count(p, 0) + f.count(p, 2);
+  const bool run_lm = ist[kIsCornerLastNum] > 10 && ist[kIsSurfLastNum] > 100;  // :465
+  if (run_lm && nq > b.cap_q) ist[kIsErr] |= ERR_CAP_ROWS;
+  ist[kIsActive] = (run_lm && nq <= b.cap_q) ? 1 : 0;
+  ist[kIsStop] = 0;
+  ist[kIsIters] = 0;
+  ist[kIsAssoc] = 0;
+  ist[kIsRows] = 0;
+}
+
+// association (:472-527, :587-650), one wave per query: TransformToStart at the current
+// transform, exact NN through the hash, then the ring-window scans.
+__global__ __launch_bounds__(kOdThreads) void k_od_assoc(OdBuffers b, FeatView f, int last_buf) {
+  const int p = blockIdx.y, lane = lane_id(), w = threadIdx.x >> 6;
+  const int* ist = b.istate + (size_t)p * kOdStateInts;
+  if (!ist[kIsActive] || ist[kIsStop]) return;
+  __shared__ int cells[kOdWaves][64];
+  const float* st = b.state + (size_t)p * kOdStateFloats;
+  float T[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) T[k] = st[k];
+  const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
   const float4* sharp = f.sharp + (size_t)p * f.sharp_stride;
   const float4* flat = f.flat + (size_t)p * f.flat_stride;
+  const size_t lp = (size_t)last_buf * b.P + p;
   const int C = b.nlast[(p * 2 + last_buf) * 2 + 0], S = b.nlast[(p * 2 + last_buf) * 2 + 1];
-  const float4* CL = b.lastC + ((size_t)last_buf * b.P + p) * b.capC;
-  const float4* SL = b.lastS + ((size_t)last_buf * b.P + p) * b.capS;
-  const int* hcs = b.hC_start + ((size_t)last_buf * b.P + p) * (b.tC + 1);
-  const int* hss = b.hS_start + ((size_t)last_buf * b.P + p) * (b.tS + 1);
-  const float4* hcp = b.hC_pts + ((size_t)last_buf * b.P + p) * b.capC;
-  const float4* hsp = b.hS_pts + ((size_t)last_buf * b.P + p) * b.capS;
-  const int TC = b.hC_T[last_buf * b.P + p], TS = b.hS_T[last_buf * b.P + p];
-  float4* rows_pt = b.rows_pt + (size_t)p * b.cap_rows;
-  float4* rows_cf = b.rows_cf + (size_t)p * b.cap_rows;
-  const int nq = nc + ns;
-  if (tid == 0) {
-    // :461-463 constant-velocity IMU prior (zero without IMU)
-    const float scanPeriod = 0.1f;
-    st[3] -= imu.veloX * scanPeriod;
-    st[4] -= imu.veloY * scanPeriod;
-    st[5] -= imu.veloZ * scanPeriod;
-    for (int k = 0; k < 6; ++k) sh.transform[k] = st[k];
-    sh.nrows = 0;
-    sh.stop = 0;
-  }
-  __syncthreads();
-  int iters = 0, assoc = 0;
-  long rows_sum = 0;
-  const bool run_lm = ist[kIsCornerLastNum] > 10 && ist[kIsSurfLastNum] > 100;
-  if (run_lm && nq > kOdMaxQ) {
-    if (tid == 0) ist[kIsErr] |= ERR_CAP_ROWS;
-  } else if (run_lm) {
-    for (int iter = 0; iter < b.max_iter; ++iter) {
-      ++iters;
-      // TransformToStart of every query point (:472, :587)
-      for (int q = tid; q < nq; q += kOdThreads)
-        sh.sel[q] = loampose::transform_to_start(sh.transform, q < nc ? sharp[q] : flat[q - nc]);
-      __syncthreads();
-      if (iter % 5 == 0) {  // association (Q10)
-        ++assoc;
-        for (int q = w; q < nq; q += kOdWaves) {
-          const float4 s4 = sh.sel[q];
-          int i1, i2, i3 = -1;
-          if (q < nc) {
-            const uint64_t nn = wave_hash_nn(hcs, hcp, TC, CL, C, 1.0f, 1.0f, s4.x, s4.y, s4.z, sh.cells[w]);
-            wave_assoc_corner(CL, C, min(nc, C), nn, s4, i1, i2);
-          } else {
-            const uint64_t nn = wave_hash_nn(hss, hsp, TS, SL, S, 1.0f, 1.0f, s4.x, s4.y, s4.z, sh.cells[w]);
-            wave_assoc_surf(SL, S, min(ns, S), nn, s4, i1, i2, i3);
-          }
-          if (lane == 0) { sh.ind[0][q] = i1; sh.ind[1][q] = i2; sh.ind[2][q] = i3; }
-        }
-        __syncthreads();
-      }
-      // residuals + weights (:530-583, :653-694), rows appended in query order
-      for (int base = 0; base < nq; base += kOdThreads) {
-        const int q = base + tid;
-        int ok = 0;
-        float4 cf = make_float4(0, 0, 0, 0);
-        if (q < nq) {
-          const float4 s4 = sh.sel[q];
-          if (q < nc) {
-            if (sh.ind[1][q] >= 0) {
-              const float4 t1 = CL[sh.ind[0][q]], t2 = CL[sh.ind[1][q]];
-              const float x0 = s4.x, y0 = s4.y, z0 = s4.z;
-              const float x1 = t1.x, y1 = t1.y, z1 = t1.z, x2 = t2.x, y2 = t2.y, z2 = t2.z;
-              const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
-              const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
-              const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
-              const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
-              const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
-              const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
-              const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
-              const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
-              const float ld2 = a012 / l12;
-              float sw = 1;
-              if (iter >= 5) sw = (float)(1 - 1.8 * fabs(D(ld2)));
-              cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
-              ok = (D(sw) > 0.1 && ld2 != 0) ? 1 : 0;
-            }
-          } else if (sh.ind[1][q] >= 0 && sh.ind[2][q] >= 0) {
-            const float4 t1 = SL[sh.ind[0][q]], t2 = SL[sh.ind[1][q]], t3 = SL[sh.ind[2][q]];
-            float pa = (t2.y - t1.y) * (t3.z - t1.z) - (t3.y - t1.y) * (t2.z - t1.z);
-            float pb = (t2.z - t1.z) * (t3.x - t1.x) - (t3.z - t1.z) * (t2.x - t1.x);
-            float pc = (t2.x - t1.x) * (t3.y - t1.y) - (t3.x - t1.x) * (t2.y - t1.y);
-            float pd = -(pa * t1.x + pb * t1.y + pc * t1.z);
-            const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
-            pa /= ps; pb /= ps; pc /= ps; pd /= ps;
-            const float pd2 = pa * s4.x + pb * s4.y + pc * s4.z + pd;
-            float sw = 1;
-            if (iter >= 5)
-              sw = (float)(1 - 1.8 * fabs(D(pd2)) / sqrt(sqrt(D(s4.x * s4.x + s4.y * s4.y + s4.z * s4.z))));
-            cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
-            ok = (D(sw) > 0.1 && pd2 != 0) ? 1 : 0;
-          }
-        }
-        int tot;
-        const int ex = block_excl_scan<kOdThreads>(ok, sh.scratch, tot);
-        const int r0 = sh.nrows;
-        if (ok && r0 + ex < b.cap_rows) {
-          rows_pt[r0 + ex] = q < nc ? sharp[q] : flat[q - nc];
-          rows_cf[r0 + ex] = cf;
-        }
-        __syncthreads();
-        if (tid == 0) sh.nrows = min(r0 + tot, b.cap_rows);
-        __syncthreads();
-      }
-      const int nrows = sh.nrows;
-      rows_sum += nrows;
-      if (nrows < 10) continue;  // :697-700
-      if (tid == 0) {
-        for (int k = 0; k < 3; ++k) {
-          sh.trig[2 * k] = (float)dsin(1 * sh.transform[k]);
-          sh.trig[2 * k + 1] = (float)dcos(1 * sh.transform[k]);
-        }
-      }
-      __syncthreads();
-      // J rows at the current transform (:708-764), JᵀJ / Jᵀb in fp64
-      const float srx = sh.trig[0], crx = sh.trig[1], sry = sh.trig[2], cry = sh.trig[3],
-                  srz = sh.trig[4], crz = sh.trig[5];
-      const float sw = 1;
-      const float tx = sw * sh.transform[3], ty = sw * sh.transform[4], tz = sw * sh.transform[5];
-      double acc[27];
-#pragma unroll
-      for (int k = 0; k < 27; ++k) acc[k] = 0.0;
-      for (int r = tid; r < nrows; r += kOdThreads) {
-        const float4 po = rows_pt[r], c4 = rows_cf[r];
-        float a[6];
-        a[0] = (-sw * crx * sry * srz * po.x + sw * crx * crz * sry * po.y + sw * srx * sry * po.z +
-                sw * tx * crx * sry * srz - sw * ty * crx * crz * sry - sw * tz * srx * sry) * c4.x +
-               (sw * srx * srz * po.x - sw * crz * srx * po.y + sw * crx * po.z + sw * ty * crz * srx -
-                sw * tz * crx - sw * tx * srx * srz) * c4.y +
-               (sw * crx * cry * srz * po.x - sw * crx * cry * crz * po.y - sw * cry * srx * po.z +
-                sw * tz * cry * srx + sw * ty * crx * cry * crz - sw * tx * crx * cry * srz) * c4.z;
-        a[1] = ((-sw * crz * sry - sw * cry * srx * srz) * po.x + (sw * cry * crz * srx - sw * sry * srz) * po.y -
-                sw * crx * cry * po.z + tx * (sw * crz * sry + sw * cry * srx * srz) +
-                ty * (sw * sry * srz - sw * cry * crz * srx) + sw * tz * crx * cry) * c4.x +
-               ((sw * cry * crz - sw * srx * sry * srz) * po.x + (sw * cry * srz + sw * crz * srx * sry) * po.y -
-                sw * crx * sry * po.z + sw * tz * crx * sry - ty * (sw * cry * srz + sw * crz * srx * sry) -
-                tx * (sw * cry * crz - sw * srx * sry * srz)) * c4.z;
-        a[2] = ((-sw * cry * srz - sw * crz * srx * sry) * po.x + (sw * cry * crz - sw * srx * sry * srz) * po.y +
-                tx * (sw * cry * srz + sw * crz * srx * sry) - ty * (sw * cry * crz - sw * srx * sry * srz)) * c4.x +
-               (-sw * crx * crz * po.x - sw * crx * srz * po.y + sw * ty * crx * srz + sw * tx * crx * crz) * c4.y +
-               ((sw * cry * crz * srx - sw * sry * srz) * po.x + (sw * crz * sry + sw * cry * srx * srz) * po.y +
-                tx * (sw * sry * srz - sw * cry * crz * srx) - ty * (sw * crz * sry + sw * cry * srx * srz)) * c4.z;
-        a[3] = -sw * (cry * crz - srx * sry * srz) * c4.x + sw * crx * srz * c4.y -
-               sw * (crz * sry + cry * srx * srz) * c4.z;
-        a[4] = -sw * (cry * srz + crz * srx * sry) * c4.x - sw * crx * crz * c4.y -
-               sw * (sry * srz - cry * crz * srx) * c4.z;
-        a[5] = sw * crx * sry * c4.x - sw * srx * c4.y - sw * crx * cry * c4.z;
-        const float bb = (float)(-0.05 * D(c4.w));
-        int k = 0;
-#pragma unroll
-        for (int i = 0; i < 6; ++i)
-#pragma unroll
-          for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
-      }
-#pragma unroll
-      for (int k = 0; k < 27; ++k) {
-        double v = acc[k];
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if (lane == 0) sh.red[w][k] = v;
-      }
-      __syncthreads();
-      if (tid == 0) {
-        float* AtA = sh.AtA;
-        float* AtB = sh.AtB;
-        float* X = sh.X;
-        double tot[27];
-        for (int k = 0; k < 27; ++k) {
-          double v = sh.red[0][k];
-          for (int ww = 1; ww < kOdWaves; ++ww) v += sh.red[ww][k];
-          tot[k] = v;
-        }
-        int k = 0;
-        for (int i = 0; i < 6; ++i)
-          for (int jj = i; jj < 6; ++jj) {
-            AtA[i * 6 + jj] = (float)tot[k];
-            AtA[jj * 6 + i] = (float)tot[k];
-            ++k;
-          }
-        for (int i = 0; i < 6; ++i) AtB[i] = (float)tot[21 + i];
-        int degen = ist[kIsDegenerate];
-        loamla::lm_step(AtA, AtB, iter, 10.0f, &degen, st + kOdMatP, X, sh.lm_ws, sh.lm_iws);
-        ist[kIsDegenerate] = degen;
-        const bool nan = isnan(X[0]) || isnan(X[1]) || isnan(X[2]) || isnan(X[3]) || isnan(X[4]) || isnan(X[5]);
-        if (!nan)  // Q16
-          for (int q = 0; q < 6; ++q) sh.transform[q] += X[q];
-        const float dR = loamla::delta_r(X), dT = loamla::delta_t(X);
-        sh.stop = (D(dR) < 0.1 && D(dT) < 0.1) ? 1 : 0;
-      }
-      __syncthreads();
-      if (sh.stop) break;
+  const float4* CL = b.lastC + lp * b.capC;
+  const float4* SL = b.lastS + lp * b.capS;
+  int* ind = b.ind + (size_t)p * 3 * b.cap_q;
+  for (int q = blockIdx.x * kOdWaves + w; q < nq; q += gridDim.x * kOdWaves) {
+    const float4 s4 = loampose::transform_to_start(T, q < nc ? sharp[q] : flat[q - nc]);
+    int i1, i2, i3 = -1;
+    if (q < nc) {
+      const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC,
+                                       b.hC_T[last_buf * b.P + p], CL, C, 1.0f, 1.0f, s4.x, s4.y, s4.z, cells[w]);
+      wave_assoc_corner(CL, C, min(nc, C), nn, s4, i1, i2);
+    } else {
+      const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS,
+                                       b.hS_T[last_buf * b.P + p], SL, S, 1.0f, 1.0f, s4.x, s4.y, s4.z, cells[w]);
+      wave_assoc_surf(SL, S, min(ns, S), nn, s4, i1, i2, i3);
+    }
+    if (lane == 0) {
+      ind[q] = i1;
+      ind[b.cap_q + q] = i2;
+      ind[2 * b.cap_q + q] = i3;
     }
   }
-  if (tid == 0) {
-    for (int k = 0; k < 6; ++k) st[k] = sh.transform[k];
-    loampose::accumulate_pose(st, imu, st + kOdSum);  // :830-856
-    ist[kIsIters] = iters;
-    ist[kIsAssoc] = assoc;
-    ist[kIsRows] = (int)rows_sum;
-    ist[kIsQueries] = assoc * nq;
+}
+
+// one iteration's rows (lane per query): this iteration's residual + weight (:530-583,
+// :653-694) stored at [iter][q]; then the Jacobian of every row accumulated so far (Q12: rows
+// of iterations 0..iter, all evaluated at the current transform, :708-764) summed in fp64 into
+// this workgroup's partial JᵀJ / Jᵀb / row count.  A rejected correspondence is stored as a zero
+// coefficient, which adds exact zeros.
+__global__ __launch_bounds__(kOdThreads) void k_od_rows(OdBuffers b, FeatView f, int last_buf, int iter) {
+  const int p = blockIdx.y, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int* ist = b.istate + (size_t)p * kOdStateInts;
+  if (!ist[kIsActive] || ist[kIsStop]) return;
+  __shared__ double red[kOdWaves][28];
+  __shared__ float trig[6];
+  const float* st = b.state + (size_t)p * kOdStateFloats;
+  float T[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) T[k] = st[k];
+  if (tid == 0)
+    for (int k = 0; k < 3; ++k) {
+      trig[2 * k] = (float)dsin(1 * T[k]);
+      trig[2 * k + 1] = (float)dcos(1 * T[k]);
+    }
+  const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
+  const int q = blockIdx.x * kOdThreads + tid;
+  const size_t lp = (size_t)last_buf * b.P + p;
+  float4* qcf = b.q_cf + (size_t)p * b.max_iter * b.cap_q;
+  int8_t* qok = b.q_ok + (size_t)p * b.max_iter * b.cap_q;
+  float4 po = make_float4(0, 0, 0, 0);
+  if (q < nq) {
+    po = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
+    const float4 s4 = loampose::transform_to_start(T, po);
+    const int* ind = b.ind + (size_t)p * 3 * b.cap_q;
+    const int i1 = ind[q], i2 = ind[b.cap_q + q], i3 = ind[2 * b.cap_q + q];
+    int ok = 0;
+    float4 cf = make_float4(0, 0, 0, 0);
+    if (q < nc) {
+      if (i2 >= 0) {
+        const float4* CL = b.lastC + lp * b.capC;
+        const float4 t1 = CL[i1], t2 = CL[i2];
+        const float x0 = s4.x, y0 = s4.y, z0 = s4.z;
+        const float x1 = t1.x, y1 = t1.y, z1 = t1.z, x2 = t2.x, y2 = t2.y, z2 = t2.z;
+        const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
+        const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
+        const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
+        const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
+        const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
+        const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
+        const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
+        const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
+        const float ld2 = a012 / l12;
+        float sw = 1;
+        if (iter >= 5) sw = (float)(1 - 1.8 * fabs(D(ld2)));
+        cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
+        ok = (D(sw) > 0.1 && ld2 != 0) ? 1 : 0;
+      }
+    } else if (i2 >= 0 && i3 >= 0) {
+      const float4* SL = b.lastS + lp * b.capS;
+      const float4 t1 = SL[i1], t2 = SL[i2], t3 = SL[i3];
+      float pa = (t2.y - t1.y) * (t3.z - t1.z) - (t3.y - t1.y) * (t2.z - t1.z);
+      float pb = (t2.z - t1.z) * (t3.x - t1.x) - (t3.z - t1.z) * (t2.x - t1.x);
+      float pc = (t2.x - t1.x) * (t3.y - t1.y) - (t3.x - t1.x) * (t2.y - t1.y);
+      float pd = -(pa * t1.x + pb * t1.y + pc * t1.z);
+      const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
+      pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+      const float pd2 = pa * s4.x + pb * s4.y + pc * s4.z + pd;
+      float sw = 1;
+      if (iter >= 5)
+        sw = (float)(1 - 1.8 * fabs(D(pd2)) / sqrt(sqrt(D(s4.x * s4.x + s4.y * s4.y + s4.z * s4.z))));
+      cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
+      ok = (D(sw) > 0.1 && pd2 != 0) ? 1 : 0;
+    }
+    if (!ok) cf = make_float4(0, 0, 0, 0);
+    qcf[(size_t)iter * b.cap_q + q] = cf;
+    qok[(size_t)iter * b.cap_q + q] = (int8_t)ok;
   }
+  __syncthreads();
+  const float srx = trig[0], crx = trig[1], sry = trig[2], cry = trig[3], srz = trig[4], crz = trig[5];
+  const float sw = 1;
+  const float tx = sw * T[3], ty = sw * T[4], tz = sw * T[5];
+  double acc[28];
+#pragma unroll
+  for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+  if (q < nq) {
+    for (int it = 0; it <= iter; ++it) {
+      if (!qok[(size_t)it * b.cap_q + q]) continue;
+      const float4 c4 = qcf[(size_t)it * b.cap_q + q];
+      float a[6];
+      a[0] = (-sw * crx * sry * srz * po.x + sw * crx * crz * sry * po.y + sw * srx * sry * po.z +
+              sw * tx * crx * sry * srz - sw * ty * crx * crz * sry - sw * tz * srx * sry) * c4.x +
+             (sw * srx * srz * po.x - sw * crz * srx * po.y + sw * crx * po.z + sw * ty * crz * srx -
+              sw * tz * crx - sw * tx * srx * srz) * c4.y +
+             (sw * crx * cry * srz * po.x - sw * crx * cry * crz * po.y - sw * cry * srx * po.z +
+              sw * tz * cry * srx + sw * ty * crx * cry * crz - sw * tx * crx * cry * srz) * c4.z;
+      a[1] = ((-sw * crz * sry - sw * cry * srx * srz) * po.x + (sw * cry * crz * srx - sw * sry * srz) * po.y -
+              sw * crx * cry * po.z + tx * (sw * crz * sry + sw * cry * srx * srz) +
+              ty * (sw * sry * srz - sw * cry * crz * srx) + sw * tz * crx * cry) * c4.x +
+             ((sw * cry * crz - sw * srx * sry * srz) * po.x + (sw * cry * srz + sw * crz * srx * sry) * po.y -
+              sw * crx * sry * po.z + sw * tz * crx * sry - ty * (sw * cry * srz + sw * crz * srx * sry) -
+              tx * (sw * cry * crz - sw * srx * sry * srz)) * c4.z;
+      a[2] = ((-sw * cry * srz - sw * crz * srx * sry) * po.x + (sw * cry * crz - sw * srx * sry * srz) * po.y +
+              tx * (sw * cry * srz + sw * crz * srx * sry) - ty * (sw * cry * crz - sw * srx * sry * srz)) * c4.x +
+             (-sw * crx * crz * po.x - sw * crx * srz * po.y + sw * ty * crx * srz + sw * tx * crx * crz) * c4.y +
+             ((sw * cry * crz * srx - sw * sry * srz) * po.x + (sw * crz * sry + sw * cry * srx * srz) * po.y +
+              tx * (sw * sry * srz - sw * cry * crz * srx) - ty * (sw * crz * sry + sw * cry * srx * srz)) * c4.z;
+      a[3] = -sw * (cry * crz - srx * sry * srz) * c4.x + sw * crx * srz * c4.y -
+             sw * (crz * sry + cry * srx * srz) * c4.z;
+      a[4] = -sw * (cry * srz + crz * srx * sry) * c4.x - sw * crx * crz * c4.y -
+             sw * (sry * srz - cry * crz * srx) * c4.z;
+      a[5] = sw * crx * sry * c4.x - sw * srx * c4.y - sw * crx * cry * c4.z;
+      const float bb = (float)(-0.05 * D(c4.w));
+      int k = 0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
+      acc[27] += 1.0;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 28; ++k) {
+    double v = acc[k];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[w][k] = v;
+  }
+  __syncthreads();
+  if (tid < 28) {
+    double v = red[0][tid];
+    for (int ww = 1; ww < kOdWaves; ++ww) v += red[ww][tid];
+    b.part[((size_t)p * b.gq + blockIdx.x) * 28 + tid] = v;
+  }
+}
+
+// the 6x6 step of one iteration (:697-828), one wave per problem: fixed-order sum of the
+// workgroup partials, QR solve / iteration-0 degeneracy analysis, NaN guard, convergence test
+__global__ __launch_bounds__(64) void k_od_step(OdBuffers b, int iter, int gq) {
+  const int p = blockIdx.x, lane = threadIdx.x;
+  int* ist = b.istate + (size_t)p * kOdStateInts;
+  if (!ist[kIsActive] || ist[kIsStop]) return;
+  __shared__ double tot[28];
+  __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs];
+  __shared__ int lm_iws[12];
+  if (lane < 28) {
+    double v = 0.0;
+    for (int g = 0; g < gq; ++g) v += b.part[((size_t)p * b.gq + g) * 28 + lane];
+    tot[lane] = v;
+  }
+  __syncthreads();
+  if (lane != 0) return;
+  float* st = b.state + (size_t)p * kOdStateFloats;
+  const int nrows = (int)tot[27];
+  ist[kIsIters] = iter + 1;
+  if (iter % 5 == 0) ist[kIsAssoc] += 1;
+  ist[kIsRows] += nrows;
+  if (nrows >= 10) {  // :697-700
+    int k = 0;
+    for (int i = 0; i < 6; ++i)
+      for (int jj = i; jj < 6; ++jj) {
+        AtA[i * 6 + jj] = (float)tot[k];
+        AtA[jj * 6 + i] = (float)tot[k];
+        ++k;
+      }
+    for (int i = 0; i < 6; ++i) AtB[i] = (float)tot[21 + i];
+    int degen = ist[kIsDegenerate];
+    loamla::lm_step(AtA, AtB, iter, 10.0f, &degen, st + kOdMatP, X, lm_ws, lm_iws);
+    ist[kIsDegenerate] = degen;
+    const bool nan = isnan(X[0]) || isnan(X[1]) || isnan(X[2]) || isnan(X[3]) || isnan(X[4]) || isnan(X[5]);
+    if (!nan)  // Q16
+      for (int q = 0; q < 6; ++q) st[q] += X[q];
+    const float dR = loamla::delta_r(X), dT = loamla::delta_t(X);
+    if (D(dR) < 0.1 && D(dT) < 0.1) ist[kIsStop] = 1;
+  }
+}
+
+// pose accumulation (:830-856) for every problem
+__global__ void k_od_fini(OdBuffers b, FeatView f) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= b.P) return;
+  float* st = b.state + (size_t)p * kOdStateFloats;
+  int* ist = b.istate + (size_t)p * kOdStateInts;
+  const loampose::Imu imu = load_imu(st);
+  loampose::accumulate_pose(st, imu, st + kOdSum);
+  ist[kIsQueries] = ist[kIsAssoc] * (f.count(p, 0) + f.count(p, 2));
 }
 
 // TransformToEnd of lessSharp / lessFlat (and full) into Last[dst] / fullEnd[dst] (:875-891).
@@ -526,7 +549,8 @@ void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   b.capC = kLessSharpPerRing * R;
   b.capS = cap_pts;
   b.max_iter = max_iter;
-  b.cap_rows = max_iter * (kSharpPerRing + kFlatPerRing) * R;
+  b.cap_q = (kSharpPerRing + kFlatPerRing) * R;
+  b.gq = (b.cap_q + kOdThreads - 1) / kOdThreads;
   b.tC = next_pow2(b.capC);
   b.tS = next_pow2(b.capS) > 65536 ? 65536 : next_pow2(b.capS);
   (void)hipMalloc(&b.state, (size_t)P * kOdStateFloats * sizeof(float));
@@ -544,8 +568,10 @@ void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   (void)hipMalloc(&b.hS_pts, (size_t)2 * P * b.capS * sizeof(float4));
   (void)hipMalloc(&b.hC_T, (size_t)2 * P * sizeof(int));
   (void)hipMalloc(&b.hS_T, (size_t)2 * P * sizeof(int));
-  (void)hipMalloc(&b.rows_pt, (size_t)P * b.cap_rows * sizeof(float4));
-  (void)hipMalloc(&b.rows_cf, (size_t)P * b.cap_rows * sizeof(float4));
+  (void)hipMalloc(&b.ind, (size_t)P * 3 * b.cap_q * sizeof(int));
+  (void)hipMalloc(&b.q_cf, (size_t)P * max_iter * b.cap_q * sizeof(float4));
+  (void)hipMalloc(&b.q_ok, (size_t)P * max_iter * b.cap_q * sizeof(int8_t));
+  (void)hipMalloc(&b.part, (size_t)P * b.gq * 28 * sizeof(double));
   (void)hipMemset(b.state, 0, (size_t)P * kOdStateFloats * sizeof(float));
   (void)hipMemset(b.istate, 0, (size_t)P * kOdStateInts * sizeof(int));
   (void)hipMemset(b.nlast, 0, (size_t)P * 4 * sizeof(int));
@@ -557,7 +583,7 @@ void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
 void od_free(OdBuffers& b) {
   void* ptrs[] = {b.state, b.istate, b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T,
-                  b.rows_pt, b.rows_cf};
+                  b.ind, b.q_cf, b.q_ok, b.part};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = OdBuffers();
@@ -591,4 +617,23 @@ void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
   hipLaunchKernelGGL(k_hash_build, dim3(b.P), dim3(256), 0, st, js);
 }
 
+}  // namespace loam
+
+namespace loam {
+void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t st, Prof* prof) {
+  const int P = b.P;
+  auto mark = [&](const char* n) { if (prof) prof->mark(n); };
+  hipLaunchKernelGGL(k_od_begin, dim3((P + 255) / 256), dim3(256), 0, st, b, f);
+  for (int it = 0; it < b.max_iter; ++it) {
+    if (it % 5 == 0) {  // Q10
+      hipLaunchKernelGGL(k_od_assoc, dim3(16, P), dim3(kOdThreads), 0, st, b, f, last_buf);
+      mark("k_od_assoc");
+    }
+    hipLaunchKernelGGL(k_od_rows, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+    mark("k_od_rows");
+    hipLaunchKernelGGL(k_od_step, dim3(P), dim3(64), 0, st, b, it, b.gq);
+    mark("k_od_step");
+  }
+  hipLaunchKernelGGL(k_od_fini, dim3((P + 255) / 256), dim3(256), 0, st, b, f);
+}
 }  // namespace loam

@@ -13,8 +13,7 @@ namespace loam {
 constexpr int kOdSum = 6, kOdMatP = 12, kOdImu = 48, kOdStateFloats = 64;
 // per-problem int state
 enum { kIsDegenerate = 0, kIsCornerLastNum, kIsSurfLastNum, kIsIters, kIsAssoc, kIsRows, kIsQueries,
-       kIsErr, kOdStateInts = 16 };
-constexpr int kOdMaxQ = 2304;  // sharp + flat queries per problem (36 per ring x 64 rings)
+       kIsErr, kIsActive, kIsStop, kOdStateInts = 16 };
 
 // read-only view of one feature set per problem (stride = elements between problems)
 struct FeatView {
@@ -44,7 +43,7 @@ struct HashJob {
 };
 
 struct OdBuffers {
-  int P = 0, capC = 0, capS = 0, cap_rows = 0, tC = 0, tS = 0, max_iter = 25;
+  int P = 0, capC = 0, capS = 0, cap_q = 0, gq = 0, tC = 0, tS = 0, max_iter = 25;
   float* state = nullptr;   // [P][kOdStateFloats]
   int* istate = nullptr;    // [P][kOdStateInts]
   float4* lastC = nullptr;  // [2][P][capC]
@@ -60,17 +59,21 @@ struct OdBuffers {
   float4* hS_pts = nullptr; // [2][P][capS]
   int* hC_T = nullptr;      // [2][P]
   int* hS_T = nullptr;      // [2][P]
-  float4* rows_pt = nullptr;  // [P][cap_rows]
-  float4* rows_cf = nullptr;
+  int* ind = nullptr;         // [P][3][cap_q] association of every query (refreshed every 5th iteration)
+  float4* q_cf = nullptr;     // [P][max_iter][cap_q] coefficients (zero when rejected)
+  int8_t* q_ok = nullptr;     // [P][max_iter][cap_q] accepted flags
+  double* part = nullptr;     // [P][gq][28] per-workgroup JᵀJ | Jᵀb | rows
 };
 
 __global__ void k_hash_build(HashJob j);
-__global__ void k_od_solve(OdBuffers b, FeatView f, int last_buf);
+
 __global__ void k_od_end(OdBuffers b, FeatView f, int dst, int mode, int do_full);
 
 void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter);
 void od_free(OdBuffers& b);
 void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st);
+// the laserOdometry L-M loop + pose accumulation for every problem against Last[last_buf]
+void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t st, Prof* prof = nullptr);
 
 }  // namespace loam
 
