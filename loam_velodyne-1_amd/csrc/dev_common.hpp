@@ -109,6 +109,8 @@ LOAM_D T block_reduce(T v, T* scratch, Op op) {
 // sorts n64 = power of two 64-bit keys in LDS with the whole block; pad with ~0ull.
 template <int NT>
 LOAM_D void block_bitonic_sort(uint64_t* k, int n64) {
+  // a stage with stride <= 64 touches, per wave, only the 128-element blocks its pairs span: two
+  // consecutive such stages are separated by a wave-level fence instead of a workgroup barrier
   for (int size = 2; size <= n64; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int t = threadIdx.x; t < (n64 >> 1); t += NT) {
@@ -118,7 +120,13 @@ LOAM_D void block_bitonic_sort(uint64_t* k, int n64) {
         uint64_t a = k[lo], b = k[hi];
         if ((a > b) == up) { k[lo] = b; k[hi] = a; }
       }
-      __syncthreads();
+      const int next = stride > 1 ? stride >> 1 : (size << 1 <= n64 ? size : 0);
+      if (stride > 64 || next > 64 || next == 0) {
+        __syncthreads();
+      } else {
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+      }
     }
   }
 }

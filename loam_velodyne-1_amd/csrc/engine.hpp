@@ -23,7 +23,6 @@ enum : int {
 constexpr int kSrThreads = 512;     // ring-sort workgroup (one per sweep)
 constexpr int kSelThreads = 256;    // per-ring selection workgroup
 constexpr int kRingCap = 4096;      // max ring span (points) handled in LDS by one workgroup
-constexpr int kSegCap = 2048;       // max segment length (LDS bitonic sort)
 constexpr int kSharpPerRing = 12, kLessSharpPerRing = 120, kFlatPerRing = 24;
 
 // Scan-registration buffers for S sweeps of capacity `cap` points each (index s*cap + i).

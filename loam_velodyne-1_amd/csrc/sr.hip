@@ -8,10 +8,12 @@
 //  k_sr_features    256-point tiles with a 6-point halo in LDS: 11-tap curvature, ring bounds
 //                   (last-write-wins transitions = atomicMax), occlusion / parallel-beam marks as a
 //                   gather over the 12 neighbouring events.  :358-452
-//  k_sr_select      one workgroup per (sweep, ring): the six segment sorts (LDS bitonic on
-//                   (curvature, position) = the reference's stable insertion sort), the greedy
-//                   sharp / flat picks by one wave with ballots, lessFlat candidates, PCL VoxelGrid
-//                   0.2 of the ring (LDS sort by (voxel, position), ordered per-voxel sums).  :460-581
+//  k_sr_select      one workgroup per (sweep, ring): the six segment sorts as one LDS bitonic sort
+//                   of the ring by (segment, curvature, position) = the reference's stable
+//                   insertion sorts, the greedy sharp / flat picks and lessFlat candidates by one
+//                   wave with ballots on LDS state (the neighbour-walk distance tests are
+//                   precomputed gap bits), PCL VoxelGrid 0.2 of the ring (LDS sort by (voxel,
+//                   position), ordered per-voxel sums).  :460-581
 //                   Rings are independent whenever their spans are >5 points apart (always for
 //                   sweeps with no empty ring); otherwise one workgroup walks the rings in order.
 //  k_sr_compact     per sweep: ring-major concatenation of the picks and the downsampled lessFlat.
@@ -256,45 +258,52 @@ __global__ __launch_bounds__(kFeatTile) void k_sr_features(SrBuffers b, SrParams
     float dis = c.x * c.x + c.y * c.y + c.z * c.z;
     if (D(diff) > 0.0002 * D(dis) && D(diff2) > 0.0002 * D(dis)) pk = 1;
   }
+  // bit 1: the neighbour walk of :495-520 stops between i-1 and i
+  int gap = 0;
+  if (i >= 1) {
+    const float4 a = sp[li], c = sp[li - 1];
+    const float ex = a.x - c.x, ey = a.y - c.y, ez = a.z - c.z;
+    gap = D(ex * ex + ey * ey + ez * ez) > 0.05 ? 1 : 0;
+  }
   b.curv[gi] = cv;
-  b.picked[gi] = (uint8_t)pk;
+  b.picked[gi] = (uint8_t)(pk | (gap << 1));
   b.sortind[gi] = i;
   b.label[gi] = 0;
 }
 
 // ---------------------------------------------------------------- per-ring selection
 struct SelShared {
-  uint64_t keys[kRingCap];
-  int sidx[kRingCap];
-  int tmp[kSegCap];     // segment permutation scratch
-  int cand[kRingCap];   // lessFlat candidate positions of the ring
-  uint8_t pk[kRingCap + 16];
+  uint64_t keys[kRingCap];  // (segment, curvature, position) of the ring; then (voxel, candidate)
+  int sidx[kRingCap];       // sortInd of the ring on entry
+  uint16_t cand[kRingCap];  // lessFlat candidate positions (relative to the ring start)
+  uint8_t pk[kRingCap + 16];  // bit 0 cloudNeighborPicked, bit 1 neighbour-walk stop (gap)
   int8_t lab[kRingCap + 16];
   int se[128];
   int picks[kSharpPerRing + kLessSharpPerRing + kFlatPerRing];
   int scratch[16];
   float red[6][kSelThreads / 64];
-  int nsharp, nlsharp, nflat, ncand, wf, wlo, whi, lo, hi;
+  int order[64];
+  int nsharp, nlsharp, nflat, ncand, wf;
 };
 
-LOAM_D void mark_neighbours(const float4* pts, int n, int ind, uint8_t* pk, int wlo) {
-  for (int l = 1; l <= 5; ++l) {  // :495-507
-    if (ind + l >= n) break;
-    const float4 a = pts[ind + l], c = pts[ind + l - 1];
-    float ex = a.x - c.x, ey = a.y - c.y, ez = a.z - c.z;
-    if (D(ex * ex + ey * ey + ez * ez) > 0.05) break;
-    pk[ind + l - wlo] = 1;
+// :495-520 with the distance tests precomputed as gap bits
+LOAM_D void mark_neighbours(int n, int ind, uint8_t* pk, int wlo) {
+  for (int l = 1; l <= 5; ++l) {
+    if (ind + l >= n || (pk[ind + l - wlo] & 2)) break;
+    pk[ind + l - wlo] |= 1;
   }
-  for (int l = -1; l >= -5; --l) {  // :508-520
-    if (ind + l < 0) break;
-    const float4 a = pts[ind + l], c = pts[ind + l + 1];
-    float ex = a.x - c.x, ey = a.y - c.y, ez = a.z - c.z;
-    if (D(ex * ex + ey * ey + ez * ez) > 0.05) break;
-    pk[ind + l - wlo] = 1;
+  for (int l = -1; l >= -5; --l) {
+    if (ind + l < 0 || (pk[ind + l + 1 - wlo] & 2)) break;
+    pk[ind + l - wlo] |= 1;
   }
 }
 
-// processes ring q of sweep s; `seq` = fallback mode (rings walked in order by one workgroup)
+LOAM_D float key_curv(uint64_t key) { return __builtin_bit_cast(float, (uint32_t)(key >> 16)); }
+
+// processes ring q of sweep s; `seq` = fallback mode (rings walked in order by one workgroup).
+// The six segment sorts (:466-474) are one LDS sort of the ring by (segment, curvature,
+// position): the segments partition the ring span and the sort does not depend on the picks.
+// The greedy picks and the lessFlat candidates of each segment are then one wave's work in LDS.
 LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq, SelShared& sh) {
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const float4* pts = b.full + (size_t)s * b.cap;
@@ -312,6 +321,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
     if (tid < 4) st_cnt[tid] = 0;
     return;
   }
+  const int len = hi - lo + 1;
   // window of point indices this ring may touch: span and the indices its sortInd holds, +-5
   int vmin = lo, vmax = hi;
   if (seq) {
@@ -340,41 +350,41 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
     sh.pk[k - wlo] = b.picked[(size_t)s * b.cap + k];
     sh.lab[k - wlo] = b.label[(size_t)s * b.cap + k];
   }
-  for (int k = lo + tid; k <= hi; k += kSelThreads) sh.sidx[k - lo] = b.sortind[(size_t)s * b.cap + k];
-  __syncthreads();
-
-  for (int j = 0; j < 6; ++j) {
-    const int sp = (sq * (6 - j) + eq * j) / 6;
-    const int ep = (sq * (5 - j) + eq * (j + 1)) / 6 - 1;
-    if (sp < 0 || ep >= n) continue;
-    const int len = ep - sp + 1;
-    if (len <= 0) continue;
-    if (len > kSegCap) {
-      if (tid == 0) b.err[s] |= ERR_CAP_RING;
-      continue;
+  int segb[7];
+#pragma unroll
+  for (int j = 0; j <= 6; ++j) segb[j] = (sq * (6 - j) + eq * j) / 6;  // sp_j; ep_j = sp_{j+1} - 1
+  const int P2 = next_pow2(len);
+  for (int t = tid; t < P2; t += kSelThreads) {
+    uint64_t key = ~0ull;
+    if (t < len) {
+      const int v = b.sortind[(size_t)s * b.cap + lo + t];
+      sh.sidx[t] = v;
+      int seg = 0;
+#pragma unroll
+      for (int j = 1; j < 6; ++j) seg += (lo + t >= segb[j]) ? 1 : 0;
+      key = ((uint64_t)seg << 48) | ((uint64_t)fkey(curv[v]) << 16) | (uint32_t)t;
     }
-    // (:466-474) stable ascending sort of sortInd[sp..ep] by curvature
-    const int P2 = next_pow2(len);
-    for (int t = tid; t < P2; t += kSelThreads)
-      sh.keys[t] = t < len ? (((uint64_t)fkey(curv[sh.sidx[sp - lo + t]]) << 32) | (uint32_t)t) : ~0ull;
-    __syncthreads();
-    block_bitonic_sort<kSelThreads>(sh.keys, P2);
-    for (int t = tid; t < len; t += kSelThreads) sh.tmp[t] = sh.sidx[sp - lo + (int)(sh.keys[t] & 0xffffffffu)];
-    __syncthreads();
-    for (int t = tid; t < len; t += kSelThreads) sh.sidx[sp - lo + t] = sh.tmp[t];
-    __syncthreads();
-    if (w == 0) {
+    sh.keys[t] = key;
+  }
+  __syncthreads();
+  block_bitonic_sort<kSelThreads>(sh.keys, P2);
+  if (w == 0) {
+    int run = 0;
+    for (int j = 0; j < 6; ++j) {
+      const int sp = segb[j] - lo, ep = segb[j + 1] - 1 - lo;  // sorted-local range of segment j
+      if (ep < sp) continue;
       // (:476-522) sharp / less sharp, walking from the largest curvature down
       int largest = 0;
       bool done = false;
       for (int base = ep; base >= sp && !done; base -= 64) {
         const int k = base - lane;
         const bool inr = k >= sp;
-        const int ind = inr ? sh.sidx[k - lo] : 0;
-        const bool elig = inr && D(curv[ind]) > 0.1;
+        const uint64_t key = inr ? sh.keys[k] : 0ull;
+        const int ind = inr ? sh.sidx[key & 0xffffu] : 0;
+        const bool elig = inr && D(key_curv(key)) > 0.1;
         uint64_t remaining = __ballot(elig);
         while (remaining) {
-          const bool cand = elig && ((remaining >> lane) & 1ull) && sh.pk[ind - wlo] == 0;
+          const bool cand = elig && ((remaining >> lane) & 1ull) && (sh.pk[ind - wlo] & 1) == 0;
           const uint64_t m = __ballot(cand);
           if (!m) break;
           const int f = __ffsll((unsigned long long)m) - 1;
@@ -389,8 +399,8 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
               sh.lab[ind - wlo] = 1;
               sh.picks[kSharpPerRing + sh.nlsharp++] = ind;
             }
-            sh.pk[ind - wlo] = 1;
-            mark_neighbours(pts, n, ind, sh.pk, wlo);
+            sh.pk[ind - wlo] |= 1;
+            mark_neighbours(n, ind, sh.pk, wlo);
           }
           __threadfence_block();
           __builtin_amdgcn_wave_barrier();
@@ -403,11 +413,12 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
       for (int base = sp; base <= ep && !done; base += 64) {
         const int k = base + lane;
         const bool inr = k <= ep;
-        const int ind = inr ? sh.sidx[k - lo] : 0;
-        const bool elig = inr && D(curv[ind]) < 0.1;
+        const uint64_t key = inr ? sh.keys[k] : 0ull;
+        const int ind = inr ? sh.sidx[key & 0xffffu] : 0;
+        const bool elig = inr && D(key_curv(key)) < 0.1;
         uint64_t remaining = __ballot(elig);
         while (remaining) {
-          const bool cand = elig && ((remaining >> lane) & 1ull) && sh.pk[ind - wlo] == 0;
+          const bool cand = elig && ((remaining >> lane) & 1ull) && (sh.pk[ind - wlo] & 1) == 0;
           const uint64_t m = __ballot(cand);
           if (!m) break;
           const int f = __ffsll((unsigned long long)m) - 1;
@@ -418,28 +429,31 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
           smallest++;
           if (smallest >= 4) { done = true; break; }
           if (lane == f) {
-            sh.pk[ind - wlo] = 1;
-            mark_neighbours(pts, n, ind, sh.pk, wlo);
+            sh.pk[ind - wlo] |= 1;
+            mark_neighbours(n, ind, sh.pk, wlo);
           }
           __threadfence_block();
           __builtin_amdgcn_wave_barrier();
           remaining &= ~((2ull << f) - 1ull);
         }
       }
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+      // (:568-572) lessFlat candidates of this segment, in position order
+      for (int base = segb[j]; base < segb[j + 1]; base += 64) {
+        const int k = base + lane;
+        const bool flag = k < segb[j + 1] && sh.lab[k - wlo] <= 0;
+        const uint64_t m = __ballot(flag);
+        if (flag) sh.cand[run + __popcll(m & lanemask_lt())] = (uint16_t)(k - lo);
+        run += __popcll(m);
+      }
     }
-    __syncthreads();
-    // (:568-572) lessFlat candidates of this segment, in position order
-    int run = sh.ncand;
-    for (int base = sp; base <= ep; base += kSelThreads) {
-      const int k = base + tid;
-      const int flag = (k <= ep && sh.lab[k - wlo] <= 0) ? 1 : 0;
-      int tot;
-      const int ex = block_excl_scan<kSelThreads>(flag, sh.scratch, tot);
-      if (flag) sh.cand[run + ex] = k;
-      run += tot;
-    }
-    __syncthreads();
-    if (tid == 0) sh.ncand = run;
+    if (lane == 0) sh.ncand = run;
+  }
+  __syncthreads();
+  if (seq) {  // the ring's sortInd after its six sorts, for the next ring (one workgroup, ordered)
+    for (int t = tid; t < len; t += kSelThreads)
+      b.sortind[(size_t)s * b.cap + lo + t] = sh.sidx[sh.keys[t] & 0xffffu];
     __syncthreads();
   }
   // ---- PCL VoxelGrid 0.2 of the ring's lessFlat candidates (:575-579)
@@ -447,7 +461,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
   float4* outp = b.st_lflat + (size_t)(s * R + q) * kRingCap;
   float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
   for (int t = tid; t < nc; t += kSelThreads) {
-    const float4 a = pts[sh.cand[t]];
+    const float4 a = pts[lo + sh.cand[t]];
     mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
     mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
   }
@@ -470,7 +484,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
     const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
     const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
     if (dx * dy * dz > (int64_t)0x7fffffff) {  // "leaf size too small": output = input
-      for (int t = tid; t < nc; t += kSelThreads) outp[t] = pts[sh.cand[t]];
+      for (int t = tid; t < nc; t += kSelThreads) outp[t] = pts[lo + sh.cand[t]];
       nout = nc;
     } else {
       int minb[3], maxb[3];
@@ -480,11 +494,11 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
       }
       const int divx = maxb[0] - minb[0] + 1, divy = maxb[1] - minb[1] + 1;
       const int mul1 = divx, mul2 = divx * divy;
-      const int P2 = next_pow2(nc);
-      for (int t = tid; t < P2; t += kSelThreads) {
+      const int P2c = next_pow2(nc);
+      for (int t = tid; t < P2c; t += kSelThreads) {
         uint64_t key = ~0ull;
         if (t < nc) {
-          const float4 a = pts[sh.cand[t]];
+          const float4 a = pts[lo + sh.cand[t]];
           int i0 = (int)(floorf(a.x * inv) - (float)minb[0]);
           int i1 = (int)(floorf(a.y * inv) - (float)minb[1]);
           int i2 = (int)(floorf(a.z * inv) - (float)minb[2]);
@@ -494,7 +508,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
         sh.keys[t] = key;
       }
       __syncthreads();
-      block_bitonic_sort<kSelThreads>(sh.keys, P2);
+      block_bitonic_sort<kSelThreads>(sh.keys, P2c);
       int run = 0;
       for (int base = 0; base < nc; base += kSelThreads) {
         const int t = base + tid;
@@ -506,7 +520,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
           float sx = 0, sy = 0, sz = 0, si = 0;
           int e = t;
           while (e < nc && (uint32_t)(sh.keys[e] >> 32) == vk) {
-            const float4 a = pts[sh.cand[(int)(sh.keys[e] & 0xffffffffu)]];
+            const float4 a = pts[lo + sh.cand[(int)(sh.keys[e] & 0xffffffffu)]];
             sx += a.x; sy += a.y; sz += a.z; si += a.w;
             ++e;
           }
@@ -531,7 +545,6 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
       b.picked[(size_t)s * b.cap + k] = sh.pk[k - wlo];
       b.label[(size_t)s * b.cap + k] = sh.lab[k - wlo];
     }
-    for (int k = lo + tid; k <= hi; k += kSelThreads) b.sortind[(size_t)s * b.cap + k] = sh.sidx[k - lo];
     __threadfence();
   }
   __syncthreads();
@@ -552,7 +565,8 @@ __global__ __launch_bounds__(kSelThreads) void k_sr_select(SrBuffers b, SrParams
   if (tid == 0) {
     // rings are independent when their active spans [start, end-1] are more than 5 points apart
     int wf = 1, prev_hi = -100000;
-    int order[64], na = 0;
+    int* order = sh.order;
+    int na = 0;
     for (int r = 0; r < R; ++r)
       if (sh.se[r] <= sh.se[R + r] - 1) order[na++] = r;
     for (int a = 1; a < na; ++a) {
