@@ -346,23 +346,32 @@ LOAM_D void top5_offer(Top5& t, float d, int idx) {
   }
 }
 
-// exact 5-NN within the 27 cells around q (1 m cells); every bucket range is fetched up front so
-// the 27 loads are in flight together
+// exact 5-NN within the 27 cells around q (1 m cells), as far as it matters: visited centre,
+// faces, edges, corners; a cell is skipped when its box distance exceeds the current 5th
+// distance or reaches the 1 m acceptance radius (the caller rejects a 5th neighbour at >= 1 m).
+// Box distances are lower bounds of the float squared distances (monotone rounding of the same
+// expression), so every neighbour that can be accepted is found exactly.
 LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t) {
 #pragma unroll
   for (int k = 0; k < 5; ++k) { t.d[k] = 3.4e38f; t.i[k] = 0x7fffffff; }
   if (T <= 0) return;
   const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
-  int b0[27], b1[27];
+  const float gxl = q.x - (float)cx, gyl = q.y - (float)cy, gzl = q.z - (float)cz;
+  const float gxh = (float)(cx + 1) - q.x, gyh = (float)(cy + 1) - q.y, gzh = (float)(cz + 1) - q.z;
+  constexpr int kOrder[27] = {13, 4, 10, 12, 14, 16, 22, 1, 3, 5, 7, 9, 11, 15, 17, 19, 21, 23, 25,
+                              0, 2, 6, 8, 18, 20, 24, 26};
 #pragma unroll
-  for (int c = 0; c < 27; ++c) {
-    const uint32_t h = cell_hash(cx + c % 3 - 1, cy + (c / 3) % 3 - 1, cz + c / 9 - 1) & (uint32_t)(T - 1);
-    b0[c] = start[h];
-    b1[c] = start[h + 1];
-  }
-#pragma unroll
-  for (int c = 0; c < 27; ++c) {
-    for (int k = b0[c]; k < b1[c]; ++k) {
+  for (int o = 0; o < 27; ++o) {
+    const int c = kOrder[o];
+    const int dx = c % 3 - 1, dy = (c / 3) % 3 - 1, dz = c / 9 - 1;
+    const float gx = dx < 0 ? gxl : (dx > 0 ? gxh : 0.0f);
+    const float gy = dy < 0 ? gyl : (dy > 0 ? gyh : 0.0f);
+    const float gz = dz < 0 ? gzl : (dz > 0 ? gzh : 0.0f);
+    const float bd = sqdist(gx, gy, gz, 0.0f, 0.0f, 0.0f);
+    if (bd >= 1.0f || bd > t.d[4]) continue;
+    const uint32_t h = cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1);
+    const int b1 = start[h + 1];
+    for (int k = start[h]; k < b1; ++k) {
       const float4 a = hp[k];
       top5_offer(t, sqdist(a.x, a.y, a.z, q.x, q.y, q.z), __builtin_bit_cast(int, a.w));
     }
@@ -913,6 +922,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
   hc.count = b.nfrom; hc.count_stride_bytes = 2 * sizeof(int);
   hc.start = b.hC_start; hc.fill = b.h_fill; hc.out = b.hC_pts; hc.tsize = b.hC_T; hc.tmax = b.tmax;
   hc.inv_h = 1.0f;
+  hc.chunks = nullptr;
   hipLaunchKernelGGL(k_hash_build, dim3(P), dim3(256), 0, st, hc);
   HashJob hs = hc;
   hs.pts_off = b.nfrom; hs.pts_off_stride = 2;

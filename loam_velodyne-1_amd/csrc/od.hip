@@ -94,23 +94,54 @@ __global__ __launch_bounds__(256) void k_hash_build(HashJob j) {
     int pos = atomicAdd(&fill[h], 1);
     out[pos] = make_float4(a.x, a.y, a.z, __int_as_float(i));
   }
+  if (j.chunks) {  // one wave per 64-point chunk of the source order
+    const int lane = lane_id(), w = tid >> 6;
+    const int nch = (n + kChunk - 1) / kChunk;
+    float4* ch = j.chunks + (size_t)p * 2 * chunks_of((int)j.pts_stride);
+    for (int c = w; c < nch; c += 4) {
+      const int i = c * kChunk + lane;
+      float4 a = pts[min(i, n - 1)];
+      const float r = (float)(int)a.w;
+      const float4 lo = make_float4(wave_min_f(a.x), wave_min_f(a.y), wave_min_f(a.z), wave_min_f(r));
+      const float4 hi = make_float4(wave_max_f(a.x), wave_max_f(a.y), wave_max_f(a.z), wave_max_f(r));
+      if (lane == 0) {
+        ch[2 * c] = lo;
+        ch[2 * c + 1] = hi;
+      }
+    }
+  }
 }
 
 namespace {
 
-// exact nearest neighbour of q among the hashed cloud (wave-cooperative); returns the packed
-// (float distance bits << 32 | index) minimum, ~0 if the cloud is empty.  `cells` = per-wave LDS
-// scratch of 64 ints.
-LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const float4* cloud, int n,
-                             float h, float inv_h, float qx, float qy, float qz, int* cells) {
+// lower bound of the float squared distance from s to any point of the box [lo, hi] (monotone
+// rounding of the same expression as sqdist)
+LOAM_D float box_d2(const float4& lo, const float4& hi, const float4& s) {
+  const float gx = fmaxf(fmaxf(lo.x - s.x, s.x - hi.x), 0.0f);
+  const float gy = fmaxf(fmaxf(lo.y - s.y, s.y - hi.y), 0.0f);
+  const float gz = fmaxf(fmaxf(lo.z - s.z, s.z - hi.z), 0.0f);
+  return sqdist(gx, gy, gz, 0.0f, 0.0f, 0.0f);
+}
+
+// exact nearest neighbour of q among the hashed cloud (wave-cooperative), as far as it matters:
+// returns the packed (float distance bits << 32 | index) minimum, or ~0 when no point lies
+// closer than 5 m (the callers reject a nearest neighbour at >= 25 m², :481, :594).  First the
+// 27 cells around q (cells whose box lies >= h away skipped); if the best is >= h, the chunk
+// boxes of the whole cloud closer than 5 m.  `cells` = per-wave LDS scratch of 64 ints.
+LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const float4* cloud, const float4* ch,
+                             int n, float h, float inv_h, float4 q, int* cells) {
   const int lane = lane_id();
-  const int cx = cell_of(qx, inv_h), cy = cell_of(qy, inv_h), cz = cell_of(qz, inv_h);
+  const int cx = cell_of(q.x, inv_h), cy = cell_of(q.y, inv_h), cz = cell_of(q.z, inv_h);
   int bucket = -1, b0 = 0, cnt = 0;
-  if (lane < 27) {
+  if (lane < 27 && T > 0) {
     const int dx = lane % 3 - 1, dy = (lane / 3) % 3 - 1, dz = lane / 9 - 1;
-    bucket = (int)(cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1));
-    b0 = start[bucket];
-    cnt = start[bucket + 1] - b0;
+    const float4 lo = make_float4((float)(cx + dx) * h, (float)(cy + dy) * h, (float)(cz + dz) * h, 0.0f);
+    const float4 hi = make_float4((float)(cx + dx + 1) * h, (float)(cy + dy + 1) * h, (float)(cz + dz + 1) * h, 0.0f);
+    if (h != 1.0f || box_d2(lo, hi, q) < 1.0f) {
+      bucket = (int)(cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1));
+      b0 = start[bucket];
+      cnt = start[bucket + 1] - b0;
+    }
   }
   // two of the 27 cells may share a bucket: count it once
   for (int o = 0; o < 27; ++o) {
@@ -126,31 +157,110 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
     int k = 0;
     while (k < 26 && cells[k + 1] <= t) ++k;
     const float4 a = hp[cells[32 + k] + (t - cells[k])];
-    const float d = sqdist(a.x, a.y, a.z, qx, qy, qz);
+    const float d = sqdist(a.x, a.y, a.z, q.x, q.y, q.z);
     const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)__float_as_int(a.w);
     best = key < best ? key : best;
   }
   best = wave_min_u64(best);
   __builtin_amdgcn_wave_barrier();
-  // exact only if the best lies within one cell of q; otherwise scan the whole cloud
-  if (best == ~0ull || __uint_as_float((uint32_t)(best >> 32)) >= h * h) {
-    best = ~0ull;
-    for (int t = lane; t < n; t += 64) {
-      const float4 a = cloud[t];
-      const float d = sqdist(a.x, a.y, a.z, qx, qy, qz);
-      const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)t;
-      best = key < best ? key : best;
+  if (best != ~0ull && __uint_as_float((uint32_t)(best >> 32)) < h * h) return best;
+  // farther than one cell: the chunks of the whole cloud that may hold a point closer than 5 m
+  best = ~0ull;
+  const int nch = (n + kChunk - 1) / kChunk;
+  for (int k0 = 0; k0 < nch; k0 += 64) {
+    const int k = k0 + lane;
+    const bool need = k < nch && box_d2(ch[2 * k], ch[2 * k + 1], q) < 25.0f;
+    uint64_t nb = __ballot(need);
+    while (nb) {
+      const int c = k0 + __ffsll((unsigned long long)nb) - 1;
+      nb &= nb - 1;
+      const int t = c * kChunk + lane;
+      if (t < n) {
+        const float4 a = cloud[t];
+        const float d = sqdist(a.x, a.y, a.z, q.x, q.y, q.z);
+        const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)t;
+        best = key < best ? key : best;
+      }
     }
-    best = wave_min_u64(best);
   }
-  return best;
+  return wave_min_u64(best);
+}
+
+// One direction of a ring-window scan (:486-523 / :598-645) over the cloud L from c (exclusive):
+// dir = +1 walks c+1 .. end-1, dir = -1 walks c-1 .. 0, stopping at the first point whose ring
+// lies beyond scan +- 2.5.  `f(j, a, d)` is called by the lane holding point j (before the stop)
+// with d < 25.  Whole 64-point chunks whose box is >= 5 m from sel are skipped; a chunk that may
+// hold the stop is always examined.
+template <typename F>
+LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int dir, int scan, float4 sel, F f) {
+  const int lane = lane_id();
+  auto stop_ring = [&](int r) { return dir > 0 ? D(r) > scan + 2.5 : D(r) < scan - 2.5; };
+  // examines points [j0 .. j0 + dir * (cnt - 1)]; true when the stop was met
+  auto run = [&](int j0, int cnt) {
+    const int j = j0 + dir * lane;
+    const bool inr = lane < cnt;
+    const float4 a = inr ? L[j] : make_float4(0, 0, 0, 0);
+    const int r = (int)a.w;
+    const uint64_t mb = __ballot(inr && stop_ring(r));
+    const int limit = mb ? __ffsll((unsigned long long)mb) - 1 : 64;
+    if (inr && lane < limit) {
+      const float d = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
+      if (d < 25) f(j, r, d);
+    }
+    return mb != 0;
+  };
+  if (dir > 0) {
+    int j = c + 1;
+    const int hend = min(end, (j + kChunk - 1) & ~(kChunk - 1));
+    if (j < hend && run(j, hend - j)) return;
+    j = max(j, hend);
+    while (j < end) {
+      const int k = (j / kChunk) + lane;
+      const bool v = k * kChunk < end;
+      float4 lo = make_float4(0, 0, 0, 0), hi = lo;
+      if (v) { lo = ch[2 * k]; hi = ch[2 * k + 1]; }
+      const uint64_t mc = __ballot(v && stop_ring((int)hi.w));
+      const int limit = mc ? __ffsll((unsigned long long)mc) - 1 : 63;
+      uint64_t nb = __ballot(v && lane <= limit && box_d2(lo, hi, sel) < 25.0f);
+      bool stopped = false;
+      while (nb && !stopped) {
+        const int kk = (j / kChunk) + __ffsll((unsigned long long)nb) - 1;
+        nb &= nb - 1;
+        stopped = run(kk * kChunk, min(kChunk, end - kk * kChunk));
+      }
+      if (mc) return;
+      j += 64 * kChunk;
+    }
+  } else {
+    int j = c - 1;
+    if (j < 0) return;
+    const int hstart = j & ~(kChunk - 1);
+    if (run(j, j - hstart + 1)) return;
+    int kt = hstart / kChunk - 1;  // next chunk (descending)
+    while (kt >= 0) {
+      const int k = kt - lane;
+      const bool v = k >= 0;
+      float4 lo = make_float4(0, 0, 0, 0), hi = lo;
+      if (v) { lo = ch[2 * k]; hi = ch[2 * k + 1]; }
+      const uint64_t mc = __ballot(v && stop_ring((int)lo.w));
+      const int limit = mc ? __ffsll((unsigned long long)mc) - 1 : 63;
+      uint64_t nb = __ballot(v && lane <= limit && box_d2(lo, hi, sel) < 25.0f);
+      bool stopped = false;
+      while (nb && !stopped) {
+        const int kk = kt - (__ffsll((unsigned long long)nb) - 1);
+        nb &= nb - 1;
+        stopped = run(kk * kChunk + kChunk - 1, kChunk);
+      }
+      if (mc) return;
+      kt -= 64;
+    }
+  }
 }
 
 // corner association (:478-527): closest (kd NN, sqDis < 25) and the best point of an adjacent
 // ring in the index window.  fwd_end = min(cornerPointsSharpNum, C) (Q11).
-LOAM_D void wave_assoc_corner(const float4* CL, int C, int fwd_end, uint64_t nn, float4 sel,
+LOAM_D void wave_assoc_corner(const float4* CL, const float4* ch, int fwd_end, uint64_t nn, float4 sel,
                               int& ind1, int& ind2) {
-  const int lane = lane_id();
   ind1 = -1;
   ind2 = -1;
   if (nn == ~0ull) return;
@@ -160,38 +270,18 @@ LOAM_D void wave_assoc_corner(const float4* CL, int C, int fwd_end, uint64_t nn,
   ind1 = c;
   const int scan = (int)CL[c].w;
   uint64_t best = ~0ull;
-  for (int base = c + 1; base < fwd_end; base += 64) {
-    const int j = base + lane;
-    const bool inr = j < fwd_end;
-    const float4 a = inr ? CL[j] : make_float4(0, 0, 0, 0);
-    const int r = (int)a.w;
-    const uint64_t mb = __ballot(inr && D(r) > scan + 2.5);
-    const int limit = mb ? __ffsll((unsigned long long)mb) - 1 : 64;
-    if (inr && lane < limit && r > scan) {
-      const float d = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
-      if (d < 25) {
-        const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)(j - c - 1);
-        best = key < best ? key : best;
-      }
+  wave_window(CL, ch, c, fwd_end, +1, scan, sel, [&](int j, int r, float d) {
+    if (r > scan) {
+      const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)(j - c - 1);
+      best = key < best ? key : best;
     }
-    if (mb) break;
-  }
-  for (int base = c - 1; base >= 0; base -= 64) {
-    const int j = base - lane;
-    const bool inr = j >= 0;
-    const float4 a = inr ? CL[j] : make_float4(0, 0, 0, 0);
-    const int r = (int)a.w;
-    const uint64_t mb = __ballot(inr && D(r) < scan - 2.5);
-    const int limit = mb ? __ffsll((unsigned long long)mb) - 1 : 64;
-    if (inr && lane < limit && r < scan) {
-      const float d = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
-      if (d < 25) {
-        const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)((1u << 30) + (c - 1 - j));
-        best = key < best ? key : best;
-      }
+  });
+  wave_window(CL, ch, c, fwd_end, -1, scan, sel, [&](int j, int r, float d) {
+    if (r < scan) {
+      const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)((1u << 30) + (c - 1 - j));
+      best = key < best ? key : best;
     }
-    if (mb) break;
-  }
+  });
   best = wave_min_u64(best);
   if (best != ~0ull) {
     const uint32_t o = (uint32_t)best;
@@ -201,9 +291,8 @@ LOAM_D void wave_assoc_corner(const float4* CL, int C, int fwd_end, uint64_t nn,
 
 // surface association (:590-650): closest, the best of the same / lower ring (min2) and of the
 // higher rings (min3) in the forward window; mirrored in the backward window.
-LOAM_D void wave_assoc_surf(const float4* SL, int S, int fwd_end, uint64_t nn, float4 sel, int& ind1,
-                            int& ind2, int& ind3) {
-  const int lane = lane_id();
+LOAM_D void wave_assoc_surf(const float4* SL, const float4* ch, int fwd_end, uint64_t nn, float4 sel,
+                            int& ind1, int& ind2, int& ind3) {
   ind1 = ind2 = ind3 = -1;
   if (nn == ~0ull) return;
   const float d0 = __uint_as_float((uint32_t)(nn >> 32));
@@ -212,40 +301,16 @@ LOAM_D void wave_assoc_surf(const float4* SL, int S, int fwd_end, uint64_t nn, f
   ind1 = c;
   const int scan = (int)SL[c].w;
   uint64_t best2 = ~0ull, best3 = ~0ull;
-  for (int base = c + 1; base < fwd_end; base += 64) {
-    const int j = base + lane;
-    const bool inr = j < fwd_end;
-    const float4 a = inr ? SL[j] : make_float4(0, 0, 0, 0);
-    const int r = (int)a.w;
-    const uint64_t mb = __ballot(inr && D(r) > scan + 2.5);
-    const int limit = mb ? __ffsll((unsigned long long)mb) - 1 : 64;
-    if (inr && lane < limit) {
-      const float d = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
-      if (d < 25) {
-        const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)(j - c - 1);
-        if (r <= scan) best2 = key < best2 ? key : best2;
-        else best3 = key < best3 ? key : best3;
-      }
-    }
-    if (mb) break;
-  }
-  for (int base = c - 1; base >= 0; base -= 64) {
-    const int j = base - lane;
-    const bool inr = j >= 0;
-    const float4 a = inr ? SL[j] : make_float4(0, 0, 0, 0);
-    const int r = (int)a.w;
-    const uint64_t mb = __ballot(inr && D(r) < scan - 2.5);
-    const int limit = mb ? __ffsll((unsigned long long)mb) - 1 : 64;
-    if (inr && lane < limit) {
-      const float d = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
-      if (d < 25) {
-        const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)((1u << 30) + (c - 1 - j));
-        if (r >= scan) best2 = key < best2 ? key : best2;
-        else best3 = key < best3 ? key : best3;
-      }
-    }
-    if (mb) break;
-  }
+  wave_window(SL, ch, c, fwd_end, +1, scan, sel, [&](int j, int r, float d) {
+    const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)(j - c - 1);
+    if (r <= scan) best2 = key < best2 ? key : best2;
+    else best3 = key < best3 ? key : best3;
+  });
+  wave_window(SL, ch, c, fwd_end, -1, scan, sel, [&](int j, int r, float d) {
+    const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)((1u << 30) + (c - 1 - j));
+    if (r >= scan) best2 = key < best2 ? key : best2;
+    else best3 = key < best3 ? key : best3;
+  });
   best2 = wave_min_u64(best2);
   best3 = wave_min_u64(best3);
   auto decode = [c](uint64_t k) {
@@ -306,13 +371,15 @@ __global__ __launch_bounds__(kOdThreads) void k_od_assoc(OdBuffers b, FeatView f
     const float4 s4 = loampose::transform_to_start(T, q < nc ? sharp[q] : flat[q - nc]);
     int i1, i2, i3 = -1;
     if (q < nc) {
+      const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
       const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC,
-                                       b.hC_T[last_buf * b.P + p], CL, C, 1.0f, 1.0f, s4.x, s4.y, s4.z, cells[w]);
-      wave_assoc_corner(CL, C, min(nc, C), nn, s4, i1, i2);
+                                       b.hC_T[last_buf * b.P + p], CL, ch, C, 1.0f, 1.0f, s4, cells[w]);
+      wave_assoc_corner(CL, ch, min(nc, C), nn, s4, i1, i2);
     } else {
+      const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
       const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS,
-                                       b.hS_T[last_buf * b.P + p], SL, S, 1.0f, 1.0f, s4.x, s4.y, s4.z, cells[w]);
-      wave_assoc_surf(SL, S, min(ns, S), nn, s4, i1, i2, i3);
+                                       b.hS_T[last_buf * b.P + p], SL, ch, S, 1.0f, 1.0f, s4, cells[w]);
+      wave_assoc_surf(SL, ch, min(ns, S), nn, s4, i1, i2, i3);
     }
     if (lane == 0) {
       ind[q] = i1;
@@ -567,6 +634,8 @@ void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   (void)hipMalloc(&b.hC_pts, (size_t)2 * P * b.capC * sizeof(float4));
   (void)hipMalloc(&b.hS_pts, (size_t)2 * P * b.capS * sizeof(float4));
   (void)hipMalloc(&b.hC_T, (size_t)2 * P * sizeof(int));
+  (void)hipMalloc(&b.cC, (size_t)2 * P * 2 * chunks_of(b.capC) * sizeof(float4));
+  (void)hipMalloc(&b.cS, (size_t)2 * P * 2 * chunks_of(b.capS) * sizeof(float4));
   (void)hipMalloc(&b.hS_T, (size_t)2 * P * sizeof(int));
   (void)hipMalloc(&b.ind, (size_t)P * 3 * b.cap_q * sizeof(int));
   (void)hipMalloc(&b.q_cf, (size_t)P * max_iter * b.cap_q * sizeof(float4));
@@ -582,7 +651,7 @@ void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
 
 void od_free(OdBuffers& b) {
   void* ptrs[] = {b.state, b.istate, b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
-                  b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T,
+                  b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
                   b.ind, b.q_cf, b.q_ok, b.part};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
@@ -604,6 +673,7 @@ void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
   jc.tsize = b.hC_T + buf * b.P;
   jc.tmax = b.tC;
   jc.inv_h = 1.0f;
+  jc.chunks = b.cC + (size_t)buf * b.P * 2 * chunks_of(b.capC);
   hipLaunchKernelGGL(k_hash_build, dim3(b.P), dim3(256), 0, st, jc);
   HashJob js = jc;
   js.pts = b.lastS + (size_t)buf * b.P * b.capS;
@@ -614,6 +684,7 @@ void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
   js.out = b.hS_pts + (size_t)buf * b.P * b.capS;
   js.tsize = b.hS_T + buf * b.P;
   js.tmax = b.tS;
+  js.chunks = b.cS + (size_t)buf * b.P * 2 * chunks_of(b.capS);
   hipLaunchKernelGGL(k_hash_build, dim3(b.P), dim3(256), 0, st, js);
 }
 

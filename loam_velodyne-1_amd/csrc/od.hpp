@@ -10,6 +10,8 @@
 namespace loam {
 
 // per-problem float state: transform[6] | transformSum[6] | matP[36] | imu_trans[12]
+constexpr int kChunk = 64;  // points per chunk box
+__host__ __device__ inline int chunks_of(int cap) { return (cap + kChunk - 1) / kChunk; }
 constexpr int kOdSum = 6, kOdMatP = 12, kOdImu = 48, kOdStateFloats = 64;
 // per-problem int state
 enum { kIsDegenerate = 0, kIsCornerLastNum, kIsSurfLastNum, kIsIters, kIsAssoc, kIsRows, kIsQueries,
@@ -40,6 +42,8 @@ struct HashJob {
   int* tsize;           // [P] table size used
   int tmax;
   float inv_h;
+  float4* chunks;       // optional [P][2 * chunks_of(pts_stride)]: per 64-point chunk of the source
+                        // order, (min x, y, z, min ring) and (max x, y, z, max ring)
 };
 
 struct OdBuffers {
@@ -59,6 +63,8 @@ struct OdBuffers {
   float4* hS_pts = nullptr; // [2][P][capS]
   int* hC_T = nullptr;      // [2][P]
   int* hS_T = nullptr;      // [2][P]
+  float4* cC = nullptr;     // [2][P][2 * chunks_of(capC)] chunk boxes of Last corner
+  float4* cS = nullptr;     // [2][P][2 * chunks_of(capS)] chunk boxes of Last surf
   int* ind = nullptr;         // [P][3][cap_q] association of every query (refreshed every 5th iteration)
   float4* q_cf = nullptr;     // [P][max_iter][cap_q] coefficients (zero when rejected)
   int8_t* q_ok = nullptr;     // [P][max_iter][cap_q] accepted flags
