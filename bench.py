@@ -96,6 +96,12 @@ def main():
 
     od, aft, st = eng.batch_download()
 
+    # host-buffer rate: the same batch handed over from host memory, upload + one step
+    a = time.perf_counter()
+    eng.batch_upload(prevs, curs)
+    sync()
+    upload_s = time.perf_counter() - a
+
     # per-kernel device times of the same workload (HIP events on the engine stream), untimed
     eng.set_profiling(True)
     for _ in range(args.profile_steps):
@@ -155,9 +161,18 @@ def main():
             err_od = max(err_od, float(np.abs(od[n_done] - od_o).max()))
             err_mp = max(err_mp, float(np.abs(aft[n_done] - aft_o).max()))
             n_done += 1
+        model = "unknown CPU"
+        try:
+            for line in open("/proc/cpuinfo"):
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+        except OSError:
+            pass
         cpu = {"value": n_done / t_cpu, "unit": "scans/s", "cores": 1, "kind": "port",
                "sample": f"first {n_done} problems of the batch (seeds 1000..{999 + n_done}), "
-                         f"oracle/liboracle.so -O3 single thread, {t_cpu:.1f} s"}
+                         f"oracle/liboracle.so -O3 single thread on {model} ({os.cpu_count()} logical CPUs "
+                         f"visible), {t_cpu:.1f} s"}
         parity = {"problems_checked": n_done, "max_abs_err_odometry": err_od, "max_abs_err_mapping": err_mp}
 
     stage_ms = {k: round(v[0] / max(args.profile_steps, 1), 4) for k, v in sorted(ktimes.items())}
@@ -181,6 +196,11 @@ def main():
         "cpu_baseline": cpu,
         "parity": parity,
         "kernel_ms_per_step": stage_ms,
+        "host_upload": {"ms": upload_s * 1e3, "pcie_inclusive_value": B / (upload_s + ms_per_step * 1e-3),
+                        "note": "rank 0; pageable host sweeps packed and copied per sweep; not the metric"},
+        "workload_stats": {"od_iters_mean": st["od_iters"] / B, "mp_iters_mean": st["mp_iters"] / B,
+                           "mp_stack_mean": st["mp_stack"] / B, "mp_map_points_mean": st["mp_map_points"] / B,
+                           "od_queries_mean": st["od_queries"] / B},
     }
     print(json.dumps(out))
     if dist:

@@ -1,0 +1,53 @@
+"""Per-kernel HBM traffic per launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) of the
+same bench command, corrected as /opt/skills/guides/MI355X_MICROARCH.md (HBM section) prescribes:
+counters are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads, so it is
+doubled; WRITE_SIZE is taken as is.  Writes profiles/traffic.json (bytes per launch per kernel,
+read by bench.py for roofline.traffic) and a per-kernel summary CSV.
+
+    python tools/pmc_traffic.py FETCH.csv WRITE.csv OUT_JSON OUT_CSV
+"""
+import collections
+import csv
+import json
+import sys
+
+
+def short(name):
+    base = name.replace("(anonymous namespace)", "").split("(")[0]
+    if "rocprim" in base:
+        return "rocprim_segmented_radix_sort" if "segmented_radix_sort" in name else "rocprim_other"
+    return base.split("::")[-1]
+
+
+def load(path):
+    agg = collections.defaultdict(lambda: [0.0, 0])
+    for r in csv.DictReader(open(path)):
+        k = short(r["Kernel_Name"])
+        agg[k][0] += float(r["Counter_Value"])
+        agg[k][1] += 1
+    return agg
+
+
+def main():
+    fetch, write, out_json, out_csv = sys.argv[1:5]
+    f, w = load(fetch), load(write)
+    res = {}
+    rows = []
+    for k in sorted(set(f) | set(w)):
+        fk, fn = f.get(k, [0.0, 0])
+        wk, wn = w.get(k, [0.0, 0])
+        fb = 2.0 * fk * 1024 / max(fn, 1)
+        wb = wk * 1024 / max(wn, 1)
+        res[k] = fb + wb
+        rows.append((k, fn, fk * 1024 / max(fn, 1), fb, wb, fb + wb))
+    res["_note"] = ("HBM-side bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> B), averaged over "
+                    "the dispatches of two separate --pmc passes of bench.py --steps 2 --warmup 1")
+    json.dump(res, open(out_json, "w"), indent=1, sort_keys=True)
+    with open(out_csv, "w") as o:
+        o.write("kernel,launches,fetch_size_bytes_raw,fetch_bytes_x2,write_bytes,traffic_bytes_per_launch\n")
+        for r in sorted(rows, key=lambda r: -r[5] * r[1]):
+            o.write("%s,%d,%.0f,%.0f,%.0f,%.0f\n" % r)
+
+
+if __name__ == "__main__":
+    main()
