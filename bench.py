@@ -35,8 +35,10 @@ def kernel_bytes(st):
         "k_sr_features": 16 * st["n_ring"],
         "k_sr_select": 16 * st["n_ring"] + feats,
         "k_od_solve": st["bytes_od"],
-        # per iteration: stack point 16 B + 5 neighbours 80 B read, row (16 B point + 16 B coeff) written
-        "k_mp_query": 96 * st["mp_stack_iters"] + 32 * st["mp_rows_sum"],
+        # per iteration: stack point 16 B (k_mp_nn), 5 neighbours 80 B read and the row (16 B point +
+        # 16 B coeff) written (k_mp_fit)
+        "k_mp_nn": 16 * st["mp_stack_iters"],
+        "k_mp_fit": 80 * st["mp_stack_iters"] + 32 * st["mp_rows_sum"],
         # rows read back for JtJ
         "k_mp_iter": 32 * st["mp_rows_sum"],
     }
@@ -200,7 +202,8 @@ def main():
                         "note": "rank 0; pageable host sweeps packed and copied per sweep; not the metric"},
         "workload_stats": {"od_iters_mean": st["od_iters"] / B, "mp_iters_mean": st["mp_iters"] / B,
                            "mp_stack_mean": st["mp_stack"] / B, "mp_map_points_mean": st["mp_map_points"] / B,
-                           "od_queries_mean": st["od_queries"] / B},
+                           "od_queries_mean": st["od_queries"] / B,
+                           "mp_fit_fraction": st["mp_fits"] / max(st["mp_stack_iters"], 1)},
     }
     print(json.dumps(out))
     if dist:

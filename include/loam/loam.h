@@ -91,6 +91,7 @@ typedef struct {
   uint64_t od_assoc_points;                     /* sum over problems of rounds x (C + S) */
   uint64_t mp_iters, mp_rows_sum, mp_stack, mp_map_points, mp_map_valid_points;
   uint64_t mp_stack_iters;                      /* sum over problems of iterations x stack size */
+  uint64_t mp_fits;                             /* line / plane fits computed (the rest reused: same ordered 5-NN) */
   uint64_t bytes_sr, bytes_od, bytes_mp;        /* algorithmic bytes, SURVEY.md §8(d) */
   double ms_sr, ms_od, ms_mp;                   /* device time per stage (HIP events) */
 } loam_stats;

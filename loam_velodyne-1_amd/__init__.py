@@ -17,7 +17,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libloam_hip.so")
+LIB_PATH = os.environ.get("LOAM_HIP_LIB") or os.path.join(_HERE, "libloam_hip.so")
 _LIB = None
 
 LOAM_OK, LOAM_E_INVAL, LOAM_E_CAPACITY, LOAM_E_HIP, LOAM_E_NOT_READY, LOAM_E_NOMEM = 0, -1, -2, -3, -4, -5
@@ -69,6 +69,7 @@ STAT_U64 = ("n_raw", "n_ring", "n_sharp", "n_less_sharp", "n_flat", "n_less_flat
             "od_iters", "od_assoc_rounds", "od_rows_sum", "od_corner_last", "od_surf_last", "od_queries",
             "od_assoc_points",
             "mp_iters", "mp_rows_sum", "mp_stack", "mp_map_points", "mp_map_valid_points", "mp_stack_iters",
+            "mp_fits",
             "bytes_sr", "bytes_od", "bytes_mp")
 
 

@@ -8,10 +8,11 @@
 //  vg_run          segmented PCL VoxelGrid (hipCUB segmented radix sort by voxel index; equal keys
 //                  keep input order) for the stacks (:693-701) and the valid cubes (:1018-1036)
 //  k_mp_gather     FromMap = valid cubes concatenated (:674-681), then voxel-hashed (k_hash_build)
-//  k_mp_query      one L-M iteration's correspondences (:714-877) for every instance at once, lane
+//  k_mp_nn         one L-M iteration's 5-NN (:714-719, :821-826) for every instance at once, lane
 //                  per stack point: exact 5-NN through the 1 m hash (any point within the 1 m
-//                  acceptance radius lies in the 27 cells), corner PCA with the 3x3 Jacobi, surface
-//                  5x3 QR plane, weight -> accepted flag + coefficients
+//                  acceptance radius lies in the 27 cells; cells pruned by box distance)
+//  k_mp_fit        corner PCA with the 3x3 Jacobi / surface 5x3 QR plane (reused while the ordered
+//                  5-NN is unchanged), weight -> accepted flag + coefficients (:721-877)
 //  k_mp_iter       per instance: fp64 JᵀJ / Jᵀb of the accepted rows, the 6x6 solve and
 //                  degeneracy projection on one lane, update, convergence (:879-974)
 //  k_mp_lm_end     transformUpdate (:199-232)
@@ -395,13 +396,55 @@ __global__ void k_mp_lm_begin(MpBuffers b) {
   ist[kMiStop] = 0;
   ist[kMiIters] = 0;
   ist[kMiRows] = 0;
+  ist[kMiFits] = 0;
 }
 
-// one L-M iteration's correspondences (:714-877): lane per stack point (corner, then surf)
-__global__ __launch_bounds__(kMpQueryThreads) void k_mp_query(MpBuffers b) {
+// one L-M iteration's correspondences (:714-877) in two passes, lane per stack point (corner,
+// then surf).  k_mp_nn: the point at the current TobeMapped pose and its exact 5-NN; small and
+// register-light so many waves hide the gather latency.  k_mp_fit: the line (corner PCA, 3x3
+// Jacobi) or plane (5x3 QR) through the 5 neighbours and the weighted residual.  A fit depends
+// on nothing but the ordered 5 neighbours, so it is kept per query and reused while the ordered
+// 5-NN is unchanged from the previous iteration (bit-identical to refitting).
+__global__ __launch_bounds__(kMpQueryThreads) void k_mp_nn(MpBuffers b) {
   const int p = blockIdx.y, tid = threadIdx.x;
   const int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan] || ist[kMiStop]) return;
+  const float* st = b.state + (size_t)p * kMpStateFloats;
+  const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
+  const int nq = nsc + nss;
+  const float4* stack = b.stack + (size_t)p * b.cap_stack;
+  const int* hcs = b.hC_start + (size_t)p * (b.tmax + 1);
+  const int* hss = b.hS_start + (size_t)p * (b.tmax + 1);
+  const float4* hcp = b.hC_pts + (size_t)p * b.map_cap;
+  const float4* hsp = b.hS_pts + (size_t)p * b.map_cap;
+  const int TC = b.hC_T[p], TS = b.hS_T[p];
+  int4* qnn = b.q_nn + (size_t)p * b.cap_stack * 2;
+  const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
+  for (int q = blockIdx.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
+    const bool corner = q < nsc;
+    const float4 sel = loampose::point_to_map(r, stack[corner ? q : b.capC + (q - nsc)]);
+    Top5 t;
+    if (corner) knn5(hcs, hcp, TC, sel, t);
+    else knn5(hss, hsp, TS, sel, t);
+    qnn[2 * q] = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
+    qnn[2 * q + 1] = make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0);
+  }
+}
+
+namespace {
+// the ordered 5-NN a fit was made for, and the fit: corner (x1, y1, z1, valid), (x2, y2, z2, -);
+// surf (pa, pb, pc, pd), (valid, -, -, -)
+struct MpFit {
+  int4 n0, n1;
+  float4 g0, g1;
+};
+}  // namespace
+
+__global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
+  const int p = blockIdx.y, tid = threadIdx.x;
+  int* ist = b.istate + (size_t)p * kMpStateInts;
+  if (!ist[kMiLmRan] || ist[kMiStop]) return;
+  const bool first = ist[kMiIters] == 0;  // fits of an earlier frame are stale
   const float* st = b.state + (size_t)p * kMpStateFloats;
   __shared__ float jac[kMpQueryThreads][33];   // per-lane 3x3 Jacobi scratch
   const int nfc = b.nfrom[p * 2 + 0];
@@ -410,94 +453,100 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_query(MpBuffers b) {
   const float4* stack = b.stack + (size_t)p * b.cap_stack;
   const float4* fromC = b.from + (size_t)p * b.map_cap;
   const float4* fromS = fromC + nfc;
-  const int* hcs = b.hC_start + (size_t)p * (b.tmax + 1);
-  const int* hss = b.hS_start + (size_t)p * (b.tmax + 1);
-  const float4* hcp = b.hC_pts + (size_t)p * b.map_cap;
-  const float4* hsp = b.hS_pts + (size_t)p * b.map_cap;
-  const int TC = b.hC_T[p], TS = b.hS_T[p];
+  const int4* qnn = b.q_nn + (size_t)p * b.cap_stack * 2;
+  MpFit* qfit = (MpFit*)b.q_fit + (size_t)p * b.cap_stack;
   int8_t* qok = b.q_ok + (size_t)p * b.cap_stack;
   float4* qcf = b.q_cf + (size_t)p * b.cap_stack;
   const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
   float* jw = jac[tid];
+  int nfits = 0;
   for (int q = blockIdx.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
+    const bool corner = q < nsc;
+    const float4* from = corner ? fromC : fromS;
+    const int4 n0 = qnn[2 * q], n1 = qnn[2 * q + 1];
     int ok = 0;
     float4 cf = make_float4(0, 0, 0, 0);
-    const float4 po = stack[q < nsc ? q : b.capC + (q - nsc)];
-    const float4 sel = loampose::point_to_map(r, po);
-    Top5 t;
-    if (q < nsc) {  // :714-819
-      knn5(hcs, hcp, TC, sel, t);
-      if (t.i[4] != 0x7fffffff && D(t.d[4]) < 1.0) {
+    if (n1.x != 0x7fffffff && D(__int_as_float(n1.y)) < 1.0) {  // :719, :826
+      const float4 sel = loampose::point_to_map(r, stack[corner ? q : b.capC + (q - nsc)]);
+      MpFit f = qfit[q];
+      if (first || f.n0.x != n0.x || f.n0.y != n0.y || f.n0.z != n0.z || f.n0.w != n0.w || f.n1.x != n1.x) {
+        ++nfits;
+        const int idx[5] = {n0.x, n0.y, n0.z, n0.w, n1.x};
         float4 nb[5];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) nb[k] = fromC[t.i[k]];
-        float cx = 0, cy = 0, cz = 0;
+        for (int k = 0; k < 5; ++k) nb[k] = from[idx[k]];
+        f.n0 = n0;
+        f.n1 = make_int4(n1.x, 0, 0, 0);
+        if (corner) {  // :721-760
+          float cx = 0, cy = 0, cz = 0;
 #pragma unroll
-        for (int k = 0; k < 5; ++k) { cx += nb[k].x; cy += nb[k].y; cz += nb[k].z; }
-        cx /= 5; cy /= 5; cz /= 5;
-        float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+          for (int k = 0; k < 5; ++k) { cx += nb[k].x; cy += nb[k].y; cz += nb[k].z; }
+          cx /= 5; cy /= 5; cz /= 5;
+          float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          const float ax = nb[k].x - cx, ay = nb[k].y - cy, az = nb[k].z - cz;
-          a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
-          a22 += ay * ay; a23 += ay * az; a33 += az * az;
+          for (int k = 0; k < 5; ++k) {
+            const float ax = nb[k].x - cx, ay = nb[k].y - cy, az = nb[k].z - cz;
+            a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
+            a22 += ay * ay; a23 += ay * az; a33 += az * az;
+          }
+          a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
+          float* A1 = jw;
+          float* D1 = jw + 9;
+          float* V1 = jw + 12;
+          int* iws = (int*)(jw + 21);
+          A1[0] = a11; A1[1] = a12; A1[2] = a13; A1[3] = a12; A1[4] = a22;
+          A1[5] = a23; A1[6] = a13; A1[7] = a23; A1[8] = a33;
+          loamla::jacobi<3>(A1, D1, V1, iws);
+          const bool valid = D1[0] > 3 * D1[1];
+          f.g0 = make_float4((float)(D(cx) + 0.1 * D(V1[0])), (float)(D(cy) + 0.1 * D(V1[1])),
+                             (float)(D(cz) + 0.1 * D(V1[2])), valid ? 1.0f : 0.0f);
+          f.g1 = make_float4((float)(D(cx) - 0.1 * D(V1[0])), (float)(D(cy) - 0.1 * D(V1[1])),
+                             (float)(D(cz) - 0.1 * D(V1[2])), 0.0f);
+        } else {  // :828-850
+          float A0[15], B0[5] = {-1, -1, -1, -1, -1}, X0[3], ws[14];
+#pragma unroll
+          for (int k = 0; k < 5; ++k) { A0[k * 3 + 0] = nb[k].x; A0[k * 3 + 1] = nb[k].y; A0[k * 3 + 2] = nb[k].z; }
+          loamla::qr_solve(A0, B0, 5, 3, X0, ws);
+          float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
+          const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
+          pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+          bool planeValid = true;
+#pragma unroll
+          for (int k = 0; k < 5; ++k)
+            if (fabs(D(pa * nb[k].x + pb * nb[k].y + pc * nb[k].z + pd)) > 0.2) planeValid = false;
+          f.g0 = make_float4(pa, pb, pc, pd);
+          f.g1 = make_float4(planeValid ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f);
         }
-        a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
-        float* A1 = jw;
-        float* D1 = jw + 9;
-        float* V1 = jw + 12;
-        int* iws = (int*)(jw + 21);
-        A1[0] = a11; A1[1] = a12; A1[2] = a13; A1[3] = a12; A1[4] = a22;
-        A1[5] = a23; A1[6] = a13; A1[7] = a23; A1[8] = a33;
-        loamla::jacobi<3>(A1, D1, V1, iws);
-        if (D1[0] > 3 * D1[1]) {
-          const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
-          const float x1 = (float)(D(cx) + 0.1 * D(V1[0])), y1 = (float)(D(cy) + 0.1 * D(V1[1])),
-                      z1 = (float)(D(cz) + 0.1 * D(V1[2]));
-          const float x2 = (float)(D(cx) - 0.1 * D(V1[0])), y2 = (float)(D(cy) - 0.1 * D(V1[1])),
-                      z2 = (float)(D(cz) - 0.1 * D(V1[2]));
-          const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
-          const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
-          const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
-          const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
-          const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
-          const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
-          const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
-          const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
-          const float ld2 = a012 / l12;
-          const float sw = (float)(1 - 0.9 * fabs(D(ld2)));
-          cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
-          ok = D(sw) > 0.1 ? 1 : 0;
-        }
+        qfit[q] = f;
       }
-    } else {  // :821-877
-      knn5(hss, hsp, TS, sel, t);
-      if (t.i[4] != 0x7fffffff && D(t.d[4]) < 1.0) {
-        float4 nb[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) nb[k] = fromS[t.i[k]];
-        float A0[15], B0[5] = {-1, -1, -1, -1, -1}, X0[3], ws[14];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) { A0[k * 3 + 0] = nb[k].x; A0[k * 3 + 1] = nb[k].y; A0[k * 3 + 2] = nb[k].z; }
-        loamla::qr_solve(A0, B0, 5, 3, X0, ws);
-        float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
-        const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
-        pa /= ps; pb /= ps; pc /= ps; pd /= ps;
-        bool planeValid = true;
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-          if (fabs(D(pa * nb[k].x + pb * nb[k].y + pc * nb[k].z + pd)) > 0.2) planeValid = false;
-        if (planeValid) {
-          const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
-          const float sw = (float)(1 - 0.9 * fabs(D(pd2)) / sqrt(sqrt(D(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z))));
-          cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
-          ok = D(sw) > 0.1 ? 1 : 0;
-        }
+      if (corner && f.g0.w != 0.0f) {  // :762-816
+        const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
+        const float x1 = f.g0.x, y1 = f.g0.y, z1 = f.g0.z, x2 = f.g1.x, y2 = f.g1.y, z2 = f.g1.z;
+        const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
+        const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
+        const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
+        const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
+        const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
+        const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
+        const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
+        const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
+        const float ld2 = a012 / l12;
+        const float sw = (float)(1 - 0.9 * fabs(D(ld2)));
+        cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
+        ok = D(sw) > 0.1 ? 1 : 0;
+      } else if (!corner && f.g1.x != 0.0f) {  // :852-874
+        const float pa = f.g0.x, pb = f.g0.y, pc = f.g0.z, pd = f.g0.w;
+        const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
+        const float sw = (float)(1 - 0.9 * fabs(D(pd2)) / sqrt(sqrt(D(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z))));
+        cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
+        ok = D(sw) > 0.1 ? 1 : 0;
       }
     }
     qok[q] = (int8_t)ok;
     qcf[q] = cf;
   }
+  nfits = wave_sum(nfits);
+  if (lane_id() == 0 && nfits) atomicAdd(&ist[kMiFits], nfits);
 }
 
 namespace {
@@ -848,6 +897,8 @@ void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter
   (void)hipMalloc(&b.nfrom, (size_t)P * 2 * sizeof(int));
   (void)hipMalloc(&b.q_ok, Ps * sizeof(int8_t));
   (void)hipMalloc(&b.q_cf, Ps * sizeof(float4));
+  (void)hipMalloc(&b.q_nn, Ps * 2 * sizeof(int4));
+  (void)hipMalloc(&b.q_fit, Ps * 4 * sizeof(float4));
   (void)hipMalloc(&b.app_cnt, (size_t)P * kCubeNum * 2 * sizeof(int));
   (void)hipMalloc(&b.app_off, (size_t)P * kCubeNum * 2 * sizeof(int));
   (void)hipMalloc(&b.app, Ps * sizeof(float4));
@@ -879,7 +930,7 @@ void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter
 void mp_free(MpBuffers& b) {
   void* ptrs[] = {b.state, b.istate, b.slots, b.pool, b.valid, b.vpre, b.inC, b.inS, b.inF, b.in_n, b.in_pose,
                   b.stack2, b.stack, b.nstack, b.from, b.hC_start, b.hS_start, b.h_fill, b.hC_T, b.hS_T,
-                  b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
+                  b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
                   b.vg_params, b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.cub_tmp, b.reg, b.nreg};
   for (void* q : ptrs)
@@ -932,8 +983,10 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
   hipLaunchKernelGGL(k_mp_lm_begin, dim3((P + 255) / 256), dim3(256), 0, st, b);
   const int gq = std::min(64, (b.cap_stack + kMpQueryThreads - 1) / kMpQueryThreads);
   for (int it = 0; it < b.max_iter; ++it) {
-    hipLaunchKernelGGL(k_mp_query, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
-    mark("k_mp_query");
+    hipLaunchKernelGGL(k_mp_nn, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
+    mark("k_mp_nn");
+    hipLaunchKernelGGL(k_mp_fit, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
+    mark("k_mp_fit");
     hipLaunchKernelGGL(k_mp_iter, dim3(P), dim3(kMpThreads), 0, st, b);
     mark("k_mp_iter");
   }
@@ -1024,6 +1077,7 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
     stats->mp_rows_sum = (uint64_t)si[kMiRows];
     stats->mp_stack = (uint64_t)(si[kMiStackC] + si[kMiStackS]);
     stats->mp_stack_iters = (uint64_t)si[kMiIters] * (si[kMiStackC] + si[kMiStackS]);
+    stats->mp_fits = (uint64_t)si[kMiFits];
     stats->mp_map_points = (uint64_t)(si[kMiFromC] + si[kMiFromS]);
     stats->mp_map_valid_points = (uint64_t)si[kMiValidPts];
     stats->ms_mp = ms;
@@ -1069,6 +1123,7 @@ int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats*
       stats->mp_rows_sum += (uint64_t)q[kMiRows];
       stats->mp_stack += (uint64_t)(q[kMiStackC] + q[kMiStackS]);
       stats->mp_stack_iters += (uint64_t)q[kMiIters] * (q[kMiStackC] + q[kMiStackS]);
+      stats->mp_fits += (uint64_t)q[kMiFits];
       stats->mp_map_points += (uint64_t)(q[kMiFromC] + q[kMiFromS]);
       stats->mp_map_valid_points += (uint64_t)q[kMiValidPts];
     }

@@ -19,7 +19,7 @@ constexpr int kMaxValid = 125;
 constexpr int kMpSum = 0, kMpIncre = 6, kMpTobe = 12, kMpBef = 18, kMpAft = 24, kMpMatP = 30, kMpOnY = 66,
               kMpStateFloats = 72;
 enum { kMiCenW = 0, kMiCenH, kMiCenD, kMiDegen, kMiNValid, kMiIters, kMiRows, kMiStackC, kMiStackS, kMiFromC,
-       kMiFromS, kMiErr, kMiLmRan, kMiValidPts, kMiStop, kMpStateInts = 16 };
+       kMiFromS, kMiErr, kMiLmRan, kMiValidPts, kMiStop, kMiFits, kMpStateInts = 16 };
 
 // one mapping frame's inputs for every instance (device pointers)
 struct MpInput {
@@ -70,6 +70,8 @@ struct MpBuffers {
   // per-query L-M outputs of the current iteration
   int8_t* q_ok = nullptr;     // [P][cap_stack]
   float4* q_cf = nullptr;     // [P][cap_stack]
+  int4* q_nn = nullptr;       // [P][cap_stack][2] this iteration's ordered 5-NN (i0..i3 | i4, d4 bits)
+  float4* q_fit = nullptr;    // [P][cap_stack][4] MpFit: the 5-NN a line / plane was fitted to + the fit
   // insertion / per-cube downsampling
   int* app_cnt = nullptr;     // [P][kCubeNum][2] appended points per cube
   int* app_off = nullptr;     // [P][kCubeNum][2]
