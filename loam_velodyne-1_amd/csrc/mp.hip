@@ -347,23 +347,25 @@ LOAM_D void top5_offer(Top5& t, float d, int idx) {
   }
 }
 
+// the 27 neighbour cells (index (dx+1) + 3(dy+1) + 9(dz+1)): centre, faces, edges, corners
+__constant__ int kCellOrder[27] = {13, 4, 10, 12, 14, 16, 22, 1, 3, 5, 7, 9, 11, 15, 17, 19, 21, 23, 25,
+                                   0, 2, 6, 8, 18, 20, 24, 26};
+
 // exact 5-NN within the 27 cells around q (1 m cells), as far as it matters: visited centre,
 // faces, edges, corners; a cell is skipped when its box distance exceeds the current 5th
 // distance or reaches the 1 m acceptance radius (the caller rejects a 5th neighbour at >= 1 m).
 // Box distances are lower bounds of the float squared distances (monotone rounding of the same
 // expression), so every neighbour that can be accepted is found exactly.
+// t may arrive seeded with real map points (their distances to q): they bound the search from
+// the start and do not change the result.
 LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t) {
-#pragma unroll
-  for (int k = 0; k < 5; ++k) { t.d[k] = 3.4e38f; t.i[k] = 0x7fffffff; }
   if (T <= 0) return;
   const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
   const float gxl = q.x - (float)cx, gyl = q.y - (float)cy, gzl = q.z - (float)cz;
   const float gxh = (float)(cx + 1) - q.x, gyh = (float)(cy + 1) - q.y, gzh = (float)(cz + 1) - q.z;
-  constexpr int kOrder[27] = {13, 4, 10, 12, 14, 16, 22, 1, 3, 5, 7, 9, 11, 15, 17, 19, 21, 23, 25,
-                              0, 2, 6, 8, 18, 20, 24, 26};
-#pragma unroll
+#pragma unroll 1
   for (int o = 0; o < 27; ++o) {
-    const int c = kOrder[o];
+    const int c = kCellOrder[o];
     const int dx = c % 3 - 1, dy = (c / 3) % 3 - 1, dz = c / 9 - 1;
     const float gx = dx < 0 ? gxl : (dx > 0 ? gxh : 0.0f);
     const float gy = dy < 0 ? gyl : (dy > 0 ? gyh : 0.0f);
@@ -371,10 +373,15 @@ LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t) {
     const float bd = sqdist(gx, gy, gz, 0.0f, 0.0f, 0.0f);
     if (bd >= 1.0f || bd > t.d[4]) continue;
     const uint32_t h = cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1);
-    const int b1 = start[h + 1];
-    for (int k = start[h]; k < b1; ++k) {
-      const float4 a = hp[k];
-      top5_offer(t, sqdist(a.x, a.y, a.z, q.x, q.y, q.z), __builtin_bit_cast(int, a.w));
+    const int b0 = start[h], b1 = start[h + 1];
+    // four independent loads in flight per step: the loop is bound by gather latency
+    for (int k = b0; k < b1; k += 4) {
+      float4 a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = hp[min(k + u, b1 - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k + u < b1) top5_offer(t, sqdist(a[u].x, a[u].y, a[u].z, q.x, q.y, q.z), __builtin_bit_cast(int, a[u].w));
     }
   }
 }
@@ -419,11 +426,27 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_nn(MpBuffers b) {
   const float4* hsp = b.hS_pts + (size_t)p * b.map_cap;
   const int TC = b.hC_T[p], TS = b.hS_T[p];
   int4* qnn = b.q_nn + (size_t)p * b.cap_stack * 2;
+  const bool first = ist[kMiIters] == 0;
+  const float4* fromC = b.from + (size_t)p * b.map_cap;
+  const float4* fromS = fromC + b.nfrom[p * 2 + 0];
   const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
   for (int q = blockIdx.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
     const bool corner = q < nsc;
     const float4 sel = loampose::point_to_map(r, stack[corner ? q : b.capC + (q - nsc)]);
     Top5 t;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { t.d[k] = 3.4e38f; t.i[k] = 0x7fffffff; }
+    if (!first) {  // seed with the previous iteration's neighbours: a tight bound from the start
+      const int4 n0 = qnn[2 * q], n1 = qnn[2 * q + 1];
+      const int prev[5] = {n0.x, n0.y, n0.z, n0.w, n1.x};
+      const float4* from = corner ? fromC : fromS;
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        if (prev[k] != 0x7fffffff) {
+          const float4 a = from[prev[k]];
+          top5_offer(t, sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z), prev[k]);
+        }
+    }
     if (corner) knn5(hcs, hcp, TC, sel, t);
     else knn5(hss, hsp, TS, sel, t);
     qnn[2 * q] = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
