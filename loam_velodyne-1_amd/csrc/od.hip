@@ -143,19 +143,18 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
       cnt = start[bucket + 1] - b0;
     }
   }
-  // two of the 27 cells may share a bucket: count it once
-  for (int o = 0; o < 27; ++o) {
-    int bo = __shfl(bucket, o, 64);
-    if (o < lane && bo == bucket) cnt = 0;
-  }
+  // (two of the 27 cells may share a bucket: its points are then offered twice, which does not
+  // change a minimum)
   const int incl = wave_incl_scan(cnt);
   const int total = __shfl(incl, 63, 64);
-  if (lane < 27) { cells[lane] = incl - cnt; cells[32 + lane] = b0; }
+  if (lane < 32) { cells[lane] = lane < 27 ? incl - cnt : 0x7fffffff; cells[32 + lane] = b0; }
   __builtin_amdgcn_wave_barrier();
   uint64_t best = ~0ull;
   for (int t = lane; t < total; t += 64) {
-    int k = 0;
-    while (k < 26 && cells[k + 1] <= t) ++k;
+    int k = 0;  // last cell whose prefix is <= t (binary search over 32 entries)
+#pragma unroll
+    for (int step = 16; step > 0; step >>= 1)
+      if (cells[k + step] <= t) k += step;
     const float4 a = hp[cells[32 + k] + (t - cells[k])];
     const float d = sqdist(a.x, a.y, a.z, q.x, q.y, q.z);
     const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)__float_as_int(a.w);
