@@ -23,6 +23,7 @@ enum : int {
 constexpr int kSrThreads = 512;     // ring-sort workgroup (one per sweep)
 constexpr int kSelThreads = 256;    // per-ring selection workgroup
 constexpr int kRingCap = 4096;      // max ring span (points) handled in LDS by one workgroup
+constexpr int kBigSlots = 8;        // workgroups (scratch slots) of the global-memory selection
 constexpr int kSharpPerRing = 12, kLessSharpPerRing = 120, kFlatPerRing = 24;
 
 // Scan-registration buffers for S sweeps of capacity `cap` points each (index s*cap + i).
@@ -51,6 +52,12 @@ struct SrBuffers {
   float4* lflat = nullptr;   // [S][cap]
   int* cnt = nullptr;        // [S][4]: sharp, less_sharp, flat, less_flat
   int* err = nullptr;        // [S]
+  int* sel_big = nullptr;    // [S] selection kernel that handles the sweep (0 fast, 1 4096 LDS, 2 global)
+  int* st_loff = nullptr;    // [S][R] offset of each ring's lessFlat in the sweep's st_lflat block
+  uint64_t* big_keys = nullptr;  // [kBigSlots][big_stride] ring state of the global-memory selection
+  int* big_sidx = nullptr;
+  int* big_cand = nullptr;
+  int big_stride = 0;
   __host__ __device__ int ntiles() const { return (cap + kSrThreads - 1) / kSrThreads; }
 };
 

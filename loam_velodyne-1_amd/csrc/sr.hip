@@ -20,6 +20,8 @@
 //
 // HBM traffic per sweep (algorithmic): 16 B/pt raw read, 16 B/pt ring-sorted
 // write + read, 16 B per feature point written.
+#include <type_traits>
+
 #include "dev_common.hpp"
 #include "engine.hpp"
 
@@ -272,18 +274,19 @@ __global__ __launch_bounds__(kFeatTile) void k_sr_features(SrBuffers b, SrParams
 }
 
 // ---------------------------------------------------------------- per-ring selection
+template <int CAP>
 struct SelShared {
-  uint64_t keys[kRingCap];  // (segment, curvature, position) of the ring; then (voxel, candidate)
-  int sidx[kRingCap];       // sortInd of the ring on entry
-  uint16_t cand[kRingCap];  // lessFlat candidate positions (relative to the ring start)
-  uint8_t pk[kRingCap + 16];  // bit 0 cloudNeighborPicked, bit 1 neighbour-walk stop (gap)
-  int8_t lab[kRingCap + 16];
+  uint64_t keys[CAP];       // (segment, curvature, position) of the ring; then (voxel, candidate)
+  int sidx[CAP];            // sortInd of the ring on entry
+  uint16_t cand[CAP];       // lessFlat candidate positions (relative to the ring start)
+  uint8_t pk[CAP + 16];     // bit 0 cloudNeighborPicked, bit 1 neighbour-walk stop (gap)
+  int8_t lab[CAP + 16];
   int se[128];
   int picks[kSharpPerRing + kLessSharpPerRing + kFlatPerRing];
   int scratch[16];
   float red[6][kSelThreads / 64];
   int order[64];
-  int nsharp, nlsharp, nflat, ncand, wf;
+  int nsharp, nlsharp, nflat, ncand, wf, big, loff;
 };
 
 // :495-520 with the distance tests precomputed as gap bits
@@ -298,25 +301,35 @@ LOAM_D void mark_neighbours(int n, int ind, uint8_t* pk, int wlo) {
   }
 }
 
-LOAM_D float key_curv(uint64_t key) { return __builtin_bit_cast(float, (uint32_t)(key >> 16)); }
+// ring sort key: segment (3 bits) | curvature bits (32) | position in the ring (29)
+constexpr int kPosBits = 29;
+constexpr uint64_t kPosMask = (1ull << kPosBits) - 1;
+LOAM_D float key_curv(uint64_t key) { return __builtin_bit_cast(float, (uint32_t)(key >> kPosBits)); }
 
-// processes ring q of sweep s; `seq` = fallback mode (rings walked in order by one workgroup).
-// The six segment sorts (:466-474) are one LDS sort of the ring by (segment, curvature,
-// position): the segments partition the ring span and the sort does not depend on the picks.
-// The greedy picks and the lessFlat candidates of each segment are then one wave's work in LDS.
-LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq, SelShared& sh) {
+// processes ring q of sweep s; `seq` = rings walked in order by one workgroup (dependent rings).
+// The six segment sorts (:466-474) are one sort of the ring by (segment, curvature, position):
+// the segments partition the ring span and the sort does not depend on the picks.  The greedy
+// picks and the lessFlat candidates of each segment are then one wave's work.
+// CAP: LDS capacity of the ring state.  BIG: the ring state lives in global scratch (slot `slot`)
+// and in the sweep's own picked / label arrays, for spans beyond any LDS capacity (an empty ring
+// leaves its successor spanning every earlier ring, Q5).
+template <int CAP, bool BIG>
+LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq, SelShared<CAP>& sh, int slot) {
+  using CandT = typename std::conditional<BIG, int, uint16_t>::type;
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const float4* pts = b.full + (size_t)s * b.cap;
   const float* curv = b.curv + (size_t)s * b.cap;
   const int sq = sh.se[q], eq = sh.se[R + q];
   const int lo = sq, hi = eq - 1;
+  const int loff = BIG ? sh.loff : q * kRingCap;   // lessFlat staging offset of this ring
   if (tid == 0) { sh.nsharp = 0; sh.nlsharp = 0; sh.nflat = 0; sh.ncand = 0; }
   int* st_cnt = b.st_cnt + (size_t)(s * R + q) * 4;
+  if (tid == 0) b.st_loff[s * R + q] = loff;
   if (lo > hi) {  // every segment is empty
     if (tid < 4) st_cnt[tid] = 0;
     return;
   }
-  if (hi - lo + 1 > kRingCap || lo < 0 || hi >= n) {
+  if ((!BIG && hi - lo + 1 > CAP) || lo < 0 || hi >= n) {
     if (tid == 0) b.err[s] |= ERR_CAP_RING;
     if (tid < 4) st_cnt[tid] = 0;
     return;
@@ -324,7 +337,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
   const int len = hi - lo + 1;
   // window of point indices this ring may touch: span and the indices its sortInd holds, +-5
   int vmin = lo, vmax = hi;
-  if (seq) {
+  if (seq && !BIG) {
     for (int k = lo + tid; k <= hi; k += kSelThreads) {
       int v = b.sortind[(size_t)s * b.cap + k];
       vmin = min(vmin, v);
@@ -340,15 +353,34 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
     }
     __syncthreads();
   }
-  const int wlo = max(0, vmin - 5), whi = min(n - 1, vmax + 5);
-  if (whi - wlo + 1 > kRingCap + 16) {
+  const int wlo = BIG ? 0 : max(0, vmin - 5), whi = BIG ? n - 1 : min(n - 1, vmax + 5);
+  if (!BIG && whi - wlo + 1 > CAP + 16) {
     if (tid == 0) b.err[s] |= ERR_CAP_RING;
     if (tid < 4) st_cnt[tid] = 0;
     return;
   }
-  for (int k = wlo + tid; k <= whi; k += kSelThreads) {
-    sh.pk[k - wlo] = b.picked[(size_t)s * b.cap + k];
-    sh.lab[k - wlo] = b.label[(size_t)s * b.cap + k];
+  uint64_t* keys;
+  int* sidx;
+  CandT* cand;
+  uint8_t* pk;
+  int8_t* lab;
+  if constexpr (BIG) {
+    const size_t so = (size_t)slot * b.big_stride;
+    keys = b.big_keys + so;
+    sidx = b.big_sidx + so;
+    cand = b.big_cand + so;
+    pk = b.picked + (size_t)s * b.cap;
+    lab = b.label + (size_t)s * b.cap;
+  } else {
+    keys = sh.keys;
+    sidx = sh.sidx;
+    cand = sh.cand;
+    pk = sh.pk;
+    lab = sh.lab;
+    for (int k = wlo + tid; k <= whi; k += kSelThreads) {
+      pk[k - wlo] = b.picked[(size_t)s * b.cap + k];
+      lab[k - wlo] = b.label[(size_t)s * b.cap + k];
+    }
   }
   int segb[7];
 #pragma unroll
@@ -358,16 +390,16 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
     uint64_t key = ~0ull;
     if (t < len) {
       const int v = b.sortind[(size_t)s * b.cap + lo + t];
-      sh.sidx[t] = v;
+      sidx[t] = v;
       int seg = 0;
 #pragma unroll
       for (int j = 1; j < 6; ++j) seg += (lo + t >= segb[j]) ? 1 : 0;
-      key = ((uint64_t)seg << 48) | ((uint64_t)fkey(curv[v]) << 16) | (uint32_t)t;
+      key = ((uint64_t)seg << 61) | ((uint64_t)fkey(curv[v]) << kPosBits) | (uint64_t)t;
     }
-    sh.keys[t] = key;
+    keys[t] = key;
   }
   __syncthreads();
-  block_bitonic_sort<kSelThreads>(sh.keys, P2);
+  block_bitonic_sort<kSelThreads>(keys, P2);
   if (w == 0) {
     int run = 0;
     for (int j = 0; j < 6; ++j) {
@@ -379,28 +411,28 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
       for (int base = ep; base >= sp && !done; base -= 64) {
         const int k = base - lane;
         const bool inr = k >= sp;
-        const uint64_t key = inr ? sh.keys[k] : 0ull;
-        const int ind = inr ? sh.sidx[key & 0xffffu] : 0;
+        const uint64_t key = inr ? keys[k] : 0ull;
+        const int ind = inr ? sidx[key & kPosMask] : 0;
         const bool elig = inr && D(key_curv(key)) > 0.1;
         uint64_t remaining = __ballot(elig);
         while (remaining) {
-          const bool cand = elig && ((remaining >> lane) & 1ull) && (sh.pk[ind - wlo] & 1) == 0;
-          const uint64_t m = __ballot(cand);
+          const bool cand_ok = elig && ((remaining >> lane) & 1ull) && (pk[ind - wlo] & 1) == 0;
+          const uint64_t m = __ballot(cand_ok);
           if (!m) break;
           const int f = __ffsll((unsigned long long)m) - 1;
           largest++;
           if (largest > 20) { done = true; break; }
           if (lane == f) {
             if (largest <= 2) {
-              sh.lab[ind - wlo] = 2;
+              lab[ind - wlo] = 2;
               sh.picks[sh.nsharp++] = ind;
               sh.picks[kSharpPerRing + sh.nlsharp++] = ind;
             } else {
-              sh.lab[ind - wlo] = 1;
+              lab[ind - wlo] = 1;
               sh.picks[kSharpPerRing + sh.nlsharp++] = ind;
             }
-            sh.pk[ind - wlo] |= 1;
-            mark_neighbours(n, ind, sh.pk, wlo);
+            pk[ind - wlo] |= 1;
+            mark_neighbours(n, ind, pk, wlo);
           }
           __threadfence_block();
           __builtin_amdgcn_wave_barrier();
@@ -413,24 +445,24 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
       for (int base = sp; base <= ep && !done; base += 64) {
         const int k = base + lane;
         const bool inr = k <= ep;
-        const uint64_t key = inr ? sh.keys[k] : 0ull;
-        const int ind = inr ? sh.sidx[key & 0xffffu] : 0;
+        const uint64_t key = inr ? keys[k] : 0ull;
+        const int ind = inr ? sidx[key & kPosMask] : 0;
         const bool elig = inr && D(key_curv(key)) < 0.1;
         uint64_t remaining = __ballot(elig);
         while (remaining) {
-          const bool cand = elig && ((remaining >> lane) & 1ull) && (sh.pk[ind - wlo] & 1) == 0;
-          const uint64_t m = __ballot(cand);
+          const bool cand_ok = elig && ((remaining >> lane) & 1ull) && (pk[ind - wlo] & 1) == 0;
+          const uint64_t m = __ballot(cand_ok);
           if (!m) break;
           const int f = __ffsll((unsigned long long)m) - 1;
           if (lane == f) {
-            sh.lab[ind - wlo] = -1;
+            lab[ind - wlo] = -1;
             sh.picks[kSharpPerRing + kLessSharpPerRing + sh.nflat++] = ind;
           }
           smallest++;
           if (smallest >= 4) { done = true; break; }
           if (lane == f) {
-            sh.pk[ind - wlo] |= 1;
-            mark_neighbours(n, ind, sh.pk, wlo);
+            pk[ind - wlo] |= 1;
+            mark_neighbours(n, ind, pk, wlo);
           }
           __threadfence_block();
           __builtin_amdgcn_wave_barrier();
@@ -442,9 +474,9 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
       // (:568-572) lessFlat candidates of this segment, in position order
       for (int base = segb[j]; base < segb[j + 1]; base += 64) {
         const int k = base + lane;
-        const bool flag = k < segb[j + 1] && sh.lab[k - wlo] <= 0;
+        const bool flag = k < segb[j + 1] && lab[k - wlo] <= 0;
         const uint64_t m = __ballot(flag);
-        if (flag) sh.cand[run + __popcll(m & lanemask_lt())] = (uint16_t)(k - lo);
+        if (flag) cand[run + __popcll(m & lanemask_lt())] = (CandT)(k - lo);
         run += __popcll(m);
       }
     }
@@ -453,15 +485,16 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
   __syncthreads();
   if (seq) {  // the ring's sortInd after its six sorts, for the next ring (one workgroup, ordered)
     for (int t = tid; t < len; t += kSelThreads)
-      b.sortind[(size_t)s * b.cap + lo + t] = sh.sidx[sh.keys[t] & 0xffffu];
+      b.sortind[(size_t)s * b.cap + lo + t] = sidx[keys[t] & kPosMask];
     __syncthreads();
   }
   // ---- PCL VoxelGrid 0.2 of the ring's lessFlat candidates (:575-579)
   const int nc = sh.ncand;
-  float4* outp = b.st_lflat + (size_t)(s * R + q) * kRingCap;
+  float4* outp = b.st_lflat + (size_t)s * R * kRingCap + loff;
+  const int outcap = BIG ? R * kRingCap - loff : kRingCap;
   float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
   for (int t = tid; t < nc; t += kSelThreads) {
-    const float4 a = pts[lo + sh.cand[t]];
+    const float4 a = pts[lo + cand[t]];
     mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
     mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
   }
@@ -484,7 +517,8 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
     const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
     const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
     if (dx * dy * dz > (int64_t)0x7fffffff) {  // "leaf size too small": output = input
-      for (int t = tid; t < nc; t += kSelThreads) outp[t] = pts[lo + sh.cand[t]];
+      for (int t = tid; t < nc; t += kSelThreads)
+        if (t < outcap) outp[t] = pts[lo + cand[t]];
       nout = nc;
     } else {
       int minb[3], maxb[3];
@@ -498,38 +532,47 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
       for (int t = tid; t < P2c; t += kSelThreads) {
         uint64_t key = ~0ull;
         if (t < nc) {
-          const float4 a = pts[lo + sh.cand[t]];
+          const float4 a = pts[lo + cand[t]];
           int i0 = (int)(floorf(a.x * inv) - (float)minb[0]);
           int i1 = (int)(floorf(a.y * inv) - (float)minb[1]);
           int i2 = (int)(floorf(a.z * inv) - (float)minb[2]);
           uint32_t idx = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
           key = ((uint64_t)idx << 32) | (uint32_t)t;
         }
-        sh.keys[t] = key;
+        keys[t] = key;
       }
       __syncthreads();
-      block_bitonic_sort<kSelThreads>(sh.keys, P2c);
+      block_bitonic_sort<kSelThreads>(keys, P2c);
       int run = 0;
       for (int base = 0; base < nc; base += kSelThreads) {
         const int t = base + tid;
-        const int head = (t < nc && (t == 0 || (sh.keys[t] >> 32) != (sh.keys[t - 1] >> 32))) ? 1 : 0;
+        const int head = (t < nc && (t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32))) ? 1 : 0;
         int tot;
         const int ex = block_excl_scan<kSelThreads>(head, sh.scratch, tot);
         if (head) {
-          const uint32_t vk = (uint32_t)(sh.keys[t] >> 32);
+          const uint32_t vk = (uint32_t)(keys[t] >> 32);
+          int e = t + 1;
+          while (e < nc && (uint32_t)(keys[e] >> 32) == vk) ++e;
+          // members summed in sorted order; four independent gathers in flight per step
           float sx = 0, sy = 0, sz = 0, si = 0;
-          int e = t;
-          while (e < nc && (uint32_t)(sh.keys[e] >> 32) == vk) {
-            const float4 a = pts[lo + sh.cand[(int)(sh.keys[e] & 0xffffffffu)]];
-            sx += a.x; sy += a.y; sz += a.z; si += a.w;
-            ++e;
+          for (int m = t; m < e; m += 4) {
+            float4 a[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a[u] = pts[lo + cand[(int)(keys[min(m + u, e - 1)] & 0xffffffffu)]];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (m + u < e) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
           }
           const float cnt = (float)(e - t);
-          outp[run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+          if (run + ex < outcap) outp[run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
         }
         run += tot;
       }
       nout = run;
+    }
+    if (nout > outcap) {
+      if (tid == 0) b.err[s] |= ERR_CAP_RING;
+      nout = outcap;
     }
   }
   // pick lists -> staging
@@ -540,56 +583,78 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
   for (int t = tid; t < nf; t += kSelThreads)
     b.st_flat[(size_t)(s * R + q) * kFlatPerRing + t] = sh.picks[kSharpPerRing + kLessSharpPerRing + t];
   if (tid == 0) { st_cnt[0] = ns; st_cnt[1] = nl; st_cnt[2] = nf; st_cnt[3] = nout; }
-  if (seq) {  // write the shared state back for the next ring (one workgroup, ordered)
+  if (BIG && tid == 0) sh.loff = loff + nout;
+  if (seq && !BIG) {  // write the shared state back for the next ring (one workgroup, ordered)
     for (int k = wlo + tid; k <= whi; k += kSelThreads) {
-      b.picked[(size_t)s * b.cap + k] = sh.pk[k - wlo];
-      b.label[(size_t)s * b.cap + k] = sh.lab[k - wlo];
+      b.picked[(size_t)s * b.cap + k] = pk[k - wlo];
+      b.label[(size_t)s * b.cap + k] = lab[k - wlo];
     }
-    __threadfence();
   }
+  __threadfence();
   __syncthreads();
 }
 
+// Three instantiations, chosen per sweep: CAP = 2048 (34 KB of LDS, four workgroups per CU)
+// takes every sweep whose rings are independent and no longer than 2048 points (VLP-16,
+// HDL-64E) and flags the others (sel_big = 1); CAP = 4096 redoes those whose spans fit it, rings
+// walked in order when they depend on each other, and flags the rest (sel_big = 2); the global-
+// memory variant walks those (gridDim.x workgroups over the flagged sweeps, one scratch slot each).
+template <int CAP, int MODE>  // MODE 0: fast, 1: 4096 / dependent rings, 2: unbounded spans
 __global__ __launch_bounds__(kSelThreads) void k_sr_select(SrBuffers b, SrParams p) {
-  const int q = blockIdx.x, s = blockIdx.y, tid = threadIdx.x, R = p.R;
-  const int n = b.n_full[s];
-  __shared__ SelShared sh;
-  if (tid < R) {
-    int st = b.ring_se[s * 2 * R + tid], en = b.ring_se[s * 2 * R + R + tid];
-    if (tid == 0) st = 5;            // :392
-    if (tid == R - 1) en = n - 5;    // :393
-    sh.se[tid] = st;
-    sh.se[R + tid] = en;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    // rings are independent when their active spans [start, end-1] are more than 5 points apart
-    int wf = 1, prev_hi = -100000;
-    int* order = sh.order;
-    int na = 0;
-    for (int r = 0; r < R; ++r)
-      if (sh.se[r] <= sh.se[R + r] - 1) order[na++] = r;
-    for (int a = 1; a < na; ++a) {
-      int v = order[a], c = a;
-      while (c > 0 && sh.se[order[c - 1]] > sh.se[v]) { order[c] = order[c - 1]; --c; }
-      order[c] = v;
+  constexpr bool BIG = MODE == 2;
+  const int tid = threadIdx.x, R = p.R;
+  __shared__ SelShared<CAP> sh;
+  for (int s = BIG ? blockIdx.x : blockIdx.y; s < b.S; s += BIG ? gridDim.x : b.S) {
+    const int q = BIG ? 0 : blockIdx.x;
+    if (MODE != 0 && b.sel_big[s] != MODE) continue;
+    const int n = b.n_full[s];
+    if (tid < R) {
+      int st = b.ring_se[s * 2 * R + tid], en = b.ring_se[s * 2 * R + R + tid];
+      if (tid == 0) st = 5;            // :392
+      if (tid == R - 1) en = n - 5;    // :393
+      sh.se[tid] = st;
+      sh.se[R + tid] = en;
     }
-    for (int a = 0; a < na; ++a) {
-      int lo = sh.se[order[a]], hi = sh.se[R + order[a]] - 1;
-      if (lo < 0 || hi >= n || lo - prev_hi <= 5) wf = 0;
-      prev_hi = hi;
+    __syncthreads();
+    if (tid == 0) {
+      // rings are independent when their active spans [start, end-1] are more than 5 points apart
+      int wf = 1, prev_hi = -100000, maxspan = 0;
+      int* order = sh.order;
+      int na = 0;
+      for (int r = 0; r < R; ++r)
+        if (sh.se[r] <= sh.se[R + r] - 1) order[na++] = r;
+      for (int a = 1; a < na; ++a) {
+        int v = order[a], c = a;
+        while (c > 0 && sh.se[order[c - 1]] > sh.se[v]) { order[c] = order[c - 1]; --c; }
+        order[c] = v;
+      }
+      for (int a = 0; a < na; ++a) {
+        int lo = sh.se[order[a]], hi = sh.se[R + order[a]] - 1;
+        if (lo < 0 || hi >= n || lo - prev_hi <= 5) wf = 0;
+        maxspan = max(maxspan, hi - lo + 1);
+        prev_hi = hi;
+      }
+      sh.wf = wf;
+      sh.loff = 0;
+      int next = MODE;
+      if (MODE == 0 && n > 0 && (!wf || maxspan > CAP)) next = 1;
+      if (MODE == 1 && n > 0 && maxspan > CAP) next = 2;
+      sh.big = next != MODE;
+      if (q == 0 && MODE != 2) b.sel_big[s] = next;
     }
-    sh.wf = wf;
-  }
-  __syncthreads();
-  if (n <= 0) {
-    if (tid < 4) b.st_cnt[(size_t)(s * R + q) * 4 + tid] = 0;
-    return;
-  }
-  if (sh.wf) {
-    select_ring(b, s, q, R, n, false, sh);
-  } else if (q == 0) {
-    for (int r = 0; r < R; ++r) select_ring(b, s, r, R, n, true, sh);
+    __syncthreads();
+    if (!sh.big) {
+      if (n <= 0) {
+        if (tid < 4) b.st_cnt[(size_t)(s * R + q) * 4 + tid] = 0;
+        if (tid == 0) b.st_loff[s * R + q] = q * kRingCap;
+      } else if (sh.wf && !BIG) {
+        select_ring<CAP, BIG>(b, s, q, R, n, false, sh, 0);
+      } else if (q == 0) {
+        for (int r = 0; r < R; ++r) select_ring<CAP, BIG>(b, s, r, R, n, true, sh, BIG ? blockIdx.x : 0);
+      }
+    }
+    __syncthreads();
+    if (!BIG) break;
   }
 }
 
@@ -620,7 +685,7 @@ __global__ __launch_bounds__(256) void k_sr_compact(SrBuffers b, SrParams p) {
       b.flat[(size_t)s * kFlatPerRing * R + off[2][r] + t] =
           pts[b.st_flat[(size_t)(s * R + r) * kFlatPerRing + t]];
     for (int t = tid; t < c[3]; t += 256)
-      b.lflat[(size_t)s * b.cap + off[3][r] + t] = b.st_lflat[(size_t)(s * R + r) * kRingCap + t];
+      b.lflat[(size_t)s * b.cap + off[3][r] + t] = b.st_lflat[(size_t)s * R * kRingCap + b.st_loff[s * R + r] + t];
   }
 }
 
@@ -654,12 +719,18 @@ void sr_alloc(SrBuffers& b, int S, int cap, int R) {
   HIPCHK(hipMalloc(&b.lflat, n * sizeof(float4)));
   HIPCHK(hipMalloc(&b.cnt, (size_t)S * 4 * sizeof(int)));
   HIPCHK(hipMalloc(&b.err, S * sizeof(int)));
+  HIPCHK(hipMalloc(&b.sel_big, S * sizeof(int)));
+  HIPCHK(hipMalloc(&b.st_loff, (size_t)S * R * sizeof(int)));
+  b.big_stride = next_pow2(cap);
+  HIPCHK(hipMalloc(&b.big_keys, (size_t)kBigSlots * b.big_stride * sizeof(uint64_t)));
+  HIPCHK(hipMalloc(&b.big_sidx, (size_t)kBigSlots * b.big_stride * sizeof(int)));
+  HIPCHK(hipMalloc(&b.big_cand, (size_t)kBigSlots * b.big_stride * sizeof(int)));
 }
 
 void sr_free(SrBuffers& b) {
   void* ptrs[] = {b.raw, b.raw_n, b.tmp_ori, b.tmp_sid, b.tilecnt, b.full, b.n_full, b.curv,
                   b.picked, b.sortind, b.label, b.ring_se, b.st_sharp, b.st_lsharp, b.st_flat,
-                  b.st_lflat, b.st_cnt, b.sharp, b.lsharp, b.flat, b.lflat, b.cnt, b.err};
+                  b.st_lflat, b.st_cnt, b.sharp, b.lsharp, b.flat, b.lflat, b.cnt, b.err, b.sel_big, b.st_loff, b.big_keys, b.big_sidx, b.big_cand};
   for (void* q : ptrs)
     if (q) HIPCHK(hipFree(q));
   b = SrBuffers();
@@ -675,7 +746,9 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
   hipLaunchKernelGGL(k_sr_features, dim3((b.cap + kFeatTile - 1) / kFeatTile, b.S), dim3(kFeatTile), 0,
                      st, b, p);
   mark("k_sr_features");
-  hipLaunchKernelGGL(k_sr_select, dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
+  hipLaunchKernelGGL((k_sr_select<2048, 0>), dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
+  hipLaunchKernelGGL((k_sr_select<kRingCap, 1>), dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
+  hipLaunchKernelGGL((k_sr_select<16, 2>), dim3(kBigSlots), dim3(kSelThreads), 0, st, b, p);
   mark("k_sr_select");
   hipLaunchKernelGGL(k_sr_compact, dim3(b.S), dim3(256), 0, st, b, p);
   mark("k_sr_compact");

@@ -67,6 +67,27 @@ def test_sr_nan_and_ragged(loam, oc, sg):
         _cmp_cloud(fg[k], fo[k], k)
 
 
+def test_sr_empty_ring(loam, oc, sg):
+    # a missing ring leaves its predecessor's end index at 0 (Q5): the ring spans overlap and the
+    # rings are selected in order by one workgroup (the dependent-ring path)
+    _, cur = sg.single_problem(0)
+    elev = np.degrees(np.arctan2(cur[:, 2], np.hypot(cur[:, 0], cur[:, 1])))
+    raw = cur[np.abs(elev - 3.0) > 0.5]
+    assert raw.shape[0] < cur.shape[0]
+    fg, fo = _sr_both(loam, oc, raw)
+    for k in ("full", "sharp", "less_sharp", "flat", "less_flat"):
+        _cmp_cloud(fg[k], fo[k], k)
+
+
+def test_sr_long_rings(loam, oc, sg):
+    # two sweeps in one message: 3600 points per ring, beyond the 2048-point fast selection kernel
+    prev, cur = sg.single_problem(0)
+    raw = np.concatenate([prev, cur])
+    fg, fo = _sr_both(loam, oc, raw, dict(max_points=80000))
+    for k in ("full", "sharp", "less_sharp", "flat", "less_flat"):
+        _cmp_cloud(fg[k], fo[k], k)
+
+
 def test_sr_stride32(loam, oc, sg):
     _, cur = sg.single_problem(0)
     raw = np.zeros((cur.shape[0], 8), np.float32)   # PointXYZI-like 32-byte records
