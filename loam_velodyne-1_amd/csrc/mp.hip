@@ -191,107 +191,157 @@ __global__ __launch_bounds__(256) void k_mp_stack(MpBuffers b, MpInput in) {
 }
 
 // ---------------------------------------------------------------- segmented VoxelGrid
+// The segmented VoxelGrid kernels run one group of G threads per segment, grid-stride over the
+// segments: G = 64 (a wave) for the many, mostly empty per-cube segments, G = 256 (the block)
+// for the few large stack segments.
+template <int G>
+struct VgGroup {
+  int g, t;  // group index in the grid, thread index in the group
+  LOAM_D VgGroup() : g((blockIdx.x * 256 + threadIdx.x) / G), t(threadIdx.x % G) {}
+  LOAM_D static int stride() { return gridDim.x * (256 / G); }
+  LOAM_D float min(float v, float* sc) {
+    if constexpr (G == 64) return wave_min_f(v);
+    else return block_reduce<256>(v, sc, [](float a, float c) { return fminf(a, c); });
+  }
+  LOAM_D float max(float v, float* sc) {
+    if constexpr (G == 64) return wave_max_f(v);
+    else return block_reduce<256>(v, sc, [](float a, float c) { return fmaxf(a, c); });
+  }
+  LOAM_D int excl_scan(int v, int* sc, int& total) {  // v in {0, 1}
+    if constexpr (G == 64) {
+      const uint64_t m = __ballot(v);
+      total = __popcll(m);
+      return __popcll(m & lanemask_lt());
+    } else {
+      return block_excl_scan<256>(v, sc, total);
+    }
+  }
+};
+
+template <int G>
 __global__ __launch_bounds__(256) void k_vg_params(VgJob j) {
-  const int s = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  const int b0 = j.begin[s], b1 = j.end[s];
-  __shared__ float red[6][4];
-  float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
-  for (int i = b0 + tid; i < b1; i += 256) {
-    const float4 a = j.in[i];
-    mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
-    mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
-  }
-  for (int d = 0; d < 3; ++d) {
-    mn[d] = wave_min_f(mn[d]);
-    mx[d] = wave_max_f(mx[d]);
-    if (lane == 0) { red[d][w] = mn[d]; red[3 + d][w] = mx[d]; }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    for (int d = 0; d < 3; ++d)
-      for (int v = 1; v < 4; ++v) { red[d][0] = fminf(red[d][0], red[d][v]); red[3 + d][0] = fmaxf(red[3 + d][0], red[3 + d][v]); }
+  __shared__ float fsc[8];
+  VgGroup<G> grp;
+  for (int s = grp.g; s < j.nseg; s += VgGroup<G>::stride()) {
+    const int b0 = j.begin[s], b1 = j.end[s];
     int* prm = j.params + (size_t)s * 8;
-    if (b1 <= b0) { prm[5] = 0; return; }
-    const float inv = 1.0f / j.leaf[s];
-    const int64_t dx = (int64_t)((red[3][0] - red[0][0]) * inv) + 1;
-    const int64_t dy = (int64_t)((red[4][0] - red[1][0]) * inv) + 1;
-    const int64_t dz = (int64_t)((red[5][0] - red[2][0]) * inv) + 1;
-    int minb[3], maxb[3];
-    for (int d = 0; d < 3; ++d) {
-      minb[d] = (int)floorf(red[d][0] * inv);
-      maxb[d] = (int)floorf(red[3 + d][0] * inv);
+    if (b1 <= b0) {
+      if (grp.t == 0) prm[5] = 0;
+      continue;
     }
-    const int divx = maxb[0] - minb[0] + 1, divy = maxb[1] - minb[1] + 1;
-    prm[0] = minb[0]; prm[1] = minb[1]; prm[2] = minb[2];
-    prm[3] = divx; prm[4] = divx * divy;
-    prm[5] = (dx * dy * dz > (int64_t)0x7fffffff) ? 1 : 0;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_vg_keys(VgJob j) {
-  const int s = blockIdx.y;
-  const int b0 = j.begin[s], b1 = j.end[s];
-  const int* prm = j.params + (size_t)s * 8;
-  const float inv = 1.0f / j.leaf[s];
-  for (int i = b0 + blockIdx.x * 256 + threadIdx.x; i < b1; i += gridDim.x * 256) {
-    uint32_t key = 0;
-    if (!prm[5]) {
+    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+    for (int i = b0 + grp.t; i < b1; i += G) {
       const float4 a = j.in[i];
-      const int i0 = (int)(floorf(a.x * inv) - (float)prm[0]);
-      const int i1 = (int)(floorf(a.y * inv) - (float)prm[1]);
-      const int i2 = (int)(floorf(a.z * inv) - (float)prm[2]);
-      key = (uint32_t)i0 + (uint32_t)i1 * (uint32_t)prm[3] + (uint32_t)i2 * (uint32_t)prm[4];
+      mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
+      mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
     }
-    j.keys[i] = key;
-    j.vals[i] = (uint32_t)i;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_vg_reduce(VgJob j) {
-  const int s = blockIdx.x, tid = threadIdx.x;
-  const int b0 = j.begin[s], b1 = j.end[s];
-  const int* prm = j.params + (size_t)s * 8;
-  __shared__ int scratch[16];
-  if (b1 <= b0) {
-    if (tid == 0) j.out_count[s] = 0;
-    return;
-  }
-  if (prm[5]) {  // "leaf size too small": output = input
-    for (int i = b0 + tid; i < b1; i += 256) j.out[i] = j.in[i];
-    if (tid == 0) j.out_count[s] = b1 - b0;
-    return;
-  }
-  int run = 0;
-  for (int base = b0; base < b1; base += 256) {
-    const int t = base + tid;
-    const int head = (t < b1 && (t == b0 || j.keys_alt[t] != j.keys_alt[t - 1])) ? 1 : 0;
-    int tot;
-    const int ex = block_excl_scan<256>(head, scratch, tot);
-    if (head) {
-      const uint32_t k = j.keys_alt[t];
-      float sx = 0, sy = 0, sz = 0, si = 0;
-      int e = t;
-      while (e < b1 && j.keys_alt[e] == k) {
-        const float4 a = j.in[j.vals_alt[e]];
-        sx += a.x; sy += a.y; sz += a.z; si += a.w;
-        ++e;
+    for (int d = 0; d < 3; ++d) {
+      mn[d] = grp.min(mn[d], fsc);
+      mx[d] = grp.max(mx[d], fsc);
+    }
+    if (grp.t == 0) {
+      const float inv = 1.0f / j.leaf[s];
+      const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
+      const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
+      const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
+      int minb[3], maxb[3];
+      for (int d = 0; d < 3; ++d) {
+        minb[d] = (int)floorf(mn[d] * inv);
+        maxb[d] = (int)floorf(mx[d] * inv);
       }
-      const float cnt = (float)(e - t);
-      j.out[b0 + run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+      const int divx = maxb[0] - minb[0] + 1, divy = maxb[1] - minb[1] + 1;
+      prm[0] = minb[0]; prm[1] = minb[1]; prm[2] = minb[2];
+      prm[3] = divx; prm[4] = divx * divy;
+      prm[5] = (dx * dy * dz > (int64_t)0x7fffffff) ? 1 : 0;
     }
-    run += tot;
   }
-  if (tid == 0) j.out_count[s] = run;
 }
 
-void vg_run(const VgJob& j, void* tmp, size_t tmp_bytes, hipStream_t st) {
+template <int G>
+__global__ __launch_bounds__(256) void k_vg_keys(VgJob j) {
+  VgGroup<G> grp;
+  for (int s = grp.g; s < j.nseg; s += VgGroup<G>::stride()) {
+    const int b0 = j.begin[s], b1 = j.end[s];
+    if (b1 <= b0) continue;
+    const int* prm = j.params + (size_t)s * 8;
+    const float inv = 1.0f / j.leaf[s];
+    const bool pass = prm[5] != 0;
+    const int m0 = prm[0], m1 = prm[1], m2 = prm[2], mul1 = prm[3], mul2 = prm[4];
+    for (int i = b0 + grp.t; i < b1; i += G) {
+      uint32_t key = 0;
+      if (!pass) {
+        const float4 a = j.in[i];
+        const int i0 = (int)(floorf(a.x * inv) - (float)m0);
+        const int i1 = (int)(floorf(a.y * inv) - (float)m1);
+        const int i2 = (int)(floorf(a.z * inv) - (float)m2);
+        key = (uint32_t)i0 + (uint32_t)i1 * (uint32_t)mul1 + (uint32_t)i2 * (uint32_t)mul2;
+      }
+      j.keys[i] = key;
+      j.vals[i] = (uint32_t)i;
+    }
+  }
+}
+
+// one output point per run of equal keys: the float mean of x, y, z, intensity summed in sorted
+// order (the reference's VoxelGrid)
+template <int G>
+__global__ __launch_bounds__(256) void k_vg_reduce(VgJob j) {
+  __shared__ int isc[16];
+  VgGroup<G> grp;
+  for (int s = grp.g; s < j.nseg; s += VgGroup<G>::stride()) {
+    const int b0 = j.begin[s], b1 = j.end[s];
+    if (b1 <= b0) {
+      if (grp.t == 0) j.out_count[s] = 0;
+      continue;
+    }
+    if (j.params[(size_t)s * 8 + 5]) {  // "leaf size too small": output = input
+      for (int i = b0 + grp.t; i < b1; i += G) j.out[i] = j.in[i];
+      if (grp.t == 0) j.out_count[s] = b1 - b0;
+      continue;
+    }
+    int run = 0;
+    for (int base = b0; base < b1; base += G) {
+      const int t = base + grp.t;
+      const uint32_t k = t < b1 ? j.keys_alt[t] : 0u;
+      const int head = (t < b1 && (t == b0 || j.keys_alt[t - 1] != k)) ? 1 : 0;
+      int tot;
+      const int ex = grp.excl_scan(head, isc, tot);
+      if (head) {
+        int e = t + 1;
+        while (e < b1 && j.keys_alt[e] == k) ++e;
+        float sx = 0, sy = 0, sz = 0, si = 0;
+        for (int mm = t; mm < e; mm += 4) {  // four independent gathers in flight per step
+          float4 a[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) a[u] = j.in[j.vals_alt[min(mm + u, e - 1)]];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (mm + u < e) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
+        }
+        const float cnt = (float)(e - t);
+        j.out[b0 + run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+      }
+      run += tot;
+    }
+    if (grp.t == 0) j.out_count[s] = run;
+  }
+}
+
+void vg_run(const VgJob& j, void* tmp, size_t tmp_bytes, hipStream_t st, bool many_small) {
   if (j.nseg == 0) return;
-  hipLaunchKernelGGL(k_vg_params, dim3(j.nseg), dim3(256), 0, st, j);
-  hipLaunchKernelGGL(k_vg_keys, dim3(8, j.nseg), dim3(256), 0, st, j);
+  const int grid = many_small ? std::min((j.nseg + 3) / 4, 4096) : std::min(j.nseg, 4096);
+  if (many_small) {
+    hipLaunchKernelGGL(k_vg_params<64>, dim3(grid), dim3(256), 0, st, j);
+    hipLaunchKernelGGL(k_vg_keys<64>, dim3(grid), dim3(256), 0, st, j);
+  } else {
+    hipLaunchKernelGGL(k_vg_params<256>, dim3(grid), dim3(256), 0, st, j);
+    hipLaunchKernelGGL(k_vg_keys<256>, dim3(grid), dim3(256), 0, st, j);
+  }
   size_t bytes = tmp_bytes;
   (void)hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
                                                     j.nseg, j.begin, j.end, 0, 32, st);
-  hipLaunchKernelGGL(k_vg_reduce, dim3(j.nseg), dim3(256), 0, st, j);
+  if (many_small) hipLaunchKernelGGL(k_vg_reduce<64>, dim3(grid), dim3(256), 0, st, j);
+  else hipLaunchKernelGGL(k_vg_reduce<256>, dim3(grid), dim3(256), 0, st, j);
 }
 
 size_t vg_tmp_bytes(int total, int nseg) {
@@ -818,13 +868,14 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_compact_table(MpBuffers b) {
   __syncthreads();
   if (tid < nv) vidx[b.valid[(size_t)p * kMaxValid + tid]] = tid;
   __syncthreads();
-  int run = 0, vpts = 0;
+  int run = 0, vpts = 0, nitems = 0;
+  int* items = b.citems + (size_t)p * 2 * kCubeNum;
   for (int kind = 0; kind < 2; ++kind)
     for (int base = 0; base < kCubeNum; base += kMpThreads) {
       const int s = base + tid;
-      int n = 0;
+      int n = 0, v = -1;
       if (s < kCubeNum) {
-        const int v = vidx[s];
+        v = vidx[s];
         n = v >= 0 ? b.vseg_cnt[p * 2 * kMaxValid + kind * kMaxValid + v] : old[s * 4 + 1 + 2 * kind] + ac[s * 2 + kind];
         if (v >= 0) vpts += n;
       }
@@ -835,9 +886,15 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_compact_table(MpBuffers b) {
         nw[s * 4 + 1 + 2 * kind] = n;
       }
       run += tot;
+      // the non-empty (kind, cube) list for the copy: kind | cube << 1 | (valid index + 1) << 14
+      int ntot;
+      const int nex = block_excl_scan<kMpThreads>(n > 0 ? 1 : 0, scratch, ntot);
+      if (n > 0) items[nitems + nex] = kind | (s << 1) | ((v + 1) << 14);
+      nitems += ntot;
     }
   vpts = block_reduce<kMpThreads>(vpts, scratch, [](int a, int c) { return a + c; });
   if (tid == 0) {
+    b.nitems[p] = nitems;
     b.istate[(size_t)p * kMpStateInts + kMiValidPts] = vpts;
     if (run > b.map_cap) b.istate[(size_t)p * kMpStateInts + kMiErr] |= ERR_CAP_MAP;
   }
@@ -853,15 +910,13 @@ __global__ __launch_bounds__(256) void k_mp_compact_copy(MpBuffers b) {
   float4* npool = b.pool + ((size_t)(1 - b.pool_cur) * b.P + p) * b.map_cap;
   const int* ao = b.app_off + (size_t)p * kCubeNum * 2;
   const float4* app = b.app + (size_t)p * b.cap_stack;
-  const int nv = b.istate[(size_t)p * kMpStateInts + kMiNValid];
-  for (int item = blockIdx.x; item < 2 * kCubeNum; item += gridDim.x) {
-    const int kind = item / kCubeNum, s = item % kCubeNum;
+  const int* items = b.citems + (size_t)p * 2 * kCubeNum;
+  const int nitems = b.nitems[p];
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const int code = items[it];
+    const int kind = code & 1, s = (code >> 1) & 8191, v = (code >> 14) - 1;
     const int n = nw[s * 4 + 1 + 2 * kind];
-    if (n == 0) continue;
     const int dst = nw[s * 4 + 2 * kind];
-    int v = -1;
-    for (int q = 0; q < nv; ++q)
-      if (b.valid[(size_t)p * kMaxValid + q] == s) v = q;
     if (v >= 0) {
       const int b0 = b.vseg_b[p * 2 * kMaxValid + kind * kMaxValid + v];
       for (int t = threadIdx.x; t < n; t += 256) npool[dst + t] = b.vout[b0 + t];
@@ -921,6 +976,8 @@ void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter
   (void)hipMalloc(&b.q_ok, Ps * sizeof(int8_t));
   (void)hipMalloc(&b.q_cf, Ps * sizeof(float4));
   (void)hipMalloc(&b.q_nn, Ps * 2 * sizeof(int4));
+  (void)hipMalloc(&b.citems, (size_t)P * 2 * kCubeNum * sizeof(int));
+  (void)hipMalloc(&b.nitems, (size_t)P * sizeof(int));
   (void)hipMalloc(&b.q_fit, Ps * 4 * sizeof(float4));
   (void)hipMalloc(&b.app_cnt, (size_t)P * kCubeNum * 2 * sizeof(int));
   (void)hipMalloc(&b.app_off, (size_t)P * kCubeNum * 2 * sizeof(int));
@@ -953,7 +1010,7 @@ void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter
 void mp_free(MpBuffers& b) {
   void* ptrs[] = {b.state, b.istate, b.slots, b.pool, b.valid, b.vpre, b.inC, b.inS, b.inF, b.in_n, b.in_pose,
                   b.stack2, b.stack, b.nstack, b.from, b.hC_start, b.hS_start, b.h_fill, b.hC_T, b.hS_T,
-                  b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
+                  b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.citems, b.nitems, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
                   b.vg_params, b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.cub_tmp, b.reg, b.nreg};
   for (void* q : ptrs)
@@ -987,7 +1044,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
   js.in = b.stack2; js.out = b.stack; js.begin = b.sseg_b; js.end = b.sseg_e; js.leaf = b.sseg_leaf;
   js.out_count = b.sseg_cnt; js.params = b.vg_params; js.keys = b.vg_k; js.keys_alt = b.vg_k2;
   js.vals = b.vg_v; js.vals_alt = b.vg_v2; js.nseg = 2 * P; js.total = P * b.cap_stack;
-  vg_run(js, b.cub_tmp, b.cub_bytes, st);
+  vg_run(js, b.cub_tmp, b.cub_bytes, st, false);
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);
   mark("k_mp_gather");
@@ -1024,7 +1081,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
   jv.in = b.vin; jv.out = b.vout; jv.begin = b.vseg_b; jv.end = b.vseg_e; jv.leaf = b.vseg_leaf;
   jv.out_count = b.vseg_cnt; jv.params = b.vg_params; jv.keys = b.vg_k; jv.keys_alt = b.vg_k2;
   jv.vals = b.vg_v; jv.vals_alt = b.vg_v2; jv.nseg = 2 * kMaxValid * P; jv.total = P * b.map_cap;
-  vg_run(jv, b.cub_tmp, b.cub_bytes, st);
+  vg_run(jv, b.cub_tmp, b.cub_bytes, st, true);
   mark("vg_cubes");
   hipLaunchKernelGGL(k_mp_compact_table, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);

@@ -74,6 +74,8 @@ struct MpBuffers {
   float4* q_fit = nullptr;    // [P][cap_stack][4] MpFit: the 5-NN a line / plane was fitted to + the fit
   // insertion / per-cube downsampling
   int* app_cnt = nullptr;     // [P][kCubeNum][2] appended points per cube
+  int* citems = nullptr;      // [P][2 * kCubeNum] non-empty (kind, cube, valid index) of the new store
+  int* nitems = nullptr;      // [P]
   int* app_off = nullptr;     // [P][kCubeNum][2]
   float4* app = nullptr;      // [P][cap_stack] stack points grouped by cube (map frame)
   float4* vin = nullptr;      // [P][map_cap] per-valid-cube DS input (old ++ appended)
