@@ -347,27 +347,39 @@ __global__ void k_od_begin(OdBuffers b, FeatView f) {
   ist[kIsRows] = 0;
 }
 
-// association (:472-527, :587-650), one wave per query: TransformToStart at the current
-// transform, exact NN through the hash, then the ring-window scans.
+// TransformToStart of every query at the current transform (:472, :587), lane per query, for
+// the association below (whose waves would otherwise each evaluate it on 64 lanes)
+__global__ __launch_bounds__(kOdThreads) void k_od_sel(OdBuffers b, FeatView f) {
+  const int p = blockIdx.y;
+  const int* ist = b.istate + (size_t)p * kOdStateInts;
+  if (!ist[kIsActive] || ist[kIsStop]) return;
+  const float* st = b.state + (size_t)p * kOdStateFloats;
+  float T[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) T[k] = st[k];
+  const int nc = f.count(p, 0), nq = nc + f.count(p, 2);
+  const int q = blockIdx.x * kOdThreads + threadIdx.x;
+  if (q >= nq) return;
+  const float4 po = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
+  b.sel[(size_t)p * b.cap_q + q] = loampose::transform_to_start(T, po);
+}
+
+// association (:472-527, :587-650), one wave per query: exact NN through the hash, then the
+// ring-window scans.
 __global__ __launch_bounds__(kOdThreads) void k_od_assoc(OdBuffers b, FeatView f, int last_buf) {
   const int p = blockIdx.y, lane = lane_id(), w = threadIdx.x >> 6;
   const int* ist = b.istate + (size_t)p * kOdStateInts;
   if (!ist[kIsActive] || ist[kIsStop]) return;
   __shared__ int cells[kOdWaves][64];
-  const float* st = b.state + (size_t)p * kOdStateFloats;
-  float T[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) T[k] = st[k];
   const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
-  const float4* sharp = f.sharp + (size_t)p * f.sharp_stride;
-  const float4* flat = f.flat + (size_t)p * f.flat_stride;
+  const float4* sel = b.sel + (size_t)p * b.cap_q;
   const size_t lp = (size_t)last_buf * b.P + p;
   const int C = b.nlast[(p * 2 + last_buf) * 2 + 0], S = b.nlast[(p * 2 + last_buf) * 2 + 1];
   const float4* CL = b.lastC + lp * b.capC;
   const float4* SL = b.lastS + lp * b.capS;
   int* ind = b.ind + (size_t)p * 3 * b.cap_q;
   for (int q = blockIdx.x * kOdWaves + w; q < nq; q += gridDim.x * kOdWaves) {
-    const float4 s4 = loampose::transform_to_start(T, q < nc ? sharp[q] : flat[q - nc]);
+    const float4 s4 = sel[q];
     int i1, i2, i3 = -1;
     if (q < nc) {
       const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
@@ -637,6 +649,7 @@ void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   (void)hipMalloc(&b.cS, (size_t)2 * P * 2 * chunks_of(b.capS) * sizeof(float4));
   (void)hipMalloc(&b.hS_T, (size_t)2 * P * sizeof(int));
   (void)hipMalloc(&b.ind, (size_t)P * 3 * b.cap_q * sizeof(int));
+  (void)hipMalloc(&b.sel, (size_t)P * b.cap_q * sizeof(float4));
   (void)hipMalloc(&b.q_cf, (size_t)P * max_iter * b.cap_q * sizeof(float4));
   (void)hipMalloc(&b.q_ok, (size_t)P * max_iter * b.cap_q * sizeof(int8_t));
   (void)hipMalloc(&b.part, (size_t)P * b.gq * 28 * sizeof(double));
@@ -651,7 +664,7 @@ void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
 void od_free(OdBuffers& b) {
   void* ptrs[] = {b.state, b.istate, b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
-                  b.ind, b.q_cf, b.q_ok, b.part};
+                  b.ind, b.sel, b.q_cf, b.q_ok, b.part};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = OdBuffers();
@@ -696,6 +709,7 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
   hipLaunchKernelGGL(k_od_begin, dim3((P + 255) / 256), dim3(256), 0, st, b, f);
   for (int it = 0; it < b.max_iter; ++it) {
     if (it % 5 == 0) {  // Q10
+      hipLaunchKernelGGL(k_od_sel, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f);
       hipLaunchKernelGGL(k_od_assoc, dim3(16, P), dim3(kOdThreads), 0, st, b, f, last_buf);
       mark("k_od_assoc");
     }

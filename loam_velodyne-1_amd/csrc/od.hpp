@@ -65,6 +65,7 @@ struct OdBuffers {
   int* hS_T = nullptr;      // [2][P]
   float4* cC = nullptr;     // [2][P][2 * chunks_of(capC)] chunk boxes of Last corner
   float4* cS = nullptr;     // [2][P][2 * chunks_of(capS)] chunk boxes of Last surf
+  float4* sel = nullptr;      // [P][cap_q] queries at the current transform (association rounds)
   int* ind = nullptr;         // [P][3][cap_q] association of every query (refreshed every 5th iteration)
   float4* q_cf = nullptr;     // [P][max_iter][cap_q] coefficients (zero when rejected)
   int8_t* q_ok = nullptr;     // [P][max_iter][cap_q] accepted flags
