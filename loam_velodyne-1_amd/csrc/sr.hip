@@ -415,6 +415,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
         const int ind = inr ? sidx[key & kPosMask] : 0;
         const bool elig = inr && D(key_curv(key)) > 0.1;
         uint64_t remaining = __ballot(elig);
+        if (remaining != __ballot(inr)) done = true;  // sorted: no eligible point below this chunk
         while (remaining) {
           const bool cand_ok = elig && ((remaining >> lane) & 1ull) && (pk[ind - wlo] & 1) == 0;
           const uint64_t m = __ballot(cand_ok);
@@ -449,6 +450,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
         const int ind = inr ? sidx[key & kPosMask] : 0;
         const bool elig = inr && D(key_curv(key)) < 0.1;
         uint64_t remaining = __ballot(elig);
+        const bool last = remaining != __ballot(inr);  // sorted: no eligible point above this chunk
         while (remaining) {
           const bool cand_ok = elig && ((remaining >> lane) & 1ull) && (pk[ind - wlo] & 1) == 0;
           const uint64_t m = __ballot(cand_ok);
@@ -468,6 +470,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
           __builtin_amdgcn_wave_barrier();
           remaining &= ~((2ull << f) - 1ull);
         }
+        if (last) done = true;
       }
       __threadfence_block();
       __builtin_amdgcn_wave_barrier();
