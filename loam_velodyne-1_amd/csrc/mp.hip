@@ -438,6 +438,59 @@ LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t) {
 
 constexpr int kMpQueryThreads = 256;
 
+// The same search with the lane's work flattened: first every cell the lane may need (box
+// distance below 1 m and not above the seeded 5th distance) is listed with its bucket range — 27
+// independent loads in flight — then one loop runs over the concatenated candidates, so a wave
+// iterates max(candidates per lane) instead of the union of its lanes' cells x buckets.  `lst` =
+// the lane's LDS column (stride kMpQueryThreads).  Ranges are packed start:19 | count:13; a lane
+// whose ranges do not fit falls back to knn5.
+LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5& t, uint32_t* lst) {
+  if (T <= 0) return;
+  const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
+  const float gxl = q.x - (float)cx, gyl = q.y - (float)cy, gzl = q.z - (float)cz;
+  const float gxh = (float)(cx + 1) - q.x, gyh = (float)(cy + 1) - q.y, gzh = (float)(cz + 1) - q.z;
+  const float bound = t.d[4];
+  int n = 0, total = 0;
+  bool fits = true;
+#pragma unroll
+  for (int o = 0; o < 27; ++o) {
+    const int c = kCellOrder[o];
+    const int dx = c % 3 - 1, dy = (c / 3) % 3 - 1, dz = c / 9 - 1;
+    const float gx = dx < 0 ? gxl : (dx > 0 ? gxh : 0.0f);
+    const float gy = dy < 0 ? gyl : (dy > 0 ? gyh : 0.0f);
+    const float gz = dz < 0 ? gzl : (dz > 0 ? gzh : 0.0f);
+    const float bd = sqdist(gx, gy, gz, 0.0f, 0.0f, 0.0f);
+    if (bd < 1.0f && bd <= bound) {
+      const uint32_t h = cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1);
+      const int b0 = start[h], cnt = start[h + 1] - b0;
+      if (cnt > 0) {
+        if (b0 >= (1 << 19) || cnt >= (1 << 13)) fits = false;
+        lst[n * kMpQueryThreads] = (uint32_t)b0 | ((uint32_t)cnt << 19);
+        ++n;
+        total += cnt;
+      }
+    }
+  }
+  if (!fits) {
+    knn5(start, hp, T, q, t);
+    return;
+  }
+  int ci = 0, left = 0, pos = 0;
+  for (int k = 0; k < total; ++k) {
+    if (left == 0) {
+      const uint32_t e = lst[ci * kMpQueryThreads];
+      ++ci;
+      pos = (int)(e & ((1u << 19) - 1));
+      left = (int)(e >> 19);
+    }
+    const float4 a = hp[pos];
+    ++pos;
+    --left;
+    top5_offer(t, sqdist(a.x, a.y, a.z, q.x, q.y, q.z), __builtin_bit_cast(int, a.w));
+  }
+}
+
+
 }  // namespace
 
 __global__ void k_mp_lm_begin(MpBuffers b) {
@@ -476,6 +529,8 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_nn(MpBuffers b) {
   const float4* hsp = b.hS_pts + (size_t)p * b.map_cap;
   const int TC = b.hC_T[p], TS = b.hS_T[p];
   int4* qnn = b.q_nn + (size_t)p * b.cap_stack * 2;
+  __shared__ uint32_t lists[27 * kMpQueryThreads];
+  uint32_t* lst = lists + tid;
   const bool first = ist[kMiIters] == 0;
   const float4* fromC = b.from + (size_t)p * b.map_cap;
   const float4* fromS = fromC + b.nfrom[p * 2 + 0];
@@ -497,8 +552,8 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_nn(MpBuffers b) {
           top5_offer(t, sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z), prev[k]);
         }
     }
-    if (corner) knn5(hcs, hcp, TC, sel, t);
-    else knn5(hss, hsp, TS, sel, t);
+    if (corner) knn5_flat(hcs, hcp, TC, sel, t, lst);
+    else knn5_flat(hss, hsp, TS, sel, t, lst);
     qnn[2 * q] = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
     qnn[2 * q + 1] = make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0);
   }
