@@ -476,17 +476,23 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
     return;
   }
   int ci = 0, left = 0, pos = 0;
-  for (int k = 0; k < total; ++k) {
+  auto next = [&]() {  // index of the lane's next candidate
     if (left == 0) {
       const uint32_t e = lst[ci * kMpQueryThreads];
       ++ci;
       pos = (int)(e & ((1u << 19) - 1));
       left = (int)(e >> 19);
     }
-    const float4 a = hp[pos];
-    ++pos;
     --left;
-    top5_offer(t, sqdist(a.x, a.y, a.z, q.x, q.y, q.z), __builtin_bit_cast(int, a.w));
+    return pos++;
+  };
+  for (int k = 0; k < total; k += 2) {  // two independent gathers in flight per step
+    const int i0 = next();
+    const bool two = k + 1 < total;
+    const int i1 = two ? next() : i0;
+    const float4 a0 = hp[i0], a1 = hp[i1];
+    top5_offer(t, sqdist(a0.x, a0.y, a0.z, q.x, q.y, q.z), __builtin_bit_cast(int, a0.w));
+    if (two) top5_offer(t, sqdist(a1.x, a1.y, a1.z, q.x, q.y, q.z), __builtin_bit_cast(int, a1.w));
   }
 }
 
