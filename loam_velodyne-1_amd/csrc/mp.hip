@@ -486,13 +486,16 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
     --left;
     return pos++;
   };
-  for (int k = 0; k < total; k += 2) {  // two independent gathers in flight per step
-    const int i0 = next();
-    const bool two = k + 1 < total;
-    const int i1 = two ? next() : i0;
-    const float4 a0 = hp[i0], a1 = hp[i1];
-    top5_offer(t, sqdist(a0.x, a0.y, a0.z, q.x, q.y, q.z), __builtin_bit_cast(int, a0.w));
-    if (two) top5_offer(t, sqdist(a1.x, a1.y, a1.z, q.x, q.y, q.z), __builtin_bit_cast(int, a1.w));
+  for (int k = 0; k < total; k += 4) {  // four independent gathers in flight per step
+    int idx[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) idx[u] = k + u < total ? next() : idx[0];
+    float4 a[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] = hp[idx[u]];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (k + u < total) top5_offer(t, sqdist(a[u].x, a[u].y, a[u].z, q.x, q.y, q.z), __builtin_bit_cast(int, a[u].w));
   }
 }
 
