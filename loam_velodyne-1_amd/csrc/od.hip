@@ -601,13 +601,14 @@ __global__ __launch_bounds__(256) void k_od_end(OdBuffers b, FeatView f, int dst
   float4* oc = b.lastC + ((size_t)dst * b.P + p) * b.capC;
   float4* os = b.lastS + ((size_t)dst * b.P + p) * b.capS;
   float4* ofl = b.fullEnd + ((size_t)dst * b.P + p) * b.capS;
+  const loampose::EndRot er = loampose::end_rot(t, imu);
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     float4 a;
     float4* o;
     if (i < cl) { a = f.lsharp[(size_t)p * f.lsharp_stride + i]; o = oc + i; }
     else if (i < cl + cf) { a = f.lflat[(size_t)p * f.lflat_stride + (i - cl)]; o = os + (i - cl); }
     else { a = f.full[(size_t)p * f.full_stride + (i - cl - cf)]; o = ofl + (i - cl - cf); }
-    *o = mode == 0 ? a : loampose::transform_to_end(t, imu, a);
+    *o = mode == 0 ? a : loampose::transform_to_end(t, imu, er, a, mode == 1);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     b.nlast[(p * 2 + dst) * 2 + 0] = cl;

@@ -40,43 +40,78 @@ LOAM_HD float4 transform_to_start(const float* t, float4 pi) {
   return o;
 }
 
-LOAM_HD float4 transform_to_end(const float* t, const Imu& m, float4 pi) {
+// the trigonometry of TransformToEnd that does not depend on the point: the transform's own
+// angles (second rotation) and the six IMU angles, evaluated once per thread
+struct EndRot {
+  double crx, srx, cry, sry, crz, srz;
+  double crs, srs, cps, sps, cys, sys, cyl, syl, cpl, spl, crl, srl;  // roll/pitch/yaw Start, yaw/pitch/roll Last
+};
+LOAM_HD EndRot end_rot(const float* t, const Imu& m) {
+  EndRot e;
+  e.crx = dcos(t[0]); e.srx = dsin(t[0]);
+  e.cry = dcos(t[1]); e.sry = dsin(t[1]);
+  e.crz = dcos(t[2]); e.srz = dsin(t[2]);
+  e.crs = dcos(m.rollStart); e.srs = dsin(m.rollStart);
+  e.cps = dcos(m.pitchStart); e.sps = dsin(m.pitchStart);
+  e.cys = dcos(m.yawStart); e.sys = dsin(m.yawStart);
+  e.cyl = dcos(m.yawLast); e.syl = dsin(m.yawLast);
+  e.cpl = dcos(m.pitchLast); e.spl = dsin(m.pitchLast);
+  e.crl = dcos(m.rollLast); e.srl = dsin(m.rollLast);
+  return e;
+}
+
+// TransformToEnd (:126-194).  `zero`: the transform is known to be all +0, so for s >= 0 the
+// scaled angles are +0 and their sines / cosines exactly 0 / 1 (no library calls).
+LOAM_HD float4 transform_to_end(const float* t, const Imu& m, const EndRot& e, float4 pi, bool zero) {
   float s = 10 * (pi.w - (int)pi.w);
   float rx = s * t[0], ry = s * t[1], rz = s * t[2];
   float tx = s * t[3], ty = s * t[4], tz = s * t[5];
-  float x1 = (float)(dcos(rz) * D(pi.x - tx) + dsin(rz) * D(pi.y - ty));
-  float y1 = (float)(-dsin(rz) * D(pi.x - tx) + dcos(rz) * D(pi.y - ty));
+  double cx, sx, cy, sy, cz, sz;
+  if (zero && s >= 0) {
+    cx = cy = cz = 1.0;
+    sx = sy = sz = 0.0;
+  } else {
+    cx = dcos(rx); sx = dsin(rx);
+    cy = dcos(ry); sy = dsin(ry);
+    cz = dcos(rz); sz = dsin(rz);
+  }
+  float x1 = (float)(cz * D(pi.x - tx) + sz * D(pi.y - ty));
+  float y1 = (float)(-sz * D(pi.x - tx) + cz * D(pi.y - ty));
   float z1 = (pi.z - tz);
-  float y2 = (float)(dcos(rx) * D(y1) + dsin(rx) * D(z1));
-  float z2 = (float)(-dsin(rx) * D(y1) + dcos(rx) * D(z1));
-  float x3 = (float)(dcos(ry) * D(x1) - dsin(ry) * D(z2));
+  float y2 = (float)(cx * D(y1) + sx * D(z1));
+  float z2 = (float)(-sx * D(y1) + cx * D(z1));
+  float x3 = (float)(cy * D(x1) - sy * D(z2));
   float y3 = y2;
-  float z3 = (float)(dsin(ry) * D(x1) + dcos(ry) * D(z2));
-  rx = t[0]; ry = t[1]; rz = t[2]; tx = t[3]; ty = t[4]; tz = t[5];
-  float x4 = (float)(dcos(ry) * D(x3) + dsin(ry) * D(z3));
-  float z4 = (float)(-dsin(ry) * D(x3) + dcos(ry) * D(z3));
-  float y5 = (float)(dcos(rx) * D(y3) - dsin(rx) * D(z4));
-  float z5 = (float)(dsin(rx) * D(y3) + dcos(rx) * D(z4));
-  float x6 = (float)(dcos(rz) * D(x4) - dsin(rz) * D(y5) + D(tx));
-  float y6 = (float)(dsin(rz) * D(x4) + dcos(rz) * D(y5) + D(ty));
+  float z3 = (float)(sy * D(x1) + cy * D(z2));
+  tx = t[3]; ty = t[4]; tz = t[5];
+  float x4 = (float)(e.cry * D(x3) + e.sry * D(z3));
+  float z4 = (float)(-e.sry * D(x3) + e.cry * D(z3));
+  float y5 = (float)(e.crx * D(y3) - e.srx * D(z4));
+  float z5 = (float)(e.srx * D(y3) + e.crx * D(z4));
+  float x6 = (float)(e.crz * D(x4) - e.srz * D(y5) + D(tx));
+  float y6 = (float)(e.srz * D(x4) + e.crz * D(y5) + D(ty));
   float z6 = z5 + tz;
-  float x7 = (float)(dcos(m.rollStart) * D(x6 - m.shiftX) - dsin(m.rollStart) * D(y6 - m.shiftY));
-  float y7 = (float)(dsin(m.rollStart) * D(x6 - m.shiftX) + dcos(m.rollStart) * D(y6 - m.shiftY));
+  float x7 = (float)(e.crs * D(x6 - m.shiftX) - e.srs * D(y6 - m.shiftY));
+  float y7 = (float)(e.srs * D(x6 - m.shiftX) + e.crs * D(y6 - m.shiftY));
   float z7 = z6 - m.shiftZ;
-  float y8 = (float)(dcos(m.pitchStart) * D(y7) - dsin(m.pitchStart) * D(z7));
-  float z8 = (float)(dsin(m.pitchStart) * D(y7) + dcos(m.pitchStart) * D(z7));
-  float x9 = (float)(dcos(m.yawStart) * D(x7) + dsin(m.yawStart) * D(z8));
-  float z9 = (float)(-dsin(m.yawStart) * D(x7) + dcos(m.yawStart) * D(z8));
-  float x10 = (float)(dcos(m.yawLast) * D(x9) - dsin(m.yawLast) * D(z9));
-  float z10 = (float)(dsin(m.yawLast) * D(x9) + dcos(m.yawLast) * D(z9));
-  float y11 = (float)(dcos(m.pitchLast) * D(y8) + dsin(m.pitchLast) * D(z10));
-  float z11 = (float)(-dsin(m.pitchLast) * D(y8) + dcos(m.pitchLast) * D(z10));
+  float y8 = (float)(e.cps * D(y7) - e.sps * D(z7));
+  float z8 = (float)(e.sps * D(y7) + e.cps * D(z7));
+  float x9 = (float)(e.cys * D(x7) + e.sys * D(z8));
+  float z9 = (float)(-e.sys * D(x7) + e.cys * D(z8));
+  float x10 = (float)(e.cyl * D(x9) - e.syl * D(z9));
+  float z10 = (float)(e.syl * D(x9) + e.cyl * D(z9));
+  float y11 = (float)(e.cpl * D(y8) + e.spl * D(z10));
+  float z11 = (float)(-e.spl * D(y8) + e.cpl * D(z10));
   float4 o;
-  o.x = (float)(dcos(m.rollLast) * D(x10) + dsin(m.rollLast) * D(y11));
-  o.y = (float)(-dsin(m.rollLast) * D(x10) + dcos(m.rollLast) * D(y11));
+  o.x = (float)(e.crl * D(x10) + e.srl * D(y11));
+  o.y = (float)(-e.srl * D(x10) + e.crl * D(y11));
   o.z = z11;
   o.w = (float)(int)pi.w;
   return o;
+}
+
+LOAM_HD float4 transform_to_end(const float* t, const Imu& m, float4 pi) {
+  return transform_to_end(t, m, end_rot(t, m), pi, false);
 }
 
 LOAM_HD void plugin_imu_rotation(float bcx, float bcy, float bcz, float blx, float bly, float blz,
