@@ -1117,6 +1117,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
   hc.count = b.nfrom; hc.count_stride_bytes = 2 * sizeof(int);
   hc.start = b.hC_start; hc.fill = b.h_fill; hc.out = b.hC_pts; hc.tsize = b.hC_T; hc.tmax = b.tmax;
   hc.inv_h = 1.0f;
+  hc.shift = 0;  // the 5-NN search scans whole buckets: keep them to single cells
   hc.chunks = nullptr;
   hipLaunchKernelGGL(k_hash_build, dim3(P), dim3(256), 0, st, hc);
   HashJob hs = hc;

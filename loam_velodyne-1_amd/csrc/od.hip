@@ -43,50 +43,48 @@ LOAM_D loampose::Imu load_imu(const float* st) {
 }  // namespace
 
 // ---------------------------------------------------------------- voxel hash build
-// One workgroup per cloud: T = pow2 >= count (clamped to [64, tmax]) buckets, CSR start[T+1],
-// points re-ordered by bucket with their source index in .w (bit pattern).
-__global__ __launch_bounds__(256) void k_hash_build(HashJob j) {
-  const int p = blockIdx.x, tid = threadIdx.x;
-  const int n = *(const int*)((const char*)j.count + (size_t)p * j.count_stride_bytes);
-  const float4* pts = j.pts + (size_t)p * j.pts_stride + (j.pts_off ? j.pts_off[p * j.pts_off_stride] : 0);
-  int* start = j.start + (size_t)p * (j.tmax + 1);
-  int* fill = j.fill + (size_t)p * j.tmax;
-  float4* out = j.out + (size_t)p * j.pts_stride;
-  __shared__ int scratch[16];
-  __shared__ int sh_T;
-  if (tid == 0) {
-    int T = next_pow2(n > 64 ? n : 64);
-    if (T > j.tmax) T = j.tmax;
-    sh_T = T;
-    j.tsize[p] = T;
-  }
-  __syncthreads();
-  const int T = sh_T;
+// One workgroup per cloud: T = pow2 >= count >> shift (clamped to [64, tmax]) buckets — a 1 m
+// cell holds several points, so even two points per bucket (shift 1) leaves distinct neighbouring
+// cells rarely sharing a bucket — CSR start[T+1], points re-ordered by bucket with their source index in .w
+// (bit pattern).  Bucket counters live in LDS up to kHashLds buckets, in global memory beyond.
+constexpr int kHashLds = 8192;
+
+// counting sort of the cloud's points by bucket; fill = LDS (LDS true) or this cloud's global
+// counters (read back with atomic loads: the counts were made by L2 atomics)
+template <bool LDS>
+LOAM_D void hash_sort(const HashJob& j, const float4* pts, int n, int T, int* start, float4* out, int* fill,
+                      int* scratch) {
+  const int tid = threadIdx.x;
+  auto ld = [&](int b) {
+    if constexpr (LDS) return fill[b];
+    else return __hip_atomic_load(&fill[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
   for (int b = tid; b < T; b += 256) fill[b] = 0;
-  __threadfence();
+  if (!LDS) __threadfence();
   __syncthreads();
   for (int i = tid; i < n; i += 256) {
     const float4 a = pts[i];
     uint32_t h = cell_hash(cell_of(a.x, j.inv_h), cell_of(a.y, j.inv_h), cell_of(a.z, j.inv_h)) & (T - 1);
     atomicAdd(&fill[h], 1);
   }
-  __threadfence();
+  if (!LDS) __threadfence();
   __syncthreads();
   // exclusive scan of fill[0..T) into start: contiguous chunk per thread
   const int per = (T + 255) / 256;
   const int b0 = tid * per, b1 = min(T, b0 + per);
   int local = 0;
-  for (int b = b0; b < b1; ++b) local += __hip_atomic_load(&fill[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int b = b0; b < b1; ++b) local += ld(b);
   int tot;
   int run = block_excl_scan<256>(local, scratch, tot);
   for (int b = b0; b < b1; ++b) {
-    int c = __hip_atomic_load(&fill[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int c = ld(b);
     start[b] = run;
-    __hip_atomic_store(&fill[b], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (LDS) fill[b] = run;
+    else __hip_atomic_store(&fill[b], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     run += c;
   }
   if (tid == 0) start[T] = tot;
-  __threadfence();
+  if (!LDS) __threadfence();
   __syncthreads();
   for (int i = tid; i < n; i += 256) {
     const float4 a = pts[i];
@@ -94,6 +92,22 @@ __global__ __launch_bounds__(256) void k_hash_build(HashJob j) {
     int pos = atomicAdd(&fill[h], 1);
     out[pos] = make_float4(a.x, a.y, a.z, __int_as_float(i));
   }
+}
+
+__global__ __launch_bounds__(256) void k_hash_build(HashJob j) {
+  const int p = blockIdx.x, tid = threadIdx.x;
+  const int n = *(const int*)((const char*)j.count + (size_t)p * j.count_stride_bytes);
+  const float4* pts = j.pts + (size_t)p * j.pts_stride + (j.pts_off ? j.pts_off[p * j.pts_off_stride] : 0);
+  int* start = j.start + (size_t)p * (j.tmax + 1);
+  float4* out = j.out + (size_t)p * j.pts_stride;
+  __shared__ int scratch[16];
+  __shared__ int lfill[kHashLds];
+  const int m = n >> j.shift;
+  int T = next_pow2(m > 64 ? m : 64);
+  if (T > j.tmax) T = j.tmax;
+  if (tid == 0) j.tsize[p] = T;
+  if (T <= kHashLds) hash_sort<true>(j, pts, n, T, start, out, lfill, scratch);
+  else hash_sort<false>(j, pts, n, T, start, out, j.fill + (size_t)p * j.tmax, scratch);
   if (j.chunks) {  // one wave per 64-point chunk of the source order
     const int lane = lane_id(), w = tid >> 6;
     const int nch = (n + kChunk - 1) / kChunk;
@@ -686,6 +700,7 @@ void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
   jc.tsize = b.hC_T + buf * b.P;
   jc.tmax = b.tC;
   jc.inv_h = 1.0f;
+  jc.shift = 1;
   jc.chunks = b.cC + (size_t)buf * b.P * 2 * chunks_of(b.capC);
   hipLaunchKernelGGL(k_hash_build, dim3(b.P), dim3(256), 0, st, jc);
   HashJob js = jc;

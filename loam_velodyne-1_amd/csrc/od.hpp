@@ -42,6 +42,7 @@ struct HashJob {
   int* tsize;           // [P] table size used
   int tmax;
   float inv_h;
+  int shift;            // T = pow2 >= count >> shift
   float4* chunks;       // optional [P][2 * chunks_of(pts_stride)]: per 64-point chunk of the source
                         // order, (min x, y, z, min ring) and (max x, y, z, max ring)
 };
