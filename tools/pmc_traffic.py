@@ -20,11 +20,21 @@ def short(name):
 
 
 def load(path):
-    agg = collections.defaultdict(lambda: [0.0, 0])
+    """{kernel: [total KiB, launches]}; template instantiations of one kernel (launched together,
+    timed as one by bench.py) are summed per launch"""
+    inst = collections.defaultdict(lambda: [0.0, 0])
     for r in csv.DictReader(open(path)):
         k = short(r["Kernel_Name"])
-        agg[k][0] += float(r["Counter_Value"])
-        agg[k][1] += 1
+        inst[k][0] += float(r["Counter_Value"])
+        inst[k][1] += 1
+    agg = collections.defaultdict(lambda: [0.0, 0])
+    for k, (v, n) in inst.items():
+        base = k.split("<")[0]
+        agg[base][0] += v / max(n, 1)   # per launch of this instantiation
+        agg[base][1] = 1
+    for k in agg:                       # report launches of the first instantiation seen
+        agg[k][1] = max(n for kk, (v, n) in inst.items() if kk.split("<")[0] == k)
+        agg[k][0] *= agg[k][1]
     return agg
 
 
