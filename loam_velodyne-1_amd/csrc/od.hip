@@ -495,32 +495,39 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows(OdBuffers b, FeatView f,
 #pragma unroll
   for (int k = 0; k < 28; ++k) acc[k] = 0.0;
   if (q < nq) {
+    // the coefficient-free factors of each Jacobian entry (:714-753): every entry is
+    // (e0)*coeff.x + (e1)*coeff.y + (e2)*coeff.z with e depending on the raw point and the current
+    // transform only, so they are evaluated once per query, in the reference's expression order
+    const float e00 = (-sw * crx * sry * srz * po.x + sw * crx * crz * sry * po.y + sw * srx * sry * po.z +
+                       sw * tx * crx * sry * srz - sw * ty * crx * crz * sry - sw * tz * srx * sry);
+    const float e01 = (sw * srx * srz * po.x - sw * crz * srx * po.y + sw * crx * po.z + sw * ty * crz * srx -
+                       sw * tz * crx - sw * tx * srx * srz);
+    const float e02 = (sw * crx * cry * srz * po.x - sw * crx * cry * crz * po.y - sw * cry * srx * po.z +
+                       sw * tz * cry * srx + sw * ty * crx * cry * crz - sw * tx * crx * cry * srz);
+    const float e10 = ((-sw * crz * sry - sw * cry * srx * srz) * po.x + (sw * cry * crz * srx - sw * sry * srz) * po.y -
+                       sw * crx * cry * po.z + tx * (sw * crz * sry + sw * cry * srx * srz) +
+                       ty * (sw * sry * srz - sw * cry * crz * srx) + sw * tz * crx * cry);
+    const float e12 = ((sw * cry * crz - sw * srx * sry * srz) * po.x + (sw * cry * srz + sw * crz * srx * sry) * po.y -
+                       sw * crx * sry * po.z + sw * tz * crx * sry - ty * (sw * cry * srz + sw * crz * srx * sry) -
+                       tx * (sw * cry * crz - sw * srx * sry * srz));
+    const float e20 = ((-sw * cry * srz - sw * crz * srx * sry) * po.x + (sw * cry * crz - sw * srx * sry * srz) * po.y +
+                       tx * (sw * cry * srz + sw * crz * srx * sry) - ty * (sw * cry * crz - sw * srx * sry * srz));
+    const float e21 = (-sw * crx * crz * po.x - sw * crx * srz * po.y + sw * ty * crx * srz + sw * tx * crx * crz);
+    const float e22 = ((sw * cry * crz * srx - sw * sry * srz) * po.x + (sw * crz * sry + sw * cry * srx * srz) * po.y +
+                       tx * (sw * sry * srz - sw * cry * crz * srx) - ty * (sw * crz * sry + sw * cry * srx * srz));
+    const float e30 = -sw * (cry * crz - srx * sry * srz), e31 = sw * crx * srz, e32 = sw * (crz * sry + cry * srx * srz);
+    const float e40 = -sw * (cry * srz + crz * srx * sry), e41 = sw * crx * crz, e42 = sw * (sry * srz - cry * crz * srx);
+    const float e50 = sw * crx * sry, e51 = sw * srx, e52 = sw * crx * cry;
     for (int it = 0; it <= iter; ++it) {
-      if (!qok[(size_t)it * b.cap_q + q]) continue;
+      // a rejected correspondence has a zero coefficient and adds exact zeros
       const float4 c4 = qcf[(size_t)it * b.cap_q + q];
       float a[6];
-      a[0] = (-sw * crx * sry * srz * po.x + sw * crx * crz * sry * po.y + sw * srx * sry * po.z +
-              sw * tx * crx * sry * srz - sw * ty * crx * crz * sry - sw * tz * srx * sry) * c4.x +
-             (sw * srx * srz * po.x - sw * crz * srx * po.y + sw * crx * po.z + sw * ty * crz * srx -
-              sw * tz * crx - sw * tx * srx * srz) * c4.y +
-             (sw * crx * cry * srz * po.x - sw * crx * cry * crz * po.y - sw * cry * srx * po.z +
-              sw * tz * cry * srx + sw * ty * crx * cry * crz - sw * tx * crx * cry * srz) * c4.z;
-      a[1] = ((-sw * crz * sry - sw * cry * srx * srz) * po.x + (sw * cry * crz * srx - sw * sry * srz) * po.y -
-              sw * crx * cry * po.z + tx * (sw * crz * sry + sw * cry * srx * srz) +
-              ty * (sw * sry * srz - sw * cry * crz * srx) + sw * tz * crx * cry) * c4.x +
-             ((sw * cry * crz - sw * srx * sry * srz) * po.x + (sw * cry * srz + sw * crz * srx * sry) * po.y -
-              sw * crx * sry * po.z + sw * tz * crx * sry - ty * (sw * cry * srz + sw * crz * srx * sry) -
-              tx * (sw * cry * crz - sw * srx * sry * srz)) * c4.z;
-      a[2] = ((-sw * cry * srz - sw * crz * srx * sry) * po.x + (sw * cry * crz - sw * srx * sry * srz) * po.y +
-              tx * (sw * cry * srz + sw * crz * srx * sry) - ty * (sw * cry * crz - sw * srx * sry * srz)) * c4.x +
-             (-sw * crx * crz * po.x - sw * crx * srz * po.y + sw * ty * crx * srz + sw * tx * crx * crz) * c4.y +
-             ((sw * cry * crz * srx - sw * sry * srz) * po.x + (sw * crz * sry + sw * cry * srx * srz) * po.y +
-              tx * (sw * sry * srz - sw * cry * crz * srx) - ty * (sw * crz * sry + sw * cry * srx * srz)) * c4.z;
-      a[3] = -sw * (cry * crz - srx * sry * srz) * c4.x + sw * crx * srz * c4.y -
-             sw * (crz * sry + cry * srx * srz) * c4.z;
-      a[4] = -sw * (cry * srz + crz * srx * sry) * c4.x - sw * crx * crz * c4.y -
-             sw * (sry * srz - cry * crz * srx) * c4.z;
-      a[5] = sw * crx * sry * c4.x - sw * srx * c4.y - sw * crx * cry * c4.z;
+      a[0] = e00 * c4.x + e01 * c4.y + e02 * c4.z;
+      a[1] = e10 * c4.x + e12 * c4.z;
+      a[2] = e20 * c4.x + e21 * c4.y + e22 * c4.z;
+      a[3] = e30 * c4.x + e31 * c4.y - e32 * c4.z;
+      a[4] = e40 * c4.x - e41 * c4.y - e42 * c4.z;
+      a[5] = e50 * c4.x - e51 * c4.y - e52 * c4.z;
       const float bb = (float)(-0.05 * D(c4.w));
       int k = 0;
 #pragma unroll
@@ -529,7 +536,7 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows(OdBuffers b, FeatView f,
         for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
 #pragma unroll
       for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
-      acc[27] += 1.0;
+      acc[27] += qok[(size_t)it * b.cap_q + q] ? 1.0 : 0.0;
     }
   }
 #pragma unroll
