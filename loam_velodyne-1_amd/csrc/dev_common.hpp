@@ -152,6 +152,66 @@ LOAM_HD uint32_t cell_hash(int ix, int iy, int iz) {
 LOAM_HD int cell_of(float v, float inv_h) { return (int)floorf(v * inv_h); }
 
 
+// ------------------------------------------------------------------ glibc-identical sinf / cosf
+// scanRegistration's IMU de-skew calls std::sin / std::cos on floats (src/scanRegistration.cpp:51-53,
+// :111-179), which glibc (>= 2.28) evaluates in double with a degree-4/3 polynomial after a
+// 2/pi range reduction, the FMA build on FMA hardware (ARM optimized-routines sincosf).  This is a
+// restatement of that algorithm with the FMAs placed as that build has them; tests/sincosf_check.cpp
+// compares it with the host's glibc on every 3rd float of |x| < 120 (0 mismatches).  Arguments
+// beyond 120 (never produced by the IMU angles) fall back to the double functions.
+struct SinCosTab {
+  double hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3;
+};
+LOAM_HD const SinCosTab& sincos_tab(int k) {
+  static constexpr SinCosTab t[2] = {
+      {0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, 0x1p0, -0x1.ffffffd0c621cp-2, 0x1.55553e1068f19p-5,
+       -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16, -0x1.555545995a603p-3, 0x1.1107605230bc4p-7,
+       -0x1.994eb3774cf24p-13},
+      {0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, -0x1p0, 0x1.ffffffd0c621cp-2, -0x1.55553e1068f19p-5,
+       0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16, -0x1.555545995a603p-3, 0x1.1107605230bc4p-7,
+       -0x1.994eb3774cf24p-13}};
+  return t[k];
+}
+LOAM_HD uint32_t sc_abstop12(float x) { return (__builtin_bit_cast(uint32_t, x) >> 20) & 0x7ff; }
+LOAM_HD float sincosf_poly(double x, double x2, const SinCosTab& p, int n) {
+  if ((n & 1) == 0) {
+    const double x3 = x * x2, s1 = fma(x2, p.s3, p.s2), x7 = x3 * x2, s = fma(x3, p.s1, x);
+    return (float)fma(x7, s1, s);
+  }
+  const double x4 = x2 * x2, c2 = fma(x2, p.c4, p.c3), c1 = fma(x2, p.c1, p.c0), x6 = x4 * x2;
+  const double c = fma(x4, p.c2, c1);
+  return (float)fma(x6, c2, c);
+}
+LOAM_HD double sincosf_reduce(double x, int& n) {
+  const double r = x * sincos_tab(0).hpi_inv;
+  n = ((int32_t)r + 0x800000) >> 24;
+  return fma(-(double)n, sincos_tab(0).hpi, x);
+}
+LOAM_HD float sinf_glibc(float y) {
+  double x = y;
+  if (sc_abstop12(y) < sc_abstop12(0x1.921FB6p-1f)) {
+    if (sc_abstop12(y) < sc_abstop12(0x1p-12f)) return y;
+    return sincosf_poly(x, x * x, sincos_tab(0), 0);
+  }
+  if (!(sc_abstop12(y) < sc_abstop12(120.0f))) return (float)sin((double)y);
+  int n;
+  x = sincosf_reduce(x, n);
+  const double s = (n & 3) == 1 || (n & 3) == 2 ? -1.0 : 1.0;
+  return sincosf_poly(x * s, x * x, sincos_tab((n & 2) ? 1 : 0), n);
+}
+LOAM_HD float cosf_glibc(float y) {
+  double x = y;
+  if (sc_abstop12(y) < sc_abstop12(0x1.921FB6p-1f)) {
+    if (sc_abstop12(y) < sc_abstop12(0x1p-12f)) return 1.0f;
+    return sincosf_poly(x, x * x, sincos_tab(0), 1);
+  }
+  if (!(sc_abstop12(y) < sc_abstop12(120.0f))) return (float)cos((double)y);
+  int n;
+  x = sincosf_reduce(x, n);
+  const double s = (n & 3) == 1 || (n & 3) == 2 ? -1.0 : 1.0;
+  return sincosf_poly(x * s, x * x, sincos_tab((n & 2) ? 1 : 0), n ^ 1);
+}
+
 // ------------------------------------------------------------------ glibc-identical atan2f
 // scanRegistration's float atan2 (`using std::atan2`, src/scanRegistration.cpp:53) resolves to
 // glibc's atan2f, the fdlibm single-precision algorithm (sysdeps/ieee754/flt-32/e_atan2f.c,

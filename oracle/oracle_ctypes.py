@@ -49,7 +49,9 @@ class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "n_raw", "n_ring", "n_sharp", "n_less_sharp", "n_flat", "n_less_flat",
         "od_iters", "od_assoc_rounds", "od_rows_sum", "od_corner_last", "od_surf_last", "od_queries",
-        "mp_iters", "mp_rows_sum", "mp_stack", "mp_map_points", "mp_map_valid_points",
+        "od_assoc_points",
+        "mp_iters", "mp_rows_sum", "mp_stack", "mp_map_points", "mp_map_valid_points", "mp_stack_iters",
+        "mp_fits",
         "bytes_sr", "bytes_od", "bytes_mp")] + [(n, ctypes.c_double) for n in ("ms_sr", "ms_od", "ms_mp")]
 
     def as_dict(self):

@@ -62,3 +62,20 @@ def test_maintenance_identity(loam):
     p = np.array([0.01, -0.2, 0.03, 1.0, -2.0, 3.0], np.float32)
     out = loam.maintenance(p, p, p)
     assert np.abs(out - p).max() < 1e-5
+
+
+def test_stats_layout_matches_header(loam, oc):
+    """loam_stats as declared in include/loam/loam.h == the ctypes mirrors (engine and oracle)."""
+    import re
+    h = open(os.path.join(ROOT, "include", "loam", "loam.h")).read()
+    body = h[h.index("typedef struct {\n  uint64_t n_raw"):h.index("} loam_stats;")]
+    names = []
+    for line in body.splitlines():
+        line = line.split("/*")[0].strip()
+        m = re.match(r"(uint64_t|double)\s+(.*);", line)
+        if m:
+            names += [(m.group(1), n.strip()) for n in m.group(2).split(",")]
+    py = [("uint64_t" if t is ctypes.c_uint64 else "double", n) for n, t in loam.Stats._fields_]
+    po = [("uint64_t" if t is ctypes.c_uint64 else "double", n) for n, t in oc.Stats._fields_]
+    assert py == names
+    assert po == names
