@@ -4,7 +4,8 @@
  * (/root/reference = Maofei/loam_velodyne-1).  Each entry point replaces one node callback:
  *
  *   loam_scan_registration  <- laserCloudHandler        src/scanRegistration.cpp:211-636
- *   loam_imu                <- imuHandler               src/scanRegistration.cpp:638-660 (§8f, not yet)
+ *   loam_imu                <- imuHandler               src/scanRegistration.cpp:638-660 and
+ *                              laserMapping imuHandler  src/laserMapping.cpp:323-335
  *   loam_odometry           <- laserOdometry loop body  src/laserOdometry.cpp:413-931
  *                              (inputs = what handlers :275-354 store)
  *   loam_mapping            <- laserMapping loop body   src/laserMapping.cpp:411-1097
@@ -102,6 +103,14 @@ void loam_config_default(loam_config *cfg);               /* reference constants
 int loam_create(loam_ctx **out, const loam_config *cfg, int device);
 void loam_destroy(loam_ctx *ctx);
 const char *loam_last_error(void);
+
+/* = the /imu/data handlers of scanRegistration (src/scanRegistration.cpp:638-660: queue entry, gravity
+ * removal, AccumulateIMUShift) and laserMapping (src/laserMapping.cpp:323-335).  quat_xyzw = the
+ * sensor_msgs/Imu orientation (x, y, z, w), lin_acc_xyz = linear_acceleration, both float64 as in the
+ * message.  Stamps must be non-decreasing (LOAM_E_INVAL otherwise).  With IMU data, scan registration
+ * de-skews each point with it (:286-349) and fills imu_trans; odometry and mapping use it through
+ * imu_trans and the mapping queue (src/laserOdometry.cpp:330-351, src/laserMapping.cpp:199-226). */
+int loam_imu(loam_ctx *ctx, double stamp, const double quat_xyzw[4], const double lin_acc_xyz[3]);
 
 /* = laserCloudHandler.  Returns LOAM_E_NOT_READY for the first system_delay sweeps (Q1). */
 int loam_scan_registration(loam_ctx *ctx, double stamp, loam_cloud_in raw, loam_features *out);

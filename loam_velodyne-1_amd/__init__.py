@@ -81,7 +81,7 @@ class Stats(ctypes.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
-EXPORTS = ("loam_config_default", "loam_create", "loam_destroy", "loam_last_error",
+EXPORTS = ("loam_config_default", "loam_create", "loam_destroy", "loam_last_error", "loam_imu",
            "loam_scan_registration", "loam_odometry", "loam_mapping", "loam_maintenance",
            "loam_batch_upload", "loam_batch_run", "loam_batch_sync", "loam_batch_download", "loam_get_stats",
            "loam_set_profiling", "loam_get_kernel_times")
@@ -99,6 +99,7 @@ def lib():
         L.loam_destroy.argtypes = [PP]
         L.loam_last_error.restype = ctypes.c_char_p
         L.loam_scan_registration.argtypes = [PP, ctypes.c_double, CloudIn, P(Features)]
+        L.loam_imu.argtypes = [PP, ctypes.c_double, P(ctypes.c_double), P(ctypes.c_double)]
         L.loam_odometry.argtypes = [PP, ctypes.c_double, P(Features), P(Pose6), P(CloudOut), P(CloudOut),
                                     P(CloudOut), P(ctypes.c_int)]
         L.loam_mapping.argtypes = [PP, ctypes.c_double, P(Pose6), P(CloudOut), P(CloudOut), P(CloudOut),
@@ -168,7 +169,13 @@ class Engine:
         _check(lib().loam_get_stats(self.h, ctypes.byref(s)))
         return s.as_dict()
 
-    # --- the four node bodies
+    # --- the node bodies
+    def imu(self, stamp, quat_xyzw, lin_acc):
+        """/imu/data (scanRegistration and laserMapping imuHandlers)"""
+        q = (ctypes.c_double * 4)(*[float(v) for v in quat_xyzw])
+        a = (ctypes.c_double * 3)(*[float(v) for v in lin_acc])
+        _check(lib().loam_imu(self.h, stamp, q, a))
+
     def scan_registration(self, raw, stamp=0.0):
         ci, keep = _cloud_in(raw)
         outs = [_Out(self.cap) for _ in range(5)]
@@ -178,11 +185,15 @@ class Engine:
             return rc, None
         _check(rc)
         names = ["full", "sharp", "less_sharp", "flat", "less_flat"]
-        return 0, {n: o.get(getattr(f, n).count) for n, o in zip(names, outs)}
+        res = {n: o.get(getattr(f, n).count) for n, o in zip(names, outs)}
+        res["imu_trans"] = np.array(f.imu_trans[:], np.float32)
+        return 0, res
 
     def odometry(self, feats, stamp=0.0):
         refs = [_cloud_ref(feats[n]) for n in ("full", "sharp", "less_sharp", "flat", "less_flat")]
         f = Features(*[r[0] for r in refs])
+        if "imu_trans" in feats:
+            f.imu_trans[:] = [float(v) for v in feats["imu_trans"]]
         pose = Pose6()
         outs = [_Out(self.cap) for _ in range(3)]
         pub = ctypes.c_int(0)

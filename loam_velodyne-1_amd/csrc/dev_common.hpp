@@ -71,7 +71,32 @@ LOAM_D int wave_incl_scan(int v) {
   return v;
 }
 
+LOAM_D int wave_incl_max(int v) {
+  for (int o = 1; o < 64; o <<= 1) {
+    int w = __shfl_up(v, o, 64);
+    if (lane_id() >= o) v = max(v, w);
+  }
+  return v;
+}
+
 // ------------------------------------------------------------------ block primitives
+// inclusive max-scan of one int per thread over a block of NT threads (thread order); returns
+// the block maximum in `total`.  scratch: at least NT/64 + 1 ints of LDS.
+template <int NT>
+LOAM_D int block_incl_max(int v, int* scratch, int& total) {
+  const int nw = NT / 64, w = threadIdx.x >> 6, l = lane_id();
+  int incl = wave_incl_max(v);
+  if (l == 63) scratch[w] = incl;
+  __syncthreads();
+  int before = -0x7fffffff;
+  for (int k = 0; k < w; ++k) before = max(before, scratch[k]);
+  int tot = -0x7fffffff;
+  for (int k = 0; k < nw; ++k) tot = max(tot, scratch[k]);
+  total = tot;
+  __syncthreads();
+  return max(before, incl);
+}
+
 // exclusive scan of one int per thread over a block of NT threads; returns the block total.
 // scratch: at least NT/64 ints of LDS.
 template <int NT>

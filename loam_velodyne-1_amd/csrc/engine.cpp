@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -73,6 +74,12 @@ struct loam_ctx {
   bool od_inited = false;
   int od_last = 0, od_frame_count = 1;
   MpBuffers mp1;        // streaming map
+  // IMU (loam_imu): scanRegistration's queue (host master copy, uploaded per sweep) and
+  // laserMapping's queue
+  loamimu::SrQueue* sr_imu = nullptr;     // host
+  loamimu::SrQueue* sr_imu_dev = nullptr; // device
+  loamimu::MpQueue mp_imu;
+  double imu_last_stamp = -1e300;
   // batch (config 4)
   int P = 0;
   SrBuffers srb;
@@ -194,6 +201,12 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   sr_alloc(x->odin, 1, x->cap, x->R);
   od_alloc(x->od1, 1, x->R, x->cap, (int)c.od_max_iter);
   mp_alloc(x->mp1, 1, x->R, x->cap, (int)c.map_capacity, (int)c.mp_max_iter);
+  x->sr_imu = new loamimu::SrQueue();
+  std::memset(x->sr_imu, 0, sizeof(loamimu::SrQueue));
+  x->sr_imu->last = -1;
+  std::memset(&x->mp_imu, 0, sizeof(x->mp_imu));
+  x->mp_imu.last = -1;
+  (void)hipMalloc(&x->sr_imu_dev, sizeof(loamimu::SrQueue));
   if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess) {
     loam_destroy(x);
     return fail(LOAM_E_NOMEM, "device allocation failed");
@@ -213,6 +226,8 @@ void loam_destroy(loam_ctx* x) {
   sr_free(x->srb);
   od_free(x->odb);
   mp_free(x->mpb);
+  if (x->sr_imu_dev) (void)hipFree(x->sr_imu_dev);
+  delete x->sr_imu;
   for (auto& e : x->ev)
     if (e) (void)hipEventDestroy(e);
   if (x->st) (void)hipStreamDestroy(x->st);
@@ -247,7 +262,6 @@ int loam_get_stats(loam_ctx* x, loam_stats* s) {
 
 // ------------------------------------------------------------------ scanRegistration
 int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_features* out) {
-  (void)stamp;
   if (!x || !out) return fail(LOAM_E_INVAL, "null argument");
   if (!x->sr_inited) {  // src/scanRegistration.cpp:213-219 (Q1)
     x->sr_init_count++;
@@ -263,10 +277,21 @@ int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_fe
   const int n = (int)raw.count;
   HIP_TRY(hipMemcpyAsync(b.raw, x->stage.data(), (size_t)n * sizeof(float4), hipMemcpyHostToDevice, x->st));
   HIP_TRY(hipMemcpyAsync(b.raw_n, &n, sizeof(int), hipMemcpyHostToDevice, x->st));
+  SrParams prm = sr_params(x);
+  loamimu::SrQueue* q = x->sr_imu;
+  const size_t tail = offsetof(loamimu::SrQueue, front);  // pointers, Start, Cur, FromStart
+  if (q->last >= 0) {  // IMU de-skew (:286-349) with the queue as loam_imu left it
+    HIP_TRY(hipMemcpyAsync(x->sr_imu_dev, q, sizeof(*q), hipMemcpyHostToDevice, x->st));
+    prm.imu = x->sr_imu_dev;
+    prm.time_scan = stamp;
+  }
   HIP_TRY(hipEventRecord(x->ev[0], x->st));
-  sr_launch(b, sr_params(x), x->st);
+  sr_launch(b, prm, x->st);
   HIP_TRY(hipEventRecord(x->ev[1], x->st));
   HIP_TRY(hipGetLastError());
+  if (q->last >= 0)
+    HIP_TRY(hipMemcpyAsync((char*)q + tail, (const char*)x->sr_imu_dev + tail, sizeof(*q) - tail,
+                           hipMemcpyDeviceToHost, x->st));
   int cnt[4], nfull, err;
   HIP_TRY(hipMemcpyAsync(cnt, b.cnt, sizeof(cnt), hipMemcpyDeviceToHost, x->st));
   HIP_TRY(hipMemcpyAsync(&nfull, b.n_full, sizeof(int), hipMemcpyDeviceToHost, x->st));
@@ -280,8 +305,11 @@ int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_fe
   e |= copy_out(x->st, b.lsharp, cnt[1], &out->less_sharp);
   e |= copy_out(x->st, b.flat, cnt[2], &out->flat);
   e |= copy_out(x->st, b.lflat, cnt[3], &out->less_flat);
-  std::memset(out->imu_trans, 0, sizeof(out->imu_trans));
   HIP_TRY(hipStreamSynchronize(x->st));
+  // /imu_trans (:614-635)
+  const float it[12] = {q->pitchStart, q->yawStart, q->rollStart, q->pitchCur, q->yawCur, q->rollCur,
+                        q->shiftFSX,   q->shiftFSY, q->shiftFSZ,  q->veloFSX,  q->veloFSY, q->veloFSZ};
+  std::memcpy(out->imu_trans, it, sizeof(it));
   float ms = 0;
   (void)hipEventElapsedTime(&ms, x->ev[0], x->ev[1]);
   std::memset(&x->stats, 0, sizeof(x->stats));
@@ -321,7 +349,12 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
   HIP_TRY(hipMemcpyAsync(fi.n_full, &cnt[4], sizeof(int), hipMemcpyHostToDevice, x->st));
   const FeatView fv = feat_view(fi, 0, 1);
   std::memset(&x->stats, 0, sizeof(x->stats));
+  // imuTransHandler (:330-351): this sweep's /imu_trans, in the state order load_imu reads
+  HIP_TRY(hipMemcpyAsync(o.state + kOdImu, in->imu_trans, 12 * sizeof(float), hipMemcpyHostToDevice, x->st));
   if (!x->od_inited) {  // src/laserOdometry.cpp:427-456: Last = raw lessSharp / lessFlat, no L-M
+    // :451-452 transformSum[0] += imuPitchStart; transformSum[2] += imuRollStart (from zero)
+    const float sum0[3] = {0.0f + in->imu_trans[0], 0.0f, 0.0f + in->imu_trans[2]};
+    HIP_TRY(hipMemcpyAsync(o.state + kOdSum, sum0, sizeof(sum0), hipMemcpyHostToDevice, x->st));
     hipLaunchKernelGGL(k_od_end, dim3(16, 1), dim3(256), 0, x->st, o, fv, 0, 0, 0);
     od_build_hashes(o, 0, x->st);
     HIP_TRY(hipGetLastError());
@@ -382,12 +415,30 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
 int loam_mapping(loam_ctx* x, double stamp, const loam_pose6* odom_sum, const loam_cloud_out* corner_last,
                  const loam_cloud_out* surf_last, const loam_cloud_out* full_end, loam_pose6* aft,
                  loam_pose6* bef, loam_cloud_out* registered) {
-  (void)stamp;
   if (!x || !odom_sum || !corner_last || !surf_last || !full_end || !aft || !bef)
     return fail(LOAM_E_INVAL, "null argument");
   HIP_TRY(hipSetDevice(x->device));
-  return mp_stream_frame(x->mp1, x->st, *odom_sum, *corner_last, *surf_last, *full_end, aft, bef,
-                         registered, &x->stats, g_err);
+  // transformUpdate's IMU blend (:199-226): roll / pitch at the odometry stamp + scanPeriod
+  float rp[2];
+  int front = 0;
+  const bool have_imu = loamimu::mp_lookup(x->mp_imu, stamp, rp[0], rp[1], front);
+  bool updated = false;
+  const int rc = mp_stream_frame(x->mp1, x->st, *odom_sum, *corner_last, *surf_last, *full_end, aft, bef,
+                                 registered, &x->stats, g_err, have_imu ? rp : nullptr, &updated);
+  if (have_imu && updated) x->mp_imu.front = front;  // the pointer walk happens inside transformUpdate
+  return rc;
+}
+
+// ------------------------------------------------------------------ IMU
+int loam_imu(loam_ctx* x, double stamp, const double* quat_xyzw, const double* lin_acc_xyz) {
+  if (!x || !quat_xyzw || !lin_acc_xyz) return fail(LOAM_E_INVAL, "null argument");
+  if (!(stamp >= x->imu_last_stamp)) return fail(LOAM_E_INVAL, "IMU stamps must be non-decreasing");
+  x->imu_last_stamp = stamp;
+  double roll, pitch, yaw;
+  loampose::rpy_from_quat(quat_xyzw, roll, pitch, yaw);  // tf::Matrix3x3(q).getRPY
+  loamimu::sr_push(*x->sr_imu, stamp, roll, pitch, yaw, lin_acc_xyz);  // scanRegistration.cpp:638-660
+  loamimu::mp_push(x->mp_imu, stamp, roll, pitch);                     // laserMapping.cpp:323-335
+  return LOAM_OK;
 }
 
 // ------------------------------------------------------------------ transformMaintenance

@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include "../../include/loam/loam.h"
+#include "imu.hpp"
 #include "prof.hpp"
 
 namespace loam {
@@ -65,6 +66,8 @@ struct SrParams {
   int R;
   int ring_model;
   float ring_lo, ring_hi;
+  loamimu::SrQueue* imu = nullptr;  // device IMU queue of sweep 0 (streaming), nullptr = no IMU
+  double time_scan = 0.0;           // timeScanCur: the sweep's stamp
 };
 
 void sr_alloc(SrBuffers& b, int S, int cap, int R);

@@ -678,6 +678,10 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
         cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
         ok = D(sw) > 0.1 ? 1 : 0;
       }
+    } else if (first) {
+      // no fit this iteration: drop a fit left by an earlier frame (whose map indices name other
+      // points) so that a later iteration cannot take it for this frame's
+      qfit[q].n0 = make_int4(-1, -1, -1, -1);
     }
     qok[q] = (int8_t)ok;
     qcf[q] = cf;
@@ -783,13 +787,19 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
   }
 }
 
-// transformUpdate (:199-232, no IMU) for the instances whose L-M ran
+// transformUpdate (:199-232) for the instances whose L-M ran; the IMU blend (:224-225) when the
+// host found IMU data for the odometry stamp
 __global__ void k_mp_lm_end(MpBuffers b) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= b.P) return;
   const int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan]) return;
   float* st = b.state + (size_t)p * kMpStateFloats;
+  if (ist[kMiImu]) {
+    const float imuRollLast = st[kMpImuRP], imuPitchLast = st[kMpImuRP + 1];
+    st[kMpTobe + 0] = (float)(0.998 * D(st[kMpTobe + 0]) + 0.002 * D(imuPitchLast));
+    st[kMpTobe + 2] = (float)(0.998 * D(st[kMpTobe + 2]) + 0.002 * D(imuRollLast));
+  }
   for (int k = 0; k < 6; ++k) {
     st[kMpBef + k] = st[kMpSum + k];
     st[kMpAft + k] = st[kMpTobe + k];
@@ -1158,7 +1168,8 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
 
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
                     const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
-                    loam_cloud_out* registered, loam_stats* stats, std::string& err) {
+                    loam_cloud_out* registered, loam_stats* stats, std::string& err, const float* imu_rp,
+                    bool* updated) {
   if (corner.count > (uint32_t)b.capC || surf.count > (uint32_t)b.capS || full.count > (uint32_t)b.capS) {
     err = "mapping input cloud exceeds capacity";
     return LOAM_E_CAPACITY;
@@ -1176,6 +1187,10 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   if (n[2]) (void)hipMemcpyAsync(b.inF, full.pts, n[2] * sizeof(float4), hipMemcpyHostToDevice, st);
   (void)hipMemcpyAsync(b.in_n, n, sizeof(n), hipMemcpyHostToDevice, st);
   (void)hipMemcpyAsync(b.in_pose, &odom_sum, 6 * sizeof(float), hipMemcpyHostToDevice, st);
+  static const float zero_rp[2] = {0.0f, 0.0f};
+  static const int imu_on = 1, imu_off = 0;
+  (void)hipMemcpyAsync(b.state + kMpImuRP, imu_rp ? imu_rp : zero_rp, 2 * sizeof(float), hipMemcpyHostToDevice, st);
+  (void)hipMemcpyAsync(b.istate + kMiImu, imu_rp ? &imu_on : &imu_off, sizeof(int), hipMemcpyHostToDevice, st);
   MpInput in;
   in.corner = b.inC; in.surf = b.inS; in.full = b.inF;
   in.corner_stride = b.capC; in.surf_stride = b.capS; in.full_stride = b.capS;
@@ -1205,6 +1220,7 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   }
   std::memcpy(aft, sf + kMpAft, sizeof(loam_pose6));
   std::memcpy(bef, sf + kMpBef, sizeof(loam_pose6));
+  if (updated) *updated = si[kMiLmRan] != 0;
   int rc = LOAM_OK;
   if (registered) {
     if ((uint32_t)nreg > registered->capacity) {

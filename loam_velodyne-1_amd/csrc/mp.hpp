@@ -17,9 +17,9 @@ constexpr int kMaxValid = 125;
 
 // per-instance float state: Sum | Incre | TobeMapped | Bef | Aft | matP[36] | pointOnYAxis[3]
 constexpr int kMpSum = 0, kMpIncre = 6, kMpTobe = 12, kMpBef = 18, kMpAft = 24, kMpMatP = 30, kMpOnY = 66,
-              kMpStateFloats = 72;
+              kMpImuRP = 69, kMpStateFloats = 72;  // kMpImuRP: IMU (roll, pitch) for transformUpdate
 enum { kMiCenW = 0, kMiCenH, kMiCenD, kMiDegen, kMiNValid, kMiIters, kMiRows, kMiStackC, kMiStackS, kMiFromC,
-       kMiFromS, kMiErr, kMiLmRan, kMiValidPts, kMiStop, kMiFits, kMpStateInts = 16 };
+       kMiFromS, kMiErr, kMiLmRan, kMiValidPts, kMiStop, kMiFits, kMiImu, kMpStateInts = 20 };
 
 // one mapping frame's inputs for every instance (device pointers)
 struct MpInput {
@@ -97,9 +97,12 @@ void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter
 void mp_free(MpBuffers& b);
 void mp_reset(MpBuffers& b, hipStream_t st);
 void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof = nullptr);
+// imu_rp: the IMU (roll, pitch) transformUpdate blends in (nullptr = no IMU); *updated = whether
+// transformUpdate ran (the caller then commits its IMU queue pointer)
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
                     const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
-                    loam_cloud_out* registered, loam_stats* stats, std::string& err);
+                    loam_cloud_out* registered, loam_stats* stats, std::string& err,
+                    const float* imu_rp = nullptr, bool* updated = nullptr);
 void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof = nullptr);
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err);
 

@@ -57,6 +57,7 @@ LOAM_D bool finite3(const float4& q) {
 }
 
 // ---------------------------------------------------------------- ring sort
+template <bool IMU>
 __global__ __launch_bounds__(kSrThreads) void k_sr_ring_sort(SrBuffers b, SrParams p) {
   const int s = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const int n = b.raw_n[s];
@@ -146,12 +147,61 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_sort(SrBuffers b, SrPara
   }
   __syncthreads();
   const int F = sh_F;
+  // IMU (:286-349, sweep 0 of a streaming context only): the Start state from the first finite
+  // point when it passed the ring filter (the reference's i == 0), else the previous sweep's
+  loamimu::SrQueue* imu = IMU && s == 0 ? p.imu : nullptr;
+  __shared__ loamimu::Start sh_S;
+  __shared__ int sh_carry, sh_imuscr[kSrThreads / 64 + 1], sh_lasti;
+  __shared__ loamimu::Cur sh_lastc;
+  __shared__ float sh_lastfs[6];
+  const int i0 = sh_first;
+  const int front0 = imu ? imu->front : 0;
+  if (imu && tid == 0) {
+    loamimu::Cur c;
+    if (tsid[i0] != 255) {
+      const float ori = ori_first(tori[i0], startOri);  // i0 <= F
+      const float relTime = (ori - startOri) / (endOri - startOri);
+      const float pointTime = (float)(D(relTime) * 0.1);  // scanPeriod (double, :55)
+      const int g = loamimu::first_later(*imu, front0, p.time_scan + pointTime);
+      c = loamimu::interpolate(*imu, (front0 + g) % loamimu::kQue, p.time_scan, pointTime);
+      imu->rollStart = c.roll; imu->pitchStart = c.pitch; imu->yawStart = c.yaw;
+      imu->veloXStart = c.vx; imu->veloYStart = c.vy; imu->veloZStart = c.vz;
+      imu->shiftXStart = c.sx; imu->shiftYStart = c.sy; imu->shiftZStart = c.sz;
+    } else {
+      c = loamimu::Cur{imu->rollStart, imu->pitchStart, imu->yawStart, imu->veloXStart, imu->veloYStart,
+                       imu->veloZStart, imu->shiftXStart, imu->shiftYStart, imu->shiftZStart};
+    }
+    sh_S = loamimu::make_start(c);
+    sh_carry = 0;
+    sh_lasti = -1;
+  }
+  __syncthreads();
   // phase C: stable scatter into ring order
   for (int t = 0; t < ntiles; ++t) {
     const int i = t * kSrThreads + tid;
     int sid = 255;
     if (i < n) sid = tsid[i];
     const bool valid = (i < n) && sid != 255;
+    // IMU queue entry of every point: the reference's forward-only pointer walk (:288-293) is the
+    // running maximum, over the points in input order, of "first entry later than the point"
+    float pointTime = 0.0f;
+    int front_i = 0;
+    if (imu) {
+      int g = -1;
+      if (valid) {
+        const float ori = (i <= F) ? ori_first(tori[i], startOri) : ori_second(tori[i], endOri);
+        const float relTime = (ori - startOri) / (endOri - startOri);
+        pointTime = (float)(D(relTime) * 0.1);
+        g = loamimu::first_later(*imu, front0, p.time_scan + pointTime);
+      }
+      int tmax;
+      const int incl = block_incl_max<kSrThreads>(g, sh_imuscr, tmax);
+      front_i = max(sh_carry, incl);
+      __syncthreads();
+      if (tid == 0) sh_carry = max(sh_carry, tmax);
+    }
+    loamimu::Cur cur;
+    float fs[6];
     if (lane < R) sh_wcnt[w][lane] = 0;
     __builtin_amdgcn_wave_barrier();
     int rank = 0;
@@ -177,11 +227,42 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_sort(SrBuffers b, SrPara
       o.y = q.z;
       o.z = q.x;
       o.w = (float)(sid + 0.1 * D(relTime));
+      if (imu) {
+        cur = loamimu::interpolate(*imu, (front0 + front_i) % loamimu::kQue, p.time_scan, pointTime);
+        if (i != i0) {  // ShiftToStartIMU, VeloToStartIMU, TransformToStartIMU (:343-347)
+          loamimu::to_start(sh_S, cur, pointTime, fs);
+          o = loamimu::transform_to_start(sh_S, cur, fs, o);
+        }
+      }
       b.full[(size_t)s * b.cap + pos] = o;
+    }
+    if (imu) {  // the last processed point leaves its Cur / FromStart values in the globals
+      int lm;
+      (void)block_incl_max<kSrThreads>(valid ? i : -1, sh_imuscr, lm);
+      if (valid && i == lm) {
+        sh_lasti = i;
+        sh_lastc = cur;
+        for (int k = 0; k < 6; ++k) sh_lastfs[k] = fs[k];
+      }
     }
     __syncthreads();
   }
-  if (tid == 0) b.n_full[s] = sh_total;
+  if (tid == 0) {
+    b.n_full[s] = sh_total;
+    if (imu) {
+      imu->front = (front0 + sh_carry) % loamimu::kQue;
+      if (sh_lasti >= 0) {
+        const loamimu::Cur& c = sh_lastc;
+        imu->rollCur = c.roll; imu->pitchCur = c.pitch; imu->yawCur = c.yaw;
+        imu->veloXCur = c.vx; imu->veloYCur = c.vy; imu->veloZCur = c.vz;
+        imu->shiftXCur = c.sx; imu->shiftYCur = c.sy; imu->shiftZCur = c.sz;
+        if (sh_lasti != i0) {
+          imu->shiftFSX = sh_lastfs[0]; imu->shiftFSY = sh_lastfs[1]; imu->shiftFSZ = sh_lastfs[2];
+          imu->veloFSX = sh_lastfs[3]; imu->veloFSY = sh_lastfs[4]; imu->veloFSZ = sh_lastfs[5];
+        }
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------- curvature + marks
@@ -744,7 +825,8 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
   HIPCHK(hipMemsetAsync(b.ring_se, 0, (size_t)b.S * 2 * b.R * sizeof(int), st));
   HIPCHK(hipMemsetAsync(b.err, 0, (size_t)b.S * sizeof(int), st));
   mark("sr_memset");
-  hipLaunchKernelGGL(k_sr_ring_sort, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
+  if (p.imu) hipLaunchKernelGGL(k_sr_ring_sort<true>, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
+  else hipLaunchKernelGGL(k_sr_ring_sort<false>, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
   mark("k_sr_ring_sort");
   hipLaunchKernelGGL(k_sr_features, dim3((b.cap + kFeatTile - 1) / kFeatTile, b.S), dim3(kFeatTile), 0,
                      st, b, p);

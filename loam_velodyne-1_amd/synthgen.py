@@ -134,3 +134,30 @@ def batch_problems(n, base_seed=1000, lidar=VLP16, nthreads=None):
         seeds += [s * 2 + 1, s * 2 + 2]
     sw = sweeps_batch(scenes, lidar, p0s, p1s, seeds, nthreads=nthreads)
     return sw[0::2], sw[1::2]
+
+
+def quat_from_rpy(roll, pitch, yaw):
+    """tf::Quaternion::setRPY as (x, y, z, w)"""
+    hy, hp, hr = yaw * 0.5, pitch * 0.5, roll * 0.5
+    cy, sy, cp, sp, cr, sr = math.cos(hy), math.sin(hy), math.cos(hp), math.sin(hp), math.cos(hr), math.sin(hr)
+    return (sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy, cr * cp * sy - sr * sp * cy,
+            cr * cp * cy + sr * sp * sy)
+
+
+def imu_stream(t_begin, t_end, rate=100.0, seed=0, radius=6.0, speed=1.0, tilt_deg=0.3):
+    """/imu/data messages (stamp, quat_xyzw, linear_acceleration) for the config-3 loop: the
+    vehicle yaw of loop_pose, a small seeded roll / pitch wobble, and the specific force of the
+    circular motion (centripetal acceleration to the left, gravity up) in the IMU frame (x forward,
+    y left, z up).  Deterministic; stamps strictly increasing."""
+    rng = np.random.default_rng(seed)
+    ph = rng.uniform(0, 2 * math.pi, size=2)
+    out = []
+    n = int(round((t_end - t_begin) * rate))
+    for k in range(n + 1):
+        t = t_begin + k / rate
+        yaw = loop_pose(t, radius, speed)[5]
+        roll = math.radians(tilt_deg) * math.sin(1.3 * t + ph[0])
+        pitch = math.radians(tilt_deg) * math.sin(0.9 * t + ph[1])
+        acc = (0.0, speed * speed / radius, 9.81)
+        out.append((t, quat_from_rpy(roll, pitch, yaw), acc))
+    return out

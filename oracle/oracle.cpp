@@ -65,6 +65,7 @@ Cfg make_cfg(const loam_config* c) {
 // ===================================================================== scan registration
 struct SrOut {
   std::vector<P> full, sharp, lsharp, flat, lflat;
+  float imu_trans[12] = {0};  // /imu_trans (:614-635)
 };
 
 // src/scanRegistration.cpp:248-260 (VLP-16) and the bk HDL-64E hint (bk :268-275)
@@ -79,7 +80,168 @@ int ring_id(const Cfg& c, float angle) {
 }
 
 // laserCloudHandler body after the systemDelay gate: src/scanRegistration.cpp:221-581
-int sr_body(const Cfg& cfg, const float* raw, size_t n, size_t stride_f, SrOut& o) {
+// scanRegistration's IMU globals (src/scanRegistration.cpp:68-97), fed by imuHandler (:638-660)
+constexpr int kImuQue = 200;  // imuQueLength
+struct SrImu {
+  int front = 0, last = -1;
+  float rollStart = 0, pitchStart = 0, yawStart = 0, rollCur = 0, pitchCur = 0, yawCur = 0;
+  float veloXStart = 0, veloYStart = 0, veloZStart = 0, shiftXStart = 0, shiftYStart = 0, shiftZStart = 0;
+  float veloXCur = 0, veloYCur = 0, veloZCur = 0, shiftXCur = 0, shiftYCur = 0, shiftZCur = 0;
+  float shiftFSX = 0, shiftFSY = 0, shiftFSZ = 0, veloFSX = 0, veloFSY = 0, veloFSZ = 0;
+  double time[kImuQue] = {0};
+  float roll[kImuQue] = {0}, pitch[kImuQue] = {0}, yaw[kImuQue] = {0};
+  float accX[kImuQue] = {0}, accY[kImuQue] = {0}, accZ[kImuQue] = {0};
+  float veloX[kImuQue] = {0}, veloY[kImuQue] = {0}, veloZ[kImuQue] = {0};
+  float shiftX[kImuQue] = {0}, shiftY[kImuQue] = {0}, shiftZ[kImuQue] = {0};
+};
+
+// float std::sin / std::cos: scanRegistration's `using std::sin; using std::cos;` (:51-52) binds the
+// float overloads for float arguments
+inline float fsin(float x) { return std::sin(x); }
+inline float fcos(float x) { return std::cos(x); }
+
+// :162-200 AccumulateIMUShift
+void accumulate_imu_shift(SrImu& m) {
+  const int L = m.last;
+  float roll = m.roll[L], pitch = m.pitch[L], yaw = m.yaw[L];
+  float accX = m.accX[L], accY = m.accY[L], accZ = m.accZ[L];
+  float x1 = fcos(roll) * accX - fsin(roll) * accY;
+  float y1 = fsin(roll) * accX + fcos(roll) * accY;
+  float z1 = accZ;
+  float x2 = x1;
+  float y2 = fcos(pitch) * y1 - fsin(pitch) * z1;
+  float z2 = fsin(pitch) * y1 + fcos(pitch) * z1;
+  accX = fcos(yaw) * x2 + fsin(yaw) * z2;
+  accY = y2;
+  accZ = -fsin(yaw) * x2 + fcos(yaw) * z2;
+  const int B = (L + kImuQue - 1) % kImuQue;
+  double timeDiff = m.time[L] - m.time[B];
+  if (timeDiff < 0.1) {  // scanPeriod (double, :55)
+    m.shiftX[L] = (float)(D(m.shiftX[B]) + D(m.veloX[B]) * timeDiff + D(accX) * timeDiff * timeDiff / 2);
+    m.shiftY[L] = (float)(D(m.shiftY[B]) + D(m.veloY[B]) * timeDiff + D(accY) * timeDiff * timeDiff / 2);
+    m.shiftZ[L] = (float)(D(m.shiftZ[B]) + D(m.veloZ[B]) * timeDiff + D(accZ) * timeDiff * timeDiff / 2);
+    m.veloX[L] = (float)(D(m.veloX[B]) + D(accX) * timeDiff);
+    m.veloY[L] = (float)(D(m.veloY[B]) + D(accY) * timeDiff);
+    m.veloZ[L] = (float)(D(m.veloZ[B]) + D(accZ) * timeDiff);
+  }
+}
+
+// :638-660 imuHandler
+void sr_imu_handler(SrImu& m, double stamp, const double* q, const double* acc) {
+  double roll, pitch, yaw;
+  tf_get_rpy(Quat{q[0], q[1], q[2], q[3]}, roll, pitch, yaw);
+  float accX = (float)(acc[1] - std::sin(roll) * std::cos(pitch) * 9.81);
+  float accY = (float)(acc[2] - std::cos(roll) * std::cos(pitch) * 9.81);
+  float accZ = (float)(acc[0] + std::sin(pitch) * 9.81);
+  m.last = (m.last + 1) % kImuQue;
+  m.time[m.last] = stamp;
+  m.roll[m.last] = (float)roll;
+  m.pitch[m.last] = (float)pitch;
+  m.yaw[m.last] = (float)yaw;
+  m.accX[m.last] = accX;
+  m.accY[m.last] = accY;
+  m.accZ[m.last] = accZ;
+  accumulate_imu_shift(m);
+}
+
+// :111-127 ShiftToStartIMU
+void shift_to_start_imu(SrImu& m, float pointTime) {
+  m.shiftFSX = m.shiftXCur - m.shiftXStart - m.veloXStart * pointTime;
+  m.shiftFSY = m.shiftYCur - m.shiftYStart - m.veloYStart * pointTime;
+  m.shiftFSZ = m.shiftZCur - m.shiftZStart - m.veloZStart * pointTime;
+  float x1 = fcos(m.yawStart) * m.shiftFSX - fsin(m.yawStart) * m.shiftFSZ;
+  float y1 = m.shiftFSY;
+  float z1 = fsin(m.yawStart) * m.shiftFSX + fcos(m.yawStart) * m.shiftFSZ;
+  float x2 = x1;
+  float y2 = fcos(m.pitchStart) * y1 + fsin(m.pitchStart) * z1;
+  float z2 = -fsin(m.pitchStart) * y1 + fcos(m.pitchStart) * z1;
+  m.shiftFSX = fcos(m.rollStart) * x2 + fsin(m.rollStart) * y2;
+  m.shiftFSY = -fsin(m.rollStart) * x2 + fcos(m.rollStart) * y2;
+  m.shiftFSZ = z2;
+}
+
+// :129-145 VeloToStartIMU
+void velo_to_start_imu(SrImu& m) {
+  m.veloFSX = m.veloXCur - m.veloXStart;
+  m.veloFSY = m.veloYCur - m.veloYStart;
+  m.veloFSZ = m.veloZCur - m.veloZStart;
+  float x1 = fcos(m.yawStart) * m.veloFSX - fsin(m.yawStart) * m.veloFSZ;
+  float y1 = m.veloFSY;
+  float z1 = fsin(m.yawStart) * m.veloFSX + fcos(m.yawStart) * m.veloFSZ;
+  float x2 = x1;
+  float y2 = fcos(m.pitchStart) * y1 + fsin(m.pitchStart) * z1;
+  float z2 = -fsin(m.pitchStart) * y1 + fcos(m.pitchStart) * z1;
+  m.veloFSX = fcos(m.rollStart) * x2 + fsin(m.rollStart) * y2;
+  m.veloFSY = -fsin(m.rollStart) * x2 + fcos(m.rollStart) * y2;
+  m.veloFSZ = z2;
+}
+
+// :147-160 TransformToStartIMU
+void transform_to_start_imu(const SrImu& m, P& p) {
+  float x1 = fcos(m.rollCur) * p.x - fsin(m.rollCur) * p.y;
+  float y1 = fsin(m.rollCur) * p.x + fcos(m.rollCur) * p.y;
+  float z1 = p.z;
+  float x2 = x1;
+  float y2 = fcos(m.pitchCur) * y1 - fsin(m.pitchCur) * z1;
+  float z2 = fsin(m.pitchCur) * y1 + fcos(m.pitchCur) * z1;
+  float x3 = fcos(m.yawCur) * x2 + fsin(m.yawCur) * z2;
+  float y3 = y2;
+  float z3 = -fsin(m.yawCur) * x2 + fcos(m.yawCur) * z2;
+  float x4 = fcos(m.yawStart) * x3 - fsin(m.yawStart) * z3;
+  float y4 = y3;
+  float z4 = fsin(m.yawStart) * x3 + fcos(m.yawStart) * z3;
+  float x5 = x4;
+  float y5 = fcos(m.pitchStart) * y4 + fsin(m.pitchStart) * z4;
+  float z5 = -fsin(m.pitchStart) * y4 + fcos(m.pitchStart) * z4;
+  p.x = fcos(m.rollStart) * x5 + fsin(m.rollStart) * y5 + m.shiftFSX;
+  p.y = -fsin(m.rollStart) * x5 + fcos(m.rollStart) * y5 + m.shiftFSY;
+  p.z = z5 + m.shiftFSZ;
+}
+
+// :286-349 the per-point IMU block
+void sr_point_imu(SrImu& m, double timeScanCur, float relTime, int i, P& point) {
+  float pointTime = (float)(D(relTime) * 0.1);  // scanPeriod (double)
+  while (m.front != m.last) {
+    if (timeScanCur + pointTime < m.time[m.front]) break;
+    m.front = (m.front + 1) % kImuQue;
+  }
+  const int F = m.front;
+  if (timeScanCur + pointTime > m.time[F]) {
+    m.rollCur = m.roll[F]; m.pitchCur = m.pitch[F]; m.yawCur = m.yaw[F];
+    m.veloXCur = m.veloX[F]; m.veloYCur = m.veloY[F]; m.veloZCur = m.veloZ[F];
+    m.shiftXCur = m.shiftX[F]; m.shiftYCur = m.shiftY[F]; m.shiftZCur = m.shiftZ[F];
+  } else {
+    const int B = (F + kImuQue - 1) % kImuQue;
+    float ratioFront = (float)((timeScanCur + pointTime - m.time[B]) / (m.time[F] - m.time[B]));
+    float ratioBack = (float)((m.time[F] - timeScanCur - pointTime) / (m.time[F] - m.time[B]));
+    m.rollCur = m.roll[F] * ratioFront + m.roll[B] * ratioBack;
+    m.pitchCur = m.pitch[F] * ratioFront + m.pitch[B] * ratioBack;
+    if (D(m.yaw[F] - m.yaw[B]) > M_PI)
+      m.yawCur = (float)(D(m.yaw[F] * ratioFront) + (D(m.yaw[B]) + 2 * M_PI) * D(ratioBack));
+    else if (D(m.yaw[F] - m.yaw[B]) < -M_PI)
+      m.yawCur = (float)(D(m.yaw[F] * ratioFront) + (D(m.yaw[B]) - 2 * M_PI) * D(ratioBack));
+    else
+      m.yawCur = m.yaw[F] * ratioFront + m.yaw[B] * ratioBack;
+    m.veloXCur = m.veloX[F] * ratioFront + m.veloX[B] * ratioBack;
+    m.veloYCur = m.veloY[F] * ratioFront + m.veloY[B] * ratioBack;
+    m.veloZCur = m.veloZ[F] * ratioFront + m.veloZ[B] * ratioBack;
+    m.shiftXCur = m.shiftX[F] * ratioFront + m.shiftX[B] * ratioBack;
+    m.shiftYCur = m.shiftY[F] * ratioFront + m.shiftY[B] * ratioBack;
+    m.shiftZCur = m.shiftZ[F] * ratioFront + m.shiftZ[B] * ratioBack;
+  }
+  if (i == 0) {
+    m.rollStart = m.rollCur; m.pitchStart = m.pitchCur; m.yawStart = m.yawCur;
+    m.veloXStart = m.veloXCur; m.veloYStart = m.veloYCur; m.veloZStart = m.veloZCur;
+    m.shiftXStart = m.shiftXCur; m.shiftYStart = m.shiftYCur; m.shiftZStart = m.shiftZCur;
+  } else {
+    shift_to_start_imu(m, pointTime);
+    velo_to_start_imu(m);
+    transform_to_start_imu(m, point);
+  }
+}
+
+int sr_body(const Cfg& cfg, const float* raw, size_t n, size_t stride_f, SrOut& o, SrImu& imu,
+            double timeScanCur) {
   const int N = cfg.n_rings;
   // fromROSMsg + removeNaNFromPointCloud (:225-228)
   std::vector<P> in;
@@ -122,9 +284,15 @@ int sr_body(const Cfg& cfg, const float* raw, size_t n, size_t stride_f, SrOut& 
     }
     float relTime = (ori - startOri) / (endOri - startOri);
     point.intensity = (float)(scanID + 0.1 * D(relTime));   // scanPeriod is double here (:55)
+    if (imu.last >= 0) sr_point_imu(imu, timeScanCur, relTime, i, point);  // :286-349
     scans[scanID].push_back(point);
   }
   cloudSize = count;
+
+  // :614-635 /imu_trans: start RPY (as pitch, yaw, roll), current RPY, shift and velocity from start
+  const float it[12] = {imu.pitchStart, imu.yawStart, imu.rollStart, imu.pitchCur, imu.yawCur, imu.rollCur,
+                        imu.shiftFSX, imu.shiftFSY, imu.shiftFSZ, imu.veloFSX, imu.veloFSY, imu.veloFSZ};
+  std::memcpy(o.imu_trans, it, sizeof(it));
 
   // :354-357 concat rings
   std::vector<P>& lc = o.full;
@@ -769,6 +937,10 @@ struct MpState {
   bool isDegenerate = false;
   float matP[36] = {0};
   uint64_t iters = 0, rows_sum = 0, stack = 0, map_points = 0, valid_points = 0;
+  // laserMapping's IMU queue (:101-108), fed by its imuHandler (:323-335)
+  int imuFront = 0, imuLast = -1;
+  double imuTime[kImuQue] = {0};
+  float imuRoll[kImuQue] = {0}, imuPitch[kImuQue] = {0};
   MpState() : corner(kNum), surf(kNum) {}
 };
 
@@ -927,7 +1099,8 @@ struct MpOut { float aft[6], bef[6]; std::vector<P> registered; };
 
 // laserMapping loop body :420-1094 (stackFrameNum = 1: every synchronised frame is processed)
 void mp_body(const Cfg& cfg, MpState& m, const std::vector<P>& cornerLast,
-             const std::vector<P>& surfLast, const std::vector<P>& full, MpOut& out) {
+             const std::vector<P>& surfLast, const std::vector<P>& full, MpOut& out,
+             double timeLaserOdometry = 0.0) {
   float* T = m.transformTobeMapped;
   std::vector<P> cornerStack2, surfStack2;
   m.frameCount++;
@@ -1113,7 +1286,28 @@ void mp_body(const Cfg& cfg, MpState& m, const std::vector<P>& cornerLast,
       float deltaR = delta_r(X), deltaT = delta_t(X);
       if (D(deltaR) < 0.05 && D(deltaT) < 0.05) break;
     }
-    // :199-232 transformUpdate (no IMU)
+    // :199-232 transformUpdate
+    if (m.imuLast >= 0) {
+      const float scanPeriod = 0.1f;  // const float in laserMapping.cpp:49
+      float imuRollLast = 0, imuPitchLast = 0;
+      while (m.imuFront != m.imuLast) {
+        if (timeLaserOdometry + scanPeriod < m.imuTime[m.imuFront]) break;
+        m.imuFront = (m.imuFront + 1) % kImuQue;
+      }
+      const int F = m.imuFront;
+      if (timeLaserOdometry + scanPeriod > m.imuTime[F]) {
+        imuRollLast = m.imuRoll[F];
+        imuPitchLast = m.imuPitch[F];
+      } else {
+        const int B = (F + kImuQue - 1) % kImuQue;
+        float ratioFront = (float)((timeLaserOdometry + scanPeriod - m.imuTime[B]) / (m.imuTime[F] - m.imuTime[B]));
+        float ratioBack = (float)((m.imuTime[F] - timeLaserOdometry - scanPeriod) / (m.imuTime[F] - m.imuTime[B]));
+        imuRollLast = m.imuRoll[F] * ratioFront + m.imuRoll[B] * ratioBack;
+        imuPitchLast = m.imuPitch[F] * ratioFront + m.imuPitch[B] * ratioBack;
+      }
+      T[0] = (float)(0.998 * D(T[0]) + 0.002 * D(imuPitchLast));
+      T[2] = (float)(0.998 * D(T[2]) + 0.002 * D(imuRollLast));
+    }
     for (int i = 0; i < 6; ++i) {
       m.transformBefMapped[i] = m.transformSum[i];
       m.transformAftMapped[i] = T[i];
@@ -1172,6 +1366,7 @@ struct Oracle {
   Cfg cfg;
   int sr_init_count = 0;
   bool sr_inited = false;
+  SrImu imu;
   OdState od;
   MpState mp;
   loam_stats stats;
@@ -1208,7 +1403,6 @@ void* oracle_create(const loam_config* cfg) { return new Oracle(make_cfg(cfg)); 
 void oracle_destroy(void* o) { delete static_cast<Oracle*>(o); }
 
 int oracle_scan_registration(void* h, double stamp, loam_cloud_in raw, loam_features* out) {
-  (void)stamp;
   Oracle* o = static_cast<Oracle*>(h);
   if (!o->sr_inited) {  // :213-219 (Q1)
     o->sr_init_count++;
@@ -1217,7 +1411,7 @@ int oracle_scan_registration(void* h, double stamp, loam_cloud_in raw, loam_feat
   }
   if (raw.stride_bytes % 4 != 0 || raw.stride_bytes < 12) return LOAM_E_INVAL;
   SrOut r;
-  int rc = sr_body(o->cfg, (const float*)raw.data, raw.count, raw.stride_bytes / 4, r);
+  int rc = sr_body(o->cfg, (const float*)raw.data, raw.count, raw.stride_bytes / 4, r, o->imu, stamp);
   if (rc) return rc;
   o->stats.n_raw = raw.count; o->stats.n_ring = r.full.size();
   o->stats.n_sharp = r.sharp.size(); o->stats.n_less_sharp = r.lsharp.size();
@@ -1228,7 +1422,7 @@ int oracle_scan_registration(void* h, double stamp, loam_cloud_in raw, loam_feat
   e |= write_cloud(r.lsharp, &out->less_sharp);
   e |= write_cloud(r.flat, &out->flat);
   e |= write_cloud(r.lflat, &out->less_flat);
-  std::memset(out->imu_trans, 0, sizeof(out->imu_trans));
+  std::memcpy(out->imu_trans, r.imu_trans, sizeof(out->imu_trans));
   return e ? LOAM_E_CAPACITY : LOAM_OK;
 }
 
@@ -1242,6 +1436,14 @@ int oracle_odometry(void* h, double stamp, const loam_features* in, loam_pose6* 
                  full = read_cloud(&in->full);
   OdIn oi{&sharp, &lsharp, &flat, &lflat, &full};
   OdOut oo;
+  {  // imuTransHandler (:330-351): the /imu_trans message of this sweep
+    const float* t = in->imu_trans;
+    OdState& d = o->od;
+    d.imuPitchStart = t[0]; d.imuYawStart = t[1]; d.imuRollStart = t[2];
+    d.imuPitchLast = t[3]; d.imuYawLast = t[4]; d.imuRollLast = t[5];
+    d.imuShiftFromStartX = t[6]; d.imuShiftFromStartY = t[7]; d.imuShiftFromStartZ = t[8];
+    d.imuVeloFromStartX = t[9]; d.imuVeloFromStartY = t[10]; d.imuVeloFromStartZ = t[11];
+  }
   uint64_t it0 = o->od.iters, as0 = o->od.assoc, rs0 = o->od.rows_sum, q0 = o->od.queries;
   o->stats.od_corner_last = o->od.cornerLast.size();
   o->stats.od_surf_last = o->od.surfLast.size();
@@ -1262,7 +1464,6 @@ int oracle_odometry(void* h, double stamp, const loam_features* in, loam_pose6* 
 int oracle_mapping(void* h, double stamp, const loam_pose6* odom_sum, const loam_cloud_out* corner_last,
                    const loam_cloud_out* surf_last, const loam_cloud_out* full_end, loam_pose6* aft,
                    loam_pose6* bef, loam_cloud_out* registered) {
-  (void)stamp;
   Oracle* o = static_cast<Oracle*>(h);
   float s[6];
   to6(odom_sum, s);
@@ -1271,13 +1472,29 @@ int oracle_mapping(void* h, double stamp, const loam_pose6* odom_sum, const loam
   MpOut mo;
   uint64_t it0 = o->mp.iters, rs0 = o->mp.rows_sum, st0 = o->mp.stack, mp0 = o->mp.map_points,
            vp0 = o->mp.valid_points;
-  mp_body(o->cfg, o->mp, cl, sl, fl, mo);
+  mp_body(o->cfg, o->mp, cl, sl, fl, mo, stamp);
   o->stats.mp_iters = o->mp.iters - it0; o->stats.mp_rows_sum = o->mp.rows_sum - rs0;
   o->stats.mp_stack = o->mp.stack - st0; o->stats.mp_map_points = o->mp.map_points - mp0;
   o->stats.mp_map_valid_points = o->mp.valid_points - vp0;
   from6(mo.aft, aft);
   from6(mo.bef, bef);
   return write_cloud(mo.registered, registered);
+}
+
+// /imu/data: scanRegistration's imuHandler (:638-660) and laserMapping's (:323-335).
+// quat = orientation (x, y, z, w), acc = linear_acceleration (x, y, z), as the sensor_msgs::Imu
+// fields (float64)
+int oracle_imu(void* h, double stamp, const double* quat, const double* acc) {
+  Oracle* o = static_cast<Oracle*>(h);
+  sr_imu_handler(o->imu, stamp, quat, acc);
+  double roll, pitch, yaw;
+  tf_get_rpy(Quat{quat[0], quat[1], quat[2], quat[3]}, roll, pitch, yaw);
+  MpState& m = o->mp;
+  m.imuLast = (m.imuLast + 1) % kImuQue;
+  m.imuTime[m.imuLast] = stamp;
+  m.imuRoll[m.imuLast] = (float)roll;
+  m.imuPitch[m.imuLast] = (float)pitch;
+  return LOAM_OK;
 }
 
 int oracle_maintenance(const loam_pose6* odom_sum, const loam_pose6* bef, const loam_pose6* aft,
@@ -1308,9 +1525,10 @@ int oracle_problem(const loam_config* cfg, loam_cloud_in prev, loam_cloud_in cur
                    loam_pose6* aft, loam_stats* st) {
   Cfg c = make_cfg(cfg);
   SrOut a, b;
-  int rc = sr_body(c, (const float*)prev.data, prev.count, prev.stride_bytes / 4, a);
+  SrImu no_imu;  // config 4 has no IMU
+  int rc = sr_body(c, (const float*)prev.data, prev.count, prev.stride_bytes / 4, a, no_imu, 0.0);
   if (rc) return rc;
-  rc = sr_body(c, (const float*)cur.data, cur.count, cur.stride_bytes / 4, b);
+  rc = sr_body(c, (const float*)cur.data, cur.count, cur.stride_bytes / 4, b, no_imu, 0.1);
   if (rc) return rc;
   OdState od;
   od.inited = true;

@@ -80,6 +80,8 @@ def lib():
                                      ctypes.POINTER(CloudOut), ctypes.POINTER(Pose6),
                                      ctypes.POINTER(Pose6), ctypes.POINTER(CloudOut)]
         L.oracle_maintenance.argtypes = [ctypes.POINTER(Pose6)] * 4
+        L.oracle_imu.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.POINTER(ctypes.c_double),
+                                 ctypes.POINTER(ctypes.c_double)]
         L.oracle_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(Stats)]
         L.oracle_problem.argtypes = [ctypes.POINTER(Config), CloudIn, CloudIn, ctypes.POINTER(Pose6),
                                      ctypes.POINTER(Pose6), ctypes.POINTER(Stats)]
@@ -129,7 +131,9 @@ def make_features(cap):
 def features_to_dict(f, bufs):
     # ctypes copies the CloudOut structs into Features: read counts from f
     names = ["full", "sharp", "less_sharp", "flat", "less_flat"]
-    return {n: b.arr[:getattr(f, n).count].copy() for n, b in zip(names, bufs)}
+    d = {n: b.arr[:getattr(f, n).count].copy() for n, b in zip(names, bufs)}
+    d["imu_trans"] = np.array(f.imu_trans[:], np.float32)
+    return d
 
 
 class Oracle:
@@ -144,6 +148,11 @@ class Oracle:
         if getattr(self, "h", None):
             lib().oracle_destroy(self.h)
             self.h = None
+
+    def imu(self, stamp, quat_xyzw, lin_acc):
+        q = (ctypes.c_double * 4)(*[float(v) for v in quat_xyzw])
+        a = (ctypes.c_double * 3)(*[float(v) for v in lin_acc])
+        assert lib().oracle_imu(self.h, stamp, q, a) == 0
 
     def scan_registration(self, raw, stamp=0.0):
         ci, keep = cloud_in(raw)
@@ -161,6 +170,8 @@ class Oracle:
             keep.append(a)
             cl.append(CloudOut(a.ctypes.data if a.shape[0] else None, a.shape[0], a.shape[0]))
         f = Features(*cl)
+        if "imu_trans" in feats:
+            f.imu_trans[:] = [float(v) for v in feats["imu_trans"]]
         pose = Pose6()
         outs = [OutBuf(self.cap) for _ in range(3)]
         pub = ctypes.c_int(0)

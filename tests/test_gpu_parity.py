@@ -242,3 +242,54 @@ def test_maintenance_chain(loam, oc, sg):
     e.batch_run()
     od, aft, st = e.batch_download()
     np.testing.assert_array_equal(loam.maintenance(od[0], od[0], aft[0]), oc.maintenance(od[0], od[0], aft[0]))
+
+
+def _stream_imu(impl, sweeps, imus, t0, with_feats=False):
+    """config-3 style stream with /imu/data delivered up to each sweep's end before the sweep"""
+    j, poses, maps, feats = 0, [], [], []
+    for k, sw in enumerate(sweeps):
+        while j < len(imus) and imus[j][0] <= t0 + 0.1 * (k + 1):
+            impl.imu(*imus[j])
+            j += 1
+        rc, f = impl.scan_registration(sw, stamp=t0 + 0.1 * k)
+        if rc != 0:
+            continue
+        if with_feats:
+            feats.append(f)
+        pub, pose, cl, sl, full = impl.odometry(f, stamp=t0 + 0.1 * k)
+        if pub & 1:
+            poses.append(pose)
+        if pub == 7:
+            aft, bef, reg = impl.mapping(pose, cl, sl, full, stamp=t0 + 0.1 * k)
+            maps.append((aft, bef))
+    return np.array(poses), maps, feats
+
+
+def test_imu_stream_parity(loam, oc, sg):
+    # the IMU path (SURVEY §8f): per-point de-skew with the interpolated IMU state and /imu_trans
+    # (scanRegistration), the IMU prior / TransformToEnd / PluginIMURotation terms (odometry), the
+    # roll / pitch blend of transformUpdate (mapping)
+    t0 = 0.0
+    sweeps = sg.stream_sweeps(24, 1, t0=t0)
+    imus = sg.imu_stream(t0 - 0.5, t0 + 2.5, seed=1)
+    cfg = dict(system_delay=2)
+    pg, mg, fg = _stream_imu(loam.Engine(loam.default_config(**cfg)), sweeps, imus, t0, with_feats=True)
+    po, mo, fo = _stream_imu(oc.Oracle(oc.default_config(**cfg)), sweeps, imus, t0, with_feats=True)
+    assert len(fg) == len(fo) >= 20
+    for a, b in zip(fg, fo):
+        np.testing.assert_array_equal(a["imu_trans"], b["imu_trans"])
+        assert np.abs(a["imu_trans"]).max() > 0
+        for k in ("full", "sharp", "less_sharp", "flat", "less_flat"):
+            _cmp_cloud(a[k], b[k], k)
+    assert len(pg) == len(po) and np.abs(pg - po).max() <= POSE_TOL
+    assert len(mg) == len(mo) >= 8
+    for (ag, bg), (ao, bo) in zip(mg, mo):
+        assert np.abs(ag - ao).max() <= POSE_TOL
+        assert np.abs(bg - bo).max() <= POSE_TOL
+
+
+def test_imu_errors(loam, sg):
+    e = loam.Engine()
+    e.imu(1.0, (0, 0, 0, 1), (0, 0, 9.81))
+    with pytest.raises(loam.LoamError):
+        e.imu(0.5, (0, 0, 0, 1), (0, 0, 9.81))   # stamps must be non-decreasing
