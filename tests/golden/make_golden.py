@@ -55,6 +55,26 @@ def main():
             rec.update(aft=a.tolist(), bef=b.tolist(), registered_sha256=digest(reg))
         traj.append(rec)
     out["config3_first30"] = traj
+    # config 3 with /imu/data: IMU messages up to each sweep's end, stamps 0.1 s apart
+    sweeps = sg.stream_sweeps(24, 1, t0=0.0)
+    imus = sg.imu_stream(-0.5, 2.5, seed=1)
+    o = oc.Oracle(oc.default_config(system_delay=2))
+    traj, j = [], 0
+    for k, sw in enumerate(sweeps):
+        while j < len(imus) and imus[j][0] <= 0.1 * (k + 1):
+            o.imu(*imus[j])
+            j += 1
+        rc, f = o.scan_registration(sw, stamp=0.1 * k)
+        if rc:
+            continue
+        pub, pose, cl, sl, full = o.odometry(f, stamp=0.1 * k)
+        rec = {"pub": int(pub), "imu_trans": f["imu_trans"].tolist(), "less_flat_sha256": digest(f["less_flat"]),
+               "od_sum": pose.tolist() if pub & 1 else None}
+        if pub == 7:
+            a, b, reg = o.mapping(pose, cl, sl, full, stamp=0.1 * k)
+            rec.update(aft=a.tolist(), bef=b.tolist(), registered_sha256=digest(reg))
+        traj.append(rec)
+    out["config3_imu_first24"] = traj
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle_golden.json")
     json.dump(out, open(path, "w"), indent=1)
     print("wrote", path)

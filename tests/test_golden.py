@@ -36,3 +36,41 @@ def test_config4_first8(oc, sg):
         od, aft, _ = oc.problem(prevs[i], curs[i])
         np.testing.assert_array_equal(od, np.float32(G["config4_first8"][i]["od_sum"]))
         np.testing.assert_array_equal(aft, np.float32(G["config4_first8"][i]["aft"]))
+
+
+def _imu_stream(impl, sg):
+    sweeps = sg.stream_sweeps(24, 1, t0=0.0)
+    imus = sg.imu_stream(-0.5, 2.5, seed=1)
+    traj, j = [], 0
+    for k, sw in enumerate(sweeps):
+        while j < len(imus) and imus[j][0] <= 0.1 * (k + 1):
+            impl.imu(*imus[j])
+            j += 1
+        rc, f = impl.scan_registration(sw, stamp=0.1 * k)
+        if rc:
+            continue
+        pub, pose, cl, sl, full = impl.odometry(f, stamp=0.1 * k)
+        rec = {"pub": pub, "imu_trans": f["imu_trans"], "lflat": digest(f["less_flat"]), "od": pose}
+        if pub == 7:
+            a, b, reg = impl.mapping(pose, cl, sl, full, stamp=0.1 * k)
+            rec.update(aft=a, bef=b, reg=digest(reg))
+        traj.append(rec)
+    return traj
+
+
+def check_imu_traj(traj, tol=0.0):
+    g = G["config3_imu_first24"]
+    assert len(traj) == len(g)
+    for r, e in zip(traj, g):
+        assert r["pub"] == e["pub"]
+        np.testing.assert_array_equal(r["imu_trans"], np.float32(e["imu_trans"]))
+        assert r["lflat"] == e["less_flat_sha256"]
+        if e["od_sum"] is not None:
+            assert np.abs(r["od"] - np.float32(e["od_sum"])).max() <= tol
+        if "aft" in e:
+            assert np.abs(r["aft"] - np.float32(e["aft"])).max() <= tol
+            assert np.abs(r["bef"] - np.float32(e["bef"])).max() <= tol
+
+
+def test_config3_imu_oracle(oc, sg):
+    check_imu_traj(_imu_stream(oc.Oracle(oc.default_config(system_delay=2)), sg))

@@ -293,3 +293,8 @@ def test_imu_errors(loam, sg):
     e.imu(1.0, (0, 0, 0, 1), (0, 0, 9.81))
     with pytest.raises(loam.LoamError):
         e.imu(0.5, (0, 0, 0, 1), (0, 0, 9.81))   # stamps must be non-decreasing
+
+
+def test_golden_config3_imu(loam, sg):
+    from test_golden import _imu_stream, check_imu_traj
+    check_imu_traj(_imu_stream(loam.Engine(loam.default_config(system_delay=2)), sg), tol=POSE_TOL)
