@@ -13,8 +13,9 @@
 //  k_od_rows      lane per query: residual + weight of this iteration stored per (iteration, query)
 //                 (the row order of the reference's append, Q12), J of every row accumulated so far
 //                 at the current transform, JᵀJ / Jᵀb partial sums in fp64
-//  k_od_step      wave per problem: fixed-order sum of the partials, 6x6 QR solve / iteration-0
-//                 degeneracy analysis on one lane, NaN guard, convergence test
+//                 the last workgroup of a problem to finish then sums the partials in a fixed
+//                 order and runs the 6x6 QR solve / iteration-0 degeneracy analysis on one lane,
+//                 NaN guard, convergence test (od_step)
 //  k_od_fini      pose accumulation (:830-856)
 //  k_od_end       TransformToEnd of lessSharp / lessFlat / full (:875-891) into the next Last clouds.
 #include "dev_common.hpp"
@@ -338,7 +339,8 @@ LOAM_D void wave_assoc_surf(const float4* SL, const float4* ch, int fwd_end, uin
 
 // ---------------------------------------------------------------- the L-M loop, split per iteration
 // Launch sequence per problem batch (od_solve): k_od_begin, then for iter = 0..max_iter-1
-// [k_od_assoc when iter % 5 == 0] k_od_rows k_od_step, then k_od_fini.  A problem that has
+// [k_od_assoc when iter % 5 == 0] k_od_rows + k_od_step (fused for small batches), then k_od_fini.
+// A problem that has
 // converged (or never runs L-M) makes every later launch return at once.
 
 __global__ void k_od_begin(OdBuffers b, FeatView f) {
@@ -359,6 +361,7 @@ __global__ void k_od_begin(OdBuffers b, FeatView f) {
   ist[kIsIters] = 0;
   ist[kIsAssoc] = 0;
   ist[kIsRows] = 0;
+  b.done[p] = 0;
 }
 
 // TransformToStart of every query at the current transform (:472, :587), lane per query, for
@@ -414,11 +417,42 @@ __global__ __launch_bounds__(kOdThreads) void k_od_assoc(OdBuffers b, FeatView f
   }
 }
 
+// the 6x6 step of one iteration (:697-828) of problem p on one lane, from the fixed-order sum of
+// the workgroup partials: QR solve / iteration-0 degeneracy analysis, NaN guard, convergence test
+LOAM_D void od_step(const OdBuffers& b, int p, int iter, const double* tot, float* AtA, float* AtB, float* X,
+                    float* lm_ws, int* lm_iws) {
+  int* ist = b.istate + (size_t)p * kOdStateInts;
+  float* st = b.state + (size_t)p * kOdStateFloats;
+  const int nrows = (int)tot[27];
+  ist[kIsIters] = iter + 1;
+  if (iter % 5 == 0) ist[kIsAssoc] += 1;
+  ist[kIsRows] += nrows;
+  if (nrows >= 10) {  // :697-700
+    int k = 0;
+    for (int i = 0; i < 6; ++i)
+      for (int jj = i; jj < 6; ++jj) {
+        AtA[i * 6 + jj] = (float)tot[k];
+        AtA[jj * 6 + i] = (float)tot[k];
+        ++k;
+      }
+    for (int i = 0; i < 6; ++i) AtB[i] = (float)tot[21 + i];
+    int degen = ist[kIsDegenerate];
+    loamla::lm_step(AtA, AtB, iter, 10.0f, &degen, st + kOdMatP, X, lm_ws, lm_iws);
+    ist[kIsDegenerate] = degen;
+    const bool nan = isnan(X[0]) || isnan(X[1]) || isnan(X[2]) || isnan(X[3]) || isnan(X[4]) || isnan(X[5]);
+    if (!nan)  // Q16
+      for (int q = 0; q < 6; ++q) st[q] += X[q];
+    const float dR = loamla::delta_r(X), dT = loamla::delta_t(X);
+    if (D(dR) < 0.1 && D(dT) < 0.1) ist[kIsStop] = 1;
+  }
+}
+
 // one iteration's rows (lane per query): this iteration's residual + weight (:530-583,
 // :653-694) stored at [iter][q]; then the Jacobian of every row accumulated so far (Q12: rows
 // of iterations 0..iter, all evaluated at the current transform, :708-764) summed in fp64 into
 // this workgroup's partial JᵀJ / Jᵀb / row count.  A rejected correspondence is stored as a zero
 // coefficient, which adds exact zeros.
+template <bool FUSED>
 __global__ __launch_bounds__(kOdThreads) void k_od_rows(OdBuffers b, FeatView f, int last_buf, int iter) {
   const int p = blockIdx.y, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const int* ist = b.istate + (size_t)p * kOdStateInts;
@@ -550,14 +584,36 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows(OdBuffers b, FeatView f,
     double v = red[0][tid];
     for (int ww = 1; ww < kOdWaves; ++ww) v += red[ww][tid];
     b.part[((size_t)p * b.gq + blockIdx.x) * 28 + tid] = v;
+    if (FUSED) __threadfence();  // partials visible device-wide before this workgroup reports done
+  }
+  if (!FUSED) return;
+  // small batches (streaming): the last workgroup of the problem to finish runs the 6x6 step,
+  // saving a dependent launch per iteration; large batches launch k_od_step instead
+  __shared__ int sh_last;
+  __shared__ double tot[28];
+  __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs];
+  __shared__ int lm_iws[12];
+  __syncthreads();
+  if (tid == 0) sh_last = atomicAdd(&b.done[p], 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!sh_last) return;
+  if (tid < 28) {  // fixed order over the workgroups
+    double v = 0.0;
+    for (int g = 0; g < (int)gridDim.x; ++g)
+      v += __hip_atomic_load(&b.part[((size_t)p * b.gq + g) * 28 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tot[tid] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    b.done[p] = 0;
+    od_step(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws);
   }
 }
 
-// the 6x6 step of one iteration (:697-828), one wave per problem: fixed-order sum of the
-// workgroup partials, QR solve / iteration-0 degeneracy analysis, NaN guard, convergence test
+// the step as its own launch (large batches): one wave per problem
 __global__ __launch_bounds__(64) void k_od_step(OdBuffers b, int iter, int gq) {
   const int p = blockIdx.x, lane = threadIdx.x;
-  int* ist = b.istate + (size_t)p * kOdStateInts;
+  const int* ist = b.istate + (size_t)p * kOdStateInts;
   if (!ist[kIsActive] || ist[kIsStop]) return;
   __shared__ double tot[28];
   __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs];
@@ -568,30 +624,7 @@ __global__ __launch_bounds__(64) void k_od_step(OdBuffers b, int iter, int gq) {
     tot[lane] = v;
   }
   __syncthreads();
-  if (lane != 0) return;
-  float* st = b.state + (size_t)p * kOdStateFloats;
-  const int nrows = (int)tot[27];
-  ist[kIsIters] = iter + 1;
-  if (iter % 5 == 0) ist[kIsAssoc] += 1;
-  ist[kIsRows] += nrows;
-  if (nrows >= 10) {  // :697-700
-    int k = 0;
-    for (int i = 0; i < 6; ++i)
-      for (int jj = i; jj < 6; ++jj) {
-        AtA[i * 6 + jj] = (float)tot[k];
-        AtA[jj * 6 + i] = (float)tot[k];
-        ++k;
-      }
-    for (int i = 0; i < 6; ++i) AtB[i] = (float)tot[21 + i];
-    int degen = ist[kIsDegenerate];
-    loamla::lm_step(AtA, AtB, iter, 10.0f, &degen, st + kOdMatP, X, lm_ws, lm_iws);
-    ist[kIsDegenerate] = degen;
-    const bool nan = isnan(X[0]) || isnan(X[1]) || isnan(X[2]) || isnan(X[3]) || isnan(X[4]) || isnan(X[5]);
-    if (!nan)  // Q16
-      for (int q = 0; q < 6; ++q) st[q] += X[q];
-    const float dR = loamla::delta_r(X), dT = loamla::delta_t(X);
-    if (D(dR) < 0.1 && D(dT) < 0.1) ist[kIsStop] = 1;
-  }
+  if (lane == 0) od_step(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws);
 }
 
 // pose accumulation (:830-856) for every problem
@@ -675,6 +708,8 @@ void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   (void)hipMalloc(&b.q_cf, (size_t)P * max_iter * b.cap_q * sizeof(float4));
   (void)hipMalloc(&b.q_ok, (size_t)P * max_iter * b.cap_q * sizeof(int8_t));
   (void)hipMalloc(&b.part, (size_t)P * b.gq * 28 * sizeof(double));
+  (void)hipMalloc(&b.done, (size_t)P * sizeof(int));
+  (void)hipMemset(b.done, 0, (size_t)P * sizeof(int));
   (void)hipMemset(b.state, 0, (size_t)P * kOdStateFloats * sizeof(float));
   (void)hipMemset(b.istate, 0, (size_t)P * kOdStateInts * sizeof(int));
   (void)hipMemset(b.nlast, 0, (size_t)P * 4 * sizeof(int));
@@ -686,7 +721,7 @@ void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
 void od_free(OdBuffers& b) {
   void* ptrs[] = {b.state, b.istate, b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
-                  b.ind, b.sel, b.q_cf, b.q_ok, b.part};
+                  b.ind, b.sel, b.q_cf, b.q_ok, b.part, b.done};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = OdBuffers();
@@ -733,13 +768,20 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
   for (int it = 0; it < b.max_iter; ++it) {
     if (it % 5 == 0) {  // Q10
       hipLaunchKernelGGL(k_od_sel, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f);
-      hipLaunchKernelGGL(k_od_assoc, dim3(16, P), dim3(kOdThreads), 0, st, b, f, last_buf);
+      // one wave per query when the batch is small (streaming), 64 waves per problem otherwise
+      const int ga = P >= 64 ? 16 : (b.cap_q + kOdWaves - 1) / kOdWaves;
+      hipLaunchKernelGGL(k_od_assoc, dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
       mark("k_od_assoc");
     }
-    hipLaunchKernelGGL(k_od_rows, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
-    mark("k_od_rows");
-    hipLaunchKernelGGL(k_od_step, dim3(P), dim3(64), 0, st, b, it, b.gq);
-    mark("k_od_step");
+    if (P < 64) {
+      hipLaunchKernelGGL(k_od_rows<true>, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+      mark("k_od_rows");
+    } else {
+      hipLaunchKernelGGL(k_od_rows<false>, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+      mark("k_od_rows");
+      hipLaunchKernelGGL(k_od_step, dim3(P), dim3(64), 0, st, b, it, b.gq);
+      mark("k_od_step");
+    }
   }
   hipLaunchKernelGGL(k_od_fini, dim3((P + 255) / 256), dim3(256), 0, st, b, f);
 }

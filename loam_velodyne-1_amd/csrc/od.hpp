@@ -71,6 +71,7 @@ struct OdBuffers {
   float4* q_cf = nullptr;     // [P][max_iter][cap_q] coefficients (zero when rejected)
   int8_t* q_ok = nullptr;     // [P][max_iter][cap_q] accepted flags
   double* part = nullptr;     // [P][gq][28] per-workgroup JᵀJ | Jᵀb | rows
+  int* done = nullptr;        // [P] workgroups of k_od_rows finished (the last one runs the step)
 };
 
 __global__ void k_hash_build(HashJob j);
