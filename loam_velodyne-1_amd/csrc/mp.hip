@@ -196,16 +196,17 @@ __global__ __launch_bounds__(256) void k_mp_stack(MpBuffers b, MpInput in) {
 // for the few large stack segments.
 template <int G>
 struct VgGroup {
+  static constexpr int NT = G < 256 ? 256 : G;  // block size
   int g, t;  // group index in the grid, thread index in the group
-  LOAM_D VgGroup() : g((blockIdx.x * 256 + threadIdx.x) / G), t(threadIdx.x % G) {}
-  LOAM_D static int stride() { return gridDim.x * (256 / G); }
+  LOAM_D VgGroup() : g((blockIdx.x * NT + threadIdx.x) / G), t(threadIdx.x % G) {}
+  LOAM_D static int stride() { return gridDim.x * (NT / G); }
   LOAM_D float min(float v, float* sc) {
     if constexpr (G == 64) return wave_min_f(v);
-    else return block_reduce<256>(v, sc, [](float a, float c) { return fminf(a, c); });
+    else return block_reduce<NT>(v, sc, [](float a, float c) { return fminf(a, c); });
   }
   LOAM_D float max(float v, float* sc) {
     if constexpr (G == 64) return wave_max_f(v);
-    else return block_reduce<256>(v, sc, [](float a, float c) { return fmaxf(a, c); });
+    else return block_reduce<NT>(v, sc, [](float a, float c) { return fmaxf(a, c); });
   }
   LOAM_D int excl_scan(int v, int* sc, int& total) {  // v in {0, 1}
     if constexpr (G == 64) {
@@ -213,14 +214,14 @@ struct VgGroup {
       total = __popcll(m);
       return __popcll(m & lanemask_lt());
     } else {
-      return block_excl_scan<256>(v, sc, total);
+      return block_excl_scan<NT>(v, sc, total);
     }
   }
 };
 
 template <int G>
-__global__ __launch_bounds__(256) void k_vg_params(VgJob j) {
-  __shared__ float fsc[8];
+__global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_params(VgJob j) {
+  __shared__ float fsc[16];
   VgGroup<G> grp;
   for (int s = grp.g; s < j.nseg; s += VgGroup<G>::stride()) {
     const int b0 = j.begin[s], b1 = j.end[s];
@@ -258,7 +259,7 @@ __global__ __launch_bounds__(256) void k_vg_params(VgJob j) {
 }
 
 template <int G>
-__global__ __launch_bounds__(256) void k_vg_keys(VgJob j) {
+__global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_keys(VgJob j) {
   VgGroup<G> grp;
   for (int s = grp.g; s < j.nseg; s += VgGroup<G>::stride()) {
     const int b0 = j.begin[s], b1 = j.end[s];
@@ -285,8 +286,8 @@ __global__ __launch_bounds__(256) void k_vg_keys(VgJob j) {
 // one output point per run of equal keys: the float mean of x, y, z, intensity summed in sorted
 // order (the reference's VoxelGrid)
 template <int G>
-__global__ __launch_bounds__(256) void k_vg_reduce(VgJob j) {
-  __shared__ int isc[16];
+__global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
+  __shared__ int isc[24];
   VgGroup<G> grp;
   for (int s = grp.g; s < j.nseg; s += VgGroup<G>::stride()) {
     const int b0 = j.begin[s], b1 = j.end[s];
@@ -327,21 +328,30 @@ __global__ __launch_bounds__(256) void k_vg_reduce(VgJob j) {
   }
 }
 
-void vg_run(const VgJob& j, void* tmp, size_t tmp_bytes, hipStream_t st, bool many_small) {
+template <int G>
+void vg_launch_params_keys(const VgJob& j, hipStream_t st) {
+  const int grid = std::min((j.nseg + VgGroup<G>::NT / G - 1) / (VgGroup<G>::NT / G), 4096);
+  hipLaunchKernelGGL(k_vg_params<G>, dim3(grid), dim3(VgGroup<G>::NT), 0, st, j);
+  hipLaunchKernelGGL(k_vg_keys<G>, dim3(grid), dim3(VgGroup<G>::NT), 0, st, j);
+}
+template <int G>
+void vg_launch_reduce(const VgJob& j, hipStream_t st) {
+  const int grid = std::min((j.nseg + VgGroup<G>::NT / G - 1) / (VgGroup<G>::NT / G), 4096);
+  hipLaunchKernelGGL(k_vg_reduce<G>, dim3(grid), dim3(VgGroup<G>::NT), 0, st, j);
+}
+
+// G = threads per segment: 64 for many mostly-empty segments, 256 / 1024 for few large ones
+void vg_run(const VgJob& j, void* tmp, size_t tmp_bytes, hipStream_t st, int G) {
   if (j.nseg == 0) return;
-  const int grid = many_small ? std::min((j.nseg + 3) / 4, 4096) : std::min(j.nseg, 4096);
-  if (many_small) {
-    hipLaunchKernelGGL(k_vg_params<64>, dim3(grid), dim3(256), 0, st, j);
-    hipLaunchKernelGGL(k_vg_keys<64>, dim3(grid), dim3(256), 0, st, j);
-  } else {
-    hipLaunchKernelGGL(k_vg_params<256>, dim3(grid), dim3(256), 0, st, j);
-    hipLaunchKernelGGL(k_vg_keys<256>, dim3(grid), dim3(256), 0, st, j);
-  }
+  if (G == 64) vg_launch_params_keys<64>(j, st);
+  else if (G == 256) vg_launch_params_keys<256>(j, st);
+  else vg_launch_params_keys<1024>(j, st);
   size_t bytes = tmp_bytes;
   (void)hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
                                                     j.nseg, j.begin, j.end, 0, 32, st);
-  if (many_small) hipLaunchKernelGGL(k_vg_reduce<64>, dim3(grid), dim3(256), 0, st, j);
-  else hipLaunchKernelGGL(k_vg_reduce<256>, dim3(grid), dim3(256), 0, st, j);
+  if (G == 64) vg_launch_reduce<64>(j, st);
+  else if (G == 256) vg_launch_reduce<256>(j, st);
+  else vg_launch_reduce<1024>(j, st);
 }
 
 size_t vg_tmp_bytes(int total, int nseg) {
@@ -1118,7 +1128,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
   js.in = b.stack2; js.out = b.stack; js.begin = b.sseg_b; js.end = b.sseg_e; js.leaf = b.sseg_leaf;
   js.out_count = b.sseg_cnt; js.params = b.vg_params; js.keys = b.vg_k; js.keys_alt = b.vg_k2;
   js.vals = b.vg_v; js.vals_alt = b.vg_v2; js.nseg = 2 * P; js.total = P * b.cap_stack;
-  vg_run(js, b.cub_tmp, b.cub_bytes, st, false);
+  vg_run(js, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 1024 : 256);  // two large segments per instance
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);
   mark("k_mp_gather");
@@ -1156,7 +1166,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
   jv.in = b.vin; jv.out = b.vout; jv.begin = b.vseg_b; jv.end = b.vseg_e; jv.leaf = b.vseg_leaf;
   jv.out_count = b.vseg_cnt; jv.params = b.vg_params; jv.keys = b.vg_k; jv.keys_alt = b.vg_k2;
   jv.vals = b.vg_v; jv.vals_alt = b.vg_v2; jv.nseg = 2 * kMaxValid * P; jv.total = P * b.map_cap;
-  vg_run(jv, b.cub_tmp, b.cub_bytes, st, true);
+  vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 256 : 64);    // 2 x 125 cube segments per instance
   mark("vg_cubes");
   hipLaunchKernelGGL(k_mp_compact_table, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);
