@@ -10,6 +10,7 @@
  *                              (inputs = what handlers :275-354 store)
  *   loam_mapping            <- laserMapping loop body   src/laserMapping.cpp:411-1097
  *                              (inputs = what handlers :274-321 store)
+ *   loam_mapping_surround   <- /laser_cloud_surround    src/laserMapping.cpp:1038-1058
  *   loam_maintenance        <- transformMaintenance     src/transformMaintenance.cpp:147-203
  *   loam_batch_*            <- config 4 of BASELINE.json (independent problems, no reference
  *                              equivalent: one problem = the bodies above composed)
@@ -130,6 +131,15 @@ int loam_mapping(loam_ctx *ctx, double stamp, const loam_pose6 *odom_sum,
                  const loam_cloud_out *corner_last, const loam_cloud_out *surf_last,
                  const loam_cloud_out *full_end, loam_pose6 *aft, loam_pose6 *bef,
                  loam_cloud_out *registered);
+
+/* = the /laser_cloud_surround publish of the laserMapping loop body (src/laserMapping.cpp:1038-1058,
+ * mapFrameNum = 5, :52, :405): the map store's 5x5x5 cube neighbourhood of the last mapping frame
+ * (laserCloudSurroundInd, :617-670), corner then surf points per cube, VoxelGrid 0.2.  The
+ * reference publishes it on the 1st successful loam_mapping frame and every 5th after it: on
+ * those frames *published = 1 and out is filled; otherwise *published = 0 and out->count = 0.
+ * Call between a loam_mapping and the next (the cloud is computed on demand from the store that
+ * frame left; a LOAM_E_CAPACITY call may be repeated with more capacity). */
+int loam_mapping_surround(loam_ctx *ctx, loam_cloud_out *out, int *published);
 
 /* = transformMaintenance laserOdometryHandler with the last odomAftMappedHandler state.
  * Pure host function (scalar pose algebra, no kernel). */

@@ -82,7 +82,8 @@ class Stats(ctypes.Structure):
 
 
 EXPORTS = ("loam_config_default", "loam_create", "loam_destroy", "loam_last_error", "loam_imu",
-           "loam_scan_registration", "loam_odometry", "loam_mapping", "loam_maintenance",
+           "loam_scan_registration", "loam_odometry", "loam_mapping", "loam_mapping_surround",
+           "loam_maintenance",
            "loam_batch_upload", "loam_batch_run", "loam_batch_sync", "loam_batch_download", "loam_get_stats",
            "loam_set_profiling", "loam_get_kernel_times")
 
@@ -104,6 +105,7 @@ def lib():
                                     P(CloudOut), P(ctypes.c_int)]
         L.loam_mapping.argtypes = [PP, ctypes.c_double, P(Pose6), P(CloudOut), P(CloudOut), P(CloudOut),
                                    P(Pose6), P(Pose6), P(CloudOut)]
+        L.loam_mapping_surround.argtypes = [PP, P(CloudOut), P(ctypes.c_int)]
         L.loam_maintenance.argtypes = [P(Pose6)] * 4
         L.loam_batch_upload.argtypes = [PP, ctypes.c_uint32, P(CloudIn), P(CloudIn)]
         L.loam_batch_run.argtypes = [PP]
@@ -209,6 +211,18 @@ class Engine:
                                   ctypes.byref(refs[1][0]), ctypes.byref(refs[2][0]), ctypes.byref(aft),
                                   ctypes.byref(bef), ctypes.byref(reg.c)))
         return aft.arr(), bef.arr(), reg.get()
+
+    def mapping_surround(self, cap=1 << 16):
+        """/laser_cloud_surround of the last mapping frame (laserMapping.cpp:1038-1058): an (n, 4)
+        array on the frames the reference publishes it (1st, then every 5th), else None"""
+        pub = ctypes.c_int(0)
+        out = _Out(cap)
+        rc = lib().loam_mapping_surround(self.h, ctypes.byref(out.c), ctypes.byref(pub))
+        if rc == LOAM_E_CAPACITY:
+            out = _Out(int(out.c.count))
+            rc = lib().loam_mapping_surround(self.h, ctypes.byref(out.c), ctypes.byref(pub))
+        _check(rc)
+        return out.get() if pub.value else None
 
     # --- config 4
     def batch_upload(self, prevs, curs):

@@ -74,6 +74,8 @@ struct loam_ctx {
   bool od_inited = false;
   int od_last = 0, od_frame_count = 1;
   MpBuffers mp1;        // streaming map
+  int map_frame_count = 4;    // mapFrameCount = mapFrameNum - 1 (src/laserMapping.cpp:405)
+  bool surround_due = false;  // the last loam_mapping frame publishes /laser_cloud_surround
   // IMU (loam_imu): scanRegistration's queue (host master copy, uploaded per sweep) and
   // laserMapping's queue
   loamimu::SrQueue* sr_imu = nullptr;     // host
@@ -426,6 +428,25 @@ int loam_mapping(loam_ctx* x, double stamp, const loam_pose6* odom_sum, const lo
   const int rc = mp_stream_frame(x->mp1, x->st, *odom_sum, *corner_last, *surf_last, *full_end, aft, bef,
                                  registered, &x->stats, g_err, have_imu ? rp : nullptr, &updated);
   if (have_imu && updated) x->mp_imu.front = front;  // the pointer walk happens inside transformUpdate
+  x->surround_due = false;
+  if (rc == LOAM_OK && ++x->map_frame_count >= 5) {  // :1038-1040
+    x->map_frame_count = 0;
+    x->surround_due = true;
+  }
+  return rc;
+}
+
+int loam_mapping_surround(loam_ctx* x, loam_cloud_out* out, int* published) {
+  if (!x || !out || !published) return fail(LOAM_E_INVAL, "null argument");
+  *published = 0;
+  if (!x->surround_due) {
+    out->count = 0;
+    return LOAM_OK;
+  }
+  if (out->capacity && !out->pts) return fail(LOAM_E_INVAL, "surround cloud pts is null");
+  HIP_TRY(hipSetDevice(x->device));
+  const int rc = mp_stream_surround(x->mp1, x->st, out, g_err);
+  if (rc == LOAM_OK) *published = 1;
   return rc;
 }
 

@@ -81,6 +81,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_prepare(MpBuffers b, MpInput 
     while (cK >= kCubeD - 3 && n < 255) { sh_shift[n++] = 2 * 2 + 0; cK--; cD--; }
     sh_nshift = n;
     sh_c[0] = cI; sh_c[1] = cJ; sh_c[2] = cK;
+    ist[kMiCubeI] = cI; ist[kMiCubeJ] = cJ; ist[kMiCubeK] = cK;
     ist[kMiCenW] = cW; ist[kMiCenH] = cH; ist[kMiCenD] = cD;
   }
   __syncthreads();
@@ -1254,6 +1255,72 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
     stats->ms_mp = ms;
   }
   return rc;
+}
+
+// /laser_cloud_surround input (:1042-1047): every in-bounds cube of the 5x5x5 neighbourhood of the
+// frame's centre cube (laserCloudSurroundInd, :617-670, FOV test or not) in (i, j, k) loop order,
+// each cube's corner points then its surf points, from the store the frame left; one VoxelGrid
+// segment (leaf 0.2, downSizeFilterCorner) over vin.
+__global__ __launch_bounds__(256) void k_mp_surround(MpBuffers b) {
+  const int tid = threadIdx.x;
+  const int* ist = b.istate;
+  const int* slots = slot_table(b, b.pool_cur, 0);
+  const float4* pool = b.pool + (size_t)b.pool_cur * b.P * b.map_cap;
+  __shared__ int sh_ind[kMaxValid], sh_pre[kMaxValid + 1], sh_n;
+  if (tid == 0) {
+    const int cI = ist[kMiCubeI], cJ = ist[kMiCubeJ], cK = ist[kMiCubeK];
+    int n = 0, acc = 0;
+    for (int i = cI - 2; i <= cI + 2; ++i)
+      for (int j = cJ - 2; j <= cJ + 2; ++j)
+        for (int k = cK - 2; k <= cK + 2; ++k) {
+          if (!(i >= 0 && i < kCubeW && j >= 0 && j < kCubeH && k >= 0 && k < kCubeD)) continue;
+          const int ind = cube_index(i, j, k);
+          sh_ind[n] = ind;
+          sh_pre[n] = acc;
+          acc += slots[ind * 4 + 1] + slots[ind * 4 + 3];
+          ++n;
+        }
+    sh_pre[n] = acc;
+    sh_n = n;
+    b.vseg_b[0] = 0;
+    b.vseg_e[0] = acc;
+    b.vseg_leaf[0] = 0.2f;
+  }
+  __syncthreads();
+  const int n = sh_n;
+  for (int c = 0; c < n; ++c) {
+    const int ind = sh_ind[c], nc = slots[ind * 4 + 1], ns = slots[ind * 4 + 3];
+    const int oc = slots[ind * 4 + 0], os = slots[ind * 4 + 2];
+    float4* dst = b.vin + sh_pre[c];
+    for (int t = tid; t < nc + ns; t += 256) dst[t] = t < nc ? pool[oc + t] : pool[os + (t - nc)];
+  }
+}
+
+int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::string& err) {
+  hipLaunchKernelGGL(k_mp_surround, dim3(1), dim3(256), 0, st, b);
+  VgJob j;
+  j.in = b.vin; j.out = b.vout; j.begin = b.vseg_b; j.end = b.vseg_e; j.leaf = b.vseg_leaf;
+  j.out_count = b.vseg_cnt; j.params = b.vg_params; j.keys = b.vg_k; j.keys_alt = b.vg_k2;
+  j.vals = b.vg_v; j.vals_alt = b.vg_v2; j.nseg = 1; j.total = b.P * b.map_cap;
+  vg_run(j, b.cub_tmp, b.cub_bytes, st, 1024);
+  int cnt = 0;
+  (void)hipMemcpyAsync(&cnt, b.vseg_cnt, sizeof(int), hipMemcpyDeviceToHost, st);
+  const hipError_t he = hipStreamSynchronize(st);
+  if (he != hipSuccess) {
+    err = std::string("surround: ") + hipGetErrorString(he);
+    return LOAM_E_HIP;
+  }
+  if ((uint32_t)cnt > out->capacity) {
+    out->count = (uint32_t)cnt;
+    err = "surround cloud capacity too small";
+    return LOAM_E_CAPACITY;
+  }
+  out->count = (uint32_t)cnt;
+  if (cnt && hipMemcpy(out->pts, b.vout, (size_t)cnt * sizeof(float4), hipMemcpyDeviceToHost) != hipSuccess) {
+    err = "surround download failed";
+    return LOAM_E_HIP;
+  }
+  return LOAM_OK;
 }
 
 void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof) {

@@ -19,7 +19,8 @@ constexpr int kMaxValid = 125;
 constexpr int kMpSum = 0, kMpIncre = 6, kMpTobe = 12, kMpBef = 18, kMpAft = 24, kMpMatP = 30, kMpOnY = 66,
               kMpImuRP = 69, kMpStateFloats = 72;  // kMpImuRP: IMU (roll, pitch) for transformUpdate
 enum { kMiCenW = 0, kMiCenH, kMiCenD, kMiDegen, kMiNValid, kMiIters, kMiRows, kMiStackC, kMiStackS, kMiFromC,
-       kMiFromS, kMiErr, kMiLmRan, kMiValidPts, kMiStop, kMiFits, kMiImu, kMpStateInts = 20 };
+       kMiFromS, kMiErr, kMiLmRan, kMiValidPts, kMiStop, kMiFits, kMiImu, kMiCubeI, kMiCubeJ, kMiCubeK, kMpStateInts = 20 };
+static_assert(kMiCubeK < kMpStateInts, "istate layout");
 
 // one mapping frame's inputs for every instance (device pointers)
 struct MpInput {
@@ -103,6 +104,9 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
                     const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
                     loam_cloud_out* registered, loam_stats* stats, std::string& err,
                     const float* imu_rp = nullptr, bool* updated = nullptr);
+// /laser_cloud_surround of the last streaming frame (instance 0): its 5x5x5 cube neighbourhood
+// concatenated and VoxelGrid 0.2 (src/laserMapping.cpp:1038-1058)
+int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::string& err);
 void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof = nullptr);
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err);
 

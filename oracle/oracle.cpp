@@ -1095,7 +1095,7 @@ void shift_axis(MpState& m, int axis, int dir) {
     }
 }
 
-struct MpOut { float aft[6], bef[6]; std::vector<P> registered; };
+struct MpOut { float aft[6], bef[6]; std::vector<P> registered, surround; bool surround_pub = false; };
 
 // laserMapping loop body :420-1094 (stackFrameNum = 1: every synchronised frame is processed)
 void mp_body(const Cfg& cfg, MpState& m, const std::vector<P>& cornerLast,
@@ -1125,7 +1125,7 @@ void mp_body(const Cfg& cfg, MpState& m, const std::vector<P>& cornerLast,
   while (cK >= kDp - 3) { shift_axis(m, 2, -1); cK--; m.cenD--; }
 
   // :616-672 FOV cube selection
-  std::vector<int> valid;
+  std::vector<int> valid, surround;
   for (int i = cI - 2; i <= cI + 2; ++i)
     for (int j = cJ - 2; j <= cJ + 2; ++j)
       for (int k = cK - 2; k <= cK + 2; ++k) {
@@ -1149,6 +1149,7 @@ void mp_body(const Cfg& cfg, MpState& m, const std::vector<P>& cornerLast,
               if (check1 < 0 && check2 > 0) inFOV = true;
             }
         if (inFOV) valid.push_back(i + kW * j + kW * kH * k);
+        surround.push_back(i + kW * j + kW * kH * k);  // laserCloudSurroundInd (:667-669)
       }
   // :674-681
   std::vector<P> cornerFromMap, surfFromMap;
@@ -1337,8 +1338,19 @@ void mp_body(const Cfg& cfg, MpState& m, const std::vector<P>& cornerLast,
     m.surf[ind].swap(tmp);
     m.valid_points += (uint64_t)(m.corner[ind].size() + m.surf[ind].size());
   }
+  // :1038-1058 /laser_cloud_surround: surround cubes' corner then surf points, VoxelGrid 0.2
   m.mapFrameCount++;
-  if (m.mapFrameCount >= 5) m.mapFrameCount = 0;  // surround cloud publish: out of scope (§8f)
+  out.surround_pub = false;
+  if (m.mapFrameCount >= 5) {
+    m.mapFrameCount = 0;
+    std::vector<P> sur2;
+    for (int ind : surround) {
+      sur2.insert(sur2.end(), m.corner[ind].begin(), m.corner[ind].end());
+      sur2.insert(sur2.end(), m.surf[ind].begin(), m.surf[ind].end());
+    }
+    voxel_grid(sur2, 0.2f, out.surround);
+    out.surround_pub = true;
+  }
   // :1060-1063
   out.registered.resize(full.size());
   for (size_t i = 0; i < full.size(); ++i) point_associate_to_map(T, full[i], out.registered[i]);
@@ -1369,6 +1381,8 @@ struct Oracle {
   SrImu imu;
   OdState od;
   MpState mp;
+  std::vector<P> surround;  // /laser_cloud_surround of the last mapping frame
+  bool surround_pub = false;
   loam_stats stats;
   explicit Oracle(const Cfg& c) : cfg(c) { std::memset(&stats, 0, sizeof(stats)); }
 };
@@ -1478,7 +1492,20 @@ int oracle_mapping(void* h, double stamp, const loam_pose6* odom_sum, const loam
   o->stats.mp_map_valid_points = o->mp.valid_points - vp0;
   from6(mo.aft, aft);
   from6(mo.bef, bef);
+  o->surround.swap(mo.surround);
+  o->surround_pub = mo.surround_pub;
   return write_cloud(mo.registered, registered);
+}
+
+// /laser_cloud_surround of the last oracle_mapping frame (src/laserMapping.cpp:1038-1058)
+int oracle_mapping_surround(void* h, loam_cloud_out* out, int* published) {
+  Oracle* o = static_cast<Oracle*>(h);
+  *published = o->surround_pub ? 1 : 0;
+  if (!o->surround_pub) {
+    out->count = 0;
+    return LOAM_OK;
+  }
+  return write_cloud(o->surround, out);
 }
 
 // /imu/data: scanRegistration's imuHandler (:638-660) and laserMapping's (:323-335).

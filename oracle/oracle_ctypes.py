@@ -79,6 +79,8 @@ def lib():
                                      ctypes.POINTER(CloudOut), ctypes.POINTER(CloudOut),
                                      ctypes.POINTER(CloudOut), ctypes.POINTER(Pose6),
                                      ctypes.POINTER(Pose6), ctypes.POINTER(CloudOut)]
+        L.oracle_mapping_surround.argtypes = [ctypes.c_void_p, ctypes.POINTER(CloudOut),
+                                              ctypes.POINTER(ctypes.c_int)]
         L.oracle_maintenance.argtypes = [ctypes.POINTER(Pose6)] * 4
         L.oracle_imu.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(ctypes.c_double)]
@@ -195,6 +197,17 @@ class Oracle:
                                   ctypes.byref(bef), ctypes.byref(reg.c))
         assert rc == 0, rc
         return aft.arr(), bef.arr(), reg.get()
+
+    def mapping_surround(self):
+        """/laser_cloud_surround of the last mapping frame, or None when it is not published"""
+        pub = ctypes.c_int(0)
+        out = OutBuf(1)
+        rc = lib().oracle_mapping_surround(self.h, ctypes.byref(out.c), ctypes.byref(pub))
+        if rc == -2:
+            out = OutBuf(int(out.c.count))
+            rc = lib().oracle_mapping_surround(self.h, ctypes.byref(out.c), ctypes.byref(pub))
+        assert rc == 0, rc
+        return out.get() if pub.value else None
 
     def stats(self):
         s = Stats()

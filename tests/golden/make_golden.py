@@ -53,6 +53,9 @@ def main():
         if pub == 7:
             a, b, reg = o.mapping(pose, cl, sl, full)
             rec.update(aft=a.tolist(), bef=b.tolist(), registered_sha256=digest(reg))
+            sur = o.mapping_surround()   # /laser_cloud_surround (1st mapping frame, then every 5th)
+            if sur is not None:
+                rec.update(surround_count=int(sur.shape[0]), surround_sha256=digest(sur))
         traj.append(rec)
     out["config3_first30"] = traj
     # config 3 with /imu/data: IMU messages up to each sweep's end, stamps 0.1 s apart

@@ -38,6 +38,38 @@ def test_config4_first8(oc, sg):
         np.testing.assert_array_equal(aft, np.float32(G["config4_first8"][i]["aft"]))
 
 
+def test_config3_oracle_stream(oc, sg):
+    # config 3 through the oracle: poses, registered clouds and /laser_cloud_surround cadence + digests
+    sweeps = sg.stream_sweeps(30, 1)
+    o = oc.Oracle(oc.default_config(system_delay=2))
+    traj = []
+    for sw in sweeps:
+        rc, f = o.scan_registration(sw)
+        if rc:
+            continue
+        pub, pose, cl, sl, full = o.odometry(f)
+        rec = {"pub": pub, "od": pose}
+        if pub == 7:
+            a, b, reg = o.mapping(pose, cl, sl, full)
+            sur = o.mapping_surround()
+            rec.update(aft=a, bef=b, reg=digest(reg), sur=None if sur is None else digest(sur))
+        traj.append(rec)
+    g = G["config3_first30"]
+    assert len(traj) == len(g)
+    nmap = 0
+    for r, e in zip(traj, g):
+        assert r["pub"] == e["pub"]
+        if e["od_sum"] is not None:
+            np.testing.assert_array_equal(r["od"], np.float32(e["od_sum"]))
+        if "aft" in e:
+            np.testing.assert_array_equal(r["aft"], np.float32(e["aft"]))
+            assert r["reg"] == e["registered_sha256"]
+            assert r["sur"] == e.get("surround_sha256")
+            assert (r["sur"] is not None) == (nmap % 5 == 0)   # mapFrameNum = 5, first frame publishes
+            nmap += 1
+    assert nmap >= 10
+
+
 def _imu_stream(impl, sg):
     sweeps = sg.stream_sweeps(24, 1, t0=0.0)
     imus = sg.imu_stream(-0.5, 2.5, seed=1)

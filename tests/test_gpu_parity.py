@@ -107,7 +107,7 @@ def _stream(impl, sweeps, mapping=False):
             poses.append(pose)
         if mapping and pub == 7:
             aft, bef, reg = impl.mapping(pose, cl, sl, full)
-            maps.append((aft, bef))
+            maps.append((aft, bef, impl.mapping_surround()))
     return np.array(poses), maps
 
 
@@ -149,9 +149,17 @@ def test_mapping_stream_parity(loam, oc, sg):
     pg, mg = _stream(loam.Engine(loam.default_config(**cfg)), sweeps, mapping=True)
     po, mo = _stream(oc.Oracle(oc.default_config(**cfg)), sweeps, mapping=True)
     assert len(mg) == len(mo) >= 10
-    for (ag, bg), (ao, bo) in zip(mg, mo):
+    nsur = 0
+    for k, ((ag, bg, sg_), (ao, bo, so)) in enumerate(zip(mg, mo)):
         assert np.abs(ag - ao).max() <= POSE_TOL
         assert np.abs(bg - bo).max() <= POSE_TOL
+        # /laser_cloud_surround: 1st mapping frame, then every 5th (laserMapping.cpp:1038-1058)
+        assert (sg_ is not None) == (so is not None) == (k % 5 == 0), k
+        if so is not None:
+            assert sg_.shape == so.shape and so.shape[0] > 100
+            assert np.array_equal(sg_, so), np.abs(sg_ - so).max()
+            nsur += 1
+    assert nsur >= 2
 
 
 def test_golden_config3_stream(loam, sg):
@@ -169,6 +177,8 @@ def test_golden_config3_stream(loam, sg):
         if pub == 7:
             a, b, reg = e.mapping(pose, cl, sl, full)
             rec.update(aft=a, bef=b, reg=hashlib.sha256(np.ascontiguousarray(reg, np.float32).tobytes()).hexdigest())
+            sur = e.mapping_surround()
+            rec["sur"] = None if sur is None else hashlib.sha256(np.ascontiguousarray(sur, np.float32).tobytes()).hexdigest()
         traj.append(rec)
     assert len(traj) == len(G["config3_first30"])
     for r, g in zip(traj, G["config3_first30"]):
@@ -177,6 +187,7 @@ def test_golden_config3_stream(loam, sg):
             assert np.abs(r["od"] - np.float32(g["od_sum"])).max() <= POSE_TOL
         if "aft" in g:
             assert np.abs(r["aft"] - np.float32(g["aft"])).max() <= POSE_TOL
+            assert r["sur"] == g.get("surround_sha256")
 
 
 def test_golden_config4(loam, sg):
