@@ -156,6 +156,108 @@ LOAM_D void block_bitonic_sort(uint64_t* k, int n64) {
   }
 }
 
+// ------------------------------------------------------------------ register bitonic sort (ascending)
+// Sorts the n (power of two) 64-bit keys of k[0, n) in LDS with a block of NT threads: the keys
+// move into registers (E = n / NT per thread, element g = tid * E + e), strides < E are compare-
+// exchanges inside a thread, strides < 64 E are lane exchanges (shuffles) inside a wave, and only
+// strides >= 64 E go through LDS — 3 of the 66 stages of a 2048-key sort, against a workgroup
+// barrier per stage for the plain LDS network.  k is the LDS scratch of those stages and receives
+// the sorted keys.  The initial placement of a key is irrelevant (a sort is a permutation), so the
+// loads are coalesced.
+LOAM_D uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+template <int E, int S>
+LOAM_D void reg_cmpx_intra(uint64_t (&v)[E], int base, int size) {
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    if constexpr (S < E) {
+      if ((e & S) == 0) {
+        const bool up = ((base + e) & size) == 0;
+        const uint64_t a = v[e], b = v[e + S];
+        const bool sw = (a > b) == up;
+        v[e] = sw ? b : a;
+        v[e + S] = sw ? a : b;
+      }
+    }
+  }
+}
+// WAVE: one wave sorts alone (NT = 64; every stride stays inside the wave, no workgroup barrier)
+template <int NT, int E, bool WAVE = false>
+LOAM_D void reg_bitonic_sort_n(uint64_t* k, int n) {
+  static_assert(!WAVE || NT == 64, "a wave sort has 64 lanes");
+  const int lane = __lane_id(), tid = WAVE ? lane : (int)threadIdx.x, base = tid * E;
+  constexpr int N = NT * E;
+  uint64_t v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int g = e * NT + tid;
+    v[e] = g < n ? k[g] : ~0ull;
+  }
+  if (!WAVE) __syncthreads();  // k becomes scratch
+  for (int size = 2; size <= N; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride < E) {
+        if (stride == 1) reg_cmpx_intra<E, 1>(v, base, size);
+        else if (stride == 2) reg_cmpx_intra<E, 2>(v, base, size);
+        else if (stride == 4) reg_cmpx_intra<E, 4>(v, base, size);
+        else reg_cmpx_intra<E, 8>(v, base, size);
+      } else if (stride < 64 * E) {
+        const int m = stride / E;
+        const bool lower = (lane & m) == 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const bool up = ((base + e) & size) == 0;
+          const uint64_t o = shfl_xor_u64(v[e], m);
+          const bool keep_min = lower == up;
+          v[e] = keep_min ? (o < v[e] ? o : v[e]) : (o > v[e] ? o : v[e]);
+        }
+      } else {
+        const int m = stride / E;
+        const bool lower = (tid & m) == 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) k[e * NT + tid] = v[e];
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const bool up = ((base + e) & size) == 0;
+          const uint64_t o = k[e * NT + (tid ^ m)];
+          const bool keep_min = lower == up;
+          v[e] = keep_min ? (o < v[e] ? o : v[e]) : (o > v[e] ? o : v[e]);
+        }
+        __syncthreads();
+      }
+    }
+  }
+  if (WAVE) __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+    if (base + e < n) k[base + e] = v[e];
+  if (WAVE) {
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    __syncthreads();
+  }
+}
+// one wave sorts n <= 512 keys of k (ascending); the other waves do not take part
+LOAM_D void wave_sort_u64(uint64_t* k, int n) {
+  if (n <= 64) reg_bitonic_sort_n<64, 1, true>(k, n);
+  else if (n <= 128) reg_bitonic_sort_n<64, 2, true>(k, n);
+  else if (n <= 256) reg_bitonic_sort_n<64, 4, true>(k, n);
+  else reg_bitonic_sort_n<64, 8, true>(k, n);
+}
+// n: power of two <= NT * EMAX (EMAX a power of two <= 16)
+template <int NT, int EMAX>
+LOAM_D void reg_bitonic_sort(uint64_t* k, int n) {
+  if (n <= NT || EMAX == 1) reg_bitonic_sort_n<NT, 1>(k, n);
+  else if (n <= 2 * NT || EMAX == 2) reg_bitonic_sort_n<NT, (EMAX < 2 ? EMAX : 2)>(k, n);
+  else if (n <= 4 * NT || EMAX == 4) reg_bitonic_sort_n<NT, (EMAX < 4 ? EMAX : 4)>(k, n);
+  else if (n <= 8 * NT || EMAX == 8) reg_bitonic_sort_n<NT, (EMAX < 8 ? EMAX : 8)>(k, n);
+  else reg_bitonic_sort_n<NT, (EMAX < 16 ? EMAX : 16)>(k, n);
+}
+
 LOAM_HD int next_pow2(int v) {
   int p = 1;
   while (p < v) p <<= 1;

@@ -31,6 +31,19 @@ namespace loam {
 
 namespace {
 
+#ifdef LOAM_EXP_PHASES
+// diagnostic build only: per-phase cycle sums of select_ring (tools/exp_phases.py)
+__device__ unsigned long long g_phase[8];
+#define PH(k)                                                   \
+  if (!BIG && threadIdx.x == 0) {                               \
+    const long long now = clock64();                            \
+    atomicAdd(&g_phase[k], (unsigned long long)(now - ph_t));   \
+    ph_t = now;                                                 \
+  }
+#else
+#define PH(k)
+#endif
+
 LOAM_D int ring_id(const SrParams& p, float angle) {
   if (p.ring_model == LOAM_RING_LINEAR) {
     const float step = (p.ring_hi - p.ring_lo) / (float)(p.R - 1);
@@ -355,10 +368,10 @@ __global__ __launch_bounds__(kFeatTile) void k_sr_features(SrBuffers b, SrParams
 }
 
 // ---------------------------------------------------------------- per-ring selection
-template <int CAP>
+template <int CAP, bool SIDX>
 struct SelShared {
   uint64_t keys[CAP];       // (segment, curvature, position) of the ring; then (voxel, candidate)
-  int sidx[CAP];            // sortInd of the ring on entry
+  int sidx[SIDX ? CAP : 1]; // sortInd of the ring on entry (identity unless rings are walked in order)
   uint16_t cand[CAP];       // lessFlat candidate positions (relative to the ring start)
   uint8_t pk[CAP + 16];     // bit 0 cloudNeighborPicked, bit 1 neighbour-walk stop (gap)
   int8_t lab[CAP + 16];
@@ -370,15 +383,93 @@ struct SelShared {
   int nsharp, nlsharp, nflat, ncand, wf, big, loff;
 };
 
-// :495-520 with the distance tests precomputed as gap bits
+// :495-520 with the distance tests precomputed as gap bits.  One wave: lanes 0-4 take offsets
+// +1..+5, lanes 8-12 offsets -1..-5; each direction marks up to its first stop (the reference's
+// break), found with one ballot.  Every lane of the wave must call it (ind is wave-uniform).
 LOAM_D void mark_neighbours(int n, int ind, uint8_t* pk, int wlo) {
-  for (int l = 1; l <= 5; ++l) {
-    if (ind + l >= n || (pk[ind + l - wlo] & 2)) break;
-    pk[ind + l - wlo] |= 1;
+  const int lane = lane_id();
+  const bool pos = lane < 5, neg = lane >= 8 && lane < 13;
+  const int off = pos ? lane + 1 : (neg ? 7 - lane : 0);
+  bool stop = false;
+  if (pos) stop = ind + off >= n || (pk[ind + off - wlo] & 2);
+  else if (neg) stop = ind + off < 0 || (pk[ind + off + 1 - wlo] & 2);
+  const uint64_t sm = __ballot(stop);
+  const uint64_t sp = sm & 0x1full, sn = (sm >> 8) & 0x1full;
+  const int np = sp ? __ffsll((unsigned long long)sp) - 1 : 5;   // offsets marked in each direction
+  const int nn = sn ? __ffsll((unsigned long long)sn) - 1 : 5;
+  if ((pos && lane < np) || (neg && lane - 8 < nn)) pk[ind + off - wlo] |= 1;
+}
+
+// The greedy picks of one segment [sp, ep] (ring-local) for independent rings (one wave):
+// :476-522 sharp / less sharp and :524-566 flat, on the ring's curvatures cv and the LDS pick state.
+LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, uint64_t* list, uint8_t* pk,
+                                int8_t* lab, int wlo, int* picks, int& nsharp, int& nlsharp, int& nflat) {
+  const int lane = lane_id();
+  // points with curvature > 0.1, as (curvature bits, position): ascending = the stable sort's order
+  int m = 0;
+  for (int base = sp; base <= ep; base += 64) {
+    const int t = base + lane;
+    const bool e = t <= ep && D(cv[t]) > 0.1;
+    const uint64_t bm = __ballot(e);
+    if (e) list[m + __popcll(bm & lanemask_lt())] = ((uint64_t)fkey(cv[t]) << 32) | (uint32_t)t;
+    m += __popcll(bm);
   }
-  for (int l = -1; l >= -5; --l) {
-    if (ind + l < 0 || (pk[ind + l + 1 - wlo] & 2)) break;
-    pk[ind + l - wlo] |= 1;
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+  if (m > 1) wave_sort_u64(list, m);
+  int largest = 0;
+  bool done = false;
+  for (int base = m - 1; base >= 0 && !done; base -= 64) {  // from the largest curvature down
+    const int k = base - lane;
+    const bool elig = k >= 0;
+    const int ind = elig ? lo + (int)(uint32_t)list[k] : 0;
+    uint64_t remaining = __ballot(elig);
+    while (remaining) {
+      const bool cand_ok = elig && ((remaining >> lane) & 1ull) && (pk[ind - wlo] & 1) == 0;
+      const uint64_t mm = __ballot(cand_ok);
+      if (!mm) break;
+      const int f = __ffsll((unsigned long long)mm) - 1;
+      largest++;
+      if (largest > 20) { done = true; break; }
+      if (lane == f) {
+        if (largest <= 2) {
+          lab[ind - wlo] = 2;
+          picks[nsharp++] = ind;
+          picks[kSharpPerRing + nlsharp++] = ind;
+        } else {
+          lab[ind - wlo] = 1;
+          picks[kSharpPerRing + nlsharp++] = ind;
+        }
+        pk[ind - wlo] |= 1;
+      }
+      mark_neighbours(n, __shfl(ind, f, 64), pk, wlo);
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+      remaining &= ~((2ull << f) - 1ull);
+    }
+  }
+  // flat: the unmarked point of smallest (curvature, position) below 0.1, four times at most
+  for (int smallest = 0;;) {
+    uint64_t best = ~0ull;
+    for (int t = sp + lane; t <= ep; t += 64) {
+      const float c = cv[t];
+      if (D(c) < 0.1 && (pk[lo + t - wlo] & 1) == 0) {
+        const uint64_t key = ((uint64_t)fkey(c) << 32) | (uint32_t)t;
+        best = key < best ? key : best;
+      }
+    }
+    best = wave_min_u64(best);
+    if (best == ~0ull) break;
+    const int ind = lo + (int)(uint32_t)best;
+    if (lane == 0) {
+      lab[ind - wlo] = -1;
+      picks[kSharpPerRing + kLessSharpPerRing + nflat++] = ind;
+    }
+    if (++smallest >= 4) break;  // after the push, before the marks (:555-557)
+    if (lane == 0) pk[ind - wlo] |= 1;
+    mark_neighbours(n, ind, pk, wlo);
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -394,10 +485,15 @@ LOAM_D float key_curv(uint64_t key) { return __builtin_bit_cast(float, (uint32_t
 // CAP: LDS capacity of the ring state.  BIG: the ring state lives in global scratch (slot `slot`)
 // and in the sweep's own picked / label arrays, for spans beyond any LDS capacity (an empty ring
 // leaves its successor spanning every earlier ring, Q5).
-template <int CAP, bool BIG>
-LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq, SelShared<CAP>& sh, int slot) {
+// SIDX: the ring's sortInd may differ from the identity (rings walked in order); without it the
+// ring state holds no sortInd copy (8 KB less LDS) and sortInd[k] = k.
+template <int CAP, bool BIG, bool SIDX>
+LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq, SelShared<CAP, SIDX>& sh, int slot) {
   using CandT = typename std::conditional<BIG, int, uint16_t>::type;
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+#ifdef LOAM_EXP_PHASES
+  long long ph_t = clock64();
+#endif
   const float4* pts = b.full + (size_t)s * b.cap;
   const float* curv = b.curv + (size_t)s * b.cap;
   const int sq = sh.se[q], eq = sh.se[R + q];
@@ -454,24 +550,35 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
     lab = b.label + (size_t)s * b.cap;
   } else {
     keys = sh.keys;
-    sidx = sh.sidx;
+    sidx = SIDX ? sh.sidx : nullptr;
     cand = sh.cand;
     pk = sh.pk;
     lab = sh.lab;
     for (int k = wlo + tid; k <= whi; k += kSelThreads) {
       pk[k - wlo] = b.picked[(size_t)s * b.cap + k];
-      lab[k - wlo] = b.label[(size_t)s * b.cap + k];
+      lab[k - wlo] = SIDX ? b.label[(size_t)s * b.cap + k] : 0;  // labels start at 0 (k_sr_features)
     }
   }
   int segb[7];
 #pragma unroll
   for (int j = 0; j <= 6; ++j) segb[j] = (sq * (6 - j) + eq * j) / 6;  // sp_j; ep_j = sp_{j+1} - 1
+  // FAST (independent rings, sortInd = identity): no ring sort.  The sharp walk visits only the
+  // points with curvature > 0.1, so those are compacted and sorted per segment (one wave, in
+  // registers); the flat walk stops at its 4th pick, so it is a repeated minimum over the eligible
+  // points (an arg-min over "unmarked and < 0.1" is the next point the ascending walk would take:
+  // marks only accumulate).  cv: the ring's curvatures in the upper half of keys.
+  constexpr bool FAST = !SIDX && !BIG;
+  float* cv = reinterpret_cast<float*>(keys + CAP / 2);
+  if constexpr (FAST) {
+    for (int t = tid; t < len; t += kSelThreads) cv[t] = curv[lo + t];
+    __syncthreads();
+  } else {
   const int P2 = next_pow2(len);
   for (int t = tid; t < P2; t += kSelThreads) {
     uint64_t key = ~0ull;
     if (t < len) {
-      const int v = b.sortind[(size_t)s * b.cap + lo + t];
-      sidx[t] = v;
+      const int v = SIDX ? b.sortind[(size_t)s * b.cap + lo + t] : lo + t;
+      if (SIDX) sidx[t] = v;
       int seg = 0;
 #pragma unroll
       for (int j = 1; j < 6; ++j) seg += (lo + t >= segb[j]) ? 1 : 0;
@@ -480,12 +587,19 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
     keys[t] = key;
   }
   __syncthreads();
-  block_bitonic_sort<kSelThreads>(keys, P2);
+  PH(0);
+  if constexpr (BIG) block_bitonic_sort<kSelThreads>(keys, P2);
+  else reg_bitonic_sort<kSelThreads, CAP / kSelThreads>(keys, P2);
+  }
+  PH(1);
   if (w == 0) {
     int run = 0;
     for (int j = 0; j < 6; ++j) {
       const int sp = segb[j] - lo, ep = segb[j + 1] - 1 - lo;  // sorted-local range of segment j
       if (ep < sp) continue;
+      if constexpr (FAST) {
+        select_segment_fast(n, lo, sp, ep, cv, keys, pk, lab, wlo, sh.picks, sh.nsharp, sh.nlsharp, sh.nflat);
+      } else {
       // (:476-522) sharp / less sharp, walking from the largest curvature down
       int largest = 0;
       bool done = false;
@@ -493,7 +607,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
         const int k = base - lane;
         const bool inr = k >= sp;
         const uint64_t key = inr ? keys[k] : 0ull;
-        const int ind = inr ? sidx[key & kPosMask] : 0;
+        const int ind = inr ? (SIDX ? sidx[key & kPosMask] : lo + (int)(key & kPosMask)) : 0;
         const bool elig = inr && D(key_curv(key)) > 0.1;
         uint64_t remaining = __ballot(elig);
         if (remaining != __ballot(inr)) done = true;  // sorted: no eligible point below this chunk
@@ -514,8 +628,8 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
               sh.picks[kSharpPerRing + sh.nlsharp++] = ind;
             }
             pk[ind - wlo] |= 1;
-            mark_neighbours(n, ind, pk, wlo);
           }
+          mark_neighbours(n, __shfl(ind, f, 64), pk, wlo);
           __threadfence_block();
           __builtin_amdgcn_wave_barrier();
           remaining &= ~((2ull << f) - 1ull);
@@ -528,7 +642,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
         const int k = base + lane;
         const bool inr = k <= ep;
         const uint64_t key = inr ? keys[k] : 0ull;
-        const int ind = inr ? sidx[key & kPosMask] : 0;
+        const int ind = inr ? (SIDX ? sidx[key & kPosMask] : lo + (int)(key & kPosMask)) : 0;
         const bool elig = inr && D(key_curv(key)) < 0.1;
         uint64_t remaining = __ballot(elig);
         const bool last = remaining != __ballot(inr);  // sorted: no eligible point above this chunk
@@ -543,16 +657,15 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
           }
           smallest++;
           if (smallest >= 4) { done = true; break; }
-          if (lane == f) {
-            pk[ind - wlo] |= 1;
-            mark_neighbours(n, ind, pk, wlo);
-          }
+          if (lane == f) pk[ind - wlo] |= 1;
+          mark_neighbours(n, __shfl(ind, f, 64), pk, wlo);
           __threadfence_block();
           __builtin_amdgcn_wave_barrier();
           remaining &= ~((2ull << f) - 1ull);
         }
         if (last) done = true;
       }
+      }  // !FAST
       __threadfence_block();
       __builtin_amdgcn_wave_barrier();
       // (:568-572) lessFlat candidates of this segment, in position order
@@ -567,7 +680,8 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
     if (lane == 0) sh.ncand = run;
   }
   __syncthreads();
-  if (seq) {  // the ring's sortInd after its six sorts, for the next ring (one workgroup, ordered)
+  PH(2);
+  if (SIDX && seq) {  // the ring's sortInd after its six sorts, for the next ring (one workgroup, ordered)
     for (int t = tid; t < len; t += kSelThreads)
       b.sortind[(size_t)s * b.cap + lo + t] = sidx[keys[t] & kPosMask];
     __syncthreads();
@@ -594,6 +708,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
       mx[d] = fmaxf(mx[d], sh.red[3 + d][v]);
     }
   __syncthreads();
+  PH(3);
   int nout = 0;
   if (nc > 0) {
     const float inv = 1.0f / 0.2f;
@@ -626,7 +741,10 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
         keys[t] = key;
       }
       __syncthreads();
-      block_bitonic_sort<kSelThreads>(keys, P2c);
+  PH(4);
+      if constexpr (BIG) block_bitonic_sort<kSelThreads>(keys, P2c);
+      else reg_bitonic_sort<kSelThreads, CAP / kSelThreads>(keys, P2c);
+  PH(5);
       int run = 0;
       for (int base = 0; base < nc; base += kSelThreads) {
         const int t = base + tid;
@@ -676,6 +794,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
   }
   __threadfence();
   __syncthreads();
+  PH(6);
 }
 
 // Three instantiations, chosen per sweep: CAP = 2048 (34 KB of LDS, four workgroups per CU)
@@ -684,10 +803,11 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
 // walked in order when they depend on each other, and flags the rest (sel_big = 2); the global-
 // memory variant walks those (gridDim.x workgroups over the flagged sweeps, one scratch slot each).
 template <int CAP, int MODE>  // MODE 0: fast, 1: 4096 / dependent rings, 2: unbounded spans
-__global__ __launch_bounds__(kSelThreads) void k_sr_select(SrBuffers b, SrParams p) {
+__global__ __launch_bounds__(kSelThreads) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? 6 : 1))) void k_sr_select(SrBuffers b, SrParams p) {
   constexpr bool BIG = MODE == 2;
   const int tid = threadIdx.x, R = p.R;
-  __shared__ SelShared<CAP> sh;
+  constexpr bool SIDX = MODE != 0;  // MODE 0 takes independent rings only
+  __shared__ SelShared<CAP, SIDX> sh;
   for (int s = BIG ? blockIdx.x : blockIdx.y; s < b.S; s += BIG ? gridDim.x : b.S) {
     const int q = BIG ? 0 : blockIdx.x;
     if (MODE != 0 && b.sel_big[s] != MODE) continue;
@@ -732,9 +852,10 @@ __global__ __launch_bounds__(kSelThreads) void k_sr_select(SrBuffers b, SrParams
         if (tid < 4) b.st_cnt[(size_t)(s * R + q) * 4 + tid] = 0;
         if (tid == 0) b.st_loff[s * R + q] = q * kRingCap;
       } else if (sh.wf && !BIG) {
-        select_ring<CAP, BIG>(b, s, q, R, n, false, sh, 0);
+        select_ring<CAP, BIG, SIDX>(b, s, q, R, n, false, sh, 0);
       } else if (q == 0) {
-        for (int r = 0; r < R; ++r) select_ring<CAP, BIG>(b, s, r, R, n, true, sh, BIG ? blockIdx.x : 0);
+        if constexpr (SIDX)
+          for (int r = 0; r < R; ++r) select_ring<CAP, BIG, SIDX>(b, s, r, R, n, true, sh, BIG ? blockIdx.x : 0);
       }
     }
     __syncthreads();
@@ -840,3 +961,9 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
 }
 
 }  // namespace loam
+
+#ifdef LOAM_EXP_PHASES
+extern "C" int loam_debug_phases(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(loam::g_phase), 8 * sizeof(unsigned long long)) == hipSuccess ? 0 : -3;
+}
+#endif
