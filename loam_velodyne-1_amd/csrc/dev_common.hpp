@@ -34,6 +34,25 @@ LOAM_HD float sqdist(float ax, float ay, float az, float bx, float by, float bz)
 LOAM_D int lane_id() { return __lane_id(); }
 LOAM_D uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
+// Workgroup coordinates of a 2-D (chunk, problem) grid renumbered so that the chunks of one
+// problem run on one XCD.  The dispatcher deals workgroups round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md, "Workgroup dispatch"), so linear id L lands on XCD L % 8; logical id
+// = (XCD-major rank of L) keeps a problem's consecutive chunks in one XCD's 4 MiB L2, where its
+// clouds / hash are shared, instead of fetching them into all eight.  A bijection on the grid:
+// placement only, never correctness.
+struct XcdBlock { int x, y; };
+LOAM_D XcdBlock xcd_block() {
+#ifdef LOAM_EXP_NOXCD
+  return {(int)blockIdx.x, (int)blockIdx.y};
+#else
+  const int gx = gridDim.x, total = gx * gridDim.y;
+  const int L = blockIdx.x + blockIdx.y * gx;
+  const int x8 = L & 7, i = L >> 3, q = total >> 3, r = total & 7;
+  const int logical = x8 < r ? x8 * (q + 1) + i : r * (q + 1) + (x8 - r) * q + i;
+  return {logical % gx, logical / gx};
+#endif
+}
+
 template <typename T>
 LOAM_D T wave_sum(T v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

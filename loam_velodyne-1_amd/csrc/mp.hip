@@ -536,7 +536,8 @@ __global__ void k_mp_lm_begin(MpBuffers b) {
 // on nothing but the ordered 5 neighbours, so it is kept per query and reused while the ordered
 // 5-NN is unchanged from the previous iteration (bit-identical to refitting).
 __global__ __launch_bounds__(kMpQueryThreads) void k_mp_nn(MpBuffers b) {
-  const int p = blockIdx.y, tid = threadIdx.x;
+  const XcdBlock blk = xcd_block();
+  const int p = blk.y, tid = threadIdx.x;
   const int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan] || ist[kMiStop]) return;
   const float* st = b.state + (size_t)p * kMpStateFloats;
@@ -555,7 +556,7 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_nn(MpBuffers b) {
   const float4* fromC = b.from + (size_t)p * b.map_cap;
   const float4* fromS = fromC + b.nfrom[p * 2 + 0];
   const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
-  for (int q = blockIdx.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
+  for (int q = blk.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
     const bool corner = q < nsc;
     const float4 sel = loampose::point_to_map(r, stack[corner ? q : b.capC + (q - nsc)]);
     Top5 t;
@@ -589,7 +590,8 @@ struct MpFit {
 }  // namespace
 
 __global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
-  const int p = blockIdx.y, tid = threadIdx.x;
+  const XcdBlock blk = xcd_block();
+  const int p = blk.y, tid = threadIdx.x;
   int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan] || ist[kMiStop]) return;
   const bool first = ist[kMiIters] == 0;  // fits of an earlier frame are stale
@@ -608,7 +610,7 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
   const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
   float* jw = jac[tid];
   int nfits = 0;
-  for (int q = blockIdx.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
+  for (int q = blk.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
     const bool corner = q < nsc;
     const float4* from = corner ? fromC : fromS;
     const int4 n0 = qnn[2 * q], n1 = qnn[2 * q + 1];

@@ -367,7 +367,8 @@ __global__ void k_od_begin(OdBuffers b, FeatView f) {
 // TransformToStart of every query at the current transform (:472, :587), lane per query, for
 // the association below (whose waves would otherwise each evaluate it on 64 lanes)
 __global__ __launch_bounds__(kOdThreads) void k_od_sel(OdBuffers b, FeatView f) {
-  const int p = blockIdx.y;
+  const XcdBlock blk = xcd_block();
+  const int p = blk.y;
   const int* ist = b.istate + (size_t)p * kOdStateInts;
   if (!ist[kIsActive] || ist[kIsStop]) return;
   const float* st = b.state + (size_t)p * kOdStateFloats;
@@ -375,7 +376,7 @@ __global__ __launch_bounds__(kOdThreads) void k_od_sel(OdBuffers b, FeatView f) 
 #pragma unroll
   for (int k = 0; k < 6; ++k) T[k] = st[k];
   const int nc = f.count(p, 0), nq = nc + f.count(p, 2);
-  const int q = blockIdx.x * kOdThreads + threadIdx.x;
+  const int q = blk.x * kOdThreads + threadIdx.x;
   if (q >= nq) return;
   const float4 po = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
   b.sel[(size_t)p * b.cap_q + q] = loampose::transform_to_start(T, po);
@@ -384,7 +385,8 @@ __global__ __launch_bounds__(kOdThreads) void k_od_sel(OdBuffers b, FeatView f) 
 // association (:472-527, :587-650), one wave per query: exact NN through the hash, then the
 // ring-window scans.
 __global__ __launch_bounds__(kOdThreads) void k_od_assoc(OdBuffers b, FeatView f, int last_buf) {
-  const int p = blockIdx.y, lane = lane_id(), w = threadIdx.x >> 6;
+  const XcdBlock blk = xcd_block();
+  const int p = blk.y, lane = lane_id(), w = threadIdx.x >> 6;
   const int* ist = b.istate + (size_t)p * kOdStateInts;
   if (!ist[kIsActive] || ist[kIsStop]) return;
   __shared__ int cells[kOdWaves][64];
@@ -395,7 +397,7 @@ __global__ __launch_bounds__(kOdThreads) void k_od_assoc(OdBuffers b, FeatView f
   const float4* CL = b.lastC + lp * b.capC;
   const float4* SL = b.lastS + lp * b.capS;
   int* ind = b.ind + (size_t)p * 3 * b.cap_q;
-  for (int q = blockIdx.x * kOdWaves + w; q < nq; q += gridDim.x * kOdWaves) {
+  for (int q = blk.x * kOdWaves + w; q < nq; q += gridDim.x * kOdWaves) {
     const float4 s4 = sel[q];
     int i1, i2, i3 = -1;
     if (q < nc) {
@@ -454,7 +456,8 @@ LOAM_D void od_step(const OdBuffers& b, int p, int iter, const double* tot, floa
 // coefficient, which adds exact zeros.
 template <bool FUSED>
 __global__ __launch_bounds__(kOdThreads) void k_od_rows(OdBuffers b, FeatView f, int last_buf, int iter) {
-  const int p = blockIdx.y, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const XcdBlock blk = xcd_block();
+  const int p = blk.y, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const int* ist = b.istate + (size_t)p * kOdStateInts;
   if (!ist[kIsActive] || ist[kIsStop]) return;
   __shared__ double red[kOdWaves][28];
@@ -469,7 +472,7 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows(OdBuffers b, FeatView f,
       trig[2 * k + 1] = (float)dcos(1 * T[k]);
     }
   const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
-  const int q = blockIdx.x * kOdThreads + tid;
+  const int q = blk.x * kOdThreads + tid;
   const size_t lp = (size_t)last_buf * b.P + p;
   float4* qcf = b.q_cf + (size_t)p * b.max_iter * b.cap_q;
   int8_t* qok = b.q_ok + (size_t)p * b.max_iter * b.cap_q;
@@ -583,7 +586,7 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows(OdBuffers b, FeatView f,
   if (tid < 28) {
     double v = red[0][tid];
     for (int ww = 1; ww < kOdWaves; ++ww) v += red[ww][tid];
-    b.part[((size_t)p * b.gq + blockIdx.x) * 28 + tid] = v;
+    b.part[((size_t)p * b.gq + blk.x) * 28 + tid] = v;
     if (FUSED) __threadfence();  // partials visible device-wide before this workgroup reports done
   }
   if (!FUSED) return;
