@@ -278,6 +278,146 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_sort(SrBuffers b, SrPara
   }
 }
 
+// ---------------------------------------------------------------- ring sort, tile-parallel
+// The same stable ring bucketing as k_sr_ring_sort for sweeps without IMU data, one workgroup per
+// kSrThreads-point tile instead of one per sweep (a single sweep then spreads over ~60 CUs instead
+// of walking its tiles on one): k_sr_ring_count finds the sweep's first / last finite point itself
+// (waves 0 / 1 scan from either end), computes ring ID and first-branch orientation of its tile,
+// the tile's ring counts and its first halfPassed flip; k_sr_ring_scatter takes the flip point F
+// as the minimum over the tiles, the ring bases and its tile's per-ring offsets from the counts,
+// and scatters with the same wave-ballot ranks.  src/scanRegistration.cpp:225-357
+__global__ __launch_bounds__(kSrThreads) void k_sr_ring_count(SrBuffers b, SrParams p) {
+  const int s = blockIdx.y, t = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int n = b.raw_n[s], R = p.R;
+  if (t * kSrThreads >= n) return;
+  const float4* raw = b.raw + (size_t)s * b.cap;
+  __shared__ int sh_first, sh_last, sh_F;
+  __shared__ float sh_start;
+  __shared__ int sh_cnt[64];
+  if (w == 0) {
+    int f = -1;
+    for (int base = 0; base < n; base += 64) {
+      const int i = base + lane;
+      const uint64_t m = __ballot(i < n && finite3(raw[i]));
+      if (m) { f = base + __ffsll((unsigned long long)m) - 1; break; }
+    }
+    if (lane == 0) sh_first = f;
+  } else if (w == 1) {
+    int l = -1;
+    for (int base = n - 1; base >= 0; base -= 64) {
+      const int i = base - lane;
+      const uint64_t m = __ballot(i >= 0 && finite3(raw[i]));
+      if (m) { l = base - (__ffsll((unsigned long long)m) - 1); break; }
+    }
+    if (lane == 0) sh_last = l;
+  }
+  if (tid < R) sh_cnt[tid] = 0;
+  if (tid == 0) sh_F = 0x7fffffff;
+  __syncthreads();
+  if (tid == 0) {  // :230-238
+    float startOri = 0.0f, endOri = 0.0f;
+    if (sh_last >= 0) {
+      const float4 a = raw[sh_first], z = raw[sh_last];
+      startOri = -atan2f_fdlibm(a.y, a.x);
+      endOri = (float)(D(-atan2f_fdlibm(z.y, z.x)) + 2 * M_PI);
+      if (D(endOri - startOri) > 3 * M_PI) endOri = (float)(D(endOri) - 2 * M_PI);
+      else if (D(endOri - startOri) < M_PI) endOri = (float)(D(endOri) + 2 * M_PI);
+    } else if (t == 0) {
+      b.err[s] |= ERR_EMPTY;
+    }
+    sh_start = startOri;
+    if (t == 0) { b.sweep_ori[2 * s] = startOri; b.sweep_ori[2 * s + 1] = endOri; }
+  }
+  __syncthreads();
+  const float startOri = sh_start;
+  const int i = t * kSrThreads + tid;
+  int Floc = 0x7fffffff;
+  if (i < n) {
+    const float4 q = raw[i];
+    uint8_t sid = 255;
+    float ori = 0.0f;
+    if (finite3(q)) {
+      const float px = q.y, py = q.z, pz = q.x;
+      const float angle = (float)(atan(D(py) / sqrt(D(px * px + pz * pz))) * 180 / M_PI);
+      const int scanID = ring_id(p, angle);
+      if (scanID >= 0 && scanID <= R - 1) {
+        sid = (uint8_t)scanID;
+        ori = -atan2f_fdlibm(px, pz);
+        const float o1 = ori_first(ori, startOri);
+        if (D(o1 - startOri) > M_PI) Floc = i;
+        atomicAdd(&sh_cnt[scanID], 1);
+      }
+    }
+    b.tmp_ori[(size_t)s * b.cap + i] = ori;
+    b.tmp_sid[(size_t)s * b.cap + i] = sid;
+  }
+  Floc = wave_min_i(Floc);
+  if (lane == 0 && Floc != 0x7fffffff) atomicMin(&sh_F, Floc);
+  __syncthreads();
+  if (tid < R) b.tilecnt[((size_t)s * b.ntiles() + t) * R + tid] = sh_cnt[tid];
+  if (tid == 0) b.tileF[(size_t)s * b.ntiles() + t] = sh_F;
+}
+
+__global__ __launch_bounds__(kSrThreads) void k_sr_ring_scatter(SrBuffers b, SrParams p) {
+  const int s = blockIdx.y, t = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int n = b.raw_n[s], R = p.R, nt = (n + kSrThreads - 1) / kSrThreads;
+  if (t >= (nt > 0 ? nt : 1)) return;
+  __shared__ int sh_tot[64], sh_pre[64], sh_base[64], sh_F;
+  __shared__ int sh_wcnt[kSrThreads / 64][64];
+  if (tid < R) { sh_tot[tid] = 0; sh_pre[tid] = 0; }
+  if (tid == 0) sh_F = 0x7fffffff;
+  __syncthreads();
+  const int* tc = b.tilecnt + (size_t)s * b.ntiles() * R;
+  for (int k = tid; k < nt * R; k += kSrThreads) {
+    const int v = tc[k];
+    if (v) {
+      atomicAdd(&sh_tot[k % R], v);
+      if (k / R < t) atomicAdd(&sh_pre[k % R], v);
+    }
+  }
+  int F = 0x7fffffff;
+  for (int k = tid; k < nt; k += kSrThreads) F = min(F, b.tileF[(size_t)s * b.ntiles() + k]);
+  F = wave_min_i(F);
+  if (lane == 0 && F != 0x7fffffff) atomicMin(&sh_F, F);
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int r = 0; r < R; ++r) { sh_base[r] = run; run += sh_tot[r]; }
+    if (t == 0) {
+      b.n_full[s] = run;
+      if (n <= 0) b.err[s] |= ERR_EMPTY;
+    }
+  }
+  if (lane < R) sh_wcnt[w][lane] = 0;
+  __syncthreads();
+  if (nt == 0) return;
+  F = sh_F;
+  const float startOri = b.sweep_ori[2 * s], endOri = b.sweep_ori[2 * s + 1];
+  const int i = t * kSrThreads + tid;
+  const int sid = i < n ? (int)b.tmp_sid[(size_t)s * b.cap + i] : 255;
+  const bool valid = i < n && sid != 255;
+  int rank = 0;
+  uint64_t mval = __ballot(valid);
+  while (mval) {
+    const int leader = __ffsll((unsigned long long)mval) - 1;
+    const int rl = __shfl(sid, leader, 64);
+    const uint64_t mm = __ballot(valid && sid == rl);
+    if (valid && sid == rl) rank = __popcll(mm & lanemask_lt());
+    if (lane == leader) sh_wcnt[w][rl] = __popcll(mm);
+    mval &= ~mm;
+  }
+  __syncthreads();
+  if (valid) {
+    int pos = sh_base[sid] + sh_pre[sid] + rank;
+    for (int v = 0; v < w; ++v) pos += sh_wcnt[v][sid];
+    const float4 q = b.raw[(size_t)s * b.cap + i];
+    float ori = b.tmp_ori[(size_t)s * b.cap + i];
+    ori = (i <= F) ? ori_first(ori, startOri) : ori_second(ori, endOri);
+    const float relTime = (ori - startOri) / (endOri - startOri);
+    b.full[(size_t)s * b.cap + pos] = make_float4(q.y, q.z, q.x, (float)(sid + 0.1 * D(relTime)));
+  }
+}
+
 // ---------------------------------------------------------------- curvature + marks
 constexpr int kFeatTile = 256;
 
@@ -906,6 +1046,8 @@ void sr_alloc(SrBuffers& b, int S, int cap, int R) {
   HIPCHK(hipMalloc(&b.tmp_ori, n * sizeof(float)));
   HIPCHK(hipMalloc(&b.tmp_sid, n));
   HIPCHK(hipMalloc(&b.tilecnt, (size_t)S * b.ntiles() * R * sizeof(int)));
+  HIPCHK(hipMalloc(&b.tileF, (size_t)S * b.ntiles() * sizeof(int)));
+  HIPCHK(hipMalloc(&b.sweep_ori, (size_t)S * 2 * sizeof(float)));
   HIPCHK(hipMalloc(&b.full, n * sizeof(float4)));
   HIPCHK(hipMalloc(&b.n_full, S * sizeof(int)));
   HIPCHK(hipMalloc(&b.curv, n * sizeof(float)));
@@ -933,7 +1075,7 @@ void sr_alloc(SrBuffers& b, int S, int cap, int R) {
 }
 
 void sr_free(SrBuffers& b) {
-  void* ptrs[] = {b.raw, b.raw_n, b.tmp_ori, b.tmp_sid, b.tilecnt, b.full, b.n_full, b.curv,
+  void* ptrs[] = {b.raw, b.raw_n, b.tmp_ori, b.tmp_sid, b.tilecnt, b.tileF, b.sweep_ori, b.full, b.n_full, b.curv,
                   b.picked, b.sortind, b.label, b.ring_se, b.st_sharp, b.st_lsharp, b.st_flat,
                   b.st_lflat, b.st_cnt, b.sharp, b.lsharp, b.flat, b.lflat, b.cnt, b.err, b.sel_big, b.st_loff, b.big_keys, b.big_sidx, b.big_cand};
   for (void* q : ptrs)
@@ -946,8 +1088,16 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
   HIPCHK(hipMemsetAsync(b.ring_se, 0, (size_t)b.S * 2 * b.R * sizeof(int), st));
   HIPCHK(hipMemsetAsync(b.err, 0, (size_t)b.S * sizeof(int), st));
   mark("sr_memset");
-  if (p.imu) hipLaunchKernelGGL(k_sr_ring_sort<true>, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
-  else hipLaunchKernelGGL(k_sr_ring_sort<false>, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
+  if (p.imu) {
+    hipLaunchKernelGGL(k_sr_ring_sort<true>, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
+  } else {
+#ifdef LOAM_EXP_RINGWG
+    hipLaunchKernelGGL(k_sr_ring_sort<false>, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
+#else
+    hipLaunchKernelGGL(k_sr_ring_count, dim3(b.ntiles(), b.S), dim3(kSrThreads), 0, st, b, p);
+    hipLaunchKernelGGL(k_sr_ring_scatter, dim3(b.ntiles(), b.S), dim3(kSrThreads), 0, st, b, p);
+#endif
+  }
   mark("k_sr_ring_sort");
   hipLaunchKernelGGL(k_sr_features, dim3((b.cap + kFeatTile - 1) / kFeatTile, b.S), dim3(kFeatTile), 0,
                      st, b, p);
