@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_prepare(MpBuffers b, MpInput 
   int* ist = b.istate + (size_t)p * kMpStateInts;
   int* slots = slot_table(b, b.pool_cur, p);
   __shared__ int sh_shift[256];
-  __shared__ int sh_nshift, sh_c[3];
+  __shared__ int sh_nshift, sh_c[3], sh_cen[3], sh_scan[16];
   if (tid == 0) {
     float pose[6] = {0, 0, 0, 0, 0, 0};
     if (in.pose)
@@ -83,6 +83,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_prepare(MpBuffers b, MpInput 
     sh_c[0] = cI; sh_c[1] = cJ; sh_c[2] = cK;
     ist[kMiCubeI] = cI; ist[kMiCubeJ] = cJ; ist[kMiCubeK] = cK;
     ist[kMiCenW] = cW; ist[kMiCenH] = cH; ist[kMiCenD] = cD;
+    sh_cen[0] = cW; sh_cen[1] = cH; sh_cen[2] = cD;
   }
   __syncthreads();
   for (int s = 0; s < sh_nshift; ++s) {  // slot-table shifts: the cleared cube wraps around
@@ -112,45 +113,49 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_prepare(MpBuffers b, MpInput 
     __threadfence();
     __syncthreads();
   }
-  if (tid == 0) {  // FOV selection (:616-672) and FromMap prefix
-    const float* T = st + kMpTobe;
-    const float ox = st[kMpOnY], oy = st[kMpOnY + 1], oz = st[kMpOnY + 2];
-    const int cI = sh_c[0], cJ = sh_c[1], cK = sh_c[2];
-    const int cW = ist[kMiCenW], cH = ist[kMiCenH], cD = ist[kMiCenD];
-    int nv = 0, accC = 0, accS = 0;
-    int* vp = b.vpre + (size_t)p * (kMaxValid + 1) * 2;
-    for (int i = cI - 2; i <= cI + 2; ++i)
-      for (int j = cJ - 2; j <= cJ + 2; ++j)
-        for (int k = cK - 2; k <= cK + 2; ++k) {
-          if (!(i >= 0 && i < kCubeW && j >= 0 && j < kCubeH && k >= 0 && k < kCubeD)) continue;
-          const float centerX = (float)(50.0 * (i - cW));
-          const float centerY = (float)(50.0 * (j - cH));
-          const float centerZ = (float)(50.0 * (k - cD));
-          bool inFOV = false;
-          for (int ii = -1; ii <= 1; ii += 2)
-            for (int jj = -1; jj <= 1; jj += 2)
-              for (int kk = -1; kk <= 1; kk += 2) {
-                const float cornerX = (float)(D(centerX) + 25.0 * ii);
-                const float cornerY = (float)(D(centerY) + 25.0 * jj);
-                const float cornerZ = (float)(D(centerZ) + 25.0 * kk);
-                const float sq1 = (T[3] - cornerX) * (T[3] - cornerX) + (T[4] - cornerY) * (T[4] - cornerY) +
-                                  (T[5] - cornerZ) * (T[5] - cornerZ);
-                const float sq2 = (ox - cornerX) * (ox - cornerX) + (oy - cornerY) * (oy - cornerY) +
-                                  (oz - cornerZ) * (oz - cornerZ);
-                const float check1 = (float)(100.0 + D(sq1) - D(sq2) - 10.0 * sqrt(3.0) * sqrt(D(sq1)));
-                const float check2 = (float)(100.0 + D(sq1) - D(sq2) + 10.0 * sqrt(3.0) * sqrt(D(sq1)));
-                if (check1 < 0 && check2 > 0) inFOV = true;
-              }
-          if (inFOV) {
-            const int ind = cube_index(i, j, k);
-            b.valid[(size_t)p * kMaxValid + nv] = ind;
-            vp[nv * 2 + 0] = accC;
-            vp[nv * 2 + 1] = accS;
-            accC += slots[ind * 4 + 1];
-            accS += slots[ind * 4 + 3];
-            ++nv;
+  // FOV selection (:616-672) and FromMap prefix: thread c tests cube c of the 5x5x5
+  // neighbourhood (the reference's i, j, k loop order), block scans keep that order
+  const float* T = st + kMpTobe;
+  const int cI = sh_c[0], cJ = sh_c[1], cK = sh_c[2];
+  const int cW = sh_cen[0], cH = sh_cen[1], cD = sh_cen[2];
+  bool inFOV = false;
+  int ind = 0;
+  if (tid < 125) {
+    const int i = cI - 2 + tid / 25, j = cJ - 2 + (tid / 5) % 5, k = cK - 2 + tid % 5;
+    if (i >= 0 && i < kCubeW && j >= 0 && j < kCubeH && k >= 0 && k < kCubeD) {
+      const float ox = st[kMpOnY], oy = st[kMpOnY + 1], oz = st[kMpOnY + 2];
+      const float centerX = (float)(50.0 * (i - cW));
+      const float centerY = (float)(50.0 * (j - cH));
+      const float centerZ = (float)(50.0 * (k - cD));
+      for (int ii = -1; ii <= 1; ii += 2)
+        for (int jj = -1; jj <= 1; jj += 2)
+          for (int kk = -1; kk <= 1; kk += 2) {
+            const float cornerX = (float)(D(centerX) + 25.0 * ii);
+            const float cornerY = (float)(D(centerY) + 25.0 * jj);
+            const float cornerZ = (float)(D(centerZ) + 25.0 * kk);
+            const float sq1 = (T[3] - cornerX) * (T[3] - cornerX) + (T[4] - cornerY) * (T[4] - cornerY) +
+                              (T[5] - cornerZ) * (T[5] - cornerZ);
+            const float sq2 = (ox - cornerX) * (ox - cornerX) + (oy - cornerY) * (oy - cornerY) +
+                              (oz - cornerZ) * (oz - cornerZ);
+            const float check1 = (float)(100.0 + D(sq1) - D(sq2) - 10.0 * sqrt(3.0) * sqrt(D(sq1)));
+            const float check2 = (float)(100.0 + D(sq1) - D(sq2) + 10.0 * sqrt(3.0) * sqrt(D(sq1)));
+            if (check1 < 0 && check2 > 0) inFOV = true;
           }
-        }
+      ind = cube_index(i, j, k);
+    }
+  }
+  const int nC = inFOV ? slots[ind * 4 + 1] : 0, nS = inFOV ? slots[ind * 4 + 3] : 0;
+  int nv, accC, accS;
+  const int xv = block_excl_scan<kMpThreads>(inFOV ? 1 : 0, sh_scan, nv);
+  const int xc = block_excl_scan<kMpThreads>(nC, sh_scan, accC);
+  const int xs = block_excl_scan<kMpThreads>(nS, sh_scan, accS);
+  int* vp = b.vpre + (size_t)p * (kMaxValid + 1) * 2;
+  if (inFOV) {
+    b.valid[(size_t)p * kMaxValid + xv] = ind;
+    vp[xv * 2 + 0] = xc;
+    vp[xv * 2 + 1] = xs;
+  }
+  if (tid == 0) {
     vp[nv * 2 + 0] = accC;
     vp[nv * 2 + 1] = accS;
     ist[kMiNValid] = nv;
@@ -293,7 +298,7 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
   for (int s = grp.g; s < j.nseg; s += VgGroup<G>::stride()) {
     const int b0 = j.begin[s], b1 = j.end[s];
     if (b1 <= b0) {
-      if (grp.t == 0) j.out_count[s] = 0;
+      if (grp.t == 0 && !j.keep_counts) j.out_count[s] = 0;
       continue;
     }
     if (j.params[(size_t)s * 8 + 5]) {  // "leaf size too small": output = input
@@ -329,6 +334,94 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
   }
 }
 
+// Fused segmented VoxelGrid for segments of at most NT*E points: one workgroup per segment does
+// bbox + parameters (as k_vg_params), keys (as k_vg_keys), an LDS register-bitonic sort of
+// (voxel << 32 | position) — the order of the stable radix sort by voxel with positions as values —
+// and the ordered per-voxel means (as k_vg_reduce), without the global key / value arrays and
+// with one launch.  Larger segments are listed in big_b / big_e for the multi-kernel path.
+template <int NT, int E>
+__global__ __launch_bounds__(NT) void k_vg_fused(VgJob j) {
+  __shared__ uint64_t keys[NT * E];
+  __shared__ float fsc[16];
+  __shared__ int isc[24];
+  const int tid = threadIdx.x;
+  for (int s = blockIdx.x; s < j.nseg; s += gridDim.x) {
+    const int b0 = j.begin[s], b1 = j.end[s], n = b1 - b0;
+    if (n <= 0 || n > NT * E) {
+      if (tid == 0) {
+        j.big_b[s] = n > 0 ? b0 : 0;
+        j.big_e[s] = n > 0 ? b1 : 0;
+        if (n <= 0) j.out_count[s] = 0;
+      }
+      continue;
+    }
+    if (tid == 0) { j.big_b[s] = 0; j.big_e[s] = 0; }
+    const float4* in = j.in + b0;
+    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+    for (int i = tid; i < n; i += NT) {
+      const float4 a = in[i];
+      mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
+      mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
+    }
+    for (int d = 0; d < 3; ++d) {
+      mn[d] = block_reduce<NT>(mn[d], fsc, [](float a, float c) { return fminf(a, c); });
+      mx[d] = block_reduce<NT>(mx[d], fsc, [](float a, float c) { return fmaxf(a, c); });
+    }
+    const float inv = 1.0f / j.leaf[s];
+    const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
+    const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
+    const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
+    if (dx * dy * dz > (int64_t)0x7fffffff) {  // "leaf size too small": output = input
+      for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
+      if (tid == 0) j.out_count[s] = n;
+      continue;
+    }
+    const int m0 = (int)floorf(mn[0] * inv), m1 = (int)floorf(mn[1] * inv), m2 = (int)floorf(mn[2] * inv);
+    const int divx = (int)floorf(mx[0] * inv) - m0 + 1, divy = (int)floorf(mx[1] * inv) - m1 + 1;
+    const uint32_t mul1 = (uint32_t)divx, mul2 = (uint32_t)(divx * divy);
+    const int P2 = next_pow2(n);
+    for (int i = tid; i < P2; i += NT) {
+      uint64_t key = ~0ull;
+      if (i < n) {
+        const float4 a = in[i];
+        const int i0 = (int)(floorf(a.x * inv) - (float)m0);
+        const int i1 = (int)(floorf(a.y * inv) - (float)m1);
+        const int i2 = (int)(floorf(a.z * inv) - (float)m2);
+        key = ((uint64_t)((uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2) << 32) | (uint32_t)i;
+      }
+      keys[i] = key;
+    }
+    __syncthreads();
+    reg_bitonic_sort<NT, E>(keys, P2);
+    int run = 0;
+    for (int base = 0; base < n; base += NT) {
+      const int t = base + tid;
+      const uint32_t k = t < n ? (uint32_t)(keys[t] >> 32) : 0u;
+      const int head = (t < n && (t == 0 || (uint32_t)(keys[t - 1] >> 32) != k)) ? 1 : 0;
+      int tot;
+      const int ex = block_excl_scan<NT>(head, isc, tot);
+      if (head) {
+        int e = t + 1;
+        while (e < n && (uint32_t)(keys[e] >> 32) == k) ++e;
+        float sx = 0, sy = 0, sz = 0, si = 0;
+        for (int mm = t; mm < e; mm += 4) {  // four independent gathers in flight per step
+          float4 a[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) a[u] = in[(uint32_t)keys[min(mm + u, e - 1)]];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (mm + u < e) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
+        }
+        const float cnt = (float)(e - t);
+        j.out[b0 + run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+      }
+      run += tot;
+    }
+    if (tid == 0) j.out_count[s] = run;
+    __syncthreads();  // keys are reused by the next segment
+  }
+}
+
 template <int G>
 void vg_launch_params_keys(const VgJob& j, hipStream_t st) {
   const int grid = std::min((j.nseg + VgGroup<G>::NT / G - 1) / (VgGroup<G>::NT / G), 4096);
@@ -342,8 +435,23 @@ void vg_launch_reduce(const VgJob& j, hipStream_t st) {
 }
 
 // G = threads per segment: 64 for many mostly-empty segments, 256 / 1024 for few large ones
-void vg_run(const VgJob& j, void* tmp, size_t tmp_bytes, hipStream_t st, int G) {
-  if (j.nseg == 0) return;
+// fcap: capacity (points per segment) of the fused kernel — 0 (multi-kernel path only), 2048,
+// 8192 or 16384 (256 x 8, 1024 x 8, 1024 x 16 keys); G: threads per segment of the multi-kernel
+// path (hipCUB segmented radix sort), which finishes the segments beyond fcap.  The fused kernel
+// pays off for a few instances (streaming: one launch instead of four, no global key arrays);
+// for large batches the radix sort's work efficiency wins over the bitonic network.
+void vg_run(const VgJob& j0, void* tmp, size_t tmp_bytes, hipStream_t st, int G, int fcap) {
+  if (j0.nseg == 0) return;
+  const int grid = std::min(j0.nseg, 65536);
+  VgJob j = j0;
+  if (fcap > 0) {
+    if (fcap <= 2048) hipLaunchKernelGGL((k_vg_fused<256, 8>), dim3(grid), dim3(256), 0, st, j0);
+    else if (fcap <= 8192) hipLaunchKernelGGL((k_vg_fused<1024, 8>), dim3(grid), dim3(1024), 0, st, j0);
+    else hipLaunchKernelGGL((k_vg_fused<1024, 16>), dim3(grid), dim3(1024), 0, st, j0);
+    j.begin = j0.big_b;  // the multi-kernel path finishes what the fused kernel could not hold
+    j.end = j0.big_e;
+    j.keep_counts = 1;
+  }
   if (G == 64) vg_launch_params_keys<64>(j, st);
   else if (G == 256) vg_launch_params_keys<256>(j, st);
   else vg_launch_params_keys<1024>(j, st);
@@ -893,32 +1001,34 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
   }
 }
 
-// per valid cube: DS input = old cube content ++ appended points (corner region, then surf region)
+// per valid cube: DS input = old cube content ++ appended points (corner region, then surf region);
+// thread per (kind, valid cube) segment, one block scan for the offsets
 __global__ __launch_bounds__(kMpThreads) void k_mp_vseg(MpBuffers b) {
+  static_assert(2 * kMaxValid <= kMpThreads, "one thread per segment");
   const int p = blockIdx.x, tid = threadIdx.x;
   const int nv = b.istate[(size_t)p * kMpStateInts + kMiNValid];
   const int* slots = slot_table(b, b.pool_cur, p);
   const int* ac = b.app_cnt + (size_t)p * kCubeNum * 2;
-  if (tid == 0) {
-    int run = (int)((size_t)p * b.map_cap);
-    const int lim = (int)((size_t)(p + 1) * b.map_cap);
-    for (int kind = 0; kind < 2; ++kind)
-      for (int v = 0; v < kMaxValid; ++v) {
-        const int sidx = p * 2 * kMaxValid + kind * kMaxValid + v;
-        int n = 0;
-        if (v < nv) {
-          const int ind = b.valid[(size_t)p * kMaxValid + v];
-          n = slots[ind * 4 + 1 + 2 * kind] + ac[ind * 2 + kind];
-        }
-        if (run + n > lim) {
-          b.istate[(size_t)p * kMpStateInts + kMiErr] |= ERR_CAP_MAP;
-          n = 0;
-        }
-        b.vseg_b[sidx] = run;
-        b.vseg_e[sidx] = run + n;
-        b.vseg_leaf[sidx] = kind == 0 ? 0.2f : 0.4f;
-        run += n;
-      }
+  __shared__ int scratch[16];
+  const int kind = tid / kMaxValid, v = tid % kMaxValid;
+  int n = 0;
+  if (tid < 2 * kMaxValid && v < nv) {
+    const int ind = b.valid[(size_t)p * kMaxValid + v];
+    n = slots[ind * 4 + 1 + 2 * kind] + ac[ind * 2 + kind];
+  }
+  int tot;
+  const int ex = block_excl_scan<kMpThreads>(n, scratch, tot);
+  const int lim = b.map_cap;
+  if (tid < 2 * kMaxValid) {
+    // the reference order fills segments in (kind, v) order; a segment that would pass the
+    // capacity is emptied and flags the instance (as the sequential walk did)
+    const bool over = ex + n > lim;
+    const int sidx = p * 2 * kMaxValid + tid;
+    const int base = (int)((size_t)p * b.map_cap) + (over ? 0 : ex);
+    b.vseg_b[sidx] = base;
+    b.vseg_e[sidx] = base + (over ? 0 : n);
+    b.vseg_leaf[sidx] = kind == 0 ? 0.2f : 0.4f;
+    if (over && n > 0) b.istate[(size_t)p * kMpStateInts + kMiErr] |= ERR_CAP_MAP;
   }
 }
 
@@ -942,43 +1052,46 @@ __global__ __launch_bounds__(256) void k_mp_vcopy(MpBuffers b) {
   }
 }
 
-// new cube store: valid cubes <- their DS output, every other cube <- old ++ appended
+// new cube store: valid cubes <- their DS output, every other cube <- old ++ appended.  The
+// (kind, cube) sizes go to LDS in coalesced passes; each thread then owns a contiguous run of
+// them, so the offsets and the non-empty list need one block scan each.
 __global__ __launch_bounds__(kMpThreads) void k_mp_compact_table(MpBuffers b) {
+  constexpr int N = 2 * kCubeNum, E = (N + kMpThreads - 1) / kMpThreads;
   const int p = blockIdx.x, tid = threadIdx.x;
   const int nv = b.istate[(size_t)p * kMpStateInts + kMiNValid];
   const int* old = slot_table(b, b.pool_cur, p);
   int* nw = slot_table(b, 1 - b.pool_cur, p);
   const int* ac = b.app_cnt + (size_t)p * kCubeNum * 2;
-  __shared__ int vidx[kCubeNum];
+  __shared__ int16_t vidx[kCubeNum];
+  __shared__ int nn[N];
   __shared__ int scratch[16];
   for (int s = tid; s < kCubeNum; s += kMpThreads) vidx[s] = -1;
   __syncthreads();
-  if (tid < nv) vidx[b.valid[(size_t)p * kMaxValid + tid]] = tid;
+  if (tid < nv) vidx[b.valid[(size_t)p * kMaxValid + tid]] = (int16_t)tid;
   __syncthreads();
-  int run = 0, vpts = 0, nitems = 0;
+  int vpts = 0;
+  for (int x = tid; x < N; x += kMpThreads) {
+    const int kind = x / kCubeNum, s = x % kCubeNum, v = vidx[s];
+    const int n = v >= 0 ? b.vseg_cnt[p * 2 * kMaxValid + kind * kMaxValid + v] : old[s * 4 + 1 + 2 * kind] + ac[s * 2 + kind];
+    nn[x] = n;
+    if (v >= 0) vpts += n;
+  }
+  __syncthreads();
+  const int x0 = tid * E, x1 = min(N, x0 + E);
+  int sum = 0, ne = 0;
+  for (int x = x0; x < x1; ++x) { sum += nn[x]; ne += nn[x] > 0 ? 1 : 0; }
+  int run, nitems;
+  int off = block_excl_scan<kMpThreads>(sum, scratch, run);
+  int it = block_excl_scan<kMpThreads>(ne, scratch, nitems);
   int* items = b.citems + (size_t)p * 2 * kCubeNum;
-  for (int kind = 0; kind < 2; ++kind)
-    for (int base = 0; base < kCubeNum; base += kMpThreads) {
-      const int s = base + tid;
-      int n = 0, v = -1;
-      if (s < kCubeNum) {
-        v = vidx[s];
-        n = v >= 0 ? b.vseg_cnt[p * 2 * kMaxValid + kind * kMaxValid + v] : old[s * 4 + 1 + 2 * kind] + ac[s * 2 + kind];
-        if (v >= 0) vpts += n;
-      }
-      int tot;
-      const int ex = block_excl_scan<kMpThreads>(n, scratch, tot);
-      if (s < kCubeNum) {
-        nw[s * 4 + 2 * kind] = run + ex;
-        nw[s * 4 + 1 + 2 * kind] = n;
-      }
-      run += tot;
-      // the non-empty (kind, cube) list for the copy: kind | cube << 1 | (valid index + 1) << 14
-      int ntot;
-      const int nex = block_excl_scan<kMpThreads>(n > 0 ? 1 : 0, scratch, ntot);
-      if (n > 0) items[nitems + nex] = kind | (s << 1) | ((v + 1) << 14);
-      nitems += ntot;
-    }
+  for (int x = x0; x < x1; ++x) {
+    const int kind = x / kCubeNum, s = x % kCubeNum, n = nn[x];
+    nw[s * 4 + 2 * kind] = off;
+    nw[s * 4 + 1 + 2 * kind] = n;
+    off += n;
+    // the non-empty (kind, cube) list for the copy: kind | cube << 1 | (valid index + 1) << 14
+    if (n > 0) items[it++] = kind | (s << 1) | (((int)vidx[s] + 1) << 14);
+  }
   vpts = block_reduce<kMpThreads>(vpts, scratch, [](int a, int c) { return a + c; });
   if (tid == 0) {
     b.nitems[p] = nitems;
@@ -1085,6 +1198,8 @@ void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter
   (void)hipMalloc(&b.vg_k2, vgn * sizeof(uint32_t));
   (void)hipMalloc(&b.vg_v, vgn * sizeof(uint32_t));
   (void)hipMalloc(&b.vg_v2, vgn * sizeof(uint32_t));
+  (void)hipMalloc(&b.vg_bb, (size_t)P * 2 * kMaxValid * sizeof(int));
+  (void)hipMalloc(&b.vg_be, (size_t)P * 2 * kMaxValid * sizeof(int));
   const size_t t1 = vg_tmp_bytes((int)vgn, P * 2 * kMaxValid), t2 = vg_tmp_bytes((int)Ps, P * 2);
   b.cub_bytes = t1 > t2 ? t1 : t2;
   (void)hipMalloc(&b.cub_tmp, b.cub_bytes);
@@ -1099,7 +1214,7 @@ void mp_free(MpBuffers& b) {
                   b.stack2, b.stack, b.nstack, b.from, b.hC_start, b.hS_start, b.h_fill, b.hC_T, b.hS_T,
                   b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.citems, b.nitems, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
-                  b.vg_params, b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.cub_tmp, b.reg, b.nreg};
+                  b.vg_params, b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_bb, b.vg_be, b.cub_tmp, b.reg, b.nreg};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = MpBuffers();
@@ -1130,8 +1245,8 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
   VgJob js;
   js.in = b.stack2; js.out = b.stack; js.begin = b.sseg_b; js.end = b.sseg_e; js.leaf = b.sseg_leaf;
   js.out_count = b.sseg_cnt; js.params = b.vg_params; js.keys = b.vg_k; js.keys_alt = b.vg_k2;
-  js.vals = b.vg_v; js.vals_alt = b.vg_v2; js.nseg = 2 * P; js.total = P * b.cap_stack;
-  vg_run(js, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 1024 : 256);  // two large segments per instance
+  js.vals = b.vg_v; js.vals_alt = b.vg_v2; js.big_b = b.vg_bb; js.big_e = b.vg_be; js.nseg = 2 * P; js.total = P * b.cap_stack;
+  vg_run(js, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 1024 : 256, P <= 4 ? 16384 : 0);  // two large segments per instance
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);
   mark("k_mp_gather");
@@ -1168,8 +1283,8 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
   VgJob jv;
   jv.in = b.vin; jv.out = b.vout; jv.begin = b.vseg_b; jv.end = b.vseg_e; jv.leaf = b.vseg_leaf;
   jv.out_count = b.vseg_cnt; jv.params = b.vg_params; jv.keys = b.vg_k; jv.keys_alt = b.vg_k2;
-  jv.vals = b.vg_v; jv.vals_alt = b.vg_v2; jv.nseg = 2 * kMaxValid * P; jv.total = P * b.map_cap;
-  vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 256 : 64);    // 2 x 125 cube segments per instance
+  jv.vals = b.vg_v; jv.vals_alt = b.vg_v2; jv.big_b = b.vg_bb; jv.big_e = b.vg_be; jv.nseg = 2 * kMaxValid * P; jv.total = P * b.map_cap;
+  vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 256 : 64, P <= 4 ? 16384 : 0);    // 2 x 125 cube segments per instance
   mark("vg_cubes");
   hipLaunchKernelGGL(k_mp_compact_table, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);
@@ -1303,8 +1418,8 @@ int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::s
   VgJob j;
   j.in = b.vin; j.out = b.vout; j.begin = b.vseg_b; j.end = b.vseg_e; j.leaf = b.vseg_leaf;
   j.out_count = b.vseg_cnt; j.params = b.vg_params; j.keys = b.vg_k; j.keys_alt = b.vg_k2;
-  j.vals = b.vg_v; j.vals_alt = b.vg_v2; j.nseg = 1; j.total = b.P * b.map_cap;
-  vg_run(j, b.cub_tmp, b.cub_bytes, st, 1024);
+  j.vals = b.vg_v; j.vals_alt = b.vg_v2; j.big_b = b.vg_bb; j.big_e = b.vg_be; j.nseg = 1; j.total = b.P * b.map_cap;
+  vg_run(j, b.cub_tmp, b.cub_bytes, st, 1024, 16384);
   int cnt = 0;
   (void)hipMemcpyAsync(&cnt, b.vseg_cnt, sizeof(int), hipMemcpyDeviceToHost, st);
   const hipError_t he = hipStreamSynchronize(st);

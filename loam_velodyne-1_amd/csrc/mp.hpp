@@ -44,6 +44,9 @@ struct VgJob {
   uint32_t *keys, *keys_alt, *vals, *vals_alt;
   int nseg;
   int total;             // size of in / out / keys arrays
+  int* big_b = nullptr;  // [nseg] segments beyond the fused kernel's LDS capacity (else empty),
+  int* big_e = nullptr;  //        finished by the multi-kernel path
+  int keep_counts = 0;   // multi-kernel path over big_b/big_e: leave other segments' counts alone
 };
 
 struct MpBuffers {
@@ -87,6 +90,7 @@ struct MpBuffers {
   float* sseg_leaf = nullptr;
   int* vg_params = nullptr;
   uint32_t *vg_k = nullptr, *vg_k2 = nullptr, *vg_v = nullptr, *vg_v2 = nullptr;
+  int *vg_bb = nullptr, *vg_be = nullptr;  // [P][2][kMaxValid] big-segment ranges of vg_run
   void* cub_tmp = nullptr;
   size_t cub_bytes = 0;
   float4* reg = nullptr;      // [P][capS] registered full cloud

@@ -1005,33 +1005,32 @@ __global__ __launch_bounds__(kSelThreads) __attribute__((amdgpu_waves_per_eu(MOD
 
 // ---------------------------------------------------------------- compaction
 __global__ __launch_bounds__(256) void k_sr_compact(SrBuffers b, SrParams p) {
-  const int s = blockIdx.x, tid = threadIdx.x, R = p.R;
-  __shared__ int off[4][65];
-  if (tid == 0) {
-    int run[4] = {0, 0, 0, 0};
-    for (int r = 0; r < R; ++r)
-      for (int k = 0; k < 4; ++k) {
-        off[k][r] = run[k];
-        run[k] += b.st_cnt[(size_t)(s * R + r) * 4 + k];
-      }
-    for (int k = 0; k < 4; ++k) { off[k][R] = run[k]; b.cnt[s * 4 + k] = run[k]; }
+  // one workgroup per (ring, sweep): the ring's offsets are the counts of the rings before it
+  const int r = blockIdx.x, s = blockIdx.y, tid = threadIdx.x, R = p.R;
+  __shared__ int off[4];
+  if (tid < 4) {
+    int run = 0, all = 0;
+    for (int q = 0; q < R; ++q) {
+      const int c = b.st_cnt[(size_t)(s * R + q) * 4 + tid];
+      run += q < r ? c : 0;
+      all += c;
+    }
+    off[tid] = run;
+    if (r == 0) b.cnt[s * 4 + tid] = all;
   }
   __syncthreads();
   const float4* pts = b.full + (size_t)s * b.cap;
-  for (int r = 0; r < R; ++r) {
-    const int* c = b.st_cnt + (size_t)(s * R + r) * 4;
-    for (int t = tid; t < c[0]; t += 256)
-      b.sharp[(size_t)s * kSharpPerRing * R + off[0][r] + t] =
-          pts[b.st_sharp[(size_t)(s * R + r) * kSharpPerRing + t]];
-    for (int t = tid; t < c[1]; t += 256)
-      b.lsharp[(size_t)s * kLessSharpPerRing * R + off[1][r] + t] =
-          pts[b.st_lsharp[(size_t)(s * R + r) * kLessSharpPerRing + t]];
-    for (int t = tid; t < c[2]; t += 256)
-      b.flat[(size_t)s * kFlatPerRing * R + off[2][r] + t] =
-          pts[b.st_flat[(size_t)(s * R + r) * kFlatPerRing + t]];
-    for (int t = tid; t < c[3]; t += 256)
-      b.lflat[(size_t)s * b.cap + off[3][r] + t] = b.st_lflat[(size_t)s * R * kRingCap + b.st_loff[s * R + r] + t];
-  }
+  const int* c = b.st_cnt + (size_t)(s * R + r) * 4;
+  const int c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
+  for (int t = tid; t < c0; t += 256)
+    b.sharp[(size_t)s * kSharpPerRing * R + off[0] + t] = pts[b.st_sharp[(size_t)(s * R + r) * kSharpPerRing + t]];
+  for (int t = tid; t < c1; t += 256)
+    b.lsharp[(size_t)s * kLessSharpPerRing * R + off[1] + t] =
+        pts[b.st_lsharp[(size_t)(s * R + r) * kLessSharpPerRing + t]];
+  for (int t = tid; t < c2; t += 256)
+    b.flat[(size_t)s * kFlatPerRing * R + off[2] + t] = pts[b.st_flat[(size_t)(s * R + r) * kFlatPerRing + t]];
+  const float4* lf = b.st_lflat + (size_t)s * R * kRingCap + b.st_loff[s * R + r];
+  for (int t = tid; t < c3; t += 256) b.lflat[(size_t)s * b.cap + off[3] + t] = lf[t];
 }
 
 }  // namespace
@@ -1106,7 +1105,7 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
   hipLaunchKernelGGL((k_sr_select<kRingCap, 1>), dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
   hipLaunchKernelGGL((k_sr_select<16, 2>), dim3(kBigSlots), dim3(kSelThreads), 0, st, b, p);
   mark("k_sr_select");
-  hipLaunchKernelGGL(k_sr_compact, dim3(b.S), dim3(256), 0, st, b, p);
+  hipLaunchKernelGGL(k_sr_compact, dim3(b.R, b.S), dim3(256), 0, st, b, p);
   mark("k_sr_compact");
 }
 
