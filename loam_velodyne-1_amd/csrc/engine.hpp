@@ -49,6 +49,8 @@ struct SrBuffers {
   int* st_flat = nullptr;    // [S][R][24]
   float4* st_lflat = nullptr;  // [S][R][kRingCap] downsampled points
   int* st_cnt = nullptr;     // [S][R][4]
+  uint16_t* st_cand = nullptr;  // [S][R][kRingCap] lessFlat candidates (ring-relative), k_sr_pick -> k_sr_ringvg
+  int* st_ncand = nullptr;   // [S][R]
   float4* sharp = nullptr;   // [S][12R]
   float4* lsharp = nullptr;  // [S][120R]
   float4* flat = nullptr;    // [S][24R]

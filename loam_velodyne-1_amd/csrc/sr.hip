@@ -523,6 +523,100 @@ struct SelShared {
   int nsharp, nlsharp, nflat, ncand, wf, big, loff;
 };
 
+// PCL VoxelGrid 0.2 of one ring's lessFlat candidates pts[lo + cand[0..nc)) into
+// outp (capacity outcap), the whole workgroup (:575-579): bbox, (voxel, candidate) keys, sort,
+// ordered per-voxel float means.  Returns the voxel count (clamped to outcap, *err flagged).
+template <int CAP, bool BIG, typename CandT>
+LOAM_D int ring_vg(const float4* pts, int lo, const CandT* cand, int nc, uint64_t* keys, float4* outp, int outcap,
+                   float (*red)[kSelThreads / 64], int* scratch, int* err) {
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+  for (int t = tid; t < nc; t += kSelThreads) {
+    const float4 a = pts[lo + cand[t]];
+    mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
+    mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
+  }
+  for (int d = 0; d < 3; ++d) {
+    mn[d] = wave_min_f(mn[d]);
+    mx[d] = wave_max_f(mx[d]);
+    if (lane == 0) { red[d][w] = mn[d]; red[3 + d][w] = mx[d]; }
+  }
+  __syncthreads();
+  for (int d = 0; d < 3; ++d)
+    for (int v = 0; v < kSelThreads / 64; ++v) {
+      mn[d] = fminf(mn[d], red[d][v]);
+      mx[d] = fmaxf(mx[d], red[3 + d][v]);
+    }
+  __syncthreads();
+  int nout = 0;
+  if (nc > 0) {
+    const float inv = 1.0f / 0.2f;
+    const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
+    const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
+    const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
+    if (dx * dy * dz > (int64_t)0x7fffffff) {  // "leaf size too small": output = input
+      for (int t = tid; t < nc; t += kSelThreads)
+        if (t < outcap) outp[t] = pts[lo + cand[t]];
+      nout = nc;
+    } else {
+      int minb[3], maxb[3];
+      for (int d = 0; d < 3; ++d) {
+        minb[d] = (int)floorf(mn[d] * inv);
+        maxb[d] = (int)floorf(mx[d] * inv);
+      }
+      const int divx = maxb[0] - minb[0] + 1, divy = maxb[1] - minb[1] + 1;
+      const int mul1 = divx, mul2 = divx * divy;
+      const int P2c = next_pow2(nc);
+      for (int t = tid; t < P2c; t += kSelThreads) {
+        uint64_t key = ~0ull;
+        if (t < nc) {
+          const float4 a = pts[lo + cand[t]];
+          int i0 = (int)(floorf(a.x * inv) - (float)minb[0]);
+          int i1 = (int)(floorf(a.y * inv) - (float)minb[1]);
+          int i2 = (int)(floorf(a.z * inv) - (float)minb[2]);
+          uint32_t idx = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
+          key = ((uint64_t)idx << 32) | (uint32_t)t;
+        }
+        keys[t] = key;
+      }
+      __syncthreads();
+      if constexpr (BIG) block_bitonic_sort<kSelThreads>(keys, P2c);
+      else reg_bitonic_sort<kSelThreads, CAP / kSelThreads>(keys, P2c);
+      int run = 0;
+      for (int base = 0; base < nc; base += kSelThreads) {
+        const int t = base + tid;
+        const int head = (t < nc && (t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32))) ? 1 : 0;
+        int tot;
+        const int ex = block_excl_scan<kSelThreads>(head, scratch, tot);
+        if (head) {
+          const uint32_t vk = (uint32_t)(keys[t] >> 32);
+          int e = t + 1;
+          while (e < nc && (uint32_t)(keys[e] >> 32) == vk) ++e;
+          // members summed in sorted order; four independent gathers in flight per step
+          float sx = 0, sy = 0, sz = 0, si = 0;
+          for (int m = t; m < e; m += 4) {
+            float4 a[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a[u] = pts[lo + cand[(int)(keys[min(m + u, e - 1)] & 0xffffffffu)]];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (m + u < e) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
+          }
+          const float cnt = (float)(e - t);
+          if (run + ex < outcap) outp[run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+        }
+        run += tot;
+      }
+      nout = run;
+    }
+    if (nout > outcap) {
+      if (tid == 0) atomicOr(err, ERR_CAP_RING);
+      nout = outcap;
+    }
+  }
+  return nout;
+}
+
 // :495-520 with the distance tests precomputed as gap bits.  One wave: lanes 0-4 take offsets
 // +1..+5, lanes 8-12 offsets -1..-5; each direction marks up to its first stop (the reference's
 // break), found with one ballot.  Every lane of the wave must call it (ind is wave-uniform).
@@ -827,96 +921,9 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
     __syncthreads();
   }
   // ---- PCL VoxelGrid 0.2 of the ring's lessFlat candidates (:575-579)
-  const int nc = sh.ncand;
-  float4* outp = b.st_lflat + (size_t)s * R * kRingCap + loff;
-  const int outcap = BIG ? R * kRingCap - loff : kRingCap;
-  float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
-  for (int t = tid; t < nc; t += kSelThreads) {
-    const float4 a = pts[lo + cand[t]];
-    mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
-    mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
-  }
-  for (int d = 0; d < 3; ++d) {
-    mn[d] = wave_min_f(mn[d]);
-    mx[d] = wave_max_f(mx[d]);
-    if (lane == 0) { sh.red[d][w] = mn[d]; sh.red[3 + d][w] = mx[d]; }
-  }
-  __syncthreads();
-  for (int d = 0; d < 3; ++d)
-    for (int v = 0; v < kSelThreads / 64; ++v) {
-      mn[d] = fminf(mn[d], sh.red[d][v]);
-      mx[d] = fmaxf(mx[d], sh.red[3 + d][v]);
-    }
-  __syncthreads();
+  const int nout = ring_vg<CAP, BIG>(pts, lo, cand, sh.ncand, keys, b.st_lflat + (size_t)s * R * kRingCap + loff,
+                                     BIG ? R * kRingCap - loff : kRingCap, sh.red, sh.scratch, b.err + s);
   PH(3);
-  int nout = 0;
-  if (nc > 0) {
-    const float inv = 1.0f / 0.2f;
-    const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
-    const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
-    const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
-    if (dx * dy * dz > (int64_t)0x7fffffff) {  // "leaf size too small": output = input
-      for (int t = tid; t < nc; t += kSelThreads)
-        if (t < outcap) outp[t] = pts[lo + cand[t]];
-      nout = nc;
-    } else {
-      int minb[3], maxb[3];
-      for (int d = 0; d < 3; ++d) {
-        minb[d] = (int)floorf(mn[d] * inv);
-        maxb[d] = (int)floorf(mx[d] * inv);
-      }
-      const int divx = maxb[0] - minb[0] + 1, divy = maxb[1] - minb[1] + 1;
-      const int mul1 = divx, mul2 = divx * divy;
-      const int P2c = next_pow2(nc);
-      for (int t = tid; t < P2c; t += kSelThreads) {
-        uint64_t key = ~0ull;
-        if (t < nc) {
-          const float4 a = pts[lo + cand[t]];
-          int i0 = (int)(floorf(a.x * inv) - (float)minb[0]);
-          int i1 = (int)(floorf(a.y * inv) - (float)minb[1]);
-          int i2 = (int)(floorf(a.z * inv) - (float)minb[2]);
-          uint32_t idx = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
-          key = ((uint64_t)idx << 32) | (uint32_t)t;
-        }
-        keys[t] = key;
-      }
-      __syncthreads();
-  PH(4);
-      if constexpr (BIG) block_bitonic_sort<kSelThreads>(keys, P2c);
-      else reg_bitonic_sort<kSelThreads, CAP / kSelThreads>(keys, P2c);
-  PH(5);
-      int run = 0;
-      for (int base = 0; base < nc; base += kSelThreads) {
-        const int t = base + tid;
-        const int head = (t < nc && (t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32))) ? 1 : 0;
-        int tot;
-        const int ex = block_excl_scan<kSelThreads>(head, sh.scratch, tot);
-        if (head) {
-          const uint32_t vk = (uint32_t)(keys[t] >> 32);
-          int e = t + 1;
-          while (e < nc && (uint32_t)(keys[e] >> 32) == vk) ++e;
-          // members summed in sorted order; four independent gathers in flight per step
-          float sx = 0, sy = 0, sz = 0, si = 0;
-          for (int m = t; m < e; m += 4) {
-            float4 a[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) a[u] = pts[lo + cand[(int)(keys[min(m + u, e - 1)] & 0xffffffffu)]];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              if (m + u < e) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
-          }
-          const float cnt = (float)(e - t);
-          if (run + ex < outcap) outp[run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
-        }
-        run += tot;
-      }
-      nout = run;
-    }
-    if (nout > outcap) {
-      if (tid == 0) b.err[s] |= ERR_CAP_RING;
-      nout = outcap;
-    }
-  }
   // pick lists -> staging
   const int ns = sh.nsharp, nl = sh.nlsharp, nf = sh.nflat;
   for (int t = tid; t < ns; t += kSelThreads) b.st_sharp[(size_t)(s * R + q) * kSharpPerRing + t] = sh.picks[t];
@@ -935,6 +942,146 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
   __threadfence();
   __syncthreads();
   PH(6);
+}
+
+// ---------------------------------------------------------------- selection split: picks / VoxelGrid
+// Sweeps whose rings are independent and at most kPickCap points long (every VLP-16 / HDL-64E
+// sweep without an empty ring) take two kernels instead of k_sr_select<2048, 0>:
+//  k_sr_pick    one WAVE per ring (kPickWaves rings per workgroup): the greedy sharp / flat picks
+//               of the six segments (select_segment_fast, wave-synchronous, no workgroup barrier)
+//               and the ring's lessFlat candidate list, to global memory;
+//  k_sr_ringvg  one workgroup per ring: the PCL VoxelGrid of the candidates (ring_vg).
+// The serial greedy walk no longer holds three idle waves of a workgroup at barriers, and the
+// VoxelGrid runs at full workgroup occupancy.  Other sweeps fall to k_sr_select<4096, 1> / <16, 2>
+// exactly as before (sel_big).
+constexpr int kPickCap = 2048;
+constexpr int kPickWaves = 4;
+
+struct PickWave {
+  uint8_t pk[kPickCap + 16];
+  int8_t lab[kPickCap + 16];
+  uint64_t list[512];
+  int picks[kSharpPerRing + kLessSharpPerRing + kFlatPerRing];
+  int nsharp, nlsharp, nflat;
+};
+
+// the sweep's ring bounds (:392-393 fix-ups) into se[0..2R), and the selection route of the sweep
+// (0: rings independent and <= cap points, 1: k_sr_select<4096, 1>), by thread 0
+LOAM_D int sweep_route(const SrBuffers& b, int s, int R, int n, int cap, int* se, int* order) {
+  const int tid = threadIdx.x;
+  if (tid < R) {
+    int st = b.ring_se[s * 2 * R + tid], en = b.ring_se[s * 2 * R + R + tid];
+    if (tid == 0) st = 5;
+    if (tid == R - 1) en = n - 5;
+    se[tid] = st;
+    se[R + tid] = en;
+  }
+  __syncthreads();
+  int next = 0;
+  if (tid == 0) {
+    // rings are independent when their active spans [start, end-1] are more than 5 points apart
+    int wf = 1, prev_hi = -100000, maxspan = 0, na = 0;
+    for (int r = 0; r < R; ++r)
+      if (se[r] <= se[R + r] - 1) order[na++] = r;
+    for (int a = 1; a < na; ++a) {
+      int v = order[a], c = a;
+      while (c > 0 && se[order[c - 1]] > se[v]) { order[c] = order[c - 1]; --c; }
+      order[c] = v;
+    }
+    for (int a = 0; a < na; ++a) {
+      const int lo = se[order[a]], hi = se[R + order[a]] - 1;
+      if (lo < 0 || hi >= n || lo - prev_hi <= 5) wf = 0;
+      maxspan = max(maxspan, hi - lo + 1);
+      prev_hi = hi;
+    }
+    if (n > 0 && (!wf || maxspan > cap)) next = 1;
+  }
+  return next;
+}
+
+__global__ __launch_bounds__(64 * kPickWaves) void k_sr_pick(SrBuffers b, SrParams p) {
+  const int s = blockIdx.y, tid = threadIdx.x, w = tid >> 6, lane = lane_id(), R = p.R;
+  const int q = blockIdx.x * kPickWaves + w;
+  __shared__ int se[128], order[64], sh_route;
+  __shared__ PickWave pw[kPickWaves];
+  const int n = b.n_full[s];
+  const int route = sweep_route(b, s, R, n, kPickCap, se, order);
+  if (tid == 0) {
+    sh_route = route;
+    if (blockIdx.x == 0) b.sel_big[s] = route;
+  }
+  __syncthreads();
+  if (sh_route != 0 || q >= R) return;  // wave-uniform from here on: no workgroup barrier below
+  PickWave& P = pw[w];
+  int* st_cnt = b.st_cnt + (size_t)(s * R + q) * 4;
+  if (lane == 0) b.st_loff[s * R + q] = q * kRingCap;
+  const int sq = se[q], eq = se[R + q];
+  const int lo = sq, hi = eq - 1;
+  if (n <= 0 || lo > hi || hi - lo + 1 > kPickCap || lo < 0 || hi >= n) {
+    if (n > 0 && lo <= hi && lane == 0) atomicOr(&b.err[s], ERR_CAP_RING);
+    if (lane < 4) st_cnt[lane] = 0;
+    if (lane == 0) b.st_ncand[s * R + q] = 0;
+    return;
+  }
+  const int wlo = max(0, lo - 5), whi = min(n - 1, hi + 5);
+  const uint8_t* pick_g = b.picked + (size_t)s * b.cap;
+  for (int k = wlo + lane; k <= whi; k += 64) {
+    P.pk[k - wlo] = pick_g[k];
+    P.lab[k - wlo] = 0;
+  }
+  if (lane == 0) { P.nsharp = 0; P.nlsharp = 0; P.nflat = 0; }
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+  const float* cv = b.curv + (size_t)s * b.cap + lo;
+  uint16_t* cand = b.st_cand + (size_t)(s * R + q) * kRingCap;
+  int run = 0;
+  for (int j = 0; j < 6; ++j) {
+    const int s0 = (sq * (6 - j) + eq * j) / 6, s1 = (sq * (5 - j) + eq * (j + 1)) / 6;  // sp_j, ep_j + 1
+    if (s1 - 1 < s0) continue;
+    select_segment_fast(n, lo, s0 - lo, s1 - 1 - lo, cv, P.list, P.pk, P.lab, wlo, P.picks, P.nsharp, P.nlsharp,
+                        P.nflat);
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    // (:568-572) lessFlat candidates of this segment, in position order
+    for (int base = s0; base < s1; base += 64) {
+      const int k = base + lane;
+      const bool flag = k < s1 && P.lab[k - wlo] <= 0;
+      const uint64_t m = __ballot(flag);
+      if (flag) cand[run + __popcll(m & lanemask_lt())] = (uint16_t)(k - lo);
+      run += __popcll(m);
+    }
+  }
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+  const int ns = P.nsharp, nl = P.nlsharp, nf = P.nflat;
+  for (int t = lane; t < ns; t += 64) b.st_sharp[(size_t)(s * R + q) * kSharpPerRing + t] = P.picks[t];
+  for (int t = lane; t < nl; t += 64) b.st_lsharp[(size_t)(s * R + q) * kLessSharpPerRing + t] = P.picks[kSharpPerRing + t];
+  for (int t = lane; t < nf; t += 64)
+    b.st_flat[(size_t)(s * R + q) * kFlatPerRing + t] = P.picks[kSharpPerRing + kLessSharpPerRing + t];
+  if (lane == 0) { st_cnt[0] = ns; st_cnt[1] = nl; st_cnt[2] = nf; b.st_ncand[s * R + q] = run; }
+}
+
+__global__ __launch_bounds__(kSelThreads) void k_sr_ringvg(SrBuffers b, SrParams p) {
+  const int q = blockIdx.x, s = blockIdx.y, tid = threadIdx.x, R = p.R;
+  if (b.sel_big[s] != 0) return;
+  const int n = b.n_full[s];
+  if (n <= 0) return;
+  int lo = b.ring_se[s * 2 * R + q], en = b.ring_se[s * 2 * R + R + q];
+  if (q == 0) lo = 5;
+  if (q == R - 1) en = n - 5;
+  if (lo > en - 1) return;
+  __shared__ uint64_t keys[kPickCap];
+  __shared__ uint16_t cand[kPickCap];
+  __shared__ float red[6][kSelThreads / 64];
+  __shared__ int scratch[16];
+  const int nc = min(b.st_ncand[s * R + q], kPickCap);
+  const uint16_t* cg = b.st_cand + (size_t)(s * R + q) * kRingCap;
+  for (int t = tid; t < nc; t += kSelThreads) cand[t] = cg[t];
+  __syncthreads();
+  const int nout = ring_vg<kPickCap, false>(b.full + (size_t)s * b.cap, lo, cand, nc, keys,
+                                            b.st_lflat + (size_t)s * R * kRingCap + q * kRingCap, kRingCap, red,
+                                            scratch, b.err + s);
+  if (tid == 0) b.st_cnt[(size_t)(s * R + q) * 4 + 3] = nout;
 }
 
 // Three instantiations, chosen per sweep: CAP = 2048 (34 KB of LDS, four workgroups per CU)
@@ -1059,6 +1206,8 @@ void sr_alloc(SrBuffers& b, int S, int cap, int R) {
   HIPCHK(hipMalloc(&b.st_flat, (size_t)S * R * kFlatPerRing * sizeof(int)));
   HIPCHK(hipMalloc(&b.st_lflat, (size_t)S * R * kRingCap * sizeof(float4)));
   HIPCHK(hipMalloc(&b.st_cnt, (size_t)S * R * 4 * sizeof(int)));
+  HIPCHK(hipMalloc(&b.st_cand, (size_t)S * R * kRingCap * sizeof(uint16_t)));
+  HIPCHK(hipMalloc(&b.st_ncand, (size_t)S * R * sizeof(int)));
   HIPCHK(hipMalloc(&b.sharp, (size_t)S * R * kSharpPerRing * sizeof(float4)));
   HIPCHK(hipMalloc(&b.lsharp, (size_t)S * R * kLessSharpPerRing * sizeof(float4)));
   HIPCHK(hipMalloc(&b.flat, (size_t)S * R * kFlatPerRing * sizeof(float4)));
@@ -1076,7 +1225,7 @@ void sr_alloc(SrBuffers& b, int S, int cap, int R) {
 void sr_free(SrBuffers& b) {
   void* ptrs[] = {b.raw, b.raw_n, b.tmp_ori, b.tmp_sid, b.tilecnt, b.tileF, b.sweep_ori, b.full, b.n_full, b.curv,
                   b.picked, b.sortind, b.label, b.ring_se, b.st_sharp, b.st_lsharp, b.st_flat,
-                  b.st_lflat, b.st_cnt, b.sharp, b.lsharp, b.flat, b.lflat, b.cnt, b.err, b.sel_big, b.st_loff, b.big_keys, b.big_sidx, b.big_cand};
+                  b.st_lflat, b.st_cnt, b.st_cand, b.st_ncand, b.sharp, b.lsharp, b.flat, b.lflat, b.cnt, b.err, b.sel_big, b.st_loff, b.big_keys, b.big_sidx, b.big_cand};
   for (void* q : ptrs)
     if (q) HIPCHK(hipFree(q));
   b = SrBuffers();
@@ -1101,7 +1250,12 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
   hipLaunchKernelGGL(k_sr_features, dim3((b.cap + kFeatTile - 1) / kFeatTile, b.S), dim3(kFeatTile), 0,
                      st, b, p);
   mark("k_sr_features");
+#ifdef LOAM_EXP_NOSPLIT
   hipLaunchKernelGGL((k_sr_select<2048, 0>), dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
+#else
+  hipLaunchKernelGGL(k_sr_pick, dim3((b.R + kPickWaves - 1) / kPickWaves, b.S), dim3(64 * kPickWaves), 0, st, b, p);
+  hipLaunchKernelGGL(k_sr_ringvg, dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
+#endif
   hipLaunchKernelGGL((k_sr_select<kRingCap, 1>), dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
   hipLaunchKernelGGL((k_sr_select<16, 2>), dim3(kBigSlots), dim3(kSelThreads), 0, st, b, p);
   mark("k_sr_select");
