@@ -457,30 +457,43 @@ LOAM_HD bool qr_solve(float* A, float* b, int m, int n, float* x, float* ws) {
   float* v = ws;
   float* h = ws + 8;
   const float eps = 1.1920928955078125e-07f * 10;
+#pragma unroll
   for (int l = 0; l < n; ++l) {
     const int len = m - l;
     float nrm = 0.0f;
+#pragma unroll
     for (int i = 0; i < len; ++i) { v[i] = A[(l + i) * n + l]; nrm += v[i] * v[i]; }
     const float v0 = v[0];
     v[0] = v[0] + sgn1(v[0]) * sqrtf(nrm);
     nrm = sqrtf(nrm + v[0] * v[0] - v0 * v0);
+#pragma unroll
     for (int i = 0; i < len; ++i) v[i] /= nrm;
+#pragma unroll
     for (int j = l; j < n; ++j) {
       float dot = 0.0f;
+#pragma unroll
       for (int i = l; i < m; ++i) dot += v[i - l] * A[i * n + j];
+#pragma unroll
       for (int i = l; i < m; ++i) A[i * n + j] -= 2 * v[i - l] * dot;
     }
     h[l] = v[0] * v[0];
+#pragma unroll
     for (int i = 1; i < len; ++i) A[(l + i) * n + l] = v[i] / v[0];
   }
+#pragma unroll
   for (int l = 0; l < n; ++l) {
     v[0] = 1.0f;
+#pragma unroll
     for (int j = 1; j < m - l; ++j) v[j] = A[(j + l) * n + l];
     float dot = 0.0f;
+#pragma unroll
     for (int i = l; i < m; ++i) dot += v[i - l] * b[i];
+#pragma unroll
     for (int i = l; i < m; ++i) b[i] -= 2 * v[i - l] * dot * h[l];
   }
+#pragma unroll
   for (int i = n - 1; i >= 0; --i) {
+#pragma unroll
     for (int j = n - 1; j > i; --j) b[i] -= b[j] * A[i * n + j];
     if (fabsf(A[i * n + i]) < eps) {
       for (int q = 0; q < n; ++q) x[q] = 0.0f;
@@ -639,8 +652,9 @@ LOAM_HD void gemm_d(const float* A, const float* B, int m, int k, int n, float* 
 constexpr int kLmWs = 36 * 6 + 6 + 14 + 6;
 LOAM_HD void lm_step(const float* AtA_in, const float* AtB_in, int iter, float eig_thresh,
                      int* isDegenerate, float* matP, float* X, float* ws, int* iws) {
-  float* A = ws;            // 36
-  float* b = ws + 36;       // 6
+  // the QR solve of every iteration works in registers (fully unrolled, constant indices); the
+  // iteration-0 analysis (pivoted Jacobi / LU, data-dependent indices) in ws
+  float A[36], b[6], qws[14];
   float* A2 = ws + 42;      // 36
   float* V = ws + 78;       // 36
   float* V2 = ws + 114;     // 36
@@ -649,7 +663,7 @@ LOAM_HD void lm_step(const float* AtA_in, const float* AtB_in, int iter, float e
   float* tmp = ws + 192;    // 36 (LU rhs) / 14 (QR) / 6 (X2)
   for (int i = 0; i < 36; ++i) A[i] = AtA_in[i];
   for (int i = 0; i < 6; ++i) b[i] = AtB_in[i];
-  qr_solve(A, b, 6, 6, X, tmp);
+  qr_solve(A, b, 6, 6, X, qws);
   if (iter == 0) {
     for (int i = 0; i < 36; ++i) A2[i] = AtA_in[i];
     jacobi<6>(A2, E, V, iws);

@@ -1032,23 +1032,45 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_vseg(MpBuffers b) {
   }
 }
 
+// the DS input of every valid-cube segment, flattened over the instance's points: the segments
+// are contiguous in (kind, valid cube) order, so a point finds its segment by binary search over
+// their starts (LDS) and copies from the old pool or the appended stack points
 __global__ __launch_bounds__(256) void k_mp_vcopy(MpBuffers b) {
-  const int p = blockIdx.y;
+  constexpr int NS = 2 * kMaxValid;
+  const int p = blockIdx.y, tid = threadIdx.x;
+  if (b.istate[(size_t)p * kMpStateInts + kMiErr] & ERR_CAP_MAP) return;
   const int nv = b.istate[(size_t)p * kMpStateInts + kMiNValid];
   const int* slots = slot_table(b, b.pool_cur, p);
   const float4* pool = b.pool + ((size_t)b.pool_cur * b.P + p) * b.map_cap;
-  const int* ac = b.app_cnt + (size_t)p * kCubeNum * 2;
   const int* ao = b.app_off + (size_t)p * kCubeNum * 2;
   const float4* app = b.app + (size_t)p * b.cap_stack;
-  for (int sg = blockIdx.x; sg < 2 * nv; sg += gridDim.x) {
-    const int kind = sg / nv, v = sg % nv;
-    const int sidx = p * 2 * kMaxValid + kind * kMaxValid + v;
-    const int ind = b.valid[(size_t)p * kMaxValid + v];
-    const int b0 = b.vseg_b[sidx], n = b.vseg_e[sidx] - b0;
-    const int nold = slots[ind * 4 + 1 + 2 * kind], off = slots[ind * 4 + 2 * kind];
-    for (int t = threadIdx.x; t < n; t += 256)
-      b.vin[b0 + t] = t < nold ? pool[off + t] : app[ao[ind * 2 + kind] + (t - nold)];
-    (void)ac;
+  __shared__ int sb[NS + 1], snold[NS], soff[NS], sapp[NS];
+  const int base = (int)((size_t)p * b.map_cap);
+  if (tid < NS) {
+    const int kind = tid / kMaxValid, v = tid % kMaxValid;
+    sb[tid] = b.vseg_b[p * NS + tid] - base;
+    int nold = 0, off = 0, ap = 0;
+    if (v < nv) {
+      const int ind = b.valid[(size_t)p * kMaxValid + v];
+      nold = slots[ind * 4 + 1 + 2 * kind];
+      off = slots[ind * 4 + 2 * kind];
+      ap = ao[ind * 2 + kind];
+    }
+    snold[tid] = nold;
+    soff[tid] = off;
+    sapp[tid] = ap;
+  }
+  if (tid == 0) sb[NS] = b.vseg_e[p * NS + NS - 1] - base;
+  __syncthreads();
+  const int total = sb[NS];
+  for (int i = blockIdx.x * 256 + tid; i < total; i += gridDim.x * 256) {
+    int lo = 0, hi = NS - 1;  // last segment whose start is <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (sb[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const int t = i - sb[lo];
+    b.vin[base + i] = t < snold[lo] ? pool[soff[lo] + t] : app[sapp[lo] + (t - snold[lo])];
   }
 }
 
@@ -1235,7 +1257,7 @@ void mp_reset(MpBuffers& b, hipStream_t st) {
   hipLaunchKernelGGL(k_mp_reset, dim3((b.P + 255) / 256), dim3(256), 0, st, b);
 }
 
-void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
+void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool map_empty) {
   const int P = b.P;
   auto mark = [&](const char* n) { if (prof) prof->mark(n); };
   hipLaunchKernelGGL(k_mp_prepare, dim3(P), dim3(kMpThreads), 0, st, b, in);
@@ -1264,8 +1286,11 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof) {
   hipLaunchKernelGGL(k_hash_build, dim3(P), dim3(256), 0, st, hs);
   mark("k_hash_build_map");
   hipLaunchKernelGGL(k_mp_lm_begin, dim3((P + 255) / 256), dim3(256), 0, st, b);
-  const int gq = std::min(64, (b.cap_stack + kMpQueryThreads - 1) / kMpQueryThreads);
-  for (int it = 0; it < b.max_iter; ++it) {
+  // workgroups per instance: all the stack's queries at once for a few instances; for large
+  // batches about one pass over a VLP-16 stack (bigger stacks loop), fewer idle workgroups
+  const int gq = std::min(P >= 64 ? 24 : 64, (b.cap_stack + kMpQueryThreads - 1) / kMpQueryThreads);
+  // an empty map store (the first frame after a reset) cannot run the L-M (:706): no launches
+  for (int it = 0; it < (map_empty ? 0 : b.max_iter); ++it) {
     hipLaunchKernelGGL(k_mp_nn, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
     mark("k_mp_nn");
     hipLaunchKernelGGL(k_mp_fit, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
@@ -1450,7 +1475,7 @@ void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof)
   in.ncorner = od.nlast + 0; in.nsurf = od.nlast + 1; in.nfull = od.nfullEnd + 0;
   in.ncorner_stride = 4; in.nsurf_stride = 4; in.nfull_stride = 2;
   in.pose = nullptr; in.pose_stride = 0;
-  mp_frame(b, in, st, prof);
+  mp_frame(b, in, st, prof, /*map_empty=*/true);
   // frame 2: cur (Last[1], fullEnd[1]) with the odometry transformSum
   in.corner = od.lastC + (size_t)od.P * od.capC;
   in.surf = od.lastS + (size_t)od.P * od.capS;

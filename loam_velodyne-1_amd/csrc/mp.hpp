@@ -101,7 +101,8 @@ inline int mp_batch_map_capacity(int cap) { return 2 * cap; }
 void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter);
 void mp_free(MpBuffers& b);
 void mp_reset(MpBuffers& b, hipStream_t st);
-void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof = nullptr);
+// map_empty: the store was just reset (no L-M can run: its launches are skipped)
+void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof = nullptr, bool map_empty = false);
 // imu_rp: the IMU (roll, pitch) transformUpdate blends in (nullptr = no IMU); *updated = whether
 // transformUpdate ran (the caller then commits its IMU queue pointer)
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
