@@ -277,6 +277,97 @@ LOAM_D void reg_bitonic_sort(uint64_t* k, int n) {
   else reg_bitonic_sort_n<NT, (EMAX < 16 ? EMAX : 16)>(k, n);
 }
 
+// ------------------------------------------------------------------ block radix sort (stable)
+// LSD radix sort of n <= NT*E (key, value) pairs held in LDS, 4-bit digits, over the low `nbits`
+// bits of the keys (the caller passes the bits its keys can differ in).  Blocked arrangement:
+// thread t ranks items [t*E, t*E+E) — digit counters packed in two 64-bit registers (8-bit fields),
+// one packed (16-bit pair) wave scan + one cross-wave scan per pass, scatter to the other buffer.
+// Stable, so equal keys keep their input order.  Returns 0 when the result is in (ka, va), 1 when
+// in (kb, vb).  sc: LDS scratch of (NT/64 + 1) * 8 words.  E <= 255, n < 65536.
+template <int NT, int E>
+LOAM_D int block_radix_sort_kv(uint32_t* ka, uint16_t* va, uint32_t* kb, uint16_t* vb, int n, int nbits,
+                               uint32_t* sc) {
+  constexpr int NW = NT / 64;
+  const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+  int cur = 0;
+  for (int shift = 0; shift < nbits; shift += 4) {
+    const uint32_t* ks = cur ? kb : ka;
+    const uint16_t* vs = cur ? vb : va;
+    uint32_t* kd = cur ? ka : kb;
+    uint16_t* vd = cur ? va : vb;
+    uint32_t k[E];
+    uint32_t meta[E];  // value | rank in thread << 16 | digit << 24 | valid << 28
+    uint64_t clo = 0, chi = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int g = tid * E + e;
+      k[e] = 0;
+      meta[e] = 0;
+      if (g < n) {
+        k[e] = ks[g];
+        const uint32_t d = (k[e] >> shift) & 15u;
+        const int sh = (int)(d & 7u) * 8;
+        const uint64_t c = d < 8 ? clo : chi;
+        meta[e] = (uint32_t)vs[g] | ((uint32_t)((c >> sh) & 255u) << 16) | (d << 24) | (1u << 28);
+        const uint64_t c2 = c + (1ull << sh);
+        if (d < 8) clo = c2; else chi = c2;
+      }
+    }
+    uint32_t p[8], inc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // counts of digits 2i, 2i+1 as 16-bit pairs
+      const uint64_t c = i < 4 ? clo : chi;
+      const int sh = (2 * i % 8) * 8;
+      p[i] = (uint32_t)((c >> sh) & 255u) | ((uint32_t)((c >> (sh + 8)) & 255u) << 16);
+      inc[i] = p[i];
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t t = (uint32_t)__shfl_up((int)inc[i], o, 64);
+        if (lane >= o) inc[i] += t;
+      }
+    if (lane == 63)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sc[w * 8 + i] = inc[i];
+    __syncthreads();
+    if (tid < 8) {
+      uint32_t run = 0;
+      for (int ww = 0; ww < NW; ++ww) {
+        const uint32_t t = sc[ww * 8 + tid];
+        sc[ww * 8 + tid] = run;
+        run += t;
+      }
+      sc[NW * 8 + tid] = run;
+    }
+    __syncthreads();
+    // digit bases (exclusive prefix of the 16 totals), folded into the thread's packed prefixes
+    uint32_t base = 0;
+    uint64_t q[4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t tot = sc[NW * 8 + i];
+      const uint32_t b0 = base, b1 = base + (tot & 0xffffu);
+      base = b1 + (tot >> 16);
+      const uint32_t ex = inc[i] - p[i] + sc[w * 8 + i] + (b0 | (b1 << 16));
+      if (i % 2 == 0) q[i / 2] = ex; else q[i / 2] |= (uint64_t)ex << 32;
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (meta[e] >> 28) {
+        const int d = (int)((meta[e] >> 24) & 15u), wd = d >> 2;
+        const uint64_t qq = wd == 0 ? q[0] : (wd == 1 ? q[1] : (wd == 2 ? q[2] : q[3]));
+        const int pos = (int)((qq >> ((d & 3) * 16)) & 0xffffu) + (int)((meta[e] >> 16) & 255u);
+        kd[pos] = k[e];
+        vd[pos] = (uint16_t)(meta[e] & 0xffffu);
+      }
+    __syncthreads();
+    cur ^= 1;
+  }
+  return cur;
+}
+
 LOAM_HD int next_pow2(int v) {
   int p = 1;
   while (p < v) p <<= 1;

@@ -422,6 +422,99 @@ __global__ __launch_bounds__(NT) void k_vg_fused(VgJob j) {
   }
 }
 
+// Fused segmented VoxelGrid with an LDS radix sort: one workgroup per segment of at most NT*E
+// points does bbox + parameters (as k_vg_params), the voxel keys (as k_vg_keys), a stable radix
+// sort of (voxel, position) pairs over the bits the keys can differ in (the order of the stable
+// hipCUB sort), and the ordered per-voxel means (as k_vg_reduce).  Larger segments are listed in
+// big_b / big_e for the multi-kernel path.
+template <int NT, int E>
+__global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
+  constexpr int N = NT * E;
+  __shared__ uint32_t ka[N], kb[N];
+  __shared__ uint16_t va[N], vb[N];
+  __shared__ uint32_t sc[(NT / 64 + 1) * 8];
+  __shared__ float fsc[16];
+  __shared__ int isc[24];
+  const int tid = threadIdx.x;
+  for (int s = blockIdx.x; s < j.nseg; s += gridDim.x) {
+    const int b0 = j.begin[s], b1 = j.end[s], n = b1 - b0;
+    if (n <= 0 || n > N) {
+      if (tid == 0) {
+        j.big_b[s] = n > 0 ? b0 : 0;
+        j.big_e[s] = n > 0 ? b1 : 0;
+        if (n <= 0) j.out_count[s] = 0;
+      }
+      continue;
+    }
+    if (tid == 0) { j.big_b[s] = 0; j.big_e[s] = 0; }
+    const float4* in = j.in + b0;
+    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+    for (int i = tid; i < n; i += NT) {
+      const float4 a = in[i];
+      mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
+      mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
+    }
+    for (int d = 0; d < 3; ++d) {
+      mn[d] = block_reduce<NT>(mn[d], fsc, [](float a, float c) { return fminf(a, c); });
+      mx[d] = block_reduce<NT>(mx[d], fsc, [](float a, float c) { return fmaxf(a, c); });
+    }
+    const float inv = 1.0f / j.leaf[s];
+    const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
+    const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
+    const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
+    if (dx * dy * dz > (int64_t)0x7fffffff) {  // "leaf size too small": output = input
+      for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
+      if (tid == 0) j.out_count[s] = n;
+      continue;
+    }
+    const int m0 = (int)floorf(mn[0] * inv), m1 = (int)floorf(mn[1] * inv), m2 = (int)floorf(mn[2] * inv);
+    const int divx = (int)floorf(mx[0] * inv) - m0 + 1, divy = (int)floorf(mx[1] * inv) - m1 + 1;
+    const uint32_t mul1 = (uint32_t)divx, mul2 = (uint32_t)(divx * divy);
+    uint32_t kmax = 0;
+    for (int i = tid; i < n; i += NT) {
+      const float4 a = in[i];
+      const int i0 = (int)(floorf(a.x * inv) - (float)m0);
+      const int i1 = (int)(floorf(a.y * inv) - (float)m1);
+      const int i2 = (int)(floorf(a.z * inv) - (float)m2);
+      const uint32_t key = (uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2;
+      ka[i] = key;
+      va[i] = (uint16_t)i;
+      kmax = key > kmax ? key : kmax;
+    }
+    kmax = (uint32_t)block_reduce<NT>((int)(kmax >> 1), (int*)isc, [](int a, int c) { return a > c ? a : c; });
+    const int nbits = kmax ? 33 - __clz((int)kmax) : (n > 1 ? 1 : 0);  // bits of the max key
+    const int cur = block_radix_sort_kv<NT, E>(ka, va, kb, vb, n, nbits, sc);
+    const uint32_t* ks = cur ? kb : ka;
+    const uint16_t* vs = cur ? vb : va;
+    int run = 0;
+    for (int base = 0; base < n; base += NT) {
+      const int t = base + tid;
+      const uint32_t k = t < n ? ks[t] : 0u;
+      const int head = (t < n && (t == 0 || ks[t - 1] != k)) ? 1 : 0;
+      int tot;
+      const int ex = block_excl_scan<NT>(head, isc, tot);
+      if (head) {
+        int e = t + 1;
+        while (e < n && ks[e] == k) ++e;
+        float sx = 0, sy = 0, sz = 0, si = 0;
+        for (int mm = t; mm < e; mm += 4) {  // four independent gathers in flight per step
+          float4 a[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) a[u] = in[vs[min(mm + u, e - 1)]];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (mm + u < e) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
+        }
+        const float cnt = (float)(e - t);
+        j.out[b0 + run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+      }
+      run += tot;
+    }
+    if (tid == 0) j.out_count[s] = run;
+    __syncthreads();  // the LDS arrays are reused by the next segment
+  }
+}
+
 template <int G>
 void vg_launch_params_keys(const VgJob& j, hipStream_t st) {
   const int grid = std::min((j.nseg + VgGroup<G>::NT / G - 1) / (VgGroup<G>::NT / G), 4096);
@@ -435,19 +528,24 @@ void vg_launch_reduce(const VgJob& j, hipStream_t st) {
 }
 
 // G = threads per segment: 64 for many mostly-empty segments, 256 / 1024 for few large ones
-// fcap: capacity (points per segment) of the fused kernel — 0 (multi-kernel path only), 2048,
-// 8192 or 16384 (256 x 8, 1024 x 8, 1024 x 16 keys); G: threads per segment of the multi-kernel
-// path (hipCUB segmented radix sort), which finishes the segments beyond fcap.  The fused kernel
-// pays off for a few instances (streaming: one launch instead of four, no global key arrays);
-// for large batches the radix sort's work efficiency wins over the bitonic network.
+// fcap: capacity (points per segment) of the fused LDS kernel — 0 (multi-kernel path only),
+// 2048 (256 threads x 8) or 12288 (1024 x 12); G: threads per segment of the multi-kernel path
+// (hipCUB segmented radix sort), which finishes the segments beyond fcap.  The fused kernel wins
+// for a few instances (streaming: one launch instead of four, no global key arrays); for large
+// batches hipCUB's multi-kernel path measured faster (both keep the stable (voxel, position) order).
 void vg_run(const VgJob& j0, void* tmp, size_t tmp_bytes, hipStream_t st, int G, int fcap) {
   if (j0.nseg == 0) return;
   const int grid = std::min(j0.nseg, 65536);
   VgJob j = j0;
   if (fcap > 0) {
+#ifdef LOAM_EXP_BITONICVG
     if (fcap <= 2048) hipLaunchKernelGGL((k_vg_fused<256, 8>), dim3(grid), dim3(256), 0, st, j0);
     else if (fcap <= 8192) hipLaunchKernelGGL((k_vg_fused<1024, 8>), dim3(grid), dim3(1024), 0, st, j0);
     else hipLaunchKernelGGL((k_vg_fused<1024, 16>), dim3(grid), dim3(1024), 0, st, j0);
+#else
+    if (fcap <= 2048) hipLaunchKernelGGL((k_vg_radix<256, 8>), dim3(grid), dim3(256), 0, st, j0);
+    else hipLaunchKernelGGL((k_vg_radix<1024, 12>), dim3(grid), dim3(1024), 0, st, j0);
+#endif
     j.begin = j0.big_b;  // the multi-kernel path finishes what the fused kernel could not hold
     j.end = j0.big_e;
     j.keep_counts = 1;
@@ -1268,7 +1366,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   js.in = b.stack2; js.out = b.stack; js.begin = b.sseg_b; js.end = b.sseg_e; js.leaf = b.sseg_leaf;
   js.out_count = b.sseg_cnt; js.params = b.vg_params; js.keys = b.vg_k; js.keys_alt = b.vg_k2;
   js.vals = b.vg_v; js.vals_alt = b.vg_v2; js.big_b = b.vg_bb; js.big_e = b.vg_be; js.nseg = 2 * P; js.total = P * b.cap_stack;
-  vg_run(js, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 1024 : 256, P <= 4 ? 16384 : 0);  // two large segments per instance
+  vg_run(js, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 1024 : 256, P <= 4 ? 12288 : 0);  // two large segments per instance
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);
   mark("k_mp_gather");
@@ -1309,7 +1407,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   jv.in = b.vin; jv.out = b.vout; jv.begin = b.vseg_b; jv.end = b.vseg_e; jv.leaf = b.vseg_leaf;
   jv.out_count = b.vseg_cnt; jv.params = b.vg_params; jv.keys = b.vg_k; jv.keys_alt = b.vg_k2;
   jv.vals = b.vg_v; jv.vals_alt = b.vg_v2; jv.big_b = b.vg_bb; jv.big_e = b.vg_be; jv.nseg = 2 * kMaxValid * P; jv.total = P * b.map_cap;
-  vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 256 : 64, P <= 4 ? 16384 : 0);    // 2 x 125 cube segments per instance
+  vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 256 : 64, P <= 4 ? 12288 : 0);    // 2 x 125 cube segments per instance
   mark("vg_cubes");
   hipLaunchKernelGGL(k_mp_compact_table, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);
@@ -1444,7 +1542,7 @@ int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::s
   j.in = b.vin; j.out = b.vout; j.begin = b.vseg_b; j.end = b.vseg_e; j.leaf = b.vseg_leaf;
   j.out_count = b.vseg_cnt; j.params = b.vg_params; j.keys = b.vg_k; j.keys_alt = b.vg_k2;
   j.vals = b.vg_v; j.vals_alt = b.vg_v2; j.big_b = b.vg_bb; j.big_e = b.vg_be; j.nseg = 1; j.total = b.P * b.map_cap;
-  vg_run(j, b.cub_tmp, b.cub_bytes, st, 1024, 16384);
+  vg_run(j, b.cub_tmp, b.cub_bytes, st, 1024, 12288);
   int cnt = 0;
   (void)hipMemcpyAsync(&cnt, b.vseg_cnt, sizeof(int), hipMemcpyDeviceToHost, st);
   const hipError_t he = hipStreamSynchronize(st);
