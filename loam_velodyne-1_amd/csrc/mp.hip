@@ -334,94 +334,6 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
   }
 }
 
-// Fused segmented VoxelGrid for segments of at most NT*E points: one workgroup per segment does
-// bbox + parameters (as k_vg_params), keys (as k_vg_keys), an LDS register-bitonic sort of
-// (voxel << 32 | position) — the order of the stable radix sort by voxel with positions as values —
-// and the ordered per-voxel means (as k_vg_reduce), without the global key / value arrays and
-// with one launch.  Larger segments are listed in big_b / big_e for the multi-kernel path.
-template <int NT, int E>
-__global__ __launch_bounds__(NT) void k_vg_fused(VgJob j) {
-  __shared__ uint64_t keys[NT * E];
-  __shared__ float fsc[16];
-  __shared__ int isc[24];
-  const int tid = threadIdx.x;
-  for (int s = blockIdx.x; s < j.nseg; s += gridDim.x) {
-    const int b0 = j.begin[s], b1 = j.end[s], n = b1 - b0;
-    if (n <= 0 || n > NT * E) {
-      if (tid == 0) {
-        j.big_b[s] = n > 0 ? b0 : 0;
-        j.big_e[s] = n > 0 ? b1 : 0;
-        if (n <= 0) j.out_count[s] = 0;
-      }
-      continue;
-    }
-    if (tid == 0) { j.big_b[s] = 0; j.big_e[s] = 0; }
-    const float4* in = j.in + b0;
-    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
-    for (int i = tid; i < n; i += NT) {
-      const float4 a = in[i];
-      mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
-      mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
-    }
-    for (int d = 0; d < 3; ++d) {
-      mn[d] = block_reduce<NT>(mn[d], fsc, [](float a, float c) { return fminf(a, c); });
-      mx[d] = block_reduce<NT>(mx[d], fsc, [](float a, float c) { return fmaxf(a, c); });
-    }
-    const float inv = 1.0f / j.leaf[s];
-    const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
-    const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
-    const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
-    if (dx * dy * dz > (int64_t)0x7fffffff) {  // "leaf size too small": output = input
-      for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
-      if (tid == 0) j.out_count[s] = n;
-      continue;
-    }
-    const int m0 = (int)floorf(mn[0] * inv), m1 = (int)floorf(mn[1] * inv), m2 = (int)floorf(mn[2] * inv);
-    const int divx = (int)floorf(mx[0] * inv) - m0 + 1, divy = (int)floorf(mx[1] * inv) - m1 + 1;
-    const uint32_t mul1 = (uint32_t)divx, mul2 = (uint32_t)(divx * divy);
-    const int P2 = next_pow2(n);
-    for (int i = tid; i < P2; i += NT) {
-      uint64_t key = ~0ull;
-      if (i < n) {
-        const float4 a = in[i];
-        const int i0 = (int)(floorf(a.x * inv) - (float)m0);
-        const int i1 = (int)(floorf(a.y * inv) - (float)m1);
-        const int i2 = (int)(floorf(a.z * inv) - (float)m2);
-        key = ((uint64_t)((uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2) << 32) | (uint32_t)i;
-      }
-      keys[i] = key;
-    }
-    __syncthreads();
-    reg_bitonic_sort<NT, E>(keys, P2);
-    int run = 0;
-    for (int base = 0; base < n; base += NT) {
-      const int t = base + tid;
-      const uint32_t k = t < n ? (uint32_t)(keys[t] >> 32) : 0u;
-      const int head = (t < n && (t == 0 || (uint32_t)(keys[t - 1] >> 32) != k)) ? 1 : 0;
-      int tot;
-      const int ex = block_excl_scan<NT>(head, isc, tot);
-      if (head) {
-        int e = t + 1;
-        while (e < n && (uint32_t)(keys[e] >> 32) == k) ++e;
-        float sx = 0, sy = 0, sz = 0, si = 0;
-        for (int mm = t; mm < e; mm += 4) {  // four independent gathers in flight per step
-          float4 a[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) a[u] = in[(uint32_t)keys[min(mm + u, e - 1)]];
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (mm + u < e) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
-        }
-        const float cnt = (float)(e - t);
-        j.out[b0 + run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
-      }
-      run += tot;
-    }
-    if (tid == 0) j.out_count[s] = run;
-    __syncthreads();  // keys are reused by the next segment
-  }
-}
-
 // Fused segmented VoxelGrid with an LDS radix sort: one workgroup per segment of at most NT*E
 // points does bbox + parameters (as k_vg_params), the voxel keys (as k_vg_keys), a stable radix
 // sort of (voxel, position) pairs over the bits the keys can differ in (the order of the stable
@@ -538,14 +450,8 @@ void vg_run(const VgJob& j0, void* tmp, size_t tmp_bytes, hipStream_t st, int G,
   const int grid = std::min(j0.nseg, 65536);
   VgJob j = j0;
   if (fcap > 0) {
-#ifdef LOAM_EXP_BITONICVG
-    if (fcap <= 2048) hipLaunchKernelGGL((k_vg_fused<256, 8>), dim3(grid), dim3(256), 0, st, j0);
-    else if (fcap <= 8192) hipLaunchKernelGGL((k_vg_fused<1024, 8>), dim3(grid), dim3(1024), 0, st, j0);
-    else hipLaunchKernelGGL((k_vg_fused<1024, 16>), dim3(grid), dim3(1024), 0, st, j0);
-#else
     if (fcap <= 2048) hipLaunchKernelGGL((k_vg_radix<256, 8>), dim3(grid), dim3(256), 0, st, j0);
     else hipLaunchKernelGGL((k_vg_radix<1024, 12>), dim3(grid), dim3(1024), 0, st, j0);
-#endif
     j.begin = j0.big_b;  // the multi-kernel path finishes what the fused kernel could not hold
     j.end = j0.big_e;
     j.keep_counts = 1;
