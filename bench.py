@@ -35,6 +35,10 @@ def kernel_bytes(st):
         "k_sr_features": 16 * st["n_ring"],
         "k_sr_select": 16 * st["n_ring"] + feats,
         "k_od_solve": st["bytes_od"],
+        # per iteration: every stored row's coefficient (16 B) + accept flag (1 B) read back (Q12:
+        # all rows so far re-evaluated at the current transform), the query point read (16 B) and
+        # its coefficient + flag written (17 B)
+        "k_od_rows": 17 * st["od_row_evals"] + 33 * st["od_query_iters"],
         # per iteration: stack point 16 B (k_mp_nn), 5 neighbours 80 B read and the row (16 B point +
         # 16 B coeff) written (k_mp_fit)
         "k_mp_nn": 16 * st["mp_stack_iters"],
@@ -42,6 +46,40 @@ def kernel_bytes(st):
         # rows read back for JtJ
         "k_mp_iter": 32 * st["mp_rows_sum"],
     }
+
+
+def stream_leg(loam, sg, n_sweeps, n_cpu):
+    """Config 3 (streaming, seed 1): scan registration -> odometry -> mapping on every published
+    frame, one sweep at a time on one GPU context, next to the CPU oracle on the first sweeps."""
+    sweeps = sg.stream_sweeps(n_sweeps, 1)
+
+    def run(impl, sw):
+        poses, n, t = [], 0, 0.0
+        for k, s in enumerate(sw):
+            a = time.perf_counter()
+            rc, f = impl.scan_registration(s, stamp=0.1 * k)
+            if rc == 0:
+                n += 1
+                pub, pose, cl, sl, full = impl.odometry(f, stamp=0.1 * k)
+                if pub == 7:
+                    poses.append(impl.mapping(pose, cl, sl, full)[0])
+            t += time.perf_counter() - a
+        return np.array(poses), n, t
+
+    warm = loam.Engine(loam.default_config(system_delay=1))
+    run(warm, sweeps[:6])
+    pg, ng, tg = run(loam.Engine(loam.default_config()), sweeps)
+    out = {"config": "config3: VLP-16 stream (seed 1), systemDelay 20, mapping every 2nd frame",
+           "sweeps_processed": ng, "scans_per_s": ng / tg, "ms_per_sweep": 1e3 * tg / max(ng, 1)}
+    if n_cpu > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_ctypes as oc
+        po, no, tc = run(oc.Oracle(oc.default_config()), sweeps[:n_cpu])
+        k = min(len(po), len(pg))
+        out["cpu_oracle"] = {"sweeps_processed": no, "scans_per_s": no / tc, "cores": 1, "kind": "port"}
+        out["speedup_vs_cpu"] = out["scans_per_s"] / out["cpu_oracle"]["scans_per_s"]
+        out["max_abs_err_mapping"] = float(np.abs(pg[:k] - po[:k]).max()) if k else None
+    return out
 
 
 def main():
@@ -52,6 +90,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1024, help="problems per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--profile-steps", type=int, default=3)
+    ap.add_argument("--stream-sweeps", type=int, default=120, help="config-3 streaming leg (0: skip)")
+    ap.add_argument("--stream-cpu-sweeps", type=int, default=40)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -178,6 +218,19 @@ def main():
         parity = {"problems_checked": n_done, "max_abs_err_odometry": err_od, "max_abs_err_mapping": err_mp}
 
     stage_ms = {k: round(v[0] / max(args.profile_steps, 1), 4) for k, v in sorted(ktimes.items())}
+    # the same achieved-vs-peak figure for every kernel with an algorithmic byte count
+    roof_all = {}
+    for k, nbytes in kb.items():
+        if k in ktimes and ktimes[k][0] > 0:
+            gbs = nbytes / (ktimes[k][0] / max(args.profile_steps, 1) * 1e-3) / 1e9  # bytes per step / s per step
+            roof_all[k] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                           "ms_per_step": round(ktimes[k][0] / max(args.profile_steps, 1), 4)}
+
+    # single-stream latency path (BASELINE configs 2/3): one context fed sweep by sweep through the
+    # node-level C-ABI with host buffers in and out, as the ROS nodes would call it (not the metric)
+    stream = None
+    if world == 1 and args.stream_sweeps > 0:
+        stream = stream_leg(loam, sg, args.stream_sweeps, args.stream_cpu_sweeps)
     out = {
         "metric": METRIC,
         "value": value,
@@ -195,9 +248,11 @@ def main():
                    "problems_per_gpu": B, "global_batch": world * B, "points_per_sweep": 28800,
                    "parallelism": f"shard{world}"},
         "roofline": roof,
+        "roofline_kernels": roof_all,
         "cpu_baseline": cpu,
         "parity": parity,
         "kernel_ms_per_step": stage_ms,
+        "single_stream": stream,
         "host_upload": {"ms": upload_s * 1e3, "pcie_inclusive_value": B / (upload_s + ms_per_step * 1e-3),
                         "note": "rank 0; pageable host sweeps packed and copied per sweep; not the metric"},
         "workload_stats": {"od_iters_mean": st["od_iters"] / B, "mp_iters_mean": st["mp_iters"] / B,

@@ -94,6 +94,8 @@ typedef struct {
   uint64_t mp_iters, mp_rows_sum, mp_stack, mp_map_points, mp_map_valid_points;
   uint64_t mp_stack_iters;                      /* sum over problems of iterations x stack size */
   uint64_t mp_fits;                             /* line / plane fits computed (the rest reused: same ordered 5-NN) */
+  uint64_t od_query_iters;                      /* sum over problems of L-M iterations x queries (sharp + flat) */
+  uint64_t od_row_evals;                        /* Jacobian rows evaluated: sum of queries x it(it+1)/2 (Q12) */
   uint64_t bytes_sr, bytes_od, bytes_mp;        /* algorithmic bytes, SURVEY.md §8(d) */
   double ms_sr, ms_od, ms_mp;                   /* device time per stage (HIP events) */
 } loam_stats;

@@ -69,7 +69,7 @@ STAT_U64 = ("n_raw", "n_ring", "n_sharp", "n_less_sharp", "n_flat", "n_less_flat
             "od_iters", "od_assoc_rounds", "od_rows_sum", "od_corner_last", "od_surf_last", "od_queries",
             "od_assoc_points",
             "mp_iters", "mp_rows_sum", "mp_stack", "mp_map_points", "mp_map_valid_points", "mp_stack_iters",
-            "mp_fits",
+            "mp_fits", "od_query_iters", "od_row_evals",
             "bytes_sr", "bytes_od", "bytes_mp")
 
 

@@ -406,6 +406,11 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
   x->stats.od_assoc_rounds = ist[kIsAssoc];
   x->stats.od_rows_sum = (uint64_t)ist[kIsRows];
   x->stats.od_queries = ist[kIsQueries];
+  {
+    const uint64_t nq = ist[kIsAssoc] ? (uint64_t)(ist[kIsQueries] / ist[kIsAssoc]) : 0, it = (uint64_t)ist[kIsIters];
+    x->stats.od_query_iters = nq * it;
+    x->stats.od_row_evals = nq * it * (it + 1) / 2;
+  }
   x->stats.od_corner_last = nl[cur * 2 + 0];
   x->stats.od_surf_last = nl[cur * 2 + 1];
   x->stats.od_assoc_points = (uint64_t)ist[kIsAssoc] * (nl[cur * 2 + 0] + nl[cur * 2 + 1]);
@@ -588,6 +593,9 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
     s.od_assoc_rounds += q[kIsAssoc];
     s.od_rows_sum += (uint64_t)q[kIsRows];
     s.od_queries += q[kIsQueries];
+    const uint64_t nq = q[kIsAssoc] ? (uint64_t)(q[kIsQueries] / q[kIsAssoc]) : 0, it = (uint64_t)q[kIsIters];
+    s.od_query_iters += nq * it;
+    s.od_row_evals += nq * it * (it + 1) / 2;
     s.od_corner_last += nl[i * 4 + 0];
     s.od_surf_last += nl[i * 4 + 1];
     s.od_assoc_points += (uint64_t)q[kIsAssoc] * (nl[i * 4 + 0] + nl[i * 4 + 1]);

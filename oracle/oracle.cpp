@@ -1464,6 +1464,11 @@ int oracle_odometry(void* h, double stamp, const loam_features* in, loam_pose6* 
   od_body(o->cfg, o->od, oi, oo);
   o->stats.od_iters = o->od.iters - it0; o->stats.od_assoc_rounds = o->od.assoc - as0;
   o->stats.od_rows_sum = o->od.rows_sum - rs0; o->stats.od_queries = o->od.queries - q0;
+  {
+    const uint64_t as = o->stats.od_assoc_rounds, it = o->stats.od_iters, nq = as ? o->stats.od_queries / as : 0;
+    o->stats.od_query_iters = nq * it;
+    o->stats.od_row_evals = nq * it * (it + 1) / 2;
+  }
   *published = oo.published;
   int e = 0;
   if (oo.published & LOAM_PUB_POSE) from6(oo.sum, sum_out);
@@ -1597,6 +1602,11 @@ int oracle_problem(const loam_config* cfg, loam_cloud_in prev, loam_cloud_in cur
     st->od_iters = od.iters; st->od_assoc_rounds = od.assoc; st->od_rows_sum = od.rows_sum;
     st->od_corner_last = prevCorner.size(); st->od_surf_last = prevSurf.size();
     st->od_queries = od.queries;
+    {
+      const uint64_t nq = od.assoc ? (uint64_t)od.queries / od.assoc : 0, it = od.iters;
+      st->od_query_iters = nq * it;
+      st->od_row_evals = nq * it * (it + 1) / 2;
+    }
     st->mp_iters = mp.iters; st->mp_rows_sum = mp.rows_sum; st->mp_stack = mp.stack;
     st->mp_map_points = mp.map_points; st->mp_map_valid_points = mp.valid_points;
   }

@@ -51,7 +51,7 @@ class Stats(ctypes.Structure):
         "od_iters", "od_assoc_rounds", "od_rows_sum", "od_corner_last", "od_surf_last", "od_queries",
         "od_assoc_points",
         "mp_iters", "mp_rows_sum", "mp_stack", "mp_map_points", "mp_map_valid_points", "mp_stack_iters",
-        "mp_fits",
+        "mp_fits", "od_query_iters", "od_row_evals",
         "bytes_sr", "bytes_od", "bytes_mp")] + [(n, ctypes.c_double) for n in ("ms_sr", "ms_od", "ms_mp")]
 
     def as_dict(self):
