@@ -149,6 +149,27 @@ LOAM_D T block_reduce(T v, T* scratch, Op op) {
   return r;
 }
 
+// In-place butterfly reduce-scatter of 28 (padded to 32) per-lane doubles over the wave: after
+// the call, a[0] of lanes 2v and 2v+1 holds the wave sum of value v.  Step s exchanges with lane
+// ^ (32 >> s) and keeps the half of the remaining values selected by that lane bit.
+LOAM_D void wave_reduce_scatter_28(double (&a)[28]) {
+  const int lane = lane_id();
+  double v[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) v[k] = k < 28 ? a[k] : 0.0;
+#pragma unroll
+  for (int h = 16; h >= 1; h >>= 1) {  // 32 -> 16 -> ... -> 1 values, partner lane ^ (2h)
+    const bool upper = (lane & (2 * h)) != 0;
+#pragma unroll
+    for (int k = 0; k < h; ++k) {
+      const double send = upper ? v[k] : v[h + k];
+      const double keep = upper ? v[h + k] : v[k];
+      v[k] = keep + __shfl_xor(send, 2 * h, 64);
+    }
+  }
+  a[0] = v[0] + __shfl_xor(v[0], 1, 64);
+}
+
 // ------------------------------------------------------------------ LDS bitonic sort (ascending)
 // sorts n64 = power of two 64-bit keys in LDS with the whole block; pad with ~0ull.
 template <int NT>

@@ -874,12 +874,8 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
     for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
     acc[27] += 1.0;
   }
-#pragma unroll
-  for (int k = 0; k < 28; ++k) {
-    double v = acc[k];
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) sh.red[w][k] = v;
-  }
+  wave_reduce_scatter_28(acc);  // lanes 2v, 2v+1: the wave sum of value v
+  if ((lane & 1) == 0 && (lane >> 1) < 28) sh.red[w][lane >> 1] = acc[0];
   __syncthreads();
   if (tid == 0) {
     double tot[28];
