@@ -47,7 +47,8 @@ LOAM_D loampose::Imu load_imu(const float* st) {
 // One workgroup per cloud: T = pow2 >= count >> shift (clamped to [64, tmax]) buckets — a 1 m
 // cell holds several points, so even two points per bucket (shift 1) leaves distinct neighbouring
 // cells rarely sharing a bucket — CSR start[T+1], points re-ordered by bucket with their source index in .w
-// (bit pattern).  Bucket counters live in LDS up to kHashLds buckets, in global memory beyond.
+// (bit pattern; for the odometry clouds index | ring << 24).  Bucket counters live in LDS up to
+// kHashLds buckets, in global memory beyond.
 constexpr int kHashLds = 8192;
 
 // counting sort of the cloud's points by bucket; fill = LDS (LDS true) or this cloud's global
@@ -91,7 +92,10 @@ LOAM_D void hash_sort(const HashJob& j, const float4* pts, int n, int T, int* st
     const float4 a = pts[i];
     uint32_t h = cell_hash(cell_of(a.x, j.inv_h), cell_of(a.y, j.inv_h), cell_of(a.z, j.inv_h)) & (T - 1);
     int pos = atomicAdd(&fill[h], 1);
-    out[pos] = make_float4(a.x, a.y, a.z, __int_as_float(i));
+    // odometry clouds (chunk boxes built): the ring rides in the top byte, so the nearest
+    // neighbour's ring needs no extra load (wave_hash_nn)
+    const int tag = j.chunks ? (i | ((int)a.w << 24)) : i;
+    out[pos] = make_float4(a.x, a.y, a.z, __int_as_float(tag));
   }
 }
 
@@ -139,7 +143,8 @@ LOAM_D float box_d2(const float4& lo, const float4& hi, const float4& s) {
 }
 
 // exact nearest neighbour of q among the hashed cloud (wave-cooperative), as far as it matters:
-// returns the packed (float distance bits << 32 | index) minimum, or ~0 when no point lies
+// returns the packed (float distance bits << 32 | index << 8 | ring) minimum (ties on the index,
+// as before: the ring is a function of the point), or ~0 when no point lies
 // closer than 5 m (the callers reject a nearest neighbour at >= 25 m², :481, :594).  First the
 // 27 cells around q (cells whose box lies >= h away skipped); if the best is >= h, the chunk
 // boxes of the whole cloud closer than 5 m.  `cells` = per-wave LDS scratch of 64 ints.
@@ -172,7 +177,8 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
       if (cells[k + step] <= t) k += step;
     const float4 a = hp[cells[32 + k] + (t - cells[k])];
     const float d = sqdist(a.x, a.y, a.z, q.x, q.y, q.z);
-    const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)__float_as_int(a.w);
+    const uint32_t tag = (uint32_t)__float_as_int(a.w);  // index | ring << 24
+    const uint64_t key = ((uint64_t)fkey(d) << 32) | ((tag & 0xffffffu) << 8) | (tag >> 24);
     best = key < best ? key : best;
   }
   best = wave_min_u64(best);
@@ -192,7 +198,7 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
       if (t < n) {
         const float4 a = cloud[t];
         const float d = sqdist(a.x, a.y, a.z, q.x, q.y, q.z);
-        const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)t;
+        const uint64_t key = ((uint64_t)fkey(d) << 32) | ((uint32_t)t << 8) | (uint32_t)(int)a.w;
         best = key < best ? key : best;
       }
     }
@@ -280,9 +286,8 @@ LOAM_D void wave_assoc_corner(const float4* CL, const float4* ch, int fwd_end, u
   if (nn == ~0ull) return;
   const float d0 = __uint_as_float((uint32_t)(nn >> 32));
   if (!(D(d0) < 25)) return;
-  const int c = (int)(uint32_t)nn;
+  const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u);
   ind1 = c;
-  const int scan = (int)CL[c].w;
   uint64_t best = ~0ull;
   wave_window(CL, ch, c, fwd_end, +1, scan, sel, [&](int j, int r, float d) {
     if (r > scan) {
@@ -311,9 +316,8 @@ LOAM_D void wave_assoc_surf(const float4* SL, const float4* ch, int fwd_end, uin
   if (nn == ~0ull) return;
   const float d0 = __uint_as_float((uint32_t)(nn >> 32));
   if (!(D(d0) < 25)) return;
-  const int c = (int)(uint32_t)nn;
+  const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u);
   ind1 = c;
-  const int scan = (int)SL[c].w;
   uint64_t best2 = ~0ull, best3 = ~0ull;
   wave_window(SL, ch, c, fwd_end, +1, scan, sel, [&](int j, int r, float d) {
     const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)(j - c - 1);
@@ -384,7 +388,9 @@ __global__ __launch_bounds__(kOdThreads) void k_od_sel(OdBuffers b, FeatView f) 
 
 // association (:472-527, :587-650), one wave per query: exact NN through the hash, then the
 // ring-window scans.
-__global__ __launch_bounds__(kOdThreads) void k_od_assoc(OdBuffers b, FeatView f, int last_buf) {
+// 8 waves per SIMD (<= 64 VGPRs, <= 100 SGPRs; 7 by default): the association is bound by its
+// dependent chain per query, so occupancy is its throughput (measured 3.8 -> 3.2 ms per step)
+__global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_od_assoc(OdBuffers b, FeatView f, int last_buf) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, lane = lane_id(), w = threadIdx.x >> 6;
   const int* ist = b.istate + (size_t)p * kOdStateInts;
