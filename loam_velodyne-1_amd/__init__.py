@@ -85,7 +85,10 @@ EXPORTS = ("loam_config_default", "loam_create", "loam_destroy", "loam_last_erro
            "loam_scan_registration", "loam_odometry", "loam_mapping", "loam_mapping_surround",
            "loam_maintenance",
            "loam_batch_upload", "loam_batch_run", "loam_batch_sync", "loam_batch_download", "loam_get_stats",
-           "loam_set_profiling", "loam_get_kernel_times")
+           "loam_set_profiling", "loam_get_kernel_times",
+           # include/loam/loam_bag.h: recorded-sweep ingest (rosbag v2, PointCloud2, Imu)
+           "loam_bag_open", "loam_bag_close", "loam_bag_next", "loam_pc2_parse", "loam_pc2_cloud",
+           "loam_imu_parse")
 
 
 def lib():

@@ -155,6 +155,10 @@ void count_bytes(loam_stats& s) {
 
 }  // namespace
 
+namespace loam {
+void set_last_error(const std::string& msg) { g_err = msg; }
+}  // namespace loam
+
 extern "C" {
 
 const char* loam_last_error(void) { return g_err.c_str(); }

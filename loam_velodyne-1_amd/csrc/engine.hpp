@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "../../include/loam/loam.h"
 #include "imu.hpp"
 #include "prof.hpp"
@@ -73,6 +75,9 @@ struct SrParams {
   loamimu::SrQueue* imu = nullptr;  // device IMU queue of sweep 0 (streaming), nullptr = no IMU
   double time_scan = 0.0;           // timeScanCur: the sweep's stamp
 };
+
+// the thread-local message loam_last_error() returns (engine.cpp)
+void set_last_error(const std::string& msg);
 
 void sr_alloc(SrBuffers& b, int S, int cap, int R);
 void sr_free(SrBuffers& b);

@@ -1,0 +1,127 @@
+"""Recorded-sweep replay through the C-ABI (include/loam/loam_bag.h): reads a rosbag v2.0 file with
+libloam_hip.so's reader, hands /velodyne_points (sensor_msgs/PointCloud2) and /imu/data
+(sensor_msgs/Imu) to the node-level entry points in file order — what `rosbag play` + the
+reference's four nodes do (src/scanRegistration.cpp:211-226, :638-660; laserOdometry /
+laserMapping loop bodies) — and collects the published poses.
+
+    from loam_velodyne-1_amd import rosbag   (importlib: the package name has a dash)
+    for m in rosbag.Bag(path): ...           # (topic, type, stamp, bytes)
+    out = rosbag.replay(path, engine)        # trajectory of /laser_odom_to_init and /aft_mapped_to_init
+"""
+import ctypes
+
+import numpy as np
+
+from . import CloudIn, LOAM_OK, _check, lib
+
+LOAM_BAG_END = 1
+
+
+class BagMsg(ctypes.Structure):
+    _fields_ = [("topic", ctypes.c_char_p), ("type", ctypes.c_char_p), ("stamp", ctypes.c_double),
+                ("data", ctypes.c_void_p), ("size", ctypes.c_uint32)]
+
+
+class Pc2(ctypes.Structure):
+    _fields_ = [("stamp", ctypes.c_double), ("width", ctypes.c_uint32), ("height", ctypes.c_uint32),
+                ("point_step", ctypes.c_uint32), ("row_step", ctypes.c_uint32),
+                ("off_x", ctypes.c_int32), ("off_y", ctypes.c_int32), ("off_z", ctypes.c_int32),
+                ("off_intensity", ctypes.c_int32), ("off_ring", ctypes.c_int32),
+                ("is_bigendian", ctypes.c_uint8), ("is_dense", ctypes.c_uint8),
+                ("data", ctypes.c_void_p), ("data_size", ctypes.c_uint32)]
+
+
+def _bag_lib():
+    L = lib()
+    if not getattr(L, "_bag_ready", False):
+        P, PP = ctypes.POINTER, ctypes.c_void_p
+        L.loam_bag_open.argtypes = [P(PP), ctypes.c_char_p]
+        L.loam_bag_close.argtypes = [PP]
+        L.loam_bag_next.argtypes = [PP, P(BagMsg)]
+        L.loam_pc2_parse.argtypes = [ctypes.c_void_p, ctypes.c_uint32, P(Pc2)]
+        L.loam_pc2_cloud.argtypes = [P(Pc2), ctypes.c_void_p, ctypes.c_uint32, P(CloudIn)]
+        L.loam_imu_parse.argtypes = [ctypes.c_void_p, ctypes.c_uint32, P(ctypes.c_double), P(ctypes.c_double),
+                                     P(ctypes.c_double)]
+        L._bag_ready = True
+    return L
+
+
+class Bag:
+    """Iterates (topic, type, stamp, payload bytes) over the message records, in file order."""
+
+    def __init__(self, path):
+        self.h = ctypes.c_void_p()
+        _check(_bag_lib().loam_bag_open(ctypes.byref(self.h), str(path).encode()))
+
+    def close(self):
+        if self.h:
+            _bag_lib().loam_bag_close(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+    def __iter__(self):
+        m = BagMsg()
+        while True:
+            rc = _bag_lib().loam_bag_next(self.h, ctypes.byref(m))
+            if rc == LOAM_BAG_END:
+                return
+            _check(rc)
+            yield m.topic.decode(), m.type.decode(), m.stamp, ctypes.string_at(m.data, m.size)
+
+
+def parse_pc2(payload):
+    """sensor_msgs/PointCloud2 -> (header stamp, (n, 4) float32 x, y, z, intensity-or-0, Pc2 view)"""
+    buf = ctypes.create_string_buffer(payload, len(payload))
+    pc = Pc2()
+    _check(_bag_lib().loam_pc2_parse(buf, len(payload), ctypes.byref(pc)))
+    n = pc.width * pc.height
+    scratch = np.zeros((max(n, 1), 4), np.float32)
+    ci = CloudIn()
+    _check(_bag_lib().loam_pc2_cloud(ctypes.byref(pc), scratch.ctypes.data, n, ctypes.byref(ci)))
+    if ci.data == scratch.ctypes.data:  # packed copy
+        pts = scratch[:n].copy()
+    else:  # zero-copy view of the message's records: read x, y, z (+ intensity) by stride
+        raw = np.frombuffer(ctypes.string_at(ci.data, n * ci.stride_bytes), np.uint8).reshape(n, ci.stride_bytes)
+        pts = np.zeros((n, 4), np.float32)
+        pts[:, :3] = raw[:, :12].copy().view(np.float32).reshape(n, 3)
+        if pc.off_intensity >= 0:
+            o = pc.off_intensity
+            pts[:, 3] = raw[:, o:o + 4].copy().view(np.float32).reshape(n)
+    return pc.stamp, pts, pc
+
+
+def parse_imu(payload):
+    """sensor_msgs/Imu -> (header stamp, quaternion x, y, z, w, linear acceleration)"""
+    buf = ctypes.create_string_buffer(payload, len(payload))
+    t = ctypes.c_double()
+    q = (ctypes.c_double * 4)()
+    a = (ctypes.c_double * 3)()
+    _check(_bag_lib().loam_imu_parse(buf, len(payload), ctypes.byref(t), q, a))
+    return t.value, np.array(q[:]), np.array(a[:])
+
+
+def replay(path, engine, cloud_topic="/velodyne_points", imu_topic="/imu/data", max_sweeps=None):
+    """Feeds a bag through the node path of one engine context: /imu/data -> loam_imu, every cloud
+    -> scan registration -> odometry -> mapping on the frames odometry publishes (Q20).  Returns
+    dict(odometry=[(stamp, pose6)], mapping=[(stamp, aft pose6)], sweeps=int)."""
+    odo, mapped, n = [], [], 0
+    for topic, _type, _t, payload in Bag(path):
+        if topic == imu_topic:
+            stamp, q, a = parse_imu(payload)
+            engine.imu(stamp, q, a)
+        elif topic == cloud_topic:
+            stamp, pts, _pc = parse_pc2(payload)
+            n += 1
+            rc, f = engine.scan_registration(pts, stamp=stamp)
+            if rc != LOAM_OK:
+                continue  # inside systemDelay (Q1)
+            pub, pose, cl, sl, full = engine.odometry(f, stamp=stamp)
+            if pub & 1:
+                odo.append((stamp, pose))
+            if pub == 7:
+                mapped.append((stamp, engine.mapping(pose, cl, sl, full, stamp=stamp)[0]))
+            if max_sweeps and n >= max_sweeps:
+                break
+    return {"odometry": odo, "mapping": mapped, "sweeps": n}

@@ -1,5 +1,5 @@
 """C-ABI boundary checks that need no GPU: the library loads, exports every function declared in
-include/loam/loam.h, reports the reference defaults, refuses to run without a GPU (no CPU
+include/loam/loam.h and loam_bag.h, reports the reference defaults, refuses to run without a GPU (no CPU
 fallback), and its host-side pose algebra (transformMaintenance) matches the oracle bit for bit."""
 import ctypes
 import os
@@ -12,9 +12,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def header_functions():
-    txt = open(os.path.join(ROOT, "include", "loam", "loam.h")).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(loam_[a-z_0-9]+)\s*\(", txt)))
+    names = set()
+    for h in ("loam.h", "loam_bag.h"):
+        txt = open(os.path.join(ROOT, "include", "loam", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        names |= set(re.findall(r"\b(loam_[a-z_0-9]+)\s*\(", txt))
+    return sorted(names)
 
 
 def test_exports_every_declared_symbol(loam):
