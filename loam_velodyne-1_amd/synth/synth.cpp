@@ -14,6 +14,7 @@
 // identical wherever glibc's libm is identical (this image, here and on the GPU box).
 #include "synth.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -87,12 +88,19 @@ void build_indoor(Scene& s, uint64_t seed) {
   const double py[8] = {-9, -9, 9, 9, 0.5, -0.5, 1, -1};
   for (int i = 0; i < 8; ++i)
     add_box(s, px[i] - 0.2, py[i] - 0.2, g, px[i] + 0.2, py[i] + 0.2, g + 5.0);
-  // boxes of random size
+  // boxes of random size, kept off the circular driving lane of the config-3 loop (radius 6 m
+  // around the origin, synthgen.loop_pose): a box whose footprint reaches radii 3.5 .. 8.5 m is
+  // re-drawn (bounded, deterministic)
   for (int i = 0; i < 10; ++i) {
-    double cx = r.uni(-8, 8), cy = r.uni(-13, 13);
-    if (std::fabs(cx) < 7.5 && std::fabs(cy) < 7.5 && std::hypot(cx, cy) > 4.0 &&
-        std::hypot(cx, cy) < 8.0) cx += 8.0;   // keep the circular driving lane clear
     double sx = r.uni(0.4, 1.5), sy = r.uni(0.4, 1.5), sz = r.uni(0.5, 2.0);
+    double cx = 0, cy = 0;
+    for (int tries = 0; tries < 64; ++tries) {
+      cx = r.uni(-8.5, 8.5);
+      cy = r.uni(-13.5, 13.5);
+      const double dmin = std::hypot(std::max(std::fabs(cx) - sx, 0.0), std::max(std::fabs(cy) - sy, 0.0));
+      const double dmax = std::hypot(std::fabs(cx) + sx, std::fabs(cy) + sy);
+      if (dmin >= 8.5 || dmax <= 3.5) break;
+    }
     add_box(s, cx - sx, cy - sy, g, cx + sx, cy + sy, g + sz);
   }
   // outdoor structures beyond the room
