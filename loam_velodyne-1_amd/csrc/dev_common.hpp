@@ -22,6 +22,16 @@ constexpr int kWave = 64;
 LOAM_HD double D(float x) { return (double)x; }
 LOAM_HD double dsin(float x) { return sin((double)x); }
 LOAM_HD double dcos(float x) { return cos((double)x); }
+// sin and cos of one float argument in double; on the device one ocml sincos (the same argument
+// reduction and polynomials as its sin and cos, so the same values, for half the work)
+LOAM_HD void dsincos(float x, double& s, double& c) {
+#ifdef __HIP_DEVICE_COMPILE__
+  sincos((double)x, &s, &c);
+#else
+  s = sin((double)x);
+  c = cos((double)x);
+#endif
+}
 LOAM_HD double rad2deg(double r) { return r * 180.0 / M_PI; }
 
 // squared distance in the reference's float order (dx*dx + dy*dy) + dz*dz

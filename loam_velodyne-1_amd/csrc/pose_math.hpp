@@ -16,6 +16,7 @@ namespace loampose {
 using loamdev::D;
 using loamdev::dcos;
 using loamdev::dsin;
+using loamdev::dsincos;
 
 // /imu_trans values (zero without IMU); layout of loam_features.imu_trans
 struct Imu {
@@ -27,15 +28,19 @@ LOAM_HD float4 transform_to_start(const float* t, float4 pi) {
   float s = 10 * (pi.w - (int)pi.w);
   float rx = s * t[0], ry = s * t[1], rz = s * t[2];
   float tx = s * t[3], ty = s * t[4], tz = s * t[5];
-  float x1 = (float)(dcos(rz) * D(pi.x - tx) + dsin(rz) * D(pi.y - ty));
-  float y1 = (float)(-dsin(rz) * D(pi.x - tx) + dcos(rz) * D(pi.y - ty));
+  double sx, cx, sy, cy, sz, cz;
+  dsincos(rx, sx, cx);
+  dsincos(ry, sy, cy);
+  dsincos(rz, sz, cz);
+  float x1 = (float)(cz * D(pi.x - tx) + sz * D(pi.y - ty));
+  float y1 = (float)(-sz * D(pi.x - tx) + cz * D(pi.y - ty));
   float z1 = (pi.z - tz);
-  float y2 = (float)(dcos(rx) * D(y1) + dsin(rx) * D(z1));
-  float z2 = (float)(-dsin(rx) * D(y1) + dcos(rx) * D(z1));
+  float y2 = (float)(cx * D(y1) + sx * D(z1));
+  float z2 = (float)(-sx * D(y1) + cx * D(z1));
   float4 o;
-  o.x = (float)(dcos(ry) * D(x1) - dsin(ry) * D(z2));
+  o.x = (float)(cy * D(x1) - sy * D(z2));
   o.y = y2;
-  o.z = (float)(dsin(ry) * D(x1) + dcos(ry) * D(z2));
+  o.z = (float)(sy * D(x1) + cy * D(z2));
   o.w = pi.w;
   return o;
 }
@@ -48,15 +53,15 @@ struct EndRot {
 };
 LOAM_HD EndRot end_rot(const float* t, const Imu& m) {
   EndRot e;
-  e.crx = dcos(t[0]); e.srx = dsin(t[0]);
-  e.cry = dcos(t[1]); e.sry = dsin(t[1]);
-  e.crz = dcos(t[2]); e.srz = dsin(t[2]);
-  e.crs = dcos(m.rollStart); e.srs = dsin(m.rollStart);
-  e.cps = dcos(m.pitchStart); e.sps = dsin(m.pitchStart);
-  e.cys = dcos(m.yawStart); e.sys = dsin(m.yawStart);
-  e.cyl = dcos(m.yawLast); e.syl = dsin(m.yawLast);
-  e.cpl = dcos(m.pitchLast); e.spl = dsin(m.pitchLast);
-  e.crl = dcos(m.rollLast); e.srl = dsin(m.rollLast);
+  dsincos(t[0], e.srx, e.crx);
+  dsincos(t[1], e.sry, e.cry);
+  dsincos(t[2], e.srz, e.crz);
+  dsincos(m.rollStart, e.srs, e.crs);
+  dsincos(m.pitchStart, e.sps, e.cps);
+  dsincos(m.yawStart, e.sys, e.cys);
+  dsincos(m.yawLast, e.syl, e.cyl);
+  dsincos(m.pitchLast, e.spl, e.cpl);
+  dsincos(m.rollLast, e.srl, e.crl);
   return e;
 }
 
@@ -71,9 +76,9 @@ LOAM_HD float4 transform_to_end(const float* t, const Imu& m, const EndRot& e, f
     cx = cy = cz = 1.0;
     sx = sy = sz = 0.0;
   } else {
-    cx = dcos(rx); sx = dsin(rx);
-    cy = dcos(ry); sy = dsin(ry);
-    cz = dcos(rz); sz = dsin(rz);
+    dsincos(rx, sx, cx);
+    dsincos(ry, sy, cy);
+    dsincos(rz, sz, cz);
   }
   float x1 = (float)(cz * D(pi.x - tx) + sz * D(pi.y - ty));
   float y1 = (float)(-sz * D(pi.x - tx) + cz * D(pi.y - ty));
