@@ -1467,24 +1467,36 @@ int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::s
   return LOAM_OK;
 }
 
-void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof) {
+// frame 1 of the batch problem: reset, then prev (Last[0], fullEnd[0]) into the empty store at
+// the zero pose.  Reads only what the odometry seeding wrote, so it may run beside od_solve.
+void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof) {
   mp_reset(b, st);
   if (prof) prof->mark("mp_reset");
   MpInput in;
-  // frame 1: prev (Last[0], fullEnd[0]) at the zero pose
   in.corner = od.lastC; in.surf = od.lastS; in.full = od.fullEnd;
   in.corner_stride = od.capC; in.surf_stride = od.capS; in.full_stride = od.capS;
   in.ncorner = od.nlast + 0; in.nsurf = od.nlast + 1; in.nfull = od.nfullEnd + 0;
   in.ncorner_stride = 4; in.nsurf_stride = 4; in.nfull_stride = 2;
   in.pose = nullptr; in.pose_stride = 0;
   mp_frame(b, in, st, prof, /*map_empty=*/true);
-  // frame 2: cur (Last[1], fullEnd[1]) with the odometry transformSum
+}
+
+// frame 2: cur (Last[1], fullEnd[1]) with the odometry transformSum
+void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof) {
+  MpInput in;
   in.corner = od.lastC + (size_t)od.P * od.capC;
   in.surf = od.lastS + (size_t)od.P * od.capS;
   in.full = od.fullEnd + (size_t)od.P * od.capS;
+  in.corner_stride = od.capC; in.surf_stride = od.capS; in.full_stride = od.capS;
   in.ncorner = od.nlast + 2; in.nsurf = od.nlast + 3; in.nfull = od.nfullEnd + 1;
+  in.ncorner_stride = 4; in.nsurf_stride = 4; in.nfull_stride = 2;
   in.pose = od.state + kOdSum; in.pose_stride = kOdStateFloats;
   mp_frame(b, in, st, prof);
+}
+
+void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof) {
+  mp_batch_frame1(b, od, st, prof);
+  mp_batch_frame2(b, od, st, prof);
 }
 
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err) {

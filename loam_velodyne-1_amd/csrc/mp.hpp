@@ -113,6 +113,8 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
 // concatenated and VoxelGrid 0.2 (src/laserMapping.cpp:1038-1058)
 int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::string& err);
 void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof = nullptr);
+void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof = nullptr);
+void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof = nullptr);
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err);
 
 }  // namespace loam
