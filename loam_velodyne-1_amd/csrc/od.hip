@@ -133,6 +133,11 @@ __global__ __launch_bounds__(256) void k_hash_build(HashJob j) {
 
 namespace {
 
+#ifdef LOAM_EXP_ASSOCPH
+// diagnostic build only: cycles of the association phases and fallback counts (tools/exp_assoc.py)
+__device__ unsigned long long g_aph[8];
+#endif
+
 // lower bound of the float squared distance from s to any point of the box [lo, hi] (monotone
 // rounding of the same expression as sqdist)
 LOAM_D float box_d2(const float4& lo, const float4& hi, const float4& s) {
@@ -185,6 +190,9 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
   __builtin_amdgcn_wave_barrier();
   if (best != ~0ull && __uint_as_float((uint32_t)(best >> 32)) < h * h) return best;
   // farther than one cell: the chunks of the whole cloud that may hold a point closer than 5 m
+#ifdef LOAM_EXP_ASSOCPH
+  if (lane == 0) atomicAdd(&g_aph[4], 1ull);
+#endif
   best = ~0ull;
   const int nch = (n + kChunk - 1) / kChunk;
   for (int k0 = 0; k0 < nch; k0 += 64) {
@@ -404,18 +412,28 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(8)))
   const float4* SL = b.lastS + lp * b.capS;
   int* ind = b.ind + (size_t)p * 3 * b.cap_q;
   for (int q = blk.x * kOdWaves + w; q < nq; q += gridDim.x * kOdWaves) {
+#ifdef LOAM_EXP_ASSOCPH
+    long long t0 = clock64();
+#define APH(k) { const long long t1 = clock64(); if (lane == 0) atomicAdd(&g_aph[k], (unsigned long long)(t1 - t0)); t0 = t1; }
+#else
+#define APH(k)
+#endif
     const float4 s4 = sel[q];
     int i1, i2, i3 = -1;
     if (q < nc) {
       const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
       const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC,
                                        b.hC_T[last_buf * b.P + p], CL, ch, C, 1.0f, 1.0f, s4, cells[w]);
+      APH(0);
       wave_assoc_corner(CL, ch, min(nc, C), nn, s4, i1, i2);
+      APH(1);
     } else {
       const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
       const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS,
                                        b.hS_T[last_buf * b.P + p], SL, ch, S, 1.0f, 1.0f, s4, cells[w]);
+      APH(2);
       wave_assoc_surf(SL, ch, min(ns, S), nn, s4, i1, i2, i3);
+      APH(3);
     }
     if (lane == 0) {
       ind[q] = i1;
@@ -793,3 +811,9 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
   hipLaunchKernelGGL(k_od_fini, dim3((P + 255) / 256), dim3(256), 0, st, b, f);
 }
 }  // namespace loam
+
+#ifdef LOAM_EXP_ASSOCPH
+extern "C" int loam_debug_assoc(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(loam::g_aph), 8 * sizeof(unsigned long long)) == hipSuccess ? 0 : -3;
+}
+#endif
