@@ -54,6 +54,18 @@ LOAM_D int ring_id(const SrParams& p, float angle) {
   return rounded > 0 ? rounded : rounded + (p.R - 1);
 }
 
+// The reference computes the vertical angle in double (:241-247).  The float evaluation is within
+// 1e-4 degrees of it, so whenever a +-1e-3 degree bracket around it maps to one ring the double
+// evaluation cannot land elsewhere; only points that close to a ring boundary pay for it.
+LOAM_D int ring_of(const SrParams& p, float px, float py, float pz) {
+#ifndef LOAM_EXP_RINGF64
+  const float af = atanf(py / sqrtf(px * px + pz * pz)) * 57.2957795f;
+  const int lo = ring_id(p, af - 1e-3f), hi = ring_id(p, af + 1e-3f);
+  if (lo == hi) return lo;
+#endif
+  return ring_id(p, (float)(atan(D(py) / sqrt(D(px * px + pz * pz))) * 180 / M_PI));
+}
+
 LOAM_D float ori_first(float ori, float startOri) {  // :263-268
   if (D(ori) < D(startOri) - M_PI / 2) ori = (float)(D(ori) + 2 * M_PI);
   else if (D(ori) > D(startOri) + M_PI * 3 / 2) ori = (float)(D(ori) - 2 * M_PI);
@@ -121,8 +133,7 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_sort(SrBuffers b, SrPara
       float ori = 0.0f;
       if (finite3(q)) {
         const float px = q.y, py = q.z, pz = q.x;
-        float angle = (float)(atan(D(py) / sqrt(D(px * px + pz * pz))) * 180 / M_PI);
-        int scanID = ring_id(p, angle);
+        int scanID = ring_of(p, px, py, pz);
         if (scanID >= 0 && scanID <= R - 1) {
           sid = (uint8_t)scanID;
           ori = -atan2f_fdlibm(px, pz);
@@ -286,13 +297,24 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_sort(SrBuffers b, SrPara
 // the tile's ring counts and its first halfPassed flip; k_sr_ring_scatter takes the flip point F
 // as the minimum over the tiles, the ring bases and its tile's per-ring offsets from the counts,
 // and scatters with the same wave-ballot ranks.  src/scanRegistration.cpp:225-357
+// A tile is kRingE sub-tiles of kSrThreads points (each thread's kRingE loads in flight at once),
+// which also cuts the per-tile fixed work (sweep ends, start orientation, tile prefix) kRingE-fold.
+#ifdef LOAM_EXP_RINGE1
+constexpr int kRingE = 1;
+#elif defined(LOAM_EXP_RINGE8)
+constexpr int kRingE = 8;
+#else
+constexpr int kRingE = 4;
+#endif
+constexpr int kRingTile = kSrThreads * kRingE;
+
 __global__ __launch_bounds__(kSrThreads) void k_sr_ring_count(SrBuffers b, SrParams p) {
   const int s = blockIdx.y, t = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const int n = b.raw_n[s], R = p.R;
-  if (t * kSrThreads >= n) return;
+  if (t * kRingTile >= n) return;
   const float4* raw = b.raw + (size_t)s * b.cap;
   __shared__ int sh_first, sh_last, sh_F;
-  __shared__ float sh_start;
+  __shared__ float sh_start, sh_end_raw;
   __shared__ int sh_cnt[64];
   if (w == 0) {
     int f = -1;
@@ -314,42 +336,50 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_count(SrBuffers b, SrPar
   if (tid < R) sh_cnt[tid] = 0;
   if (tid == 0) sh_F = 0x7fffffff;
   __syncthreads();
-  if (tid == 0) {  // :230-238
-    float startOri = 0.0f, endOri = 0.0f;
-    if (sh_last >= 0) {
-      const float4 a = raw[sh_first], z = raw[sh_last];
-      startOri = -atan2f_fdlibm(a.y, a.x);
-      endOri = (float)(D(-atan2f_fdlibm(z.y, z.x)) + 2 * M_PI);
-      if (D(endOri - startOri) > 3 * M_PI) endOri = (float)(D(endOri) - 2 * M_PI);
-      else if (D(endOri - startOri) < M_PI) endOri = (float)(D(endOri) + 2 * M_PI);
-    } else if (t == 0) {
-      b.err[s] |= ERR_EMPTY;
-    }
-    sh_start = startOri;
-    if (t == 0) { b.sweep_ori[2 * s] = startOri; b.sweep_ori[2 * s + 1] = endOri; }
-  }
+  // :230-238, the two orientations on two waves; only tile 0 needs endOri
+  if (tid == 0) sh_start = sh_last >= 0 ? -atan2f_fdlibm(raw[sh_first].y, raw[sh_first].x) : 0.0f;
+  if (tid == 64 && t == 0 && sh_last >= 0) sh_end_raw = -atan2f_fdlibm(raw[sh_last].y, raw[sh_last].x);
   __syncthreads();
   const float startOri = sh_start;
-  const int i = t * kSrThreads + tid;
-  int Floc = 0x7fffffff;
-  if (i < n) {
-    const float4 q = raw[i];
-    uint8_t sid = 255;
-    float ori = 0.0f;
-    if (finite3(q)) {
-      const float px = q.y, py = q.z, pz = q.x;
-      const float angle = (float)(atan(D(py) / sqrt(D(px * px + pz * pz))) * 180 / M_PI);
-      const int scanID = ring_id(p, angle);
-      if (scanID >= 0 && scanID <= R - 1) {
-        sid = (uint8_t)scanID;
-        ori = -atan2f_fdlibm(px, pz);
-        const float o1 = ori_first(ori, startOri);
-        if (D(o1 - startOri) > M_PI) Floc = i;
-        atomicAdd(&sh_cnt[scanID], 1);
-      }
+  if (tid == 0 && t == 0) {
+    float endOri = 0.0f;
+    if (sh_last >= 0) {
+      endOri = (float)(D(sh_end_raw) + 2 * M_PI);
+      if (D(endOri - startOri) > 3 * M_PI) endOri = (float)(D(endOri) - 2 * M_PI);
+      else if (D(endOri - startOri) < M_PI) endOri = (float)(D(endOri) + 2 * M_PI);
+    } else {
+      b.err[s] |= ERR_EMPTY;
     }
-    b.tmp_ori[(size_t)s * b.cap + i] = ori;
-    b.tmp_sid[(size_t)s * b.cap + i] = sid;
+    b.sweep_ori[2 * s] = startOri;
+    b.sweep_ori[2 * s + 1] = endOri;
+  }
+  float4 q[kRingE];
+#pragma unroll
+  for (int e = 0; e < kRingE; ++e) {
+    const int i = t * kRingTile + e * kSrThreads + tid;
+    q[e] = i < n ? raw[i] : make_float4(0, 0, 0, 0);
+  }
+  int Floc = 0x7fffffff;
+#pragma unroll
+  for (int e = 0; e < kRingE; ++e) {
+    const int i = t * kRingTile + e * kSrThreads + tid;
+    if (i < n) {
+      uint8_t sid = 255;
+      float ori = 0.0f;
+      if (finite3(q[e])) {
+        const float px = q[e].y, py = q[e].z, pz = q[e].x;
+        const int scanID = ring_of(p, px, py, pz);
+        if (scanID >= 0 && scanID <= R - 1) {
+          sid = (uint8_t)scanID;
+          ori = -atan2f_fdlibm(px, pz);
+          const float o1 = ori_first(ori, startOri);
+          if (D(o1 - startOri) > M_PI) Floc = min(Floc, i);
+          atomicAdd(&sh_cnt[scanID], 1);
+        }
+      }
+      b.tmp_ori[(size_t)s * b.cap + i] = ori;
+      b.tmp_sid[(size_t)s * b.cap + i] = sid;
+    }
   }
   Floc = wave_min_i(Floc);
   if (lane == 0 && Floc != 0x7fffffff) atomicMin(&sh_F, Floc);
@@ -359,13 +389,16 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_count(SrBuffers b, SrPar
 }
 
 __global__ __launch_bounds__(kSrThreads) void k_sr_ring_scatter(SrBuffers b, SrParams p) {
+  constexpr int kW = kSrThreads / 64, kSlots = kRingE * kW;  // (sub-tile, wave) slots in point order
+  static_assert(kSlots <= 64 && (kSlots & (kSlots - 1)) == 0, "slot scan width");
   const int s = blockIdx.y, t = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  const int n = b.raw_n[s], R = p.R, nt = (n + kSrThreads - 1) / kSrThreads;
+  const int n = b.raw_n[s], R = p.R, nt = (n + kRingTile - 1) / kRingTile;
   if (t >= (nt > 0 ? nt : 1)) return;
   __shared__ int sh_tot[64], sh_pre[64], sh_base[64], sh_F;
-  __shared__ int sh_wcnt[kSrThreads / 64][64];
+  __shared__ int sh_wcnt[64][kSlots];  // per ring: points of each slot, then their exclusive prefix
   if (tid < R) { sh_tot[tid] = 0; sh_pre[tid] = 0; }
   if (tid == 0) sh_F = 0x7fffffff;
+  for (int k = tid; k < 64 * kSlots; k += kSrThreads) (&sh_wcnt[0][0])[k] = 0;
   __syncthreads();
   const int* tc = b.tilecnt + (size_t)s * b.ntiles() * R;
   for (int k = tid; k < nt * R; k += kSrThreads) {
@@ -379,6 +412,27 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_scatter(SrBuffers b, SrP
   for (int k = tid; k < nt; k += kSrThreads) F = min(F, b.tileF[(size_t)s * b.ntiles() + k]);
   F = wave_min_i(F);
   if (lane == 0 && F != 0x7fffffff) atomicMin(&sh_F, F);
+  // stable ranks within each (sub-tile, wave) slot by wave ballots
+  int sid[kRingE], rank[kRingE];
+#pragma unroll
+  for (int e = 0; e < kRingE; ++e) {
+    const int i = t * kRingTile + e * kSrThreads + tid;
+    sid[e] = i < n ? (int)b.tmp_sid[(size_t)s * b.cap + i] : 255;
+  }
+#pragma unroll
+  for (int e = 0; e < kRingE; ++e) {
+    const bool valid = sid[e] != 255;
+    rank[e] = 0;
+    uint64_t mval = __ballot(valid);
+    while (mval) {
+      const int leader = __ffsll((unsigned long long)mval) - 1;
+      const int rl = __shfl(sid[e], leader, 64);
+      const uint64_t mm = __ballot(valid && sid[e] == rl);
+      if (valid && sid[e] == rl) rank[e] = __popcll(mm & lanemask_lt());
+      if (lane == leader) sh_wcnt[rl][e * kW + w] = __popcll(mm);
+      mval &= ~mm;
+    }
+  }
   __syncthreads();
   if (tid == 0) {
     int run = 0;
@@ -388,53 +442,67 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_scatter(SrBuffers b, SrP
       if (n <= 0) b.err[s] |= ERR_EMPTY;
     }
   }
-  if (lane < R) sh_wcnt[w][lane] = 0;
+  // per ring, exclusive prefix over the slots: kSlots lanes per ring, groups aligned to kSlots
+  for (int k = tid; k < R * kSlots; k += kSrThreads) {
+    const int r = k / kSlots, j = k % kSlots;
+    const int v = sh_wcnt[r][j];
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < kSlots; o <<= 1) {
+      const int u = __shfl_up(incl, o, kSlots);
+      if (j >= o) incl += u;
+    }
+    sh_wcnt[r][j] = incl - v;
+  }
   __syncthreads();
   if (nt == 0) return;
   F = sh_F;
   const float startOri = b.sweep_ori[2 * s], endOri = b.sweep_ori[2 * s + 1];
-  const int i = t * kSrThreads + tid;
-  const int sid = i < n ? (int)b.tmp_sid[(size_t)s * b.cap + i] : 255;
-  const bool valid = i < n && sid != 255;
-  int rank = 0;
-  uint64_t mval = __ballot(valid);
-  while (mval) {
-    const int leader = __ffsll((unsigned long long)mval) - 1;
-    const int rl = __shfl(sid, leader, 64);
-    const uint64_t mm = __ballot(valid && sid == rl);
-    if (valid && sid == rl) rank = __popcll(mm & lanemask_lt());
-    if (lane == leader) sh_wcnt[w][rl] = __popcll(mm);
-    mval &= ~mm;
+  float4 q[kRingE];
+  float ori[kRingE];
+#pragma unroll
+  for (int e = 0; e < kRingE; ++e) {
+    const int i = t * kRingTile + e * kSrThreads + tid;
+    if (sid[e] != 255) {
+      q[e] = b.raw[(size_t)s * b.cap + i];
+      ori[e] = b.tmp_ori[(size_t)s * b.cap + i];
+    }
   }
-  __syncthreads();
-  if (valid) {
-    int pos = sh_base[sid] + sh_pre[sid] + rank;
-    for (int v = 0; v < w; ++v) pos += sh_wcnt[v][sid];
-    const float4 q = b.raw[(size_t)s * b.cap + i];
-    float ori = b.tmp_ori[(size_t)s * b.cap + i];
-    ori = (i <= F) ? ori_first(ori, startOri) : ori_second(ori, endOri);
-    const float relTime = (ori - startOri) / (endOri - startOri);
-    b.full[(size_t)s * b.cap + pos] = make_float4(q.y, q.z, q.x, (float)(sid + 0.1 * D(relTime)));
+#pragma unroll
+  for (int e = 0; e < kRingE; ++e) {
+    const int i = t * kRingTile + e * kSrThreads + tid;
+    if (sid[e] != 255) {
+      const int pos = sh_base[sid[e]] + sh_pre[sid[e]] + sh_wcnt[sid[e]][e * kW + w] + rank[e];
+      const float o = (i <= F) ? ori_first(ori[e], startOri) : ori_second(ori[e], endOri);
+      const float relTime = (o - startOri) / (endOri - startOri);
+      b.full[(size_t)s * b.cap + pos] = make_float4(q[e].y, q[e].z, q[e].x, (float)(sid[e] + 0.1 * D(relTime)));
+    }
   }
 }
 
 // ---------------------------------------------------------------- curvature + marks
-constexpr int kFeatTile = 256;
+constexpr int kFeatTile = 256;  // threads
+#ifdef LOAM_EXP_FEATE1
+constexpr int kFeatE = 1;
+#else
+constexpr int kFeatE = 4;  // points per thread
+#endif
+constexpr int kFeatSpan = kFeatTile * kFeatE;
 
 __global__ __launch_bounds__(kFeatTile) void k_sr_features(SrBuffers b, SrParams p) {
   const int s = blockIdx.y, tid = threadIdx.x;
   const int n = b.n_full[s];
-  const int i0 = blockIdx.x * kFeatTile;
+  const int i0 = blockIdx.x * kFeatSpan;
   if (i0 >= n) return;
   const float4* pts = b.full + (size_t)s * b.cap;
-  __shared__ float4 sp[kFeatTile + 12];
-  __shared__ int8_t evt[kFeatTile + 12];
-  for (int t = tid; t < kFeatTile + 12; t += kFeatTile) {
+  __shared__ float4 sp[kFeatSpan + 12];
+  __shared__ int8_t evt[kFeatSpan + 12];
+  for (int t = tid; t < kFeatSpan + 12; t += kFeatTile) {
     int g = i0 - 6 + t;
     if (g >= 0 && g < n) sp[t] = pts[g];
   }
   __syncthreads();
-  for (int t = tid; t < kFeatTile + 11; t += kFeatTile) {  // occlusion events (:395-438)
+  for (int t = tid; t < kFeatSpan + 11; t += kFeatTile) {  // occlusion events (:395-438)
     const int k = i0 - 6 + t;
     int8_t e = 0;
     if (k >= 5 && k <= n - 7) {
@@ -460,51 +528,54 @@ __global__ __launch_bounds__(kFeatTile) void k_sr_features(SrBuffers b, SrParams
     evt[t] = e;
   }
   __syncthreads();
-  const int i = i0 + tid;
-  if (i >= n) return;
-  const int li = tid + 6;
-  const size_t gi = (size_t)s * b.cap + i;
-  float cv = 0.0f;
-  if (i >= 5 && i < n - 5) {  // :359-378
-    const float4* q = sp + li;
-    float dX = q[-5].x + q[-4].x + q[-3].x + q[-2].x + q[-1].x - 10 * q[0].x + q[1].x + q[2].x +
-               q[3].x + q[4].x + q[5].x;
-    float dY = q[-5].y + q[-4].y + q[-3].y + q[-2].y + q[-1].y - 10 * q[0].y + q[1].y + q[2].y +
-               q[3].y + q[4].y + q[5].y;
-    float dZ = q[-5].z + q[-4].z + q[-3].z + q[-2].z + q[-1].z - 10 * q[0].z + q[1].z + q[2].z +
-               q[3].z + q[4].z + q[5].z;
-    cv = dX * dX + dY * dY + dZ * dZ;
-    // ring bounds (:383-390): the last transition into ring v wins
-    const int v = (int)q[0].w;
-    const int pv = (i == 5) ? -1 : (int)q[-1].w;
-    if (v != pv && v > 0 && v < p.R) {
-      atomicMax(&b.ring_se[s * 2 * p.R + v], i + 5);
-      atomicMax(&b.ring_se[s * 2 * p.R + p.R + v - 1], i - 5);
+#pragma unroll
+  for (int fe = 0; fe < kFeatE; ++fe) {
+    const int i = i0 + fe * kFeatTile + tid;
+    if (i >= n) return;
+    const int li = fe * kFeatTile + tid + 6;
+    const size_t gi = (size_t)s * b.cap + i;
+    float cv = 0.0f;
+    if (i >= 5 && i < n - 5) {  // :359-378
+      const float4* q = sp + li;
+      float dX = q[-5].x + q[-4].x + q[-3].x + q[-2].x + q[-1].x - 10 * q[0].x + q[1].x + q[2].x +
+                 q[3].x + q[4].x + q[5].x;
+      float dY = q[-5].y + q[-4].y + q[-3].y + q[-2].y + q[-1].y - 10 * q[0].y + q[1].y + q[2].y +
+                 q[3].y + q[4].y + q[5].y;
+      float dZ = q[-5].z + q[-4].z + q[-3].z + q[-2].z + q[-1].z - 10 * q[0].z + q[1].z + q[2].z +
+                 q[3].z + q[4].z + q[5].z;
+      cv = dX * dX + dY * dY + dZ * dZ;
+      // ring bounds (:383-390): the last transition into ring v wins
+      const int v = (int)q[0].w;
+      const int pv = (i == 5) ? -1 : (int)q[-1].w;
+      if (v != pv && v > 0 && v < p.R) {
+        atomicMax(&b.ring_se[s * 2 * p.R + v], i + 5);
+        atomicMax(&b.ring_se[s * 2 * p.R + p.R + v - 1], i - 5);
+      }
     }
+    int pk = 0;
+    for (int k = 0; k <= 5; ++k) pk |= (evt[li + k] == 1);
+    for (int k = 1; k <= 6; ++k) pk |= (evt[li - k] == 2);
+    if (i >= 5 && i <= n - 7) {  // :440-451
+      const float4 a = sp[li - 1], c = sp[li], e = sp[li + 1];
+      float dX = e.x - c.x, dY = e.y - c.y, dZ = e.z - c.z;
+      float diff = dX * dX + dY * dY + dZ * dZ;
+      float dX2 = c.x - a.x, dY2 = c.y - a.y, dZ2 = c.z - a.z;
+      float diff2 = dX2 * dX2 + dY2 * dY2 + dZ2 * dZ2;
+      float dis = c.x * c.x + c.y * c.y + c.z * c.z;
+      if (D(diff) > 0.0002 * D(dis) && D(diff2) > 0.0002 * D(dis)) pk = 1;
+    }
+    // bit 1: the neighbour walk of :495-520 stops between i-1 and i
+    int gap = 0;
+    if (i >= 1) {
+      const float4 a = sp[li], c = sp[li - 1];
+      const float ex = a.x - c.x, ey = a.y - c.y, ez = a.z - c.z;
+      gap = D(ex * ex + ey * ey + ez * ez) > 0.05 ? 1 : 0;
+    }
+    b.curv[gi] = cv;
+    b.picked[gi] = (uint8_t)(pk | (gap << 1));
+    b.sortind[gi] = i;
+    b.label[gi] = 0;
   }
-  int pk = 0;
-  for (int k = 0; k <= 5; ++k) pk |= (evt[li + k] == 1);
-  for (int k = 1; k <= 6; ++k) pk |= (evt[li - k] == 2);
-  if (i >= 5 && i <= n - 7) {  // :440-451
-    const float4 a = sp[li - 1], c = sp[li], e = sp[li + 1];
-    float dX = e.x - c.x, dY = e.y - c.y, dZ = e.z - c.z;
-    float diff = dX * dX + dY * dY + dZ * dZ;
-    float dX2 = c.x - a.x, dY2 = c.y - a.y, dZ2 = c.z - a.z;
-    float diff2 = dX2 * dX2 + dY2 * dY2 + dZ2 * dZ2;
-    float dis = c.x * c.x + c.y * c.y + c.z * c.z;
-    if (D(diff) > 0.0002 * D(dis) && D(diff2) > 0.0002 * D(dis)) pk = 1;
-  }
-  // bit 1: the neighbour walk of :495-520 stops between i-1 and i
-  int gap = 0;
-  if (i >= 1) {
-    const float4 a = sp[li], c = sp[li - 1];
-    const float ex = a.x - c.x, ey = a.y - c.y, ez = a.z - c.z;
-    gap = D(ex * ex + ey * ey + ez * ez) > 0.05 ? 1 : 0;
-  }
-  b.curv[gi] = cv;
-  b.picked[gi] = (uint8_t)(pk | (gap << 1));
-  b.sortind[gi] = i;
-  b.label[gi] = 0;
 }
 
 // ---------------------------------------------------------------- per-ring selection
@@ -566,48 +637,126 @@ LOAM_D int ring_vg(const float4* pts, int lo, const CandT* cand, int nc, uint64_
       }
       const int divx = maxb[0] - minb[0] + 1, divy = maxb[1] - minb[1] + 1;
       const int mul1 = divx, mul2 = divx * divy;
-      const int P2c = next_pow2(nc);
-      for (int t = tid; t < P2c; t += kSelThreads) {
-        uint64_t key = ~0ull;
-        if (t < nc) {
-          const float4 a = pts[lo + cand[t]];
-          int i0 = (int)(floorf(a.x * inv) - (float)minb[0]);
-          int i1 = (int)(floorf(a.y * inv) - (float)minb[1]);
-          int i2 = (int)(floorf(a.z * inv) - (float)minb[2]);
-          uint32_t idx = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
-          key = ((uint64_t)idx << 32) | (uint32_t)t;
-        }
-        keys[t] = key;
-      }
-      __syncthreads();
-      if constexpr (BIG) block_bitonic_sort<kSelThreads>(keys, P2c);
-      else reg_bitonic_sort<kSelThreads, CAP / kSelThreads>(keys, P2c);
-      int run = 0;
-      for (int base = 0; base < nc; base += kSelThreads) {
-        const int t = base + tid;
-        const int head = (t < nc && (t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32))) ? 1 : 0;
-        int tot;
-        const int ex = block_excl_scan<kSelThreads>(head, scratch, tot);
-        if (head) {
-          const uint32_t vk = (uint32_t)(keys[t] >> 32);
-          int e = t + 1;
-          while (e < nc && (uint32_t)(keys[e] >> 32) == vk) ++e;
-          // members summed in sorted order; four independent gathers in flight per step
-          float sx = 0, sy = 0, sz = 0, si = 0;
-          for (int m = t; m < e; m += 4) {
-            float4 a[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) a[u] = pts[lo + cand[(int)(keys[min(m + u, e - 1)] & 0xffffffffu)]];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              if (m + u < e) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
+#ifndef LOAM_EXP_VGOLD
+      if constexpr (!BIG) {
+        // Candidates come in ring order, so consecutive ones mostly share a voxel (~2.2 per run on
+        // VLP-16): sort the runs, (voxel, first candidate, length), instead of the candidates.
+        // Runs of one voxel sorted by their first candidate list its members in the same order as
+        // the stable (voxel, candidate) sort, so the means are summed in the same order.
+        uint32_t* edge = reinterpret_cast<uint32_t*>(&red[0][0]);  // last voxel of each wave's chunk
+        int nruns = 0;
+        for (int base = 0; base < nc; base += kSelThreads) {
+          const int t = base + tid;
+          uint32_t idx = 0xffffffffu;
+          if (t < nc) {
+            const float4 a = pts[lo + cand[t]];
+            const int i0 = (int)(floorf(a.x * inv) - (float)minb[0]);
+            const int i1 = (int)(floorf(a.y * inv) - (float)minb[1]);
+            const int i2 = (int)(floorf(a.z * inv) - (float)minb[2]);
+            idx = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
           }
-          const float cnt = (float)(e - t);
-          if (run + ex < outcap) outp[run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+          uint32_t up = (uint32_t)__shfl_up((int)idx, 1, 64);
+          if (lane == 63) edge[w + 1] = idx;
+          __syncthreads();
+          if (lane == 0) up = edge[w];  // edge[0]: the previous chunk's last candidate
+          const int head = (t < nc && (t == 0 || idx != up)) ? 1 : 0;
+          int tot;
+          const int ex = block_excl_scan<kSelThreads>(head, scratch, tot);
+          if (head) keys[nruns + ex] = ((uint64_t)idx << 32) | ((uint32_t)t << 16);
+          if (tid == kSelThreads - 1) edge[0] = idx;
+          nruns += tot;
         }
-        run += tot;
+        __syncthreads();
+        constexpr int RE = CAP / kSelThreads;
+        uint32_t nxt[RE];
+#pragma unroll
+        for (int e = 0; e < RE; ++e) {
+          const int r = e * kSelThreads + tid;
+          nxt[e] = r + 1 < nruns ? (uint32_t)keys[r + 1] >> 16 : (uint32_t)nc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < RE; ++e) {
+          const int r = e * kSelThreads + tid;
+          if (r < nruns) keys[r] |= nxt[e] - ((uint32_t)keys[r] >> 16);
+        }
+        __syncthreads();
+        reg_bitonic_sort<kSelThreads, CAP / kSelThreads>(keys, nruns);
+        int run = 0;
+        for (int base = 0; base < nruns; base += kSelThreads) {
+          const int r = base + tid;
+          const int head = (r < nruns && (r == 0 || (keys[r] >> 32) != (keys[r - 1] >> 32))) ? 1 : 0;
+          int tot;
+          const int ex = block_excl_scan<kSelThreads>(head, scratch, tot);
+          if (head) {
+            const uint32_t vk = (uint32_t)(keys[r] >> 32);
+            float sx = 0, sy = 0, sz = 0, si = 0;
+            int cnt = 0;
+            for (int e = r; e < nruns && (uint32_t)(keys[e] >> 32) == vk; ++e) {
+              const uint32_t k = (uint32_t)keys[e];
+              const int m0 = (int)(k >> 16), m1 = m0 + (int)(k & 0xffffu);
+              cnt += m1 - m0;
+              for (int m = m0; m < m1; m += 4) {  // four independent gathers in flight per step
+                float4 a[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) a[u] = pts[lo + cand[min(m + u, m1 - 1)]];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                  if (m + u < m1) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
+              }
+            }
+            const float fc = (float)cnt;
+            if (run + ex < outcap) outp[run + ex] = make_float4(sx / fc, sy / fc, sz / fc, si / fc);
+          }
+          run += tot;
+        }
+        nout = run;
+      } else
+#endif
+      {
+        const int P2c = next_pow2(nc);
+        for (int t = tid; t < P2c; t += kSelThreads) {
+          uint64_t key = ~0ull;
+          if (t < nc) {
+            const float4 a = pts[lo + cand[t]];
+            int i0 = (int)(floorf(a.x * inv) - (float)minb[0]);
+            int i1 = (int)(floorf(a.y * inv) - (float)minb[1]);
+            int i2 = (int)(floorf(a.z * inv) - (float)minb[2]);
+            uint32_t idx = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
+            key = ((uint64_t)idx << 32) | (uint32_t)t;
+          }
+          keys[t] = key;
+        }
+        __syncthreads();
+        if constexpr (BIG) block_bitonic_sort<kSelThreads>(keys, P2c);
+        else reg_bitonic_sort<kSelThreads, CAP / kSelThreads>(keys, P2c);
+        int run = 0;
+        for (int base = 0; base < nc; base += kSelThreads) {
+          const int t = base + tid;
+          const int head = (t < nc && (t == 0 || (keys[t] >> 32) != (keys[t - 1] >> 32))) ? 1 : 0;
+          int tot;
+          const int ex = block_excl_scan<kSelThreads>(head, scratch, tot);
+          if (head) {
+            const uint32_t vk = (uint32_t)(keys[t] >> 32);
+            int e = t + 1;
+            while (e < nc && (uint32_t)(keys[e] >> 32) == vk) ++e;
+            // members summed in sorted order; four independent gathers in flight per step
+            float sx = 0, sy = 0, sz = 0, si = 0;
+            for (int m = t; m < e; m += 4) {
+              float4 a[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) a[u] = pts[lo + cand[(int)(keys[min(m + u, e - 1)] & 0xffffffffu)]];
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                if (m + u < e) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
+            }
+            const float cnt = (float)(e - t);
+            if (run + ex < outcap) outp[run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+          }
+          run += tot;
+        }
+        nout = run;
       }
-      nout = run;
     }
     if (nout > outcap) {
       if (tid == 0) atomicOr(err, ERR_CAP_RING);
@@ -1242,12 +1391,13 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
 #ifdef LOAM_EXP_RINGWG
     hipLaunchKernelGGL(k_sr_ring_sort<false>, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
 #else
-    hipLaunchKernelGGL(k_sr_ring_count, dim3(b.ntiles(), b.S), dim3(kSrThreads), 0, st, b, p);
-    hipLaunchKernelGGL(k_sr_ring_scatter, dim3(b.ntiles(), b.S), dim3(kSrThreads), 0, st, b, p);
+    const int rtiles = (b.cap + kRingTile - 1) / kRingTile;  // <= b.ntiles(): tilecnt rows fit
+    hipLaunchKernelGGL(k_sr_ring_count, dim3(rtiles, b.S), dim3(kSrThreads), 0, st, b, p);
+    hipLaunchKernelGGL(k_sr_ring_scatter, dim3(rtiles, b.S), dim3(kSrThreads), 0, st, b, p);
 #endif
   }
   mark("k_sr_ring_sort");
-  hipLaunchKernelGGL(k_sr_features, dim3((b.cap + kFeatTile - 1) / kFeatTile, b.S), dim3(kFeatTile), 0,
+  hipLaunchKernelGGL(k_sr_features, dim3((b.cap + kFeatSpan - 1) / kFeatSpan, b.S), dim3(kFeatTile), 0,
                      st, b, p);
   mark("k_sr_features");
 #ifdef LOAM_EXP_NOSPLIT
