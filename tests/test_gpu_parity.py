@@ -88,6 +88,33 @@ def test_sr_long_rings(loam, oc, sg):
         _cmp_cloud(fg[k], fo[k], k)
 
 
+@pytest.mark.parametrize("model", ["vlp16", "linear64"])
+def test_sr_ring_boundaries(loam, oc, sg, model):
+    """Every third point moved to within 1e-7..3e-3 degrees of a ring boundary: the engine's float
+    ring ID defers to the double evaluation there (sr.hip ring_of), the oracle always uses double."""
+    if model == "vlp16":
+        _, raw = sg.single_problem(0)
+        kw = {}
+        bounds = np.arange(-16.0, 17.0, 2.0)  # round((angle + 15) / 2) steps at even degrees
+    else:
+        _, raw = sg.single_problem(2, lidar=sg.HDL64)
+        kw = dict(n_rings=64, ring_model=loam.RING_LINEAR, max_points=160000)
+        c = loam.default_config(**kw)
+        step = (c.ring_hi_deg - c.ring_lo_deg) / 63
+        bounds = c.ring_lo_deg + (np.arange(64) + 0.5) * step
+    raw = raw.copy()
+    rng = np.random.default_rng(7)
+    sel = np.arange(0, raw.shape[0], 3)
+    h = np.hypot(raw[sel, 0], raw[sel, 1]).astype(np.float64)
+    ang = np.degrees(np.arctan2(raw[sel, 2], h))
+    near = bounds[np.abs(ang[:, None] - bounds[None, :]).argmin(axis=1)]
+    off = rng.choice([-1.0, 1.0], sel.size) * 10.0 ** rng.uniform(-7, np.log10(3e-3), sel.size)
+    raw[sel, 2] = (np.tan(np.radians(near + off)) * h).astype(np.float32)
+    fg, fo = _sr_both(loam, oc, raw, kw)
+    for k in ("full", "sharp", "less_sharp", "flat", "less_flat"):
+        _cmp_cloud(fg[k], fo[k], k)
+
+
 def test_sr_stride32(loam, oc, sg):
     _, cur = sg.single_problem(0)
     raw = np.zeros((cur.shape[0], 8), np.float32)   # PointXYZI-like 32-byte records
