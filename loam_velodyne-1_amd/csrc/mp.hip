@@ -445,6 +445,16 @@ void vg_launch_reduce(const VgJob& j, hipStream_t st) {
 // (hipCUB segmented radix sort), which finishes the segments beyond fcap.  The fused kernel wins
 // for a few instances (streaming: one launch instead of four, no global key arrays); for large
 // batches hipCUB's multi-kernel path measured faster (both keep the stable (voxel, position) order).
+#if defined(LOAM_EXP_VGFUSED) || defined(LOAM_EXP_VGFUSED2)
+constexpr bool kVgFusedBatch = true;
+#else
+constexpr bool kVgFusedBatch = false;
+#endif
+#if defined(LOAM_EXP_VGCUBE2K) || defined(LOAM_EXP_VGFUSED2)
+constexpr int kVgCubeCap = 2048;
+#else
+constexpr int kVgCubeCap = 12288;
+#endif
 void vg_run(const VgJob& j0, void* tmp, size_t tmp_bytes, hipStream_t st, int G, int fcap) {
   if (j0.nseg == 0) return;
   const int grid = std::min(j0.nseg, 65536);
@@ -1270,7 +1280,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   js.in = b.stack2; js.out = b.stack; js.begin = b.sseg_b; js.end = b.sseg_e; js.leaf = b.sseg_leaf;
   js.out_count = b.sseg_cnt; js.params = b.vg_params; js.keys = b.vg_k; js.keys_alt = b.vg_k2;
   js.vals = b.vg_v; js.vals_alt = b.vg_v2; js.big_b = b.vg_bb; js.big_e = b.vg_be; js.nseg = 2 * P; js.total = P * b.cap_stack;
-  vg_run(js, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 1024 : 256, P <= 4 ? 12288 : 0);  // two large segments per instance
+  vg_run(js, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 1024 : 256, P <= 4 || kVgFusedBatch ? 12288 : 0);  // two large segments per instance
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);
   mark("k_mp_gather");
@@ -1311,7 +1321,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   jv.in = b.vin; jv.out = b.vout; jv.begin = b.vseg_b; jv.end = b.vseg_e; jv.leaf = b.vseg_leaf;
   jv.out_count = b.vseg_cnt; jv.params = b.vg_params; jv.keys = b.vg_k; jv.keys_alt = b.vg_k2;
   jv.vals = b.vg_v; jv.vals_alt = b.vg_v2; jv.big_b = b.vg_bb; jv.big_e = b.vg_be; jv.nseg = 2 * kMaxValid * P; jv.total = P * b.map_cap;
-  vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 256 : 64, P <= 4 ? 12288 : 0);    // 2 x 125 cube segments per instance
+  vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 256 : 64, P <= 4 || kVgFusedBatch ? kVgCubeCap : 0);    // 2 x 125 cube segments per instance
   mark("vg_cubes");
   hipLaunchKernelGGL(k_mp_compact_table, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);

@@ -785,17 +785,39 @@ LOAM_D void mark_neighbours(int n, int ind, uint8_t* pk, int wlo) {
 
 // The greedy picks of one segment [sp, ep] (ring-local) for independent rings (one wave):
 // :476-522 sharp / less sharp and :524-566 flat, on the ring's curvatures cv and the LDS pick state.
+// SR > 0: the segment is at most 64 * SR points and its curvatures are read once into SR registers
+// per lane (the flat walk rescans them up to four times).
+template <int SR = 0>
 LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, uint64_t* list, uint8_t* pk,
                                 int8_t* lab, int wlo, int* picks, int& nsharp, int& nlsharp, int& nflat) {
   const int lane = lane_id();
+  float cr[SR > 0 ? SR : 1];
+  if constexpr (SR > 0) {
+#pragma unroll
+    for (int k = 0; k < SR; ++k) {
+      const int t = sp + k * 64 + lane;
+      cr[k] = t <= ep ? cv[t] : 0.0f;
+    }
+  }
   // points with curvature > 0.1, as (curvature bits, position): ascending = the stable sort's order
   int m = 0;
-  for (int base = sp; base <= ep; base += 64) {
-    const int t = base + lane;
-    const bool e = t <= ep && D(cv[t]) > 0.1;
-    const uint64_t bm = __ballot(e);
-    if (e) list[m + __popcll(bm & lanemask_lt())] = ((uint64_t)fkey(cv[t]) << 32) | (uint32_t)t;
-    m += __popcll(bm);
+  if constexpr (SR > 0) {
+#pragma unroll
+    for (int k = 0; k < SR; ++k) {
+      const int t = sp + k * 64 + lane;
+      const bool e = t <= ep && D(cr[k]) > 0.1;
+      const uint64_t bm = __ballot(e);
+      if (e) list[m + __popcll(bm & lanemask_lt())] = ((uint64_t)fkey(cr[k]) << 32) | (uint32_t)t;
+      m += __popcll(bm);
+    }
+  } else {
+    for (int base = sp; base <= ep; base += 64) {
+      const int t = base + lane;
+      const bool e = t <= ep && D(cv[t]) > 0.1;
+      const uint64_t bm = __ballot(e);
+      if (e) list[m + __popcll(bm & lanemask_lt())] = ((uint64_t)fkey(cv[t]) << 32) | (uint32_t)t;
+      m += __popcll(bm);
+    }
   }
   __threadfence_block();
   __builtin_amdgcn_wave_barrier();
@@ -834,11 +856,22 @@ LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, 
   // flat: the unmarked point of smallest (curvature, position) below 0.1, four times at most
   for (int smallest = 0;;) {
     uint64_t best = ~0ull;
-    for (int t = sp + lane; t <= ep; t += 64) {
-      const float c = cv[t];
-      if (D(c) < 0.1 && (pk[lo + t - wlo] & 1) == 0) {
-        const uint64_t key = ((uint64_t)fkey(c) << 32) | (uint32_t)t;
-        best = key < best ? key : best;
+    if constexpr (SR > 0) {
+#pragma unroll
+      for (int k = 0; k < SR; ++k) {
+        const int t = sp + k * 64 + lane;
+        if (t <= ep && D(cr[k]) < 0.1 && (pk[lo + t - wlo] & 1) == 0) {
+          const uint64_t key = ((uint64_t)fkey(cr[k]) << 32) | (uint32_t)t;
+          best = key < best ? key : best;
+        }
+      }
+    } else {
+      for (int t = sp + lane; t <= ep; t += 64) {
+        const float c = cv[t];
+        if (D(c) < 0.1 && (pk[lo + t - wlo] & 1) == 0) {
+          const uint64_t key = ((uint64_t)fkey(c) << 32) | (uint32_t)t;
+          best = key < best ? key : best;
+        }
       }
     }
     best = wave_min_u64(best);
@@ -1105,6 +1138,12 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
 // exactly as before (sel_big).
 constexpr int kPickCap = 2048;
 constexpr int kPickWaves = 4;
+#ifdef LOAM_EXP_PICKW3
+constexpr int kPickWpe = 3;
+#else
+constexpr int kPickWpe = 4;  // <= 128 VGPRs: four waves per SIMD (the LDS allows four workgroups per CU)
+#endif
+constexpr int kPickSegRegs = (kPickCap / 6 + 2 + 63) / 64;  // a segment of a <= kPickCap ring, per lane
 
 struct PickWave {
   uint8_t pk[kPickCap + 16];
@@ -1148,7 +1187,7 @@ LOAM_D int sweep_route(const SrBuffers& b, int s, int R, int n, int cap, int* se
   return next;
 }
 
-__global__ __launch_bounds__(64 * kPickWaves) void k_sr_pick(SrBuffers b, SrParams p) {
+__global__ __launch_bounds__(64 * kPickWaves) __attribute__((amdgpu_waves_per_eu(kPickWpe))) void k_sr_pick(SrBuffers b, SrParams p) {
   const int s = blockIdx.y, tid = threadIdx.x, w = tid >> 6, lane = lane_id(), R = p.R;
   const int q = blockIdx.x * kPickWaves + w;
   __shared__ int se[128], order[64], sh_route;
@@ -1187,8 +1226,13 @@ __global__ __launch_bounds__(64 * kPickWaves) void k_sr_pick(SrBuffers b, SrPara
   for (int j = 0; j < 6; ++j) {
     const int s0 = (sq * (6 - j) + eq * j) / 6, s1 = (sq * (5 - j) + eq * (j + 1)) / 6;  // sp_j, ep_j + 1
     if (s1 - 1 < s0) continue;
+#ifdef LOAM_EXP_PICKG
     select_segment_fast(n, lo, s0 - lo, s1 - 1 - lo, cv, P.list, P.pk, P.lab, wlo, P.picks, P.nsharp, P.nlsharp,
                         P.nflat);
+#else
+    select_segment_fast<kPickSegRegs>(n, lo, s0 - lo, s1 - 1 - lo, cv, P.list, P.pk, P.lab, wlo, P.picks, P.nsharp,
+                                      P.nlsharp, P.nflat);
+#endif
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
     // (:568-572) lessFlat candidates of this segment, in position order
