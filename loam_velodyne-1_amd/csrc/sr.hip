@@ -40,8 +40,16 @@ __device__ unsigned long long g_phase[8];
     atomicAdd(&g_phase[k], (unsigned long long)(now - ph_t));   \
     ph_t = now;                                                 \
   }
+// k_sr_pick phases per wave (select_segment_fast<SR > 0>, k_sr_pick)
+#define PPH(k)                                                          \
+  if (lane_id() == 0) {                                                 \
+    const long long now = clock64();                                    \
+    atomicAdd(&g_phase[k], (unsigned long long)(now - pph_t));          \
+    pph_t = now;                                                        \
+  }
 #else
 #define PH(k)
+#define PPH(k)
 #endif
 
 LOAM_D int ring_id(const SrParams& p, float angle) {
@@ -787,17 +795,23 @@ LOAM_D void mark_neighbours(int n, int ind, uint8_t* pk, int wlo) {
 // :476-522 sharp / less sharp and :524-566 flat, on the ring's curvatures cv and the LDS pick state.
 // SR > 0: the segment is at most 64 * SR points and its curvatures are read once into SR registers
 // per lane (the flat walk rescans them up to four times).
-template <int SR = 0>
+// crin: the caller's registers with cv[sp + 64 k + lane] (loaded ahead, during the previous segment).
+// pre(): called once the compaction has consumed crin (the caller issues its next loads there).
+struct NoPre {
+  LOAM_D void operator()() const {}
+};
+template <int SR = 0, typename Pre = NoPre>
 LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, uint64_t* list, uint8_t* pk,
-                                int8_t* lab, int wlo, int* picks, int& nsharp, int& nlsharp, int& nflat) {
+                                int8_t* lab, int wlo, int* picks, int& nsharp, int& nlsharp, int& nflat,
+                                const float* crin = nullptr, Pre pre = Pre()) {
   const int lane = lane_id();
+#ifdef LOAM_EXP_PHASES
+  long long pph_t = clock64();
+#endif
   float cr[SR > 0 ? SR : 1];
   if constexpr (SR > 0) {
 #pragma unroll
-    for (int k = 0; k < SR; ++k) {
-      const int t = sp + k * 64 + lane;
-      cr[k] = t <= ep ? cv[t] : 0.0f;
-    }
+    for (int k = 0; k < SR; ++k) cr[k] = crin[k];
   }
   // points with curvature > 0.1, as (curvature bits, position): ascending = the stable sort's order
   int m = 0;
@@ -819,9 +833,12 @@ LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, 
       m += __popcll(bm);
     }
   }
+  pre();
   __threadfence_block();
   __builtin_amdgcn_wave_barrier();
+  if constexpr (SR > 0) { PPH(0); }
   if (m > 1) wave_sort_u64(list, m);
+  if constexpr (SR > 0) { PPH(1); }
   int largest = 0;
   bool done = false;
   for (int base = m - 1; base >= 0 && !done; base -= 64) {  // from the largest curvature down
@@ -853,6 +870,7 @@ LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, 
       remaining &= ~((2ull << f) - 1ull);
     }
   }
+  if constexpr (SR > 0) { PPH(2); }
   // flat: the unmarked point of smallest (curvature, position) below 0.1, four times at most
   for (int smallest = 0;;) {
     uint64_t best = ~0ull;
@@ -887,6 +905,7 @@ LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, 
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
   }
+  if constexpr (SR > 0) { PPH(3); }
 }
 
 // ring sort key: segment (3 bits) | curvature bits (32) | position in the ring (29)
@@ -1154,7 +1173,9 @@ struct PickWave {
 };
 
 // the sweep's ring bounds (:392-393 fix-ups) into se[0..2R), and the selection route of the sweep
-// (0: rings independent and <= cap points, 1: k_sr_select<4096, 1>), by thread 0
+// (0: rings independent and <= cap points, 1: k_sr_select<4096, 1>), valid in thread 0.  Wave 0
+// evaluates the ordered walk below with a lane per ring: each active ring's predecessor in the
+// (start, ring) order is found by a max over the other lanes (no serial insertion sort).
 LOAM_D int sweep_route(const SrBuffers& b, int s, int R, int n, int cap, int* se, int* order) {
   const int tid = threadIdx.x;
   if (tid < R) {
@@ -1166,6 +1187,7 @@ LOAM_D int sweep_route(const SrBuffers& b, int s, int R, int n, int cap, int* se
   }
   __syncthreads();
   int next = 0;
+#ifdef LOAM_EXP_ROUTESER
   if (tid == 0) {
     // rings are independent when their active spans [start, end-1] are more than 5 points apart
     int wf = 1, prev_hi = -100000, maxspan = 0, na = 0;
@@ -1184,11 +1206,38 @@ LOAM_D int sweep_route(const SrBuffers& b, int s, int R, int n, int cap, int* se
     }
     if (n > 0 && (!wf || maxspan > cap)) next = 1;
   }
+#else
+  (void)order;
+  if (tid < 64) {  // R <= 64
+    const int r = tid;
+    const bool act = r < R && se[r] <= se[R + r] - 1;
+    const int lo = act ? se[r] : 0, hi = act ? se[R + r] - 1 : 0;
+    const uint64_t am = __ballot(act);
+    // predecessor of r in the insertion sort's order (start ascending, ring index on ties)
+    int pst = 0, pidx = -1, phi = -100000;  // -100000: the walk's initial prev_hi
+    for (int k = 0; k < R; ++k) {
+      const int ks = __shfl(lo, k, 64), kh = __shfl(hi, k, 64);
+      const bool before = (ks < lo || (ks == lo && k < r));
+      if (((am >> k) & 1) && before && (pidx < 0 || ks > pst || (ks == pst && k > pidx))) {
+        pst = ks;
+        pidx = k;
+        phi = kh;
+      }
+    }
+    const bool fail = act && (lo < 0 || hi >= n || lo - phi <= 5);
+    const int maxspan = wave_max_i(act ? hi - lo + 1 : 0);
+    const bool wf = __ballot(fail) == 0;
+    if (n > 0 && (!wf || maxspan > cap)) next = 1;
+  }
+#endif
   return next;
 }
 
 __global__ __launch_bounds__(64 * kPickWaves) __attribute__((amdgpu_waves_per_eu(kPickWpe))) void k_sr_pick(SrBuffers b, SrParams p) {
   const int s = blockIdx.y, tid = threadIdx.x, w = tid >> 6, lane = lane_id(), R = p.R;
+#ifdef LOAM_EXP_PHASES
+  long long pph_t = clock64();
+#endif
   const int q = blockIdx.x * kPickWaves + w;
   __shared__ int se[128], order[64], sh_route;
   __shared__ PickWave pw[kPickWaves];
@@ -1213,6 +1262,7 @@ __global__ __launch_bounds__(64 * kPickWaves) __attribute__((amdgpu_waves_per_eu
   }
   const int wlo = max(0, lo - 5), whi = min(n - 1, hi + 5);
   const uint8_t* pick_g = b.picked + (size_t)s * b.cap;
+  PPH(5);
   for (int k = wlo + lane; k <= whi; k += 64) {
     P.pk[k - wlo] = pick_g[k];
     P.lab[k - wlo] = 0;
@@ -1223,18 +1273,37 @@ __global__ __launch_bounds__(64 * kPickWaves) __attribute__((amdgpu_waves_per_eu
   const float* cv = b.curv + (size_t)s * b.cap + lo;
   uint16_t* cand = b.st_cand + (size_t)(s * R + q) * kRingCap;
   int run = 0;
+  PPH(6);
+  // each segment's curvatures are loaded while the previous segment is walked
+  float cra[kPickSegRegs], crb[kPickSegRegs];
+  auto load_seg = [&](int j, float* cr) {
+    const int s0 = (sq * (6 - j) + eq * j) / 6, s1 = (sq * (5 - j) + eq * (j + 1)) / 6;
+#pragma unroll
+    for (int k = 0; k < kPickSegRegs; ++k) {
+      const int t = s0 - lo + k * 64 + lane;
+      cr[k] = t <= s1 - 1 - lo ? cv[t] : 0.0f;
+    }
+  };
+  load_seg(0, cra);
   for (int j = 0; j < 6; ++j) {
     const int s0 = (sq * (6 - j) + eq * j) / 6, s1 = (sq * (5 - j) + eq * (j + 1)) / 6;  // sp_j, ep_j + 1
-    if (s1 - 1 < s0) continue;
+    auto pre = [&]() {
+      if (j < 5) load_seg(j + 1, crb);
+    };
+    if (s1 - 1 < s0) pre();
+    if (s1 - 1 >= s0) {
 #ifdef LOAM_EXP_PICKG
     select_segment_fast(n, lo, s0 - lo, s1 - 1 - lo, cv, P.list, P.pk, P.lab, wlo, P.picks, P.nsharp, P.nlsharp,
                         P.nflat);
 #else
     select_segment_fast<kPickSegRegs>(n, lo, s0 - lo, s1 - 1 - lo, cv, P.list, P.pk, P.lab, wlo, P.picks, P.nsharp,
-                                      P.nlsharp, P.nflat);
+                                      P.nlsharp, P.nflat, cra, pre);
 #endif
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
+#ifdef LOAM_EXP_PHASES
+    pph_t = clock64();
+#endif
     // (:568-572) lessFlat candidates of this segment, in position order
     for (int base = s0; base < s1; base += 64) {
       const int k = base + lane;
@@ -1243,6 +1312,10 @@ __global__ __launch_bounds__(64 * kPickWaves) __attribute__((amdgpu_waves_per_eu
       if (flag) cand[run + __popcll(m & lanemask_lt())] = (uint16_t)(k - lo);
       run += __popcll(m);
     }
+    PPH(4);
+    }
+#pragma unroll
+    for (int k = 0; k < kPickSegRegs; ++k) cra[k] = crb[k];
   }
   __threadfence_block();
   __builtin_amdgcn_wave_barrier();

@@ -16,6 +16,6 @@ eng.batch_run(); eng.sync()
 L.loam_debug_phases(arr)
 d = [x - y for x, y in zip(arr, a)]
 tot = sum(d)
-names = ["load+keys", "ring sort", "greedy+cand", "seq wb + vg bbox", "vg keys", "vg sort", "vg heads", "-"]
+names = ["pick: load+compact", "pick: sort", "pick: sharp walk", "pick: flat walk", "pick: candidates", "pick: setup route", "pick: setup pk window", "-"] if "--pick" in sys.argv else ["load+keys", "ring sort", "greedy+cand", "seq wb + vg bbox", "vg keys", "vg sort", "vg heads", "-"]
 for n, v in zip(names, d):
     print(f"{n:18s} {v:14d} {100.0 * v / max(tot, 1):6.1f}%")
