@@ -294,6 +294,7 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_keys(VgJob j) {
 template <int G>
 __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
   __shared__ int isc[24];
+  __shared__ int hpos[G == 64 ? 1 : G];  // the chunk's head positions (workgroup groups)
   VgGroup<G> grp;
   for (int s = grp.g; s < j.nseg; s += VgGroup<G>::stride()) {
     const int b0 = j.begin[s], b1 = j.end[s];
@@ -313,9 +314,28 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
       const int head = (t < b1 && (t == b0 || j.keys_alt[t - 1] != k)) ? 1 : 0;
       int tot;
       const int ex = grp.excl_scan(head, isc, tot);
+      // a run ends at the chunk's next head; only the chunk's last run reads on past the chunk
+      int nxt = -1;
+#ifndef LOAM_EXP_VGWHILE
+      if constexpr (G == 64) {
+        const uint64_t hm = __ballot(head);
+        const uint64_t after = grp.t == 63 ? 0ull : hm & (~0ull << (grp.t + 1));
+        if (after) nxt = base + __ffsll((unsigned long long)after) - 1;
+      } else {
+        if (head) hpos[ex] = t;
+        __syncthreads();
+        if (head && ex + 1 < tot) nxt = hpos[ex + 1];
+      }
+#endif
       if (head) {
-        int e = t + 1;
-        while (e < b1 && j.keys_alt[e] == k) ++e;
+        int e = nxt;
+        if (e < 0) {
+          e = min(base + G, b1);
+#ifdef LOAM_EXP_VGWHILE
+          e = t + 1;
+#endif
+          while (e < b1 && j.keys_alt[e] == k) ++e;
+        }
         float sx = 0, sy = 0, sz = 0, si = 0;
         for (int mm = t; mm < e; mm += 4) {  // four independent gathers in flight per step
           float4 a[4];
