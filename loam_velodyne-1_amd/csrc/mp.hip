@@ -295,7 +295,9 @@ template <int G>
 __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
   __shared__ int isc[24];
   __shared__ int hpos[G == 64 ? 1 : G];  // the chunk's head positions (workgroup groups)
+  __shared__ uint32_t cval[VgGroup<G>::NT];  // the chunk's sorted source indices, per group
   VgGroup<G> grp;
+  uint32_t* gval = cval + (threadIdx.x / G) * G;
   for (int s = grp.g; s < j.nseg; s += VgGroup<G>::stride()) {
     const int b0 = j.begin[s], b1 = j.end[s];
     if (b1 <= b0) {
@@ -313,7 +315,14 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
       const uint32_t k = t < b1 ? j.keys_alt[t] : 0u;
       const int head = (t < b1 && (t == b0 || j.keys_alt[t - 1] != k)) ? 1 : 0;
       int tot;
-      const int ex = grp.excl_scan(head, isc, tot);
+#ifndef LOAM_EXP_VGNOCVAL
+      gval[grp.t] = t < b1 ? j.vals_alt[t] : 0u;  // coalesced; read back by the run heads
+      if constexpr (G == 64) {
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+      }
+#endif
+      const int ex = grp.excl_scan(head, isc, tot);  // (its barrier / wave sync publishes gval)
       // a run ends at the chunk's next head; only the chunk's last run reads on past the chunk
       int nxt = -1;
 #ifndef LOAM_EXP_VGWHILE
@@ -340,7 +349,14 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
         for (int mm = t; mm < e; mm += 4) {  // four independent gathers in flight per step
           float4 a[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) a[u] = j.in[j.vals_alt[min(mm + u, e - 1)]];
+          for (int u = 0; u < 4; ++u) {
+            const int m = min(mm + u, e - 1);
+#ifdef LOAM_EXP_VGNOCVAL
+            a[u] = j.in[j.vals_alt[m]];
+#else
+            a[u] = j.in[m < base + G ? gval[m - base] : j.vals_alt[m]];
+#endif
+          }
 #pragma unroll
           for (int u = 0; u < 4; ++u)
             if (mm + u < e) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
@@ -349,6 +365,12 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
         j.out[b0 + run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
       }
       run += tot;
+      if constexpr (G == 64) {  // gval / hpos are rewritten by the next chunk
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+      } else {
+        __syncthreads();
+      }
     }
     if (grp.t == 0) j.out_count[s] = run;
   }
