@@ -1031,9 +1031,11 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
     }
   }
   __syncthreads();
-  // per-kind exclusive prefix over the cube slots
+  // exclusive prefix over (kind, cube slot), kind-major: each thread owns a contiguous run of the
+  // flattened counts (one block scan instead of one per 256 slots); offsets replace the counts in LDS
   int* ac = b.app_cnt + (size_t)p * kCubeNum * 2;
   int* ao = b.app_off + (size_t)p * kCubeNum * 2;
+#ifdef LOAM_EXP_INSSCAN
   int run = 0;
   for (int kind = 0; kind < 2; ++kind)
     for (int base = 0; base < kCubeNum; base += kMpThreads) {
@@ -1044,6 +1046,34 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
       if (s < kCubeNum) { ac[s * 2 + kind] = c; ao[s * 2 + kind] = run + ex; }
       run += tot;
     }
+#else
+  {
+    constexpr int kFlat = 2 * kCubeNum, kPer = (kFlat + kMpThreads - 1) / kMpThreads;
+    int* cf = &cnt[0][0];
+    int sum = 0;
+    for (int k = 0; k < kPer; ++k) {
+      const int i = tid * kPer + k;
+      if (i < kFlat) sum += cf[i];
+    }
+    int tot;
+    int run = block_excl_scan<kMpThreads>(sum, scratch, tot);
+    for (int k = 0; k < kPer; ++k) {
+      const int i = tid * kPer + k;
+      if (i < kFlat) {
+        const int c = cf[i];
+        cf[i] = run;
+        run += c;
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < kFlat; i += kMpThreads) {
+      const int kind = i / kCubeNum, s = i % kCubeNum;
+      const int o = cf[i], nx = i + 1 < kFlat ? cf[i + 1] : tot;
+      ac[s * 2 + kind] = nx - o;
+      ao[s * 2 + kind] = o;
+    }
+  }
+#endif
   __threadfence_block();
   __syncthreads();
   float4* app = b.app + (size_t)p * b.cap_stack;
