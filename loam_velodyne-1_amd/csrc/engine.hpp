@@ -21,6 +21,7 @@ enum : int {
   ERR_EMPTY = 4,        // no finite input point
   ERR_CAP_MAP = 8,      // map store overflow
   ERR_CAP_STACK = 16,   // stack / FromMap capacity
+  ERR_VG_BITS = 32,     // a VoxelGrid segment's voxel keys exceed the bits its sort was given
 };
 
 constexpr int kSrThreads = 512;     // ring-sort workgroup (one per sweep)

@@ -260,6 +260,9 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_params(VgJob j) {
       prm[0] = minb[0]; prm[1] = minb[1]; prm[2] = minb[2];
       prm[3] = divx; prm[4] = divx * divy;
       prm[5] = (dx * dy * dz > (int64_t)0x7fffffff) ? 1 : 0;
+      const int64_t divz = (int64_t)(maxb[2] - minb[2] + 1);
+      if (!prm[5] && j.end_bit < 32 && (int64_t)divx * divy * divz > ((int64_t)1 << j.end_bit) && j.err)
+        atomicOr(&j.err[(s / j.seg_per_err) * j.err_stride], ERR_VG_BITS);
     }
   }
 }
@@ -513,7 +516,7 @@ void vg_run(const VgJob& j0, void* tmp, size_t tmp_bytes, hipStream_t st, int G,
   else vg_launch_params_keys<1024>(j, st);
   size_t bytes = tmp_bytes;
   (void)hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
-                                                    j.nseg, j.begin, j.end, 0, 32, st);
+                                                    j.nseg, j.begin, j.end, 0, j.end_bit, st);
   if (G == 64) vg_launch_reduce<64>(j, st);
   else if (G == 256) vg_launch_reduce<256>(j, st);
   else vg_launch_reduce<1024>(j, st);
@@ -1393,6 +1396,11 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   jv.in = b.vin; jv.out = b.vout; jv.begin = b.vseg_b; jv.end = b.vseg_e; jv.leaf = b.vseg_leaf;
   jv.out_count = b.vseg_cnt; jv.params = b.vg_params; jv.keys = b.vg_k; jv.keys_alt = b.vg_k2;
   jv.vals = b.vg_v; jv.vals_alt = b.vg_v2; jv.big_b = b.vg_bb; jv.big_e = b.vg_be; jv.nseg = 2 * kMaxValid * P; jv.total = P * b.map_cap;
+  // a cube spans at most 50 m: <= 252 voxels of 0.2 m per axis, keys below 2^24 (three 8-bit passes)
+#ifndef LOAM_EXP_CUBE32
+  jv.end_bit = 24;
+#endif
+  jv.err = b.istate + kMiErr; jv.err_stride = kMpStateInts; jv.seg_per_err = 2 * kMaxValid;
   vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 256 : 64, P <= 4 || kVgFusedBatch ? kVgCubeCap : 0);    // 2 x 125 cube segments per instance
   mark("vg_cubes");
   hipLaunchKernelGGL(k_mp_compact_table, dim3(P), dim3(kMpThreads), 0, st, b);

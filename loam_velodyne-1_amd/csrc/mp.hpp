@@ -47,6 +47,9 @@ struct VgJob {
   int* big_b = nullptr;  // [nseg] segments beyond the fused kernel's LDS capacity (else empty),
   int* big_e = nullptr;  //        finished by the multi-kernel path
   int keep_counts = 0;   // multi-kernel path over big_b/big_e: leave other segments' counts alone
+  int end_bit = 32;      // voxel key bits the multi-kernel sort orders; a segment whose key range
+  int* err = nullptr;    //   exceeds it raises ERR_VG_BITS in err[(s / seg_per_err) * err_stride]
+  int err_stride = 0, seg_per_err = 1;
 };
 
 struct MpBuffers {
