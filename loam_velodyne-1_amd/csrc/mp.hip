@@ -233,7 +233,10 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_params(VgJob j) {
     const int b0 = j.begin[s], b1 = j.end[s];
     int* prm = j.params + (size_t)s * 8;
     if (b1 <= b0) {
-      if (grp.t == 0) prm[5] = 0;
+      if (grp.t == 0) {
+        prm[5] = 0;
+        if (j.sb24) { j.sb24[s] = 0; j.se24[s] = 0; j.sb32[s] = 0; j.se32[s] = 0; }
+      }
       continue;
     }
     float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
@@ -263,6 +266,11 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_params(VgJob j) {
       const int64_t divz = (int64_t)(maxb[2] - minb[2] + 1);
       if (!prm[5] && j.end_bit < 32 && (int64_t)divx * divy * divz > ((int64_t)1 << j.end_bit) && j.err)
         atomicOr(&j.err[(s / j.seg_per_err) * j.err_stride], ERR_VG_BITS);
+      if (j.sb24) {
+        const bool fits = prm[5] || (int64_t)divx * divy * divz <= ((int64_t)1 << 24);
+        j.sb24[s] = fits ? b0 : 0; j.se24[s] = fits ? b1 : 0;
+        j.sb32[s] = fits ? 0 : b0; j.se32[s] = fits ? 0 : b1;
+      }
     }
   }
 }
@@ -515,8 +523,16 @@ void vg_run(const VgJob& j0, void* tmp, size_t tmp_bytes, hipStream_t st, int G,
   else if (G == 256) vg_launch_params_keys<256>(j, st);
   else vg_launch_params_keys<1024>(j, st);
   size_t bytes = tmp_bytes;
-  (void)hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
-                                                    j.nseg, j.begin, j.end, 0, j.end_bit, st);
+  if (j.sb24) {
+    (void)hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
+                                                      j.nseg, j.sb24, j.se24, 0, 24, st);
+    bytes = tmp_bytes;
+    (void)hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
+                                                      j.nseg, j.sb32, j.se32, 0, 32, st);
+  } else {
+    (void)hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
+                                                      j.nseg, j.begin, j.end, 0, j.end_bit, st);
+  }
   if (G == 64) vg_launch_reduce<64>(j, st);
   else if (G == 256) vg_launch_reduce<256>(j, st);
   else vg_launch_reduce<1024>(j, st);
@@ -1308,6 +1324,7 @@ void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter
   (void)hipMalloc(&b.vg_v, vgn * sizeof(uint32_t));
   (void)hipMalloc(&b.vg_v2, vgn * sizeof(uint32_t));
   (void)hipMalloc(&b.vg_bb, (size_t)P * 2 * kMaxValid * sizeof(int));
+  (void)hipMalloc(&b.vg_split, (size_t)4 * P * 2 * kMaxValid * sizeof(int));
   (void)hipMalloc(&b.vg_be, (size_t)P * 2 * kMaxValid * sizeof(int));
   const size_t t1 = vg_tmp_bytes((int)vgn, P * 2 * kMaxValid), t2 = vg_tmp_bytes((int)Ps, P * 2);
   b.cub_bytes = t1 > t2 ? t1 : t2;
@@ -1323,7 +1340,7 @@ void mp_free(MpBuffers& b) {
                   b.stack2, b.stack, b.nstack, b.from, b.hC_start, b.hS_start, b.h_fill, b.hC_T, b.hS_T,
                   b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.citems, b.nitems, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
-                  b.vg_params, b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_bb, b.vg_be, b.cub_tmp, b.reg, b.nreg};
+                  b.vg_params, b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_bb, b.vg_be, b.vg_split, b.cub_tmp, b.reg, b.nreg};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = MpBuffers();
@@ -1355,6 +1372,12 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   js.in = b.stack2; js.out = b.stack; js.begin = b.sseg_b; js.end = b.sseg_e; js.leaf = b.sseg_leaf;
   js.out_count = b.sseg_cnt; js.params = b.vg_params; js.keys = b.vg_k; js.keys_alt = b.vg_k2;
   js.vals = b.vg_v; js.vals_alt = b.vg_v2; js.big_b = b.vg_bb; js.big_e = b.vg_be; js.nseg = 2 * P; js.total = P * b.cap_stack;
+#ifndef LOAM_EXP_STACK32
+  if (P > 4) {  // batches: segments whose keys fit 24 bits sort in three passes, the rest in four
+    const size_t ns = (size_t)P * 2 * kMaxValid;
+    js.sb24 = b.vg_split; js.se24 = b.vg_split + ns; js.sb32 = b.vg_split + 2 * ns; js.se32 = b.vg_split + 3 * ns;
+  }
+#endif
   vg_run(js, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 1024 : 256, P <= 4 || kVgFusedBatch ? 12288 : 0);  // two large segments per instance
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);

@@ -50,6 +50,9 @@ struct VgJob {
   int end_bit = 32;      // voxel key bits the multi-kernel sort orders; a segment whose key range
   int* err = nullptr;    //   exceeds it raises ERR_VG_BITS in err[(s / seg_per_err) * err_stride]
   int err_stride = 0, seg_per_err = 1;
+  // split sort (when set): k_vg_params lists each segment in sb24/se24 when its keys fit 24 bits,
+  // else in sb32/se32; vg_run sorts the two lists separately (three / four 8-bit passes)
+  int *sb24 = nullptr, *se24 = nullptr, *sb32 = nullptr, *se32 = nullptr;
 };
 
 struct MpBuffers {
@@ -94,6 +97,7 @@ struct MpBuffers {
   int* vg_params = nullptr;
   uint32_t *vg_k = nullptr, *vg_k2 = nullptr, *vg_v = nullptr, *vg_v2 = nullptr;
   int *vg_bb = nullptr, *vg_be = nullptr;  // [P][2][kMaxValid] big-segment ranges of vg_run
+  int* vg_split = nullptr;                 // [4][P][2][kMaxValid] split-sort segment lists of vg_run
   void* cub_tmp = nullptr;
   size_t cub_bytes = 0;
   float4* reg = nullptr;      // [P][capS] registered full cloud

@@ -248,6 +248,41 @@ def test_batch_mapping_parity_64(loam, oc, sg):
     np.testing.assert_array_equal(aft, aft2)
 
 
+def _push_out(raw, rng_m=250.0, az_deg=(0.0, 12.0)):
+    """top-ring returns within an azimuth block moved out to rng_m metres along their rays"""
+    raw = raw.copy()
+    h = np.hypot(raw[:, 0], raw[:, 1])
+    el = np.degrees(np.arctan2(raw[:, 2], h))
+    az = np.degrees(np.arctan2(raw[:, 1], raw[:, 0])) % 360.0
+    sel = (el > 14.0) & (az >= az_deg[0]) & (az < az_deg[1])
+    r = np.linalg.norm(raw[sel, :3], axis=1, keepdims=True)
+    raw[sel, :3] = (raw[sel, :3] / r * rng_m).astype(np.float32)
+    return raw, int(sel.sum())
+
+
+def test_batch_stack_keys_beyond_24_bits(loam, oc, sg):
+    """Batch mapping with stacks whose 0.4 m VoxelGrid spans more than 2^24 voxels (far returns on
+    the top ring): those segments take vg_run's 32-bit sort list, the others the 24-bit one."""
+    prevs, curs = sg.batch_problems(8, base_seed=1300)
+    for i in (0, 3, 6):
+        prevs[i], n0 = _push_out(prevs[i])
+        curs[i], n1 = _push_out(curs[i])
+        assert n0 > 20 and n1 > 20
+    o = oc.Oracle(oc.default_config(system_delay=1))
+    o.scan_registration(curs[0])
+    _, f = o.scan_registration(curs[0])
+    lf = f["less_flat"][:, :3]
+    ext = np.floor(lf.max(axis=0) / 0.4) - np.floor(lf.min(axis=0) / 0.4) + 1
+    assert np.prod(ext) > 2 ** 25, ext
+    e = loam.Engine()
+    e.batch_upload(prevs, curs)
+    e.batch_run()
+    od, aft, _ = e.batch_download()
+    for i in range(8):
+        od_o, aft_o, _ = oc.problem(prevs[i], curs[i])
+        assert max(np.abs(od[i] - od_o).max(), np.abs(aft[i] - aft_o).max()) <= POSE_TOL, i
+
+
 def test_hdl64_problem_config5(loam, oc, sg):
     prev, cur = sg.single_problem(2, lidar=sg.HDL64)
     kw = dict(n_rings=64, ring_model=loam.RING_LINEAR, max_points=160000)
