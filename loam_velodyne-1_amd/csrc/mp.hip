@@ -922,9 +922,27 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
   double acc[28];
 #pragma unroll
   for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+#ifdef LOAM_EXP_ITERSER
   for (int q = tid; q < nq; q += kMpThreads) {  // :897-921
     if (!qok[q]) continue;
     const float4 o = stack[q < nsc ? q : b.capC + (q - nsc)], c = qcf[q];
+#else
+  // four rows' loads in flight per step; the rows are still summed in the lane's q order
+  for (int q0 = tid; q0 < nq; q0 += 4 * kMpThreads) {  // :897-921
+    int8_t okv[4];
+    float4 ov[4], cv4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = q0 + u * kMpThreads;
+      okv[u] = q < nq ? qok[q] : (int8_t)0;
+      ov[u] = q < nq ? stack[q < nsc ? q : b.capC + (q - nsc)] : make_float4(0, 0, 0, 0);
+      cv4[u] = q < nq ? qcf[q] : make_float4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+    if (!okv[u]) continue;
+    const float4 o = ov[u], c = cv4[u];
+#endif
     float a[6];
     a[0] = (crx * sry * srz * o.x + crx * crz * sry * o.y - srx * sry * o.z) * c.x +
            (-srx * srz * o.x - crz * srx * o.y - crx * o.z) * c.y +
@@ -947,6 +965,9 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
     for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
     acc[27] += 1.0;
   }
+#ifndef LOAM_EXP_ITERSER
+  }
+#endif
   wave_reduce_scatter_28(acc);  // lanes 2v, 2v+1: the wave sum of value v
   if ((lane & 1) == 0 && (lane >> 1) < 28) sh.red[w][lane >> 1] = acc[0];
   __syncthreads();

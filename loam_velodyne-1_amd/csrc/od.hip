@@ -643,9 +643,21 @@ __global__ __launch_bounds__(64) void k_od_step(OdBuffers b, int iter, int gq) {
   __shared__ double tot[28];
   __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs];
   __shared__ int lm_iws[12];
-  if (lane < 28) {
+  if (lane < 28) {  // fixed order over the workgroups; eight partials in flight per step
     double v = 0.0;
+#ifdef LOAM_EXP_PARTSER
     for (int g = 0; g < gq; ++g) v += b.part[((size_t)p * b.gq + g) * 28 + lane];
+#else
+    const double* pp = b.part + (size_t)p * b.gq * 28 + lane;
+    for (int g = 0; g < gq; g += 8) {
+      double t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = g + u < gq ? pp[(size_t)(g + u) * 28] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (g + u < gq) v += t[u];
+    }
+#endif
     tot[lane] = v;
   }
   __syncthreads();
