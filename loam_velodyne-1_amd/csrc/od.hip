@@ -478,8 +478,9 @@ LOAM_D void od_step(const OdBuffers& b, int p, int iter, const double* tot, floa
 // of iterations 0..iter, all evaluated at the current transform, :708-764) summed in fp64 into
 // this workgroup's partial JᵀJ / Jᵀb / row count.  A rejected correspondence is stored as a zero
 // coefficient, which adds exact zeros.
+constexpr int kOdRowsWpe = 4;  // <= 128 VGPRs with two rows' loads in flight
 template <bool FUSED>
-__global__ __launch_bounds__(kOdThreads) void k_od_rows(OdBuffers b, FeatView f, int last_buf, int iter) {
+__global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdRowsWpe))) void k_od_rows(OdBuffers b, FeatView f, int last_buf, int iter) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const int* ist = b.istate + (size_t)p * kOdStateInts;
@@ -579,9 +580,28 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows(OdBuffers b, FeatView f,
     const float e30 = -sw * (cry * crz - srx * sry * srz), e31 = sw * crx * srz, e32 = sw * (crz * sry + cry * srx * srz);
     const float e40 = -sw * (cry * srz + crz * srx * sry), e41 = sw * crx * crz, e42 = sw * (sry * srz - cry * crz * srx);
     const float e50 = sw * crx * sry, e51 = sw * srx, e52 = sw * crx * cry;
+#ifdef LOAM_EXP_ROWSEQ
     for (int it = 0; it <= iter; ++it) {
       // a rejected correspondence has a zero coefficient and adds exact zeros
       const float4 c4 = qcf[(size_t)it * b.cap_q + q];
+      const bool okit = qok[(size_t)it * b.cap_q + q] != 0;
+#else
+    // the stored rows two iterations at a time (their loads in flight together), summed in order
+    for (int it0 = 0; it0 <= iter; it0 += 2) {
+      float4 cv4[2];
+      bool okv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int it = it0 + u;
+        cv4[u] = it <= iter ? qcf[(size_t)it * b.cap_q + q] : make_float4(0, 0, 0, 0);
+        okv[u] = it <= iter ? qok[(size_t)it * b.cap_q + q] != 0 : false;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+      if (it0 + u > iter) break;
+      const float4 c4 = cv4[u];
+      const bool okit = okv[u];
+#endif
       float a[6];
       a[0] = e00 * c4.x + e01 * c4.y + e02 * c4.z;
       a[1] = e10 * c4.x + e12 * c4.z;
@@ -597,8 +617,11 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows(OdBuffers b, FeatView f,
         for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
 #pragma unroll
       for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
-      acc[27] += qok[(size_t)it * b.cap_q + q] ? 1.0 : 0.0;
+      acc[27] += okit ? 1.0 : 0.0;
     }
+#ifndef LOAM_EXP_ROWSEQ
+    }
+#endif
   }
   // wave sums of the 28 values as a butterfly reduce-scatter (32 slots halved per step: 32
   // shuffles instead of 28 x 6); lanes 2v, 2v+1 end with the sum of value v
