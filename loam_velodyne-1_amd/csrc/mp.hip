@@ -480,15 +480,20 @@ __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
   }
 }
 
+#ifdef LOAM_EXP_VGGRID4K
+constexpr int kVgGridCap = 4096;
+#else
+constexpr int kVgGridCap = 16384;  // measured: 4096 / 16384 / 65536 within 0.5% of each other, 16384 best
+#endif
 template <int G>
 void vg_launch_params_keys(const VgJob& j, hipStream_t st) {
-  const int grid = std::min((j.nseg + VgGroup<G>::NT / G - 1) / (VgGroup<G>::NT / G), 4096);
+  const int grid = std::min((j.nseg + VgGroup<G>::NT / G - 1) / (VgGroup<G>::NT / G), kVgGridCap);
   hipLaunchKernelGGL(k_vg_params<G>, dim3(grid), dim3(VgGroup<G>::NT), 0, st, j);
   hipLaunchKernelGGL(k_vg_keys<G>, dim3(grid), dim3(VgGroup<G>::NT), 0, st, j);
 }
 template <int G>
 void vg_launch_reduce(const VgJob& j, hipStream_t st) {
-  const int grid = std::min((j.nseg + VgGroup<G>::NT / G - 1) / (VgGroup<G>::NT / G), 4096);
+  const int grid = std::min((j.nseg + VgGroup<G>::NT / G - 1) / (VgGroup<G>::NT / G), kVgGridCap);
   hipLaunchKernelGGL(k_vg_reduce<G>, dim3(grid), dim3(VgGroup<G>::NT), 0, st, j);
 }
 
@@ -507,6 +512,11 @@ constexpr bool kVgFusedBatch = false;
 constexpr int kVgCubeCap = 2048;
 #else
 constexpr int kVgCubeCap = 12288;
+#endif
+#ifdef LOAM_EXP_CUBEG64
+constexpr bool kVgCubeG256 = false;
+#else
+constexpr bool kVgCubeG256 = true;  // a workgroup per cube segment also in batches: a few large cubes dominate
 #endif
 void vg_run(const VgJob& j0, void* tmp, size_t tmp_bytes, hipStream_t st, int G, int fcap) {
   if (j0.nseg == 0) return;
@@ -1445,7 +1455,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   jv.end_bit = 24;
 #endif
   jv.err = b.istate + kMiErr; jv.err_stride = kMpStateInts; jv.seg_per_err = 2 * kMaxValid;
-  vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 256 : 64, P <= 4 || kVgFusedBatch ? kVgCubeCap : 0);    // 2 x 125 cube segments per instance
+  vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 || kVgCubeG256 ? 256 : 64, P <= 4 || kVgFusedBatch ? kVgCubeCap : 0);    // 2 x 125 cube segments per instance
   mark("vg_cubes");
   hipLaunchKernelGGL(k_mp_compact_table, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);
