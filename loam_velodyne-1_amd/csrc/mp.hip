@@ -648,6 +648,13 @@ constexpr int kMpQueryThreads = 256;
 // iterates max(candidates per lane) instead of the union of its lanes' cells x buckets.  `lst` =
 // the lane's LDS column (stride kMpQueryThreads).  Ranges are packed start:19 | count:13; a lane
 // whose ranges do not fit falls back to knn5.
+#if defined(LOAM_EXP_NNG4)
+constexpr int kNnInFlight = 4;
+#elif defined(LOAM_EXP_NNG16)
+constexpr int kNnInFlight = 16;
+#else
+constexpr int kNnInFlight = 8;  // measured k_mp_nn ms/step: 2 -> 4.17, 4 -> 3.95, 8 -> 3.88, 16 -> 5.33
+#endif
 LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5& t, uint32_t* lst) {
   if (T <= 0) return;
   const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
@@ -690,15 +697,15 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
     --left;
     return pos++;
   };
-  for (int k = 0; k < total; k += 4) {  // four independent gathers in flight per step
-    int idx[4];
+  for (int k = 0; k < total; k += kNnInFlight) {  // independent gathers in flight per step
+    int idx[kNnInFlight];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) idx[u] = k + u < total ? next() : idx[0];
-    float4 a[4];
+    for (int u = 0; u < kNnInFlight; ++u) idx[u] = k + u < total ? next() : idx[0];
+    float4 a[kNnInFlight];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) a[u] = hp[idx[u]];
+    for (int u = 0; u < kNnInFlight; ++u) a[u] = hp[idx[u]];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < kNnInFlight; ++u)
       if (k + u < total) top5_offer(t, sqdist(a[u].x, a[u].y, a[u].z, q.x, q.y, q.z), __builtin_bit_cast(int, a[u].w));
   }
 }
