@@ -98,6 +98,12 @@ typedef struct {
   uint64_t od_row_evals;                        /* Jacobian rows evaluated: sum of queries x it(it+1)/2 (Q12) */
   uint64_t bytes_sr, bytes_od, bytes_mp;        /* algorithmic bytes, SURVEY.md §8(d) */
   double ms_sr, ms_od, ms_mp;                   /* device time per stage (HIP events) */
+  /* reference branches taken (batch: summed over problems) */
+  uint64_t od_degenerate_steps; /* odometry L-M updates projected by the iteration-0 degeneracy
+                                   analysis (src/laserOdometry.cpp:770-797, Q15) */
+  uint64_t od_nan_skips;        /* odometry L-M updates skipped by the NaN guard (:799-811, Q16) */
+  uint64_t mp_degenerate_steps; /* mapping L-M updates projected (src/laserMapping.cpp:927-954) */
+  uint64_t mp_grid_shifts;      /* cube-grid slab shifts of the recentring (:454-614, Q23) */
 } loam_stats;
 
 typedef struct loam_ctx loam_ctx;

@@ -52,15 +52,11 @@ LOAM_D uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 // placement only, never correctness.
 struct XcdBlock { int x, y; };
 LOAM_D XcdBlock xcd_block() {
-#ifdef LOAM_EXP_NOXCD
-  return {(int)blockIdx.x, (int)blockIdx.y};
-#else
   const int gx = gridDim.x, total = gx * gridDim.y;
   const int L = blockIdx.x + blockIdx.y * gx;
   const int x8 = L & 7, i = L >> 3, q = total >> 3, r = total & 7;
   const int logical = x8 < r ? x8 * (q + 1) + i : r * (q + 1) + (x8 - r) * q + i;
   return {logical % gx, logical / gx};
-#endif
 }
 
 template <typename T>

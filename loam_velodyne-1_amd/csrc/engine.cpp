@@ -72,7 +72,7 @@ struct loam_ctx {
   SrBuffers odin;       // odometry input feature set (host topics uploaded here)
   OdBuffers od1;        // one odometry problem
   bool od_inited = false;
-  int od_last = 0, od_frame_count = 1;
+  int od_last = 0, od_frame_count = 1;  // frameCount = skipFrameNum (src/laserOdometry.cpp:407)
   MpBuffers mp1;        // streaming map
   int map_frame_count = 4;    // mapFrameCount = mapFrameNum - 1 (src/laserMapping.cpp:405)
   bool surround_due = false;  // the last loam_mapping frame publishes /laser_cloud_surround
@@ -100,7 +100,7 @@ namespace {
 int check_cloud_in(const loam_cloud_in& c, int cap) {
   if (c.count > 0 && c.data == nullptr) return fail(LOAM_E_INVAL, "cloud data is null");
   if (c.stride_bytes < 12 || c.stride_bytes % 4 != 0) return fail(LOAM_E_INVAL, "bad stride_bytes");
-  if ((int)c.count > cap) return fail(LOAM_E_CAPACITY, "cloud exceeds max_points");
+  if (c.count > (uint32_t)cap) return fail(LOAM_E_CAPACITY, "cloud exceeds max_points");
   return LOAM_OK;
 }
 
@@ -189,6 +189,9 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   if (c.max_points < 64 || c.max_points > (1u << 22)) return fail(LOAM_E_INVAL, "bad max_points");
   if (c.od_max_iter < 1 || c.od_max_iter > 1000 || c.mp_max_iter < 1 || c.mp_max_iter > 1000)
     return fail(LOAM_E_INVAL, "bad iteration limits");
+  if (c.map_capacity < 1024 || c.map_capacity > (1u << 28))
+    return fail(LOAM_E_INVAL, "map_capacity must be in [1024, 2^28] points");
+  if (c.skip_frame_num > (1u << 20)) return fail(LOAM_E_INVAL, "bad skip_frame_num");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return fail(LOAM_E_HIP, "no HIP device available (the engine has no CPU fallback)");
@@ -199,28 +202,37 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   x->device = device;
   x->R = (int)c.n_rings;
   x->cap = (int)c.max_points;
+  x->od_frame_count = (int)c.skip_frame_num;
   std::memset(&x->stats, 0, sizeof(x->stats));
   if (hipStreamCreateWithFlags(&x->st, hipStreamNonBlocking) != hipSuccess) {
     delete x;
     return fail(LOAM_E_HIP, "hipStreamCreate failed");
   }
-  for (auto& e : x->ev) (void)hipEventCreate(&e);
-  if (hipStreamCreateWithFlags(&x->st2, hipStreamNonBlocking) != hipSuccess) x->st2 = nullptr;
-  (void)hipEventCreateWithFlags(&x->fork, hipEventDisableTiming);
-  (void)hipEventCreateWithFlags(&x->join, hipEventDisableTiming);
-  sr_alloc(x->sr1, 1, x->cap, x->R);
-  sr_alloc(x->odin, 1, x->cap, x->R);
-  od_alloc(x->od1, 1, x->R, x->cap, (int)c.od_max_iter);
-  mp_alloc(x->mp1, 1, x->R, x->cap, (int)c.map_capacity, (int)c.mp_max_iter);
+  hipError_t he = hipSuccess;
+  for (auto& e : x->ev)
+    if (he == hipSuccess) he = hipEventCreate(&e);
+  if (he == hipSuccess && hipStreamCreateWithFlags(&x->st2, hipStreamNonBlocking) != hipSuccess) x->st2 = nullptr;
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&x->fork, hipEventDisableTiming);
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&x->join, hipEventDisableTiming);
+  if (he != hipSuccess) {
+    loam_destroy(x);
+    return fail(LOAM_E_HIP, std::string("event creation failed: ") + hipGetErrorString(he));
+  }
+  if (he == hipSuccess) he = sr_alloc(x->sr1, 1, x->cap, x->R);
+  if (he == hipSuccess) he = sr_alloc(x->odin, 1, x->cap, x->R);
+  if (he == hipSuccess) he = od_alloc(x->od1, 1, x->R, x->cap, (int)c.od_max_iter);
+  if (he == hipSuccess) he = mp_alloc(x->mp1, 1, x->R, x->cap, (int)c.map_capacity, (int)c.mp_max_iter);
+  if (he == hipSuccess) he = hipMalloc(&x->sr_imu_dev, sizeof(loamimu::SrQueue));
+  if (he != hipSuccess) x->sr_imu_dev = nullptr;
   x->sr_imu = new loamimu::SrQueue();
   std::memset(x->sr_imu, 0, sizeof(loamimu::SrQueue));
   x->sr_imu->last = -1;
   std::memset(&x->mp_imu, 0, sizeof(x->mp_imu));
   x->mp_imu.last = -1;
-  (void)hipMalloc(&x->sr_imu_dev, sizeof(loamimu::SrQueue));
-  if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess) {
+  if (he == hipSuccess) he = hipDeviceSynchronize();
+  if (he != hipSuccess) {
     loam_destroy(x);
-    return fail(LOAM_E_NOMEM, "device allocation failed");
+    return fail(LOAM_E_NOMEM, std::string("device allocation failed: ") + hipGetErrorString(he));
   }
   *out = x;
   return LOAM_OK;
@@ -419,6 +431,8 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
   x->stats.od_assoc_rounds = ist[kIsAssoc];
   x->stats.od_rows_sum = (uint64_t)ist[kIsRows];
   x->stats.od_queries = ist[kIsQueries];
+  x->stats.od_degenerate_steps = (uint64_t)ist[kIsDegSteps];
+  x->stats.od_nan_skips = (uint64_t)ist[kIsNanSkips];
   {
     const uint64_t nq = ist[kIsAssoc] ? (uint64_t)(ist[kIsQueries] / ist[kIsAssoc]) : 0, it = (uint64_t)ist[kIsIters];
     x->stats.od_query_iters = nq * it;
@@ -506,15 +520,22 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
   }
   if ((int)n != x->P) {
     HIP_TRY(hipStreamSynchronize(x->st));
+    if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
     sr_free(x->srb);
     od_free(x->odb);
     mp_free(x->mpb);
+    x->P = 0;  // no batch until every buffer of the new size exists
+    hipError_t he = sr_alloc(x->srb, 2 * (int)n, x->cap, x->R);
+    if (he == hipSuccess) he = od_alloc(x->odb, (int)n, x->R, x->cap, (int)x->cfg.od_max_iter);
+    if (he == hipSuccess)
+      he = mp_alloc(x->mpb, (int)n, x->R, x->cap, mp_batch_map_capacity(x->cap), (int)x->cfg.mp_max_iter);
+    if (he != hipSuccess) {
+      sr_free(x->srb);
+      od_free(x->odb);
+      mp_free(x->mpb);
+      return fail(LOAM_E_NOMEM, std::string("batch allocation failed: ") + hipGetErrorString(he));
+    }
     x->P = (int)n;
-    sr_alloc(x->srb, 2 * x->P, x->cap, x->R);
-    od_alloc(x->odb, x->P, x->R, x->cap, (int)x->cfg.od_max_iter);
-    mp_alloc(x->mpb, x->P, x->R, x->cap, mp_batch_map_capacity(x->cap), (int)x->cfg.mp_max_iter);
-    HIP_TRY(hipDeviceSynchronize());
-    if (hipGetLastError() != hipSuccess) return fail(LOAM_E_NOMEM, "batch allocation failed");
   }
   std::vector<float4> h((size_t)x->cap);
   std::vector<int> counts(2 * n);
@@ -622,6 +643,8 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
     s.od_assoc_rounds += q[kIsAssoc];
     s.od_rows_sum += (uint64_t)q[kIsRows];
     s.od_queries += q[kIsQueries];
+    s.od_degenerate_steps += (uint64_t)q[kIsDegSteps];
+    s.od_nan_skips += (uint64_t)q[kIsNanSkips];
     const uint64_t nq = q[kIsAssoc] ? (uint64_t)(q[kIsQueries] / q[kIsAssoc]) : 0, it = (uint64_t)q[kIsIters];
     s.od_query_iters += nq * it;
     s.od_row_evals += nq * it * (it + 1) / 2;

@@ -77,10 +77,25 @@ struct SrParams {
   double time_scan = 0.0;           // timeScanCur: the sweep's stamp
 };
 
+// Device allocation of the *_alloc functions: every request goes through one DevAlloc, which
+// keeps the first failure and skips later requests (their pointers stay null), so an allocator
+// returns one error and its *_free releases whatever was obtained.
+struct DevAlloc {
+  hipError_t err = hipSuccess;
+  template <class T>
+  void operator()(T** p, size_t bytes) {
+    *p = nullptr;
+    if (err != hipSuccess) return;
+    void* q = nullptr;
+    err = hipMalloc(&q, bytes ? bytes : 16);
+    if (err == hipSuccess) *p = (T*)q;
+  }
+};
+
 // the thread-local message loam_last_error() returns (engine.cpp)
 void set_last_error(const std::string& msg);
 
-void sr_alloc(SrBuffers& b, int S, int cap, int R);
+hipError_t sr_alloc(SrBuffers& b, int S, int cap, int R);  // on failure: freed, b empty
 void sr_free(SrBuffers& b);
 // runs the whole scan registration for sweeps [0, S) already in b.raw / b.raw_n
 void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof = nullptr);

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_prepare(MpBuffers b, MpInput 
   float* st = b.state + (size_t)p * kMpStateFloats;
   int* ist = b.istate + (size_t)p * kMpStateInts;
   int* slots = slot_table(b, b.pool_cur, p);
-  __shared__ int sh_shift[256];
+  __shared__ int sh_shift[3], sh_count[3];
   __shared__ int sh_nshift, sh_c[3], sh_cen[3], sh_scan[16];
   if (tid == 0) {
     float pose[6] = {0, 0, 0, 0, 0, 0};
@@ -71,14 +71,30 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_prepare(MpBuffers b, MpInput 
     st[kMpOnY] = onY.x; st[kMpOnY + 1] = onY.y; st[kMpOnY + 2] = onY.z;
     int cW = ist[kMiCenW], cH = ist[kMiCenH], cD = ist[kMiCenD];
     int cI = cube_of(T[3], cW), cJ = cube_of(T[4], cH), cK = cube_of(T[5], cD);
+    // :454-614: each `while` moves the grid one slab per pass until the centre cube is >= 3 from
+    // the edge.  The pass counts are closed-form; a line of cubes shifted by its full length (or
+    // more) is entirely cleared, so at most that many slot-table shifts are replayed per axis
+    // while the centre indices take every pass (ist[kMiShifts] counts the reference's passes).
+    const int dim[3] = {kCubeW, kCubeH, kCubeD};
+    int* c[3] = {&cI, &cJ, &cK};
+    int* cen[3] = {&cW, &cH, &cD};
     int n = 0;
-    // encoded shift: axis * 2 + (dir > 0); bounded to the table size
-    while (cI < 3 && n < 255) { sh_shift[n++] = 0 * 2 + 1; cI++; cW++; }
-    while (cI >= kCubeW - 3 && n < 255) { sh_shift[n++] = 0 * 2 + 0; cI--; cW--; }
-    while (cJ < 3 && n < 255) { sh_shift[n++] = 1 * 2 + 1; cJ++; cH++; }
-    while (cJ >= kCubeH - 3 && n < 255) { sh_shift[n++] = 1 * 2 + 0; cJ--; cH--; }
-    while (cK < 3 && n < 255) { sh_shift[n++] = 2 * 2 + 1; cK++; cD++; }
-    while (cK >= kCubeD - 3 && n < 255) { sh_shift[n++] = 2 * 2 + 0; cK--; cD--; }
+    long long passes = 0;
+    for (int axis = 0; axis < 3; ++axis) {
+      long long up = 0, down = 0;
+      if (*c[axis] < 3) up = 3 - (long long)*c[axis];
+      else if (*c[axis] >= dim[axis] - 3) down = (long long)*c[axis] - (dim[axis] - 4);
+      const long long moves = up ? up : down;
+      if (moves) {
+        *c[axis] += (int)(up - down);
+        *cen[axis] += (int)(up - down);
+        sh_shift[n] = axis * 2 + (up ? 1 : 0);
+        sh_count[n] = (int)(moves < dim[axis] ? moves : dim[axis]);
+        ++n;
+        passes += moves;
+      }
+    }
+    ist[kMiShifts] = (int)(passes < 0x7fffffff ? passes : 0x7fffffff);
     sh_nshift = n;
     sh_c[0] = cI; sh_c[1] = cJ; sh_c[2] = cK;
     ist[kMiCubeI] = cI; ist[kMiCubeJ] = cJ; ist[kMiCubeK] = cK;
@@ -86,7 +102,8 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_prepare(MpBuffers b, MpInput 
     sh_cen[0] = cW; sh_cen[1] = cH; sh_cen[2] = cD;
   }
   __syncthreads();
-  for (int s = 0; s < sh_nshift; ++s) {  // slot-table shifts: the cleared cube wraps around
+  for (int s = 0; s < sh_nshift; ++s)
+  for (int rep = 0; rep < sh_count[s]; ++rep) {  // slot-table shifts: the cleared cube wraps around
     const int axis = sh_shift[s] >> 1, up = sh_shift[s] & 1;
     const int nAx = axis == 0 ? kCubeW : (axis == 1 ? kCubeH : kCubeD);
     const int na = axis == 0 ? kCubeH : kCubeW, nb = axis == 2 ? kCubeH : kCubeD;
@@ -326,17 +343,14 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
       const uint32_t k = t < b1 ? j.keys_alt[t] : 0u;
       const int head = (t < b1 && (t == b0 || j.keys_alt[t - 1] != k)) ? 1 : 0;
       int tot;
-#ifndef LOAM_EXP_VGNOCVAL
       gval[grp.t] = t < b1 ? j.vals_alt[t] : 0u;  // coalesced; read back by the run heads
       if constexpr (G == 64) {
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
       }
-#endif
       const int ex = grp.excl_scan(head, isc, tot);  // (its barrier / wave sync publishes gval)
       // a run ends at the chunk's next head; only the chunk's last run reads on past the chunk
       int nxt = -1;
-#ifndef LOAM_EXP_VGWHILE
       if constexpr (G == 64) {
         const uint64_t hm = __ballot(head);
         const uint64_t after = grp.t == 63 ? 0ull : hm & (~0ull << (grp.t + 1));
@@ -346,14 +360,10 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
         __syncthreads();
         if (head && ex + 1 < tot) nxt = hpos[ex + 1];
       }
-#endif
       if (head) {
         int e = nxt;
         if (e < 0) {
           e = min(base + G, b1);
-#ifdef LOAM_EXP_VGWHILE
-          e = t + 1;
-#endif
           while (e < b1 && j.keys_alt[e] == k) ++e;
         }
         float sx = 0, sy = 0, sz = 0, si = 0;
@@ -362,11 +372,7 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int m = min(mm + u, e - 1);
-#ifdef LOAM_EXP_VGNOCVAL
-            a[u] = j.in[j.vals_alt[m]];
-#else
             a[u] = j.in[m < base + G ? gval[m - base] : j.vals_alt[m]];
-#endif
           }
 #pragma unroll
           for (int u = 0; u < 4; ++u)
@@ -480,11 +486,7 @@ __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
   }
 }
 
-#ifdef LOAM_EXP_VGGRID4K
-constexpr int kVgGridCap = 4096;
-#else
 constexpr int kVgGridCap = 16384;  // measured: 4096 / 16384 / 65536 within 0.5% of each other, 16384 best
-#endif
 template <int G>
 void vg_launch_params_keys(const VgJob& j, hipStream_t st) {
   const int grid = std::min((j.nseg + VgGroup<G>::NT / G - 1) / (VgGroup<G>::NT / G), kVgGridCap);
@@ -503,23 +505,11 @@ void vg_launch_reduce(const VgJob& j, hipStream_t st) {
 // (hipCUB segmented radix sort), which finishes the segments beyond fcap.  The fused kernel wins
 // for a few instances (streaming: one launch instead of four, no global key arrays); for large
 // batches hipCUB's multi-kernel path measured faster (both keep the stable (voxel, position) order).
-#if defined(LOAM_EXP_VGFUSED) || defined(LOAM_EXP_VGFUSED2)
-constexpr bool kVgFusedBatch = true;
-#else
 constexpr bool kVgFusedBatch = false;
-#endif
-#if defined(LOAM_EXP_VGCUBE2K) || defined(LOAM_EXP_VGFUSED2)
-constexpr int kVgCubeCap = 2048;
-#else
 constexpr int kVgCubeCap = 12288;
-#endif
-#ifdef LOAM_EXP_CUBEG64
-constexpr bool kVgCubeG256 = false;
-#else
 constexpr bool kVgCubeG256 = true;  // a workgroup per cube segment also in batches: a few large cubes dominate
-#endif
-void vg_run(const VgJob& j0, void* tmp, size_t tmp_bytes, hipStream_t st, int G, int fcap) {
-  if (j0.nseg == 0) return;
+hipError_t vg_run(const VgJob& j0, void* tmp, size_t tmp_bytes, hipStream_t st, int G, int fcap) {
+  if (j0.nseg == 0) return hipSuccess;
   const int grid = std::min(j0.nseg, 65536);
   VgJob j = j0;
   if (fcap > 0) {
@@ -533,26 +523,31 @@ void vg_run(const VgJob& j0, void* tmp, size_t tmp_bytes, hipStream_t st, int G,
   else if (G == 256) vg_launch_params_keys<256>(j, st);
   else vg_launch_params_keys<1024>(j, st);
   size_t bytes = tmp_bytes;
+  hipError_t e;
   if (j.sb24) {
-    (void)hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
-                                                      j.nseg, j.sb24, j.se24, 0, 24, st);
+    e = hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
+                                                    j.nseg, j.sb24, j.se24, 0, 24, st);
     bytes = tmp_bytes;
-    (void)hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
+    if (e == hipSuccess)
+      e = hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
                                                       j.nseg, j.sb32, j.se32, 0, 32, st);
   } else {
-    (void)hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
-                                                      j.nseg, j.begin, j.end, 0, j.end_bit, st);
+    e = hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
+                                                    j.nseg, j.begin, j.end, 0, j.end_bit, st);
   }
+  if (e != hipSuccess) return e;
   if (G == 64) vg_launch_reduce<64>(j, st);
   else if (G == 256) vg_launch_reduce<256>(j, st);
   else vg_launch_reduce<1024>(j, st);
+  return hipGetLastError();
 }
 
 size_t vg_tmp_bytes(int total, int nseg) {
   size_t bytes = 0;
-  (void)hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                    (uint32_t*)nullptr, (uint32_t*)nullptr, total, nseg,
-                                                    (int*)nullptr, (int*)nullptr, 0, 32);
+  if (hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                  (uint32_t*)nullptr, (uint32_t*)nullptr, total, nseg,
+                                                  (int*)nullptr, (int*)nullptr, 0, 32) != hipSuccess)
+    return 0;
   return bytes;
 }
 
@@ -648,13 +643,7 @@ constexpr int kMpQueryThreads = 256;
 // iterates max(candidates per lane) instead of the union of its lanes' cells x buckets.  `lst` =
 // the lane's LDS column (stride kMpQueryThreads).  Ranges are packed start:19 | count:13; a lane
 // whose ranges do not fit falls back to knn5.
-#if defined(LOAM_EXP_NNG4)
-constexpr int kNnInFlight = 4;
-#elif defined(LOAM_EXP_NNG16)
-constexpr int kNnInFlight = 16;
-#else
 constexpr int kNnInFlight = 8;  // measured k_mp_nn ms/step: 2 -> 4.17, 4 -> 3.95, 8 -> 3.88, 16 -> 5.33
-#endif
 LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5& t, uint32_t* lst) {
   if (T <= 0) return;
   const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
@@ -727,6 +716,7 @@ __global__ void k_mp_lm_begin(MpBuffers b) {
   ist[kMiIters] = 0;
   ist[kMiRows] = 0;
   ist[kMiFits] = 0;
+  ist[kMiDegSteps] = 0;
 }
 
 // one L-M iteration's correspondences (:714-877) in two passes, lane per stack point (corner,
@@ -939,11 +929,6 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
   double acc[28];
 #pragma unroll
   for (int k = 0; k < 28; ++k) acc[k] = 0.0;
-#ifdef LOAM_EXP_ITERSER
-  for (int q = tid; q < nq; q += kMpThreads) {  // :897-921
-    if (!qok[q]) continue;
-    const float4 o = stack[q < nsc ? q : b.capC + (q - nsc)], c = qcf[q];
-#else
   // four rows' loads in flight per step; the rows are still summed in the lane's q order
   for (int q0 = tid; q0 < nq; q0 += 4 * kMpThreads) {  // :897-921
     int8_t okv[4];
@@ -959,7 +944,6 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
     for (int u = 0; u < 4; ++u) {
     if (!okv[u]) continue;
     const float4 o = ov[u], c = cv4[u];
-#endif
     float a[6];
     a[0] = (crx * sry * srz * o.x + crx * crz * sry * o.y - srx * sry * o.z) * c.x +
            (-srx * srz * o.x - crz * srx * o.y - crx * o.z) * c.y +
@@ -982,9 +966,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
     for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
     acc[27] += 1.0;
   }
-#ifndef LOAM_EXP_ITERSER
   }
-#endif
   wave_reduce_scatter_28(acc);  // lanes 2v, 2v+1: the wave sum of value v
   if ((lane & 1) == 0 && (lane >> 1) < 28) sh.red[w][lane >> 1] = acc[0];
   __syncthreads();
@@ -1011,6 +993,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
       int degen = ist[kMiDegen];
       loamla::lm_step(sh.AtA, sh.AtB, iter, 100.0f, &degen, st + kMpMatP, sh.X, sh.lm_ws, sh.lm_iws);
       ist[kMiDegen] = degen;
+      if (degen) ist[kMiDegSteps] += 1;
       for (int q = 0; q < 6; ++q) st[kMpTobe + q] += sh.X[q];  // no NaN guard in mapping (:956-961)
       const float dR = loamla::delta_r(sh.X), dT = loamla::delta_t(sh.X);
       if (D(dR) < 0.05 && D(dT) < 0.05) ist[kMiStop] = 1;
@@ -1092,18 +1075,6 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
   // flattened counts (one block scan instead of one per 256 slots); offsets replace the counts in LDS
   int* ac = b.app_cnt + (size_t)p * kCubeNum * 2;
   int* ao = b.app_off + (size_t)p * kCubeNum * 2;
-#ifdef LOAM_EXP_INSSCAN
-  int run = 0;
-  for (int kind = 0; kind < 2; ++kind)
-    for (int base = 0; base < kCubeNum; base += kMpThreads) {
-      const int s = base + tid;
-      const int c = s < kCubeNum ? cnt[kind][s] : 0;
-      int tot;
-      const int ex = block_excl_scan<kMpThreads>(c, scratch, tot);
-      if (s < kCubeNum) { ac[s * 2 + kind] = c; ao[s * 2 + kind] = run + ex; }
-      run += tot;
-    }
-#else
   {
     constexpr int kFlat = 2 * kCubeNum, kPer = (kFlat + kMpThreads - 1) / kMpThreads;
     int* cf = &cnt[0][0];
@@ -1130,7 +1101,6 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
       ao[s * 2 + kind] = o;
     }
   }
-#endif
   __threadfence_block();
   __syncthreads();
   float4* app = b.app + (size_t)p * b.cap_stack;
@@ -1303,7 +1273,8 @@ __global__ __launch_bounds__(256) void k_mp_register(MpBuffers b, MpInput in) {
 }  // namespace
 
 // ---------------------------------------------------------------- host side
-void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter) {
+hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter) {
+  DevAlloc A;
   b.P = P;
   b.capC = kLessSharpPerRing * R;
   b.capS = cap_pts;
@@ -1313,64 +1284,67 @@ void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter
   b.tmax = next_pow2(map_cap) > (1 << 20) ? (1 << 20) : next_pow2(map_cap);
   b.pool_cur = 0;
   const size_t Pm = (size_t)P * map_cap, Ps = (size_t)P * b.cap_stack;
-  (void)hipMalloc(&b.state, (size_t)P * kMpStateFloats * sizeof(float));
-  (void)hipMalloc(&b.istate, (size_t)P * kMpStateInts * sizeof(int));
-  (void)hipMalloc(&b.slots, (size_t)2 * P * kCubeNum * 4 * sizeof(int));
-  (void)hipMalloc(&b.pool, 2 * Pm * sizeof(float4));
-  (void)hipMalloc(&b.valid, (size_t)P * kMaxValid * sizeof(int));
-  (void)hipMalloc(&b.vpre, (size_t)P * (kMaxValid + 1) * 2 * sizeof(int));
-  (void)hipMalloc(&b.inC, (size_t)P * b.capC * sizeof(float4));
-  (void)hipMalloc(&b.inS, (size_t)P * b.capS * sizeof(float4));
-  (void)hipMalloc(&b.inF, (size_t)P * b.capS * sizeof(float4));
-  (void)hipMalloc(&b.in_n, (size_t)P * 3 * sizeof(int));
-  (void)hipMalloc(&b.in_pose, (size_t)P * 6 * sizeof(float));
-  (void)hipMalloc(&b.stack2, Ps * sizeof(float4));
-  (void)hipMalloc(&b.stack, Ps * sizeof(float4));
-  (void)hipMalloc(&b.nstack, (size_t)P * 2 * sizeof(int));
-  (void)hipMalloc(&b.from, Pm * sizeof(float4));
-  (void)hipMalloc(&b.hC_start, (size_t)P * (b.tmax + 1) * sizeof(int));
-  (void)hipMalloc(&b.hS_start, (size_t)P * (b.tmax + 1) * sizeof(int));
-  (void)hipMalloc(&b.h_fill, (size_t)P * b.tmax * sizeof(int));
-  (void)hipMalloc(&b.hC_T, (size_t)P * sizeof(int));
-  (void)hipMalloc(&b.hS_T, (size_t)P * sizeof(int));
-  (void)hipMalloc(&b.hC_pts, Pm * sizeof(float4));
-  (void)hipMalloc(&b.hS_pts, Pm * sizeof(float4));
-  (void)hipMalloc(&b.nfrom, (size_t)P * 2 * sizeof(int));
-  (void)hipMalloc(&b.q_ok, Ps * sizeof(int8_t));
-  (void)hipMalloc(&b.q_cf, Ps * sizeof(float4));
-  (void)hipMalloc(&b.q_nn, Ps * 2 * sizeof(int4));
-  (void)hipMalloc(&b.citems, (size_t)P * 2 * kCubeNum * sizeof(int));
-  (void)hipMalloc(&b.nitems, (size_t)P * sizeof(int));
-  (void)hipMalloc(&b.q_fit, Ps * 4 * sizeof(float4));
-  (void)hipMalloc(&b.app_cnt, (size_t)P * kCubeNum * 2 * sizeof(int));
-  (void)hipMalloc(&b.app_off, (size_t)P * kCubeNum * 2 * sizeof(int));
-  (void)hipMalloc(&b.app, Ps * sizeof(float4));
-  (void)hipMalloc(&b.vin, Pm * sizeof(float4));
-  (void)hipMalloc(&b.vout, Pm * sizeof(float4));
-  (void)hipMalloc(&b.vseg_b, (size_t)P * 2 * kMaxValid * sizeof(int));
-  (void)hipMalloc(&b.vseg_e, (size_t)P * 2 * kMaxValid * sizeof(int));
-  (void)hipMalloc(&b.vseg_cnt, (size_t)P * 2 * kMaxValid * sizeof(int));
-  (void)hipMalloc(&b.vseg_leaf, (size_t)P * 2 * kMaxValid * sizeof(float));
-  (void)hipMalloc(&b.sseg_b, (size_t)P * 2 * sizeof(int));
-  (void)hipMalloc(&b.sseg_e, (size_t)P * 2 * sizeof(int));
-  (void)hipMalloc(&b.sseg_cnt, (size_t)P * 2 * sizeof(int));
-  (void)hipMalloc(&b.sseg_leaf, (size_t)P * 2 * sizeof(float));
+  A(&b.state, (size_t)P * kMpStateFloats * sizeof(float));
+  A(&b.istate, (size_t)P * kMpStateInts * sizeof(int));
+  A(&b.slots, (size_t)2 * P * kCubeNum * 4 * sizeof(int));
+  A(&b.pool, 2 * Pm * sizeof(float4));
+  A(&b.valid, (size_t)P * kMaxValid * sizeof(int));
+  A(&b.vpre, (size_t)P * (kMaxValid + 1) * 2 * sizeof(int));
+  A(&b.inC, (size_t)P * b.capC * sizeof(float4));
+  A(&b.inS, (size_t)P * b.capS * sizeof(float4));
+  A(&b.inF, (size_t)P * b.capS * sizeof(float4));
+  A(&b.in_n, (size_t)P * 3 * sizeof(int));
+  A(&b.in_pose, (size_t)P * 6 * sizeof(float));
+  A(&b.stack2, Ps * sizeof(float4));
+  A(&b.stack, Ps * sizeof(float4));
+  A(&b.nstack, (size_t)P * 2 * sizeof(int));
+  A(&b.from, Pm * sizeof(float4));
+  A(&b.hC_start, (size_t)P * (b.tmax + 1) * sizeof(int));
+  A(&b.hS_start, (size_t)P * (b.tmax + 1) * sizeof(int));
+  A(&b.h_fill, (size_t)P * b.tmax * sizeof(int));
+  A(&b.hC_T, (size_t)P * sizeof(int));
+  A(&b.hS_T, (size_t)P * sizeof(int));
+  A(&b.hC_pts, Pm * sizeof(float4));
+  A(&b.hS_pts, Pm * sizeof(float4));
+  A(&b.nfrom, (size_t)P * 2 * sizeof(int));
+  A(&b.q_ok, Ps * sizeof(int8_t));
+  A(&b.q_cf, Ps * sizeof(float4));
+  A(&b.q_nn, Ps * 2 * sizeof(int4));
+  A(&b.citems, (size_t)P * 2 * kCubeNum * sizeof(int));
+  A(&b.nitems, (size_t)P * sizeof(int));
+  A(&b.q_fit, Ps * 4 * sizeof(float4));
+  A(&b.app_cnt, (size_t)P * kCubeNum * 2 * sizeof(int));
+  A(&b.app_off, (size_t)P * kCubeNum * 2 * sizeof(int));
+  A(&b.app, Ps * sizeof(float4));
+  A(&b.vin, Pm * sizeof(float4));
+  A(&b.vout, Pm * sizeof(float4));
+  A(&b.vseg_b, (size_t)P * 2 * kMaxValid * sizeof(int));
+  A(&b.vseg_e, (size_t)P * 2 * kMaxValid * sizeof(int));
+  A(&b.vseg_cnt, (size_t)P * 2 * kMaxValid * sizeof(int));
+  A(&b.vseg_leaf, (size_t)P * 2 * kMaxValid * sizeof(float));
+  A(&b.sseg_b, (size_t)P * 2 * sizeof(int));
+  A(&b.sseg_e, (size_t)P * 2 * sizeof(int));
+  A(&b.sseg_cnt, (size_t)P * 2 * sizeof(int));
+  A(&b.sseg_leaf, (size_t)P * 2 * sizeof(float));
   const size_t vgn = Pm > Ps ? Pm : Ps;
-  (void)hipMalloc(&b.vg_params, (size_t)P * 2 * kMaxValid * 8 * sizeof(int));
-  (void)hipMalloc(&b.vg_k, vgn * sizeof(uint32_t));
-  (void)hipMalloc(&b.vg_k2, vgn * sizeof(uint32_t));
-  (void)hipMalloc(&b.vg_v, vgn * sizeof(uint32_t));
-  (void)hipMalloc(&b.vg_v2, vgn * sizeof(uint32_t));
-  (void)hipMalloc(&b.vg_bb, (size_t)P * 2 * kMaxValid * sizeof(int));
-  (void)hipMalloc(&b.vg_split, (size_t)4 * P * 2 * kMaxValid * sizeof(int));
-  (void)hipMalloc(&b.vg_be, (size_t)P * 2 * kMaxValid * sizeof(int));
+  A(&b.vg_params, (size_t)P * 2 * kMaxValid * 8 * sizeof(int));
+  A(&b.vg_k, vgn * sizeof(uint32_t));
+  A(&b.vg_k2, vgn * sizeof(uint32_t));
+  A(&b.vg_v, vgn * sizeof(uint32_t));
+  A(&b.vg_v2, vgn * sizeof(uint32_t));
+  A(&b.vg_bb, (size_t)P * 2 * kMaxValid * sizeof(int));
+  A(&b.vg_split, (size_t)4 * P * 2 * kMaxValid * sizeof(int));
+  A(&b.vg_be, (size_t)P * 2 * kMaxValid * sizeof(int));
   const size_t t1 = vg_tmp_bytes((int)vgn, P * 2 * kMaxValid), t2 = vg_tmp_bytes((int)Ps, P * 2);
   b.cub_bytes = t1 > t2 ? t1 : t2;
-  (void)hipMalloc(&b.cub_tmp, b.cub_bytes);
-  (void)hipMalloc(&b.reg, (size_t)P * b.capS * sizeof(float4));
-  (void)hipMalloc(&b.nreg, (size_t)P * sizeof(int));
-  mp_reset(b, nullptr);
-  (void)hipDeviceSynchronize();
+  if (t1 == 0 || t2 == 0) A.err = hipErrorInvalidValue;
+  A(&b.cub_tmp, b.cub_bytes);
+  A(&b.reg, (size_t)P * b.capS * sizeof(float4));
+  A(&b.nreg, (size_t)P * sizeof(int));
+  if (A.err == hipSuccess) A.err = mp_reset(b, nullptr);
+  if (A.err == hipSuccess) A.err = hipDeviceSynchronize();
+  if (A.err != hipSuccess) mp_free(b);
+  return A.err;
 }
 
 void mp_free(MpBuffers& b) {
@@ -1391,12 +1365,14 @@ __global__ void k_mp_reset(MpBuffers b) {
   ist[kMiCenW] = 10; ist[kMiCenH] = 5; ist[kMiCenD] = 10;  // :64-66
 }
 
-void mp_reset(MpBuffers& b, hipStream_t st) {
+hipError_t mp_reset(MpBuffers& b, hipStream_t st) {
   b.pool_cur = 0;
-  (void)hipMemsetAsync(b.state, 0, (size_t)b.P * kMpStateFloats * sizeof(float), st);
-  (void)hipMemsetAsync(b.istate, 0, (size_t)b.P * kMpStateInts * sizeof(int), st);
-  (void)hipMemsetAsync(b.slots, 0, (size_t)2 * b.P * kCubeNum * 4 * sizeof(int), st);
+  hipError_t e = hipMemsetAsync(b.state, 0, (size_t)b.P * kMpStateFloats * sizeof(float), st);
+  if (e == hipSuccess) e = hipMemsetAsync(b.istate, 0, (size_t)b.P * kMpStateInts * sizeof(int), st);
+  if (e == hipSuccess) e = hipMemsetAsync(b.slots, 0, (size_t)2 * b.P * kCubeNum * 4 * sizeof(int), st);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_mp_reset, dim3((b.P + 255) / 256), dim3(256), 0, st, b);
+  return hipGetLastError();
 }
 
 void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool map_empty) {
@@ -1410,13 +1386,11 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   js.in = b.stack2; js.out = b.stack; js.begin = b.sseg_b; js.end = b.sseg_e; js.leaf = b.sseg_leaf;
   js.out_count = b.sseg_cnt; js.params = b.vg_params; js.keys = b.vg_k; js.keys_alt = b.vg_k2;
   js.vals = b.vg_v; js.vals_alt = b.vg_v2; js.big_b = b.vg_bb; js.big_e = b.vg_be; js.nseg = 2 * P; js.total = P * b.cap_stack;
-#ifndef LOAM_EXP_STACK32
   if (P > 4) {  // batches: segments whose keys fit 24 bits sort in three passes, the rest in four
     const size_t ns = (size_t)P * 2 * kMaxValid;
     js.sb24 = b.vg_split; js.se24 = b.vg_split + ns; js.sb32 = b.vg_split + 2 * ns; js.se32 = b.vg_split + 3 * ns;
   }
-#endif
-  vg_run(js, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 1024 : 256, P <= 4 || kVgFusedBatch ? 12288 : 0);  // two large segments per instance
+  b.note(vg_run(js, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 1024 : 256, P <= 4 || kVgFusedBatch ? 12288 : 0));  // two large segments per instance
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);
   mark("k_mp_gather");
@@ -1458,11 +1432,9 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   jv.out_count = b.vseg_cnt; jv.params = b.vg_params; jv.keys = b.vg_k; jv.keys_alt = b.vg_k2;
   jv.vals = b.vg_v; jv.vals_alt = b.vg_v2; jv.big_b = b.vg_bb; jv.big_e = b.vg_be; jv.nseg = 2 * kMaxValid * P; jv.total = P * b.map_cap;
   // a cube spans at most 50 m: <= 252 voxels of 0.2 m per axis, keys below 2^24 (three 8-bit passes)
-#ifndef LOAM_EXP_CUBE32
   jv.end_bit = 24;
-#endif
   jv.err = b.istate + kMiErr; jv.err_stride = kMpStateInts; jv.seg_per_err = 2 * kMaxValid;
-  vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 || kVgCubeG256 ? 256 : 64, P <= 4 || kVgFusedBatch ? kVgCubeCap : 0);    // 2 x 125 cube segments per instance
+  b.note(vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 || kVgCubeG256 ? 256 : 64, P <= 4 || kVgFusedBatch ? kVgCubeCap : 0));  // 2 x 125 cube segments per instance
   mark("vg_cubes");
   hipLaunchKernelGGL(k_mp_compact_table, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);
@@ -1516,6 +1488,7 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   (void)hipEventElapsedTime(&ms, e0, e1);
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
+  if (he == hipSuccess) he = b.take_error();
   if (he != hipSuccess) {
     err = std::string("mapping: ") + hipGetErrorString(he);
     return LOAM_E_HIP;
@@ -1547,6 +1520,8 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
     stats->mp_fits = (uint64_t)si[kMiFits];
     stats->mp_map_points = (uint64_t)(si[kMiFromC] + si[kMiFromS]);
     stats->mp_map_valid_points = (uint64_t)si[kMiValidPts];
+    stats->mp_degenerate_steps = (uint64_t)si[kMiDegSteps];
+    stats->mp_grid_shifts = (uint64_t)si[kMiShifts];
     stats->ms_mp = ms;
   }
   return rc;
@@ -1597,10 +1572,11 @@ int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::s
   j.in = b.vin; j.out = b.vout; j.begin = b.vseg_b; j.end = b.vseg_e; j.leaf = b.vseg_leaf;
   j.out_count = b.vseg_cnt; j.params = b.vg_params; j.keys = b.vg_k; j.keys_alt = b.vg_k2;
   j.vals = b.vg_v; j.vals_alt = b.vg_v2; j.big_b = b.vg_bb; j.big_e = b.vg_be; j.nseg = 1; j.total = b.P * b.map_cap;
-  vg_run(j, b.cub_tmp, b.cub_bytes, st, 1024, 12288);
+  b.note(vg_run(j, b.cub_tmp, b.cub_bytes, st, 1024, 12288));
   int cnt = 0;
   (void)hipMemcpyAsync(&cnt, b.vseg_cnt, sizeof(int), hipMemcpyDeviceToHost, st);
-  const hipError_t he = hipStreamSynchronize(st);
+  hipError_t he = hipStreamSynchronize(st);
+  if (he == hipSuccess) he = b.take_error();
   if (he != hipSuccess) {
     err = std::string("surround: ") + hipGetErrorString(he);
     return LOAM_E_HIP;
@@ -1621,7 +1597,7 @@ int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::s
 // frame 1 of the batch problem: reset, then prev (Last[0], fullEnd[0]) into the empty store at
 // the zero pose.  Reads only what the odometry seeding wrote, so it may run beside od_solve.
 void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof) {
-  mp_reset(b, st);
+  b.note(mp_reset(b, st));
   if (prof) prof->mark("mp_reset");
   MpInput in;
   in.corner = od.lastC; in.surf = od.lastS; in.full = od.fullEnd;
@@ -1651,11 +1627,16 @@ void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof)
 }
 
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err) {
-  (void)hipStreamSynchronize(st);
   std::vector<float> sf((size_t)b.P * kMpStateFloats);
   std::vector<int> si((size_t)b.P * kMpStateInts);
-  (void)hipMemcpy(sf.data(), b.state, sf.size() * sizeof(float), hipMemcpyDeviceToHost);
-  (void)hipMemcpy(si.data(), b.istate, si.size() * sizeof(int), hipMemcpyDeviceToHost);
+  hipError_t he = hipStreamSynchronize(st);
+  if (he == hipSuccess) he = b.take_error();
+  if (he == hipSuccess) he = hipMemcpy(sf.data(), b.state, sf.size() * sizeof(float), hipMemcpyDeviceToHost);
+  if (he == hipSuccess) he = hipMemcpy(si.data(), b.istate, si.size() * sizeof(int), hipMemcpyDeviceToHost);
+  if (he != hipSuccess) {
+    err = std::string("mapping: ") + hipGetErrorString(he);
+    return LOAM_E_HIP;
+  }
   for (int p = 0; p < b.P; ++p) {
     const int* q = &si[(size_t)p * kMpStateInts];
     if (q[kMiErr]) {
@@ -1671,6 +1652,8 @@ int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats*
       stats->mp_fits += (uint64_t)q[kMiFits];
       stats->mp_map_points += (uint64_t)(q[kMiFromC] + q[kMiFromS]);
       stats->mp_map_valid_points += (uint64_t)q[kMiValidPts];
+      stats->mp_degenerate_steps += (uint64_t)q[kMiDegSteps];
+      stats->mp_grid_shifts += (uint64_t)q[kMiShifts];
     }
   }
   return LOAM_OK;

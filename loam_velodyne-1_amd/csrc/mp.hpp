@@ -19,8 +19,11 @@ constexpr int kMaxValid = 125;
 constexpr int kMpSum = 0, kMpIncre = 6, kMpTobe = 12, kMpBef = 18, kMpAft = 24, kMpMatP = 30, kMpOnY = 66,
               kMpImuRP = 69, kMpStateFloats = 72;  // kMpImuRP: IMU (roll, pitch) for transformUpdate
 enum { kMiCenW = 0, kMiCenH, kMiCenD, kMiDegen, kMiNValid, kMiIters, kMiRows, kMiStackC, kMiStackS, kMiFromC,
-       kMiFromS, kMiErr, kMiLmRan, kMiValidPts, kMiStop, kMiFits, kMiImu, kMiCubeI, kMiCubeJ, kMiCubeK, kMpStateInts = 20 };
-static_assert(kMiCubeK < kMpStateInts, "istate layout");
+       kMiFromS, kMiErr, kMiLmRan, kMiValidPts, kMiStop, kMiFits, kMiImu, kMiCubeI, kMiCubeJ, kMiCubeK,
+       kMiDegSteps,  // L-M updates of this frame projected by the iteration-0 degeneracy analysis
+       kMiShifts,    // cube-grid slab shifts of this frame's recentring (the reference's passes)
+       kMpStateInts = 24 };
+static_assert(kMiShifts < kMpStateInts, "istate layout");
 
 // one mapping frame's inputs for every instance (device pointers)
 struct MpInput {
@@ -102,12 +105,22 @@ struct MpBuffers {
   size_t cub_bytes = 0;
   float4* reg = nullptr;      // [P][capS] registered full cloud
   int* nreg = nullptr;
+  hipError_t sticky = hipSuccess;  // first failed library call of the launch sequences (hipCUB)
+  void note(hipError_t e) {
+    if (sticky == hipSuccess) sticky = e;
+  }
+  // returns the sticky error and clears it
+  hipError_t take_error() {
+    const hipError_t e = sticky;
+    sticky = hipSuccess;
+    return e;
+  }
 };
 
 inline int mp_batch_map_capacity(int cap) { return 2 * cap; }
-void mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter);
+hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int max_iter);  // on failure: freed, b empty
 void mp_free(MpBuffers& b);
-void mp_reset(MpBuffers& b, hipStream_t st);
+hipError_t mp_reset(MpBuffers& b, hipStream_t st);
 // map_empty: the store was just reset (no L-M can run: its launches are skipped)
 void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof = nullptr, bool map_empty = false);
 // imu_rp: the IMU (roll, pitch) transformUpdate blends in (nullptr = no IMU); *updated = whether

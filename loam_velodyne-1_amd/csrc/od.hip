@@ -133,10 +133,6 @@ __global__ __launch_bounds__(256) void k_hash_build(HashJob j) {
 
 namespace {
 
-#ifdef LOAM_EXP_ASSOCPH
-// diagnostic build only: cycles of the association phases and fallback counts (tools/exp_assoc.py)
-__device__ unsigned long long g_aph[8];
-#endif
 
 // lower bound of the float squared distance from s to any point of the box [lo, hi] (monotone
 // rounding of the same expression as sqdist)
@@ -190,9 +186,6 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
   __builtin_amdgcn_wave_barrier();
   if (best != ~0ull && __uint_as_float((uint32_t)(best >> 32)) < h * h) return best;
   // farther than one cell: the chunks of the whole cloud that may hold a point closer than 5 m
-#ifdef LOAM_EXP_ASSOCPH
-  if (lane == 0) atomicAdd(&g_aph[4], 1ull);
-#endif
   best = ~0ull;
   const int nch = (n + kChunk - 1) / kChunk;
   for (int k0 = 0; k0 < nch; k0 += 64) {
@@ -373,6 +366,8 @@ __global__ void k_od_begin(OdBuffers b, FeatView f) {
   ist[kIsIters] = 0;
   ist[kIsAssoc] = 0;
   ist[kIsRows] = 0;
+  ist[kIsDegSteps] = 0;
+  ist[kIsNanSkips] = 0;
   b.done[p] = 0;
 }
 
@@ -412,28 +407,18 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(8)))
   const float4* SL = b.lastS + lp * b.capS;
   int* ind = b.ind + (size_t)p * 3 * b.cap_q;
   for (int q = blk.x * kOdWaves + w; q < nq; q += gridDim.x * kOdWaves) {
-#ifdef LOAM_EXP_ASSOCPH
-    long long t0 = clock64();
-#define APH(k) { const long long t1 = clock64(); if (lane == 0) atomicAdd(&g_aph[k], (unsigned long long)(t1 - t0)); t0 = t1; }
-#else
-#define APH(k)
-#endif
     const float4 s4 = sel[q];
     int i1, i2, i3 = -1;
     if (q < nc) {
       const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
       const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC,
                                        b.hC_T[last_buf * b.P + p], CL, ch, C, 1.0f, 1.0f, s4, cells[w]);
-      APH(0);
       wave_assoc_corner(CL, ch, min(nc, C), nn, s4, i1, i2);
-      APH(1);
     } else {
       const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
       const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS,
                                        b.hS_T[last_buf * b.P + p], SL, ch, S, 1.0f, 1.0f, s4, cells[w]);
-      APH(2);
       wave_assoc_surf(SL, ch, min(ns, S), nn, s4, i1, i2, i3);
-      APH(3);
     }
     if (lane == 0) {
       ind[q] = i1;
@@ -465,9 +450,12 @@ LOAM_D void od_step(const OdBuffers& b, int p, int iter, const double* tot, floa
     int degen = ist[kIsDegenerate];
     loamla::lm_step(AtA, AtB, iter, 10.0f, &degen, st + kOdMatP, X, lm_ws, lm_iws);
     ist[kIsDegenerate] = degen;
+    if (degen) ist[kIsDegSteps] += 1;
     const bool nan = isnan(X[0]) || isnan(X[1]) || isnan(X[2]) || isnan(X[3]) || isnan(X[4]) || isnan(X[5]);
     if (!nan)  // Q16
       for (int q = 0; q < 6; ++q) st[q] += X[q];
+    else
+      ist[kIsNanSkips] += 1;
     const float dR = loamla::delta_r(X), dT = loamla::delta_t(X);
     if (D(dR) < 0.1 && D(dT) < 0.1) ist[kIsStop] = 1;
   }
@@ -580,12 +568,6 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdR
     const float e30 = -sw * (cry * crz - srx * sry * srz), e31 = sw * crx * srz, e32 = sw * (crz * sry + cry * srx * srz);
     const float e40 = -sw * (cry * srz + crz * srx * sry), e41 = sw * crx * crz, e42 = sw * (sry * srz - cry * crz * srx);
     const float e50 = sw * crx * sry, e51 = sw * srx, e52 = sw * crx * cry;
-#ifdef LOAM_EXP_ROWSEQ
-    for (int it = 0; it <= iter; ++it) {
-      // a rejected correspondence has a zero coefficient and adds exact zeros
-      const float4 c4 = qcf[(size_t)it * b.cap_q + q];
-      const bool okit = qok[(size_t)it * b.cap_q + q] != 0;
-#else
     // the stored rows two iterations at a time (their loads in flight together), summed in order
     for (int it0 = 0; it0 <= iter; it0 += 2) {
       float4 cv4[2];
@@ -601,7 +583,6 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdR
       if (it0 + u > iter) break;
       const float4 c4 = cv4[u];
       const bool okit = okv[u];
-#endif
       float a[6];
       a[0] = e00 * c4.x + e01 * c4.y + e02 * c4.z;
       a[1] = e10 * c4.x + e12 * c4.z;
@@ -619,9 +600,7 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdR
       for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
       acc[27] += okit ? 1.0 : 0.0;
     }
-#ifndef LOAM_EXP_ROWSEQ
     }
-#endif
   }
   // wave sums of the 28 values as a butterfly reduce-scatter (32 slots halved per step: 32
   // shuffles instead of 28 x 6); lanes 2v, 2v+1 end with the sum of value v
@@ -668,9 +647,6 @@ __global__ __launch_bounds__(64) void k_od_step(OdBuffers b, int iter, int gq) {
   __shared__ int lm_iws[12];
   if (lane < 28) {  // fixed order over the workgroups; eight partials in flight per step
     double v = 0.0;
-#ifdef LOAM_EXP_PARTSER
-    for (int g = 0; g < gq; ++g) v += b.part[((size_t)p * b.gq + g) * 28 + lane];
-#else
     const double* pp = b.part + (size_t)p * b.gq * 28 + lane;
     for (int g = 0; g < gq; g += 8) {
       double t[8];
@@ -680,7 +656,6 @@ __global__ __launch_bounds__(64) void k_od_step(OdBuffers b, int iter, int gq) {
       for (int u = 0; u < 8; ++u)
         if (g + u < gq) v += t[u];
     }
-#endif
     tot[lane] = v;
   }
   __syncthreads();
@@ -737,7 +712,8 @@ __global__ __launch_bounds__(256) void k_od_end(OdBuffers b, FeatView f, int dst
 }
 
 // ---------------------------------------------------------------- host side
-void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
+hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
+  DevAlloc A;
   b.P = P;
   b.capC = kLessSharpPerRing * R;
   b.capS = cap_pts;
@@ -746,36 +722,42 @@ void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   b.gq = (b.cap_q + kOdThreads - 1) / kOdThreads;
   b.tC = next_pow2(b.capC);
   b.tS = next_pow2(b.capS) > 65536 ? 65536 : next_pow2(b.capS);
-  (void)hipMalloc(&b.state, (size_t)P * kOdStateFloats * sizeof(float));
-  (void)hipMalloc(&b.istate, (size_t)P * kOdStateInts * sizeof(int));
-  (void)hipMalloc(&b.lastC, (size_t)2 * P * b.capC * sizeof(float4));
-  (void)hipMalloc(&b.lastS, (size_t)2 * P * b.capS * sizeof(float4));
-  (void)hipMalloc(&b.fullEnd, (size_t)2 * P * b.capS * sizeof(float4));
-  (void)hipMalloc(&b.nlast, (size_t)P * 4 * sizeof(int));
-  (void)hipMalloc(&b.nfullEnd, (size_t)P * 2 * sizeof(int));
-  (void)hipMalloc(&b.hC_start, (size_t)2 * P * (b.tC + 1) * sizeof(int));
-  (void)hipMalloc(&b.hS_start, (size_t)2 * P * (b.tS + 1) * sizeof(int));
-  (void)hipMalloc(&b.hC_fill, (size_t)P * b.tC * sizeof(int));
-  (void)hipMalloc(&b.hS_fill, (size_t)P * b.tS * sizeof(int));
-  (void)hipMalloc(&b.hC_pts, (size_t)2 * P * b.capC * sizeof(float4));
-  (void)hipMalloc(&b.hS_pts, (size_t)2 * P * b.capS * sizeof(float4));
-  (void)hipMalloc(&b.hC_T, (size_t)2 * P * sizeof(int));
-  (void)hipMalloc(&b.cC, (size_t)2 * P * 2 * chunks_of(b.capC) * sizeof(float4));
-  (void)hipMalloc(&b.cS, (size_t)2 * P * 2 * chunks_of(b.capS) * sizeof(float4));
-  (void)hipMalloc(&b.hS_T, (size_t)2 * P * sizeof(int));
-  (void)hipMalloc(&b.ind, (size_t)P * 3 * b.cap_q * sizeof(int));
-  (void)hipMalloc(&b.sel, (size_t)P * b.cap_q * sizeof(float4));
-  (void)hipMalloc(&b.q_cf, (size_t)P * max_iter * b.cap_q * sizeof(float4));
-  (void)hipMalloc(&b.q_ok, (size_t)P * max_iter * b.cap_q * sizeof(int8_t));
-  (void)hipMalloc(&b.part, (size_t)P * b.gq * 28 * sizeof(double));
-  (void)hipMalloc(&b.done, (size_t)P * sizeof(int));
-  (void)hipMemset(b.done, 0, (size_t)P * sizeof(int));
-  (void)hipMemset(b.state, 0, (size_t)P * kOdStateFloats * sizeof(float));
-  (void)hipMemset(b.istate, 0, (size_t)P * kOdStateInts * sizeof(int));
-  (void)hipMemset(b.nlast, 0, (size_t)P * 4 * sizeof(int));
-  (void)hipMemset(b.nfullEnd, 0, (size_t)P * 2 * sizeof(int));
-  (void)hipMemset(b.hC_T, 0, (size_t)2 * P * sizeof(int));
-  (void)hipMemset(b.hS_T, 0, (size_t)2 * P * sizeof(int));
+  A(&b.state, (size_t)P * kOdStateFloats * sizeof(float));
+  A(&b.istate, (size_t)P * kOdStateInts * sizeof(int));
+  A(&b.lastC, (size_t)2 * P * b.capC * sizeof(float4));
+  A(&b.lastS, (size_t)2 * P * b.capS * sizeof(float4));
+  A(&b.fullEnd, (size_t)2 * P * b.capS * sizeof(float4));
+  A(&b.nlast, (size_t)P * 4 * sizeof(int));
+  A(&b.nfullEnd, (size_t)P * 2 * sizeof(int));
+  A(&b.hC_start, (size_t)2 * P * (b.tC + 1) * sizeof(int));
+  A(&b.hS_start, (size_t)2 * P * (b.tS + 1) * sizeof(int));
+  A(&b.hC_fill, (size_t)P * b.tC * sizeof(int));
+  A(&b.hS_fill, (size_t)P * b.tS * sizeof(int));
+  A(&b.hC_pts, (size_t)2 * P * b.capC * sizeof(float4));
+  A(&b.hS_pts, (size_t)2 * P * b.capS * sizeof(float4));
+  A(&b.hC_T, (size_t)2 * P * sizeof(int));
+  A(&b.cC, (size_t)2 * P * 2 * chunks_of(b.capC) * sizeof(float4));
+  A(&b.cS, (size_t)2 * P * 2 * chunks_of(b.capS) * sizeof(float4));
+  A(&b.hS_T, (size_t)2 * P * sizeof(int));
+  A(&b.ind, (size_t)P * 3 * b.cap_q * sizeof(int));
+  A(&b.sel, (size_t)P * b.cap_q * sizeof(float4));
+  A(&b.q_cf, (size_t)P * max_iter * b.cap_q * sizeof(float4));
+  A(&b.q_ok, (size_t)P * max_iter * b.cap_q * sizeof(int8_t));
+  A(&b.part, (size_t)P * b.gq * 28 * sizeof(double));
+  A(&b.done, (size_t)P * sizeof(int));
+  if (A.err != hipSuccess) {
+    od_free(b);
+    return A.err;
+  }
+  if (A.err == hipSuccess) A.err = hipMemset(b.done, 0, (size_t)P * sizeof(int));
+  if (A.err == hipSuccess) A.err = hipMemset(b.state, 0, (size_t)P * kOdStateFloats * sizeof(float));
+  if (A.err == hipSuccess) A.err = hipMemset(b.istate, 0, (size_t)P * kOdStateInts * sizeof(int));
+  if (A.err == hipSuccess) A.err = hipMemset(b.nlast, 0, (size_t)P * 4 * sizeof(int));
+  if (A.err == hipSuccess) A.err = hipMemset(b.nfullEnd, 0, (size_t)P * 2 * sizeof(int));
+  if (A.err == hipSuccess) A.err = hipMemset(b.hC_T, 0, (size_t)2 * P * sizeof(int));
+  if (A.err == hipSuccess) A.err = hipMemset(b.hS_T, 0, (size_t)2 * P * sizeof(int));
+  if (A.err != hipSuccess) od_free(b);
+  return A.err;
 }
 
 void od_free(OdBuffers& b) {
@@ -847,8 +829,3 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
 }
 }  // namespace loam
 
-#ifdef LOAM_EXP_ASSOCPH
-extern "C" int loam_debug_assoc(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(loam::g_aph), 8 * sizeof(unsigned long long)) == hipSuccess ? 0 : -3;
-}
-#endif

@@ -15,7 +15,10 @@ __host__ __device__ inline int chunks_of(int cap) { return (cap + kChunk - 1) / 
 constexpr int kOdSum = 6, kOdMatP = 12, kOdImu = 48, kOdStateFloats = 64;
 // per-problem int state
 enum { kIsDegenerate = 0, kIsCornerLastNum, kIsSurfLastNum, kIsIters, kIsAssoc, kIsRows, kIsQueries,
-       kIsErr, kIsActive, kIsStop, kOdStateInts = 16 };
+       kIsErr, kIsActive, kIsStop,
+       kIsDegSteps,  // L-M updates of this frame projected by the iteration-0 degeneracy analysis (Q15)
+       kIsNanSkips,  // L-M updates of this frame skipped by the NaN guard (Q16)
+       kOdStateInts = 16 };
 
 // read-only view of one feature set per problem (stride = elements between problems)
 struct FeatView {
@@ -78,7 +81,7 @@ __global__ void k_hash_build(HashJob j);
 
 __global__ void k_od_end(OdBuffers b, FeatView f, int dst, int mode, int do_full);
 
-void od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter);
+hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter);  // on failure: freed, b empty
 void od_free(OdBuffers& b);
 void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st);
 // the laserOdometry L-M loop + pose accumulation for every problem against Last[last_buf]

@@ -31,26 +31,6 @@ namespace loam {
 
 namespace {
 
-#ifdef LOAM_EXP_PHASES
-// diagnostic build only: per-phase cycle sums of select_ring (tools/exp_phases.py)
-__device__ unsigned long long g_phase[8];
-#define PH(k)                                                   \
-  if (!BIG && threadIdx.x == 0) {                               \
-    const long long now = clock64();                            \
-    atomicAdd(&g_phase[k], (unsigned long long)(now - ph_t));   \
-    ph_t = now;                                                 \
-  }
-// k_sr_pick phases per wave (select_segment_fast<SR > 0>, k_sr_pick)
-#define PPH(k)                                                          \
-  if (lane_id() == 0) {                                                 \
-    const long long now = clock64();                                    \
-    atomicAdd(&g_phase[k], (unsigned long long)(now - pph_t));          \
-    pph_t = now;                                                        \
-  }
-#else
-#define PH(k)
-#define PPH(k)
-#endif
 
 LOAM_D int ring_id(const SrParams& p, float angle) {
   if (p.ring_model == LOAM_RING_LINEAR) {
@@ -66,11 +46,9 @@ LOAM_D int ring_id(const SrParams& p, float angle) {
 // 1e-4 degrees of it, so whenever a +-1e-3 degree bracket around it maps to one ring the double
 // evaluation cannot land elsewhere; only points that close to a ring boundary pay for it.
 LOAM_D int ring_of(const SrParams& p, float px, float py, float pz) {
-#ifndef LOAM_EXP_RINGF64
   const float af = atanf(py / sqrtf(px * px + pz * pz)) * 57.2957795f;
   const int lo = ring_id(p, af - 1e-3f), hi = ring_id(p, af + 1e-3f);
   if (lo == hi) return lo;
-#endif
   return ring_id(p, (float)(atan(D(py) / sqrt(D(px * px + pz * pz))) * 180 / M_PI));
 }
 
@@ -307,13 +285,7 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_sort(SrBuffers b, SrPara
 // and scatters with the same wave-ballot ranks.  src/scanRegistration.cpp:225-357
 // A tile is kRingE sub-tiles of kSrThreads points (each thread's kRingE loads in flight at once),
 // which also cuts the per-tile fixed work (sweep ends, start orientation, tile prefix) kRingE-fold.
-#ifdef LOAM_EXP_RINGE1
-constexpr int kRingE = 1;
-#elif defined(LOAM_EXP_RINGE8)
-constexpr int kRingE = 8;
-#else
 constexpr int kRingE = 4;
-#endif
 constexpr int kRingTile = kSrThreads * kRingE;
 
 __global__ __launch_bounds__(kSrThreads) void k_sr_ring_count(SrBuffers b, SrParams p) {
@@ -490,11 +462,7 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_scatter(SrBuffers b, SrP
 
 // ---------------------------------------------------------------- curvature + marks
 constexpr int kFeatTile = 256;  // threads
-#ifdef LOAM_EXP_FEATE1
-constexpr int kFeatE = 1;
-#else
 constexpr int kFeatE = 4;  // points per thread
-#endif
 constexpr int kFeatSpan = kFeatTile * kFeatE;
 
 __global__ __launch_bounds__(kFeatTile) void k_sr_features(SrBuffers b, SrParams p) {
@@ -645,7 +613,6 @@ LOAM_D int ring_vg(const float4* pts, int lo, const CandT* cand, int nc, uint64_
       }
       const int divx = maxb[0] - minb[0] + 1, divy = maxb[1] - minb[1] + 1;
       const int mul1 = divx, mul2 = divx * divy;
-#ifndef LOAM_EXP_VGOLD
       if constexpr (!BIG) {
         // Candidates come in ring order, so consecutive ones mostly share a voxel (~2.2 per run on
         // VLP-16): sort the runs, (voxel, first candidate, length), instead of the candidates.
@@ -720,7 +687,6 @@ LOAM_D int ring_vg(const float4* pts, int lo, const CandT* cand, int nc, uint64_
         }
         nout = run;
       } else
-#endif
       {
         const int P2c = next_pow2(nc);
         for (int t = tid; t < P2c; t += kSelThreads) {
@@ -805,9 +771,6 @@ LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, 
                                 int8_t* lab, int wlo, int* picks, int& nsharp, int& nlsharp, int& nflat,
                                 const float* crin = nullptr, Pre pre = Pre()) {
   const int lane = lane_id();
-#ifdef LOAM_EXP_PHASES
-  long long pph_t = clock64();
-#endif
   float cr[SR > 0 ? SR : 1];
   if constexpr (SR > 0) {
 #pragma unroll
@@ -836,9 +799,7 @@ LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, 
   pre();
   __threadfence_block();
   __builtin_amdgcn_wave_barrier();
-  if constexpr (SR > 0) { PPH(0); }
   if (m > 1) wave_sort_u64(list, m);
-  if constexpr (SR > 0) { PPH(1); }
   int largest = 0;
   bool done = false;
   for (int base = m - 1; base >= 0 && !done; base -= 64) {  // from the largest curvature down
@@ -870,7 +831,6 @@ LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, 
       remaining &= ~((2ull << f) - 1ull);
     }
   }
-  if constexpr (SR > 0) { PPH(2); }
   // flat: the unmarked point of smallest (curvature, position) below 0.1, four times at most
   for (int smallest = 0;;) {
     uint64_t best = ~0ull;
@@ -905,7 +865,6 @@ LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, 
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
   }
-  if constexpr (SR > 0) { PPH(3); }
 }
 
 // ring sort key: segment (3 bits) | curvature bits (32) | position in the ring (29)
@@ -926,9 +885,6 @@ template <int CAP, bool BIG, bool SIDX>
 LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq, SelShared<CAP, SIDX>& sh, int slot) {
   using CandT = typename std::conditional<BIG, int, uint16_t>::type;
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-#ifdef LOAM_EXP_PHASES
-  long long ph_t = clock64();
-#endif
   const float4* pts = b.full + (size_t)s * b.cap;
   const float* curv = b.curv + (size_t)s * b.cap;
   const int sq = sh.se[q], eq = sh.se[R + q];
@@ -1022,11 +978,9 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
     keys[t] = key;
   }
   __syncthreads();
-  PH(0);
   if constexpr (BIG) block_bitonic_sort<kSelThreads>(keys, P2);
   else reg_bitonic_sort<kSelThreads, CAP / kSelThreads>(keys, P2);
   }
-  PH(1);
   if (w == 0) {
     int run = 0;
     for (int j = 0; j < 6; ++j) {
@@ -1115,7 +1069,6 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
     if (lane == 0) sh.ncand = run;
   }
   __syncthreads();
-  PH(2);
   if (SIDX && seq) {  // the ring's sortInd after its six sorts, for the next ring (one workgroup, ordered)
     for (int t = tid; t < len; t += kSelThreads)
       b.sortind[(size_t)s * b.cap + lo + t] = sidx[keys[t] & kPosMask];
@@ -1124,7 +1077,6 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
   // ---- PCL VoxelGrid 0.2 of the ring's lessFlat candidates (:575-579)
   const int nout = ring_vg<CAP, BIG>(pts, lo, cand, sh.ncand, keys, b.st_lflat + (size_t)s * R * kRingCap + loff,
                                      BIG ? R * kRingCap - loff : kRingCap, sh.red, sh.scratch, b.err + s);
-  PH(3);
   // pick lists -> staging
   const int ns = sh.nsharp, nl = sh.nlsharp, nf = sh.nflat;
   for (int t = tid; t < ns; t += kSelThreads) b.st_sharp[(size_t)(s * R + q) * kSharpPerRing + t] = sh.picks[t];
@@ -1142,7 +1094,6 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
   }
   __threadfence();
   __syncthreads();
-  PH(6);
 }
 
 // ---------------------------------------------------------------- selection split: picks / VoxelGrid
@@ -1157,11 +1108,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
 // exactly as before (sel_big).
 constexpr int kPickCap = 2048;
 constexpr int kPickWaves = 4;
-#ifdef LOAM_EXP_PICKW3
-constexpr int kPickWpe = 3;
-#else
 constexpr int kPickWpe = 4;  // <= 128 VGPRs: four waves per SIMD (the LDS allows four workgroups per CU)
-#endif
 constexpr int kPickSegRegs = (kPickCap / 6 + 2 + 63) / 64;  // a segment of a <= kPickCap ring, per lane
 
 struct PickWave {
@@ -1187,26 +1134,6 @@ LOAM_D int sweep_route(const SrBuffers& b, int s, int R, int n, int cap, int* se
   }
   __syncthreads();
   int next = 0;
-#ifdef LOAM_EXP_ROUTESER
-  if (tid == 0) {
-    // rings are independent when their active spans [start, end-1] are more than 5 points apart
-    int wf = 1, prev_hi = -100000, maxspan = 0, na = 0;
-    for (int r = 0; r < R; ++r)
-      if (se[r] <= se[R + r] - 1) order[na++] = r;
-    for (int a = 1; a < na; ++a) {
-      int v = order[a], c = a;
-      while (c > 0 && se[order[c - 1]] > se[v]) { order[c] = order[c - 1]; --c; }
-      order[c] = v;
-    }
-    for (int a = 0; a < na; ++a) {
-      const int lo = se[order[a]], hi = se[R + order[a]] - 1;
-      if (lo < 0 || hi >= n || lo - prev_hi <= 5) wf = 0;
-      maxspan = max(maxspan, hi - lo + 1);
-      prev_hi = hi;
-    }
-    if (n > 0 && (!wf || maxspan > cap)) next = 1;
-  }
-#else
   (void)order;
   if (tid < 64) {  // R <= 64
     const int r = tid;
@@ -1229,15 +1156,11 @@ LOAM_D int sweep_route(const SrBuffers& b, int s, int R, int n, int cap, int* se
     const bool wf = __ballot(fail) == 0;
     if (n > 0 && (!wf || maxspan > cap)) next = 1;
   }
-#endif
   return next;
 }
 
 __global__ __launch_bounds__(64 * kPickWaves) __attribute__((amdgpu_waves_per_eu(kPickWpe))) void k_sr_pick(SrBuffers b, SrParams p) {
   const int s = blockIdx.y, tid = threadIdx.x, w = tid >> 6, lane = lane_id(), R = p.R;
-#ifdef LOAM_EXP_PHASES
-  long long pph_t = clock64();
-#endif
   const int q = blockIdx.x * kPickWaves + w;
   __shared__ int se[128], order[64], sh_route;
   __shared__ PickWave pw[kPickWaves];
@@ -1262,7 +1185,6 @@ __global__ __launch_bounds__(64 * kPickWaves) __attribute__((amdgpu_waves_per_eu
   }
   const int wlo = max(0, lo - 5), whi = min(n - 1, hi + 5);
   const uint8_t* pick_g = b.picked + (size_t)s * b.cap;
-  PPH(5);
   for (int k = wlo + lane; k <= whi; k += 64) {
     P.pk[k - wlo] = pick_g[k];
     P.lab[k - wlo] = 0;
@@ -1273,7 +1195,6 @@ __global__ __launch_bounds__(64 * kPickWaves) __attribute__((amdgpu_waves_per_eu
   const float* cv = b.curv + (size_t)s * b.cap + lo;
   uint16_t* cand = b.st_cand + (size_t)(s * R + q) * kRingCap;
   int run = 0;
-  PPH(6);
   // each segment's curvatures are loaded while the previous segment is walked
   float cra[kPickSegRegs], crb[kPickSegRegs];
   auto load_seg = [&](int j, float* cr) {
@@ -1292,18 +1213,10 @@ __global__ __launch_bounds__(64 * kPickWaves) __attribute__((amdgpu_waves_per_eu
     };
     if (s1 - 1 < s0) pre();
     if (s1 - 1 >= s0) {
-#ifdef LOAM_EXP_PICKG
-    select_segment_fast(n, lo, s0 - lo, s1 - 1 - lo, cv, P.list, P.pk, P.lab, wlo, P.picks, P.nsharp, P.nlsharp,
-                        P.nflat);
-#else
     select_segment_fast<kPickSegRegs>(n, lo, s0 - lo, s1 - 1 - lo, cv, P.list, P.pk, P.lab, wlo, P.picks, P.nsharp,
                                       P.nlsharp, P.nflat, cra, pre);
-#endif
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-#ifdef LOAM_EXP_PHASES
-    pph_t = clock64();
-#endif
     // (:568-572) lessFlat candidates of this segment, in position order
     for (int base = s0; base < s1; base += 64) {
       const int k = base + lane;
@@ -1312,7 +1225,6 @@ __global__ __launch_bounds__(64 * kPickWaves) __attribute__((amdgpu_waves_per_eu
       if (flag) cand[run + __popcll(m & lanemask_lt())] = (uint16_t)(k - lo);
       run += __popcll(m);
     }
-    PPH(4);
     }
 #pragma unroll
     for (int k = 0; k < kPickSegRegs; ++k) cra[k] = crb[k];
@@ -1450,42 +1362,45 @@ __global__ __launch_bounds__(256) void k_sr_compact(SrBuffers b, SrParams p) {
 
 #define HIPCHK(x) (void)(x)
 
-void sr_alloc(SrBuffers& b, int S, int cap, int R) {
+hipError_t sr_alloc(SrBuffers& b, int S, int cap, int R) {
+  DevAlloc A;
   b.S = S; b.cap = cap; b.R = R;
   const size_t n = (size_t)S * cap;
-  HIPCHK(hipMalloc(&b.raw, n * sizeof(float4)));
-  HIPCHK(hipMalloc(&b.raw_n, S * sizeof(int)));
-  HIPCHK(hipMalloc(&b.tmp_ori, n * sizeof(float)));
-  HIPCHK(hipMalloc(&b.tmp_sid, n));
-  HIPCHK(hipMalloc(&b.tilecnt, (size_t)S * b.ntiles() * R * sizeof(int)));
-  HIPCHK(hipMalloc(&b.tileF, (size_t)S * b.ntiles() * sizeof(int)));
-  HIPCHK(hipMalloc(&b.sweep_ori, (size_t)S * 2 * sizeof(float)));
-  HIPCHK(hipMalloc(&b.full, n * sizeof(float4)));
-  HIPCHK(hipMalloc(&b.n_full, S * sizeof(int)));
-  HIPCHK(hipMalloc(&b.curv, n * sizeof(float)));
-  HIPCHK(hipMalloc(&b.picked, n));
-  HIPCHK(hipMalloc(&b.sortind, n * sizeof(int)));
-  HIPCHK(hipMalloc(&b.label, n));
-  HIPCHK(hipMalloc(&b.ring_se, (size_t)S * 2 * R * sizeof(int)));
-  HIPCHK(hipMalloc(&b.st_sharp, (size_t)S * R * kSharpPerRing * sizeof(int)));
-  HIPCHK(hipMalloc(&b.st_lsharp, (size_t)S * R * kLessSharpPerRing * sizeof(int)));
-  HIPCHK(hipMalloc(&b.st_flat, (size_t)S * R * kFlatPerRing * sizeof(int)));
-  HIPCHK(hipMalloc(&b.st_lflat, (size_t)S * R * kRingCap * sizeof(float4)));
-  HIPCHK(hipMalloc(&b.st_cnt, (size_t)S * R * 4 * sizeof(int)));
-  HIPCHK(hipMalloc(&b.st_cand, (size_t)S * R * kRingCap * sizeof(uint16_t)));
-  HIPCHK(hipMalloc(&b.st_ncand, (size_t)S * R * sizeof(int)));
-  HIPCHK(hipMalloc(&b.sharp, (size_t)S * R * kSharpPerRing * sizeof(float4)));
-  HIPCHK(hipMalloc(&b.lsharp, (size_t)S * R * kLessSharpPerRing * sizeof(float4)));
-  HIPCHK(hipMalloc(&b.flat, (size_t)S * R * kFlatPerRing * sizeof(float4)));
-  HIPCHK(hipMalloc(&b.lflat, n * sizeof(float4)));
-  HIPCHK(hipMalloc(&b.cnt, (size_t)S * 4 * sizeof(int)));
-  HIPCHK(hipMalloc(&b.err, S * sizeof(int)));
-  HIPCHK(hipMalloc(&b.sel_big, S * sizeof(int)));
-  HIPCHK(hipMalloc(&b.st_loff, (size_t)S * R * sizeof(int)));
+  A(&b.raw, n * sizeof(float4));
+  A(&b.raw_n, S * sizeof(int));
+  A(&b.tmp_ori, n * sizeof(float));
+  A(&b.tmp_sid, n);
+  A(&b.tilecnt, (size_t)S * b.ntiles() * R * sizeof(int));
+  A(&b.tileF, (size_t)S * b.ntiles() * sizeof(int));
+  A(&b.sweep_ori, (size_t)S * 2 * sizeof(float));
+  A(&b.full, n * sizeof(float4));
+  A(&b.n_full, S * sizeof(int));
+  A(&b.curv, n * sizeof(float));
+  A(&b.picked, n);
+  A(&b.sortind, n * sizeof(int));
+  A(&b.label, n);
+  A(&b.ring_se, (size_t)S * 2 * R * sizeof(int));
+  A(&b.st_sharp, (size_t)S * R * kSharpPerRing * sizeof(int));
+  A(&b.st_lsharp, (size_t)S * R * kLessSharpPerRing * sizeof(int));
+  A(&b.st_flat, (size_t)S * R * kFlatPerRing * sizeof(int));
+  A(&b.st_lflat, (size_t)S * R * kRingCap * sizeof(float4));
+  A(&b.st_cnt, (size_t)S * R * 4 * sizeof(int));
+  A(&b.st_cand, (size_t)S * R * kRingCap * sizeof(uint16_t));
+  A(&b.st_ncand, (size_t)S * R * sizeof(int));
+  A(&b.sharp, (size_t)S * R * kSharpPerRing * sizeof(float4));
+  A(&b.lsharp, (size_t)S * R * kLessSharpPerRing * sizeof(float4));
+  A(&b.flat, (size_t)S * R * kFlatPerRing * sizeof(float4));
+  A(&b.lflat, n * sizeof(float4));
+  A(&b.cnt, (size_t)S * 4 * sizeof(int));
+  A(&b.err, S * sizeof(int));
+  A(&b.sel_big, S * sizeof(int));
+  A(&b.st_loff, (size_t)S * R * sizeof(int));
   b.big_stride = next_pow2(cap);
-  HIPCHK(hipMalloc(&b.big_keys, (size_t)kBigSlots * b.big_stride * sizeof(uint64_t)));
-  HIPCHK(hipMalloc(&b.big_sidx, (size_t)kBigSlots * b.big_stride * sizeof(int)));
-  HIPCHK(hipMalloc(&b.big_cand, (size_t)kBigSlots * b.big_stride * sizeof(int)));
+  A(&b.big_keys, (size_t)kBigSlots * b.big_stride * sizeof(uint64_t));
+  A(&b.big_sidx, (size_t)kBigSlots * b.big_stride * sizeof(int));
+  A(&b.big_cand, (size_t)kBigSlots * b.big_stride * sizeof(int));
+  if (A.err != hipSuccess) sr_free(b);
+  return A.err;
 }
 
 void sr_free(SrBuffers& b) {
@@ -1505,24 +1420,16 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
   if (p.imu) {
     hipLaunchKernelGGL(k_sr_ring_sort<true>, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
   } else {
-#ifdef LOAM_EXP_RINGWG
-    hipLaunchKernelGGL(k_sr_ring_sort<false>, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
-#else
     const int rtiles = (b.cap + kRingTile - 1) / kRingTile;  // <= b.ntiles(): tilecnt rows fit
     hipLaunchKernelGGL(k_sr_ring_count, dim3(rtiles, b.S), dim3(kSrThreads), 0, st, b, p);
     hipLaunchKernelGGL(k_sr_ring_scatter, dim3(rtiles, b.S), dim3(kSrThreads), 0, st, b, p);
-#endif
   }
   mark("k_sr_ring_sort");
   hipLaunchKernelGGL(k_sr_features, dim3((b.cap + kFeatSpan - 1) / kFeatSpan, b.S), dim3(kFeatTile), 0,
                      st, b, p);
   mark("k_sr_features");
-#ifdef LOAM_EXP_NOSPLIT
-  hipLaunchKernelGGL((k_sr_select<2048, 0>), dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
-#else
   hipLaunchKernelGGL(k_sr_pick, dim3((b.R + kPickWaves - 1) / kPickWaves, b.S), dim3(64 * kPickWaves), 0, st, b, p);
   hipLaunchKernelGGL(k_sr_ringvg, dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
-#endif
   hipLaunchKernelGGL((k_sr_select<kRingCap, 1>), dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
   hipLaunchKernelGGL((k_sr_select<16, 2>), dim3(kBigSlots), dim3(kSelThreads), 0, st, b, p);
   mark("k_sr_select");
@@ -1532,8 +1439,3 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
 
 }  // namespace loam
 
-#ifdef LOAM_EXP_PHASES
-extern "C" int loam_debug_phases(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(loam::g_phase), 8 * sizeof(unsigned long long)) == hipSuccess ? 0 : -3;
-}
-#endif

@@ -20,7 +20,10 @@
 //     other three files) binds the C double function, so the expression around it is evaluated in
 //     double and rounded once on assignment to float — written here with explicit (double) casts;
 //   * double literals (0.1, 1.8, 25.0, M_PI, ...) promote their expression to double.
-// IMU input (§8f) is not modelled yet: the IMU terms are carried with their zero values.
+// IMU input (§8f rank 1) is modelled: scanRegistration's imuHandler queue, per-point de-skew and
+// /imu_trans (src/scanRegistration.cpp:68-209, 286-349, 614-660), the odometry IMU terms
+// (src/laserOdometry.cpp:196-254, 330-354) and the mapping roll / pitch blend
+// (src/laserMapping.cpp:199-226, 323-335).
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -450,6 +453,7 @@ struct OdState {
   float imuVeloFromStartX = 0, imuVeloFromStartY = 0, imuVeloFromStartZ = 0;
   // stats
   uint64_t iters = 0, assoc = 0, rows_sum = 0, queries = 0;
+  uint64_t deg_steps = 0, nan_skips = 0;  // updates through the degeneracy projection / NaN guard
 };
 
 // :101-124
@@ -845,10 +849,13 @@ void od_lm(const Cfg& cfg, OdState& s, const std::vector<P>& sharp, const std::v
     }
     float X[6];
     lm_solve(A, B, pointSelNum, iterCount, 10.0f, s.isDegenerate, s.matP, X);
+    if (s.isDegenerate) s.deg_steps++;
     bool nan = std::isnan(X[0]) || std::isnan(X[1]) || std::isnan(X[2]) || std::isnan(X[3]) ||
                std::isnan(X[4]) || std::isnan(X[5]);
     if (!nan)  // :799-811 NaN guard (Q16)
       for (int q = 0; q < 6; ++q) transform[q] += X[q];
+    else
+      s.nan_skips++;
     float deltaR = delta_r(X), deltaT = delta_t(X);
     if (D(deltaR) < 0.1 && D(deltaT) < 0.1) break;
   }
@@ -937,6 +944,7 @@ struct MpState {
   bool isDegenerate = false;
   float matP[36] = {0};
   uint64_t iters = 0, rows_sum = 0, stack = 0, map_points = 0, valid_points = 0;
+  uint64_t deg_steps = 0, shifts = 0;  // updates through the degeneracy projection / slab shifts
   // laserMapping's IMU queue (:101-108), fed by its imuHandler (:323-335)
   int imuFront = 0, imuLast = -1;
   double imuTime[kImuQue] = {0};
@@ -1117,12 +1125,12 @@ void mp_body(const Cfg& cfg, MpState& m, const std::vector<P>& cornerLast,
   point_associate_to_map(T, onY, onY);
   int cI = cube_of(T[3], m.cenW), cJ = cube_of(T[4], m.cenH), cK = cube_of(T[5], m.cenD);
   // :454-614
-  while (cI < 3) { shift_axis(m, 0, +1); cI++; m.cenW++; }
-  while (cI >= kW - 3) { shift_axis(m, 0, -1); cI--; m.cenW--; }
-  while (cJ < 3) { shift_axis(m, 1, +1); cJ++; m.cenH++; }
-  while (cJ >= kH - 3) { shift_axis(m, 1, -1); cJ--; m.cenH--; }
-  while (cK < 3) { shift_axis(m, 2, +1); cK++; m.cenD++; }
-  while (cK >= kDp - 3) { shift_axis(m, 2, -1); cK--; m.cenD--; }
+  while (cI < 3) { shift_axis(m, 0, +1); cI++; m.cenW++; m.shifts++; }
+  while (cI >= kW - 3) { shift_axis(m, 0, -1); cI--; m.cenW--; m.shifts++; }
+  while (cJ < 3) { shift_axis(m, 1, +1); cJ++; m.cenH++; m.shifts++; }
+  while (cJ >= kH - 3) { shift_axis(m, 1, -1); cJ--; m.cenH--; m.shifts++; }
+  while (cK < 3) { shift_axis(m, 2, +1); cK++; m.cenD++; m.shifts++; }
+  while (cK >= kDp - 3) { shift_axis(m, 2, -1); cK--; m.cenD--; m.shifts++; }
 
   // :616-672 FOV cube selection
   std::vector<int> valid, surround;
@@ -1283,6 +1291,7 @@ void mp_body(const Cfg& cfg, MpState& m, const std::vector<P>& cornerLast,
       }
       float X[6];
       lm_solve(A, Bv, selNum, iterCount, 100.0f, m.isDegenerate, m.matP, X);
+      if (m.isDegenerate) m.deg_steps++;
       for (int q = 0; q < 6; ++q) T[q] += X[q];
       float deltaR = delta_r(X), deltaT = delta_t(X);
       if (D(deltaR) < 0.05 && D(deltaT) < 0.05) break;
@@ -1384,7 +1393,10 @@ struct Oracle {
   std::vector<P> surround;  // /laser_cloud_surround of the last mapping frame
   bool surround_pub = false;
   loam_stats stats;
-  explicit Oracle(const Cfg& c) : cfg(c) { std::memset(&stats, 0, sizeof(stats)); }
+  explicit Oracle(const Cfg& c) : cfg(c) {
+    std::memset(&stats, 0, sizeof(stats));
+    od.frameCount = c.skip_frame_num;  // int frameCount = skipFrameNum (src/laserOdometry.cpp:407)
+  }
 };
 
 int write_cloud(const std::vector<P>& v, loam_cloud_out* o) {
@@ -1458,12 +1470,14 @@ int oracle_odometry(void* h, double stamp, const loam_features* in, loam_pose6* 
     d.imuShiftFromStartX = t[6]; d.imuShiftFromStartY = t[7]; d.imuShiftFromStartZ = t[8];
     d.imuVeloFromStartX = t[9]; d.imuVeloFromStartY = t[10]; d.imuVeloFromStartZ = t[11];
   }
-  uint64_t it0 = o->od.iters, as0 = o->od.assoc, rs0 = o->od.rows_sum, q0 = o->od.queries;
+  uint64_t it0 = o->od.iters, as0 = o->od.assoc, rs0 = o->od.rows_sum, q0 = o->od.queries,
+           dg0 = o->od.deg_steps, ns0 = o->od.nan_skips;
   o->stats.od_corner_last = o->od.cornerLast.size();
   o->stats.od_surf_last = o->od.surfLast.size();
   od_body(o->cfg, o->od, oi, oo);
   o->stats.od_iters = o->od.iters - it0; o->stats.od_assoc_rounds = o->od.assoc - as0;
   o->stats.od_rows_sum = o->od.rows_sum - rs0; o->stats.od_queries = o->od.queries - q0;
+  o->stats.od_degenerate_steps = o->od.deg_steps - dg0; o->stats.od_nan_skips = o->od.nan_skips - ns0;
   {
     const uint64_t as = o->stats.od_assoc_rounds, it = o->stats.od_iters, nq = as ? o->stats.od_queries / as : 0;
     o->stats.od_query_iters = nq * it;
@@ -1490,11 +1504,12 @@ int oracle_mapping(void* h, double stamp, const loam_pose6* odom_sum, const loam
   std::vector<P> cl = read_cloud(corner_last), sl = read_cloud(surf_last), fl = read_cloud(full_end);
   MpOut mo;
   uint64_t it0 = o->mp.iters, rs0 = o->mp.rows_sum, st0 = o->mp.stack, mp0 = o->mp.map_points,
-           vp0 = o->mp.valid_points;
+           vp0 = o->mp.valid_points, dg0 = o->mp.deg_steps, sh0 = o->mp.shifts;
   mp_body(o->cfg, o->mp, cl, sl, fl, mo, stamp);
   o->stats.mp_iters = o->mp.iters - it0; o->stats.mp_rows_sum = o->mp.rows_sum - rs0;
   o->stats.mp_stack = o->mp.stack - st0; o->stats.mp_map_points = o->mp.map_points - mp0;
   o->stats.mp_map_valid_points = o->mp.valid_points - vp0;
+  o->stats.mp_degenerate_steps = o->mp.deg_steps - dg0; o->stats.mp_grid_shifts = o->mp.shifts - sh0;
   from6(mo.aft, aft);
   from6(mo.bef, bef);
   o->surround.swap(mo.surround);
@@ -1609,6 +1624,8 @@ int oracle_problem(const loam_config* cfg, loam_cloud_in prev, loam_cloud_in cur
     }
     st->mp_iters = mp.iters; st->mp_rows_sum = mp.rows_sum; st->mp_stack = mp.stack;
     st->mp_map_points = mp.map_points; st->mp_map_valid_points = mp.valid_points;
+    st->od_degenerate_steps = od.deg_steps; st->od_nan_skips = od.nan_skips;
+    st->mp_degenerate_steps = mp.deg_steps; st->mp_grid_shifts = mp.shifts;
   }
   return LOAM_OK;
 }

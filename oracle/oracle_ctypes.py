@@ -52,7 +52,9 @@ class Stats(ctypes.Structure):
         "od_assoc_points",
         "mp_iters", "mp_rows_sum", "mp_stack", "mp_map_points", "mp_map_valid_points", "mp_stack_iters",
         "mp_fits", "od_query_iters", "od_row_evals",
-        "bytes_sr", "bytes_od", "bytes_mp")] + [(n, ctypes.c_double) for n in ("ms_sr", "ms_od", "ms_mp")]
+        "bytes_sr", "bytes_od", "bytes_mp")] + [(n, ctypes.c_double) for n in ("ms_sr", "ms_od", "ms_mp")] + \
+        [(n, ctypes.c_uint64) for n in ("od_degenerate_steps", "od_nan_skips", "mp_degenerate_steps",
+                                        "mp_grid_shifts")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

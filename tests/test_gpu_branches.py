@@ -1,0 +1,146 @@
+"""GPU parity on the reference branches the default streams never reach, and on the node outputs
+themselves (not only the poses that consume them).  Engine (C-ABI via ctypes) against the CPU
+oracle on identical inputs; the branch counters of loam_stats show that each branch was taken on
+both sides the same number of times.
+
+  recentring        src/laserMapping.cpp:446-614 (Q23)
+  degeneracy        src/laserOdometry.cpp:770-797, src/laserMapping.cpp:927-954 (Q15)
+  NaN guard         src/laserOdometry.cpp:799-811 (Q16)
+  node clouds       /laser_cloud_corner_last, /laser_cloud_surf_last, /velodyne_cloud_3
+                    (src/laserOdometry.cpp:875-930), /velodyne_cloud_registered
+                    (src/laserMapping.cpp:1060-1069), /laser_cloud_surround (:1038-1058)
+  skipFrameNum      src/laserOdometry.cpp:407, 885-891
+  large batches     config 4 at 768 problems (batch-scaled indexing)
+
+Tolerances: clouds bit-exact in x, y, z (intensity within 2e-6 where it carries relTime, exact
+after TransformToEnd); poses within the north-star 1e-4 m / 1e-4 rad (BASELINE.json)."""
+import numpy as np
+import pytest
+
+import scenarios
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-4
+INT_TOL = 2e-6
+
+
+def _cloud_eq(a, b, name):
+    assert a.shape == b.shape, f"{name}: {a.shape} vs {b.shape}"
+    np.testing.assert_array_equal(a[:, :3], b[:, :3], err_msg=name)
+    if a.shape[0]:
+        assert np.max(np.abs(a[:, 3] - b[:, 3])) <= INT_TOL, name
+
+
+def _compare_streams(rg, ro, *, counters=True):
+    assert len(rg) == len(ro)
+    nmap = 0
+    for g, o in zip(rg, ro):
+        assert g["k"] == o["k"] and g["pub"] == o["pub"], (g["k"], g["pub"], o["pub"])
+        if g["pub"] & 1:
+            assert np.abs(g["pose"] - o["pose"]).max() <= POSE_TOL, (g["k"], g["pose"], o["pose"])
+        if g["pub"] & 2:
+            _cloud_eq(g["corner_last"], o["corner_last"], f"corner_last@{g['k']}")
+            _cloud_eq(g["surf_last"], o["surf_last"], f"surf_last@{g['k']}")
+        if g["pub"] & 4:
+            _cloud_eq(g["full_end"], o["full_end"], f"full_end@{g['k']}")
+        if counters:
+            assert (g["od_deg"], g["od_nan"], g["od_iters"]) == (o["od_deg"], o["od_nan"], o["od_iters"]), g["k"]
+        assert ("aft" in g) == ("aft" in o)
+        if "aft" in g:
+            nmap += 1
+            assert np.abs(g["aft"] - o["aft"]).max() <= POSE_TOL, (g["k"], g["aft"], o["aft"])
+            assert np.abs(g["bef"] - o["bef"]).max() <= POSE_TOL, g["k"]
+            _cloud_eq(g["registered"], o["registered"], f"registered@{g['k']}")
+            assert (g["surround"] is None) == (o["surround"] is None), g["k"]
+            if o["surround"] is not None:
+                np.testing.assert_array_equal(g["surround"], o["surround"], err_msg=f"surround@{g['k']}")
+            if counters:
+                assert (g["mp_deg"], g["mp_shifts"], g["mp_iters"]) == (o["mp_deg"], o["mp_shifts"], o["mp_iters"]), \
+                    (g["k"], g["mp_deg"], g["mp_shifts"], g["mp_iters"], o["mp_deg"], o["mp_shifts"], o["mp_iters"])
+    return nmap
+
+
+def _both(loam, oc, sweeps, cfg_kw=None, **kw):
+    cfg_kw = dict(cfg_kw or {})
+    cfg_kw.setdefault("system_delay", 1)
+    rg = scenarios.run_stream(loam.Engine(loam.default_config(**cfg_kw)), sweeps, **kw)
+    ro = scenarios.run_stream(oc.Oracle(oc.default_config(**cfg_kw)), sweeps, **kw)
+    return rg, ro
+
+
+def test_node_clouds_bitexact(loam, oc, sg):
+    """every published odometry cloud, every registered cloud and surround map of 30 sweeps"""
+    rg, ro = _both(loam, oc, sg.stream_sweeps(30, 1))
+    assert _compare_streams(rg, ro) >= 12
+    assert sum(1 for r in rg if r["pub"] & 4) >= 12
+
+
+def test_grid_recentring_parity(loam, oc, sg):
+    rg, ro = _both(loam, oc, sg.stream_sweeps(34, 1), jumps=scenarios.GRID_JUMPS)
+    assert _compare_streams(rg, ro) >= len(scenarios.GRID_JUMPS)
+    shifts = [r["mp_shifts"] for r in rg if "aft" in r]
+    assert sum(shifts) >= 40 and max(shifts) == 16, shifts
+
+
+def test_degeneracy_stream_parity(loam, oc, sg):
+    sweeps = [scenarios.ground_only(s) for s in sg.stream_sweeps(16, 1)]
+    rg, ro = _both(loam, oc, sweeps)
+    _compare_streams(rg, ro)
+    assert sum(r["od_deg"] for r in rg) > 0
+    assert sum(r.get("mp_deg", 0) for r in rg) > 0
+
+
+def test_degeneracy_batch_parity(loam, oc, sg):
+    prev, cur = sg.single_problem(0)
+    prevs = [scenarios.ground_only(prev), scenarios.ground_only(prev, -1.2), prev]
+    curs = [scenarios.ground_only(cur), scenarios.ground_only(cur, -1.2), cur]
+    e = loam.Engine()
+    e.batch_upload(prevs, curs)
+    e.batch_run()
+    od, aft, st = e.batch_download()
+    tot = {"od_degenerate_steps": 0, "mp_degenerate_steps": 0, "od_nan_skips": 0}
+    for i in range(3):
+        od_o, aft_o, st_o = oc.problem(prevs[i], curs[i])
+        assert np.abs(od[i] - od_o).max() <= POSE_TOL, i
+        assert np.abs(aft[i] - aft_o).max() <= POSE_TOL, i
+        for k in tot:
+            tot[k] += st_o[k]
+    for k, v in tot.items():
+        assert st[k] == v, (k, st[k], v)
+    assert tot["od_degenerate_steps"] > 0 and tot["mp_degenerate_steps"] > 0
+
+
+def test_nan_guard_parity(loam, oc, sg):
+    rg, ro = _both(loam, oc, sg.stream_sweeps(10, 1), inject_nan_at=4)
+    _compare_streams(rg, ro)
+    hit = [r for r in rg if r["od_nan"]]
+    assert len(hit) == 1 and hit[0]["od_nan"] == 25
+
+
+@pytest.mark.parametrize("skip", [0, 2])
+def test_skip_frame_num_parity(loam, oc, sg, skip):
+    rg, ro = _both(loam, oc, sg.stream_sweeps(12, 1), {"skip_frame_num": skip})
+    _compare_streams(rg, ro)
+    assert [r["pub"] for r in rg[1:4]] == ([7, 7, 7] if skip == 0 else [7, 1, 1])
+
+
+def test_batch_768_parity(loam, oc, sg):
+    """batch-scaled indexing: 768 problems in one launch sequence; problems spread over the whole
+    batch (the last ones included) against the oracle, and the last 64 against their own batch"""
+    P = 768
+    prevs, curs = sg.batch_problems(P, base_seed=1000)
+    e = loam.Engine()
+    e.batch_upload(prevs, curs)
+    e.batch_run()
+    od, aft, st = e.batch_download()
+    assert np.all(np.isfinite(od)) and np.all(np.isfinite(aft))
+    for i in list(range(0, P, 24)) + [P - 2, P - 1]:
+        od_o, aft_o, _ = oc.problem(prevs[i], curs[i])
+        assert max(np.abs(od[i] - od_o).max(), np.abs(aft[i] - aft_o).max()) <= POSE_TOL, i
+    e2 = loam.Engine()
+    e2.batch_upload(prevs[-64:], curs[-64:])
+    e2.batch_run()
+    od2, aft2, _ = e2.batch_download()
+    np.testing.assert_array_equal(od[-64:], od2)
+    np.testing.assert_array_equal(aft[-64:], aft2)

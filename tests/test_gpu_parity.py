@@ -214,6 +214,7 @@ def test_golden_config3_stream(loam, sg):
             assert np.abs(r["od"] - np.float32(g["od_sum"])).max() <= POSE_TOL
         if "aft" in g:
             assert np.abs(r["aft"] - np.float32(g["aft"])).max() <= POSE_TOL
+            assert r["reg"] == g["registered_sha256"]   # /velodyne_cloud_registered, bit-exact
             assert r["sur"] == g.get("surround_sha256")
 
 
