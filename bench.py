@@ -3,17 +3,28 @@ MI355X, BASELINE.json config 4 shape: independent synthetic VLP-16 problems, sha
 
 One step = one pass of the whole hot path over this rank's batch of problems, inputs resident in
 HBM: scan registration of both sweeps of every problem, odometry seeded from prev and solved on
-cur, mapping of prev into an empty map and solved for cur.  Weak scaling: every
-rank owns --batch problems (seeds 1000 + global index); the data path has no collective; one RCCL
+cur, mapping of prev into an empty map and solved for cur.  Sharding: contiguous
+ranges of problems per rank (seeds 1000 + global index), no collective on the data path; one
 all-gather of the poses after the timed steps.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--cpu-seconds S]
+  --split weak   (default, the `value`): every rank owns --batch problems
+  --split strong (reported beside it in "strong", or as `value` when chosen): --global-batch
+                 problems in total (BASELINE config 4: 1024), global_batch / N per rank
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--split weak|strong]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+With --gpus N > 1 and no WORLD_SIZE in the environment the script launches the N ranks itself
+(torch.distributed.run as a child process; the parent touches no GPU).  Ranks use RCCL ("nccl")
+when a GPU is present, gloo otherwise (the CPU test harness).
 """
 import argparse
+import hashlib
 import importlib
 import json
 import os
+import statistics
+import subprocess
 import sys
 import time
 
@@ -24,28 +35,57 @@ sys.path.insert(0, ROOT)
 
 METRIC = "scans/sec (odometry+mapping L-M solve) VLP-16 sweep, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# chip-wide rate of rows gathered from an XCD's L2 (MI355X_MICROARCH.md, "Indexed rows: gather into
+# LDS": 16.8-18.8 TB/s): the ceiling of the search kernels, whose gathers hit L2, not HBM
+L2_GATHER_PEAK_GBS = 16800.0
+BASE_SEED = 1000
+
+
+def shard(rank, world, batch, split, global_batch):
+    """(first global problem index, problems) owned by `rank`: weak = `batch` per rank, strong =
+    `global_batch` split into contiguous equal ranges"""
+    if split == "weak":
+        return rank * batch, batch
+    if global_batch % world:
+        raise ValueError(f"global batch {global_batch} does not split over {world} ranks")
+    per = global_batch // world
+    return rank * per, per
 
 
 def kernel_bytes(st):
-    """Algorithmic HBM bytes of each kernel over one step of the whole batch (SURVEY.md §8(d),
-    split by the kernel that moves them)."""
+    """Bytes each kernel moves over one step of the whole batch, split by the kernel that moves them
+    (DESIGN.md §4).  Streaming kernels: the algorithmic bytes of SURVEY.md §8(d).  Search kernels
+    (k_od_assoc, k_mp_nn): the bytes they actually gather, from the engine's work counters (cells,
+    candidates, window points, chunk boxes), since their cost is the search, not the algorithmic
+    16 B per query."""
     feats = 16 * (st["n_sharp"] + st["n_less_sharp"] + st["n_flat"] + st["n_less_flat"])
     return {
         "k_sr_ring_sort": 16 * st["n_raw"] + 16 * st["n_ring"],
         "k_sr_features": 16 * st["n_ring"],
         "k_sr_select": 16 * st["n_ring"] + feats,
-        "k_od_solve": st["bytes_od"],
+        # per query and round: its point (16 B), 27 bucket bounds (8 B each), the three indices
+        # written (12 B); plus every Last point (16 B) and chunk box (32 B) loaded
+        "k_od_assoc": (16 + 27 * 8 + 12) * st["od_queries"] + 16 * st["od_assoc_gathered"]
+                      + 32 * st["od_assoc_boxes"],
         # per iteration: every stored row's coefficient (16 B) + accept flag (1 B) read back (Q12:
         # all rows so far re-evaluated at the current transform), the query point read (16 B) and
         # its coefficient + flag written (17 B)
         "k_od_rows": 17 * st["od_row_evals"] + 33 * st["od_query_iters"],
-        # per iteration: stack point 16 B (k_mp_nn), 5 neighbours 80 B read and the row (16 B point +
-        # 16 B coeff) written (k_mp_fit)
-        "k_mp_nn": 16 * st["mp_stack_iters"],
-        "k_mp_fit": 80 * st["mp_stack_iters"] + 32 * st["mp_rows_sum"],
-        # rows read back for JtJ
-        "k_mp_iter": 32 * st["mp_rows_sum"],
+        # per query-iteration: stack point read, ordered 5-NN written and last iteration's read
+        # (16 + 32 + 32 B); 8 B per bucket range and 16 B per map point evaluated (seeds included)
+        "k_mp_nn": 80 * st["mp_stack_iters"] + 8 * st["mp_nn_cells"] + 16 * st["mp_nn_candidates"],
+        # per query-iteration: 5-NN read (32 B), stack point (16 B), stored fit (64 B), row
+        # written (17 B); per refit: 5 neighbours (80 B) and the fit written (64 B)
+        "k_mp_fit": 129 * st["mp_stack_iters"] + 144 * st["mp_fits"],
+        # per query-iteration: accept flag, stack point and coefficient read back for JtJ
+        "k_mp_iter": 33 * st["mp_stack_iters"],
     }
+
+
+# what bounds each kernel in practice (DESIGN.md §4): the roofline is priced against HBM, but the
+# search kernels are limited by dependent gathers, not bandwidth
+LIMITED_BY = {"k_mp_nn": "latency (dependent gathers)", "k_od_assoc": "latency (dependent gathers)",
+              "k_sr_select": "latency (serial greedy picks)", "k_mp_fit": "latency (gathers + VALU)"}
 
 
 def stream_leg(loam, sg, n_sweeps, n_cpu):
@@ -69,95 +109,247 @@ def stream_leg(loam, sg, n_sweeps, n_cpu):
     warm = loam.Engine(loam.default_config(system_delay=1))
     run(warm, sweeps[:6])
     pg, ng, tg = run(loam.Engine(loam.default_config()), sweeps)
-    out = {"config": "config3: VLP-16 stream (seed 1), systemDelay 20, mapping every 2nd frame",
+    out = {"config": f"config3: VLP-16 stream (seed 1), {n_sweeps} sweeps, systemDelay 20, mapping every 2nd frame",
            "sweeps_processed": ng, "scans_per_s": ng / tg, "ms_per_sweep": 1e3 * tg / max(ng, 1)}
     if n_cpu > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_ctypes as oc
-        po, no, tc = run(oc.Oracle(oc.default_config()), sweeps[:n_cpu])
+        with pinned_core() as core:
+            po, no, tc = run(oc.Oracle(oc.default_config()), sweeps[:n_cpu])
         k = min(len(po), len(pg))
-        out["cpu_oracle"] = {"sweeps_processed": no, "scans_per_s": no / tc, "cores": 1, "kind": "port"}
+        out["cpu_oracle"] = {"sweeps_processed": no, "scans_per_s": no / tc, "cores": 1, "kind": "port",
+                             "pinned_cpu": core}
         out["speedup_vs_cpu"] = out["scans_per_s"] / out["cpu_oracle"]["scans_per_s"]
         out["max_abs_err_mapping"] = float(np.abs(pg[:k] - po[:k]).max()) if k else None
     return out
 
 
-def main():
+def latency_leg(loam, sg, runs, warmup):
+    """Config 2: one VLP-16 problem (prev, cur) at a time, warm (context and buffers reused), the
+    whole problem on the device per call; ms per problem (median of `runs`)"""
+    prev, cur = sg.single_problem(0)
+    eng = loam.Engine()
+    eng.batch_upload([prev], [cur])
+    for _ in range(warmup):
+        eng.batch_run()
+        eng.sync()
+    ts = []
+    for _ in range(runs):
+        a = time.perf_counter()
+        eng.batch_run()
+        eng.sync()
+        ts.append(time.perf_counter() - a)
+    od, aft, _ = eng.batch_download()
+    eng.close()
+    return {"config": "config2: one VLP-16 problem (seed 0), warm context, inputs resident",
+            "ms_median": 1e3 * statistics.median(ts), "ms_min": 1e3 * min(ts), "runs": runs}, (prev, cur, od, aft)
+
+
+class pinned_core:
+    """pin the calling thread to one core for the CPU baseline (taskset -c 0)"""
+
+    def __enter__(self):
+        self.old = os.sched_getaffinity(0)
+        self.core = min(self.old)
+        os.sched_setaffinity(0, {self.core})
+        return self.core
+
+    def __exit__(self, *a):
+        os.sched_setaffinity(0, self.old)
+
+
+def cpu_leg(oc, prevs, curs, od, aft, n_sample, reps):
+    """The oracle (single-thread C++ restatement), pinned to one core, over a bounded sample of the
+    batch's problems spread across it: 1 warm-up run, then the median of `reps` runs (BASELINE.md
+    §2).  Also checks the engine's poses of the sampled problems against the oracle."""
+    B = len(prevs)
+    idx = sorted(set(int(round(v)) for v in np.linspace(0, B - 1, min(n_sample, B))))
+    times = []
+    err_od = err_mp = 0.0
+    with pinned_core() as core:
+        for r in range(reps + 1):
+            a = time.perf_counter()
+            outs = [oc.problem(prevs[i], curs[i]) for i in idx]
+            t = time.perf_counter() - a
+            if r == 0:
+                for i, (od_o, aft_o, _) in zip(idx, outs):
+                    err_od = max(err_od, float(np.abs(od[i] - od_o).max()))
+                    err_mp = max(err_mp, float(np.abs(aft[i] - aft_o).max()))
+            else:
+                times.append(t)
+    med = statistics.median(times)
+    model = "unknown CPU"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    cpu = {"value": len(idx) / med, "unit": "scans/s", "cores": 1, "kind": "port",
+           "sample": f"{len(idx)} problems spread over the batch (global indices {idx[0]}..{idx[-1]}), "
+                     f"oracle/liboracle.so -O3, one thread pinned to CPU {core} of {model} "
+                     f"({os.cpu_count()} logical CPUs visible); median of {reps} runs after 1 warm-up, "
+                     f"{med:.2f} s per run (runs: {', '.join(f'{t:.2f}' for t in times)})"}
+    parity = {"problems_checked": len(idx), "max_abs_err_odometry": err_od, "max_abs_err_mapping": err_mp}
+    return cpu, parity
+
+
+def engine_factory():
+    """the engine under measurement: libloam_hip.so through its ctypes binding.  LOAM_BENCH_ENGINE
+    ("module:attr") substitutes a stand-in for the harness tests on CPU-only machines (gloo);
+    it is never set for a measurement."""
+    spec = os.environ.get("LOAM_BENCH_ENGINE")
+    if spec:
+        mod, attr = spec.split(":")
+        return getattr(importlib.import_module(mod), attr)
+    return importlib.import_module("loam_velodyne-1_amd").Engine
+
+
+def timed(eng, steps, warmup, dist, sync_dev):
+    """W untimed steps, then exactly K steps between barrier + sync; the max over ranks (s)"""
+    for _ in range(warmup):
+        eng.batch_run()
+    eng.sync()
+    if dist:
+        dist.barrier()
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.batch_run()
+    eng.sync()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=sync_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    return elapsed
+
+
+def gather_poses(dist, od, aft, world, dev):
+    """the one collective of the sharded path: every rank's (odometry, mapping) poses, in global
+    problem order (RCCL all-gather on GPUs)"""
+    import torch
+    mine = torch.from_numpy(np.concatenate([od, aft], axis=1).astype(np.float32)).to(dev)
+    if dev == "cpu":  # gloo
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine)
+        return torch.cat(parts).numpy()
+    allp = torch.empty((world * mine.shape[0], 12), dtype=torch.float32, device=dev)
+    dist.all_gather_into_tensor(allp, mine)
+    return allp.cpu().numpy()
+
+
+def spawn(args_list, n):
+    """launch n ranks of this script (torch.distributed.run) as a child; returns its exit code"""
+    port = os.environ.get("MASTER_PORT", "29511")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", port, os.path.abspath(__file__)] + args_list
+    return subprocess.call(cmd)
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1024, help="problems per GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--batch", type=int, default=1024, help="problems per GPU (weak split)")
+    ap.add_argument("--global-batch", type=int, default=1024, help="problems in total (strong split)")
+    ap.add_argument("--split", choices=("weak", "strong"), default="weak", help="which split is `value`")
+    ap.add_argument("--strong-leg", type=int, default=1, help="also measure the other split (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=32, help="problems in the CPU baseline sample (0: skip)")
+    ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--profile-steps", type=int, default=3)
-    ap.add_argument("--stream-sweeps", type=int, default=120, help="config-3 streaming leg (0: skip)")
-    ap.add_argument("--stream-cpu-sweeps", type=int, default=40)
-    args = ap.parse_args()
+    ap.add_argument("--stream-sweeps", type=int, default=220, help="config-3 streaming leg (0: skip)")
+    ap.add_argument("--stream-cpu-sweeps", type=int, default=60)
+    ap.add_argument("--latency-runs", type=int, default=50, help="config-2 warm latency leg (0: skip)")
+    argv = sys.argv[1:] if argv is None else argv
+    args = ap.parse_args(argv)
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn(argv, args.gpus))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dist, dev = None, "cpu"
     if world > 1:
         import torch
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+            dev = f"cuda:{local}"
+            tdist.init_process_group("nccl")
+        else:  # CPU-only harness test
+            tdist.init_process_group("gloo")
         dist = tdist
 
-    loam = importlib.import_module("loam_velodyne-1_amd")
+    Engine = engine_factory()
     sg = importlib.import_module("loam_velodyne-1_amd.synthgen")
 
-    B = args.batch
-    prevs, curs = sg.batch_problems(B, base_seed=1000 + rank * B)
-    eng = loam.Engine(device=local)
-    eng.batch_upload(prevs, curs)
+    def leg(split):
+        first, B = shard(rank, world, args.batch, split, args.global_batch)
+        prevs, curs = sg.batch_problems(B, base_seed=BASE_SEED + first)
+        eng = Engine(device=local)
+        eng.batch_upload(prevs, curs)
+        elapsed = timed(eng, args.steps, args.warmup, dist, dev)
+        od, aft, st = eng.batch_download()
+        return {"first": first, "B": B, "prevs": prevs, "curs": curs, "eng": eng, "elapsed": elapsed,
+                "od": od, "aft": aft, "st": st}
 
-    def sync():
-        eng.sync()
+    main_leg = leg(args.split)
+    other = None
+    same = shard(rank, world, args.batch, "weak", args.global_batch) == \
+        shard(rank, world, args.batch, "strong", args.global_batch)
+    if args.strong_leg and same:  # the other split is this very workload (N = 1, batch = global batch)
+        other = {"split": "strong" if args.split == "weak" else "weak", "global_batch": world * main_leg["B"],
+                 "problems_per_gpu": main_leg["B"], "value": world * main_leg["B"] * args.steps / main_leg["elapsed"],
+                 "ms_per_step": main_leg["elapsed"] / args.steps * 1e3, "note": "same workload as value"}
+    elif args.strong_leg:
+        other_split = "strong" if args.split == "weak" else "weak"
+        o = leg(other_split)
+        o["eng"].close()
+        other = {"split": other_split, "global_batch": world * o["B"], "problems_per_gpu": o["B"],
+                 "value": world * o["B"] * args.steps / o["elapsed"], "ms_per_step": o["elapsed"] / args.steps * 1e3}
+    if args.strong_leg and world == 1 and args.global_batch % 8 == 0:
+        # the per-GPU share of config 4 on 8 GPUs (1024 / 8), measured on one GPU
+        first, B8 = shard(0, 8, args.batch, "strong", args.global_batch)
+        prevs, curs = sg.batch_problems(B8, base_seed=BASE_SEED + first)
+        e8 = Engine(device=local)
+        e8.batch_upload(prevs, curs)
+        el = timed(e8, args.steps, args.warmup, None, dev)
+        e8.close()
+        other["one_gpu_at_8gpu_share"] = {"problems": B8, "value": B8 * args.steps / el,
+                                          "ms_per_step": el / args.steps * 1e3}
 
-    for _ in range(args.warmup):
-        eng.batch_run()
-    sync()
-
-    if dist:
-        dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.batch_run()
-    sync()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        dist.barrier()
-
-    od, aft, st = eng.batch_download()
+    eng, B, elapsed, st = main_leg["eng"], main_leg["B"], main_leg["elapsed"], main_leg["st"]
+    od, aft = main_leg["od"], main_leg["aft"]
 
     # host-buffer rate (DESIGN.md §7): the same batch handed over from host memory, upload + one step
     a = time.perf_counter()
-    eng.batch_upload(prevs, curs)
-    sync()
+    eng.batch_upload(main_leg["prevs"], main_leg["curs"])
+    eng.sync()
     upload_s = time.perf_counter() - a
 
     # per-kernel device times of the same workload (HIP events on the engine stream), untimed
-    eng.set_profiling(True)
-    for _ in range(args.profile_steps):
-        eng.batch_run()
-    eng.batch_download()
-    ktimes = eng.kernel_times()
-    eng.set_profiling(False)
+    # (the profiling pass also runs the search kernels' counting variants: their work counters, which
+    # kernel_bytes needs, come from this pass, st_prof)
+    ktimes, st_prof = {}, st
+    if args.profile_steps > 0:
+        eng.set_profiling(True)
+        for _ in range(args.profile_steps):
+            eng.batch_run()
+        _, _, st_prof = eng.batch_download()
+        ktimes = eng.kernel_times()
+        eng.set_profiling(False)
 
-    if dist:  # the one collective: gather every rank's poses (RCCL all-gather)
-        import torch
-        mine = torch.from_numpy(np.concatenate([od, aft], axis=1).astype(np.float32)).to(f"cuda:{local}")
-        allp = torch.empty((world * B, 12), dtype=torch.float32, device=f"cuda:{local}")
-        dist.all_gather_into_tensor(allp, mine)
-        torch.cuda.synchronize()
+    gathered = None
+    if dist:
+        gathered = gather_poses(dist, od, aft, world, dev)
 
     if rank != 0:
         if dist:
@@ -166,16 +358,17 @@ def main():
 
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
+    psteps = max(args.profile_steps, 1)
 
-    # roofline of the dominant kernel: algorithmic bytes per launch / average launch duration
-    kb = kernel_bytes(st)
+    # roofline of the dominant kernel: bytes per launch / average launch duration
+    kb = kernel_bytes(st_prof)
     dom = max(ktimes.items(), key=lambda kv: kv[1][0])[0] if ktimes else None
     roof = None
     if dom:
         tot_ms, launches = ktimes[dom]
         avg_ms = tot_ms / max(launches, 1)
         nbytes = kb.get(dom)
-        launches_per_step = launches / max(args.profile_steps, 1)
+        launches_per_step = launches / psteps
         per_launch = nbytes / launches_per_step if nbytes is not None else None
         achieved = per_launch / (avg_ms * 1e-3) / 1e9 if per_launch is not None else None
         traffic = None
@@ -185,52 +378,57 @@ def main():
                 traffic = json.load(open(tpath)).get(dom)
             except Exception:
                 traffic = None
-        roof = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        roof = {"kernel": dom, "bound": "hbm", "limited_by": LIMITED_BY.get(dom, "hbm"),
+                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved is not None else None,
-                "traffic": traffic, "avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": per_launch}
+                "traffic": traffic, "avg_launch_ms": avg_ms, "bytes_per_launch": per_launch,
+                "bytes_model": "gathered bytes from the engine's work counters (bench.kernel_bytes)"
+                if dom in ("k_mp_nn", "k_od_assoc") else "algorithmic bytes (SURVEY.md §8(d))"}
+        if dom in ("k_mp_nn", "k_od_assoc") and achieved is not None:
+            roof["l2_gather_peak"] = L2_GATHER_PEAK_GBS
+            roof["l2_frac"] = achieved / L2_GATHER_PEAK_GBS
 
-    # CPU baseline: the oracle (single-thread C++ restatement) on a bounded sample, N=1 only
-    cpu = None
-    parity = None
-    if world == 1 and args.cpu_seconds > 0:
+    # CPU baseline: the oracle on a bounded sample, N=1 only
+    cpu = parity = None
+    if world == 1 and args.cpu_sample > 0 and not os.environ.get("LOAM_BENCH_ENGINE"):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_ctypes as oc
-        n_done, t_cpu, err_od, err_mp = 0, 0.0, 0.0, 0.0
-        while n_done < B and (t_cpu < args.cpu_seconds or n_done < 4):
-            a = time.perf_counter()
-            od_o, aft_o, _ = oc.problem(prevs[n_done], curs[n_done])
-            t_cpu += time.perf_counter() - a
-            err_od = max(err_od, float(np.abs(od[n_done] - od_o).max()))
-            err_mp = max(err_mp, float(np.abs(aft[n_done] - aft_o).max()))
-            n_done += 1
-        model = "unknown CPU"
-        try:
-            for line in open("/proc/cpuinfo"):
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
-        except OSError:
-            pass
-        cpu = {"value": n_done / t_cpu, "unit": "scans/s", "cores": 1, "kind": "port",
-               "sample": f"first {n_done} problems of the batch (seeds 1000..{999 + n_done}), "
-                         f"oracle/liboracle.so -O3 single thread on {model} ({os.cpu_count()} logical CPUs "
-                         f"visible), {t_cpu:.1f} s"}
-        parity = {"problems_checked": n_done, "max_abs_err_odometry": err_od, "max_abs_err_mapping": err_mp}
+        cpu, parity = cpu_leg(oc, main_leg["prevs"], main_leg["curs"], od, aft, args.cpu_sample, args.cpu_reps)
 
-    stage_ms = {k: round(v[0] / max(args.profile_steps, 1), 4) for k, v in sorted(ktimes.items())}
-    # the same achieved-vs-peak figure for every kernel with an algorithmic byte count
+    stage_ms = {k: round(v[0] / psteps, 4) for k, v in sorted(ktimes.items())}
     roof_all = {}
     for k, nbytes in kb.items():
         if k in ktimes and ktimes[k][0] > 0:
-            gbs = nbytes / (ktimes[k][0] / max(args.profile_steps, 1) * 1e-3) / 1e9  # bytes per step / s per step
+            gbs = nbytes / (ktimes[k][0] / psteps * 1e-3) / 1e9  # bytes per step / s per step
             roof_all[k] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-                           "ms_per_step": round(ktimes[k][0] / max(args.profile_steps, 1), 4)}
+                           "ms_per_step": round(ktimes[k][0] / psteps, 4),
+                           "bytes_per_step": int(nbytes), "limited_by": LIMITED_BY.get(k, "hbm")}
+    # the whole pipeline against HBM: SURVEY.md §8(d)'s algorithmic bytes per step / step time
+    alg = int(st["bytes_sr"] + st["bytes_od"] + st["bytes_mp"])
+    pipeline = {"algorithmic_bytes_per_step": alg, "achieved_gbs": alg / (ms_per_step * 1e-3) / 1e9,
+                "frac": alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "kernel_busy_ms_per_step": round(sum(v[0] for v in ktimes.values()) / psteps, 4) if ktimes else None}
 
-    # single-stream latency path (BASELINE configs 2/3): one context fed sweep by sweep through the
-    # node-level C-ABI with host buffers in and out, as the ROS nodes would call it (not the metric)
-    stream = None
-    if world == 1 and args.stream_sweeps > 0:
-        stream = stream_leg(loam, sg, args.stream_sweeps, args.stream_cpu_sweeps)
+    stream = latency = None
+    if world == 1 and not os.environ.get("LOAM_BENCH_ENGINE"):
+        loam = importlib.import_module("loam_velodyne-1_amd")
+        if args.stream_sweeps > 0:
+            stream = stream_leg(loam, sg, args.stream_sweeps, args.stream_cpu_sweeps)
+        if args.latency_runs > 0:
+            latency, (p0, c0, od0, aft0) = latency_leg(loam, sg, args.latency_runs, 5)
+            if args.cpu_sample > 0:
+                sys.path.insert(0, os.path.join(ROOT, "oracle"))
+                import oracle_ctypes as oc
+                with pinned_core():
+                    ts = []
+                    for _ in range(4):
+                        a = time.perf_counter()
+                        od_o, aft_o, _ = oc.problem(p0, c0)
+                        ts.append(time.perf_counter() - a)
+                cpu_ms = 1e3 * statistics.median(ts[1:])
+                latency["cpu_oracle_ms"] = cpu_ms
+                latency["speedup_vs_cpu"] = cpu_ms / latency["ms_median"]
+                latency["max_abs_err"] = float(max(np.abs(od0[0] - od_o).max(), np.abs(aft0[0] - aft_o).max()))
     out = {
         "metric": METRIC,
         "value": value,
@@ -240,27 +438,37 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.split == "weak" else "strong",
         "vs_baseline": None,
         "dtype": "fp32 (fp64 JtJ accumulation)",
         "data": "synthetic (seeded VLP-16 ray-cast sweeps, random planes+edges scenes; bags unavailable offline)",
         "config": {"workload": "config4: independent VLP-16 problems (SR prev+cur, odometry L-M, mapping L-M)",
                    "problems_per_gpu": B, "global_batch": world * B, "points_per_sweep": 28800,
-                   "parallelism": f"shard{world}"},
+                   "split": args.split, "parallelism": f"shard{world}"},
         "roofline": roof,
         "roofline_kernels": roof_all,
+        "pipeline": pipeline,
         "cpu_baseline": cpu,
         "parity": parity,
+        "strong" if args.split == "weak" else "weak": other,
         "kernel_ms_per_step": stage_ms,
         "single_stream": stream,
+        "latency": latency,
+        "gathered": {"problems": int(gathered.shape[0]),
+                     "sha1": hashlib.sha1(np.ascontiguousarray(gathered, np.float32).tobytes()).hexdigest()}
+        if gathered is not None else None,
         "host_upload": {"ms": upload_s * 1e3, "pcie_inclusive_value": B / (upload_s + ms_per_step * 1e-3),
                         "note": "rank 0; pageable host sweeps packed and copied per sweep; not the metric"},
         "workload_stats": {"od_iters_mean": st["od_iters"] / B, "mp_iters_mean": st["mp_iters"] / B,
                            "mp_stack_mean": st["mp_stack"] / B, "mp_map_points_mean": st["mp_map_points"] / B,
                            "od_queries_mean": st["od_queries"] / B,
-                           "mp_fit_fraction": st["mp_fits"] / max(st["mp_stack_iters"], 1)},
+                           "mp_fit_fraction": st["mp_fits"] / max(st["mp_stack_iters"], 1),
+                           "mp_nn_candidates_per_query": st_prof["mp_nn_candidates"] / max(st["mp_stack_iters"], 1),
+                           "mp_nn_cells_per_query": st_prof["mp_nn_cells"] / max(st["mp_stack_iters"], 1),
+                           "od_assoc_points_per_query": st_prof["od_assoc_gathered"] / max(st["od_queries"], 1),
+                           "od_assoc_boxes_per_query": st_prof["od_assoc_boxes"] / max(st["od_queries"], 1)},
     }
-    print(json.dumps(out))
+    print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -104,6 +104,11 @@ typedef struct {
   uint64_t od_nan_skips;        /* odometry L-M updates skipped by the NaN guard (:799-811, Q16) */
   uint64_t mp_degenerate_steps; /* mapping L-M updates projected (src/laserMapping.cpp:927-954) */
   uint64_t mp_grid_shifts;      /* cube-grid slab shifts of the recentring (:454-614, Q23) */
+  /* memory work the search kernels actually did (the bench's gathered-byte roofline) */
+  uint64_t mp_nn_candidates;    /* map points whose distance the 5-NN evaluated (incl. the seeds) */
+  uint64_t mp_nn_cells;         /* hash bucket ranges the 5-NN read */
+  uint64_t od_assoc_gathered;   /* Last-cloud points the association loaded (cells, fallback, windows) */
+  uint64_t od_assoc_boxes;      /* 64-point chunk boxes the association loaded */
 } loam_stats;
 
 typedef struct loam_ctx loam_ctx;

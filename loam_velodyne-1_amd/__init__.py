@@ -74,12 +74,13 @@ STAT_U64 = ("n_raw", "n_ring", "n_sharp", "n_less_sharp", "n_flat", "n_less_flat
 
 
 STAT_BRANCH = ("od_degenerate_steps", "od_nan_skips", "mp_degenerate_steps", "mp_grid_shifts")
+STAT_WORK = ("mp_nn_candidates", "mp_nn_cells", "od_assoc_gathered", "od_assoc_boxes")
 
 
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in STAT_U64] + \
                [(n, ctypes.c_double) for n in ("ms_sr", "ms_od", "ms_mp")] + \
-               [(n, ctypes.c_uint64) for n in STAT_BRANCH]
+               [(n, ctypes.c_uint64) for n in STAT_BRANCH + STAT_WORK]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

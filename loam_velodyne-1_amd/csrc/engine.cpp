@@ -433,6 +433,8 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
   x->stats.od_queries = ist[kIsQueries];
   x->stats.od_degenerate_steps = (uint64_t)ist[kIsDegSteps];
   x->stats.od_nan_skips = (uint64_t)ist[kIsNanSkips];
+  x->stats.od_assoc_gathered = (uint64_t)(uint32_t)ist[kIsGathered];
+  x->stats.od_assoc_boxes = (uint64_t)(uint32_t)ist[kIsBoxes];
   {
     const uint64_t nq = ist[kIsAssoc] ? (uint64_t)(ist[kIsQueries] / ist[kIsAssoc]) : 0, it = (uint64_t)ist[kIsIters];
     x->stats.od_query_iters = nq * it;
@@ -645,6 +647,8 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
     s.od_queries += q[kIsQueries];
     s.od_degenerate_steps += (uint64_t)q[kIsDegSteps];
     s.od_nan_skips += (uint64_t)q[kIsNanSkips];
+    s.od_assoc_gathered += (uint64_t)(uint32_t)q[kIsGathered];
+    s.od_assoc_boxes += (uint64_t)(uint32_t)q[kIsBoxes];
     const uint64_t nq = q[kIsAssoc] ? (uint64_t)(q[kIsQueries] / q[kIsAssoc]) : 0, it = (uint64_t)q[kIsIters];
     s.od_query_iters += nq * it;
     s.od_row_evals += nq * it * (it + 1) / 2;

@@ -607,7 +607,9 @@ __constant__ int kCellOrder[27] = {13, 4, 10, 12, 14, 16, 22, 1, 3, 5, 7, 9, 11,
 // expression), so every neighbour that can be accepted is found exactly.
 // t may arrive seeded with real map points (their distances to q): they bound the search from
 // the start and do not change the result.
-LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t) {
+// work: candidates evaluated + (bucket ranges read << kWorkCellShift), summed per lane
+constexpr int kWorkCellShift = 21;
+LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t, int& work) {
   if (T <= 0) return;
   const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
   const float gxl = q.x - (float)cx, gyl = q.y - (float)cy, gzl = q.z - (float)cz;
@@ -623,6 +625,7 @@ LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t) {
     if (bd >= 1.0f || bd > t.d[4]) continue;
     const uint32_t h = cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1);
     const int b0 = start[h], b1 = start[h + 1];
+    work += (b1 - b0) + (1 << kWorkCellShift);
     // four independent loads in flight per step: the loop is bound by gather latency
     for (int k = b0; k < b1; k += 4) {
       float4 a[4];
@@ -644,7 +647,7 @@ constexpr int kMpQueryThreads = 256;
 // the lane's LDS column (stride kMpQueryThreads).  Ranges are packed start:19 | count:13; a lane
 // whose ranges do not fit falls back to knn5.
 constexpr int kNnInFlight = 8;  // measured k_mp_nn ms/step: 2 -> 4.17, 4 -> 3.95, 8 -> 3.88, 16 -> 5.33
-LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5& t, uint32_t* lst) {
+LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5& t, uint32_t* lst, int& work) {
   if (T <= 0) return;
   const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
   const float gxl = q.x - (float)cx, gyl = q.y - (float)cy, gzl = q.z - (float)cz;
@@ -672,9 +675,10 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
     }
   }
   if (!fits) {
-    knn5(start, hp, T, q, t);
+    knn5(start, hp, T, q, t, work);
     return;
   }
+  work += total + (n << kWorkCellShift);
   int ci = 0, left = 0, pos = 0;
   auto next = [&]() {  // index of the lane's next candidate
     if (left == 0) {
@@ -717,6 +721,8 @@ __global__ void k_mp_lm_begin(MpBuffers b) {
   ist[kMiRows] = 0;
   ist[kMiFits] = 0;
   ist[kMiDegSteps] = 0;
+  ist[kMiNnCand] = 0;
+  ist[kMiNnCells] = 0;
 }
 
 // one L-M iteration's correspondences (:714-877) in two passes, lane per stack point (corner,
@@ -725,7 +731,10 @@ __global__ void k_mp_lm_begin(MpBuffers b) {
 // Jacobi) or plane (5x3 QR) through the 5 neighbours and the weighted residual.  A fit depends
 // on nothing but the ordered 5 neighbours, so it is kept per query and reused while the ordered
 // 5-NN is unchanged from the previous iteration (bit-identical to refitting).
-__global__ __launch_bounds__(kMpQueryThreads) void k_mp_nn(MpBuffers b) {
+// five waves per SIMD (<= 96 VGPRs; the LDS lists allow five workgroups per CU).  COUNT: the
+// profiling variant that also sums its work (candidates, bucket ranges) into the frame's istate
+template <bool COUNT>
+__global__ __launch_bounds__(kMpQueryThreads) __attribute__((amdgpu_waves_per_eu(5))) void k_mp_nn(MpBuffers b) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, tid = threadIdx.x;
   const int* ist = b.istate + (size_t)p * kMpStateInts;
@@ -746,6 +755,7 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_nn(MpBuffers b) {
   const float4* fromC = b.from + (size_t)p * b.map_cap;
   const float4* fromS = fromC + b.nfrom[p * 2 + 0];
   const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
+  int work = 0;  // work counter (loam_stats mp_nn_candidates / mp_nn_cells), packed as in knn5
   for (int q = blk.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
     const bool corner = q < nsc;
     const float4 sel = loampose::point_to_map(r, stack[corner ? q : b.capC + (q - nsc)]);
@@ -761,12 +771,19 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_nn(MpBuffers b) {
         if (prev[k] != 0x7fffffff) {
           const float4 a = from[prev[k]];
           top5_offer(t, sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z), prev[k]);
+          ++work;
         }
     }
-    if (corner) knn5_flat(hcs, hcp, TC, sel, t, lst);
-    else knn5_flat(hss, hsp, TS, sel, t, lst);
+    if (corner) knn5_flat(hcs, hcp, TC, sel, t, lst, work);
+    else knn5_flat(hss, hsp, TS, sel, t, lst, work);
     qnn[2 * q] = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
     qnn[2 * q + 1] = make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0);
+  }
+  if (!COUNT) return;
+  const int ncand = wave_sum(work & ((1 << kWorkCellShift) - 1)), ncell = wave_sum(work >> kWorkCellShift);
+  if (lane_id() == 0 && ncand) {
+    atomicAdd((int*)&ist[kMiNnCand], ncand);
+    atomicAdd((int*)&ist[kMiNnCells], ncell);
   }
 }
 
@@ -1413,7 +1430,8 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   const int gq = std::min(P >= 64 ? 24 : 64, (b.cap_stack + kMpQueryThreads - 1) / kMpQueryThreads);
   // an empty map store (the first frame after a reset) cannot run the L-M (:706): no launches
   for (int it = 0; it < (map_empty ? 0 : b.max_iter); ++it) {
-    hipLaunchKernelGGL(k_mp_nn, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
+    if (prof) hipLaunchKernelGGL(k_mp_nn<true>, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
+    else hipLaunchKernelGGL(k_mp_nn<false>, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
     mark("k_mp_nn");
     hipLaunchKernelGGL(k_mp_fit, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
     mark("k_mp_fit");
@@ -1522,6 +1540,8 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
     stats->mp_map_valid_points = (uint64_t)si[kMiValidPts];
     stats->mp_degenerate_steps = (uint64_t)si[kMiDegSteps];
     stats->mp_grid_shifts = (uint64_t)si[kMiShifts];
+    stats->mp_nn_candidates = (uint64_t)(uint32_t)si[kMiNnCand];
+    stats->mp_nn_cells = (uint64_t)(uint32_t)si[kMiNnCells];
     stats->ms_mp = ms;
   }
   return rc;
@@ -1654,6 +1674,8 @@ int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats*
       stats->mp_map_valid_points += (uint64_t)q[kMiValidPts];
       stats->mp_degenerate_steps += (uint64_t)q[kMiDegSteps];
       stats->mp_grid_shifts += (uint64_t)q[kMiShifts];
+      stats->mp_nn_candidates += (uint64_t)(uint32_t)q[kMiNnCand];
+      stats->mp_nn_cells += (uint64_t)(uint32_t)q[kMiNnCells];
     }
   }
   return LOAM_OK;

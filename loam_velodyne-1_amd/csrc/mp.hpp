@@ -22,8 +22,10 @@ enum { kMiCenW = 0, kMiCenH, kMiCenD, kMiDegen, kMiNValid, kMiIters, kMiRows, kM
        kMiFromS, kMiErr, kMiLmRan, kMiValidPts, kMiStop, kMiFits, kMiImu, kMiCubeI, kMiCubeJ, kMiCubeK,
        kMiDegSteps,  // L-M updates of this frame projected by the iteration-0 degeneracy analysis
        kMiShifts,    // cube-grid slab shifts of this frame's recentring (the reference's passes)
+       kMiNnCand,    // map points the 5-NN evaluated this frame (seeds included)
+       kMiNnCells,   // hash bucket ranges the 5-NN read this frame
        kMpStateInts = 24 };
-static_assert(kMiShifts < kMpStateInts, "istate layout");
+static_assert(kMiNnCells < kMpStateInts, "istate layout");
 
 // one mapping frame's inputs for every instance (device pointers)
 struct MpInput {

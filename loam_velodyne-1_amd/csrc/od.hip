@@ -150,7 +150,7 @@ LOAM_D float box_d2(const float4& lo, const float4& hi, const float4& s) {
 // 27 cells around q (cells whose box lies >= h away skipped); if the best is >= h, the chunk
 // boxes of the whole cloud closer than 5 m.  `cells` = per-wave LDS scratch of 64 ints.
 LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const float4* cloud, const float4* ch,
-                             int n, float h, float inv_h, float4 q, int* cells) {
+                             int n, float h, float inv_h, float4 q, int* cells, int& wpts, int& wbox) {
   const int lane = lane_id();
   const int cx = cell_of(q.x, inv_h), cy = cell_of(q.y, inv_h), cz = cell_of(q.z, inv_h);
   int bucket = -1, b0 = 0, cnt = 0;
@@ -168,6 +168,7 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
   // change a minimum)
   const int incl = wave_incl_scan(cnt);
   const int total = __shfl(incl, 63, 64);
+  wpts += total;
   if (lane < 32) { cells[lane] = lane < 27 ? incl - cnt : 0x7fffffff; cells[32 + lane] = b0; }
   __builtin_amdgcn_wave_barrier();
   uint64_t best = ~0ull;
@@ -192,9 +193,11 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
     const int k = k0 + lane;
     const bool need = k < nch && box_d2(ch[2 * k], ch[2 * k + 1], q) < 25.0f;
     uint64_t nb = __ballot(need);
+    wbox += min(64, nch - k0);
     while (nb) {
       const int c = k0 + __ffsll((unsigned long long)nb) - 1;
       nb &= nb - 1;
+      wpts += min(kChunk, n - c * kChunk);
       const int t = c * kChunk + lane;
       if (t < n) {
         const float4 a = cloud[t];
@@ -213,11 +216,13 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
 // with d < 25.  Whole 64-point chunks whose box is >= 5 m from sel are skipped; a chunk that may
 // hold the stop is always examined.
 template <typename F>
-LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int dir, int scan, float4 sel, F f) {
+LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int dir, int scan, float4 sel, int& wpts,
+                        int& wbox, F f) {
   const int lane = lane_id();
   auto stop_ring = [&](int r) { return dir > 0 ? D(r) > scan + 2.5 : D(r) < scan - 2.5; };
   // examines points [j0 .. j0 + dir * (cnt - 1)]; true when the stop was met
   auto run = [&](int j0, int cnt) {
+    wpts += cnt;
     const int j = j0 + dir * lane;
     const bool inr = lane < cnt;
     const float4 a = inr ? L[j] : make_float4(0, 0, 0, 0);
@@ -238,6 +243,7 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
     while (j < end) {
       const int k = (j / kChunk) + lane;
       const bool v = k * kChunk < end;
+      wbox += min(64, (end - j + kChunk - 1) / kChunk);
       float4 lo = make_float4(0, 0, 0, 0), hi = lo;
       if (v) { lo = ch[2 * k]; hi = ch[2 * k + 1]; }
       const uint64_t mc = __ballot(v && stop_ring((int)hi.w));
@@ -261,6 +267,7 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
     while (kt >= 0) {
       const int k = kt - lane;
       const bool v = k >= 0;
+      wbox += min(64, kt + 1);
       float4 lo = make_float4(0, 0, 0, 0), hi = lo;
       if (v) { lo = ch[2 * k]; hi = ch[2 * k + 1]; }
       const uint64_t mc = __ballot(v && stop_ring((int)lo.w));
@@ -281,7 +288,7 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
 // corner association (:478-527): closest (kd NN, sqDis < 25) and the best point of an adjacent
 // ring in the index window.  fwd_end = min(cornerPointsSharpNum, C) (Q11).
 LOAM_D void wave_assoc_corner(const float4* CL, const float4* ch, int fwd_end, uint64_t nn, float4 sel,
-                              int& ind1, int& ind2) {
+                              int& ind1, int& ind2, int& wpts, int& wbox) {
   ind1 = -1;
   ind2 = -1;
   if (nn == ~0ull) return;
@@ -290,13 +297,13 @@ LOAM_D void wave_assoc_corner(const float4* CL, const float4* ch, int fwd_end, u
   const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u);
   ind1 = c;
   uint64_t best = ~0ull;
-  wave_window(CL, ch, c, fwd_end, +1, scan, sel, [&](int j, int r, float d) {
+  wave_window(CL, ch, c, fwd_end, +1, scan, sel, wpts, wbox, [&](int j, int r, float d) {
     if (r > scan) {
       const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)(j - c - 1);
       best = key < best ? key : best;
     }
   });
-  wave_window(CL, ch, c, fwd_end, -1, scan, sel, [&](int j, int r, float d) {
+  wave_window(CL, ch, c, fwd_end, -1, scan, sel, wpts, wbox, [&](int j, int r, float d) {
     if (r < scan) {
       const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)((1u << 30) + (c - 1 - j));
       best = key < best ? key : best;
@@ -312,7 +319,7 @@ LOAM_D void wave_assoc_corner(const float4* CL, const float4* ch, int fwd_end, u
 // surface association (:590-650): closest, the best of the same / lower ring (min2) and of the
 // higher rings (min3) in the forward window; mirrored in the backward window.
 LOAM_D void wave_assoc_surf(const float4* SL, const float4* ch, int fwd_end, uint64_t nn, float4 sel,
-                            int& ind1, int& ind2, int& ind3) {
+                            int& ind1, int& ind2, int& ind3, int& wpts, int& wbox) {
   ind1 = ind2 = ind3 = -1;
   if (nn == ~0ull) return;
   const float d0 = __uint_as_float((uint32_t)(nn >> 32));
@@ -320,12 +327,12 @@ LOAM_D void wave_assoc_surf(const float4* SL, const float4* ch, int fwd_end, uin
   const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u);
   ind1 = c;
   uint64_t best2 = ~0ull, best3 = ~0ull;
-  wave_window(SL, ch, c, fwd_end, +1, scan, sel, [&](int j, int r, float d) {
+  wave_window(SL, ch, c, fwd_end, +1, scan, sel, wpts, wbox, [&](int j, int r, float d) {
     const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)(j - c - 1);
     if (r <= scan) best2 = key < best2 ? key : best2;
     else best3 = key < best3 ? key : best3;
   });
-  wave_window(SL, ch, c, fwd_end, -1, scan, sel, [&](int j, int r, float d) {
+  wave_window(SL, ch, c, fwd_end, -1, scan, sel, wpts, wbox, [&](int j, int r, float d) {
     const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)((1u << 30) + (c - 1 - j));
     if (r >= scan) best2 = key < best2 ? key : best2;
     else best3 = key < best3 ? key : best3;
@@ -368,6 +375,8 @@ __global__ void k_od_begin(OdBuffers b, FeatView f) {
   ist[kIsRows] = 0;
   ist[kIsDegSteps] = 0;
   ist[kIsNanSkips] = 0;
+  ist[kIsGathered] = 0;
+  ist[kIsBoxes] = 0;
   b.done[p] = 0;
 }
 
@@ -393,6 +402,8 @@ __global__ __launch_bounds__(kOdThreads) void k_od_sel(OdBuffers b, FeatView f) 
 // ring-window scans.
 // 8 waves per SIMD (<= 64 VGPRs, <= 100 SGPRs; 7 by default): the association is bound by its
 // dependent chain per query, so occupancy is its throughput (measured 3.8 -> 3.2 ms per step)
+// COUNT: the profiling variant that also sums the points / chunk boxes it loads into istate
+template <bool COUNT>
 __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_od_assoc(OdBuffers b, FeatView f, int last_buf) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, lane = lane_id(), w = threadIdx.x >> 6;
@@ -406,25 +417,30 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(8)))
   const float4* CL = b.lastC + lp * b.capC;
   const float4* SL = b.lastS + lp * b.capS;
   int* ind = b.ind + (size_t)p * 3 * b.cap_q;
+  int wpts = 0, wbox = 0;  // wave-uniform work counters (loam_stats od_assoc_gathered / _boxes)
   for (int q = blk.x * kOdWaves + w; q < nq; q += gridDim.x * kOdWaves) {
     const float4 s4 = sel[q];
     int i1, i2, i3 = -1;
     if (q < nc) {
       const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
       const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC,
-                                       b.hC_T[last_buf * b.P + p], CL, ch, C, 1.0f, 1.0f, s4, cells[w]);
-      wave_assoc_corner(CL, ch, min(nc, C), nn, s4, i1, i2);
+                                       b.hC_T[last_buf * b.P + p], CL, ch, C, 1.0f, 1.0f, s4, cells[w], wpts, wbox);
+      wave_assoc_corner(CL, ch, min(nc, C), nn, s4, i1, i2, wpts, wbox);
     } else {
       const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
       const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS,
-                                       b.hS_T[last_buf * b.P + p], SL, ch, S, 1.0f, 1.0f, s4, cells[w]);
-      wave_assoc_surf(SL, ch, min(ns, S), nn, s4, i1, i2, i3);
+                                       b.hS_T[last_buf * b.P + p], SL, ch, S, 1.0f, 1.0f, s4, cells[w], wpts, wbox);
+      wave_assoc_surf(SL, ch, min(ns, S), nn, s4, i1, i2, i3, wpts, wbox);
     }
     if (lane == 0) {
       ind[q] = i1;
       ind[b.cap_q + q] = i2;
       ind[2 * b.cap_q + q] = i3;
     }
+  }
+  if (COUNT && lane == 0 && wpts) {
+    atomicAdd((int*)&ist[kIsGathered], wpts);
+    atomicAdd((int*)&ist[kIsBoxes], wbox);
   }
 }
 
@@ -812,7 +828,8 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
       hipLaunchKernelGGL(k_od_sel, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f);
       // one wave per query when the batch is small (streaming), 64 waves per problem otherwise
       const int ga = P >= 64 ? 16 : (b.cap_q + kOdWaves - 1) / kOdWaves;
-      hipLaunchKernelGGL(k_od_assoc, dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
+      if (prof) hipLaunchKernelGGL(k_od_assoc<true>, dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
+      else hipLaunchKernelGGL(k_od_assoc<false>, dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
       mark("k_od_assoc");
     }
     if (P < 64) {  // measured: the fused step loses for large batches (its serial tail)

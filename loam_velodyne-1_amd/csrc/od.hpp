@@ -18,6 +18,8 @@ enum { kIsDegenerate = 0, kIsCornerLastNum, kIsSurfLastNum, kIsIters, kIsAssoc, 
        kIsErr, kIsActive, kIsStop,
        kIsDegSteps,  // L-M updates of this frame projected by the iteration-0 degeneracy analysis (Q15)
        kIsNanSkips,  // L-M updates of this frame skipped by the NaN guard (Q16)
+       kIsGathered,  // Last-cloud points the association loaded this frame (work counter)
+       kIsBoxes,     // chunk boxes the association loaded this frame (work counter)
        kOdStateInts = 16 };
 
 // read-only view of one feature set per problem (stride = elements between problems)

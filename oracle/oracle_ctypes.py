@@ -54,7 +54,11 @@ class Stats(ctypes.Structure):
         "mp_fits", "od_query_iters", "od_row_evals",
         "bytes_sr", "bytes_od", "bytes_mp")] + [(n, ctypes.c_double) for n in ("ms_sr", "ms_od", "ms_mp")] + \
         [(n, ctypes.c_uint64) for n in ("od_degenerate_steps", "od_nan_skips", "mp_degenerate_steps",
-                                        "mp_grid_shifts")]
+                                        "mp_grid_shifts",
+                                        # engine-only search counters (zero here: the oracle's kd-tree
+                                        # does different work)
+                                        "mp_nn_candidates", "mp_nn_cells", "od_assoc_gathered",
+                                        "od_assoc_boxes")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

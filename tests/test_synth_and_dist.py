@@ -1,4 +1,5 @@
-"""Synthetic input determinism and the multi-rank sharding of bench.py (gloo, world size 2)."""
+"""Synthetic input determinism and the multi-rank sharding of bench.py (gloo, world size 2): the
+tests call bench.py's own shard function and run bench.py itself with two ranks."""
 import os
 import socket
 
@@ -31,42 +32,63 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, B, q):
-    import importlib
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_shard_ranges():
+    import bench
+    # weak: B per rank, contiguous, seeds 1000 + global index
+    assert [bench.shard(r, 4, 1024, "weak", 1024) for r in range(4)] == [(0, 1024), (1024, 1024), (2048, 1024),
+                                                                        (3072, 1024)]
+    # strong: config 4's 1024 problems split 1024 / N: 128 per GPU on 8 GPUs
+    s8 = [bench.shard(r, 8, 1024, "strong", 1024) for r in range(8)]
+    assert s8 == [(128 * r, 128) for r in range(8)]
+    assert sum(n for _, n in s8) == 1024
+    with pytest.raises(ValueError):
+        bench.shard(0, 3, 1024, "strong", 1024)
+
+
+def _run_bench(args, env_extra):
+    import json
+    import subprocess
     import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path.insert(0, root)
-    sys.path.insert(0, os.path.join(root, "oracle"))
-    import torch
-    import torch.distributed as dist
-    import oracle_ctypes as oc
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    sg = importlib.import_module("loam_velodyne-1_amd.synthgen")
-    prevs, curs = sg.batch_problems(B, base_seed=1000 + rank * B)     # bench.py's shard
-    mine = torch.tensor(np.stack([np.concatenate(oc.problem(prevs[i], curs[i])[:2]) for i in range(B)]))
-    out = [torch.zeros_like(mine) for _ in range(world)]
-    dist.all_gather(out, mine)
-    t = torch.tensor([float(rank + 1)])
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    if rank == 0:
-        q.put((torch.cat(out).numpy(), float(t.item())))
-    dist.destroy_process_group()
+    env = dict(os.environ)
+    env.update(env_extra)
+    env["PYTHONPATH"] = os.path.join(ROOT, "tests") + os.pathsep + env.get("PYTHONPATH", "")
+    env["LOAM_BENCH_ENGINE"] = "bench_stub:Engine"
+    env["MASTER_PORT"] = str(_free_port())
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-4000:]
+    return json.loads(lines[0])
 
 
-def test_sharded_batch_equals_single_process(oc, sg):
-    import torch.multiprocessing as mp
-    B, world = 1, 2
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, B, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    gathered, tmax = q.get(timeout=300)
-    for p in procs:
-        p.join(timeout=60)
-    assert tmax == 2.0
-    prevs, curs = sg.batch_problems(world * B, base_seed=1000)
-    ref = np.stack([np.concatenate(oc.problem(prevs[i], curs[i])[:2]) for i in range(world * B)])
-    np.testing.assert_array_equal(gathered, ref)
+def _expected_sha(sg, first, n):
+    import hashlib
+    import bench_stub
+    prevs, curs = sg.batch_problems(n, base_seed=1000 + first)
+    rows = [np.concatenate(bench_stub.poses_of(p, c)) for p, c in zip(prevs, curs)]
+    return hashlib.sha1(np.ascontiguousarray(np.stack(rows), np.float32).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("split", ["weak", "strong"])
+def test_bench_spawns_two_ranks_gloo(sg, split):
+    """`python bench.py --gpus 2` (no torchrun in front) launches two ranks itself; on a CPU-only
+    machine they use gloo.  One JSON line from rank 0 with n_gpus 2; the gathered poses are the
+    global problems in order (checked against a single-process run of the same stand-in engine)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    out = _run_bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "3", "--global-batch", "4",
+                      "--split", split, "--profile-steps", "1"], {})
+    assert out["n_gpus"] == 2
+    assert out["scaling"] == split
+    per, other_per = (3, 2) if split == "weak" else (2, 3)
+    assert out["config"]["problems_per_gpu"] == per and out["config"]["global_batch"] == 2 * per
+    assert out["gathered"]["problems"] == 2 * per
+    assert out["gathered"]["sha1"] == _expected_sha(sg, 0, 2 * per)
+    other = out["strong" if split == "weak" else "weak"]
+    assert other["global_batch"] == 2 * other_per and other["problems_per_gpu"] == other_per
+    assert out["value"] > 0 and out["roofline"]["kernel"] == "k_mp_nn"
