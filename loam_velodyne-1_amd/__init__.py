@@ -57,6 +57,21 @@ class Pose6(ctypes.Structure):
         return p
 
 
+class OdometryMsg(ctypes.Structure):
+    """include/loam/loam_msg.h loam_odometry_msg (nav_msgs/Odometry fields the reference writes)"""
+    _fields_ = [("stamp", ctypes.c_double), ("frame_id", ctypes.c_char_p), ("child_frame_id", ctypes.c_char_p),
+                ("orientation", ctypes.c_double * 4), ("position", ctypes.c_double * 3),
+                ("twist_angular", ctypes.c_double * 3), ("twist_linear", ctypes.c_double * 3)]
+
+
+class TfMsg(ctypes.Structure):
+    _fields_ = [("stamp", ctypes.c_double), ("frame_id", ctypes.c_char_p), ("child_frame_id", ctypes.c_char_p),
+                ("rotation", ctypes.c_double * 4), ("origin", ctypes.c_double * 3)]
+
+
+MSG_LASER_ODOM, MSG_AFT_MAPPED, MSG_INTEGRATED = 0, 1, 2
+
+
 class Config(ctypes.Structure):
     _fields_ = [("n_rings", ctypes.c_uint32), ("ring_model", ctypes.c_uint32),
                 ("ring_lo_deg", ctypes.c_float), ("ring_hi_deg", ctypes.c_float),
@@ -93,7 +108,9 @@ EXPORTS = ("loam_config_default", "loam_create", "loam_destroy", "loam_last_erro
            "loam_set_profiling", "loam_get_kernel_times",
            # include/loam/loam_bag.h: recorded-sweep ingest (rosbag v2, PointCloud2, Imu)
            "loam_bag_open", "loam_bag_close", "loam_bag_next", "loam_pc2_parse", "loam_pc2_cloud",
-           "loam_imu_parse")
+           "loam_imu_parse",
+           # include/loam/loam_msg.h: the reference's pose message conventions
+           "loam_msg_from_pose", "loam_pose_from_msg")
 
 
 def lib():
@@ -122,6 +139,8 @@ def lib():
         L.loam_get_kernel_times.argtypes = [PP, ctypes.c_char_p, ctypes.c_uint32]
         L.loam_batch_download.argtypes = [PP, P(Pose6), P(Pose6), P(Stats)]
         L.loam_get_stats.argtypes = [PP, P(Stats)]
+        L.loam_msg_from_pose.argtypes = [ctypes.c_int, ctypes.c_double, P(Pose6), P(Pose6), P(OdometryMsg), P(TfMsg)]
+        L.loam_pose_from_msg.argtypes = [P(OdometryMsg), P(Pose6), P(Pose6)]
         _LIB = L
     return _LIB
 
@@ -277,3 +296,18 @@ def maintenance(odom_sum, bef, aft):
     _check(lib().loam_maintenance(ctypes.byref(Pose6.of(odom_sum)), ctypes.byref(Pose6.of(bef)),
                                   ctypes.byref(Pose6.of(aft)), ctypes.byref(out)))
     return out.arr()
+
+
+def msg_from_pose(kind, pose, bef=None, stamp=0.0):
+    """pose (+ bef for MSG_AFT_MAPPED) -> (OdometryMsg, TfMsg) as the reference publishes them"""
+    m, t = OdometryMsg(), TfMsg()
+    b = ctypes.byref(Pose6.of(bef)) if bef is not None else None
+    _check(lib().loam_msg_from_pose(kind, stamp, ctypes.byref(Pose6.of(pose)), b, ctypes.byref(m), ctypes.byref(t)))
+    return m, t
+
+
+def pose_from_msg(m):
+    """OdometryMsg -> (pose, bef) as the receiving handlers read it"""
+    p, b = Pose6(), Pose6()
+    _check(lib().loam_pose_from_msg(ctypes.byref(m), ctypes.byref(p), ctypes.byref(b)))
+    return p.arr(), b.arr()

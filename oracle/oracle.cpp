@@ -1654,5 +1654,11 @@ int oracle_qr_solve(const float* A, const float* b, int m, int n, float* x) {
 void oracle_jacobi(const float* A, int n, float* W, float* V) { jacobi(A, n, W, V); }
 int oracle_lu_inv(const float* A, int n, float* inv) { return lu_inv(A, n, inv) ? 1 : 0; }
 void oracle_pose_through_msg(const float* in, float* out) { pose_through_msg(in, out); }
+// the published orientation of a pose message (laserOdometry.cpp:858-864): (-q.y, -q.z, q.x, q.w)
+// of createQuaternionMsgFromRollPitchYaw(rz, -rx, -ry)
+void oracle_msg_orientation(const float* in, double* xyzw) {
+  Quat g = tf_from_rpy(D(in[2]), -D(in[0]), -D(in[1]));
+  xyzw[0] = -g.y; xyzw[1] = -g.z; xyzw[2] = g.x; xyzw[3] = g.w;
+}
 
 }  // extern "C"

@@ -102,6 +102,7 @@ def lib():
         L.oracle_jacobi.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_lu_inv.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         L.oracle_pose_through_msg.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_msg_orientation.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         _LIB = L
     return _LIB
 

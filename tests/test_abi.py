@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_functions():
     names = set()
-    for h in ("loam.h", "loam_bag.h"):
+    for h in ("loam.h", "loam_bag.h", "loam_msg.h"):
         txt = open(os.path.join(ROOT, "include", "loam", h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         names |= set(re.findall(r"\b(loam_[a-z_0-9]+)\s*\(", txt))
