@@ -15,6 +15,19 @@
 #define LOAM_HD __host__ __device__ __forceinline__
 #define LOAM_D __device__ __forceinline__
 
+// Index bounds checks of the batch-scaled buffers (the per-problem strides of the association,
+// coefficient and 5-NN stores): compiled in only by `make BOUNDS=1` (libloam_hip_checked.so, run
+// through LOAM_HIP_LIB), where a violated bound prints one line and the kernel carries on.
+#ifdef LOAM_BOUNDS_CHECK
+#define LOAM_CHECK(cond, a, b)                                                                      \
+  do {                                                                                              \
+    if (!(cond)) printf("LOAM_CHECK %s:%d %s (%lld, %lld)\n", __FILE__, __LINE__, #cond, (long long)(a), \
+                        (long long)(b));                                                            \
+  } while (0)
+#else
+#define LOAM_CHECK(cond, a, b) ((void)0)
+#endif
+
 namespace loamdev {
 
 constexpr int kWave = 64;

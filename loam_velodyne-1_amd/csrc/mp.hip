@@ -666,6 +666,7 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
     if (bd < 1.0f && bd <= bound) {
       const uint32_t h = cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1);
       const int b0 = start[h], cnt = start[h + 1] - b0;
+      LOAM_CHECK(b0 >= 0 && cnt >= 0, b0, cnt);
       if (cnt > 0) {
         if (b0 >= (1 << 19) || cnt >= (1 << 13)) fits = false;
         lst[n * kMpQueryThreads] = (uint32_t)b0 | ((uint32_t)cnt << 19);
@@ -694,6 +695,9 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
     int idx[kNnInFlight];
 #pragma unroll
     for (int u = 0; u < kNnInFlight; ++u) idx[u] = k + u < total ? next() : idx[0];
+#ifdef LOAM_BOUNDS_CHECK
+    for (int u = 0; u < kNnInFlight; ++u) LOAM_CHECK(idx[u] >= 0 && idx[u] < (1 << 19) + (1 << 13), idx[u], total);
+#endif
     float4 a[kNnInFlight];
 #pragma unroll
     for (int u = 0; u < kNnInFlight; ++u) a[u] = hp[idx[u]];
@@ -769,6 +773,7 @@ __global__ __launch_bounds__(kMpQueryThreads) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int k = 0; k < 5; ++k)
         if (prev[k] != 0x7fffffff) {
+          LOAM_CHECK(prev[k] >= 0 && prev[k] < (corner ? b.nfrom[p * 2 + 0] : b.nfrom[p * 2 + 1]), prev[k], q);
           const float4 a = from[prev[k]];
           top5_offer(t, sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z), prev[k]);
           ++work;
@@ -776,6 +781,8 @@ __global__ __launch_bounds__(kMpQueryThreads) __attribute__((amdgpu_waves_per_eu
     }
     if (corner) knn5_flat(hcs, hcp, TC, sel, t, lst, work);
     else knn5_flat(hss, hsp, TS, sel, t, lst, work);
+    LOAM_CHECK(q < b.cap_stack && (t.i[4] == 0x7fffffff || t.i[4] < (corner ? b.nfrom[p * 2 + 0] : b.nfrom[p * 2 + 1])),
+               q, t.i[4]);
     qnn[2 * q] = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
     qnn[2 * q + 1] = make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0);
   }
@@ -833,7 +840,10 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
         const int idx[5] = {n0.x, n0.y, n0.z, n0.w, n1.x};
         float4 nb[5];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) nb[k] = from[idx[k]];
+        for (int k = 0; k < 5; ++k) {
+          LOAM_CHECK(idx[k] >= 0 && idx[k] < (corner ? nfc : b.nfrom[p * 2 + 1]), idx[k], q);
+          nb[k] = from[idx[k]];
+        }
         f.n0 = n0;
         f.n1 = make_int4(n1.x, 0, 0, 0);
         if (corner) {  // :721-760

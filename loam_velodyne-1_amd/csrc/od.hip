@@ -162,6 +162,7 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
       bucket = (int)(cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1));
       b0 = start[bucket];
       cnt = start[bucket + 1] - b0;
+      LOAM_CHECK(b0 >= 0 && cnt >= 0 && b0 + cnt <= n, b0, cnt);
     }
   }
   // (two of the 27 cells may share a bucket: its points are then offered twice, which does not
@@ -177,6 +178,7 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
 #pragma unroll
     for (int step = 16; step > 0; step >>= 1)
       if (cells[k + step] <= t) k += step;
+    LOAM_CHECK(cells[32 + k] + (t - cells[k]) < n && cells[32 + k] >= 0, cells[32 + k] + (t - cells[k]), n);
     const float4 a = hp[cells[32 + k] + (t - cells[k])];
     const float d = sqdist(a.x, a.y, a.z, q.x, q.y, q.z);
     const uint32_t tag = (uint32_t)__float_as_int(a.w);  // index | ring << 24
@@ -225,6 +227,7 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
     wpts += cnt;
     const int j = j0 + dir * lane;
     const bool inr = lane < cnt;
+    if (inr) LOAM_CHECK(j >= 0 && (dir < 0 ? j < c : j < end), j, end);
     const float4 a = inr ? L[j] : make_float4(0, 0, 0, 0);
     const int r = (int)a.w;
     const uint64_t mb = __ballot(inr && stop_ring(r));
@@ -433,6 +436,8 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(8)))
       wave_assoc_surf(SL, ch, min(ns, S), nn, s4, i1, i2, i3, wpts, wbox);
     }
     if (lane == 0) {
+      LOAM_CHECK(q < b.cap_q && p < b.P, q, p);
+      LOAM_CHECK(i1 < (q < nc ? C : S) && i2 < (q < nc ? C : S) && i3 < S, i1, i2);
       ind[q] = i1;
       ind[b.cap_q + q] = i2;
       ind[2 * b.cap_q + q] = i3;
@@ -511,6 +516,8 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdR
     const float4 s4 = loampose::transform_to_start(T, po);
     const int* ind = b.ind + (size_t)p * 3 * b.cap_q;
     const int i1 = ind[q], i2 = ind[b.cap_q + q], i3 = ind[2 * b.cap_q + q];
+    LOAM_CHECK(q < b.cap_q && iter < b.max_iter, q, iter);
+    LOAM_CHECK(i1 < (q < nc ? b.nlast[(p * 2 + last_buf) * 2 + 0] : b.nlast[(p * 2 + last_buf) * 2 + 1]), i1, q);
     int ok = 0;
     float4 cf = make_float4(0, 0, 0, 0);
     if (q < nc) {

@@ -10,7 +10,7 @@ both sides the same number of times.
                     (src/laserOdometry.cpp:875-930), /velodyne_cloud_registered
                     (src/laserMapping.cpp:1060-1069), /laser_cloud_surround (:1038-1058)
   skipFrameNum      src/laserOdometry.cpp:407, 885-891
-  large batches     config 4 at 768 problems (batch-scaled indexing)
+  large batches     config 4 at 1024 problems, the bench's batch (batch-scaled indexing)
 
 Tolerances: clouds bit-exact in x, y, z (intensity within 2e-6 where it carries relTime, exact
 after TransformToEnd); poses within the north-star 1e-4 m / 1e-4 rad (BASELINE.json)."""
@@ -125,17 +125,18 @@ def test_skip_frame_num_parity(loam, oc, sg, skip):
     assert [r["pub"] for r in rg[1:4]] == ([7, 7, 7] if skip == 0 else [7, 1, 1])
 
 
-def test_batch_768_parity(loam, oc, sg):
-    """batch-scaled indexing: 768 problems in one launch sequence; problems spread over the whole
-    batch (the last ones included) against the oracle, and the last 64 against their own batch"""
-    P = 768
+def test_batch_1024_parity(loam, oc, sg):
+    """batch-scaled indexing: the bench's 1024 problems in one launch sequence; problems spread over
+    the whole batch (the last ones included) against the oracle, and the last 64 against their own
+    batch"""
+    P = 1024
     prevs, curs = sg.batch_problems(P, base_seed=1000)
     e = loam.Engine()
     e.batch_upload(prevs, curs)
     e.batch_run()
     od, aft, st = e.batch_download()
     assert np.all(np.isfinite(od)) and np.all(np.isfinite(aft))
-    for i in list(range(0, P, 24)) + [P - 2, P - 1]:
+    for i in list(range(0, P, 32)) + [P - 2, P - 1]:
         od_o, aft_o, _ = oc.problem(prevs[i], curs[i])
         assert max(np.abs(od[i] - od_o).max(), np.abs(aft[i] - aft_o).max()) <= POSE_TOL, i
     e2 = loam.Engine()
