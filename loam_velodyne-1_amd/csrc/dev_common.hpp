@@ -16,7 +16,7 @@
 #define LOAM_D __device__ __forceinline__
 
 // Index bounds checks of the batch-scaled buffers (the per-problem strides of the association,
-// coefficient and 5-NN stores): compiled in only by `make BOUNDS=1` (libloam_hip_checked.so, run
+// coefficient and 5-NN stores): compiled in only by `make checked` (libloam_hip_checked.so, run
 // through LOAM_HIP_LIB), where a violated bound prints one line and the kernel carries on.
 #ifdef LOAM_BOUNDS_CHECK
 #define LOAM_CHECK(cond, a, b)                                                                      \
