@@ -166,7 +166,7 @@ def _cloud_in(a):
 
 class _Out:
     def __init__(self, cap):
-        self.arr = np.zeros((max(cap, 1), 4), np.float32)
+        self.arr = np.empty((max(cap, 1), 4), np.float32)
         self.c = CloudOut(self.arr.ctypes.data, 0, cap)
 
     def get(self, count=None):
@@ -184,6 +184,9 @@ class Engine:
         self.h = ctypes.c_void_p()
         _check(lib().loam_create(ctypes.byref(self.h), ctypes.byref(self.cfg), device))
         self.cap = cap or int(self.cfg.max_points)
+        # output storage reused by every call (the results are copied out of it)
+        self._sr_outs = [_Out(self.cap) for _ in range(5)]
+        self._od_outs = [_Out(self.cap) for _ in range(3)]
 
     def close(self):
         if getattr(self, "h", None) and self.h.value:
@@ -207,7 +210,7 @@ class Engine:
 
     def scan_registration(self, raw, stamp=0.0):
         ci, keep = _cloud_in(raw)
-        outs = [_Out(self.cap) for _ in range(5)]
+        outs = self._sr_outs
         f = Features(*[o.c for o in outs])
         rc = lib().loam_scan_registration(self.h, stamp, ci, ctypes.byref(f))
         if rc == LOAM_E_NOT_READY:
@@ -224,7 +227,9 @@ class Engine:
         if "imu_trans" in feats:
             f.imu_trans[:] = [float(v) for v in feats["imu_trans"]]
         pose = Pose6()
-        outs = [_Out(self.cap) for _ in range(3)]
+        outs = self._od_outs
+        for o in outs:
+            o.c.count = 0
         pub = ctypes.c_int(0)
         _check(lib().loam_odometry(self.h, stamp, ctypes.byref(f), ctypes.byref(pose), ctypes.byref(outs[0].c),
                                    ctypes.byref(outs[1].c), ctypes.byref(outs[2].c), ctypes.byref(pub)))

@@ -73,6 +73,7 @@ struct loam_ctx {
   OdBuffers od1;        // one odometry problem
   bool od_inited = false;
   int od_last = 0, od_frame_count = 1;  // frameCount = skipFrameNum (src/laserOdometry.cpp:407)
+  float od_sum[6] = {0, 0, 0, 0, 0, 0};  // transformSum: the streaming path accumulates it on the host
   MpBuffers mp1;        // streaming map
   int map_frame_count = 4;    // mapFrameCount = mapFrameNum - 1 (src/laserMapping.cpp:405)
   bool surround_due = false;  // the last loam_mapping frame publishes /laser_cloud_surround
@@ -88,6 +89,8 @@ struct loam_ctx {
   OdBuffers odb;
   MpBuffers mpb;
   std::vector<float4> stage;
+  Staging pin;                  // pinned staging of the node calls' host clouds
+  char* meta = nullptr;         // pinned scratch (8 KB) for the node calls' small D2H / H2D copies
   loam_stats stats;
   Prof prof;
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -112,22 +115,23 @@ void pack(const loam_cloud_in& c, float4* dst) {
   }
 }
 
-int copy_out(hipStream_t st, const float4* dev, int n, loam_cloud_out* o) {
+// device cloud -> caller storage through the pinned arena (completed by pin.finish() after a sync)
+int copy_out(hipStream_t st, Staging& pin, const float4* dev, int n, loam_cloud_out* o) {
   if (o == nullptr) return LOAM_OK;
   if ((uint32_t)n > o->capacity) {
     o->count = (uint32_t)n;
     return fail(LOAM_E_CAPACITY, "output cloud capacity too small");
   }
   o->count = (uint32_t)n;
-  if (n > 0) HIP_TRY(hipMemcpyAsync(o->pts, dev, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost, st));
+  if (n > 0) HIP_TRY(pin.down(st, o->pts, dev, (size_t)n));
   return LOAM_OK;
 }
 
-int upload_cloud(hipStream_t st, const loam_cloud_out& c, float4* dev, int cap) {
+int upload_cloud(hipStream_t st, Staging& pin, const loam_cloud_out& c, float4* dev, int cap) {
   if (c.count > (uint32_t)cap) return fail(LOAM_E_CAPACITY, "input feature cloud exceeds capacity");
   if (c.count > 0) {
     if (c.pts == nullptr) return fail(LOAM_E_INVAL, "feature cloud pts is null");
-    HIP_TRY(hipMemcpyAsync(dev, c.pts, (size_t)c.count * sizeof(float4), hipMemcpyHostToDevice, st));
+    HIP_TRY(pin.up(st, dev, c.pts, (size_t)c.count));
   }
   return LOAM_OK;
 }
@@ -224,6 +228,8 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   if (he == hipSuccess) he = mp_alloc(x->mp1, 1, x->R, x->cap, (int)c.map_capacity, (int)c.mp_max_iter);
   if (he == hipSuccess) he = hipMalloc(&x->sr_imu_dev, sizeof(loamimu::SrQueue));
   if (he != hipSuccess) x->sr_imu_dev = nullptr;
+  if (he == hipSuccess) he = hipHostMalloc((void**)&x->meta, 8192, hipHostMallocDefault);
+  if (he != hipSuccess) x->meta = nullptr;
   x->sr_imu = new loamimu::SrQueue();
   std::memset(x->sr_imu, 0, sizeof(loamimu::SrQueue));
   x->sr_imu->last = -1;
@@ -250,6 +256,8 @@ void loam_destroy(loam_ctx* x) {
   od_free(x->odb);
   mp_free(x->mpb);
   if (x->sr_imu_dev) (void)hipFree(x->sr_imu_dev);
+  if (x->meta) (void)hipHostFree(x->meta);
+  x->pin.release();
   delete x->sr_imu;
   for (auto& e : x->ev)
     if (e) (void)hipEventDestroy(e);
@@ -298,12 +306,17 @@ int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_fe
   int rc = check_cloud_in(raw, x->cap);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(x->device));
-  x->stage.resize(raw.count);
-  pack(raw, x->stage.data());
   SrBuffers& b = x->sr1;
   const int n = (int)raw.count;
-  HIP_TRY(hipMemcpyAsync(b.raw, x->stage.data(), (size_t)n * sizeof(float4), hipMemcpyHostToDevice, x->st));
-  HIP_TRY(hipMemcpyAsync(b.raw_n, &n, sizeof(int), hipMemcpyHostToDevice, x->st));
+  x->pin.reset();
+  HIP_TRY(x->pin.reserve((size_t)n, x->st));
+  float4* praw = x->pin.buf;  // the sweep packed straight into pinned memory
+  pack(raw, praw);
+  x->pin.off = (size_t)n;
+  int* mi = (int*)x->meta;  // [0] n, [1..4] counts, [5] nfull, [6] err
+  mi[0] = n;
+  if (n) HIP_TRY(hipMemcpyAsync(b.raw, praw, (size_t)n * sizeof(float4), hipMemcpyHostToDevice, x->st));
+  HIP_TRY(hipMemcpyAsync(b.raw_n, &mi[0], sizeof(int), hipMemcpyHostToDevice, x->st));
   SrParams prm = sr_params(x);
   loamimu::SrQueue* q = x->sr_imu;
   const size_t tail = offsetof(loamimu::SrQueue, front);  // pointers, Start, Cur, FromStart
@@ -319,20 +332,23 @@ int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_fe
   if (q->last >= 0)
     HIP_TRY(hipMemcpyAsync((char*)q + tail, (const char*)x->sr_imu_dev + tail, sizeof(*q) - tail,
                            hipMemcpyDeviceToHost, x->st));
-  int cnt[4], nfull, err;
-  HIP_TRY(hipMemcpyAsync(cnt, b.cnt, sizeof(cnt), hipMemcpyDeviceToHost, x->st));
-  HIP_TRY(hipMemcpyAsync(&nfull, b.n_full, sizeof(int), hipMemcpyDeviceToHost, x->st));
-  HIP_TRY(hipMemcpyAsync(&err, b.err, sizeof(int), hipMemcpyDeviceToHost, x->st));
+  HIP_TRY(hipMemcpyAsync(&mi[1], b.cnt, 4 * sizeof(int), hipMemcpyDeviceToHost, x->st));
+  HIP_TRY(hipMemcpyAsync(&mi[5], b.n_full, sizeof(int), hipMemcpyDeviceToHost, x->st));
+  HIP_TRY(hipMemcpyAsync(&mi[6], b.err, sizeof(int), hipMemcpyDeviceToHost, x->st));
   HIP_TRY(hipStreamSynchronize(x->st));
-  rc = sr_errors(err);
+  int cnt[4] = {mi[1], mi[2], mi[3], mi[4]};
+  const int nfull = mi[5];
+  rc = sr_errors(mi[6]);
   if (rc) return rc;
   int e = 0;
-  e |= copy_out(x->st, b.full, nfull, &out->full);
-  e |= copy_out(x->st, b.sharp, cnt[0], &out->sharp);
-  e |= copy_out(x->st, b.lsharp, cnt[1], &out->less_sharp);
-  e |= copy_out(x->st, b.flat, cnt[2], &out->flat);
-  e |= copy_out(x->st, b.lflat, cnt[3], &out->less_flat);
+  x->pin.reset();
+  e |= copy_out(x->st, x->pin, b.full, nfull, &out->full);
+  e |= copy_out(x->st, x->pin, b.sharp, cnt[0], &out->sharp);
+  e |= copy_out(x->st, x->pin, b.lsharp, cnt[1], &out->less_sharp);
+  e |= copy_out(x->st, x->pin, b.flat, cnt[2], &out->flat);
+  e |= copy_out(x->st, x->pin, b.lflat, cnt[3], &out->less_flat);
   HIP_TRY(hipStreamSynchronize(x->st));
+  x->pin.finish();
   // /imu_trans (:614-635)
   const float it[12] = {q->pitchStart, q->yawStart, q->rollStart, q->pitchCur, q->yawCur, q->rollCur,
                         q->shiftFSX,   q->shiftFSY, q->shiftFSZ,  q->veloFSX,  q->veloFSY, q->veloFSZ};
@@ -364,65 +380,89 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
       in->less_sharp.count > (uint32_t)(kLessSharpPerRing * R))
     return fail(LOAM_E_CAPACITY, "feature cloud larger than scan registration can produce");
   int rc = 0;
-  if ((rc = upload_cloud(x->st, in->sharp, fi.sharp, kSharpPerRing * R)) ||
-      (rc = upload_cloud(x->st, in->less_sharp, fi.lsharp, kLessSharpPerRing * R)) ||
-      (rc = upload_cloud(x->st, in->flat, fi.flat, kFlatPerRing * R)) ||
-      (rc = upload_cloud(x->st, in->less_flat, fi.lflat, x->cap)) ||
-      (rc = upload_cloud(x->st, in->full, fi.full, x->cap)))
+  x->pin.reset();
+  if ((rc = upload_cloud(x->st, x->pin, in->sharp, fi.sharp, kSharpPerRing * R)) ||
+      (rc = upload_cloud(x->st, x->pin, in->less_sharp, fi.lsharp, kLessSharpPerRing * R)) ||
+      (rc = upload_cloud(x->st, x->pin, in->flat, fi.flat, kFlatPerRing * R)) ||
+      (rc = upload_cloud(x->st, x->pin, in->less_flat, fi.lflat, x->cap)) ||
+      (rc = upload_cloud(x->st, x->pin, in->full, fi.full, x->cap)))
     return rc;
   int cnt[5] = {(int)in->sharp.count, (int)in->less_sharp.count, (int)in->flat.count,
                 (int)in->less_flat.count, (int)in->full.count};
-  HIP_TRY(hipMemcpyAsync(fi.cnt, cnt, 4 * sizeof(int), hipMemcpyHostToDevice, x->st));
-  HIP_TRY(hipMemcpyAsync(fi.n_full, &cnt[4], sizeof(int), hipMemcpyHostToDevice, x->st));
+  int* mi = (int*)x->meta;  // [0..4] counts, [8..19] imu_trans, [24..] downloads below
+  std::memcpy(mi, cnt, sizeof(cnt));
+  std::memcpy(mi + 8, in->imu_trans, 12 * sizeof(float));
+  HIP_TRY(hipMemcpyAsync(fi.cnt, mi, 4 * sizeof(int), hipMemcpyHostToDevice, x->st));
+  HIP_TRY(hipMemcpyAsync(fi.n_full, &mi[4], sizeof(int), hipMemcpyHostToDevice, x->st));
   const FeatView fv = feat_view(fi, 0, 1);
   std::memset(&x->stats, 0, sizeof(x->stats));
   // imuTransHandler (:330-351): this sweep's /imu_trans, in the state order load_imu reads
-  HIP_TRY(hipMemcpyAsync(o.state + kOdImu, in->imu_trans, 12 * sizeof(float), hipMemcpyHostToDevice, x->st));
+  HIP_TRY(hipMemcpyAsync(o.state + kOdImu, mi + 8, 12 * sizeof(float), hipMemcpyHostToDevice, x->st));
   if (!x->od_inited) {  // src/laserOdometry.cpp:427-456: Last = raw lessSharp / lessFlat, no L-M
     // :451-452 transformSum[0] += imuPitchStart; transformSum[2] += imuRollStart (from zero)
     const float sum0[3] = {0.0f + in->imu_trans[0], 0.0f, 0.0f + in->imu_trans[2]};
     HIP_TRY(hipMemcpyAsync(o.state + kOdSum, sum0, sizeof(sum0), hipMemcpyHostToDevice, x->st));
+    x->od_sum[0] = sum0[0];
+    x->od_sum[2] = sum0[2];
     hipLaunchKernelGGL(k_od_end, dim3(16, 1), dim3(256), 0, x->st, o, fv, 0, 0, 0);
     od_build_hashes(o, 0, x->st);
     HIP_TRY(hipGetLastError());
     x->od_last = 0;
     x->od_inited = true;
-    int nl[2];
+    int* nl = mi + 24;
     HIP_TRY(hipMemcpyAsync(nl, o.nlast, 2 * sizeof(int), hipMemcpyDeviceToHost, x->st));
     HIP_TRY(hipStreamSynchronize(x->st));
     *published = LOAM_PUB_CLOUDS;
-    int e = copy_out(x->st, o.lastC, nl[0], corner_last) | copy_out(x->st, o.lastS, nl[1], surf_last);
+    x->pin.reset();
+    int e = copy_out(x->st, x->pin, o.lastC, nl[0], corner_last) | copy_out(x->st, x->pin, o.lastS, nl[1], surf_last);
     HIP_TRY(hipStreamSynchronize(x->st));
+    x->pin.finish();
     return e ? LOAM_E_CAPACITY : LOAM_OK;
   }
   const int cur = x->od_last, nxt = 1 - cur;
   HIP_TRY(hipEventRecord(x->ev[0], x->st));
-  od_solve(o, fv, cur, x->st);
+  // the pose accumulation (:830-856) runs on the host after the download: one scalar chain of
+  // double trig, which a one-thread kernel took ~16 us for (the batch path keeps it on the device)
+  od_solve(o, fv, cur, x->st, nullptr, /*device_fini=*/false);
   x->od_frame_count++;
   const bool pub = x->od_frame_count >= (int)x->cfg.skip_frame_num + 1;
-  hipLaunchKernelGGL(k_od_end, dim3(16, 1), dim3(256), 0, x->st, o, fv, nxt, 2, pub ? 1 : 0);
+  hipLaunchKernelGGL(k_od_end, dim3(64, 1), dim3(256), 0, x->st, o, fv, nxt, 2, pub ? 1 : 0);  // one sweep: a wider grid
   od_build_hashes(o, nxt, x->st);
   HIP_TRY(hipEventRecord(x->ev[1], x->st));
   HIP_TRY(hipGetLastError());
   x->od_last = nxt;
-  float st[kOdStateFloats];
-  int ist[kOdStateInts], nl[4], nfe[2];
-  HIP_TRY(hipMemcpyAsync(st, o.state, sizeof(st), hipMemcpyDeviceToHost, x->st));
-  HIP_TRY(hipMemcpyAsync(ist, o.istate, sizeof(ist), hipMemcpyDeviceToHost, x->st));
-  HIP_TRY(hipMemcpyAsync(nl, o.nlast, sizeof(nl), hipMemcpyDeviceToHost, x->st));
-  HIP_TRY(hipMemcpyAsync(nfe, o.nfullEnd, sizeof(nfe), hipMemcpyDeviceToHost, x->st));
+  float* st = (float*)(mi + 32);                  // kOdStateFloats
+  int* ist = mi + 32 + kOdStateFloats;             // kOdStateInts
+  int* nl = ist + kOdStateInts;                    // 4
+  int* nfe = nl + 4;                               // 2
+  HIP_TRY(hipMemcpyAsync(st, o.state, kOdStateFloats * sizeof(float), hipMemcpyDeviceToHost, x->st));
+  HIP_TRY(hipMemcpyAsync(ist, o.istate, kOdStateInts * sizeof(int), hipMemcpyDeviceToHost, x->st));
+  HIP_TRY(hipMemcpyAsync(nl, o.nlast, 4 * sizeof(int), hipMemcpyDeviceToHost, x->st));
+  HIP_TRY(hipMemcpyAsync(nfe, o.nfullEnd, 2 * sizeof(int), hipMemcpyDeviceToHost, x->st));
   HIP_TRY(hipStreamSynchronize(x->st));
   if (ist[kIsErr]) return fail(LOAM_E_CAPACITY, "odometry capacity exceeded");
-  if (sum_out) std::memcpy(sum_out, st + kOdSum, sizeof(loam_pose6));
+  {  // :830-856 (k_od_fini's body, host side): transformSum from this frame's transform
+    const float* q = in->imu_trans;
+    loampose::Imu m;
+    m.pitchStart = q[0]; m.yawStart = q[1]; m.rollStart = q[2];
+    m.pitchLast = q[3]; m.yawLast = q[4]; m.rollLast = q[5];
+    m.shiftX = q[6]; m.shiftY = q[7]; m.shiftZ = q[8];
+    m.veloX = q[9]; m.veloY = q[10]; m.veloZ = q[11];
+    loampose::accumulate_pose(st, m, x->od_sum);
+    ist[kIsQueries] = ist[kIsAssoc] * (cnt[0] + cnt[2]);
+  }
+  if (sum_out) std::memcpy(sum_out, x->od_sum, sizeof(loam_pose6));
   *published = LOAM_PUB_POSE;
   int e = 0;
   if (pub) {
     x->od_frame_count = 0;
     *published |= LOAM_PUB_CLOUDS | LOAM_PUB_FULL;
-    e |= copy_out(x->st, o.lastC + (size_t)nxt * o.P * o.capC, nl[nxt * 2 + 0], corner_last);
-    e |= copy_out(x->st, o.lastS + (size_t)nxt * o.P * o.capS, nl[nxt * 2 + 1], surf_last);
-    e |= copy_out(x->st, o.fullEnd + (size_t)nxt * o.P * o.capS, nfe[nxt], full_end);
+    x->pin.reset();
+    e |= copy_out(x->st, x->pin, o.lastC + (size_t)nxt * o.P * o.capC, nl[nxt * 2 + 0], corner_last);
+    e |= copy_out(x->st, x->pin, o.lastS + (size_t)nxt * o.P * o.capS, nl[nxt * 2 + 1], surf_last);
+    e |= copy_out(x->st, x->pin, o.fullEnd + (size_t)nxt * o.P * o.capS, nfe[nxt], full_end);
     HIP_TRY(hipStreamSynchronize(x->st));
+    x->pin.finish();
   }
   float ms = 0;
   (void)hipEventElapsedTime(&ms, x->ev[0], x->ev[1]);
@@ -460,7 +500,7 @@ int loam_mapping(loam_ctx* x, double stamp, const loam_pose6* odom_sum, const lo
   const bool have_imu = loamimu::mp_lookup(x->mp_imu, stamp, rp[0], rp[1], front);
   bool updated = false;
   const int rc = mp_stream_frame(x->mp1, x->st, *odom_sum, *corner_last, *surf_last, *full_end, aft, bef,
-                                 registered, &x->stats, g_err, have_imu ? rp : nullptr, &updated);
+                                 registered, &x->stats, g_err, x->pin, x->meta, have_imu ? rp : nullptr, &updated);
   if (have_imu && updated) x->mp_imu.front = front;  // the pointer walk happens inside transformUpdate
   x->surround_due = false;
   if (rc == LOAM_OK && ++x->map_frame_count >= 5) {  // :1038-1040

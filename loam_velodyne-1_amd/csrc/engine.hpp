@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstring>
 #include <string>
 
 #include "../../include/loam/loam.h"
@@ -89,6 +90,78 @@ struct DevAlloc {
     void* q = nullptr;
     err = hipMalloc(&q, bytes ? bytes : 16);
     if (err == hipSuccess) *p = (T*)q;
+  }
+};
+
+// Pinned host staging for the node calls' host clouds: a caller buffer is memcpy'd into the arena
+// and DMA'd from there (and the reverse for outputs), instead of a pageable hipMemcpy each.  One
+// arena per context, grown on demand (after a stream sync, so no copy is in flight).
+struct Staging {
+  float4* buf = nullptr;
+  size_t cap = 0, off = 0;
+  struct Pending {
+    void* dst;
+    const void* src;
+    size_t bytes;
+  };
+  Pending out[8];
+  int nout = 0;
+  hipError_t reserve(size_t n, hipStream_t st) {  // room for n float4 from off
+    if (off + n <= cap) return hipSuccess;
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    finish();
+    size_t want = (off + n) * 2;
+    if (want < ((size_t)1 << 17)) want = (size_t)1 << 17;
+    float4* nb = nullptr;
+    e = hipHostMalloc((void**)&nb, want * sizeof(float4), hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    if (buf) {
+      if (off) memcpy(nb, buf, off * sizeof(float4));
+      (void)hipHostFree(buf);
+    }
+    buf = nb;
+    cap = want;
+    return hipSuccess;
+  }
+  void reset() {
+    off = 0;
+    nout = 0;
+  }
+  // caller buffer -> device (async DMA from the arena)
+  hipError_t up(hipStream_t st, void* dev, const void* src, size_t n) {
+    if (n == 0) return hipSuccess;
+    hipError_t e = reserve(n, st);
+    if (e != hipSuccess) return e;
+    float4* p = buf + off;
+    off += n;
+    memcpy(p, src, n * sizeof(float4));
+    return hipMemcpyAsync(dev, p, n * sizeof(float4), hipMemcpyHostToDevice, st);
+  }
+  // device -> caller buffer: DMA into the arena now, the copy to dst in finish() (after a sync)
+  hipError_t down(hipStream_t st, void* dst, const void* dev, size_t n) {
+    if (n == 0) return hipSuccess;
+    if (nout == 8) {
+      hipError_t e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return e;
+      finish();
+    }
+    hipError_t e = reserve(n, st);
+    if (e != hipSuccess) return e;
+    float4* p = buf + off;
+    off += n;
+    out[nout++] = {dst, p, n * sizeof(float4)};
+    return hipMemcpyAsync(p, dev, n * sizeof(float4), hipMemcpyDeviceToHost, st);
+  }
+  void finish() {  // the stream has been synchronised
+    for (int i = 0; i < nout; ++i) memcpy(out[i].dst, out[i].src, out[i].bytes);
+    nout = 0;
+  }
+  void release() {
+    if (buf) (void)hipHostFree(buf);
+    buf = nullptr;
+    cap = off = 0;
+    nout = 0;
   }
 };
 

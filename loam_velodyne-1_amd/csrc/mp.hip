@@ -729,14 +729,246 @@ __global__ void k_mp_lm_begin(MpBuffers b) {
   ist[kMiNnCells] = 0;
 }
 
-// one L-M iteration's correspondences (:714-877) in two passes, lane per stack point (corner,
-// then surf).  k_mp_nn: the point at the current TobeMapped pose and its exact 5-NN; small and
-// register-light so many waves hide the gather latency.  k_mp_fit: the line (corner PCA, 3x3
-// Jacobi) or plane (5x3 QR) through the 5 neighbours and the weighted residual.  A fit depends
-// on nothing but the ordered 5 neighbours, so it is kept per query and reused while the ordered
-// 5-NN is unchanged from the previous iteration (bit-identical to refitting).
-// five waves per SIMD (<= 96 VGPRs; the LDS lists allow five workgroups per CU).  COUNT: the
-// profiling variant that also sums its work (candidates, bucket ranges) into the frame's istate
+// One L-M iteration's correspondences (:714-877), lane per stack point (corner, then surf), in
+// per-query pieces shared by the batch kernels (k_mp_nn, k_mp_fit, k_mp_iter: one launch each) and
+// the small-batch kernel (k_mp_lm_small: all three and the step in one launch).
+//   mp_nn_query   the point at the current TobeMapped pose and its exact 5-NN (seeded with the
+//                 previous iteration's), stored in q_nn
+//   mp_fit_query  the line (corner PCA, 3x3 Jacobi) or plane (5x3 QR) through the 5 neighbours and
+//                 the weighted residual.  A fit depends on nothing but the ordered 5 neighbours, so
+//                 it is kept per query and reused while the ordered 5-NN is unchanged from the
+//                 previous iteration (bit-identical to refitting)
+//   mp_row_accum  the accepted row's J (:897-921) added in fp64
+//   mp_step       the 6x6 step on the summed normal equations (:922-974)
+namespace {
+// the ordered 5-NN a fit was made for, and the fit: corner (x1, y1, z1, valid), (x2, y2, z2, -);
+// surf (pa, pb, pc, pd), (valid, -, -, -)
+struct MpFit {
+  int4 n0, n1;
+  float4 g0, g1;
+};
+
+// an instance's search inputs, resolved once per workgroup
+struct MpNnCtx {
+  const float4* stack;
+  const int *hcs, *hss;
+  const float4 *hcp, *hsp, *fromC, *fromS;
+  int TC, TS, nfc, nfs;
+  int4* qnn;
+};
+LOAM_D MpNnCtx mp_nn_ctx(const MpBuffers& b, int p) {
+  MpNnCtx c;
+  c.stack = b.stack + (size_t)p * b.cap_stack;
+  c.hcs = b.hC_start + (size_t)p * (b.tmax + 1);
+  c.hss = b.hS_start + (size_t)p * (b.tmax + 1);
+  c.hcp = b.hC_pts + (size_t)p * b.map_cap;
+  c.hsp = b.hS_pts + (size_t)p * b.map_cap;
+  c.TC = b.hC_T[p];
+  c.TS = b.hS_T[p];
+  c.nfc = b.nfrom[p * 2 + 0];
+  c.nfs = b.nfrom[p * 2 + 1];
+  c.fromC = b.from + (size_t)p * b.map_cap;
+  c.fromS = c.fromC + c.nfc;
+  c.qnn = b.q_nn + (size_t)p * b.cap_stack * 2;
+  return c;
+}
+
+LOAM_D void mp_nn_query(const MpBuffers& b, const MpNnCtx& c, int q, int nsc, bool first, const loampose::MapRot& r,
+                        uint32_t* lst, float4& sel, Top5& t, int& work) {
+  const bool corner = q < nsc;
+  int4* qnn = c.qnn;
+  sel = loampose::point_to_map(r, c.stack[corner ? q : b.capC + (q - nsc)]);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) { t.d[k] = 3.4e38f; t.i[k] = 0x7fffffff; }
+  if (!first) {  // seed with the previous iteration's neighbours: a tight bound from the start
+    const int4 n0 = qnn[2 * q], n1 = qnn[2 * q + 1];
+    const int prev[5] = {n0.x, n0.y, n0.z, n0.w, n1.x};
+    const float4* from = corner ? c.fromC : c.fromS;
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      if (prev[k] != 0x7fffffff) {
+        LOAM_CHECK(prev[k] >= 0 && prev[k] < (corner ? c.nfc : c.nfs), prev[k], q);
+        const float4 a = from[prev[k]];
+        top5_offer(t, sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z), prev[k]);
+        ++work;
+      }
+  }
+  if (corner) knn5_flat(c.hcs, c.hcp, c.TC, sel, t, lst, work);
+  else knn5_flat(c.hss, c.hsp, c.TS, sel, t, lst, work);
+  LOAM_CHECK(q < b.cap_stack && (t.i[4] == 0x7fffffff || t.i[4] < (corner ? c.nfc : c.nfs)), q, t.i[4]);
+  qnn[2 * q] = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
+  qnn[2 * q + 1] = make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0);
+}
+
+// jw: this lane's 27 words of LDS scratch for the 3x3 Jacobi
+LOAM_D void mp_fit_query(const MpBuffers& b, int p, int q, int nsc, bool first, int4 n0, int4 n1, float4 sel,
+                         float* jw, int& nfits, float4& cf, int& ok) {
+  const bool corner = q < nsc;
+  const int nfc = b.nfrom[p * 2 + 0];
+  const float4* from = b.from + (size_t)p * b.map_cap + (corner ? 0 : nfc);
+  MpFit* qfit = (MpFit*)b.q_fit + (size_t)p * b.cap_stack;
+  ok = 0;
+  cf = make_float4(0, 0, 0, 0);
+  if (n1.x != 0x7fffffff && D(__int_as_float(n1.y)) < 1.0) {  // :719, :826
+    MpFit f = qfit[q];
+    if (first || f.n0.x != n0.x || f.n0.y != n0.y || f.n0.z != n0.z || f.n0.w != n0.w || f.n1.x != n1.x) {
+      ++nfits;
+      const int idx[5] = {n0.x, n0.y, n0.z, n0.w, n1.x};
+      float4 nb[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        LOAM_CHECK(idx[k] >= 0 && idx[k] < (corner ? nfc : b.nfrom[p * 2 + 1]), idx[k], q);
+        nb[k] = from[idx[k]];
+      }
+      f.n0 = n0;
+      f.n1 = make_int4(n1.x, 0, 0, 0);
+      if (corner) {  // :721-760
+        float cx = 0, cy = 0, cz = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { cx += nb[k].x; cy += nb[k].y; cz += nb[k].z; }
+        cx /= 5; cy /= 5; cz /= 5;
+        float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const float ax = nb[k].x - cx, ay = nb[k].y - cy, az = nb[k].z - cz;
+          a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
+          a22 += ay * ay; a23 += ay * az; a33 += az * az;
+        }
+        a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
+        float* A1 = jw;
+        float* D1 = jw + 9;
+        float* V1 = jw + 12;
+        int* iws = (int*)(jw + 21);
+        A1[0] = a11; A1[1] = a12; A1[2] = a13; A1[3] = a12; A1[4] = a22;
+        A1[5] = a23; A1[6] = a13; A1[7] = a23; A1[8] = a33;
+        loamla::jacobi<3>(A1, D1, V1, iws);
+        const bool valid = D1[0] > 3 * D1[1];
+        f.g0 = make_float4((float)(D(cx) + 0.1 * D(V1[0])), (float)(D(cy) + 0.1 * D(V1[1])),
+                           (float)(D(cz) + 0.1 * D(V1[2])), valid ? 1.0f : 0.0f);
+        f.g1 = make_float4((float)(D(cx) - 0.1 * D(V1[0])), (float)(D(cy) - 0.1 * D(V1[1])),
+                           (float)(D(cz) - 0.1 * D(V1[2])), 0.0f);
+      } else {  // :828-850
+        float A0[15], B0[5] = {-1, -1, -1, -1, -1}, X0[3], ws[14];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { A0[k * 3 + 0] = nb[k].x; A0[k * 3 + 1] = nb[k].y; A0[k * 3 + 2] = nb[k].z; }
+        loamla::qr_solve(A0, B0, 5, 3, X0, ws);
+        float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
+        const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
+        pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+        bool planeValid = true;
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+          if (fabs(D(pa * nb[k].x + pb * nb[k].y + pc * nb[k].z + pd)) > 0.2) planeValid = false;
+        f.g0 = make_float4(pa, pb, pc, pd);
+        f.g1 = make_float4(planeValid ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f);
+      }
+      qfit[q] = f;
+    }
+    if (corner && f.g0.w != 0.0f) {  // :762-816
+      const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
+      const float x1 = f.g0.x, y1 = f.g0.y, z1 = f.g0.z, x2 = f.g1.x, y2 = f.g1.y, z2 = f.g1.z;
+      const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
+      const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
+      const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
+      const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
+      const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
+      const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
+      const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
+      const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
+      const float ld2 = a012 / l12;
+      const float sw = (float)(1 - 0.9 * fabs(D(ld2)));
+      cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
+      ok = D(sw) > 0.1 ? 1 : 0;
+    } else if (!corner && f.g1.x != 0.0f) {  // :852-874
+      const float pa = f.g0.x, pb = f.g0.y, pc = f.g0.z, pd = f.g0.w;
+      const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
+      const float sw = (float)(1 - 0.9 * fabs(D(pd2)) / sqrt(sqrt(D(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z))));
+      cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
+      ok = D(sw) > 0.1 ? 1 : 0;
+    }
+  } else if (first) {
+    // no fit this iteration: drop a fit left by an earlier frame (whose map indices name other
+    // points) so that a later iteration cannot take it for this frame's
+    qfit[q].n0 = make_int4(-1, -1, -1, -1);
+  }
+}
+
+// sin / cos of the TobeMapped rotation for the rows
+LOAM_D void mp_trig(const float* st, float* trig) {
+  for (int k = 0; k < 3; ++k) {
+    trig[2 * k] = (float)dsin(st[kMpTobe + k]);
+    trig[2 * k + 1] = (float)dcos(st[kMpTobe + k]);
+  }
+}
+struct MpTrig {
+  float srx, crx, sry, cry, srz, crz;
+};
+LOAM_D MpTrig mp_trig_of(const float* trig) { return {trig[0], trig[1], trig[2], trig[3], trig[4], trig[5]}; }
+
+LOAM_D void mp_row_accum(const MpTrig& tg, float4 o, float4 c, double (&acc)[28]) {
+  const float srx = tg.srx, crx = tg.crx, sry = tg.sry, cry = tg.cry, srz = tg.srz, crz = tg.crz;
+  float a[6];
+  a[0] = (crx * sry * srz * o.x + crx * crz * sry * o.y - srx * sry * o.z) * c.x +
+         (-srx * srz * o.x - crz * srx * o.y - crx * o.z) * c.y +
+         (crx * cry * srz * o.x + crx * cry * crz * o.y - cry * srx * o.z) * c.z;
+  a[1] = ((cry * srx * srz - crz * sry) * o.x + (sry * srz + cry * crz * srx) * o.y + crx * cry * o.z) * c.x +
+         ((-cry * crz - srx * sry * srz) * o.x + (cry * srz - crz * srx * sry) * o.y - crx * sry * o.z) * c.z;
+  a[2] = ((crz * srx * sry - cry * srz) * o.x + (-cry * crz - srx * sry * srz) * o.y) * c.x +
+         (crx * crz * o.x - crx * srz * o.y) * c.y +
+         ((sry * srz + cry * crz * srx) * o.x + (crz * sry - cry * srx * srz) * o.y) * c.z;
+  a[3] = c.x;
+  a[4] = c.y;
+  a[5] = c.z;
+  const float bb = -c.w;
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
+  acc[27] += 1.0;
+}
+
+struct MpStepScratch {
+  float lm_ws[loamla::kLmWs];
+  int lm_iws[12];
+  float AtA[36], AtB[6], X[6];
+};
+
+// one lane: iteration bookkeeping, the 6x6 step when there are >= 50 rows (:886-889), the
+// update (no NaN guard in mapping, :956-961) and the convergence test (:972)
+LOAM_D void mp_step(const MpBuffers& b, int p, const double* tot, MpStepScratch& sh) {
+  int* ist = b.istate + (size_t)p * kMpStateInts;
+  float* st = b.state + (size_t)p * kMpStateFloats;
+  const int iter = ist[kMiIters];
+  const int nrows = (int)tot[27];
+  ist[kMiIters] = iter + 1;
+  ist[kMiRows] += nrows;
+  if (nrows >= 50) {
+    int k = 0;
+    for (int i = 0; i < 6; ++i)
+      for (int jj = i; jj < 6; ++jj) {
+        sh.AtA[i * 6 + jj] = (float)tot[k];
+        sh.AtA[jj * 6 + i] = (float)tot[k];
+        ++k;
+      }
+    for (int i = 0; i < 6; ++i) sh.AtB[i] = (float)tot[21 + i];
+    int degen = ist[kMiDegen];
+    loamla::lm_step(sh.AtA, sh.AtB, iter, 100.0f, &degen, st + kMpMatP, sh.X, sh.lm_ws, sh.lm_iws);
+    ist[kMiDegen] = degen;
+    if (degen) ist[kMiDegSteps] += 1;
+    for (int q = 0; q < 6; ++q) st[kMpTobe + q] += sh.X[q];
+    const float dR = loamla::delta_r(sh.X), dT = loamla::delta_t(sh.X);
+    if (D(dR) < 0.05 && D(dT) < 0.05) ist[kMiStop] = 1;
+  }
+  if (ist[kMiIters] >= b.max_iter) ist[kMiStop] = 1;
+}
+}  // namespace
+
+// batch kernels.  k_mp_nn: small and register-light so many waves hide the gather latency; five
+// waves per SIMD (<= 96 VGPRs; the LDS lists allow five workgroups per CU).  COUNT: the profiling
+// variant that also sums its work (candidates, bucket ranges) into the frame's istate
 template <bool COUNT>
 __global__ __launch_bounds__(kMpQueryThreads) __attribute__((amdgpu_waves_per_eu(5))) void k_mp_nn(MpBuffers b) {
   const XcdBlock blk = xcd_block();
@@ -746,45 +978,16 @@ __global__ __launch_bounds__(kMpQueryThreads) __attribute__((amdgpu_waves_per_eu
   const float* st = b.state + (size_t)p * kMpStateFloats;
   const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
   const int nq = nsc + nss;
-  const float4* stack = b.stack + (size_t)p * b.cap_stack;
-  const int* hcs = b.hC_start + (size_t)p * (b.tmax + 1);
-  const int* hss = b.hS_start + (size_t)p * (b.tmax + 1);
-  const float4* hcp = b.hC_pts + (size_t)p * b.map_cap;
-  const float4* hsp = b.hS_pts + (size_t)p * b.map_cap;
-  const int TC = b.hC_T[p], TS = b.hS_T[p];
-  int4* qnn = b.q_nn + (size_t)p * b.cap_stack * 2;
   __shared__ uint32_t lists[27 * kMpQueryThreads];
   uint32_t* lst = lists + tid;
   const bool first = ist[kMiIters] == 0;
-  const float4* fromC = b.from + (size_t)p * b.map_cap;
-  const float4* fromS = fromC + b.nfrom[p * 2 + 0];
   const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
+  const MpNnCtx c = mp_nn_ctx(b, p);
   int work = 0;  // work counter (loam_stats mp_nn_candidates / mp_nn_cells), packed as in knn5
   for (int q = blk.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
-    const bool corner = q < nsc;
-    const float4 sel = loampose::point_to_map(r, stack[corner ? q : b.capC + (q - nsc)]);
+    float4 sel;
     Top5 t;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) { t.d[k] = 3.4e38f; t.i[k] = 0x7fffffff; }
-    if (!first) {  // seed with the previous iteration's neighbours: a tight bound from the start
-      const int4 n0 = qnn[2 * q], n1 = qnn[2 * q + 1];
-      const int prev[5] = {n0.x, n0.y, n0.z, n0.w, n1.x};
-      const float4* from = corner ? fromC : fromS;
-#pragma unroll
-      for (int k = 0; k < 5; ++k)
-        if (prev[k] != 0x7fffffff) {
-          LOAM_CHECK(prev[k] >= 0 && prev[k] < (corner ? b.nfrom[p * 2 + 0] : b.nfrom[p * 2 + 1]), prev[k], q);
-          const float4 a = from[prev[k]];
-          top5_offer(t, sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z), prev[k]);
-          ++work;
-        }
-    }
-    if (corner) knn5_flat(hcs, hcp, TC, sel, t, lst, work);
-    else knn5_flat(hss, hsp, TS, sel, t, lst, work);
-    LOAM_CHECK(q < b.cap_stack && (t.i[4] == 0x7fffffff || t.i[4] < (corner ? b.nfrom[p * 2 + 0] : b.nfrom[p * 2 + 1])),
-               q, t.i[4]);
-    qnn[2 * q] = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
-    qnn[2 * q + 1] = make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0);
+    mp_nn_query(b, c, q, nsc, first, r, lst, sel, t, work);
   }
   if (!COUNT) return;
   const int ncand = wave_sum(work & ((1 << kWorkCellShift) - 1)), ncell = wave_sum(work >> kWorkCellShift);
@@ -793,15 +996,6 @@ __global__ __launch_bounds__(kMpQueryThreads) __attribute__((amdgpu_waves_per_eu
     atomicAdd((int*)&ist[kMiNnCells], ncell);
   }
 }
-
-namespace {
-// the ordered 5-NN a fit was made for, and the fit: corner (x1, y1, z1, valid), (x2, y2, z2, -);
-// surf (pa, pb, pc, pd), (valid, -, -, -)
-struct MpFit {
-  int4 n0, n1;
-  float4 g0, g1;
-};
-}  // namespace
 
 __global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
   const XcdBlock blk = xcd_block();
@@ -813,14 +1007,10 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
   // per-lane 3x3 Jacobi scratch (27 words; the odd stride keeps lanes on distinct banks): 27 KB,
   // five workgroups per CU (33-word rows allowed four; measured 1.56 -> 1.40 ms per step)
   __shared__ float jac[kMpQueryThreads][27];
-  const int nfc = b.nfrom[p * 2 + 0];
   const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
   const int nq = nsc + nss;
   const float4* stack = b.stack + (size_t)p * b.cap_stack;
-  const float4* fromC = b.from + (size_t)p * b.map_cap;
-  const float4* fromS = fromC + nfc;
   const int4* qnn = b.q_nn + (size_t)p * b.cap_stack * 2;
-  MpFit* qfit = (MpFit*)b.q_fit + (size_t)p * b.cap_stack;
   int8_t* qok = b.q_ok + (size_t)p * b.cap_stack;
   float4* qcf = b.q_cf + (size_t)p * b.cap_stack;
   const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
@@ -828,93 +1018,13 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
   int nfits = 0;
   for (int q = blk.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
     const bool corner = q < nsc;
-    const float4* from = corner ? fromC : fromS;
     const int4 n0 = qnn[2 * q], n1 = qnn[2 * q + 1];
-    int ok = 0;
-    float4 cf = make_float4(0, 0, 0, 0);
-    if (n1.x != 0x7fffffff && D(__int_as_float(n1.y)) < 1.0) {  // :719, :826
-      const float4 sel = loampose::point_to_map(r, stack[corner ? q : b.capC + (q - nsc)]);
-      MpFit f = qfit[q];
-      if (first || f.n0.x != n0.x || f.n0.y != n0.y || f.n0.z != n0.z || f.n0.w != n0.w || f.n1.x != n1.x) {
-        ++nfits;
-        const int idx[5] = {n0.x, n0.y, n0.z, n0.w, n1.x};
-        float4 nb[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          LOAM_CHECK(idx[k] >= 0 && idx[k] < (corner ? nfc : b.nfrom[p * 2 + 1]), idx[k], q);
-          nb[k] = from[idx[k]];
-        }
-        f.n0 = n0;
-        f.n1 = make_int4(n1.x, 0, 0, 0);
-        if (corner) {  // :721-760
-          float cx = 0, cy = 0, cz = 0;
-#pragma unroll
-          for (int k = 0; k < 5; ++k) { cx += nb[k].x; cy += nb[k].y; cz += nb[k].z; }
-          cx /= 5; cy /= 5; cz /= 5;
-          float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
-#pragma unroll
-          for (int k = 0; k < 5; ++k) {
-            const float ax = nb[k].x - cx, ay = nb[k].y - cy, az = nb[k].z - cz;
-            a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
-            a22 += ay * ay; a23 += ay * az; a33 += az * az;
-          }
-          a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
-          float* A1 = jw;
-          float* D1 = jw + 9;
-          float* V1 = jw + 12;
-          int* iws = (int*)(jw + 21);
-          A1[0] = a11; A1[1] = a12; A1[2] = a13; A1[3] = a12; A1[4] = a22;
-          A1[5] = a23; A1[6] = a13; A1[7] = a23; A1[8] = a33;
-          loamla::jacobi<3>(A1, D1, V1, iws);
-          const bool valid = D1[0] > 3 * D1[1];
-          f.g0 = make_float4((float)(D(cx) + 0.1 * D(V1[0])), (float)(D(cy) + 0.1 * D(V1[1])),
-                             (float)(D(cz) + 0.1 * D(V1[2])), valid ? 1.0f : 0.0f);
-          f.g1 = make_float4((float)(D(cx) - 0.1 * D(V1[0])), (float)(D(cy) - 0.1 * D(V1[1])),
-                             (float)(D(cz) - 0.1 * D(V1[2])), 0.0f);
-        } else {  // :828-850
-          float A0[15], B0[5] = {-1, -1, -1, -1, -1}, X0[3], ws[14];
-#pragma unroll
-          for (int k = 0; k < 5; ++k) { A0[k * 3 + 0] = nb[k].x; A0[k * 3 + 1] = nb[k].y; A0[k * 3 + 2] = nb[k].z; }
-          loamla::qr_solve(A0, B0, 5, 3, X0, ws);
-          float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
-          const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
-          pa /= ps; pb /= ps; pc /= ps; pd /= ps;
-          bool planeValid = true;
-#pragma unroll
-          for (int k = 0; k < 5; ++k)
-            if (fabs(D(pa * nb[k].x + pb * nb[k].y + pc * nb[k].z + pd)) > 0.2) planeValid = false;
-          f.g0 = make_float4(pa, pb, pc, pd);
-          f.g1 = make_float4(planeValid ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f);
-        }
-        qfit[q] = f;
-      }
-      if (corner && f.g0.w != 0.0f) {  // :762-816
-        const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
-        const float x1 = f.g0.x, y1 = f.g0.y, z1 = f.g0.z, x2 = f.g1.x, y2 = f.g1.y, z2 = f.g1.z;
-        const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
-        const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
-        const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
-        const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
-        const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
-        const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
-        const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
-        const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
-        const float ld2 = a012 / l12;
-        const float sw = (float)(1 - 0.9 * fabs(D(ld2)));
-        cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
-        ok = D(sw) > 0.1 ? 1 : 0;
-      } else if (!corner && f.g1.x != 0.0f) {  // :852-874
-        const float pa = f.g0.x, pb = f.g0.y, pc = f.g0.z, pd = f.g0.w;
-        const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
-        const float sw = (float)(1 - 0.9 * fabs(D(pd2)) / sqrt(sqrt(D(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z))));
-        cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
-        ok = D(sw) > 0.1 ? 1 : 0;
-      }
-    } else if (first) {
-      // no fit this iteration: drop a fit left by an earlier frame (whose map indices name other
-      // points) so that a later iteration cannot take it for this frame's
-      qfit[q].n0 = make_int4(-1, -1, -1, -1);
-    }
+    float4 sel = make_float4(0, 0, 0, 0);
+    if (n1.x != 0x7fffffff && D(__int_as_float(n1.y)) < 1.0)
+      sel = loampose::point_to_map(r, stack[corner ? q : b.capC + (q - nsc)]);
+    float4 cf;
+    int ok;
+    mp_fit_query(b, p, q, nsc, first, n0, n1, sel, jw, nfits, cf, ok);
     qok[q] = (int8_t)ok;
     qcf[q] = cf;
   }
@@ -1026,6 +1136,97 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
       if (D(dR) < 0.05 && D(dT) < 0.05) ist[kMiStop] = 1;
     }
     if (ist[kMiIters] >= b.max_iter) ist[kMiStop] = 1;
+  }
+}
+
+
+// Small batches (streaming, config 2): the whole iteration in one launch — each lane its query's
+// 5-NN, fit and row, fp64 partials per workgroup, and the last workgroup of the instance to finish
+// sums them in a fixed order and runs the step (three launches and a one-workgroup row pass fewer
+// per iteration).
+__global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
+  const int p = blockIdx.y, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  int* ist = b.istate + (size_t)p * kMpStateInts;
+  if (!ist[kMiLmRan] || ist[kMiStop]) return;
+  const float* st = b.state + (size_t)p * kMpStateFloats;
+  __shared__ uint32_t lists[27 * kMpQueryThreads];
+  __shared__ float jac[kMpQueryThreads][27];
+  __shared__ double red[kMpQueryThreads / 64][28];
+  __shared__ float trig[6];
+  const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
+  const int nq = nsc + nss;
+  const float4* stack = b.stack + (size_t)p * b.cap_stack;
+  int8_t* qok = b.q_ok + (size_t)p * b.cap_stack;
+  float4* qcf = b.q_cf + (size_t)p * b.cap_stack;
+  const bool first = ist[kMiIters] == 0;
+  if (tid == 0) mp_trig(st, trig);
+  const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
+  const MpNnCtx c = mp_nn_ctx(b, p);
+  int work = 0, nfits = 0;  // (work: the batch kernel's profiling counter; not summed here)
+  for (int q = blockIdx.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
+    float4 sel;
+    Top5 t;
+    mp_nn_query(b, c, q, nsc, first, r, lists + tid, sel, t, work);
+    float4 cf;
+    int ok;
+    mp_fit_query(b, p, q, nsc, first, make_int4(t.i[0], t.i[1], t.i[2], t.i[3]),
+                 make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0), sel, jac[tid], nfits, cf, ok);
+    qok[q] = (int8_t)ok;
+    qcf[q] = cf;
+  }
+  __syncthreads();  // trig
+  const MpTrig tg = mp_trig_of(trig);
+  double acc[28];
+#pragma unroll
+  for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+  for (int q = blockIdx.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads)
+    if (qok[q]) mp_row_accum(tg, stack[q < nsc ? q : b.capC + (q - nsc)], qcf[q], acc);
+  nfits = wave_sum(nfits);
+  if (lane == 0 && nfits) atomicAdd(&ist[kMiFits], nfits);
+  wave_reduce_scatter_28(acc);
+  if ((lane & 1) == 0 && (lane >> 1) < 28) red[w][lane >> 1] = acc[0];
+  __syncthreads();
+  const int G = (int)gridDim.x;
+  if (tid < 28) {
+    double v = red[0][tid];
+    for (int ww = 1; ww < kMpQueryThreads / 64; ++ww) v += red[ww][tid];
+    b.part[((size_t)p * kMpSmallGrid + blockIdx.x) * 28 + tid] = v;
+    __threadfence();  // partials visible device-wide before this workgroup reports done
+  }
+  __shared__ int sh_last;
+  __shared__ double slice[8][28];
+  __shared__ double tot[28];
+  __shared__ MpStepScratch sh;
+  __syncthreads();
+  if (tid == 0) sh_last = atomicAdd(&b.done[p], 1) == G - 1;
+  __syncthreads();
+  if (!sh_last) return;
+  if (tid < 8 * 28) {  // fixed-order sum: slice s holds partials s, s + 8, ... (all in flight)
+    const int v = tid % 28, sl = tid / 28;
+    const double* pp = b.part + (size_t)p * kMpSmallGrid * 28 + v;
+    double t8[kMpSmallGrid / 8];
+#pragma unroll
+    for (int u = 0; u < kMpSmallGrid / 8; ++u) {
+      const int g = sl + 8 * u;
+      t8[u] = g < G ? __hip_atomic_load(&pp[(size_t)g * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    }
+    double a1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < kMpSmallGrid / 8; ++u)
+      if (sl + 8 * u < G) a1 += t8[u];
+    slice[sl][v] = a1;
+  }
+  __syncthreads();
+  if (tid < 28) {
+    double v = slice[0][tid];
+#pragma unroll
+    for (int sl = 1; sl < 8; ++sl) v += slice[sl][tid];
+    tot[tid] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    b.done[p] = 0;
+    mp_step(b, p, tot, sh);
   }
 }
 
@@ -1328,7 +1529,8 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
   A(&b.from, Pm * sizeof(float4));
   A(&b.hC_start, (size_t)P * (b.tmax + 1) * sizeof(int));
   A(&b.hS_start, (size_t)P * (b.tmax + 1) * sizeof(int));
-  A(&b.h_fill, (size_t)P * b.tmax * sizeof(int));
+  // bucket counters: one set per cloud kind for small batches, whose two builds run together
+  A(&b.h_fill, (size_t)(P <= 4 ? 2 : 1) * P * b.tmax * sizeof(int));
   A(&b.hC_T, (size_t)P * sizeof(int));
   A(&b.hS_T, (size_t)P * sizeof(int));
   A(&b.hC_pts, Pm * sizeof(float4));
@@ -1367,6 +1569,8 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
   if (t1 == 0 || t2 == 0) A.err = hipErrorInvalidValue;
   A(&b.cub_tmp, b.cub_bytes);
   A(&b.reg, (size_t)P * b.capS * sizeof(float4));
+  A(&b.part, (size_t)P * kMpSmallGrid * 28 * sizeof(double));
+  A(&b.done, (size_t)P * sizeof(int));
   A(&b.nreg, (size_t)P * sizeof(int));
   if (A.err == hipSuccess) A.err = mp_reset(b, nullptr);
   if (A.err == hipSuccess) A.err = hipDeviceSynchronize();
@@ -1379,7 +1583,7 @@ void mp_free(MpBuffers& b) {
                   b.stack2, b.stack, b.nstack, b.from, b.hC_start, b.hS_start, b.h_fill, b.hC_T, b.hS_T,
                   b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.citems, b.nitems, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
-                  b.vg_params, b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_bb, b.vg_be, b.vg_split, b.cub_tmp, b.reg, b.nreg};
+                  b.vg_params, b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_bb, b.vg_be, b.vg_split, b.cub_tmp, b.reg, b.nreg, b.part, b.done};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = MpBuffers();
@@ -1395,6 +1599,7 @@ __global__ void k_mp_reset(MpBuffers b) {
 hipError_t mp_reset(MpBuffers& b, hipStream_t st) {
   b.pool_cur = 0;
   hipError_t e = hipMemsetAsync(b.state, 0, (size_t)b.P * kMpStateFloats * sizeof(float), st);
+  if (e == hipSuccess) e = hipMemsetAsync(b.done, 0, (size_t)b.P * sizeof(int), st);
   if (e == hipSuccess) e = hipMemsetAsync(b.istate, 0, (size_t)b.P * kMpStateInts * sizeof(int), st);
   if (e == hipSuccess) e = hipMemsetAsync(b.slots, 0, (size_t)2 * b.P * kCubeNum * 4 * sizeof(int), st);
   if (e != hipSuccess) return e;
@@ -1428,11 +1633,11 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   hc.inv_h = 1.0f;
   hc.shift = 0;  // the 5-NN search scans whole buckets: keep them to single cells
   hc.chunks = nullptr;
-  hipLaunchKernelGGL(k_hash_build, dim3(P), dim3(256), 0, st, hc);
   HashJob hs = hc;
   hs.pts_off = b.nfrom; hs.pts_off_stride = 2;
   hs.count = b.nfrom + 1; hs.start = b.hS_start; hs.out = b.hS_pts; hs.tsize = b.hS_T;
-  hipLaunchKernelGGL(k_hash_build, dim3(P), dim3(256), 0, st, hs);
+  if (P <= 4) hs.fill = b.h_fill + (size_t)P * b.tmax;
+  hash_build_pair(hc, hs, P, st);
   mark("k_hash_build_map");
   hipLaunchKernelGGL(k_mp_lm_begin, dim3((P + 255) / 256), dim3(256), 0, st, b);
   // workgroups per instance: all the stack's queries at once for a few instances; for large
@@ -1440,6 +1645,11 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   const int gq = std::min(P >= 64 ? 24 : 64, (b.cap_stack + kMpQueryThreads - 1) / kMpQueryThreads);
   // an empty map store (the first frame after a reset) cannot run the L-M (:706): no launches
   for (int it = 0; it < (map_empty ? 0 : b.max_iter); ++it) {
+    if (P <= 4) {  // small batches: one launch per iteration
+      hipLaunchKernelGGL(k_mp_lm_small, dim3(kMpSmallGrid, P), dim3(kMpQueryThreads), 0, st, b);
+      mark("k_mp_lm_small");
+      continue;
+    }
     if (prof) hipLaunchKernelGGL(k_mp_nn<true>, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
     else hipLaunchKernelGGL(k_mp_nn<false>, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
     mark("k_mp_nn");
@@ -1474,8 +1684,8 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
 
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
                     const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
-                    loam_cloud_out* registered, loam_stats* stats, std::string& err, const float* imu_rp,
-                    bool* updated) {
+                    loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, void* meta,
+                    const float* imu_rp, bool* updated) {
   if (corner.count > (uint32_t)b.capC || surf.count > (uint32_t)b.capS || full.count > (uint32_t)b.capS) {
     err = "mapping input cloud exceeds capacity";
     return LOAM_E_CAPACITY;
@@ -1487,16 +1697,27 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  int n[3] = {(int)corner.count, (int)surf.count, (int)full.count};
-  if (n[0]) (void)hipMemcpyAsync(b.inC, corner.pts, n[0] * sizeof(float4), hipMemcpyHostToDevice, st);
-  if (n[1]) (void)hipMemcpyAsync(b.inS, surf.pts, n[1] * sizeof(float4), hipMemcpyHostToDevice, st);
-  if (n[2]) (void)hipMemcpyAsync(b.inF, full.pts, n[2] * sizeof(float4), hipMemcpyHostToDevice, st);
-  (void)hipMemcpyAsync(b.in_n, n, sizeof(n), hipMemcpyHostToDevice, st);
-  (void)hipMemcpyAsync(b.in_pose, &odom_sum, 6 * sizeof(float), hipMemcpyHostToDevice, st);
-  static const float zero_rp[2] = {0.0f, 0.0f};
-  static const int imu_on = 1, imu_off = 0;
-  (void)hipMemcpyAsync(b.state + kMpImuRP, imu_rp ? imu_rp : zero_rp, 2 * sizeof(float), hipMemcpyHostToDevice, st);
-  (void)hipMemcpyAsync(b.istate + kMiImu, imu_rp ? &imu_on : &imu_off, sizeof(int), hipMemcpyHostToDevice, st);
+  // host inputs through the pinned arena / scratch: [0..2] counts, [4..9] pose, [10..11] IMU
+  // (roll, pitch), [12] IMU flag; downloads below from [16]
+  int* mi = (int*)meta;
+  int* n = mi;
+  n[0] = (int)corner.count; n[1] = (int)surf.count; n[2] = (int)full.count;
+  std::memcpy(mi + 4, &odom_sum, 6 * sizeof(float));
+  const float rp[2] = {imu_rp ? imu_rp[0] : 0.0f, imu_rp ? imu_rp[1] : 0.0f};
+  std::memcpy(mi + 10, rp, sizeof(rp));
+  mi[12] = imu_rp ? 1 : 0;
+  pin.reset();
+  hipError_t ue = pin.up(st, b.inC, corner.pts, (size_t)n[0]);
+  if (ue == hipSuccess) ue = pin.up(st, b.inS, surf.pts, (size_t)n[1]);
+  if (ue == hipSuccess) ue = pin.up(st, b.inF, full.pts, (size_t)n[2]);
+  if (ue == hipSuccess) ue = hipMemcpyAsync(b.in_n, n, 3 * sizeof(int), hipMemcpyHostToDevice, st);
+  if (ue == hipSuccess) ue = hipMemcpyAsync(b.in_pose, mi + 4, 6 * sizeof(float), hipMemcpyHostToDevice, st);
+  if (ue == hipSuccess) ue = hipMemcpyAsync(b.state + kMpImuRP, mi + 10, 2 * sizeof(float), hipMemcpyHostToDevice, st);
+  if (ue == hipSuccess) ue = hipMemcpyAsync(b.istate + kMiImu, mi + 12, sizeof(int), hipMemcpyHostToDevice, st);
+  if (ue != hipSuccess) {
+    err = std::string("mapping upload: ") + hipGetErrorString(ue);
+    return LOAM_E_HIP;
+  }
   MpInput in;
   in.corner = b.inC; in.surf = b.inS; in.full = b.inF;
   in.corner_stride = b.capC; in.surf_stride = b.capS; in.full_stride = b.capS;
@@ -1506,12 +1727,14 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   (void)hipEventRecord(e0, st);
   mp_frame(b, in, st);
   (void)hipEventRecord(e1, st);
-  float sf[kMpStateFloats];
-  int si[kMpStateInts], nreg = 0;
-  (void)hipMemcpyAsync(sf, b.state, sizeof(sf), hipMemcpyDeviceToHost, st);
-  (void)hipMemcpyAsync(si, b.istate, sizeof(si), hipMemcpyDeviceToHost, st);
-  (void)hipMemcpyAsync(&nreg, b.nreg, sizeof(int), hipMemcpyDeviceToHost, st);
-  hipError_t he = hipStreamSynchronize(st);
+  float* sf = (float*)(mi + 16);                  // kMpStateFloats
+  int* si = mi + 16 + kMpStateFloats;             // kMpStateInts
+  int* pnreg = si + kMpStateInts;
+  hipError_t he = hipMemcpyAsync(sf, b.state, kMpStateFloats * sizeof(float), hipMemcpyDeviceToHost, st);
+  if (he == hipSuccess) he = hipMemcpyAsync(si, b.istate, kMpStateInts * sizeof(int), hipMemcpyDeviceToHost, st);
+  if (he == hipSuccess) he = hipMemcpyAsync(pnreg, b.nreg, sizeof(int), hipMemcpyDeviceToHost, st);
+  if (he == hipSuccess) he = hipStreamSynchronize(st);
+  const int nreg = *pnreg;
   float ms = 0;
   (void)hipEventElapsedTime(&ms, e0, e1);
   (void)hipEventDestroy(e0);
@@ -1536,7 +1759,14 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
       rc = LOAM_E_CAPACITY;
     } else {
       registered->count = (uint32_t)nreg;
-      if (nreg) (void)hipMemcpy(registered->pts, b.reg, (size_t)nreg * sizeof(float4), hipMemcpyDeviceToHost);
+      pin.reset();
+      he = pin.down(st, registered->pts, b.reg, (size_t)nreg);
+      if (he == hipSuccess) he = hipStreamSynchronize(st);
+      if (he != hipSuccess) {
+        err = std::string("registered cloud download: ") + hipGetErrorString(he);
+        return LOAM_E_HIP;
+      }
+      pin.finish();
     }
   }
   if (stats) {

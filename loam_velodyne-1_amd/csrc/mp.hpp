@@ -14,6 +14,7 @@ namespace loam {
 // cube grid of src/laserMapping.cpp:64-70
 constexpr int kCubeW = 21, kCubeH = 11, kCubeD = 21, kCubeNum = kCubeW * kCubeH * kCubeD;
 constexpr int kMaxValid = 125;
+constexpr int kMpSmallGrid = 64;  // workgroups per instance of the small-batch L-M iteration (multiple of 8)
 
 // per-instance float state: Sum | Incre | TobeMapped | Bef | Aft | matP[36] | pointOnYAxis[3]
 constexpr int kMpSum = 0, kMpIncre = 6, kMpTobe = 12, kMpBef = 18, kMpAft = 24, kMpMatP = 30, kMpOnY = 66,
@@ -106,6 +107,8 @@ struct MpBuffers {
   void* cub_tmp = nullptr;
   size_t cub_bytes = 0;
   float4* reg = nullptr;      // [P][capS] registered full cloud
+  double* part = nullptr;     // [P][kMpSmallGrid][28] k_mp_lm_small's per-workgroup JᵀJ | Jᵀb | rows
+  int* done = nullptr;        // [P] its workgroups finished (the last one runs the step)
   int* nreg = nullptr;
   hipError_t sticky = hipSuccess;  // first failed library call of the launch sequences (hipCUB)
   void note(hipError_t e) {
@@ -129,7 +132,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof = null
 // transformUpdate ran (the caller then commits its IMU queue pointer)
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
                     const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
-                    loam_cloud_out* registered, loam_stats* stats, std::string& err,
+                    loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, void* meta,
                     const float* imu_rp = nullptr, bool* updated = nullptr);
 // /laser_cloud_surround of the last streaming frame (instance 0): its 5x5x5 cube neighbourhood
 // concatenated and VoxelGrid 0.2 (src/laserMapping.cpp:1038-1058)

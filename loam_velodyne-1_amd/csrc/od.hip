@@ -131,6 +131,120 @@ __global__ __launch_bounds__(256) void k_hash_build(HashJob j) {
   }
 }
 
+// ---- the same index built by many workgroups per cloud (small batches: streaming, config 2).  One
+// workgroup per cloud left a few CUs busy for 40-60 us per map; here a grid per cloud zeroes the
+// bucket counters, counts with global atomics, one workgroup scans, and the grid scatters.  The
+// order of points inside a bucket differs from the single-workgroup build (both are atomic
+// orders); no consumer depends on it (every search breaks ties on the source index).
+struct HashPair {
+  HashJob j[2];
+};
+constexpr int kHashGrid = 32;  // workgroups per cloud
+
+LOAM_D int hash_table_size(const HashJob& j, int n) {
+  const int m = n >> j.shift;
+  const int T = next_pow2(m > 64 ? m : 64);
+  return T > j.tmax ? j.tmax : T;
+}
+LOAM_D int hash_count_of(const HashJob& j, int p) {
+  return *(const int*)((const char*)j.count + (size_t)p * j.count_stride_bytes);
+}
+
+__global__ __launch_bounds__(256) void k_hash_zero(HashPair hp) {
+  const HashJob& j = hp.j[blockIdx.z];
+  const int p = blockIdx.y;
+  const int T = hash_table_size(j, hash_count_of(j, p));
+  if (blockIdx.x == 0 && threadIdx.x == 0) j.tsize[p] = T;
+  int* fill = j.fill + (size_t)p * j.tmax;
+  for (int b = blockIdx.x * 256 + threadIdx.x; b < T; b += gridDim.x * 256) fill[b] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_hash_count(HashPair hp) {
+  const HashJob& j = hp.j[blockIdx.z];
+  const int p = blockIdx.y, tid = threadIdx.x;
+  const int n = hash_count_of(j, p);
+  const int T = hash_table_size(j, n);
+  const float4* pts = j.pts + (size_t)p * j.pts_stride + (j.pts_off ? j.pts_off[p * j.pts_off_stride] : 0);
+  int* fill = j.fill + (size_t)p * j.tmax;
+  for (int i = blockIdx.x * 256 + tid; i < n; i += gridDim.x * 256) {
+    const float4 a = pts[i];
+    const uint32_t h = cell_hash(cell_of(a.x, j.inv_h), cell_of(a.y, j.inv_h), cell_of(a.z, j.inv_h)) & (T - 1);
+    atomicAdd(&fill[h], 1);
+  }
+  if (j.chunks) {  // chunk boxes of the source order, one wave per 64-point chunk (as k_hash_build)
+    const int lane = lane_id(), w = tid >> 6;
+    const int nch = (n + kChunk - 1) / kChunk;
+    float4* ch = j.chunks + (size_t)p * 2 * chunks_of((int)j.pts_stride);
+    for (int c = blockIdx.x * 4 + w; c < nch; c += gridDim.x * 4) {
+      const int i = c * kChunk + lane;
+      float4 a = pts[min(i, n - 1)];
+      const float r = (float)(int)a.w;
+      const float4 lo = make_float4(wave_min_f(a.x), wave_min_f(a.y), wave_min_f(a.z), wave_min_f(r));
+      const float4 hi = make_float4(wave_max_f(a.x), wave_max_f(a.y), wave_max_f(a.z), wave_max_f(r));
+      if (lane == 0) {
+        ch[2 * c] = lo;
+        ch[2 * c + 1] = hi;
+      }
+    }
+  }
+}
+
+// exclusive scan of the counters into start (and back into fill as the scatter's cursors)
+__global__ __launch_bounds__(1024) void k_hash_scan(HashPair hp) {
+  const HashJob& j = hp.j[blockIdx.z];
+  const int p = blockIdx.y, tid = threadIdx.x;
+  const int n = hash_count_of(j, p);
+  const int T = hash_table_size(j, n);
+  int* fill = j.fill + (size_t)p * j.tmax;
+  int* start = j.start + (size_t)p * (j.tmax + 1);
+  __shared__ int scratch[32];
+  const int per = (T + 1023) / 1024;
+  const int b0 = tid * per, b1 = min(T, b0 + per);
+  int local = 0;
+  for (int b = b0; b < b1; ++b) local += fill[b];
+  int tot;
+  int run = block_excl_scan<1024>(local, scratch, tot);
+  for (int b = b0; b < b1; ++b) {
+    const int c = fill[b];
+    start[b] = run;
+    fill[b] = run;
+    run += c;
+  }
+  if (tid == 0) start[T] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_hash_scatter(HashPair hp) {
+  const HashJob& j = hp.j[blockIdx.z];
+  const int p = blockIdx.y;
+  const int n = hash_count_of(j, p);
+  const int T = hash_table_size(j, n);
+  const float4* pts = j.pts + (size_t)p * j.pts_stride + (j.pts_off ? j.pts_off[p * j.pts_off_stride] : 0);
+  int* fill = j.fill + (size_t)p * j.tmax;
+  float4* out = j.out + (size_t)p * j.pts_stride;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const float4 a = pts[i];
+    const uint32_t h = cell_hash(cell_of(a.x, j.inv_h), cell_of(a.y, j.inv_h), cell_of(a.z, j.inv_h)) & (T - 1);
+    const int pos = atomicAdd(&fill[h], 1);
+    const int tag = j.chunks ? (i | ((int)a.w << 24)) : i;
+    out[pos] = make_float4(a.x, a.y, a.z, __int_as_float(tag));
+  }
+}
+
+void hash_build_pair(const HashJob& a, const HashJob& b, int P, hipStream_t st) {
+  if (P > 4) {  // batches: a workgroup per cloud fills the chip
+    hipLaunchKernelGGL(k_hash_build, dim3(P), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_hash_build, dim3(P), dim3(256), 0, st, b);
+    return;
+  }
+  HashPair hp;
+  hp.j[0] = a;
+  hp.j[1] = b;
+  hipLaunchKernelGGL(k_hash_zero, dim3(kHashGrid, P, 2), dim3(256), 0, st, hp);
+  hipLaunchKernelGGL(k_hash_count, dim3(kHashGrid, P, 2), dim3(256), 0, st, hp);
+  hipLaunchKernelGGL(k_hash_scan, dim3(1, P, 2), dim3(1024), 0, st, hp);
+  hipLaunchKernelGGL(k_hash_scatter, dim3(kHashGrid, P, 2), dim3(256), 0, st, hp);
+}
+
 namespace {
 
 
@@ -406,7 +520,9 @@ __global__ __launch_bounds__(kOdThreads) void k_od_sel(OdBuffers b, FeatView f) 
 // 8 waves per SIMD (<= 64 VGPRs, <= 100 SGPRs; 7 by default): the association is bound by its
 // dependent chain per query, so occupancy is its throughput (measured 3.8 -> 3.2 ms per step)
 // COUNT: the profiling variant that also sums the points / chunk boxes it loads into istate
-template <bool COUNT>
+// SEL: the wave computes its query's TransformToStart itself (small batches: one launch fewer per
+// association round); otherwise it reads k_od_sel's result
+template <bool COUNT, bool SEL>
 __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_od_assoc(OdBuffers b, FeatView f, int last_buf) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, lane = lane_id(), w = threadIdx.x >> 6;
@@ -422,7 +538,17 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(8)))
   int* ind = b.ind + (size_t)p * 3 * b.cap_q;
   int wpts = 0, wbox = 0;  // wave-uniform work counters (loam_stats od_assoc_gathered / _boxes)
   for (int q = blk.x * kOdWaves + w; q < nq; q += gridDim.x * kOdWaves) {
-    const float4 s4 = sel[q];
+    float4 s4;
+    if constexpr (SEL) {
+      const float* st = b.state + (size_t)p * kOdStateFloats;
+      float T[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) T[k] = st[k];
+      const float4 po = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
+      s4 = loampose::transform_to_start(T, po);
+    } else {
+      s4 = sel[q];
+    }
     int i1, i2, i3 = -1;
     if (q < nc) {
       const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
@@ -482,13 +608,122 @@ LOAM_D void od_step(const OdBuffers& b, int p, int iter, const double* tot, floa
   }
 }
 
-// one iteration's rows (lane per query): this iteration's residual + weight (:530-583,
-// :653-694) stored at [iter][q]; then the Jacobian of every row accumulated so far (Q12: rows
-// of iterations 0..iter, all evaluated at the current transform, :708-764) summed in fp64 into
-// this workgroup's partial JᵀJ / Jᵀb / row count.  A rejected correspondence is stored as a zero
-// coefficient, which adds exact zeros.
+// The residual + weight of query q at this iteration (:530-583 corner, :653-694 surf) against its
+// association; a rejected correspondence is a zero coefficient (it then adds exact zeros).
+LOAM_D void od_row_coeff(const OdBuffers& b, const FeatView& f, int p, int q, int nc, size_t lp, int iter,
+                         const float* T, float4 po, float4& cf, int& ok) {
+  const float4 s4 = loampose::transform_to_start(T, po);
+  const int* ind = b.ind + (size_t)p * 3 * b.cap_q;
+  const int i1 = ind[q], i2 = ind[b.cap_q + q], i3 = ind[2 * b.cap_q + q];
+  LOAM_CHECK(q < b.cap_q && iter < b.max_iter, q, iter);
+  LOAM_CHECK(i1 < b.nlast[(p * 2 + (int)(lp / (size_t)b.P)) * 2 + (q < nc ? 0 : 1)], i1, q);
+  ok = 0;
+  cf = make_float4(0, 0, 0, 0);
+  if (q < nc) {
+    if (i2 >= 0) {
+      const float4* CL = b.lastC + lp * b.capC;
+      const float4 t1 = CL[i1], t2 = CL[i2];
+      const float x0 = s4.x, y0 = s4.y, z0 = s4.z;
+      const float x1 = t1.x, y1 = t1.y, z1 = t1.z, x2 = t2.x, y2 = t2.y, z2 = t2.z;
+      const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
+      const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
+      const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
+      const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
+      const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
+      const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
+      const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
+      const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
+      const float ld2 = a012 / l12;
+      float sw = 1;
+      if (iter >= 5) sw = (float)(1 - 1.8 * fabs(D(ld2)));
+      cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
+      ok = (D(sw) > 0.1 && ld2 != 0) ? 1 : 0;
+    }
+  } else if (i2 >= 0 && i3 >= 0) {
+    const float4* SL = b.lastS + lp * b.capS;
+    const float4 t1 = SL[i1], t2 = SL[i2], t3 = SL[i3];
+    float pa = (t2.y - t1.y) * (t3.z - t1.z) - (t3.y - t1.y) * (t2.z - t1.z);
+    float pb = (t2.z - t1.z) * (t3.x - t1.x) - (t3.z - t1.z) * (t2.x - t1.x);
+    float pc = (t2.x - t1.x) * (t3.y - t1.y) - (t3.x - t1.x) * (t2.y - t1.y);
+    float pd = -(pa * t1.x + pb * t1.y + pc * t1.z);
+    const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
+    pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+    const float pd2 = pa * s4.x + pb * s4.y + pc * s4.z + pd;
+    float sw = 1;
+    if (iter >= 5)
+      sw = (float)(1 - 1.8 * fabs(D(pd2)) / sqrt(sqrt(D(s4.x * s4.x + s4.y * s4.y + s4.z * s4.z))));
+    cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
+    ok = (D(sw) > 0.1 && pd2 != 0) ? 1 : 0;
+  }
+  if (!ok) cf = make_float4(0, 0, 0, 0);
+}
+
+// The coefficient-free factors of each Jacobian entry (:714-753) of a row whose raw point is po:
+// every entry is (e0)*coeff.x + (e1)*coeff.y + (e2)*coeff.z with e depending on the raw point and
+// the current transform only, evaluated in the reference's expression order
+struct OdJf {
+  float e00, e01, e02, e10, e12, e20, e21, e22, e30, e31, e32, e40, e41, e42, e50, e51, e52;
+};
+LOAM_D OdJf od_jfactors(const float* trig, const float* T, float4 po) {
+  const float srx = trig[0], crx = trig[1], sry = trig[2], cry = trig[3], srz = trig[4], crz = trig[5];
+  const float sw = 1;
+  const float tx = sw * T[3], ty = sw * T[4], tz = sw * T[5];
+  OdJf e;
+  e.e00 = (-sw * crx * sry * srz * po.x + sw * crx * crz * sry * po.y + sw * srx * sry * po.z +
+           sw * tx * crx * sry * srz - sw * ty * crx * crz * sry - sw * tz * srx * sry);
+  e.e01 = (sw * srx * srz * po.x - sw * crz * srx * po.y + sw * crx * po.z + sw * ty * crz * srx -
+           sw * tz * crx - sw * tx * srx * srz);
+  e.e02 = (sw * crx * cry * srz * po.x - sw * crx * cry * crz * po.y - sw * cry * srx * po.z +
+           sw * tz * cry * srx + sw * ty * crx * cry * crz - sw * tx * crx * cry * srz);
+  e.e10 = ((-sw * crz * sry - sw * cry * srx * srz) * po.x + (sw * cry * crz * srx - sw * sry * srz) * po.y -
+           sw * crx * cry * po.z + tx * (sw * crz * sry + sw * cry * srx * srz) +
+           ty * (sw * sry * srz - sw * cry * crz * srx) + sw * tz * crx * cry);
+  e.e12 = ((sw * cry * crz - sw * srx * sry * srz) * po.x + (sw * cry * srz + sw * crz * srx * sry) * po.y -
+           sw * crx * sry * po.z + sw * tz * crx * sry - ty * (sw * cry * srz + sw * crz * srx * sry) -
+           tx * (sw * cry * crz - sw * srx * sry * srz));
+  e.e20 = ((-sw * cry * srz - sw * crz * srx * sry) * po.x + (sw * cry * crz - sw * srx * sry * srz) * po.y +
+           tx * (sw * cry * srz + sw * crz * srx * sry) - ty * (sw * cry * crz - sw * srx * sry * srz));
+  e.e21 = (-sw * crx * crz * po.x - sw * crx * srz * po.y + sw * ty * crx * srz + sw * tx * crx * crz);
+  e.e22 = ((sw * cry * crz * srx - sw * sry * srz) * po.x + (sw * crz * sry + sw * cry * srx * srz) * po.y +
+           tx * (sw * sry * srz - sw * cry * crz * srx) - ty * (sw * crz * sry + sw * cry * srx * srz));
+  e.e30 = -sw * (cry * crz - srx * sry * srz); e.e31 = sw * crx * srz; e.e32 = sw * (crz * sry + cry * srx * srz);
+  e.e40 = -sw * (cry * srz + crz * srx * sry); e.e41 = sw * crx * crz; e.e42 = sw * (sry * srz - cry * crz * srx);
+  e.e50 = sw * crx * sry; e.e51 = sw * srx; e.e52 = sw * crx * cry;
+  return e;
+}
+
+// one row's J (:708-753), B = -0.05 * d2 (:763), JᵀJ / Jᵀb / count added in fp64
+LOAM_D void od_row_accum(const OdJf& e, float4 c4, bool okit, double (&acc)[28]) {
+  float a[6];
+  a[0] = e.e00 * c4.x + e.e01 * c4.y + e.e02 * c4.z;
+  a[1] = e.e10 * c4.x + e.e12 * c4.z;
+  a[2] = e.e20 * c4.x + e.e21 * c4.y + e.e22 * c4.z;
+  a[3] = e.e30 * c4.x + e.e31 * c4.y - e.e32 * c4.z;
+  a[4] = e.e40 * c4.x - e.e41 * c4.y - e.e42 * c4.z;
+  a[5] = e.e50 * c4.x - e.e51 * c4.y - e.e52 * c4.z;
+  const float bb = (float)(-0.05 * D(c4.w));
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
+  acc[27] += okit ? 1.0 : 0.0;
+}
+
+LOAM_D void od_trig(const float* T, float* trig) {
+  for (int k = 0; k < 3; ++k) {
+    trig[2 * k] = (float)dsin(1 * T[k]);
+    trig[2 * k + 1] = (float)dcos(1 * T[k]);
+  }
+}
+
+// one iteration's rows (lane per query): this iteration's residual + weight stored at [iter][q];
+// then the Jacobian of every row accumulated so far (Q12: rows of iterations 0..iter, all
+// evaluated at the current transform, :708-764) summed in fp64 into this workgroup's partial
+// JᵀJ / Jᵀb / row count; k_od_step sums the partials.  Large batches.
 constexpr int kOdRowsWpe = 4;  // <= 128 VGPRs with two rows' loads in flight
-template <bool FUSED>
 __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdRowsWpe))) void k_od_rows(OdBuffers b, FeatView f, int last_buf, int iter) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
@@ -500,11 +735,7 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdR
   float T[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) T[k] = st[k];
-  if (tid == 0)
-    for (int k = 0; k < 3; ++k) {
-      trig[2 * k] = (float)dsin(1 * T[k]);
-      trig[2 * k + 1] = (float)dcos(1 * T[k]);
-    }
+  if (tid == 0) od_trig(T, trig);
   const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
   const int q = blk.x * kOdThreads + tid;
   const size_t lp = (size_t)last_buf * b.P + p;
@@ -513,84 +744,18 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdR
   float4 po = make_float4(0, 0, 0, 0);
   if (q < nq) {
     po = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
-    const float4 s4 = loampose::transform_to_start(T, po);
-    const int* ind = b.ind + (size_t)p * 3 * b.cap_q;
-    const int i1 = ind[q], i2 = ind[b.cap_q + q], i3 = ind[2 * b.cap_q + q];
-    LOAM_CHECK(q < b.cap_q && iter < b.max_iter, q, iter);
-    LOAM_CHECK(i1 < (q < nc ? b.nlast[(p * 2 + last_buf) * 2 + 0] : b.nlast[(p * 2 + last_buf) * 2 + 1]), i1, q);
-    int ok = 0;
-    float4 cf = make_float4(0, 0, 0, 0);
-    if (q < nc) {
-      if (i2 >= 0) {
-        const float4* CL = b.lastC + lp * b.capC;
-        const float4 t1 = CL[i1], t2 = CL[i2];
-        const float x0 = s4.x, y0 = s4.y, z0 = s4.z;
-        const float x1 = t1.x, y1 = t1.y, z1 = t1.z, x2 = t2.x, y2 = t2.y, z2 = t2.z;
-        const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
-        const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
-        const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
-        const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
-        const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
-        const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
-        const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
-        const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
-        const float ld2 = a012 / l12;
-        float sw = 1;
-        if (iter >= 5) sw = (float)(1 - 1.8 * fabs(D(ld2)));
-        cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
-        ok = (D(sw) > 0.1 && ld2 != 0) ? 1 : 0;
-      }
-    } else if (i2 >= 0 && i3 >= 0) {
-      const float4* SL = b.lastS + lp * b.capS;
-      const float4 t1 = SL[i1], t2 = SL[i2], t3 = SL[i3];
-      float pa = (t2.y - t1.y) * (t3.z - t1.z) - (t3.y - t1.y) * (t2.z - t1.z);
-      float pb = (t2.z - t1.z) * (t3.x - t1.x) - (t3.z - t1.z) * (t2.x - t1.x);
-      float pc = (t2.x - t1.x) * (t3.y - t1.y) - (t3.x - t1.x) * (t2.y - t1.y);
-      float pd = -(pa * t1.x + pb * t1.y + pc * t1.z);
-      const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
-      pa /= ps; pb /= ps; pc /= ps; pd /= ps;
-      const float pd2 = pa * s4.x + pb * s4.y + pc * s4.z + pd;
-      float sw = 1;
-      if (iter >= 5)
-        sw = (float)(1 - 1.8 * fabs(D(pd2)) / sqrt(sqrt(D(s4.x * s4.x + s4.y * s4.y + s4.z * s4.z))));
-      cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
-      ok = (D(sw) > 0.1 && pd2 != 0) ? 1 : 0;
-    }
-    if (!ok) cf = make_float4(0, 0, 0, 0);
+    float4 cf;
+    int ok;
+    od_row_coeff(b, f, p, q, nc, lp, iter, T, po, cf, ok);
     qcf[(size_t)iter * b.cap_q + q] = cf;
     qok[(size_t)iter * b.cap_q + q] = (int8_t)ok;
   }
   __syncthreads();
-  const float srx = trig[0], crx = trig[1], sry = trig[2], cry = trig[3], srz = trig[4], crz = trig[5];
-  const float sw = 1;
-  const float tx = sw * T[3], ty = sw * T[4], tz = sw * T[5];
   double acc[28];
 #pragma unroll
   for (int k = 0; k < 28; ++k) acc[k] = 0.0;
   if (q < nq) {
-    // the coefficient-free factors of each Jacobian entry (:714-753): every entry is
-    // (e0)*coeff.x + (e1)*coeff.y + (e2)*coeff.z with e depending on the raw point and the current
-    // transform only, so they are evaluated once per query, in the reference's expression order
-    const float e00 = (-sw * crx * sry * srz * po.x + sw * crx * crz * sry * po.y + sw * srx * sry * po.z +
-                       sw * tx * crx * sry * srz - sw * ty * crx * crz * sry - sw * tz * srx * sry);
-    const float e01 = (sw * srx * srz * po.x - sw * crz * srx * po.y + sw * crx * po.z + sw * ty * crz * srx -
-                       sw * tz * crx - sw * tx * srx * srz);
-    const float e02 = (sw * crx * cry * srz * po.x - sw * crx * cry * crz * po.y - sw * cry * srx * po.z +
-                       sw * tz * cry * srx + sw * ty * crx * cry * crz - sw * tx * crx * cry * srz);
-    const float e10 = ((-sw * crz * sry - sw * cry * srx * srz) * po.x + (sw * cry * crz * srx - sw * sry * srz) * po.y -
-                       sw * crx * cry * po.z + tx * (sw * crz * sry + sw * cry * srx * srz) +
-                       ty * (sw * sry * srz - sw * cry * crz * srx) + sw * tz * crx * cry);
-    const float e12 = ((sw * cry * crz - sw * srx * sry * srz) * po.x + (sw * cry * srz + sw * crz * srx * sry) * po.y -
-                       sw * crx * sry * po.z + sw * tz * crx * sry - ty * (sw * cry * srz + sw * crz * srx * sry) -
-                       tx * (sw * cry * crz - sw * srx * sry * srz));
-    const float e20 = ((-sw * cry * srz - sw * crz * srx * sry) * po.x + (sw * cry * crz - sw * srx * sry * srz) * po.y +
-                       tx * (sw * cry * srz + sw * crz * srx * sry) - ty * (sw * cry * crz - sw * srx * sry * srz));
-    const float e21 = (-sw * crx * crz * po.x - sw * crx * srz * po.y + sw * ty * crx * srz + sw * tx * crx * crz);
-    const float e22 = ((sw * cry * crz * srx - sw * sry * srz) * po.x + (sw * crz * sry + sw * cry * srx * srz) * po.y +
-                       tx * (sw * sry * srz - sw * cry * crz * srx) - ty * (sw * crz * sry + sw * cry * srx * srz));
-    const float e30 = -sw * (cry * crz - srx * sry * srz), e31 = sw * crx * srz, e32 = sw * (crz * sry + cry * srx * srz);
-    const float e40 = -sw * (cry * srz + crz * srx * sry), e41 = sw * crx * crz, e42 = sw * (sry * srz - cry * crz * srx);
-    const float e50 = sw * crx * sry, e51 = sw * srx, e52 = sw * crx * cry;
+    const OdJf e = od_jfactors(trig, T, po);
     // the stored rows two iterations at a time (their loads in flight together), summed in order
     for (int it0 = 0; it0 <= iter; it0 += 2) {
       float4 cv4[2];
@@ -602,31 +767,12 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdR
         okv[u] = it <= iter ? qok[(size_t)it * b.cap_q + q] != 0 : false;
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-      if (it0 + u > iter) break;
-      const float4 c4 = cv4[u];
-      const bool okit = okv[u];
-      float a[6];
-      a[0] = e00 * c4.x + e01 * c4.y + e02 * c4.z;
-      a[1] = e10 * c4.x + e12 * c4.z;
-      a[2] = e20 * c4.x + e21 * c4.y + e22 * c4.z;
-      a[3] = e30 * c4.x + e31 * c4.y - e32 * c4.z;
-      a[4] = e40 * c4.x - e41 * c4.y - e42 * c4.z;
-      a[5] = e50 * c4.x - e51 * c4.y - e52 * c4.z;
-      const float bb = (float)(-0.05 * D(c4.w));
-      int k = 0;
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
-      acc[27] += okit ? 1.0 : 0.0;
-    }
+      for (int u = 0; u < 2; ++u)
+        if (it0 + u <= iter) od_row_accum(e, cv4[u], okv[u], acc);
     }
   }
-  // wave sums of the 28 values as a butterfly reduce-scatter (32 slots halved per step: 32
-  // shuffles instead of 28 x 6); lanes 2v, 2v+1 end with the sum of value v
+  // wave sums of the 28 values as a butterfly reduce-scatter (32 shuffles instead of 28 x 6);
+  // lanes 2v, 2v+1 end with the sum of value v
   wave_reduce_scatter_28(acc);
   if ((lane & 1) == 0 && (lane >> 1) < 28) red[w][lane >> 1] = acc[0];
   __syncthreads();
@@ -634,23 +780,93 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdR
     double v = red[0][tid];
     for (int ww = 1; ww < kOdWaves; ++ww) v += red[ww][tid];
     b.part[((size_t)p * b.gq + blk.x) * 28 + tid] = v;
-    if (FUSED) __threadfence();  // partials visible device-wide before this workgroup reports done
   }
-  if (!FUSED) return;
-  // small batches (streaming): the last workgroup of the problem to finish runs the 6x6 step,
-  // saving a dependent launch per iteration; large batches launch k_od_step instead
+}
+
+// Small batches (streaming, config 2): a workgroup per (256 queries, stored iteration) pair, each
+// lane one row, so the Q12 re-evaluation of every stored row is one load deep instead of a chain
+// of (iter + 1) per lane; the workgroups of the current iteration compute and store the new
+// residuals.  The last workgroup of the problem to finish sums the gq * (iter + 1) partials in a
+// fixed order and runs the 6x6 step (one launch per iteration).
+__global__ __launch_bounds__(kOdThreads) void k_od_rows_small(OdBuffers b, FeatView f, int last_buf, int iter) {
+  const int p = blockIdx.y, it = blockIdx.z, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int* ist = b.istate + (size_t)p * kOdStateInts;
+  if (!ist[kIsActive] || ist[kIsStop]) return;
+  __shared__ double red[kOdWaves][28];
+  __shared__ float trig[6];
+  const float* st = b.state + (size_t)p * kOdStateFloats;
+  float T[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) T[k] = st[k];
+  if (tid == 0) od_trig(T, trig);
+  const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
+  const int q = blockIdx.x * kOdThreads + tid;
+  const size_t lp = (size_t)last_buf * b.P + p;
+  float4* qcf = b.q_cf + (size_t)p * b.max_iter * b.cap_q;
+  int8_t* qok = b.q_ok + (size_t)p * b.max_iter * b.cap_q;
+  float4 po = make_float4(0, 0, 0, 0), c4 = po;
+  bool okit = false;
+  if (q < nq) {
+    po = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
+    if (it == iter) {
+      int ok;
+      od_row_coeff(b, f, p, q, nc, lp, iter, T, po, c4, ok);
+      okit = ok != 0;
+      qcf[(size_t)iter * b.cap_q + q] = c4;
+      qok[(size_t)iter * b.cap_q + q] = (int8_t)ok;
+    } else {
+      c4 = qcf[(size_t)it * b.cap_q + q];
+      okit = qok[(size_t)it * b.cap_q + q] != 0;
+    }
+  }
+  __syncthreads();
+  double acc[28];
+#pragma unroll
+  for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+  if (q < nq) od_row_accum(od_jfactors(trig, T, po), c4, okit, acc);
+  wave_reduce_scatter_28(acc);
+  if ((lane & 1) == 0 && (lane >> 1) < 28) red[w][lane >> 1] = acc[0];
+  __syncthreads();
+  const int G = (int)gridDim.x * (iter + 1), g = it * (int)gridDim.x + (int)blockIdx.x;
+  if (tid < 28) {
+    double v = red[0][tid];
+    for (int ww = 1; ww < kOdWaves; ++ww) v += red[ww][tid];
+    b.part[((size_t)p * b.gq * b.max_iter + g) * 28 + tid] = v;
+    __threadfence();  // partials visible device-wide before this workgroup reports done
+  }
   __shared__ int sh_last;
   __shared__ double tot[28];
   __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs];
   __shared__ int lm_iws[12];
   __syncthreads();
-  if (tid == 0) sh_last = atomicAdd(&b.done[p], 1) == (int)gridDim.x - 1;
+  if (tid == 0) sh_last = atomicAdd(&b.done[p], 1) == G - 1;
   __syncthreads();
   if (!sh_last) return;
-  if (tid < 28) {  // fixed order over the workgroups
-    double v = 0.0;
-    for (int g = 0; g < (int)gridDim.x; ++g)
-      v += __hip_atomic_load(&b.part[((size_t)p * b.gq + g) * 28 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // fixed-order sum of the G partials: thread (slice s, value v) sums partials s, s + 8, ... with
+  // all its loads in flight at once, then the eight slice sums are added in slice order
+  __shared__ double slice[8][28];
+  if (tid < 8 * 28) {
+    const int v = tid % 28, sl = tid / 28;
+    const double* pp = b.part + (size_t)p * b.gq * b.max_iter * 28 + v;
+    double t16[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int g = sl + 8 * u;
+      t16[u] = g < G ? __hip_atomic_load(&pp[(size_t)g * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    }
+    double acc1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (sl + 8 * u < G) acc1 += t16[u];
+    for (int g = sl + 8 * 16; g < G; g += 8)  // beyond 128 partials (larger sweeps)
+      acc1 += __hip_atomic_load(&pp[(size_t)g * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    slice[sl][v] = acc1;
+  }
+  __syncthreads();
+  if (tid < 28) {
+    double v = slice[0][tid];
+#pragma unroll
+    for (int sl = 1; sl < 8; ++sl) v += slice[sl][tid];
     tot[tid] = v;
   }
   __syncthreads();
@@ -766,7 +982,8 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   A(&b.sel, (size_t)P * b.cap_q * sizeof(float4));
   A(&b.q_cf, (size_t)P * max_iter * b.cap_q * sizeof(float4));
   A(&b.q_ok, (size_t)P * max_iter * b.cap_q * sizeof(int8_t));
-  A(&b.part, (size_t)P * b.gq * 28 * sizeof(double));
+  // per-workgroup partials: [P][gq][28], or [P][gq * max_iter][28] for the small-batch rows kernel
+  A(&b.part, (size_t)P * b.gq * (P < 64 ? max_iter : 1) * 28 * sizeof(double));
   A(&b.done, (size_t)P * sizeof(int));
   if (A.err != hipSuccess) {
     od_free(b);
@@ -809,7 +1026,6 @@ void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
   jc.inv_h = 1.0f;
   jc.shift = 1;
   jc.chunks = b.cC + (size_t)buf * b.P * 2 * chunks_of(b.capC);
-  hipLaunchKernelGGL(k_hash_build, dim3(b.P), dim3(256), 0, st, jc);
   HashJob js = jc;
   js.pts = b.lastS + (size_t)buf * b.P * b.capS;
   js.pts_stride = b.capS;
@@ -820,36 +1036,42 @@ void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
   js.tsize = b.hS_T + buf * b.P;
   js.tmax = b.tS;
   js.chunks = b.cS + (size_t)buf * b.P * 2 * chunks_of(b.capS);
-  hipLaunchKernelGGL(k_hash_build, dim3(b.P), dim3(256), 0, st, js);
+  hash_build_pair(jc, js, b.P, st);
 }
 
 }  // namespace loam
 
 namespace loam {
-void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t st, Prof* prof) {
+void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t st, Prof* prof, bool device_fini) {
   const int P = b.P;
   auto mark = [&](const char* n) { if (prof) prof->mark(n); };
   hipLaunchKernelGGL(k_od_begin, dim3((P + 255) / 256), dim3(256), 0, st, b, f);
   for (int it = 0; it < b.max_iter; ++it) {
     if (it % 5 == 0) {  // Q10
-      hipLaunchKernelGGL(k_od_sel, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f);
-      // one wave per query when the batch is small (streaming), 64 waves per problem otherwise
+      // one wave per query when the batch is small (streaming: TransformToStart in the wave), 64
+      // waves per problem otherwise (the queries transformed by k_od_sel first)
       const int ga = P >= 64 ? 16 : (b.cap_q + kOdWaves - 1) / kOdWaves;
-      if (prof) hipLaunchKernelGGL(k_od_assoc<true>, dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
-      else hipLaunchKernelGGL(k_od_assoc<false>, dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
+      if (P >= 64) {
+        hipLaunchKernelGGL(k_od_sel, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f);
+        if (prof) hipLaunchKernelGGL((k_od_assoc<true, false>), dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
+        else hipLaunchKernelGGL((k_od_assoc<false, false>), dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
+      } else {
+        if (prof) hipLaunchKernelGGL((k_od_assoc<true, true>), dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
+        else hipLaunchKernelGGL((k_od_assoc<false, true>), dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
+      }
       mark("k_od_assoc");
     }
     if (P < 64) {  // measured: the fused step loses for large batches (its serial tail)
-      hipLaunchKernelGGL(k_od_rows<true>, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+      hipLaunchKernelGGL(k_od_rows_small, dim3(b.gq, P, it + 1), dim3(kOdThreads), 0, st, b, f, last_buf, it);
       mark("k_od_rows");
     } else {
-      hipLaunchKernelGGL(k_od_rows<false>, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+      hipLaunchKernelGGL(k_od_rows, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
       mark("k_od_rows");
       hipLaunchKernelGGL(k_od_step, dim3(P), dim3(64), 0, st, b, it, b.gq);
       mark("k_od_step");
     }
   }
-  hipLaunchKernelGGL(k_od_fini, dim3((P + 255) / 256), dim3(256), 0, st, b, f);
+  if (device_fini) hipLaunchKernelGGL(k_od_fini, dim3((P + 255) / 256), dim3(256), 0, st, b, f);
 }
 }  // namespace loam
 

@@ -80,6 +80,8 @@ struct OdBuffers {
 };
 
 __global__ void k_hash_build(HashJob j);
+// both clouds' indexes: a workgroup per cloud for batches, a grid per cloud for P <= 4
+void hash_build_pair(const HashJob& a, const HashJob& b, int P, hipStream_t st);
 
 __global__ void k_od_end(OdBuffers b, FeatView f, int dst, int mode, int do_full);
 
@@ -87,7 +89,9 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter);  // 
 void od_free(OdBuffers& b);
 void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st);
 // the laserOdometry L-M loop + pose accumulation for every problem against Last[last_buf]
-void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t st, Prof* prof = nullptr);
+// device_fini: the pose accumulation (k_od_fini) on the device; the streaming path does it on the host
+void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t st, Prof* prof = nullptr,
+              bool device_fini = true);
 
 }  // namespace loam
 
