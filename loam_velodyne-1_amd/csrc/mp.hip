@@ -52,6 +52,24 @@ LOAM_D int* slot_table(const MpBuffers& b, int pool, int p) {
 }
 
 // ---------------------------------------------------------------- prepare
+// sin / cos of the TobeMapped rotation in double (pointAssociateToMap, :240-257), kept per instance
+// in b.rot beside the state: written wherever transformTobeMapped changes (prepare, each L-M
+// step, the IMU blend), read by every kernel that maps points.  Per thread they were six double
+// sin / cos calls, the larger part of the 5-NN kernel's instructions.
+LOAM_D void rot_store(const MpBuffers& b, int p, const float* T) {
+  const loampose::MapRot r = loampose::map_rot(T);
+  double* d = b.rot + (size_t)p * 6;
+  d[0] = r.c0; d[1] = r.s0; d[2] = r.c1; d[3] = r.s1; d[4] = r.c2; d[5] = r.s2;
+}
+LOAM_D loampose::MapRot rot_load(const MpBuffers& b, int p) {
+  const double* d = b.rot + (size_t)p * 6;
+  const float* T = b.state + (size_t)p * kMpStateFloats + kMpTobe;
+  loampose::MapRot r;
+  r.c0 = d[0]; r.s0 = d[1]; r.c1 = d[2]; r.s1 = d[3]; r.c2 = d[4]; r.s2 = d[5];
+  r.t3 = T[3]; r.t4 = T[4]; r.t5 = T[5];
+  return r;
+}
+
 __global__ __launch_bounds__(kMpThreads) void k_mp_prepare(MpBuffers b, MpInput in) {
   const int p = blockIdx.x, tid = threadIdx.x;
   float* st = b.state + (size_t)p * kMpStateFloats;
@@ -67,6 +85,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_prepare(MpBuffers b, MpInput 
     loampose::associate_to_map(st + kMpSum, st + kMpBef, st + kMpAft, st + kMpIncre, st + kMpTobe);
     const float* T = st + kMpTobe;
     const loampose::MapRot r = loampose::map_rot(T);
+    rot_store(b, p, T);
     const float4 onY = loampose::point_to_map(r, make_float4(0.0f, 10.0f, 0.0f, 0.0f));
     st[kMpOnY] = onY.x; st[kMpOnY + 1] = onY.y; st[kMpOnY + 2] = onY.z;
     int cW = ist[kMiCenW], cH = ist[kMiCenH], cD = ist[kMiCenD];
@@ -190,7 +209,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_prepare(MpBuffers b, MpInput 
 __global__ __launch_bounds__(256) void k_mp_stack(MpBuffers b, MpInput in) {
   const int p = blockIdx.y;
   const float* st = b.state + (size_t)p * kMpStateFloats;
-  const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
+  const loampose::MapRot r = rot_load(b, p);
   const int nc = min(in.ncorner[p * in.ncorner_stride], b.capC);
   const int ns = min(in.nsurf[p * in.nsurf_stride], b.capS);
   float4* out = b.stack2 + (size_t)p * b.cap_stack;
@@ -959,6 +978,7 @@ LOAM_D void mp_step(const MpBuffers& b, int p, const double* tot, MpStepScratch&
     ist[kMiDegen] = degen;
     if (degen) ist[kMiDegSteps] += 1;
     for (int q = 0; q < 6; ++q) st[kMpTobe + q] += sh.X[q];
+    rot_store(b, p, st + kMpTobe);
     const float dR = loamla::delta_r(sh.X), dT = loamla::delta_t(sh.X);
     if (D(dR) < 0.05 && D(dT) < 0.05) ist[kMiStop] = 1;
   }
@@ -981,7 +1001,7 @@ __global__ __launch_bounds__(kMpQueryThreads) __attribute__((amdgpu_waves_per_eu
   __shared__ uint32_t lists[27 * kMpQueryThreads];
   uint32_t* lst = lists + tid;
   const bool first = ist[kMiIters] == 0;
-  const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
+  const loampose::MapRot r = rot_load(b, p);
   const MpNnCtx c = mp_nn_ctx(b, p);
   int work = 0;  // work counter (loam_stats mp_nn_candidates / mp_nn_cells), packed as in knn5
   for (int q = blk.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
@@ -1013,7 +1033,7 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
   const int4* qnn = b.q_nn + (size_t)p * b.cap_stack * 2;
   int8_t* qok = b.q_ok + (size_t)p * b.cap_stack;
   float4* qcf = b.q_cf + (size_t)p * b.cap_stack;
-  const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
+  const loampose::MapRot r = rot_load(b, p);
   float* jw = jac[tid];
   int nfits = 0;
   for (int q = blk.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
@@ -1132,6 +1152,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
       ist[kMiDegen] = degen;
       if (degen) ist[kMiDegSteps] += 1;
       for (int q = 0; q < 6; ++q) st[kMpTobe + q] += sh.X[q];  // no NaN guard in mapping (:956-961)
+      rot_store(b, p, st + kMpTobe);
       const float dR = loamla::delta_r(sh.X), dT = loamla::delta_t(sh.X);
       if (D(dR) < 0.05 && D(dT) < 0.05) ist[kMiStop] = 1;
     }
@@ -1160,7 +1181,7 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
   float4* qcf = b.q_cf + (size_t)p * b.cap_stack;
   const bool first = ist[kMiIters] == 0;
   if (tid == 0) mp_trig(st, trig);
-  const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
+  const loampose::MapRot r = rot_load(b, p);
   const MpNnCtx c = mp_nn_ctx(b, p);
   int work = 0, nfits = 0;  // (work: the batch kernel's profiling counter; not summed here)
   for (int q = blockIdx.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
@@ -1242,6 +1263,7 @@ __global__ void k_mp_lm_end(MpBuffers b) {
     const float imuRollLast = st[kMpImuRP], imuPitchLast = st[kMpImuRP + 1];
     st[kMpTobe + 0] = (float)(0.998 * D(st[kMpTobe + 0]) + 0.002 * D(imuPitchLast));
     st[kMpTobe + 2] = (float)(0.998 * D(st[kMpTobe + 2]) + 0.002 * D(imuRollLast));
+    rot_store(b, p, st + kMpTobe);
   }
   for (int k = 0; k < 6; ++k) {
     st[kMpBef + k] = st[kMpSum + k];
@@ -1260,7 +1282,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
   const int* ist = b.istate + (size_t)p * kMpStateInts;
   const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
   const float4* stack = b.stack + (size_t)p * b.cap_stack;
-  const loampose::MapRot r = loampose::map_rot(st + kMpTobe);
+  const loampose::MapRot r = rot_load(b, p);
   const int cW = ist[kMiCenW], cH = ist[kMiCenH], cD = ist[kMiCenD];
   int* so = slot_of + (size_t)p * b.cap_stack;
   int* ro = rank_of + (size_t)p * b.cap_stack;
@@ -1491,7 +1513,7 @@ __global__ __launch_bounds__(256) void k_mp_compact_copy(MpBuffers b) {
 
 __global__ __launch_bounds__(256) void k_mp_register(MpBuffers b, MpInput in) {
   const int p = blockIdx.y;
-  const loampose::MapRot r = loampose::map_rot(b.state + (size_t)p * kMpStateFloats + kMpTobe);
+  const loampose::MapRot r = rot_load(b, p);
   const int n = min(in.nfull[p * in.nfull_stride], b.capS);
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
     b.reg[(size_t)p * b.capS + i] = loampose::point_to_map(r, in.full[(size_t)p * in.full_stride + i]);
@@ -1570,6 +1592,7 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
   A(&b.cub_tmp, b.cub_bytes);
   A(&b.reg, (size_t)P * b.capS * sizeof(float4));
   A(&b.part, (size_t)P * kMpSmallGrid * 28 * sizeof(double));
+  A(&b.rot, (size_t)P * 6 * sizeof(double));
   A(&b.done, (size_t)P * sizeof(int));
   A(&b.nreg, (size_t)P * sizeof(int));
   if (A.err == hipSuccess) A.err = mp_reset(b, nullptr);
@@ -1583,7 +1606,7 @@ void mp_free(MpBuffers& b) {
                   b.stack2, b.stack, b.nstack, b.from, b.hC_start, b.hS_start, b.h_fill, b.hC_T, b.hS_T,
                   b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.citems, b.nitems, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
-                  b.vg_params, b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_bb, b.vg_be, b.vg_split, b.cub_tmp, b.reg, b.nreg, b.part, b.done};
+                  b.vg_params, b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_bb, b.vg_be, b.vg_split, b.cub_tmp, b.reg, b.nreg, b.part, b.done, b.rot};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = MpBuffers();

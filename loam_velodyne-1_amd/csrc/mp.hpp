@@ -109,6 +109,7 @@ struct MpBuffers {
   float4* reg = nullptr;      // [P][capS] registered full cloud
   double* part = nullptr;     // [P][kMpSmallGrid][28] k_mp_lm_small's per-workgroup JᵀJ | Jᵀb | rows
   int* done = nullptr;        // [P] its workgroups finished (the last one runs the step)
+  double* rot = nullptr;      // [P][6] cos / sin of the TobeMapped rotation (rot_store in mp.hip)
   int* nreg = nullptr;
   hipError_t sticky = hipSuccess;  // first failed library call of the launch sequences (hipCUB)
   void note(hipError_t e) {
