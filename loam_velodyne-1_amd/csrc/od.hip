@@ -335,7 +335,8 @@ template <typename F>
 LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int dir, int scan, float4 sel, int& wpts,
                         int& wbox, F f) {
   const int lane = lane_id();
-  auto stop_ring = [&](int r) { return dir > 0 ? D(r) > scan + 2.5 : D(r) < scan - 2.5; };
+  // int(intensity) > scan + 2.5 (double) <=> r > scan + 2 for integers (and < scan - 2.5 <=> < scan - 2)
+  auto stop_ring = [&](int r) { return dir > 0 ? r > scan + 2 : r < scan - 2; };
   // examines points [j0 .. j0 + dir * (cnt - 1)]; true when the stop was met
   auto run = [&](int j0, int cnt) {
     wpts += cnt;
@@ -523,7 +524,7 @@ __global__ __launch_bounds__(kOdThreads) void k_od_sel(OdBuffers b, FeatView f) 
 // SEL: the wave computes its query's TransformToStart itself (small batches: one launch fewer per
 // association round); otherwise it reads k_od_sel's result
 template <bool COUNT, bool SEL>
-__global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_od_assoc(OdBuffers b, FeatView f, int last_buf) {
+__global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(SEL ? 1 : 8))) void k_od_assoc(OdBuffers b, FeatView f, int last_buf) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, lane = lane_id(), w = threadIdx.x >> 6;
   const int* ist = b.istate + (size_t)p * kOdStateInts;
