@@ -387,6 +387,17 @@ def main(argv=None):
         if dom in ("k_mp_nn", "k_od_assoc") and achieved is not None:
             roof["l2_gather_peak"] = L2_GATHER_PEAK_GBS
             roof["l2_frac"] = achieved / L2_GATHER_PEAK_GBS
+            # SURVEY.md §8(d)'s algorithmic bytes of the same launches: per query-iteration the stack
+            # point and its 5 neighbours (16 + 80 B, B_MP), per association round every Last point
+            # once (16 B (C + S), B_OD)
+            alg = 96 * st_prof["mp_stack_iters"] if dom == "k_mp_nn" else 16 * st_prof["od_assoc_points"]
+            alg_launch = alg / launches_per_step
+            roof["survey_algorithmic"] = {"bytes_per_launch": alg_launch,
+                                          "achieved": alg_launch / (avg_ms * 1e-3) / 1e9,
+                                          "frac": alg_launch / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            if traffic:
+                roof["traffic_gbs"] = traffic / (avg_ms * 1e-3) / 1e9
+                roof["traffic_frac"] = roof["traffic_gbs"] / HBM_PEAK_GBS
 
     # CPU baseline: the oracle on a bounded sample, N=1 only
     cpu = parity = None
