@@ -263,8 +263,10 @@ LOAM_D float box_d2(const float4& lo, const float4& hi, const float4& s) {
 // closer than 5 m (the callers reject a nearest neighbour at >= 25 m², :481, :594).  First the
 // 27 cells around q (cells whose box lies >= h away skipped); if the best is >= h, the chunk
 // boxes of the whole cloud closer than 5 m.  `cells` = per-wave LDS scratch of 64 ints.
+// bound: the squared distance of a known point of the cloud (a seed), or above 25: cells and chunks
+// whose box lies beyond it cannot hold the minimum (which is <= the seed's) and are skipped
 LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const float4* cloud, const float4* ch,
-                             int n, float h, float inv_h, float4 q, int* cells, int& wpts, int& wbox) {
+                             int n, float h, float inv_h, float4 q, float bound, int* cells, int& wpts, int& wbox) {
   const int lane = lane_id();
   const int cx = cell_of(q.x, inv_h), cy = cell_of(q.y, inv_h), cz = cell_of(q.z, inv_h);
   int bucket = -1, b0 = 0, cnt = 0;
@@ -272,7 +274,8 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
     const int dx = lane % 3 - 1, dy = (lane / 3) % 3 - 1, dz = lane / 9 - 1;
     const float4 lo = make_float4((float)(cx + dx) * h, (float)(cy + dy) * h, (float)(cz + dz) * h, 0.0f);
     const float4 hi = make_float4((float)(cx + dx + 1) * h, (float)(cy + dy + 1) * h, (float)(cz + dz + 1) * h, 0.0f);
-    if (h != 1.0f || box_d2(lo, hi, q) < 1.0f) {
+    const float bd = box_d2(lo, hi, q);
+    if (h != 1.0f || (bd < 1.0f && bd <= bound)) {
       bucket = (int)(cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1));
       b0 = start[bucket];
       cnt = start[bucket + 1] - b0;
@@ -307,7 +310,9 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
   const int nch = (n + kChunk - 1) / kChunk;
   for (int k0 = 0; k0 < nch; k0 += 64) {
     const int k = k0 + lane;
-    const bool need = k < nch && box_d2(ch[2 * k], ch[2 * k + 1], q) < 25.0f;
+    float bd = 0.0f;
+    if (k < nch) bd = box_d2(ch[2 * k], ch[2 * k + 1], q);
+    const bool need = k < nch && bd < 25.0f && bd <= bound;
     uint64_t nb = __ballot(need);
     wbox += min(64, nch - k0);
     while (nb) {
@@ -331,9 +336,10 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
 // lies beyond scan +- 2.5.  `f(j, a, d)` is called by the lane holding point j (before the stop)
 // with d < 25.  Whole 64-point chunks whose box is >= 5 m from sel are skipped; a chunk that may
 // hold the stop is always examined.
+// bw: chunks whose box lies beyond it are skipped too (a seed's squared distance, or 25)
 template <typename F>
-LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int dir, int scan, float4 sel, int& wpts,
-                        int& wbox, F f) {
+LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int dir, int scan, float4 sel, float bw,
+                        int& wpts, int& wbox, F f) {
   const int lane = lane_id();
   // int(intensity) > scan + 2.5 (double) <=> r > scan + 2 for integers (and < scan - 2.5 <=> < scan - 2)
   auto stop_ring = [&](int r) { return dir > 0 ? r > scan + 2 : r < scan - 2; };
@@ -366,7 +372,8 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
       if (v) { lo = ch[2 * k]; hi = ch[2 * k + 1]; }
       const uint64_t mc = __ballot(v && stop_ring((int)hi.w));
       const int limit = mc ? __ffsll((unsigned long long)mc) - 1 : 63;
-      uint64_t nb = __ballot(v && lane <= limit && box_d2(lo, hi, sel) < 25.0f);
+      const float bd = box_d2(lo, hi, sel);
+      uint64_t nb = __ballot(v && lane <= limit && bd < 25.0f && bd <= bw);
       bool stopped = false;
       while (nb && !stopped) {
         const int kk = (j / kChunk) + __ffsll((unsigned long long)nb) - 1;
@@ -390,7 +397,8 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
       if (v) { lo = ch[2 * k]; hi = ch[2 * k + 1]; }
       const uint64_t mc = __ballot(v && stop_ring((int)lo.w));
       const int limit = mc ? __ffsll((unsigned long long)mc) - 1 : 63;
-      uint64_t nb = __ballot(v && lane <= limit && box_d2(lo, hi, sel) < 25.0f);
+      const float bd = box_d2(lo, hi, sel);
+      uint64_t nb = __ballot(v && lane <= limit && bd < 25.0f && bd <= bw);
       bool stopped = false;
       while (nb && !stopped) {
         const int kk = kt - (__ffsll((unsigned long long)nb) - 1);
@@ -405,8 +413,17 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
 
 // corner association (:478-527): closest (kd NN, sqDis < 25) and the best point of an adjacent
 // ring in the index window.  fwd_end = min(cornerPointsSharpNum, C) (Q11).
+// A seed (sj, sd): the previous association round's choice for this query and its squared distance
+// now (sj < 0: none).  When it belongs to this round's window set (the sets are ring ranges of the
+// ring-major Last cloud, see wave_window) it bounds the window minimum, so chunks beyond it are
+// skipped; the minimum itself is still taken over every point the walk visits.
+LOAM_D bool window_member(int j, int r, int c, int scan, int fwd_end, bool corner, bool same) {
+  if (j > c) return j < fwd_end && r <= scan + 2 && (corner ? r > scan : (same ? r <= scan : r > scan));
+  return j < c && r >= scan - 2 && (corner ? r < scan : (same ? r >= scan : r < scan));
+}
+
 LOAM_D void wave_assoc_corner(const float4* CL, const float4* ch, int fwd_end, uint64_t nn, float4 sel,
-                              int& ind1, int& ind2, int& wpts, int& wbox) {
+                              int sj, int sr, float sd, int& ind1, int& ind2, int& wpts, int& wbox) {
   ind1 = -1;
   ind2 = -1;
   if (nn == ~0ull) return;
@@ -414,14 +431,15 @@ LOAM_D void wave_assoc_corner(const float4* CL, const float4* ch, int fwd_end, u
   if (!(D(d0) < 25)) return;
   const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u);
   ind1 = c;
+  const float bw = sj >= 0 && window_member(sj, sr, c, scan, fwd_end, true, false) ? sd : 25.0f;
   uint64_t best = ~0ull;
-  wave_window(CL, ch, c, fwd_end, +1, scan, sel, wpts, wbox, [&](int j, int r, float d) {
+  wave_window(CL, ch, c, fwd_end, +1, scan, sel, bw, wpts, wbox, [&](int j, int r, float d) {
     if (r > scan) {
       const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)(j - c - 1);
       best = key < best ? key : best;
     }
   });
-  wave_window(CL, ch, c, fwd_end, -1, scan, sel, wpts, wbox, [&](int j, int r, float d) {
+  wave_window(CL, ch, c, fwd_end, -1, scan, sel, bw, wpts, wbox, [&](int j, int r, float d) {
     if (r < scan) {
       const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)((1u << 30) + (c - 1 - j));
       best = key < best ? key : best;
@@ -437,6 +455,7 @@ LOAM_D void wave_assoc_corner(const float4* CL, const float4* ch, int fwd_end, u
 // surface association (:590-650): closest, the best of the same / lower ring (min2) and of the
 // higher rings (min3) in the forward window; mirrored in the backward window.
 LOAM_D void wave_assoc_surf(const float4* SL, const float4* ch, int fwd_end, uint64_t nn, float4 sel,
+                            int sj2, int sr2, float sd2, int sj3, int sr3, float sd3,
                             int& ind1, int& ind2, int& ind3, int& wpts, int& wbox) {
   ind1 = ind2 = ind3 = -1;
   if (nn == ~0ull) return;
@@ -444,13 +463,16 @@ LOAM_D void wave_assoc_surf(const float4* SL, const float4* ch, int fwd_end, uin
   if (!(D(d0) < 25)) return;
   const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u);
   ind1 = c;
+  const float b2 = sj2 >= 0 && window_member(sj2, sr2, c, scan, fwd_end, false, true) ? sd2 : 25.0f;
+  const float b3 = sj3 >= 0 && window_member(sj3, sr3, c, scan, fwd_end, false, false) ? sd3 : 25.0f;
+  const float bw = fmaxf(b2, b3);
   uint64_t best2 = ~0ull, best3 = ~0ull;
-  wave_window(SL, ch, c, fwd_end, +1, scan, sel, wpts, wbox, [&](int j, int r, float d) {
+  wave_window(SL, ch, c, fwd_end, +1, scan, sel, bw, wpts, wbox, [&](int j, int r, float d) {
     const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)(j - c - 1);
     if (r <= scan) best2 = key < best2 ? key : best2;
     else best3 = key < best3 ? key : best3;
   });
-  wave_window(SL, ch, c, fwd_end, -1, scan, sel, wpts, wbox, [&](int j, int r, float d) {
+  wave_window(SL, ch, c, fwd_end, -1, scan, sel, bw, wpts, wbox, [&](int j, int r, float d) {
     const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)((1u << 30) + (c - 1 - j));
     if (r >= scan) best2 = key < best2 ? key : best2;
     else best3 = key < best3 ? key : best3;
@@ -538,6 +560,7 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(SEL 
   const float4* SL = b.lastS + lp * b.capS;
   int* ind = b.ind + (size_t)p * 3 * b.cap_q;
   int wpts = 0, wbox = 0;  // wave-uniform work counters (loam_stats od_assoc_gathered / _boxes)
+  const bool seeded = ist[kIsIters] > 0;  // ind holds this frame's previous round
   for (int q = blk.x * kOdWaves + w; q < nq; q += gridDim.x * kOdWaves) {
     float4 s4;
     if constexpr (SEL) {
@@ -550,17 +573,33 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(SEL 
     } else {
       s4 = sel[q];
     }
+    // seeds: the previous round's choices (ind, rounds after the first), their rings and squared
+    // distances at this round's transform (lanes 0..2 load one each)
+    const bool corner = q < nc;
+    const float4* Lc = corner ? CL : SL;
+    int sj = -1;
+    float4 sp = make_float4(0, 0, 0, 0);
+    if (seeded && lane < 3) {
+      sj = ind[lane * b.cap_q + q];
+      if (sj >= 0) sp = Lc[sj];
+    }
+    const int j0 = __shfl(sj, 0, 64), j1 = __shfl(sj, 1, 64), j2 = __shfl(sj, 2, 64);
+    const float4 p0 = make_float4(__shfl(sp.x, 0, 64), __shfl(sp.y, 0, 64), __shfl(sp.z, 0, 64), __shfl(sp.w, 0, 64));
+    const float4 p1 = make_float4(__shfl(sp.x, 1, 64), __shfl(sp.y, 1, 64), __shfl(sp.z, 1, 64), __shfl(sp.w, 1, 64));
+    const float4 p2 = make_float4(__shfl(sp.x, 2, 64), __shfl(sp.y, 2, 64), __shfl(sp.z, 2, 64), __shfl(sp.w, 2, 64));
+    const float nnb = j0 >= 0 ? sqdist(p0.x, p0.y, p0.z, s4.x, s4.y, s4.z) : 3.4e38f;
+    const float d1 = sqdist(p1.x, p1.y, p1.z, s4.x, s4.y, s4.z), d2 = sqdist(p2.x, p2.y, p2.z, s4.x, s4.y, s4.z);
     int i1, i2, i3 = -1;
-    if (q < nc) {
+    if (corner) {
       const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
       const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC,
-                                       b.hC_T[last_buf * b.P + p], CL, ch, C, 1.0f, 1.0f, s4, cells[w], wpts, wbox);
-      wave_assoc_corner(CL, ch, min(nc, C), nn, s4, i1, i2, wpts, wbox);
+                                       b.hC_T[last_buf * b.P + p], CL, ch, C, 1.0f, 1.0f, s4, nnb, cells[w], wpts, wbox);
+      wave_assoc_corner(CL, ch, min(nc, C), nn, s4, j1, (int)p1.w, d1, i1, i2, wpts, wbox);
     } else {
       const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
       const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS,
-                                       b.hS_T[last_buf * b.P + p], SL, ch, S, 1.0f, 1.0f, s4, cells[w], wpts, wbox);
-      wave_assoc_surf(SL, ch, min(ns, S), nn, s4, i1, i2, i3, wpts, wbox);
+                                       b.hS_T[last_buf * b.P + p], SL, ch, S, 1.0f, 1.0f, s4, nnb, cells[w], wpts, wbox);
+      wave_assoc_surf(SL, ch, min(ns, S), nn, s4, j1, (int)p1.w, d1, j2, (int)p2.w, d2, i1, i2, i3, wpts, wbox);
     }
     if (lane == 0) {
       LOAM_CHECK(q < b.cap_q && p < b.P, q, p);
