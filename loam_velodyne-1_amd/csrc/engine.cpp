@@ -10,6 +10,7 @@
 
 #include <cstdio>
 #include <cstddef>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -309,10 +310,11 @@ int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_fe
   SrBuffers& b = x->sr1;
   const int n = (int)raw.count;
   x->pin.reset();
-  HIP_TRY(x->pin.reserve((size_t)n, x->st));
+  HIP_TRY(x->pin.reserve((size_t)2 * n, x->st));
   float4* praw = x->pin.buf;  // the sweep packed straight into pinned memory
+  float4* pfull = x->pin.buf + n;  // the early download of the full cloud (below)
   pack(raw, praw);
-  x->pin.off = (size_t)n;
+  x->pin.off = (size_t)2 * n;
   int* mi = (int*)x->meta;  // [0] n, [1..4] counts, [5] nfull, [6] err
   mi[0] = n;
   if (n) HIP_TRY(hipMemcpyAsync(b.raw, praw, (size_t)n * sizeof(float4), hipMemcpyHostToDevice, x->st));
@@ -326,15 +328,28 @@ int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_fe
     prm.time_scan = stamp;
   }
   HIP_TRY(hipEventRecord(x->ev[0], x->st));
-  sr_launch(b, prm, x->st);
+  // /velodyne_cloud_2 is final once the rings are sorted: its n (>= the kept points) points come
+  // down on the second stream, and reach the caller's buffer on the host, while the curvature /
+  // pick / VoxelGrid kernels run
+  const bool early = x->st2 != nullptr && n > 0;
+  sr_launch(b, prm, x->st, nullptr, early ? x->fork : nullptr);
   HIP_TRY(hipEventRecord(x->ev[1], x->st));
   HIP_TRY(hipGetLastError());
+  if (early) {
+    HIP_TRY(hipStreamWaitEvent(x->st2, x->fork, 0));
+    HIP_TRY(hipMemcpyAsync(pfull, b.full, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost, x->st2));
+    HIP_TRY(hipEventRecord(x->join, x->st2));
+  }
   if (q->last >= 0)
     HIP_TRY(hipMemcpyAsync((char*)q + tail, (const char*)x->sr_imu_dev + tail, sizeof(*q) - tail,
                            hipMemcpyDeviceToHost, x->st));
   HIP_TRY(hipMemcpyAsync(&mi[1], b.cnt, 4 * sizeof(int), hipMemcpyDeviceToHost, x->st));
   HIP_TRY(hipMemcpyAsync(&mi[5], b.n_full, sizeof(int), hipMemcpyDeviceToHost, x->st));
   HIP_TRY(hipMemcpyAsync(&mi[6], b.err, sizeof(int), hipMemcpyDeviceToHost, x->st));
+  if (early) {  // (points past the kept count land in the caller's spare capacity only)
+    HIP_TRY(hipEventSynchronize(x->join));
+    if (out->full.pts) std::memcpy(out->full.pts, pfull, (size_t)std::min<uint32_t>((uint32_t)n, out->full.capacity) * sizeof(float4));
+  }
   HIP_TRY(hipStreamSynchronize(x->st));
   int cnt[4] = {mi[1], mi[2], mi[3], mi[4]};
   const int nfull = mi[5];
@@ -342,7 +357,12 @@ int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_fe
   if (rc) return rc;
   int e = 0;
   x->pin.reset();
-  e |= copy_out(x->st, x->pin, b.full, nfull, &out->full);
+  if (early) {
+    out->full.count = (uint32_t)nfull;
+    if ((uint32_t)nfull > out->full.capacity) e |= fail(LOAM_E_CAPACITY, "output cloud capacity too small");
+  } else {
+    e |= copy_out(x->st, x->pin, b.full, nfull, &out->full);
+  }
   e |= copy_out(x->st, x->pin, b.sharp, cnt[0], &out->sharp);
   e |= copy_out(x->st, x->pin, b.lsharp, cnt[1], &out->less_sharp);
   e |= copy_out(x->st, x->pin, b.flat, cnt[2], &out->flat);
@@ -379,13 +399,20 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
   if (in->sharp.count > (uint32_t)(kSharpPerRing * R) || in->flat.count > (uint32_t)(kFlatPerRing * R) ||
       in->less_sharp.count > (uint32_t)(kLessSharpPerRing * R))
     return fail(LOAM_E_CAPACITY, "feature cloud larger than scan registration can produce");
+  if (in->full.count > (uint32_t)x->cap) return fail(LOAM_E_CAPACITY, "input feature cloud exceeds capacity");
+  if (in->full.count > 0 && in->full.pts == nullptr) return fail(LOAM_E_INVAL, "feature cloud pts is null");
   int rc = 0;
   x->pin.reset();
+  HIP_TRY(x->pin.reserve((size_t)in->sharp.count + in->less_sharp.count + in->flat.count + in->less_flat.count +
+                             in->full.count, x->st));
+  // only k_od_end reads the full cloud: after the first frame, with a second stream, it is staged
+  // while the L-M kernels run (late_full below)
+  const bool late = x->od_inited && x->st2 != nullptr && in->full.count > 0;
   if ((rc = upload_cloud(x->st, x->pin, in->sharp, fi.sharp, kSharpPerRing * R)) ||
       (rc = upload_cloud(x->st, x->pin, in->less_sharp, fi.lsharp, kLessSharpPerRing * R)) ||
       (rc = upload_cloud(x->st, x->pin, in->flat, fi.flat, kFlatPerRing * R)) ||
       (rc = upload_cloud(x->st, x->pin, in->less_flat, fi.lflat, x->cap)) ||
-      (rc = upload_cloud(x->st, x->pin, in->full, fi.full, x->cap)))
+      (!late && (rc = upload_cloud(x->st, x->pin, in->full, fi.full, x->cap))))
     return rc;
   int cnt[5] = {(int)in->sharp.count, (int)in->less_sharp.count, (int)in->flat.count,
                 (int)in->less_flat.count, (int)in->full.count};
@@ -424,6 +451,11 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
   // the pose accumulation (:830-856) runs on the host after the download: one scalar chain of
   // double trig, which a one-thread kernel took ~16 us for (the batch path keeps it on the device)
   od_solve(o, fv, cur, x->st, nullptr, /*device_fini=*/false);
+  if (late) {  // late_full: host copy + DMA on the second stream, overlapping the L-M above
+    HIP_TRY(x->pin.up(x->st2, fi.full, in->full.pts, (size_t)in->full.count));
+    HIP_TRY(hipEventRecord(x->join, x->st2));
+    HIP_TRY(hipStreamWaitEvent(x->st, x->join, 0));
+  }
   x->od_frame_count++;
   const bool pub = x->od_frame_count >= (int)x->cfg.skip_frame_num + 1;
   hipLaunchKernelGGL(k_od_end, dim3(64, 1), dim3(256), 0, x->st, o, fv, nxt, 2, pub ? 1 : 0);  // one sweep: a wider grid
@@ -500,7 +532,8 @@ int loam_mapping(loam_ctx* x, double stamp, const loam_pose6* odom_sum, const lo
   const bool have_imu = loamimu::mp_lookup(x->mp_imu, stamp, rp[0], rp[1], front);
   bool updated = false;
   const int rc = mp_stream_frame(x->mp1, x->st, *odom_sum, *corner_last, *surf_last, *full_end, aft, bef,
-                                 registered, &x->stats, g_err, x->pin, x->meta, have_imu ? rp : nullptr, &updated);
+                                 registered, &x->stats, g_err, x->pin, x->meta, have_imu ? rp : nullptr, &updated,
+                                 x->st2, x->join);
   if (have_imu && updated) x->mp_imu.front = front;  // the pointer walk happens inside transformUpdate
   x->surround_due = false;
   if (rc == LOAM_OK && ++x->map_frame_count >= 5) {  // :1038-1040

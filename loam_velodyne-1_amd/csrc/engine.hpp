@@ -171,7 +171,10 @@ void set_last_error(const std::string& msg);
 hipError_t sr_alloc(SrBuffers& b, int S, int cap, int R);  // on failure: freed, b empty
 void sr_free(SrBuffers& b);
 // runs the whole scan registration for sweeps [0, S) already in b.raw / b.raw_n
-void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof = nullptr);
+// sorted (optional): recorded once the ring sort has written the full cloud (the later kernels
+// only read it), so that its download can start while the feature kernels run
+void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof = nullptr,
+               hipEvent_t sorted = nullptr);
 
 }  // namespace loam
 

@@ -23,6 +23,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <functional>
 #include <cstring>
 #include <vector>
 
@@ -1630,7 +1631,8 @@ hipError_t mp_reset(MpBuffers& b, hipStream_t st) {
   return hipGetLastError();
 }
 
-void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool map_empty) {
+void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool map_empty,
+              const std::function<void()>& before_register) {
   const int P = b.P;
   auto mark = [&](const char* n) { if (prof) prof->mark(n); };
   hipLaunchKernelGGL(k_mp_prepare, dim3(P), dim3(kMpThreads), 0, st, b, in);
@@ -1700,6 +1702,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   hipLaunchKernelGGL(k_mp_compact_table, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);
   mark("k_mp_compact");
+  if (before_register) before_register();
   hipLaunchKernelGGL(k_mp_register, dim3(16, P), dim3(256), 0, st, b, in);
   mark("k_mp_register");
   b.pool_cur = 1 - b.pool_cur;
@@ -1708,7 +1711,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
                     const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
                     loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, void* meta,
-                    const float* imu_rp, bool* updated) {
+                    const float* imu_rp, bool* updated, hipStream_t st2, hipEvent_t ev2) {
   if (corner.count > (uint32_t)b.capC || surf.count > (uint32_t)b.capS || full.count > (uint32_t)b.capS) {
     err = "mapping input cloud exceeds capacity";
     return LOAM_E_CAPACITY;
@@ -1730,9 +1733,14 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   std::memcpy(mi + 10, rp, sizeof(rp));
   mi[12] = imu_rp ? 1 : 0;
   pin.reset();
-  hipError_t ue = pin.up(st, b.inC, corner.pts, (size_t)n[0]);
+  // room for all three clouds now: the full cloud is staged later, while the kernels run
+  hipError_t ue = pin.reserve((size_t)n[0] + n[1] + n[2], st);
+  if (ue == hipSuccess) ue = pin.up(st, b.inC, corner.pts, (size_t)n[0]);
   if (ue == hipSuccess) ue = pin.up(st, b.inS, surf.pts, (size_t)n[1]);
-  if (ue == hipSuccess) ue = pin.up(st, b.inF, full.pts, (size_t)n[2]);
+  // only k_mp_register reads the full cloud: with a second stream its staging copy and DMA
+  // overlap the frame's kernels (enqueued just before k_mp_register)
+  const bool late = st2 != nullptr && n[2] > 0;
+  if (ue == hipSuccess && !late) ue = pin.up(st, b.inF, full.pts, (size_t)n[2]);
   if (ue == hipSuccess) ue = hipMemcpyAsync(b.in_n, n, 3 * sizeof(int), hipMemcpyHostToDevice, st);
   if (ue == hipSuccess) ue = hipMemcpyAsync(b.in_pose, mi + 4, 6 * sizeof(float), hipMemcpyHostToDevice, st);
   if (ue == hipSuccess) ue = hipMemcpyAsync(b.state + kMpImuRP, mi + 10, 2 * sizeof(float), hipMemcpyHostToDevice, st);
@@ -1748,7 +1756,13 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   in.ncorner_stride = in.nsurf_stride = in.nfull_stride = 3;
   in.pose = b.in_pose; in.pose_stride = 6;
   (void)hipEventRecord(e0, st);
-  mp_frame(b, in, st);
+  hipError_t le = hipSuccess;
+  mp_frame(b, in, st, nullptr, false, [&]() {
+    if (!late) return;
+    le = pin.up(st2, b.inF, full.pts, (size_t)n[2]);
+    if (le == hipSuccess) le = hipEventRecord(ev2, st2);
+    if (le == hipSuccess) le = hipStreamWaitEvent(st, ev2, 0);
+  });
   (void)hipEventRecord(e1, st);
   float* sf = (float*)(mi + 16);                  // kMpStateFloats
   int* si = mi + 16 + kMpStateFloats;             // kMpStateInts
@@ -1763,6 +1777,7 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   if (he == hipSuccess) he = b.take_error();
+  if (he == hipSuccess) he = le;
   if (he != hipSuccess) {
     err = std::string("mapping: ") + hipGetErrorString(he);
     return LOAM_E_HIP;

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <string>
 
 #include "engine.hpp"
@@ -128,13 +129,17 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
 void mp_free(MpBuffers& b);
 hipError_t mp_reset(MpBuffers& b, hipStream_t st);
 // map_empty: the store was just reset (no L-M can run: its launches are skipped)
-void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof = nullptr, bool map_empty = false);
+// before_register: called once every kernel before k_mp_register is enqueued (the streaming path
+// stages the full cloud there)
+void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof = nullptr, bool map_empty = false,
+              const std::function<void()>& before_register = nullptr);
 // imu_rp: the IMU (roll, pitch) transformUpdate blends in (nullptr = no IMU); *updated = whether
 // transformUpdate ran (the caller then commits its IMU queue pointer)
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
                     const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
                     loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, void* meta,
-                    const float* imu_rp = nullptr, bool* updated = nullptr);
+                    const float* imu_rp = nullptr, bool* updated = nullptr, hipStream_t st2 = nullptr,
+                    hipEvent_t ev2 = nullptr);
 // /laser_cloud_surround of the last streaming frame (instance 0): its 5x5x5 cube neighbourhood
 // concatenated and VoxelGrid 0.2 (src/laserMapping.cpp:1038-1058)
 int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::string& err);

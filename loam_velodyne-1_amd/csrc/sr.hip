@@ -1412,7 +1412,7 @@ void sr_free(SrBuffers& b) {
   b = SrBuffers();
 }
 
-void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof) {
+void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof, hipEvent_t sorted) {
   auto mark = [&](const char* n) { if (prof) prof->mark(n); };
   HIPCHK(hipMemsetAsync(b.ring_se, 0, (size_t)b.S * 2 * b.R * sizeof(int), st));
   HIPCHK(hipMemsetAsync(b.err, 0, (size_t)b.S * sizeof(int), st));
@@ -1425,6 +1425,7 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
     hipLaunchKernelGGL(k_sr_ring_scatter, dim3(rtiles, b.S), dim3(kSrThreads), 0, st, b, p);
   }
   mark("k_sr_ring_sort");
+  if (sorted) HIPCHK(hipEventRecord(sorted, st));  // the ring-sorted full cloud is final here
   hipLaunchKernelGGL(k_sr_features, dim3((b.cap + kFeatSpan - 1) / kFeatSpan, b.S), dim3(kFeatTile), 0,
                      st, b, p);
   mark("k_sr_features");
