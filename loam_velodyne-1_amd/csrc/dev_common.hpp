@@ -732,6 +732,121 @@ LOAM_HD void jacobi(float* A, float* W, float* V, int* iws) {
   }
 }
 
+// jacobi<6> by one whole wave (all 64 lanes active), bit-identical: lane 6r + c (< 36) holds
+// A[r][c] and V[r][c] in registers, lanes 0..5 hold W and the tracked row / column maxima (indR,
+// indC).  A rotation's element pairs are disjoint, so every affected lane updates at once from its
+// partner's value (one cross-lane read each); the pivot scan, the rotation and the tracking scans
+// keep the sequential first-maximum order of the one-lane version on wave-uniform values.  The
+// one-lane version's chain of dependent LDS accesses per rotation was the iteration-0 cost
+// (73-84 us per call).  A (row-major, 36) is read from memory; W, V (rows) are written.
+LOAM_D float wl_read(float v, int lane) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane)); }
+LOAM_D int wl_readi(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+LOAM_D float wl_perm(float v, int src) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src << 2, __builtin_bit_cast(int, v)));
+}
+LOAM_D void jacobi6_wave(const float* Ain, float* Wout, float* Vout) {
+  constexpr int N = 6;
+  const float eps = 1.1920928955078125e-07f;
+  const int lane = __lane_id();
+  const int r = lane / N, c = lane % N;
+  float a = lane < N * N ? Ain[lane] : 0.0f;
+  float v = lane < N * N ? (r == c ? 1.0f : 0.0f) : 0.0f;
+  float w = wl_perm(a, lane < N ? lane * (N + 1) : 0);  // W[k] = A[k][k] on lane k
+  // the tracked maxima: row k over A[k][k+1..5] (indR), column k over A[0..k-1][k] (indC)
+  auto rowmax = [&](int k) {
+    int m = k + 1;
+    float mv = fabsf(wl_read(a, k * N + m));
+    for (int i = k + 2; i < N; ++i) {
+      const float val = fabsf(wl_read(a, k * N + i));
+      if (mv < val) { mv = val; m = i; }
+    }
+    return m;
+  };
+  auto colmax = [&](int k) {
+    int m = 0;
+    float mv = fabsf(wl_read(a, k));
+    for (int i = 1; i < k; ++i) {
+      const float val = fabsf(wl_read(a, i * N + k));
+      if (mv < val) { mv = val; m = i; }
+    }
+    return m;
+  };
+  int indR[N], indC[N];  // wave-uniform
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    indR[k] = k < N - 1 ? rowmax(k) : 0;
+    indC[k] = k > 0 ? colmax(k) : 0;
+  }
+  for (int iters = 0; iters < N * N * 30; ++iters) {
+    int k = 0;
+    float mv = fabsf(wl_read(a, indR[0]));
+    for (int i = 1; i < N - 1; ++i) {
+      const float val = fabsf(wl_read(a, i * N + indR[i]));
+      if (mv < val) { mv = val; k = i; }
+    }
+    int l = indR[k];
+    for (int i = 1; i < N; ++i) {
+      const float val = fabsf(wl_read(a, indC[i] * N + i));
+      if (mv < val) { mv = val; k = indC[i]; l = i; }
+    }
+    k = __builtin_amdgcn_readfirstlane(k);
+    l = __builtin_amdgcn_readfirstlane(l);
+    const float p = wl_read(a, k * N + l);
+    if (fabsf(p) <= eps) break;
+    const float Wk = wl_read(w, k), Wl = wl_read(w, l);
+    float y = (float)((Wl - Wk) * 0.5);
+    float t = fabsf(y) + hypot_cv(p, y);
+    float s = hypot_cv(p, t);
+    const float cc = t / s;
+    s = p / s;
+    t = (p / t) * p;
+    if (y < 0) { s = -s; t = -t; }
+    if (lane == k) w = Wk - t;
+    if (lane == l) w = Wl + t;
+    // A pairs (v0, v1): (A[i][k], A[i][l]) i < k; (A[k][i], A[i][l]) k < i < l; (A[k][i], A[l][i]) i > l
+    int partner = lane, role = 0;  // role 1: v0, 2: v1
+    if (c == k && r < k) { role = 1; partner = r * N + l; }
+    else if (c == l && r < k) { role = 2; partner = r * N + k; }
+    else if (r == k && c > k && c < l) { role = 1; partner = c * N + l; }
+    else if (c == l && r > k && r < l) { role = 2; partner = k * N + r; }
+    else if (r == k && c > l) { role = 1; partner = l * N + c; }
+    else if (r == l && c > l) { role = 2; partner = k * N + c; }
+    if (lane >= N * N) role = 0;
+    const float other = wl_perm(a, partner);
+    if (role == 1) a = a * cc - other * s;
+    else if (role == 2) a = other * s + a * cc;
+    if (lane == k * N + l) a = 0.0f;
+    // V rows k, l
+    const int vpart = r == k ? l * N + c : (r == l ? k * N + c : lane);
+    const float vo = wl_perm(v, lane < N * N ? vpart : lane);
+    if (lane < N * N) {
+      if (r == k) v = v * cc - vo * s;
+      else if (r == l) v = vo * s + v * cc;
+    }
+    if (k < N - 1) indR[k] = rowmax(k);
+    if (k > 0) indC[k] = colmax(k);
+    if (l < N - 1) indR[l] = rowmax(l);
+    if (l > 0) indC[l] = colmax(l);
+  }
+  if (lane < N) Wout[lane] = w;
+  if (lane < N * N) Vout[lane] = v;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {  // descending order (rows of V follow)
+    for (int k = 0; k < N - 1; ++k) {
+      int m = k;
+      for (int i = k + 1; i < N; ++i)
+        if (Wout[m] < Wout[i]) m = i;
+      if (k != m) {
+        float tq = Wout[m]; Wout[m] = Wout[k]; Wout[k] = tq;
+        for (int i = 0; i < N; ++i) { float q = Vout[m * N + i]; Vout[m * N + i] = Vout[k * N + i]; Vout[k * N + i] = q; }
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // 6 x 6 LU inverse with partial pivoting (A destroyed)
 LOAM_HD bool lu_inv6(float* A, float* Inv, float* b) {
   const int n = 6;
@@ -781,8 +896,10 @@ LOAM_HD void gemm_d(const float* A, const float* B, int m, int k, int n, float* 
 // AtA (6x6 float), AtB (6), iteration-0 degeneracy analysis.  One lane.
 // ws: >= kLmWs floats of scratch (LDS when called from a kernel lane), iws: >= 12 ints
 constexpr int kLmWs = 36 * 6 + 6 + 14 + 6;
+// pre_E / pre_V (optional): jacobi<6>(AtA) already computed (jacobi6_wave, by the caller's wave)
 LOAM_HD void lm_step(const float* AtA_in, const float* AtB_in, int iter, float eig_thresh,
-                     int* isDegenerate, float* matP, float* X, float* ws, int* iws) {
+                     int* isDegenerate, float* matP, float* X, float* ws, int* iws,
+                     const float* pre_E = nullptr, const float* pre_V = nullptr) {
   // the QR solve of every iteration works in registers (fully unrolled, constant indices); the
   // iteration-0 analysis (pivoted Jacobi / LU, data-dependent indices) in ws
   float A[36], b[6], qws[14];
@@ -796,8 +913,13 @@ LOAM_HD void lm_step(const float* AtA_in, const float* AtB_in, int iter, float e
   for (int i = 0; i < 6; ++i) b[i] = AtB_in[i];
   qr_solve(A, b, 6, 6, X, qws);
   if (iter == 0) {
-    for (int i = 0; i < 36; ++i) A2[i] = AtA_in[i];
-    jacobi<6>(A2, E, V, iws);
+    if (pre_E) {
+      for (int i = 0; i < 6; ++i) E[i] = pre_E[i];
+      for (int i = 0; i < 36; ++i) V[i] = pre_V[i];
+    } else {
+      for (int i = 0; i < 36; ++i) A2[i] = AtA_in[i];
+      jacobi<6>(A2, E, V, iws);
+    }
     for (int i = 0; i < 36; ++i) V2[i] = V[i];
     int degen = 0;
     for (int i = 5; i >= 0; --i) {

@@ -954,18 +954,19 @@ struct MpStepScratch {
   float lm_ws[loamla::kLmWs];
   int lm_iws[12];
   float AtA[36], AtB[6], X[6];
+  float jE[6], jV[36];  // iteration 0: jacobi6_wave's eigen decomposition of AtA
 };
 
-// one lane: iteration bookkeeping, the 6x6 step when there are >= 50 rows (:886-889), the
-// update (no NaN guard in mapping, :956-961) and the convergence test (:972)
+// the first wave of the workgroup (the iteration-0 eigen decomposition, jacobi6_wave), the rest on
+// lane 0: iteration bookkeeping, the 6x6 step when there are >= 50 rows (:886-889), the update (no
+// NaN guard in mapping, :956-961) and the convergence test (:972)
 LOAM_D void mp_step(const MpBuffers& b, int p, const double* tot, MpStepScratch& sh) {
+  const int lane = lane_id();
   int* ist = b.istate + (size_t)p * kMpStateInts;
   float* st = b.state + (size_t)p * kMpStateFloats;
   const int iter = ist[kMiIters];
   const int nrows = (int)tot[27];
-  ist[kMiIters] = iter + 1;
-  ist[kMiRows] += nrows;
-  if (nrows >= 50) {
+  if (nrows >= 50 && lane == 0) {
     int k = 0;
     for (int i = 0; i < 6; ++i)
       for (int jj = i; jj < 6; ++jj) {
@@ -974,8 +975,21 @@ LOAM_D void mp_step(const MpBuffers& b, int p, const double* tot, MpStepScratch&
         ++k;
       }
     for (int i = 0; i < 6; ++i) sh.AtB[i] = (float)tot[21 + i];
+  }
+  const bool eig = nrows >= 50 && iter == 0;
+  if (eig) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    loamla::jacobi6_wave(sh.AtA, sh.jE, sh.jV);
+  }
+  if (lane != 0) return;
+  ist[kMiIters] = iter + 1;
+  ist[kMiRows] += nrows;
+  if (nrows >= 50) {
     int degen = ist[kMiDegen];
-    loamla::lm_step(sh.AtA, sh.AtB, iter, 100.0f, &degen, st + kMpMatP, sh.X, sh.lm_ws, sh.lm_iws);
+    loamla::lm_step(sh.AtA, sh.AtB, iter, 100.0f, &degen, st + kMpMatP, sh.X, sh.lm_ws, sh.lm_iws,
+                    eig ? sh.jE : nullptr, eig ? sh.jV : nullptr);
     ist[kMiDegen] = degen;
     if (degen) ist[kMiDegSteps] += 1;
     for (int q = 0; q < 6; ++q) st[kMpTobe + q] += sh.X[q];
@@ -1056,10 +1070,9 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
 namespace {
 struct MpIterShared {
   double red[kMpWaves][28];
+  double tot[28];
   float trig[6];
-  float lm_ws[loamla::kLmWs];
-  int lm_iws[12];
-  float AtA[36], AtB[6], X[6];
+  MpStepScratch step;
 };
 }  // namespace
 
@@ -1128,37 +1141,13 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
   wave_reduce_scatter_28(acc);  // lanes 2v, 2v+1: the wave sum of value v
   if ((lane & 1) == 0 && (lane >> 1) < 28) sh.red[w][lane >> 1] = acc[0];
   __syncthreads();
-  if (tid == 0) {
-    double tot[28];
-    for (int k = 0; k < 28; ++k) {
-      double v = sh.red[0][k];
-      for (int ww = 1; ww < kMpWaves; ++ww) v += sh.red[ww][k];
-      tot[k] = v;
-    }
-    const int iter = ist[kMiIters];
-    const int nrows = (int)tot[27];
-    ist[kMiIters] = iter + 1;
-    ist[kMiRows] += nrows;
-    if (nrows >= 50) {  // :886-889
-      int k = 0;
-      for (int i = 0; i < 6; ++i)
-        for (int jj = i; jj < 6; ++jj) {
-          sh.AtA[i * 6 + jj] = (float)tot[k];
-          sh.AtA[jj * 6 + i] = (float)tot[k];
-          ++k;
-        }
-      for (int i = 0; i < 6; ++i) sh.AtB[i] = (float)tot[21 + i];
-      int degen = ist[kMiDegen];
-      loamla::lm_step(sh.AtA, sh.AtB, iter, 100.0f, &degen, st + kMpMatP, sh.X, sh.lm_ws, sh.lm_iws);
-      ist[kMiDegen] = degen;
-      if (degen) ist[kMiDegSteps] += 1;
-      for (int q = 0; q < 6; ++q) st[kMpTobe + q] += sh.X[q];  // no NaN guard in mapping (:956-961)
-      rot_store(b, p, st + kMpTobe);
-      const float dR = loamla::delta_r(sh.X), dT = loamla::delta_t(sh.X);
-      if (D(dR) < 0.05 && D(dT) < 0.05) ist[kMiStop] = 1;
-    }
-    if (ist[kMiIters] >= b.max_iter) ist[kMiStop] = 1;
+  if (tid < 28) {
+    double v = sh.red[0][tid];
+    for (int ww = 1; ww < kMpWaves; ++ww) v += sh.red[ww][tid];
+    sh.tot[tid] = v;
   }
+  __syncthreads();
+  if (tid < 64) mp_step(b, p, sh.tot, sh.step);  // the first wave
 }
 
 
@@ -1246,8 +1235,8 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
     tot[tid] = v;
   }
   __syncthreads();
-  if (tid == 0) {
-    b.done[p] = 0;
+  if (tid < 64) {  // the first wave
+    if (tid == 0) b.done[p] = 0;
     mp_step(b, p, tot, sh);
   }
 }

@@ -617,35 +617,49 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(SEL 
 
 // the 6x6 step of one iteration (:697-828) of problem p on one lane, from the fixed-order sum of
 // the workgroup partials: QR solve / iteration-0 degeneracy analysis, NaN guard, convergence test
+// by the whole first wave of the workgroup (jacobi6_wave), the rest on lane 0.  jE / jV: LDS
+// for the iteration-0 eigen decomposition
 LOAM_D void od_step(const OdBuffers& b, int p, int iter, const double* tot, float* AtA, float* AtB, float* X,
-                    float* lm_ws, int* lm_iws) {
+                    float* lm_ws, int* lm_iws, float* jE, float* jV) {
+  const int lane = lane_id();
   int* ist = b.istate + (size_t)p * kOdStateInts;
   float* st = b.state + (size_t)p * kOdStateFloats;
   const int nrows = (int)tot[27];
-  ist[kIsIters] = iter + 1;
-  if (iter % 5 == 0) ist[kIsAssoc] += 1;
-  ist[kIsRows] += nrows;
-  if (nrows >= 10) {  // :697-700
-    int k = 0;
-    for (int i = 0; i < 6; ++i)
-      for (int jj = i; jj < 6; ++jj) {
-        AtA[i * 6 + jj] = (float)tot[k];
-        AtA[jj * 6 + i] = (float)tot[k];
-        ++k;
-      }
-    for (int i = 0; i < 6; ++i) AtB[i] = (float)tot[21 + i];
-    int degen = ist[kIsDegenerate];
-    loamla::lm_step(AtA, AtB, iter, 10.0f, &degen, st + kOdMatP, X, lm_ws, lm_iws);
-    ist[kIsDegenerate] = degen;
-    if (degen) ist[kIsDegSteps] += 1;
-    const bool nan = isnan(X[0]) || isnan(X[1]) || isnan(X[2]) || isnan(X[3]) || isnan(X[4]) || isnan(X[5]);
-    if (!nan)  // Q16
-      for (int q = 0; q < 6; ++q) st[q] += X[q];
-    else
-      ist[kIsNanSkips] += 1;
-    const float dR = loamla::delta_r(X), dT = loamla::delta_t(X);
-    if (D(dR) < 0.1 && D(dT) < 0.1) ist[kIsStop] = 1;
+  if (lane == 0) {
+    ist[kIsIters] = iter + 1;
+    if (iter % 5 == 0) ist[kIsAssoc] += 1;
+    ist[kIsRows] += nrows;
+    if (nrows >= 10) {  // :697-700
+      int k = 0;
+      for (int i = 0; i < 6; ++i)
+        for (int jj = i; jj < 6; ++jj) {
+          AtA[i * 6 + jj] = (float)tot[k];
+          AtA[jj * 6 + i] = (float)tot[k];
+          ++k;
+        }
+      for (int i = 0; i < 6; ++i) AtB[i] = (float)tot[21 + i];
+    }
   }
+  if (nrows < 10) return;
+  const bool eig = iter == 0;
+  if (eig) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    loamla::jacobi6_wave(AtA, jE, jV);
+  }
+  if (lane != 0) return;
+  int degen = ist[kIsDegenerate];
+  loamla::lm_step(AtA, AtB, iter, 10.0f, &degen, st + kOdMatP, X, lm_ws, lm_iws, eig ? jE : nullptr, eig ? jV : nullptr);
+  ist[kIsDegenerate] = degen;
+  if (degen) ist[kIsDegSteps] += 1;
+  const bool nan = isnan(X[0]) || isnan(X[1]) || isnan(X[2]) || isnan(X[3]) || isnan(X[4]) || isnan(X[5]);
+  if (!nan)  // Q16
+    for (int q = 0; q < 6; ++q) st[q] += X[q];
+  else
+    ist[kIsNanSkips] += 1;
+  const float dR = loamla::delta_r(X), dT = loamla::delta_t(X);
+  if (D(dR) < 0.1 && D(dT) < 0.1) ist[kIsStop] = 1;
 }
 
 // The residual + weight of query q at this iteration (:530-583 corner, :653-694 surf) against its
@@ -876,7 +890,7 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows_small(OdBuffers b, FeatV
   }
   __shared__ int sh_last;
   __shared__ double tot[28];
-  __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs];
+  __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs], jE[6], jV[36];
   __shared__ int lm_iws[12];
   __syncthreads();
   if (tid == 0) sh_last = atomicAdd(&b.done[p], 1) == G - 1;
@@ -910,9 +924,9 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows_small(OdBuffers b, FeatV
     tot[tid] = v;
   }
   __syncthreads();
-  if (tid == 0) {
-    b.done[p] = 0;
-    od_step(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws);
+  if (tid < 64) {  // the first wave
+    if (tid == 0) b.done[p] = 0;
+    od_step(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
   }
 }
 
@@ -922,7 +936,7 @@ __global__ __launch_bounds__(64) void k_od_step(OdBuffers b, int iter, int gq) {
   const int* ist = b.istate + (size_t)p * kOdStateInts;
   if (!ist[kIsActive] || ist[kIsStop]) return;
   __shared__ double tot[28];
-  __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs];
+  __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs], jE[6], jV[36];
   __shared__ int lm_iws[12];
   if (lane < 28) {  // fixed order over the workgroups; eight partials in flight per step
     double v = 0.0;
@@ -938,7 +952,7 @@ __global__ __launch_bounds__(64) void k_od_step(OdBuffers b, int iter, int gq) {
     tot[lane] = v;
   }
   __syncthreads();
-  if (lane == 0) od_step(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws);
+  od_step(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
 }
 
 // pose accumulation (:830-856) for every problem
