@@ -82,6 +82,21 @@ def kernel_bytes(st):
     }
 
 
+SEARCH_KERNELS = ("k_mp_nn", "k_od_assoc")
+
+
+def algorithmic_bytes(st):
+    """SURVEY.md §8(d)'s algorithmic bytes per kernel and step: what the kernel must read and write
+    at minimum.  Equal to kernel_bytes except for the two search kernels, whose algorithmic cost is
+    the query and its answer, not the candidates the search visits: k_mp_nn = per query-iteration
+    the stack point and its 5 neighbours (16 + 80 B, B_MP); k_od_assoc = per association round every
+    Last point once (16 B (C + S), B_OD)."""
+    alg = dict(kernel_bytes(st))
+    alg["k_mp_nn"] = 96 * st["mp_stack_iters"]
+    alg["k_od_assoc"] = 16 * st["od_assoc_points"]
+    return alg
+
+
 # what bounds each kernel in practice (DESIGN.md §4): the roofline is priced against HBM, but the
 # search kernels are limited by dependent gathers, not bandwidth
 LIMITED_BY = {"k_mp_nn": "latency (dependent gathers)", "k_od_assoc": "latency (dependent gathers)",
@@ -110,7 +125,25 @@ def stream_leg(loam, sg, n_sweeps, n_cpu):
     run(warm, sweeps[:6])
     pg, ng, tg = run(loam.Engine(loam.default_config()), sweeps)
     out = {"config": f"config3: VLP-16 stream (seed 1), {n_sweeps} sweeps, systemDelay 20, mapping every 2nd frame",
-           "sweeps_processed": ng, "scans_per_s": ng / tg, "ms_per_sweep": 1e3 * tg / max(ng, 1)}
+           "sweeps_processed": ng, "scans_per_s": ng / tg, "ms_per_sweep": 1e3 * tg / max(ng, 1),
+           "mode": "sequential: one thread calls the three node bodies in turn on one context (per-sweep latency)"}
+
+    # the same sweeps through the node pipeline (loam_velodyne-1_amd/pipeline.py): one context and
+    # one thread per node, as the reference's node processes run; outputs must equal the sequential run
+    pl_mod = importlib.import_module("loam_velodyne-1_amd.pipeline")
+    warm_pl = pl_mod.NodePipeline(loam.Engine, loam.default_config(system_delay=1))
+    warm_pl.run(sweeps[:6])
+    warm_pl.close()
+    pl = pl_mod.NodePipeline(loam.Engine, loam.default_config())
+    a = time.perf_counter()
+    res, n_pl = pl.run(sweeps)
+    t_pl = time.perf_counter() - a
+    pl.close()
+    pp = np.array([r[0] for r in res])
+    out["pipelined"] = {"mode": "node pipeline: scanRegistration / laserOdometry / laserMapping on three "
+                                "contexts and three threads (reference: separate node processes)",
+                        "sweeps_processed": n_pl, "scans_per_s": n_pl / t_pl, "ms_per_sweep": 1e3 * t_pl / max(n_pl, 1),
+                        "max_abs_err_vs_sequential": float(np.abs(pp - pg).max()) if pp.shape == pg.shape else None}
     if n_cpu > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_ctypes as oc
@@ -120,6 +153,7 @@ def stream_leg(loam, sg, n_sweeps, n_cpu):
         out["cpu_oracle"] = {"sweeps_processed": no, "scans_per_s": no / tc, "cores": 1, "kind": "port",
                              "pinned_cpu": core}
         out["speedup_vs_cpu"] = out["scans_per_s"] / out["cpu_oracle"]["scans_per_s"]
+        out["pipelined"]["speedup_vs_cpu"] = out["pipelined"]["scans_per_s"] / out["cpu_oracle"]["scans_per_s"]
         out["max_abs_err_mapping"] = float(np.abs(pg[:k] - po[:k]).max()) if k else None
     return out
 
@@ -362,15 +396,14 @@ def main(argv=None):
 
     # roofline of the dominant kernel: bytes per launch / average launch duration
     kb = kernel_bytes(st_prof)
-    dom = max(ktimes.items(), key=lambda kv: kv[1][0])[0] if ktimes else None
+    alg_kb = algorithmic_bytes(st_prof)
+    priced = {k: v for k, v in ktimes.items() if k in alg_kb}
+    dom = max(priced.items(), key=lambda kv: kv[1][0])[0] if priced else None
     roof = None
     if dom:
         tot_ms, launches = ktimes[dom]
         avg_ms = tot_ms / max(launches, 1)
-        nbytes = kb.get(dom)
         launches_per_step = launches / psteps
-        per_launch = nbytes / launches_per_step if nbytes is not None else None
-        achieved = per_launch / (avg_ms * 1e-3) / 1e9 if per_launch is not None else None
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tpath):
@@ -378,26 +411,22 @@ def main(argv=None):
                 traffic = json.load(open(tpath)).get(dom)
             except Exception:
                 traffic = None
+        alg_launch = alg_kb[dom] / launches_per_step
+        achieved = alg_launch / (avg_ms * 1e-3) / 1e9
         roof = {"kernel": dom, "bound": "hbm", "limited_by": LIMITED_BY.get(dom, "hbm"),
-                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved is not None else None,
-                "traffic": traffic, "avg_launch_ms": avg_ms, "bytes_per_launch": per_launch,
-                "bytes_model": "gathered bytes from the engine's work counters (bench.kernel_bytes)"
-                if dom in ("k_mp_nn", "k_od_assoc") else "algorithmic bytes (SURVEY.md §8(d))"}
-        if dom in ("k_mp_nn", "k_od_assoc") and achieved is not None:
-            roof["l2_gather_peak"] = L2_GATHER_PEAK_GBS
-            roof["l2_frac"] = achieved / L2_GATHER_PEAK_GBS
-            # SURVEY.md §8(d)'s algorithmic bytes of the same launches: per query-iteration the stack
-            # point and its 5 neighbours (16 + 80 B, B_MP), per association round every Last point
-            # once (16 B (C + S), B_OD)
-            alg = 96 * st_prof["mp_stack_iters"] if dom == "k_mp_nn" else 16 * st_prof["od_assoc_points"]
-            alg_launch = alg / launches_per_step
-            roof["survey_algorithmic"] = {"bytes_per_launch": alg_launch,
-                                          "achieved": alg_launch / (avg_ms * 1e-3) / 1e9,
-                                          "frac": alg_launch / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
-            if traffic:
-                roof["traffic_gbs"] = traffic / (avg_ms * 1e-3) / 1e9
-                roof["traffic_frac"] = roof["traffic_gbs"] / HBM_PEAK_GBS
+                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic, "avg_launch_ms": avg_ms, "bytes_per_launch": alg_launch,
+                "bytes_model": "algorithmic bytes, SURVEY.md §8(d) per-unit figure x units (bench.algorithmic_bytes)"}
+        if traffic:
+            roof["traffic_gbs"] = traffic / (avg_ms * 1e-3) / 1e9
+            roof["traffic_frac"] = roof["traffic_gbs"] / HBM_PEAK_GBS
+        if dom in SEARCH_KERNELS:
+            # what the search actually reads (candidate cells, window points, chunk boxes), from the
+            # work counters: L2-resident gathers, priced against the chip's L2 gather rate
+            g_launch = kb[dom] / launches_per_step
+            g = g_launch / (avg_ms * 1e-3) / 1e9
+            roof["gathered"] = {"bytes_per_launch": g_launch, "achieved_gbs": g,
+                                "l2_gather_peak": L2_GATHER_PEAK_GBS, "l2_frac": g / L2_GATHER_PEAK_GBS}
 
     # CPU baseline: the oracle on a bounded sample, N=1 only
     cpu = parity = None
@@ -408,12 +437,17 @@ def main(argv=None):
 
     stage_ms = {k: round(v[0] / psteps, 4) for k, v in sorted(ktimes.items())}
     roof_all = {}
-    for k, nbytes in kb.items():
+    for k, nbytes in alg_kb.items():
         if k in ktimes and ktimes[k][0] > 0:
-            gbs = nbytes / (ktimes[k][0] / psteps * 1e-3) / 1e9  # bytes per step / s per step
+            sec = ktimes[k][0] / psteps * 1e-3
+            gbs = nbytes / sec / 1e9  # algorithmic bytes per step / s per step
             roof_all[k] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                            "ms_per_step": round(ktimes[k][0] / psteps, 4),
                            "bytes_per_step": int(nbytes), "limited_by": LIMITED_BY.get(k, "hbm")}
+            if k in SEARCH_KERNELS:
+                ggbs = kb[k] / sec / 1e9
+                roof_all[k]["gathered"] = {"bytes_per_step": int(kb[k]), "achieved_gbs": round(ggbs, 1),
+                                           "l2_frac": round(ggbs / L2_GATHER_PEAK_GBS, 4)}
     # the whole pipeline against HBM: SURVEY.md §8(d)'s algorithmic bytes per step / step time
     alg = int(st["bytes_sr"] + st["bytes_od"] + st["bytes_mp"])
     pipeline = {"algorithmic_bytes_per_step": alg, "achieved_gbs": alg / (ms_per_step * 1e-3) / 1e9,

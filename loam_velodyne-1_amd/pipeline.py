@@ -1,0 +1,109 @@
+"""The reference's node graph as a host-side pipeline: scanRegistration -> laserOdometry ->
+laserMapping, each node on its own engine context (own HIP stream, own device state) and its own
+thread, connected by FIFO queues that play the ROS topics.
+
+The reference runs the four nodes as separate processes ("odometry and mapping
+running in parallel", reference README.md:42): while laserMapping solves frame k, laserOdometry is
+already on frame k+1 and scanRegistration on frame k+2.  Each node consumes its own topic in order,
+so every node sees exactly the inputs it sees in a sequential run and the outputs are identical;
+only the overlap changes.  The engine calls release the GIL (ctypes), so the three threads' host
+copies and the three contexts' kernels overlap on the device.
+
+Topics (reference file:line of the publish / subscribe pair):
+  features   /laser_cloud_sharp .. /velodyne_cloud_2   scanRegistration.cpp:593-635 -> laserOdometry.cpp:365-379
+  odometry   /laser_cloud_corner_last, _surf_last, /velodyne_cloud_3, /laser_odom_to_init
+             laserOdometry.cpp:858-930 -> laserMapping.cpp:353-366
+Mapping consumes a frame only when odometry published it (every skipFrameNum-th frame, `pub == 7`).
+"""
+import queue
+import threading
+
+_END = object()
+
+
+class NodePipeline:
+    """Three node contexts on three threads.  `engine_cls(cfg)` makes one context; `imu` entries are
+    not routed here (configs 3/4 carry none; the IMU path is the single-context `Engine.imu`)."""
+
+    def __init__(self, engine_cls, cfg=None, depth=4):
+        self.sr = engine_cls(cfg)
+        self.od = engine_cls(cfg)
+        self.mp = engine_cls(cfg)
+        self.depth = depth
+
+    def close(self):
+        for e in (self.sr, self.od, self.mp):
+            e.close()
+
+    def run(self, sweeps, stamps=None, on_mapping=None):
+        """feed `sweeps` (raw (n, >=3) float32 clouds) in order; returns (mapping results in frame
+        order as (aft, bef, registered) tuples, number of sweeps odometry processed).  Raises the
+        first node error after all threads have stopped."""
+        q_feat = queue.Queue(self.depth)
+        q_odom = queue.Queue(self.depth)
+        results, err = [], []
+        n_od = [0]
+
+        def guard(fn, out_q):
+            def body():
+                try:
+                    fn()
+                except BaseException as e:  # noqa: BLE001 - re-raised in the caller
+                    err.append(e)
+                finally:
+                    if out_q is not None:
+                        out_q.put(_END)
+            return body
+
+        def node_sr():
+            for k, s in enumerate(sweeps):
+                if err:
+                    return
+                t = stamps[k] if stamps is not None else 0.1 * k
+                rc, f = self.sr.scan_registration(s, stamp=t)
+                if rc == 0:
+                    q_feat.put((t, f))
+
+        def node_od():
+            while True:
+                it = q_feat.get()
+                if it is _END:
+                    return
+                if err:
+                    continue  # drain so the producer never blocks
+                t, f = it
+                n_od[0] += 1
+                try:
+                    pub, pose, cl, sl, full = self.od.odometry(f, stamp=t)
+                except BaseException as e:  # noqa: BLE001 - keep draining, re-raised in the caller
+                    err.append(e)
+                    continue
+                if pub == 7:
+                    q_odom.put((t, pose, cl, sl, full))
+
+        def node_mp():
+            while True:
+                it = q_odom.get()
+                if it is _END:
+                    return
+                if err:
+                    continue
+                t, pose, cl, sl, full = it
+                try:
+                    r = self.mp.mapping(pose, cl, sl, full, stamp=t)
+                    results.append(r)
+                    if on_mapping is not None:
+                        on_mapping(self.mp, r)
+                except BaseException as e:  # noqa: BLE001 - keep draining, re-raised in the caller
+                    err.append(e)
+
+        threads = [threading.Thread(target=guard(node_sr, q_feat), name="scanRegistration"),
+                   threading.Thread(target=guard(node_od, q_odom), name="laserOdometry"),
+                   threading.Thread(target=guard(node_mp, None), name="laserMapping")]
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join()
+        if err:
+            raise err[0]
+        return results, n_od[0]

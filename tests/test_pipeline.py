@@ -1,0 +1,102 @@
+"""Host logic of the node pipeline (loam_velodyne-1_amd/pipeline.py) with a stand-in engine: every
+node sees its topic in order, mapping gets exactly the frames odometry published, the results equal
+the sequential composition, and a node error is raised without leaving a thread blocked.  The GPU
+parity of the pipeline (three real contexts) is tests/test_gpu_branches.py::test_pipeline_matches_sequential."""
+import importlib
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+pipeline = importlib.import_module("loam_velodyne-1_amd.pipeline")
+
+
+class FakeNode:
+    """scan_registration drops the first `delay` sweeps; odometry publishes every 2nd frame and
+    carries a running state; mapping carries its own running state.  Random sleeps shuffle the
+    threads' interleaving."""
+
+    def __init__(self, cfg=None):
+        self.cfg = cfg or {}
+        self.n_sr = 0
+        self.od_sum = 0.0
+        self.od_frames = 0
+        self.mp_sum = 0.0
+        self.rng = np.random.default_rng(len(threading.enumerate()))
+        self.closed = False
+
+    def _nap(self):
+        time.sleep(float(self.rng.uniform(0, 2e-4)))
+
+    def scan_registration(self, s, stamp=0.0):
+        self._nap()
+        self.n_sr += 1
+        if self.n_sr <= self.cfg.get("delay", 2):
+            return -5, None
+        return 0, {"v": float(s[0, 0]), "stamp": stamp}
+
+    def odometry(self, f, stamp=0.0):
+        self._nap()
+        if self.cfg.get("fail_at") is not None and self.od_frames == self.cfg["fail_at"]:
+            raise RuntimeError("odometry failed")
+        self.od_frames += 1
+        self.od_sum = self.od_sum * 0.5 + f["v"]
+        pub = 7 if self.od_frames % 2 == 1 else 0
+        pose = np.array([self.od_sum, stamp, 0, 0, 0, 0], np.float32)
+        return pub, pose, np.zeros((1, 4)), np.zeros((2, 4)), np.zeros((3, 4))
+
+    def mapping(self, pose, cl, sl, full, stamp=0.0):
+        self._nap()
+        self.mp_sum = self.mp_sum * 0.25 + float(pose[0])
+        return np.array([self.mp_sum, stamp], np.float32), None, full
+
+    def close(self):
+        self.closed = True
+
+
+def sequential(sweeps, cfg):
+    e = FakeNode(cfg)
+    out, n = [], 0
+    for k, s in enumerate(sweeps):
+        rc, f = e.scan_registration(s, stamp=0.1 * k)
+        if rc:
+            continue
+        n += 1
+        pub, pose, cl, sl, full = e.odometry(f, stamp=0.1 * k)
+        if pub == 7:
+            out.append(e.mapping(pose, cl, sl, full, stamp=0.1 * k)[0])
+    return np.array(out), n
+
+
+@pytest.mark.parametrize("depth", [1, 4])
+def test_pipeline_equals_sequential(depth):
+    sweeps = [np.full((3, 4), float(k), np.float32) for k in range(40)]
+    cfg = {"delay": 3}
+    ref, n_ref = sequential(sweeps, cfg)
+    pl = pipeline.NodePipeline(FakeNode, cfg, depth=depth)
+    res, n = pl.run(sweeps)
+    pl.close()
+    assert n == n_ref == 37
+    got = np.array([r[0] for r in res])
+    assert got.shape == ref.shape and np.array_equal(got, ref)
+    assert all(e.closed for e in (pl.sr, pl.od, pl.mp))
+
+
+def test_pipeline_error_propagates_without_hang():
+    sweeps = [np.full((3, 4), float(k), np.float32) for k in range(50)]
+    pl = pipeline.NodePipeline(FakeNode, {"delay": 0, "fail_at": 5}, depth=1)
+    done = []
+
+    def go():
+        with pytest.raises(RuntimeError, match="odometry failed"):
+            pl.run(sweeps)
+        done.append(True)
+
+    th = threading.Thread(target=go)
+    th.start()
+    th.join(timeout=30)
+    assert done, "pipeline did not stop after a node error"
