@@ -32,6 +32,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# hardware queues per process (HIP's default is 4): the config-3 node pipeline runs three contexts
+# with two streams each; with 4 queues streams of different nodes share a queue and serialise
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 METRIC = "scans/sec (odometry+mapping L-M solve) VLP-16 sweep, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -103,7 +106,7 @@ LIMITED_BY = {"k_mp_nn": "latency (dependent gathers)", "k_od_assoc": "latency (
               "k_sr_select": "latency (serial greedy picks)", "k_mp_fit": "latency (gathers + VALU)"}
 
 
-def stream_leg(loam, sg, n_sweeps, n_cpu):
+def stream_leg(loam, sg, n_sweeps, n_cpu, stages=3, priority="default"):
     """Config 3 (streaming, seed 1): scan registration -> odometry -> mapping on every published
     frame, one sweep at a time on one GPU context, next to the CPU oracle on the first sweeps."""
     sweeps = sg.stream_sweeps(n_sweeps, 1)
@@ -131,10 +134,12 @@ def stream_leg(loam, sg, n_sweeps, n_cpu):
     # the same sweeps through the node pipeline (loam_velodyne-1_amd/pipeline.py): one context and
     # one thread per node, as the reference's node processes run; outputs must equal the sequential run
     pl_mod = importlib.import_module("loam_velodyne-1_amd.pipeline")
-    warm_pl = pl_mod.NodePipeline(loam.Engine, loam.default_config(system_delay=1))
+    warm_pl = pl_mod.NodePipeline(loam.Engine, loam.default_config(system_delay=1), stages=stages)
     warm_pl.run(sweeps[:6])
     warm_pl.close()
-    pl = pl_mod.NodePipeline(loam.Engine, loam.default_config())
+    if priority == "default":
+        priority = pl_mod.NodePipeline.DEFAULT_PRIORITY
+    pl = pl_mod.NodePipeline(loam.Engine, loam.default_config(), stages=stages, priority=priority)
     a = time.perf_counter()
     res, n_pl = pl.run(sweeps)
     t_pl = time.perf_counter() - a
@@ -143,6 +148,7 @@ def stream_leg(loam, sg, n_sweeps, n_cpu):
     out["pipelined"] = {"mode": "node pipeline: scanRegistration / laserOdometry / laserMapping on three "
                                 "contexts and three threads (reference: separate node processes)",
                         "sweeps_processed": n_pl, "scans_per_s": n_pl / t_pl, "ms_per_sweep": 1e3 * t_pl / max(n_pl, 1),
+                        "node_busy_ms_per_sweep": {k: round(1e3 * v / max(n_pl, 1), 4) for k, v in pl.busy_s.items()},
                         "max_abs_err_vs_sequential": float(np.abs(pp - pg).max()) if pp.shape == pg.shape else None}
     if n_cpu > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

@@ -170,6 +170,12 @@ int loam_batch_run(loam_ctx *ctx);
 int loam_batch_sync(loam_ctx *ctx);   /* waits for the work enqueued by loam_batch_run */
 int loam_batch_download(loam_ctx *ctx, loam_pose6 *od_sum, loam_pose6 *aft, loam_stats *stats);
 
+/* scheduling (no reference equivalent; the reference's nodes are OS processes): priority of the
+ * context's HIP streams.  priority > 0 = the device's highest stream priority, 0 = normal,
+ * < 0 = lowest.  Used by a node pipeline to favour its critical node (laserMapping) when several
+ * contexts share one GPU.  Waits for the context's queued work, then replaces its streams. */
+int loam_set_stream_priority(loam_ctx *ctx, int priority);
+
 /* last-call statistics of a context (stage device times, counts, algorithmic bytes) */
 int loam_get_stats(loam_ctx *ctx, loam_stats *stats);
 

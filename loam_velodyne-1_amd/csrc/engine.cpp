@@ -270,6 +270,29 @@ void loam_destroy(loam_ctx* x) {
   delete x;
 }
 
+int loam_set_stream_priority(loam_ctx* x, int priority) {
+  if (!x) return fail(LOAM_E_INVAL, "null argument");
+  HIP_TRY(hipSetDevice(x->device));
+  int least = 0, greatest = 0;  // HIP: a numerically lower value is a higher priority
+  HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  const int prio = priority > 0 ? greatest : priority < 0 ? least : 0;
+  hipStream_t st = nullptr, st2 = nullptr;
+  HIP_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio));
+  if (hipStreamCreateWithPriority(&st2, hipStreamNonBlocking, prio) != hipSuccess) {
+    (void)hipStreamDestroy(st);
+    return fail(LOAM_E_HIP, "hipStreamCreateWithPriority failed");
+  }
+  HIP_TRY(hipStreamSynchronize(x->st));
+  if (x->st2) {
+    HIP_TRY(hipStreamSynchronize(x->st2));
+    (void)hipStreamDestroy(x->st2);
+  }
+  (void)hipStreamDestroy(x->st);
+  x->st = st;
+  x->st2 = st2;
+  return LOAM_OK;
+}
+
 int loam_set_profiling(loam_ctx* x, int on) {
   if (!x) return fail(LOAM_E_INVAL, "null argument");
   x->prof.on = on != 0;

@@ -1278,16 +1278,102 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
   int* ro = rank_of + (size_t)p * b.cap_stack;
   __shared__ int cnt[2][kCubeNum];
   __shared__ int scratch[16];
+  // the (slot, kind) keys the stack uses, as a bitmap; their dense numbering (prefix popcounts)
+  // lets every wave keep its own counts when few keys occur (the usual case: a sweep touches a
+  // few dozen cubes)
+  constexpr int kKeyWords = (2 * kCubeNum + 31) / 32, kDense = 512, kWaves = kMpThreads / 64;
+  __shared__ unsigned keybits[kKeyWords];
+  __shared__ int keypre[kKeyWords + 1];
+  __shared__ int wcnt[kWaves][kDense];
   for (int i = tid; i < 2 * kCubeNum; i += kMpThreads) cnt[i / kCubeNum][i % kCubeNum] = 0;
-  for (int q = tid; q < nsc + nss; q += kMpThreads) {
+  for (int i = tid; i < kKeyWords; i += kMpThreads) keybits[i] = 0u;
+  for (int i = tid; i < kWaves * kDense; i += kMpThreads) wcnt[i / kDense][i % kDense] = 0;
+  __syncthreads();
+  const int nst = nsc + nss;
+  for (int q = tid; q < nst; q += kMpThreads) {
     const float4 a = loampose::point_to_map(r, stack[q < nsc ? q : b.capC + (q - nsc)]);
     const int ci = cube_of(a.x, cW), cj = cube_of(a.y, cH), ck = cube_of(a.z, cD);
     const bool in = ci >= 0 && ci < kCubeW && cj >= 0 && cj < kCubeH && ck >= 0 && ck < kCubeD;
-    so[q] = in ? cube_index(ci, cj, ck) : -1;
+    const int s = in ? cube_index(ci, cj, ck) : -1;
+    so[q] = s;
+    if (s >= 0) {
+      const int key = s * 2 + (q < nsc ? 0 : 1);
+      atomicOr(&keybits[key >> 5], 1u << (key & 31));
+    }
   }
   __threadfence_block();
   __syncthreads();
-  if (tid < 64) {  // stable ranks: one wave, stack order
+  {  // exclusive prefix of the words' popcounts
+    constexpr int kPer = (kKeyWords + kMpThreads - 1) / kMpThreads;
+    int sum = 0;
+    for (int k = 0; k < kPer; ++k) {
+      const int i = tid * kPer + k;
+      if (i < kKeyWords) sum += __popc(keybits[i]);
+    }
+    int tot;
+    int run = block_excl_scan<kMpThreads>(sum, scratch, tot);
+    for (int k = 0; k < kPer; ++k) {
+      const int i = tid * kPer + k;
+      if (i < kKeyWords) {
+        keypre[i] = run;
+        run += __popc(keybits[i]);
+      }
+    }
+    if (tid == 0) keypre[kKeyWords] = tot;
+  }
+  __syncthreads();
+  const int nkeys = keypre[kKeyWords];
+  if (nkeys <= kDense) {
+    // stable ranks, all waves: wave w ranks its contiguous chunk of the stack (in order, per dense
+    // key), then each key's chunk counts are prefixed in wave order
+    const int w = tid >> 6, chunk = ((nst + kWaves * 64 - 1) / (kWaves * 64)) * 64;
+    const int q0 = w * chunk, q1 = min(nst, q0 + chunk);
+    for (int base = q0; base < q1; base += 64) {
+      const int q = base + lane;
+      const bool v = q < q1;
+      const int s = v ? so[q] : -1;
+      const int key = s < 0 ? -1 : s * 2 + (q < nsc ? 0 : 1);
+      const int id = key < 0 ? -1 : keypre[key >> 5] + __popc(keybits[key >> 5] & ((1u << (key & 31)) - 1u));
+      uint64_t m = __ballot(v && id >= 0);
+      int rank = 0;
+      while (m) {
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        const int il = __shfl(id, leader, 64);
+        const uint64_t mm = __ballot(v && id == il);
+        const int basecnt = wcnt[w][il];
+        if (v && id == il) rank = basecnt + __popcll(mm & lanemask_lt());
+        __builtin_amdgcn_wave_barrier();
+        if (lane == leader) wcnt[w][il] = basecnt + __popcll(mm);
+        __builtin_amdgcn_wave_barrier();
+        m &= ~mm;
+      }
+      if (v) ro[q] = rank;
+    }
+    __threadfence_block();
+    __syncthreads();
+    // per dense key: chunk bases in wave order (wcnt becomes the base), total into cnt
+    for (int i = tid; i < 2 * kCubeNum; i += kMpThreads) {
+      if (!(keybits[i >> 5] & (1u << (i & 31)))) continue;
+      const int id = keypre[i >> 5] + __popc(keybits[i >> 5] & ((1u << (i & 31)) - 1u));
+      int run = 0;
+#pragma unroll
+      for (int ww = 0; ww < kWaves; ++ww) {
+        const int c = wcnt[ww][id];
+        wcnt[ww][id] = run;
+        run += c;
+      }
+      cnt[i & 1][i >> 1] = run;
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int q = tid; q < nst; q += kMpThreads) {
+      const int s = so[q];
+      if (s < 0) continue;
+      const int key = s * 2 + (q < nsc ? 0 : 1);
+      const int id = keypre[key >> 5] + __popc(keybits[key >> 5] & ((1u << (key & 31)) - 1u));
+      ro[q] += wcnt[q / chunk][id];
+    }
+  } else if (tid < 64) {  // many keys: stable ranks by one wave, stack order
     for (int base = 0; base < nsc + nss; base += 64) {
       const int q = base + lane;
       const bool v = q < nsc + nss;

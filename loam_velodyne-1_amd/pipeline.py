@@ -17,6 +17,7 @@ Mapping consumes a frame only when odometry published it (every skipFrameNum-th 
 """
 import queue
 import threading
+import time
 
 _END = object()
 
@@ -25,14 +26,26 @@ class NodePipeline:
     """Three node contexts on three threads.  `engine_cls(cfg)` makes one context; `imu` entries are
     not routed here (configs 3/4 carry none; the IMU path is the single-context `Engine.imu`)."""
 
-    def __init__(self, engine_cls, cfg=None, depth=4):
+    # measured on config 3 (tools/pipe_bench.py, GPU_MAX_HW_QUEUES=8): laserMapping is the critical
+    # node; its streams at the highest priority take the pipeline from 0.63-0.71 to 0.60-0.62 ms/sweep
+    DEFAULT_PRIORITY = {"mp": 1}
+
+    def __init__(self, engine_cls, cfg=None, depth=4, stages=3, priority=DEFAULT_PRIORITY):
+        """stages = 3: one context / thread per node; 2: scanRegistration and laserOdometry share
+        one context and thread (the front end), laserMapping has its own.  priority: optional
+        {"sr" | "od" | "mp": > 0 high, 0 normal, < 0 low} stream priorities of the node contexts."""
+        if stages not in (2, 3):
+            raise ValueError("stages must be 2 or 3")
         self.sr = engine_cls(cfg)
-        self.od = engine_cls(cfg)
+        self.od = engine_cls(cfg) if stages == 3 else self.sr
         self.mp = engine_cls(cfg)
+        self.stages = stages
         self.depth = depth
+        for k, v in (priority or {}).items():
+            getattr(self, k).set_stream_priority(v)
 
     def close(self):
-        for e in (self.sr, self.od, self.mp):
+        for e in {id(e): e for e in (self.sr, self.od, self.mp)}.values():
             e.close()
 
     def run(self, sweeps, stamps=None, on_mapping=None):
@@ -43,6 +56,7 @@ class NodePipeline:
         q_odom = queue.Queue(self.depth)
         results, err = [], []
         n_od = [0]
+        busy = {"scanRegistration": 0.0, "laserOdometry": 0.0, "laserMapping": 0.0}
 
         def guard(fn, out_q):
             def body():
@@ -60,9 +74,22 @@ class NodePipeline:
                 if err:
                     return
                 t = stamps[k] if stamps is not None else 0.1 * k
+                a = time.perf_counter()
                 rc, f = self.sr.scan_registration(s, stamp=t)
+                busy["scanRegistration"] += time.perf_counter() - a
                 if rc == 0:
-                    q_feat.put((t, f))
+                    if self.stages == 3:
+                        q_feat.put((t, f))
+                    else:
+                        odometry(t, f)
+
+        def odometry(t, f):
+            n_od[0] += 1
+            a = time.perf_counter()
+            pub, pose, cl, sl, full = self.od.odometry(f, stamp=t)
+            busy["laserOdometry"] += time.perf_counter() - a
+            if pub == 7:
+                q_odom.put((t, pose, cl, sl, full))
 
         def node_od():
             while True:
@@ -71,15 +98,10 @@ class NodePipeline:
                     return
                 if err:
                     continue  # drain so the producer never blocks
-                t, f = it
-                n_od[0] += 1
                 try:
-                    pub, pose, cl, sl, full = self.od.odometry(f, stamp=t)
+                    odometry(*it)
                 except BaseException as e:  # noqa: BLE001 - keep draining, re-raised in the caller
                     err.append(e)
-                    continue
-                if pub == 7:
-                    q_odom.put((t, pose, cl, sl, full))
 
         def node_mp():
             while True:
@@ -90,20 +112,26 @@ class NodePipeline:
                     continue
                 t, pose, cl, sl, full = it
                 try:
+                    a = time.perf_counter()
                     r = self.mp.mapping(pose, cl, sl, full, stamp=t)
+                    busy["laserMapping"] += time.perf_counter() - a
                     results.append(r)
                     if on_mapping is not None:
                         on_mapping(self.mp, r)
                 except BaseException as e:  # noqa: BLE001 - keep draining, re-raised in the caller
                     err.append(e)
 
-        threads = [threading.Thread(target=guard(node_sr, q_feat), name="scanRegistration"),
-                   threading.Thread(target=guard(node_od, q_odom), name="laserOdometry"),
-                   threading.Thread(target=guard(node_mp, None), name="laserMapping")]
+        if self.stages == 3:
+            threads = [threading.Thread(target=guard(node_sr, q_feat), name="scanRegistration"),
+                       threading.Thread(target=guard(node_od, q_odom), name="laserOdometry")]
+        else:
+            threads = [threading.Thread(target=guard(node_sr, q_odom), name="frontEnd")]
+        threads.append(threading.Thread(target=guard(node_mp, None), name="laserMapping"))
         for th in threads:
             th.start()
         for th in threads:
             th.join()
+        self.busy_s = busy  # seconds each node spent inside its engine calls (the rest is waiting)
         if err:
             raise err[0]
         return results, n_od[0]

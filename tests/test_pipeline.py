@@ -54,6 +54,9 @@ class FakeNode:
         self.mp_sum = self.mp_sum * 0.25 + float(pose[0])
         return np.array([self.mp_sum, stamp], np.float32), None, full
 
+    def set_stream_priority(self, p):
+        self.priority = p
+
     def close(self):
         self.closed = True
 
@@ -73,11 +76,12 @@ def sequential(sweeps, cfg):
 
 
 @pytest.mark.parametrize("depth", [1, 4])
-def test_pipeline_equals_sequential(depth):
+@pytest.mark.parametrize("stages", [2, 3])
+def test_pipeline_equals_sequential(depth, stages):
     sweeps = [np.full((3, 4), float(k), np.float32) for k in range(40)]
     cfg = {"delay": 3}
     ref, n_ref = sequential(sweeps, cfg)
-    pl = pipeline.NodePipeline(FakeNode, cfg, depth=depth)
+    pl = pipeline.NodePipeline(FakeNode, cfg, depth=depth, stages=stages)
     res, n = pl.run(sweeps)
     pl.close()
     assert n == n_ref == 37
