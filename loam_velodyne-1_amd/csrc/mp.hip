@@ -477,31 +477,58 @@ __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
     const int cur = block_radix_sort_kv<NT, E>(ka, va, kb, vb, n, nbits, sc);
     const uint32_t* ks = cur ? kb : ka;
     const uint16_t* vs = cur ? vb : va;
-    int run = 0;
-    for (int base = 0; base < n; base += NT) {
-      const int t = base + tid;
-      const uint32_t k = t < n ? ks[t] : 0u;
-      const int head = (t < n && (t == 0 || ks[t - 1] != k)) ? 1 : 0;
-      int tot;
-      const int ex = block_excl_scan<NT>(head, isc, tot);
-      if (head) {
-        int e = t + 1;
-        while (e < n && ks[e] == k) ++e;
-        float sx = 0, sy = 0, sz = 0, si = 0;
-        for (int mm = t; mm < e; mm += 4) {  // four independent gathers in flight per step
-          float4 a[4];
+    // ordered per-voxel means in one pass: thread t owns sorted positions [t E, t E + E); its E
+    // members are gathered at once, each run that starts in the range is summed from its head in
+    // sorted order (a run reaching past the range reads on from global memory), and the runs'
+    // output slots come from one block scan of the heads per thread
+    {
+      const int i0 = tid * E;
+      uint32_t kk[E];
+      float4 a[E];
+      int nh = 0;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) a[u] = in[vs[min(mm + u, e - 1)]];
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (mm + u < e) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
-        }
-        const float cnt = (float)(e - t);
-        j.out[b0 + run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+      for (int e = 0; e < E; ++e) {
+        const int i = i0 + e;
+        kk[e] = i < n ? ks[i] : 0u;
+        a[e] = i < n ? in[vs[i]] : make_float4(0, 0, 0, 0);
+        nh += (i < n && (i == 0 || ks[i - 1] != kk[e])) ? 1 : 0;
       }
-      run += tot;
+      int tot;
+      int slot = block_excl_scan<NT>(nh, isc, tot);
+      bool open = false;
+      uint32_t ck = 0;
+      int cstart = 0;
+      float sx = 0, sy = 0, sz = 0, si = 0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = i0 + e;
+        if (i < n) {
+          const bool head = i == 0 || (e > 0 ? kk[e - 1] != kk[e] : ks[i - 1] != kk[e]);
+          if (head) {
+            if (open) {
+              const float cnt = (float)(i - cstart);
+              j.out[b0 + slot++] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+            }
+            open = true;
+            ck = kk[e];
+            cstart = i;
+            sx = 0; sy = 0; sz = 0; si = 0;
+          }
+          if (open) { sx += a[e].x; sy += a[e].y; sz += a[e].z; si += a[e].w; }
+        }
+      }
+      if (open) {
+        int m = min(i0 + E, n);  // (the range may end past the segment)
+        while (m < n && ks[m] == ck) {
+          const float4 b4 = in[vs[m]];
+          sx += b4.x; sy += b4.y; sz += b4.z; si += b4.w;
+          ++m;
+        }
+        const float cnt = (float)(m - cstart);
+        j.out[b0 + slot] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+      }
+      if (tid == 0) j.out_count[s] = tot;
     }
-    if (tid == 0) j.out_count[s] = run;
     __syncthreads();  // the LDS arrays are reused by the next segment
   }
 }
@@ -528,13 +555,15 @@ void vg_launch_reduce(const VgJob& j, hipStream_t st) {
 constexpr bool kVgFusedBatch = false;
 constexpr int kVgCubeCap = 12288;
 constexpr bool kVgCubeG256 = true;  // a workgroup per cube segment also in batches: a few large cubes dominate
-hipError_t vg_run(const VgJob& j0, void* tmp, size_t tmp_bytes, hipStream_t st, int G, int fcap) {
+// finish = false: the caller guarantees every segment fits fcap (the fused launch is all)
+hipError_t vg_run(const VgJob& j0, void* tmp, size_t tmp_bytes, hipStream_t st, int G, int fcap, bool finish = true) {
   if (j0.nseg == 0) return hipSuccess;
   const int grid = std::min(j0.nseg, 65536);
   VgJob j = j0;
   if (fcap > 0) {
     if (fcap <= 2048) hipLaunchKernelGGL((k_vg_radix<256, 8>), dim3(grid), dim3(256), 0, st, j0);
     else hipLaunchKernelGGL((k_vg_radix<1024, 12>), dim3(grid), dim3(1024), 0, st, j0);
+    if (!finish) return hipGetLastError();
     j.begin = j0.big_b;  // the multi-kernel path finishes what the fused kernel could not hold
     j.end = j0.big_e;
     j.keep_counts = 1;
@@ -1174,6 +1203,13 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
   const loampose::MapRot r = rot_load(b, p);
   const MpNnCtx c = mp_nn_ctx(b, p);
   int work = 0, nfits = 0;  // (work: the batch kernel's profiling counter; not summed here)
+  __syncthreads();  // trig
+  const MpTrig tg = mp_trig_of(trig);
+  double acc[28];
+#pragma unroll
+  for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+  // each lane's row is added right after its fit (same queries, same order per lane as a
+  // separate pass over the stored rows: identical sums, one reload round trip fewer)
   for (int q = blockIdx.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
     float4 sel;
     Top5 t;
@@ -1184,14 +1220,8 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
                  make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0), sel, jac[tid], nfits, cf, ok);
     qok[q] = (int8_t)ok;
     qcf[q] = cf;
+    if (ok) mp_row_accum(tg, stack[q < nsc ? q : b.capC + (q - nsc)], cf, acc);
   }
-  __syncthreads();  // trig
-  const MpTrig tg = mp_trig_of(trig);
-  double acc[28];
-#pragma unroll
-  for (int k = 0; k < 28; ++k) acc[k] = 0.0;
-  for (int q = blockIdx.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads)
-    if (qok[q]) mp_row_accum(tg, stack[q < nsc ? q : b.capC + (q - nsc)], qcf[q], acc);
   nfits = wave_sum(nfits);
   if (lane == 0 && nfits) atomicAdd(&ist[kMiFits], nfits);
   wave_reduce_scatter_28(acc);
@@ -1266,7 +1296,8 @@ namespace {
 // ---------------------------------------------------------------- insertion (:980-1016)
 // one workgroup per instance: cube slot of every stack point (corner, then surf), stable ranks by
 // one wave walking the stack in order, per-cube prefix, scatter of the map-frame points.
-__global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot_of, int* rank_of) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_mp_insert(MpBuffers b, int* slot_of, int* rank_of) {
   const int p = blockIdx.x, tid = threadIdx.x, lane = lane_id();
   const float* st = b.state + (size_t)p * kMpStateFloats;
   const int* ist = b.istate + (size_t)p * kMpStateInts;
@@ -1277,20 +1308,20 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
   int* so = slot_of + (size_t)p * b.cap_stack;
   int* ro = rank_of + (size_t)p * b.cap_stack;
   __shared__ int cnt[2][kCubeNum];
-  __shared__ int scratch[16];
+  __shared__ int scratch[NT / 64 + 1];
   // the (slot, kind) keys the stack uses, as a bitmap; their dense numbering (prefix popcounts)
   // lets every wave keep its own counts when few keys occur (the usual case: a sweep touches a
   // few dozen cubes)
-  constexpr int kKeyWords = (2 * kCubeNum + 31) / 32, kDense = 512, kWaves = kMpThreads / 64;
+  constexpr int kKeyWords = (2 * kCubeNum + 31) / 32, kDense = 512, kWaves = NT / 64;
   __shared__ unsigned keybits[kKeyWords];
   __shared__ int keypre[kKeyWords + 1];
   __shared__ int wcnt[kWaves][kDense];
-  for (int i = tid; i < 2 * kCubeNum; i += kMpThreads) cnt[i / kCubeNum][i % kCubeNum] = 0;
-  for (int i = tid; i < kKeyWords; i += kMpThreads) keybits[i] = 0u;
-  for (int i = tid; i < kWaves * kDense; i += kMpThreads) wcnt[i / kDense][i % kDense] = 0;
+  for (int i = tid; i < 2 * kCubeNum; i += NT) cnt[i / kCubeNum][i % kCubeNum] = 0;
+  for (int i = tid; i < kKeyWords; i += NT) keybits[i] = 0u;
+  for (int i = tid; i < kWaves * kDense; i += NT) wcnt[i / kDense][i % kDense] = 0;
   __syncthreads();
   const int nst = nsc + nss;
-  for (int q = tid; q < nst; q += kMpThreads) {
+  for (int q = tid; q < nst; q += NT) {
     const float4 a = loampose::point_to_map(r, stack[q < nsc ? q : b.capC + (q - nsc)]);
     const int ci = cube_of(a.x, cW), cj = cube_of(a.y, cH), ck = cube_of(a.z, cD);
     const bool in = ci >= 0 && ci < kCubeW && cj >= 0 && cj < kCubeH && ck >= 0 && ck < kCubeD;
@@ -1304,14 +1335,14 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
   __threadfence_block();
   __syncthreads();
   {  // exclusive prefix of the words' popcounts
-    constexpr int kPer = (kKeyWords + kMpThreads - 1) / kMpThreads;
+    constexpr int kPer = (kKeyWords + NT - 1) / NT;
     int sum = 0;
     for (int k = 0; k < kPer; ++k) {
       const int i = tid * kPer + k;
       if (i < kKeyWords) sum += __popc(keybits[i]);
     }
     int tot;
-    int run = block_excl_scan<kMpThreads>(sum, scratch, tot);
+    int run = block_excl_scan<NT>(sum, scratch, tot);
     for (int k = 0; k < kPer; ++k) {
       const int i = tid * kPer + k;
       if (i < kKeyWords) {
@@ -1328,10 +1359,23 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
     // key), then each key's chunk counts are prefixed in wave order
     const int w = tid >> 6, chunk = ((nst + kWaves * 64 - 1) / (kWaves * 64)) * 64;
     const int q0 = w * chunk, q1 = min(nst, q0 + chunk);
+    constexpr int kAhead = 8;  // slot loads of eight 64-point steps in flight (the walk is load-latency bound)
+    int sa[kAhead];
     for (int base = q0; base < q1; base += 64) {
+      const int step = ((base - q0) >> 6) % kAhead;
+      if (step == 0) {
+#pragma unroll
+        for (int u = 0; u < kAhead; ++u) {
+          const int qq = base + u * 64 + lane;
+          sa[u] = qq < q1 ? so[qq] : -1;
+        }
+      }
       const int q = base + lane;
       const bool v = q < q1;
-      const int s = v ? so[q] : -1;
+      int s = -1;
+#pragma unroll
+      for (int u = 0; u < kAhead; ++u)
+        if (u == step) s = sa[u];
       const int key = s < 0 ? -1 : s * 2 + (q < nsc ? 0 : 1);
       const int id = key < 0 ? -1 : keypre[key >> 5] + __popc(keybits[key >> 5] & ((1u << (key & 31)) - 1u));
       uint64_t m = __ballot(v && id >= 0);
@@ -1352,7 +1396,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
     __threadfence_block();
     __syncthreads();
     // per dense key: chunk bases in wave order (wcnt becomes the base), total into cnt
-    for (int i = tid; i < 2 * kCubeNum; i += kMpThreads) {
+    for (int i = tid; i < 2 * kCubeNum; i += NT) {
       if (!(keybits[i >> 5] & (1u << (i & 31)))) continue;
       const int id = keypre[i >> 5] + __popc(keybits[i >> 5] & ((1u << (i & 31)) - 1u));
       int run = 0;
@@ -1366,7 +1410,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
     }
     __threadfence_block();
     __syncthreads();
-    for (int q = tid; q < nst; q += kMpThreads) {
+    for (int q = tid; q < nst; q += NT) {
       const int s = so[q];
       if (s < 0) continue;
       const int key = s * 2 + (q < nsc ? 0 : 1);
@@ -1402,7 +1446,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
   int* ac = b.app_cnt + (size_t)p * kCubeNum * 2;
   int* ao = b.app_off + (size_t)p * kCubeNum * 2;
   {
-    constexpr int kFlat = 2 * kCubeNum, kPer = (kFlat + kMpThreads - 1) / kMpThreads;
+    constexpr int kFlat = 2 * kCubeNum, kPer = (kFlat + NT - 1) / NT;
     int* cf = &cnt[0][0];
     int sum = 0;
     for (int k = 0; k < kPer; ++k) {
@@ -1410,7 +1454,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
       if (i < kFlat) sum += cf[i];
     }
     int tot;
-    int run = block_excl_scan<kMpThreads>(sum, scratch, tot);
+    int run = block_excl_scan<NT>(sum, scratch, tot);
     for (int k = 0; k < kPer; ++k) {
       const int i = tid * kPer + k;
       if (i < kFlat) {
@@ -1420,7 +1464,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
       }
     }
     __syncthreads();
-    for (int i = tid; i < kFlat; i += kMpThreads) {
+    for (int i = tid; i < kFlat; i += NT) {
       const int kind = i / kCubeNum, s = i % kCubeNum;
       const int o = cf[i], nx = i + 1 < kFlat ? cf[i + 1] : tot;
       ac[s * 2 + kind] = nx - o;
@@ -1430,7 +1474,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_insert(MpBuffers b, int* slot
   __threadfence_block();
   __syncthreads();
   float4* app = b.app + (size_t)p * b.cap_stack;
-  for (int q = tid; q < nsc + nss; q += kMpThreads) {
+  for (int q = tid; q < nsc + nss; q += NT) {
     const int s = so[q];
     if (s < 0) continue;
     const int kind = q < nsc ? 0 : 1;
@@ -1514,8 +1558,9 @@ __global__ __launch_bounds__(256) void k_mp_vcopy(MpBuffers b) {
 // new cube store: valid cubes <- their DS output, every other cube <- old ++ appended.  The
 // (kind, cube) sizes go to LDS in coalesced passes; each thread then owns a contiguous run of
 // them, so the offsets and the non-empty list need one block scan each.
-__global__ __launch_bounds__(kMpThreads) void k_mp_compact_table(MpBuffers b) {
-  constexpr int N = 2 * kCubeNum, E = (N + kMpThreads - 1) / kMpThreads;
+template <int NT>
+__global__ __launch_bounds__(NT) void k_mp_compact_table(MpBuffers b) {
+  constexpr int N = 2 * kCubeNum, E = (N + NT - 1) / NT;
   const int p = blockIdx.x, tid = threadIdx.x;
   const int nv = b.istate[(size_t)p * kMpStateInts + kMiNValid];
   const int* old = slot_table(b, b.pool_cur, p);
@@ -1523,13 +1568,13 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_compact_table(MpBuffers b) {
   const int* ac = b.app_cnt + (size_t)p * kCubeNum * 2;
   __shared__ int16_t vidx[kCubeNum];
   __shared__ int nn[N];
-  __shared__ int scratch[16];
-  for (int s = tid; s < kCubeNum; s += kMpThreads) vidx[s] = -1;
+  __shared__ int scratch[NT / 64 + 1];
+  for (int s = tid; s < kCubeNum; s += NT) vidx[s] = -1;
   __syncthreads();
   if (tid < nv) vidx[b.valid[(size_t)p * kMaxValid + tid]] = (int16_t)tid;
   __syncthreads();
   int vpts = 0;
-  for (int x = tid; x < N; x += kMpThreads) {
+  for (int x = tid; x < N; x += NT) {
     const int kind = x / kCubeNum, s = x % kCubeNum, v = vidx[s];
     const int n = v >= 0 ? b.vseg_cnt[p * 2 * kMaxValid + kind * kMaxValid + v] : old[s * 4 + 1 + 2 * kind] + ac[s * 2 + kind];
     nn[x] = n;
@@ -1540,8 +1585,8 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_compact_table(MpBuffers b) {
   int sum = 0, ne = 0;
   for (int x = x0; x < x1; ++x) { sum += nn[x]; ne += nn[x] > 0 ? 1 : 0; }
   int run, nitems;
-  int off = block_excl_scan<kMpThreads>(sum, scratch, run);
-  int it = block_excl_scan<kMpThreads>(ne, scratch, nitems);
+  int off = block_excl_scan<NT>(sum, scratch, run);
+  int it = block_excl_scan<NT>(ne, scratch, nitems);
   int* items = b.citems + (size_t)p * 2 * kCubeNum;
   for (int x = x0; x < x1; ++x) {
     const int kind = x / kCubeNum, s = x % kCubeNum, n = nn[x];
@@ -1551,7 +1596,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_compact_table(MpBuffers b) {
     // the non-empty (kind, cube) list for the copy: kind | cube << 1 | (valid index + 1) << 14
     if (n > 0) items[it++] = kind | (s << 1) | (((int)vidx[s] + 1) << 14);
   }
-  vpts = block_reduce<kMpThreads>(vpts, scratch, [](int a, int c) { return a + c; });
+  vpts = block_reduce<NT>(vpts, scratch, [](int a, int c) { return a + c; });
   if (tid == 0) {
     b.nitems[p] = nitems;
     b.istate[(size_t)p * kMpStateInts + kMiValidPts] = vpts;
@@ -1707,7 +1752,7 @@ hipError_t mp_reset(MpBuffers& b, hipStream_t st) {
 }
 
 void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool map_empty,
-              const std::function<void()>& before_register) {
+              const std::function<void()>& before_register, int stack_max) {
   const int P = b.P;
   auto mark = [&](const char* n) { if (prof) prof->mark(n); };
   hipLaunchKernelGGL(k_mp_prepare, dim3(P), dim3(kMpThreads), 0, st, b, in);
@@ -1722,7 +1767,11 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     const size_t ns = (size_t)P * 2 * kMaxValid;
     js.sb24 = b.vg_split; js.se24 = b.vg_split + ns; js.sb32 = b.vg_split + 2 * ns; js.se32 = b.vg_split + 3 * ns;
   }
-  b.note(vg_run(js, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 1024 : 256, P <= 4 || kVgFusedBatch ? 12288 : 0));  // two large segments per instance
+  // two large segments per instance; when the host knows both fit the fused kernel, its
+  // multi-kernel finish (four launches over empty segment lists) is not enqueued
+  const int fcap_s = P <= 4 || kVgFusedBatch ? 12288 : 0;
+  const bool fits = fcap_s > 0 && stack_max >= 0 && stack_max <= fcap_s;
+  b.note(vg_run(js, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 1024 : 256, fcap_s, !fits));
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);
   mark("k_mp_gather");
@@ -1760,7 +1809,9 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   }
   hipLaunchKernelGGL(k_mp_lm_end, dim3((P + 255) / 256), dim3(256), 0, st, b);
   // insertion + per-valid-cube downsampling into the other pool
-  hipLaunchKernelGGL(k_mp_insert, dim3(P), dim3(kMpThreads), 0, st, b, (int*)b.vg_k, (int*)b.vg_v);
+  // a few instances: 1024 threads per instance (the per-instance serial parts are the cost)
+  if (P <= 4) hipLaunchKernelGGL(k_mp_insert<1024>, dim3(P), dim3(1024), 0, st, b, (int*)b.vg_k, (int*)b.vg_v);
+  else hipLaunchKernelGGL(k_mp_insert<kMpThreads>, dim3(P), dim3(kMpThreads), 0, st, b, (int*)b.vg_k, (int*)b.vg_v);
   mark("k_mp_insert");
   hipLaunchKernelGGL(k_mp_vseg, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_vcopy, dim3(32, P), dim3(256), 0, st, b);
@@ -1774,7 +1825,8 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   jv.err = b.istate + kMiErr; jv.err_stride = kMpStateInts; jv.seg_per_err = 2 * kMaxValid;
   b.note(vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 || kVgCubeG256 ? 256 : 64, P <= 4 || kVgFusedBatch ? kVgCubeCap : 0));  // 2 x 125 cube segments per instance
   mark("vg_cubes");
-  hipLaunchKernelGGL(k_mp_compact_table, dim3(P), dim3(kMpThreads), 0, st, b);
+  if (P <= 4) hipLaunchKernelGGL(k_mp_compact_table<1024>, dim3(P), dim3(1024), 0, st, b);
+  else hipLaunchKernelGGL(k_mp_compact_table<kMpThreads>, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);
   mark("k_mp_compact");
   if (before_register) before_register();
@@ -1837,7 +1889,7 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
     le = pin.up(st2, b.inF, full.pts, (size_t)n[2]);
     if (le == hipSuccess) le = hipEventRecord(ev2, st2);
     if (le == hipSuccess) le = hipStreamWaitEvent(st, ev2, 0);
-  });
+  }, std::max(n[0], n[1]));
   (void)hipEventRecord(e1, st);
   float* sf = (float*)(mi + 16);                  // kMpStateFloats
   int* si = mi + 16 + kMpStateFloats;             // kMpStateInts

@@ -130,9 +130,10 @@ void mp_free(MpBuffers& b);
 hipError_t mp_reset(MpBuffers& b, hipStream_t st);
 // map_empty: the store was just reset (no L-M can run: its launches are skipped)
 // before_register: called once every kernel before k_mp_register is enqueued (the streaming path
-// stages the full cloud there)
+// stages the full cloud there); stack_max: the largest stack segment (corner or surf input count)
+// when the host knows it, else -1
 void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof = nullptr, bool map_empty = false,
-              const std::function<void()>& before_register = nullptr);
+              const std::function<void()>& before_register = nullptr, int stack_max = -1);
 // imu_rp: the IMU (roll, pitch) transformUpdate blends in (nullptr = no IMU); *updated = whether
 // transformUpdate ran (the caller then commits its IMU queue pointer)
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,

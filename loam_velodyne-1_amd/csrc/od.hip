@@ -200,6 +200,39 @@ __global__ __launch_bounds__(1024) void k_hash_scan(HashPair hp) {
   __shared__ int scratch[32];
   const int per = (T + 1023) / 1024;
   const int b0 = tid * per, b1 = min(T, b0 + per);
+  if (per % 4 == 0 && per <= 64 && T % 1024 == 0) {  // uniform: every run is full
+    // the thread's run as up to sixteen 16-B loads, all in flight (T is a power of two: per divides it)
+    constexpr int kV = 16;
+    int4 v[kV];
+    const int4* f4 = (const int4*)(fill + b0);
+    const int nv = per / 4;
+#pragma unroll
+    for (int k = 0; k < kV; ++k)
+      if (k < nv) v[k] = f4[k];
+    int local = 0;
+#pragma unroll
+    for (int k = 0; k < kV; ++k)
+      if (k < nv) local += v[k].x + v[k].y + v[k].z + v[k].w;
+    int tot;
+    int run = block_excl_scan<1024>(local, scratch, tot);
+    int4* o4 = (int4*)(fill + b0);
+#pragma unroll
+    for (int k = 0; k < kV; ++k)
+      if (k < nv) {
+        int4 r;
+        r.x = run; run += v[k].x;
+        r.y = run; run += v[k].y;
+        r.z = run; run += v[k].z;
+        r.w = run; run += v[k].w;
+        o4[k] = r;
+        start[b0 + 4 * k] = r.x;
+        start[b0 + 4 * k + 1] = r.y;
+        start[b0 + 4 * k + 2] = r.z;
+        start[b0 + 4 * k + 3] = r.w;
+      }
+    if (tid == 0) start[T] = tot;
+    return;
+  }
   int local = 0;
   for (int b = b0; b < b1; ++b) local += fill[b];
   int tot;
@@ -902,18 +935,19 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows_small(OdBuffers b, FeatV
   if (tid < 8 * 28) {
     const int v = tid % 28, sl = tid / 28;
     const double* pp = b.part + (size_t)p * b.gq * b.max_iter * 28 + v;
-    double t16[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int g = sl + 8 * u;
-      t16[u] = g < G ? __hip_atomic_load(&pp[(size_t)g * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-    }
+    // the slice's partials in order, sixteen loads in flight per round (G grows to gq * (iter + 1))
     double acc1 = 0.0;
+    for (int g0 = sl; g0 < G; g0 += 8 * 16) {
+      double t16[16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u)
-      if (sl + 8 * u < G) acc1 += t16[u];
-    for (int g = sl + 8 * 16; g < G; g += 8)  // beyond 128 partials (larger sweeps)
-      acc1 += __hip_atomic_load(&pp[(size_t)g * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int u = 0; u < 16; ++u) {
+        const int g = g0 + 8 * u;
+        t16[u] = g < G ? __hip_atomic_load(&pp[(size_t)g * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (g0 + 8 * u < G) acc1 += t16[u];
+    }
     slice[sl][v] = acc1;
   }
   __syncthreads();
