@@ -209,7 +209,6 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_prepare(MpBuffers b, MpInput 
 // ---------------------------------------------------------------- stacks
 __global__ __launch_bounds__(256) void k_mp_stack(MpBuffers b, MpInput in) {
   const int p = blockIdx.y;
-  const float* st = b.state + (size_t)p * kMpStateFloats;
   const loampose::MapRot r = rot_load(b, p);
   const int nc = min(in.ncorner[p * in.ncorner_stride], b.capC);
   const int ns = min(in.nsurf[p * in.nsurf_stride], b.capS);
@@ -1039,7 +1038,6 @@ __global__ __launch_bounds__(kMpQueryThreads) __attribute__((amdgpu_waves_per_eu
   const int p = blk.y, tid = threadIdx.x;
   const int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan] || ist[kMiStop]) return;
-  const float* st = b.state + (size_t)p * kMpStateFloats;
   const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
   const int nq = nsc + nss;
   __shared__ uint32_t lists[27 * kMpQueryThreads];
@@ -1067,7 +1065,6 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
   int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan] || ist[kMiStop]) return;
   const bool first = ist[kMiIters] == 0;  // fits of an earlier frame are stale
-  const float* st = b.state + (size_t)p * kMpStateFloats;
   // per-lane 3x3 Jacobi scratch (27 words; the odd stride keeps lanes on distinct banks): 27 KB,
   // five workgroups per CU (33-word rows allowed four; measured 1.56 -> 1.40 ms per step)
   __shared__ float jac[kMpQueryThreads][27];
@@ -1299,7 +1296,6 @@ namespace {
 template <int NT>
 __global__ __launch_bounds__(NT) void k_mp_insert(MpBuffers b, int* slot_of, int* rank_of) {
   const int p = blockIdx.x, tid = threadIdx.x, lane = lane_id();
-  const float* st = b.state + (size_t)p * kMpStateFloats;
   const int* ist = b.istate + (size_t)p * kMpStateInts;
   const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
   const float4* stack = b.stack + (size_t)p * b.cap_stack;
