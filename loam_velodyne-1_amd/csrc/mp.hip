@@ -687,6 +687,10 @@ LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t, i
 }
 
 constexpr int kMpQueryThreads = 256;
+#ifndef LOAM_NN_THREADS
+#define LOAM_NN_THREADS 256
+#endif
+constexpr int kMpNnThreads = LOAM_NN_THREADS;
 
 // The same search with the lane's work flattened: first every cell the lane may need (box
 // distance below 1 m and not above the seeded 5th distance) is listed with its bucket range — 27
@@ -695,6 +699,7 @@ constexpr int kMpQueryThreads = 256;
 // the lane's LDS column (stride kMpQueryThreads).  Ranges are packed start:19 | count:13; a lane
 // whose ranges do not fit falls back to knn5.
 constexpr int kNnInFlight = 8;  // measured k_mp_nn ms/step: 2 -> 4.17, 4 -> 3.95, 8 -> 3.88, 16 -> 5.33
+template <int S = kMpQueryThreads>
 LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5& t, uint32_t* lst, int& work) {
   if (T <= 0) return;
   const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
@@ -717,7 +722,7 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
       LOAM_CHECK(b0 >= 0 && cnt >= 0, b0, cnt);
       if (cnt > 0) {
         if (b0 >= (1 << 19) || cnt >= (1 << 13)) fits = false;
-        lst[n * kMpQueryThreads] = (uint32_t)b0 | ((uint32_t)cnt << 19);
+        lst[n * S] = (uint32_t)b0 | ((uint32_t)cnt << 19);
         ++n;
         total += cnt;
       }
@@ -731,7 +736,7 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
   int ci = 0, left = 0, pos = 0;
   auto next = [&]() {  // index of the lane's next candidate
     if (left == 0) {
-      const uint32_t e = lst[ci * kMpQueryThreads];
+      const uint32_t e = lst[ci * S];
       ++ci;
       pos = (int)(e & ((1u << 19) - 1));
       left = (int)(e >> 19);
@@ -821,6 +826,7 @@ LOAM_D MpNnCtx mp_nn_ctx(const MpBuffers& b, int p) {
   return c;
 }
 
+template <int S = kMpQueryThreads>
 LOAM_D void mp_nn_query(const MpBuffers& b, const MpNnCtx& c, int q, int nsc, bool first, const loampose::MapRot& r,
                         uint32_t* lst, float4& sel, Top5& t, int& work) {
   const bool corner = q < nsc;
@@ -841,8 +847,8 @@ LOAM_D void mp_nn_query(const MpBuffers& b, const MpNnCtx& c, int q, int nsc, bo
         ++work;
       }
   }
-  if (corner) knn5_flat(c.hcs, c.hcp, c.TC, sel, t, lst, work);
-  else knn5_flat(c.hss, c.hsp, c.TS, sel, t, lst, work);
+  if (corner) knn5_flat<S>(c.hcs, c.hcp, c.TC, sel, t, lst, work);
+  else knn5_flat<S>(c.hss, c.hsp, c.TS, sel, t, lst, work);
   LOAM_CHECK(q < b.cap_stack && (t.i[4] == 0x7fffffff || t.i[4] < (corner ? c.nfc : c.nfs)), q, t.i[4]);
   qnn[2 * q] = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
   qnn[2 * q + 1] = make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0);
@@ -1033,23 +1039,23 @@ LOAM_D void mp_step(const MpBuffers& b, int p, const double* tot, MpStepScratch&
 // waves per SIMD (<= 96 VGPRs; the LDS lists allow five workgroups per CU).  COUNT: the profiling
 // variant that also sums its work (candidates, bucket ranges) into the frame's istate
 template <bool COUNT>
-__global__ __launch_bounds__(kMpQueryThreads) __attribute__((amdgpu_waves_per_eu(5))) void k_mp_nn(MpBuffers b) {
+__global__ __launch_bounds__(kMpNnThreads) __attribute__((amdgpu_waves_per_eu(5))) void k_mp_nn(MpBuffers b) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, tid = threadIdx.x;
   const int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan] || ist[kMiStop]) return;
   const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
   const int nq = nsc + nss;
-  __shared__ uint32_t lists[27 * kMpQueryThreads];
+  __shared__ uint32_t lists[27 * kMpNnThreads];
   uint32_t* lst = lists + tid;
   const bool first = ist[kMiIters] == 0;
   const loampose::MapRot r = rot_load(b, p);
   const MpNnCtx c = mp_nn_ctx(b, p);
   int work = 0;  // work counter (loam_stats mp_nn_candidates / mp_nn_cells), packed as in knn5
-  for (int q = blk.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
+  for (int q = blk.x * kMpNnThreads + tid; q < nq; q += gridDim.x * kMpNnThreads) {
     float4 sel;
     Top5 t;
-    mp_nn_query(b, c, q, nsc, first, r, lst, sel, t, work);
+    mp_nn_query<kMpNnThreads>(b, c, q, nsc, first, r, lst, sel, t, work);
   }
   if (!COUNT) return;
   const int ncand = wave_sum(work & ((1 << kWorkCellShift) - 1)), ncell = wave_sum(work >> kWorkCellShift);
@@ -1795,8 +1801,9 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
       mark("k_mp_lm_small");
       continue;
     }
-    if (prof) hipLaunchKernelGGL(k_mp_nn<true>, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
-    else hipLaunchKernelGGL(k_mp_nn<false>, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
+    const int gnn = gq * (kMpQueryThreads / kMpNnThreads);
+    if (prof) hipLaunchKernelGGL(k_mp_nn<true>, dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
+    else hipLaunchKernelGGL(k_mp_nn<false>, dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
     mark("k_mp_nn");
     hipLaunchKernelGGL(k_mp_fit, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
     mark("k_mp_fit");
