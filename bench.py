@@ -164,11 +164,12 @@ def stream_leg(loam, sg, n_sweeps, n_cpu, stages=3, priority="default"):
     return out
 
 
-def latency_leg(loam, sg, runs, warmup):
-    """Config 2: one VLP-16 problem (prev, cur) at a time, warm (context and buffers reused), the
-    whole problem on the device per call; ms per problem (median of `runs`)"""
-    prev, cur = sg.single_problem(0)
-    eng = loam.Engine()
+def latency_leg(loam, sg, runs, warmup, seed=0, lidar=None, cfg=None,
+                config="config2: one VLP-16 problem (seed 0), warm context, inputs resident"):
+    """Config 2 (and config 5 with lidar=HDL64): one problem (prev, cur) at a time, warm (context and
+    buffers reused), the whole problem on the device per call; ms per problem (median of `runs`)"""
+    prev, cur = sg.single_problem(seed) if lidar is None else sg.single_problem(seed, lidar=lidar)
+    eng = loam.Engine(cfg) if cfg is not None else loam.Engine()
     eng.batch_upload([prev], [cur])
     for _ in range(warmup):
         eng.batch_run()
@@ -181,7 +182,7 @@ def latency_leg(loam, sg, runs, warmup):
         ts.append(time.perf_counter() - a)
     od, aft, _ = eng.batch_download()
     eng.close()
-    return {"config": "config2: one VLP-16 problem (seed 0), warm context, inputs resident",
+    return {"config": config,
             "ms_median": 1e3 * statistics.median(ts), "ms_min": 1e3 * min(ts), "runs": runs}, (prev, cur, od, aft)
 
 
@@ -466,20 +467,34 @@ def main(argv=None):
         if args.stream_sweeps > 0:
             stream = stream_leg(loam, sg, args.stream_sweeps, args.stream_cpu_sweeps)
         if args.latency_runs > 0:
-            latency, (p0, c0, od0, aft0) = latency_leg(loam, sg, args.latency_runs, 5)
-            if args.cpu_sample > 0:
-                sys.path.insert(0, os.path.join(ROOT, "oracle"))
-                import oracle_ctypes as oc
-                with pinned_core():
-                    ts = []
-                    for _ in range(4):
-                        a = time.perf_counter()
-                        od_o, aft_o, _ = oc.problem(p0, c0)
-                        ts.append(time.perf_counter() - a)
-                cpu_ms = 1e3 * statistics.median(ts[1:])
-                latency["cpu_oracle_ms"] = cpu_ms
-                latency["speedup_vs_cpu"] = cpu_ms / latency["ms_median"]
-                latency["max_abs_err"] = float(max(np.abs(od0[0] - od_o).max(), np.abs(aft0[0] - aft_o).max()))
+            def with_cpu(lat, p0, c0, od0, aft0, ocfg=None):
+                """the pinned oracle on the same problem: median of 3 after a warm-up, and the parity"""
+                if args.cpu_sample > 0:
+                    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+                    import oracle_ctypes as oc
+                    with pinned_core():
+                        ts = []
+                        for _ in range(4):
+                            a = time.perf_counter()
+                            od_o, aft_o, _ = oc.problem(p0, c0) if ocfg is None else oc.problem(p0, c0, ocfg(oc))
+                            ts.append(time.perf_counter() - a)
+                    cpu_ms = 1e3 * statistics.median(ts[1:])
+                    lat["cpu_oracle_ms"] = cpu_ms
+                    lat["speedup_vs_cpu"] = cpu_ms / lat["ms_median"]
+                    lat["max_abs_err"] = float(max(np.abs(od0[0] - od_o).max(), np.abs(aft0[0] - aft_o).max()))
+                return lat
+
+            latency, prob = latency_leg(loam, sg, args.latency_runs, 5)
+            latency = with_cpu(latency, *prob)
+            # config 5: one dense HDL-64E problem (64 rings, ~131k points per sweep)
+            # (the reference's 64-ring settings: linear ring model, 100 odometry / 20 mapping iterations)
+            dense_cfg = dict(n_rings=64, max_points=160000, od_max_iter=100, mp_max_iter=20)
+            dense, prob = latency_leg(loam, sg, max(args.latency_runs // 5, 3), 2, seed=2, lidar=sg.HDL64,
+                                      cfg=loam.default_config(ring_model=loam.RING_LINEAR, **dense_cfg),
+                                      config="config5: one HDL-64E problem (seed 2, 64 rings), warm context, "
+                                             "inputs resident")
+            dense["points_per_sweep"] = int(len(prob[1]))
+            latency["config5"] = with_cpu(dense, *prob, ocfg=lambda oc: oc.default_config(ring_model=1, **dense_cfg))
     out = {
         "metric": METRIC,
         "value": value,

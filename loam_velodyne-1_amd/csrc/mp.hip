@@ -687,10 +687,9 @@ LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t, i
 }
 
 constexpr int kMpQueryThreads = 256;
-#ifndef LOAM_NN_THREADS
-#define LOAM_NN_THREADS 256
-#endif
-constexpr int kMpNnThreads = LOAM_NN_THREADS;
+// k_mp_nn workgroup size (measured k_mp_nn ms/step at batch 1024: 64 -> 3.83, 128 -> 3.81-3.86,
+// 256 -> 3.92-3.95): a workgroup's LDS is released when its slowest lane is done
+constexpr int kMpNnThreads = 128;
 
 // The same search with the lane's work flattened: first every cell the lane may need (box
 // distance below 1 m and not above the seeded 5th distance) is listed with its bucket range — 27
