@@ -1849,9 +1849,14 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
     err = "mapping input cloud pts is null";
     return LOAM_E_INVAL;
   }
-  hipEvent_t e0, e1;
-  (void)hipEventCreate(&e0);
-  (void)hipEventCreate(&e1);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipError_t ce = hipEventCreate(&e0);
+  if (ce == hipSuccess) ce = hipEventCreate(&e1);
+  if (ce != hipSuccess) {
+    if (e0) (void)hipEventDestroy(e0);
+    err = std::string("mapping timing events: ") + hipGetErrorString(ce);
+    return LOAM_E_HIP;
+  }
   // host inputs through the pinned arena / scratch: [0..2] counts, [4..9] pose, [10..11] IMU
   // (roll, pitch), [12] IMU flag; downloads below from [16]
   int* mi = (int*)meta;
@@ -1875,6 +1880,8 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   if (ue == hipSuccess) ue = hipMemcpyAsync(b.state + kMpImuRP, mi + 10, 2 * sizeof(float), hipMemcpyHostToDevice, st);
   if (ue == hipSuccess) ue = hipMemcpyAsync(b.istate + kMiImu, mi + 12, sizeof(int), hipMemcpyHostToDevice, st);
   if (ue != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     err = std::string("mapping upload: ") + hipGetErrorString(ue);
     return LOAM_E_HIP;
   }
@@ -1884,15 +1891,14 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   in.ncorner = b.in_n; in.nsurf = b.in_n + 1; in.nfull = b.in_n + 2;
   in.ncorner_stride = in.nsurf_stride = in.nfull_stride = 3;
   in.pose = b.in_pose; in.pose_stride = 6;
-  (void)hipEventRecord(e0, st);
-  hipError_t le = hipSuccess;
+  hipError_t le = hipEventRecord(e0, st);
   mp_frame(b, in, st, nullptr, false, [&]() {
-    if (!late) return;
+    if (!late || le != hipSuccess) return;
     le = pin.up(st2, b.inF, full.pts, (size_t)n[2]);
     if (le == hipSuccess) le = hipEventRecord(ev2, st2);
     if (le == hipSuccess) le = hipStreamWaitEvent(st, ev2, 0);
   }, std::max(n[0], n[1]));
-  (void)hipEventRecord(e1, st);
+  if (le == hipSuccess) le = hipEventRecord(e1, st);
   float* sf = (float*)(mi + 16);                  // kMpStateFloats
   int* si = mi + 16 + kMpStateFloats;             // kMpStateInts
   int* pnreg = si + kMpStateInts;
@@ -2001,8 +2007,8 @@ int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::s
   j.vals = b.vg_v; j.vals_alt = b.vg_v2; j.big_b = b.vg_bb; j.big_e = b.vg_be; j.nseg = 1; j.total = b.P * b.map_cap;
   b.note(vg_run(j, b.cub_tmp, b.cub_bytes, st, 1024, 12288));
   int cnt = 0;
-  (void)hipMemcpyAsync(&cnt, b.vseg_cnt, sizeof(int), hipMemcpyDeviceToHost, st);
-  hipError_t he = hipStreamSynchronize(st);
+  hipError_t he = hipMemcpyAsync(&cnt, b.vseg_cnt, sizeof(int), hipMemcpyDeviceToHost, st);
+  if (he == hipSuccess) he = hipStreamSynchronize(st);
   if (he == hipSuccess) he = b.take_error();
   if (he != hipSuccess) {
     err = std::string("surround: ") + hipGetErrorString(he);
