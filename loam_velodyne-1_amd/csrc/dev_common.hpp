@@ -882,6 +882,11 @@ LOAM_HD bool lu_inv6(float* A, float* Inv, float* b) {
   return true;
 }
 
+// acc + x * y in double for float x, y: the double product of two floats is exact (48 significand
+// bits), so one fused multiply-add rounds exactly like the separate multiply and add (half the fp64
+// instructions of the normal-equation sums, bit-identical)
+LOAM_D double dmac(double acc, float x, float y) { return __builtin_fma((double)x, (double)y, acc); }
+
 // C[m x n] = A[m x k] B[k x n], products and sums in double, one rounding (OpenCV CV_32F gemm)
 LOAM_HD void gemm_d(const float* A, const float* B, int m, int k, int n, float* C) {
   for (int i = 0; i < m; ++i)

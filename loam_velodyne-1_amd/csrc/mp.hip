@@ -690,6 +690,8 @@ constexpr int kMpQueryThreads = 256;
 // k_mp_nn workgroup size (measured k_mp_nn ms/step at batch 1024: 64 -> 3.83, 128 -> 3.81-3.86,
 // 256 -> 3.92-3.95): a workgroup's LDS is released when its slowest lane is done
 constexpr int kMpNnThreads = 128;
+// k_mp_fit workgroup size (ms/step at batch 1024: 256 -> 1.27-1.29, 128 -> 1.16-1.20, 64 -> 1.17)
+constexpr int kMpFitThreads = 64;
 
 // The same search with the lane's work flattened: first every cell the lane may need (box
 // distance below 1 m and not above the seeded 5th distance) is listed with its bucket range — 27
@@ -977,9 +979,9 @@ LOAM_D void mp_row_accum(const MpTrig& tg, float4 o, float4 c, double (&acc)[28]
 #pragma unroll
   for (int i = 0; i < 6; ++i)
 #pragma unroll
-    for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
+    for (int jj = i; jj < 6; ++jj) { acc[k] = loamla::dmac(acc[k], a[i], a[jj]); ++k; }
 #pragma unroll
-  for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
+  for (int i = 0; i < 6; ++i) acc[21 + i] = loamla::dmac(acc[21 + i], a[i], bb);
   acc[27] += 1.0;
 }
 
@@ -1064,7 +1066,7 @@ __global__ __launch_bounds__(kMpNnThreads) __attribute__((amdgpu_waves_per_eu(5)
   }
 }
 
-__global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
+__global__ __launch_bounds__(kMpFitThreads) void k_mp_fit(MpBuffers b) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, tid = threadIdx.x;
   int* ist = b.istate + (size_t)p * kMpStateInts;
@@ -1072,7 +1074,7 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
   const bool first = ist[kMiIters] == 0;  // fits of an earlier frame are stale
   // per-lane 3x3 Jacobi scratch (27 words; the odd stride keeps lanes on distinct banks): 27 KB,
   // five workgroups per CU (33-word rows allowed four; measured 1.56 -> 1.40 ms per step)
-  __shared__ float jac[kMpQueryThreads][27];
+  __shared__ float jac[kMpFitThreads][27];
   const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
   const int nq = nsc + nss;
   const float4* stack = b.stack + (size_t)p * b.cap_stack;
@@ -1082,7 +1084,7 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_fit(MpBuffers b) {
   const loampose::MapRot r = rot_load(b, p);
   float* jw = jac[tid];
   int nfits = 0;
-  for (int q = blk.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
+  for (int q = blk.x * kMpFitThreads + tid; q < nq; q += gridDim.x * kMpFitThreads) {
     const bool corner = q < nsc;
     const int4 n0 = qnn[2 * q], n1 = qnn[2 * q + 1];
     float4 sel = make_float4(0, 0, 0, 0);
@@ -1163,7 +1165,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
-      for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
+      for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];  // (dmac measured slower here)
 #pragma unroll
     for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
     acc[27] += 1.0;
@@ -1804,7 +1806,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     if (prof) hipLaunchKernelGGL(k_mp_nn<true>, dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
     else hipLaunchKernelGGL(k_mp_nn<false>, dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
     mark("k_mp_nn");
-    hipLaunchKernelGGL(k_mp_fit, dim3(gq, P), dim3(kMpQueryThreads), 0, st, b);
+    hipLaunchKernelGGL(k_mp_fit, dim3(gq * (kMpQueryThreads / kMpFitThreads), P), dim3(kMpFitThreads), 0, st, b);
     mark("k_mp_fit");
     hipLaunchKernelGGL(k_mp_iter, dim3(P), dim3(kMpThreads), 0, st, b);
     mark("k_mp_iter");

@@ -793,9 +793,9 @@ LOAM_D void od_row_accum(const OdJf& e, float4 c4, bool okit, double (&acc)[28])
 #pragma unroll
   for (int i = 0; i < 6; ++i)
 #pragma unroll
-    for (int jj = i; jj < 6; ++jj) acc[k++] += (double)a[i] * (double)a[jj];
+    for (int jj = i; jj < 6; ++jj) { acc[k] = loamla::dmac(acc[k], a[i], a[jj]); ++k; }
 #pragma unroll
-  for (int i = 0; i < 6; ++i) acc[21 + i] += (double)a[i] * (double)bb;
+  for (int i = 0; i < 6; ++i) acc[21 + i] = loamla::dmac(acc[21 + i], a[i], bb);
   acc[27] += okit ? 1.0 : 0.0;
 }
 
@@ -1138,7 +1138,7 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
     if (it % 5 == 0) {  // Q10
       // one wave per query when the batch is small (streaming: TransformToStart in the wave), 64
       // waves per problem otherwise (the queries transformed by k_od_sel first)
-      const int ga = P >= 64 ? 16 : (b.cap_q + kOdWaves - 1) / kOdWaves;
+      const int ga = P >= 64 ? 16 : (b.cap_q + kOdWaves - 1) / kOdWaves;  // (8 / 32 / 64 measured slower)
       if (P >= 64) {
         hipLaunchKernelGGL(k_od_sel, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f);
         if (prof) hipLaunchKernelGGL((k_od_assoc<true, false>), dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
