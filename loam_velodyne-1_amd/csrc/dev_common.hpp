@@ -33,6 +33,13 @@ namespace loamdev {
 constexpr int kWave = 64;
 
 LOAM_HD double D(float x) { return (double)x; }
+// two consecutive ints (4-byte aligned) as one 8-byte load: one address per lane for the gather
+// unit instead of two (hash bucket ranges start[h], start[h + 1])
+struct __attribute__((aligned(4))) IntPair4 { int x, y; };
+LOAM_D int2 load_pair(const int* p) {
+  const IntPair4 v = *reinterpret_cast<const IntPair4*>(p);
+  return make_int2(v.x, v.y);
+}
 LOAM_HD double dsin(float x) { return sin((double)x); }
 LOAM_HD double dcos(float x) { return cos((double)x); }
 // sin and cos of one float argument in double; on the device one ocml sincos (the same argument

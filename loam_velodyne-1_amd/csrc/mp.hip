@@ -719,7 +719,8 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
     const float bd = sqdist(gx, gy, gz, 0.0f, 0.0f, 0.0f);
     if (bd < 1.0f && bd <= bound) {
       const uint32_t h = cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1);
-      const int b0 = start[h], cnt = start[h + 1] - b0;
+      const int2 rg = load_pair(start + h);  // start[h], start[h + 1]: one 8-byte request
+      const int b0 = rg.x, cnt = rg.y - b0;
       LOAM_CHECK(b0 >= 0 && cnt >= 0, b0, cnt);
       if (cnt > 0) {
         if (b0 >= (1 << 19) || cnt >= (1 << 13)) fits = false;

@@ -310,8 +310,9 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
     const float bd = box_d2(lo, hi, q);
     if (h != 1.0f || (bd < 1.0f && bd <= bound)) {
       bucket = (int)(cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1));
-      b0 = start[bucket];
-      cnt = start[bucket + 1] - b0;
+      const int2 rg = load_pair(start + bucket);
+      b0 = rg.x;
+      cnt = rg.y - b0;
       LOAM_CHECK(b0 >= 0 && cnt >= 0 && b0 + cnt <= n, b0, cnt);
     }
   }
