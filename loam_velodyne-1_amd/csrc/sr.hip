@@ -1107,7 +1107,9 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
 // VoxelGrid runs at full workgroup occupancy.  Other sweeps fall to k_sr_select<4096, 1> / <16, 2>
 // exactly as before (sel_big).
 constexpr int kPickCap = 2048;
-constexpr int kPickWaves = 4;
+// rings (waves) per k_sr_pick workgroup: one, so a workgroup's LDS is freed as soon as its own ring's
+// greedy walk ends (k_sr_select ms/step at batch 1024: 4 -> 1.67-1.69, 2 -> 1.66, 1 -> 1.63-1.65)
+constexpr int kPickWaves = 1;
 constexpr int kPickWpe = 4;  // <= 128 VGPRs: four waves per SIMD (the LDS allows four workgroups per CU)
 constexpr int kPickSegRegs = (kPickCap / 6 + 2 + 63) / 64;  // a segment of a <= kPickCap ring, per lane
 
