@@ -30,6 +30,9 @@ namespace {
 
 constexpr int kOdThreads = 256;
 constexpr int kOdWaves = kOdThreads / 64;
+// k_od_assoc: one wave (query) per workgroup, so a finished wave's slot is not held for its
+// workgroup's slowest query (ms/step at batch 1024: 256 threads -> 2.91, 128 -> 2.88, 64 -> 2.82-2.85)
+constexpr int kAsThreads = 64, kAsWaves = kAsThreads / 64;
 
 LOAM_D loampose::Imu load_imu(const float* st) {
   loampose::Imu m;
@@ -580,12 +583,12 @@ __global__ __launch_bounds__(kOdThreads) void k_od_sel(OdBuffers b, FeatView f) 
 // SEL: the wave computes its query's TransformToStart itself (small batches: one launch fewer per
 // association round); otherwise it reads k_od_sel's result
 template <bool COUNT, bool SEL>
-__global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(SEL ? 1 : 8))) void k_od_assoc(OdBuffers b, FeatView f, int last_buf) {
+__global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL ? 1 : 8))) void k_od_assoc(OdBuffers b, FeatView f, int last_buf) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, lane = lane_id(), w = threadIdx.x >> 6;
   const int* ist = b.istate + (size_t)p * kOdStateInts;
   if (!ist[kIsActive] || ist[kIsStop]) return;
-  __shared__ int cells[kOdWaves][64];
+  __shared__ int cells[kAsWaves][64];
   const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
   const float4* sel = b.sel + (size_t)p * b.cap_q;
   const size_t lp = (size_t)last_buf * b.P + p;
@@ -595,7 +598,7 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(SEL 
   int* ind = b.ind + (size_t)p * 3 * b.cap_q;
   int wpts = 0, wbox = 0;  // wave-uniform work counters (loam_stats od_assoc_gathered / _boxes)
   const bool seeded = ist[kIsIters] > 0;  // ind holds this frame's previous round
-  for (int q = blk.x * kOdWaves + w; q < nq; q += gridDim.x * kOdWaves) {
+  for (int q = blk.x * kAsWaves + w; q < nq; q += gridDim.x * kAsWaves) {
     float4 s4;
     if constexpr (SEL) {
       const float* st = b.state + (size_t)p * kOdStateFloats;
@@ -1139,14 +1142,14 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
     if (it % 5 == 0) {  // Q10
       // one wave per query when the batch is small (streaming: TransformToStart in the wave), 64
       // waves per problem otherwise (the queries transformed by k_od_sel first)
-      const int ga = P >= 64 ? 16 : (b.cap_q + kOdWaves - 1) / kOdWaves;  // (8 / 32 / 64 measured slower)
+      const int ga = P >= 64 ? 16 * kOdWaves / kAsWaves : (b.cap_q + kAsWaves - 1) / kAsWaves;  // (8 / 32 / 64 measured slower)
       if (P >= 64) {
         hipLaunchKernelGGL(k_od_sel, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f);
-        if (prof) hipLaunchKernelGGL((k_od_assoc<true, false>), dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
-        else hipLaunchKernelGGL((k_od_assoc<false, false>), dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
+        if (prof) hipLaunchKernelGGL((k_od_assoc<true, false>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
+        else hipLaunchKernelGGL((k_od_assoc<false, false>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
       } else {
-        if (prof) hipLaunchKernelGGL((k_od_assoc<true, true>), dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
-        else hipLaunchKernelGGL((k_od_assoc<false, true>), dim3(ga, P), dim3(kOdThreads), 0, st, b, f, last_buf);
+        if (prof) hipLaunchKernelGGL((k_od_assoc<true, true>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
+        else hipLaunchKernelGGL((k_od_assoc<false, true>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
       }
       mark("k_od_assoc");
     }
