@@ -1,7 +1,7 @@
 """Host logic of the node pipeline (loam_velodyne-1_amd/pipeline.py) with a stand-in engine: every
 node sees its topic in order, mapping gets exactly the frames odometry published, the results equal
 the sequential composition, and a node error is raised without leaving a thread blocked.  The GPU
-parity of the pipeline (three real contexts) is tests/test_gpu_branches.py::test_pipeline_matches_sequential."""
+parity of the pipeline (three real contexts) is tests/test_gpu_branches.py::test_pipeline_matches_oracle."""
 import importlib
 import os
 import sys
