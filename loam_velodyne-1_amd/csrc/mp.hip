@@ -1790,7 +1790,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   hs.pts_off = b.nfrom; hs.pts_off_stride = 2;
   hs.count = b.nfrom + 1; hs.start = b.hS_start; hs.out = b.hS_pts; hs.tsize = b.hS_T;
   if (P <= 4) hs.fill = b.h_fill + (size_t)P * b.tmax;
-  hash_build_pair(hc, hs, P, st);
+  hash_build_pair(hc, hs, P, st, false);
   mark("k_hash_build_map");
   hipLaunchKernelGGL(k_mp_lm_begin, dim3((P + 255) / 256), dim3(256), 0, st, b);
   // workgroups per instance: all the stack's queries at once for a few instances; for large

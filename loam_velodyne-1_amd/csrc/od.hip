@@ -54,9 +54,10 @@ LOAM_D loampose::Imu load_imu(const float* st) {
 // kHashLds buckets, in global memory beyond.
 constexpr int kHashLds = 8192;
 
+
 // counting sort of the cloud's points by bucket; fill = LDS (LDS true) or this cloud's global
 // counters (read back with atomic loads: the counts were made by L2 atomics)
-template <bool LDS>
+template <int NT, bool LDS>
 LOAM_D void hash_sort(const HashJob& j, const float4* pts, int n, int T, int* start, float4* out, int* fill,
                       int* scratch) {
   const int tid = threadIdx.x;
@@ -64,10 +65,10 @@ LOAM_D void hash_sort(const HashJob& j, const float4* pts, int n, int T, int* st
     if constexpr (LDS) return fill[b];
     else return __hip_atomic_load(&fill[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
-  for (int b = tid; b < T; b += 256) fill[b] = 0;
+  for (int b = tid; b < T; b += NT) fill[b] = 0;
   if (!LDS) __threadfence();
   __syncthreads();
-  for (int i = tid; i < n; i += 256) {
+  for (int i = tid; i < n; i += NT) {
     const float4 a = pts[i];
     uint32_t h = cell_hash(cell_of(a.x, j.inv_h), cell_of(a.y, j.inv_h), cell_of(a.z, j.inv_h)) & (T - 1);
     atomicAdd(&fill[h], 1);
@@ -75,12 +76,12 @@ LOAM_D void hash_sort(const HashJob& j, const float4* pts, int n, int T, int* st
   if (!LDS) __threadfence();
   __syncthreads();
   // exclusive scan of fill[0..T) into start: contiguous chunk per thread
-  const int per = (T + 255) / 256;
+  const int per = (T + NT - 1) / NT;
   const int b0 = tid * per, b1 = min(T, b0 + per);
   int local = 0;
   for (int b = b0; b < b1; ++b) local += ld(b);
   int tot;
-  int run = block_excl_scan<256>(local, scratch, tot);
+  int run = block_excl_scan<NT>(local, scratch, tot);
   for (int b = b0; b < b1; ++b) {
     const int c = ld(b);
     start[b] = run;
@@ -91,7 +92,7 @@ LOAM_D void hash_sort(const HashJob& j, const float4* pts, int n, int T, int* st
   if (tid == 0) start[T] = tot;
   if (!LDS) __threadfence();
   __syncthreads();
-  for (int i = tid; i < n; i += 256) {
+  for (int i = tid; i < n; i += NT) {
     const float4 a = pts[i];
     uint32_t h = cell_hash(cell_of(a.x, j.inv_h), cell_of(a.y, j.inv_h), cell_of(a.z, j.inv_h)) & (T - 1);
     int pos = atomicAdd(&fill[h], 1);
@@ -102,25 +103,26 @@ LOAM_D void hash_sort(const HashJob& j, const float4* pts, int n, int T, int* st
   }
 }
 
-__global__ __launch_bounds__(256) void k_hash_build(HashJob j) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_hash_build(HashJob j) {
   const int p = blockIdx.x, tid = threadIdx.x;
   const int n = *(const int*)((const char*)j.count + (size_t)p * j.count_stride_bytes);
   const float4* pts = j.pts + (size_t)p * j.pts_stride + (j.pts_off ? j.pts_off[p * j.pts_off_stride] : 0);
   int* start = j.start + (size_t)p * (j.tmax + 1);
   float4* out = j.out + (size_t)p * j.pts_stride;
-  __shared__ int scratch[16];
+  __shared__ int scratch[NT / 64 + 1];
   __shared__ int lfill[kHashLds];
   const int m = n >> j.shift;
   int T = next_pow2(m > 64 ? m : 64);
   if (T > j.tmax) T = j.tmax;
   if (tid == 0) j.tsize[p] = T;
-  if (T <= kHashLds) hash_sort<true>(j, pts, n, T, start, out, lfill, scratch);
-  else hash_sort<false>(j, pts, n, T, start, out, j.fill + (size_t)p * j.tmax, scratch);
+  if (T <= kHashLds) hash_sort<NT, true>(j, pts, n, T, start, out, lfill, scratch);
+  else hash_sort<NT, false>(j, pts, n, T, start, out, j.fill + (size_t)p * j.tmax, scratch);
   if (j.chunks) {  // one wave per 64-point chunk of the source order
     const int lane = lane_id(), w = tid >> 6;
     const int nch = (n + kChunk - 1) / kChunk;
     float4* ch = j.chunks + (size_t)p * 2 * chunks_of((int)j.pts_stride);
-    for (int c = w; c < nch; c += 4) {
+    for (int c = w; c < nch; c += NT / 64) {
       const int i = c * kChunk + lane;
       float4 a = pts[min(i, n - 1)];
       const float r = (float)(int)a.w;
@@ -266,10 +268,15 @@ __global__ __launch_bounds__(256) void k_hash_scatter(HashPair hp) {
   }
 }
 
-void hash_build_pair(const HashJob& a, const HashJob& b, int P, hipStream_t st) {
+void hash_build_pair(const HashJob& a, const HashJob& b, int P, hipStream_t st, bool wide) {
   if (P > 4) {  // batches: a workgroup per cloud fills the chip
-    hipLaunchKernelGGL(k_hash_build, dim3(P), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(k_hash_build, dim3(P), dim3(256), 0, st, b);
+    if (wide) {
+      hipLaunchKernelGGL(k_hash_build<1024>, dim3(P), dim3(1024), 0, st, a);
+      hipLaunchKernelGGL(k_hash_build<1024>, dim3(P), dim3(1024), 0, st, b);
+    } else {
+      hipLaunchKernelGGL(k_hash_build<512>, dim3(P), dim3(512), 0, st, a);
+      hipLaunchKernelGGL(k_hash_build<512>, dim3(P), dim3(512), 0, st, b);
+    }
     return;
   }
   HashPair hp;
@@ -1128,7 +1135,7 @@ void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
   js.tsize = b.hS_T + buf * b.P;
   js.tmax = b.tS;
   js.chunks = b.cS + (size_t)buf * b.P * 2 * chunks_of(b.capS);
-  hash_build_pair(jc, js, b.P, st);
+  hash_build_pair(jc, js, b.P, st, true);
 }
 
 }  // namespace loam
