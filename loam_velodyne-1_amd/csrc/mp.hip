@@ -1815,8 +1815,8 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   hipLaunchKernelGGL(k_mp_lm_end, dim3((P + 255) / 256), dim3(256), 0, st, b);
   // insertion + per-valid-cube downsampling into the other pool
   // a few instances: 1024 threads per instance (the per-instance serial parts are the cost)
-  if (P <= 4) hipLaunchKernelGGL(k_mp_insert<1024>, dim3(P), dim3(1024), 0, st, b, (int*)b.vg_k, (int*)b.vg_v);
-  else hipLaunchKernelGGL(k_mp_insert<kMpThreads>, dim3(P), dim3(kMpThreads), 0, st, b, (int*)b.vg_k, (int*)b.vg_v);
+  // 1024 threads per instance also for batches (k_mp_insert 0.40 -> 0.25 ms/step at batch 1024 against 256)
+  hipLaunchKernelGGL(k_mp_insert<1024>, dim3(P), dim3(1024), 0, st, b, (int*)b.vg_k, (int*)b.vg_v);
   mark("k_mp_insert");
   hipLaunchKernelGGL(k_mp_vseg, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_vcopy, dim3(32, P), dim3(256), 0, st, b);
@@ -1830,8 +1830,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   jv.err = b.istate + kMiErr; jv.err_stride = kMpStateInts; jv.seg_per_err = 2 * kMaxValid;
   b.note(vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 || kVgCubeG256 ? 256 : 64, P <= 4 || kVgFusedBatch ? kVgCubeCap : 0));  // 2 x 125 cube segments per instance
   mark("vg_cubes");
-  if (P <= 4) hipLaunchKernelGGL(k_mp_compact_table<1024>, dim3(P), dim3(1024), 0, st, b);
-  else hipLaunchKernelGGL(k_mp_compact_table<kMpThreads>, dim3(P), dim3(kMpThreads), 0, st, b);
+  hipLaunchKernelGGL(k_mp_compact_table<1024>, dim3(P), dim3(1024), 0, st, b);
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);
   mark("k_mp_compact");
   if (before_register) before_register();
