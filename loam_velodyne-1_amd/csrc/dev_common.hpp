@@ -40,6 +40,21 @@ LOAM_D int2 load_pair(const int* p) {
   const IntPair4 v = *reinterpret_cast<const IntPair4*>(p);
   return make_int2(v.x, v.y);
 }
+// PCL 1.7.1 VoxelGrid's "leaf size too small" test (output = input when the (int64) voxel count
+// dx·dy·dz of the bbox exceeds INT_MAX), written without PCL's undefined cases: PCL multiplies
+// three int64 extents (overflows for spans beyond ~4·10^5 km at 0.2 m) and converts the scaled
+// bbox corners to int; both count as "too small" here.  Identical to PCL wherever PCL is defined.
+// The oracle restates it (oracle_math.hpp vg_leaf_too_small).
+LOAM_HD bool vg_leaf_too_small(const float* mn, const float* mx, float inv) {
+  int64_t e[3];
+  for (int d = 0; d < 3; ++d) {
+    const float sp = (mx[d] - mn[d]) * inv, lo = mn[d] * inv, hi = mx[d] * inv;
+    if (!(sp < 2147483648.0f) || !(lo >= -2147483648.0f) || !(hi < 2147483648.0f)) return true;
+    e[d] = (int64_t)sp + 1;
+  }
+  const int64_t xy = e[0] * e[1];  // each factor <= 2^31: no overflow
+  return xy > (int64_t)0x7fffffff || xy * e[2] > (int64_t)0x7fffffff;
+}
 LOAM_HD double dsin(float x) { return sin((double)x); }
 LOAM_HD double dcos(float x) { return cos((double)x); }
 // sin and cos of one float argument in double; on the device one ocml sincos (the same argument

@@ -287,18 +287,17 @@ __global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_params(VgJob j) {
     }
     if (grp.t == 0) {
       const float inv = 1.0f / j.leaf[s];
-      const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
-      const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
-      const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
-      int minb[3], maxb[3];
-      for (int d = 0; d < 3; ++d) {
-        minb[d] = (int)floorf(mn[d] * inv);
-        maxb[d] = (int)floorf(mx[d] * inv);
-      }
+      const bool too_small = vg_leaf_too_small(mn, mx, inv);
+      int minb[3] = {0, 0, 0}, maxb[3] = {0, 0, 0};
+      if (!too_small)
+        for (int d = 0; d < 3; ++d) {
+          minb[d] = (int)floorf(mn[d] * inv);
+          maxb[d] = (int)floorf(mx[d] * inv);
+        }
       const int divx = maxb[0] - minb[0] + 1, divy = maxb[1] - minb[1] + 1;
       prm[0] = minb[0]; prm[1] = minb[1]; prm[2] = minb[2];
       prm[3] = divx; prm[4] = divx * divy;
-      prm[5] = (dx * dy * dz > (int64_t)0x7fffffff) ? 1 : 0;
+      prm[5] = too_small ? 1 : 0;
       const int64_t divz = (int64_t)(maxb[2] - minb[2] + 1);
       if (!prm[5] && j.end_bit < 32 && (int64_t)divx * divy * divz > ((int64_t)1 << j.end_bit) && j.err)
         atomicOr(&j.err[(s / j.seg_per_err) * j.err_stride], ERR_VG_BITS);
@@ -449,10 +448,7 @@ __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
       mx[d] = block_reduce<NT>(mx[d], fsc, [](float a, float c) { return fmaxf(a, c); });
     }
     const float inv = 1.0f / j.leaf[s];
-    const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
-    const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
-    const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
-    if (dx * dy * dz > (int64_t)0x7fffffff) {  // "leaf size too small": output = input
+    if (vg_leaf_too_small(mn, mx, inv)) {  // "leaf size too small": output = input
       for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
       if (tid == 0) j.out_count[s] = n;
       continue;

@@ -598,10 +598,7 @@ LOAM_D int ring_vg(const float4* pts, int lo, const CandT* cand, int nc, uint64_
   int nout = 0;
   if (nc > 0) {
     const float inv = 1.0f / 0.2f;
-    const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
-    const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
-    const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
-    if (dx * dy * dz > (int64_t)0x7fffffff) {  // "leaf size too small": output = input
+    if (vg_leaf_too_small(mn, mx, inv)) {  // "leaf size too small": output = input
       for (int t = tid; t < nc; t += kSelThreads)
         if (t < outcap) outp[t] = pts[lo + cand[t]];
       nout = nc;

@@ -28,7 +28,7 @@ SIGMA = 0.01                # range noise (m)
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "synth", "libloam_synth.so")
+        path = os.environ.get("LOAM_SYNTH_LIB") or os.path.join(_HERE, "synth", "libloam_synth.so")
         if not os.path.exists(path):
             raise RuntimeError("libloam_synth.so not built (run __graft_entry__.build())")
         L = ctypes.CDLL(path)

@@ -662,8 +662,8 @@ void od_lm(const Cfg& cfg, OdState& s, const std::vector<P>& sharp, const std::v
       ind3s(surfPointsFlatNum, -1);
   std::vector<P> cloudOri, coeffSel;  // cleared once per frame (:458-459): rows accumulate (Q12)
   std::vector<int> nanIdx;
-  int nnI[1];
-  float nnD[1];
+  int nnI[2];  // k = 1 results (one spare slot keeps -Warray-bounds provable)
+  float nnD[2];
   const std::vector<P>& CL = s.cornerLast;
   const std::vector<P>& SL = s.surfLast;
   for (int iterCount = 0; iterCount < cfg.od_max_iter; ++iterCount) {
@@ -683,7 +683,11 @@ void od_lm(const Cfg& cfg, OdState& s, const std::vector<P>& sharp, const std::v
           closestPointInd = nnI[0];
           int closestPointScan = (int)CL[closestPointInd].intensity;
           float minPointSqDis2 = 25;
-          for (int j = closestPointInd + 1; j < cornerPointsSharpNum; ++j) {  // Q11 bound
+          // Q11: the reference bounds the forward window by this sweep's cornerPointsSharpNum
+          // (:486), reading past CornerLast when that exceeds it (UB).  Defined here, as in the
+          // engine (od.hip k_od_assoc), as min(cornerPointsSharpNum, |CornerLast|).
+          const int fwdEnd = std::min(cornerPointsSharpNum, (int)CL.size());
+          for (int j = closestPointInd + 1; j < fwdEnd; ++j) {
             if (D((int)CL[j].intensity) > closestPointScan + 2.5) break;
             float pointSqDis = (CL[j].x - pointSel.x) * (CL[j].x - pointSel.x) +
                                (CL[j].y - pointSel.y) * (CL[j].y - pointSel.y) +
@@ -750,7 +754,9 @@ void od_lm(const Cfg& cfg, OdState& s, const std::vector<P>& sharp, const std::v
           closestPointInd = nnI[0];
           int closestPointScan = (int)SL[closestPointInd].intensity;
           float minPointSqDis2 = 25, minPointSqDis3 = 25;
-          for (int j = closestPointInd + 1; j < surfPointsFlatNum; ++j) {  // Q11 bound
+          // Q11 (:598): same clamp, min(surfPointsFlatNum, |SurfLast|)
+          const int fwdEnd = std::min(surfPointsFlatNum, (int)SL.size());
+          for (int j = closestPointInd + 1; j < fwdEnd; ++j) {
             if (D((int)SL[j].intensity) > closestPointScan + 2.5) break;
             float pointSqDis = (SL[j].x - pointSel.x) * (SL[j].x - pointSel.x) +
                                (SL[j].y - pointSel.y) * (SL[j].y - pointSel.y) +

@@ -67,7 +67,8 @@ class Stats(ctypes.Structure):
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "liboracle.so")
+        # LOAM_ORACLE_LIB: the sanitizer build (make -C oracle asan -> liboracle_asan.so)
+        path = os.environ.get("LOAM_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
         if not os.path.exists(path):
             raise RuntimeError("oracle/liboracle.so not built (make -C oracle)")
         L = ctypes.CDLL(path)

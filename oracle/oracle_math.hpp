@@ -143,6 +143,20 @@ class KdTree {
 };
 
 // ---------------------------------------------------------------- PCL VoxelGrid
+// PCL's overflow test: (int64)((max-min)*inv)+1 per axis, product > INT_MAX -> output = input.
+// PCL's own product (and its int conversion of the scaled bbox) is undefined for spans beyond
+// int range; those cases are defined here as "too small" too (same rule as the engine).
+inline bool vg_leaf_too_small(const float* mn, const float* mx, float inv) {
+  int64_t e[3];
+  for (int d = 0; d < 3; ++d) {
+    const float sp = (mx[d] - mn[d]) * inv, lo = mn[d] * inv, hi = mx[d] * inv;
+    if (!(sp < 2147483648.0f) || !(lo >= -2147483648.0f) || !(hi < 2147483648.0f)) return true;
+    e[d] = (int64_t)sp + 1;
+  }
+  const int64_t xy = e[0] * e[1];
+  return xy > (int64_t)INT32_MAX || xy * e[2] > (int64_t)INT32_MAX;
+}
+
 inline void voxel_grid(const std::vector<P>& in, float leaf, std::vector<P>& out) {
   out.clear();
   if (in.empty()) return;
@@ -152,10 +166,7 @@ inline void voxel_grid(const std::vector<P>& in, float leaf, std::vector<P>& out
     const float c[3] = {p.x, p.y, p.z};
     for (int d = 0; d < 3; ++d) { mn[d] = std::min(mn[d], c[d]); mx[d] = std::max(mx[d], c[d]); }
   }
-  int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
-  int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
-  int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
-  if (dx * dy * dz > (int64_t)INT32_MAX) {  // "Leaf size is too small": output = input
+  if (vg_leaf_too_small(mn, mx, inv)) {  // "Leaf size is too small": output = input
     out = in;
     return;
   }

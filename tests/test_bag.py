@@ -130,3 +130,71 @@ def test_replay_matches_array_path(rb, loam, sg, tmp_path):
     assert len(got["odometry"]) == len(odo) > 5 and len(got["mapping"]) == len(mapped) > 2
     np.testing.assert_array_equal(np.array([p for _, p in got["odometry"]]), np.array(odo))
     np.testing.assert_array_equal(np.array([p for _, p in got["mapping"]]), np.array(mapped))
+
+
+def _mutations(data, rng, n):
+    """n corrupted copies of a byte string: bit flips, overwritten 32-bit length fields, truncations,
+    inserted / deleted ranges (the reader parses untrusted bytes: it must fail with an error code,
+    never read out of bounds — tools/asan_suite.sh runs this under AddressSanitizer)."""
+    out = []
+    for _ in range(n):
+        b = bytearray(data)
+        kind = rng.integers(5)
+        if kind == 0:
+            for _ in range(rng.integers(1, 8)):
+                b[rng.integers(len(b))] ^= 1 << rng.integers(8)
+        elif kind == 1:
+            at = int(rng.integers(0, len(b) - 4))
+            v = int(rng.choice([0, 1, 0x7fffffff, 0xffffffff, len(b), int(rng.integers(0, 1 << 32))]))
+            b[at:at + 4] = v.to_bytes(4, "little")
+        elif kind == 2:
+            b = b[:int(rng.integers(0, len(b)))]
+        elif kind == 3:
+            at = int(rng.integers(0, len(b)))
+            b[at:at] = bytes(rng.integers(0, 256, int(rng.integers(1, 64)), dtype=np.uint8))
+        else:
+            at = int(rng.integers(0, len(b)))
+            del b[at:at + int(rng.integers(1, 64))]
+        out.append(bytes(b))
+    return out
+
+
+@pytest.mark.parametrize("comp", ["none", "bz2", "lz4"])
+def test_bag_fuzz_no_crash(rb, loam, tmp_path, comp):
+    path = tmp_path / "f.bag"
+    msgs = _messages()[:14]
+    bw.write_bag(path, msgs, chunk_messages=5, compression=comp)
+    rng = np.random.default_rng({"none": 1, "bz2": 2, "lz4": 3}[comp])
+    ok = bad = 0
+    for k, b in enumerate(_mutations(path.read_bytes(), rng, 150)):
+        q = tmp_path / f"m{k}.bag"
+        q.write_bytes(b)
+        try:
+            for _topic, ty, _s, payload in rb.Bag(q):
+                try:
+                    if ty == "sensor_msgs/PointCloud2":
+                        rb.parse_pc2(payload)
+                    elif ty == "sensor_msgs/Imu":
+                        rb.parse_imu(payload)
+                except loam.LoamError:
+                    pass
+            ok += 1
+        except loam.LoamError:
+            bad += 1
+    assert ok + bad == 150 and bad > 0
+
+
+def test_pointcloud2_fuzz_no_crash(rb, loam):
+    rng = np.random.default_rng(7)
+    base = bw.pointcloud2(_cloud(8, n=64, nan=3), 2.0, seq=3)
+    for m in _mutations(base, rng, 400) + _mutations(bw.pointcloud2(_cloud(9, n=40), 1.0, layout="shuffled"), rng, 200):
+        try:
+            _, pts, pc = rb.parse_pc2(m)
+            assert pts.shape[0] == pc.width * pc.height
+        except loam.LoamError:
+            pass
+    for m in _mutations(bw.imu(3.5, [0.1, -0.2, 0.3, 0.9], [1.0, 9.8, -0.5]), rng, 200):
+        try:
+            rb.parse_imu(m)
+        except loam.LoamError:
+            pass
