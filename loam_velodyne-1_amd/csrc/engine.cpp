@@ -217,6 +217,8 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   for (auto& e : x->ev)
     if (he == hipSuccess) he = hipEventCreate(&e);
   if (he == hipSuccess && hipStreamCreateWithFlags(&x->st2, hipStreamNonBlocking) != hipSuccess) x->st2 = nullptr;
+  x->pin.streams[0] = x->st;
+  x->pin.streams[1] = x->st2;
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->fork, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->join, hipEventDisableTiming);
   if (he != hipSuccess) {
@@ -276,20 +278,21 @@ int loam_set_stream_priority(loam_ctx* x, int priority) {
   int least = 0, greatest = 0;  // HIP: a numerically lower value is a higher priority
   HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
   const int prio = priority > 0 ? greatest : priority < 0 ? least : 0;
+  // drain the old streams first: a failure here leaves the context on its old streams, unchanged
+  HIP_TRY(hipStreamSynchronize(x->st));
+  if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
   hipStream_t st = nullptr, st2 = nullptr;
   HIP_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio));
   if (hipStreamCreateWithPriority(&st2, hipStreamNonBlocking, prio) != hipSuccess) {
     (void)hipStreamDestroy(st);
-    return fail(LOAM_E_HIP, "hipStreamCreateWithPriority failed");
+    return fail(LOAM_E_HIP, "hipStreamCreateWithPriority failed (context keeps its old streams)");
   }
-  HIP_TRY(hipStreamSynchronize(x->st));
-  if (x->st2) {
-    HIP_TRY(hipStreamSynchronize(x->st2));
-    (void)hipStreamDestroy(x->st2);
-  }
+  if (x->st2) (void)hipStreamDestroy(x->st2);
   (void)hipStreamDestroy(x->st);
   x->st = st;
   x->st2 = st2;
+  x->pin.streams[0] = st;
+  x->pin.streams[1] = st2;
   return LOAM_OK;
 }
 
@@ -354,7 +357,8 @@ int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_fe
   // /velodyne_cloud_2 is final once the rings are sorted: its n (>= the kept points) points come
   // down on the second stream, and reach the caller's buffer on the host, while the curvature /
   // pick / VoxelGrid kernels run
-  const bool early = x->st2 != nullptr && n > 0;
+  // (only when the caller's buffer holds all n points: nfull <= n can then not fail on capacity)
+  const bool early = x->st2 != nullptr && n > 0 && out->full.pts && (uint32_t)n <= out->full.capacity;
   sr_launch(b, prm, x->st, nullptr, early ? x->fork : nullptr);
   HIP_TRY(hipEventRecord(x->ev[1], x->st));
   HIP_TRY(hipGetLastError());
@@ -369,15 +373,18 @@ int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_fe
   HIP_TRY(hipMemcpyAsync(&mi[1], b.cnt, 4 * sizeof(int), hipMemcpyDeviceToHost, x->st));
   HIP_TRY(hipMemcpyAsync(&mi[5], b.n_full, sizeof(int), hipMemcpyDeviceToHost, x->st));
   HIP_TRY(hipMemcpyAsync(&mi[6], b.err, sizeof(int), hipMemcpyDeviceToHost, x->st));
-  if (early) {  // (points past the kept count land in the caller's spare capacity only)
-    HIP_TRY(hipEventSynchronize(x->join));
-    if (out->full.pts) std::memcpy(out->full.pts, pfull, (size_t)std::min<uint32_t>((uint32_t)n, out->full.capacity) * sizeof(float4));
-  }
   HIP_TRY(hipStreamSynchronize(x->st));
   int cnt[4] = {mi[1], mi[2], mi[3], mi[4]};
   const int nfull = mi[5];
   rc = sr_errors(mi[6]);
-  if (rc) return rc;
+  if (rc) {
+    if (early) HIP_TRY(hipEventSynchronize(x->join));  // the arena is reused by the next call
+    return rc;  // (nothing written to the caller's buffers)
+  }
+  if (early) {
+    HIP_TRY(hipEventSynchronize(x->join));
+    std::memcpy(out->full.pts, pfull, (size_t)nfull * sizeof(float4));
+  }
   int e = 0;
   x->pin.reset();
   if (early) {
@@ -505,6 +512,10 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
     m.veloX = q[9]; m.veloY = q[10]; m.veloZ = q[11];
     loampose::accumulate_pose(st, m, x->od_sum);
     ist[kIsQueries] = ist[kIsAssoc] * (cnt[0] + cnt[2]);
+    // keep the device copy of transformSum current (it is seeded only on the init frame): the
+    // host result goes back from the pinned state block, ordered before the next frame's kernels
+    std::memcpy(st + kOdSum, x->od_sum, sizeof(loam_pose6));
+    HIP_TRY(hipMemcpyAsync(o.state + kOdSum, st + kOdSum, sizeof(loam_pose6), hipMemcpyHostToDevice, x->st));
   }
   if (sum_out) std::memcpy(sum_out, x->od_sum, sizeof(loam_pose6));
   *published = LOAM_PUB_POSE;

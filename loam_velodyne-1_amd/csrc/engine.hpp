@@ -106,9 +106,14 @@ struct Staging {
   };
   Pending out[8];
   int nout = 0;
+  // the context's streams: any of them may still hold DMAs from the arena, so growing it (a free
+  // of the old buffer) drains all of them, not only the caller's (loam_create / set_stream_priority)
+  hipStream_t streams[2] = {nullptr, nullptr};
   hipError_t reserve(size_t n, hipStream_t st) {  // room for n float4 from off
     if (off + n <= cap) return hipSuccess;
     hipError_t e = hipStreamSynchronize(st);
+    for (hipStream_t s : streams)
+      if (e == hipSuccess && s && s != st) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
     finish();
     size_t want = (off + n) * 2;

@@ -1240,9 +1240,13 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
   __shared__ double tot[28];
   __shared__ MpStepScratch sh;
   __syncthreads();
-  if (tid == 0) sh_last = atomicAdd(&b.done[p], 1) == G - 1;
+  // the done counter is an agent-scope acq_rel RMW, and the last workgroup's threads acquire at
+  // agent scope before reading the other workgroups' partials (they may sit on other XCDs)
+  if (tid == 0)
+    sh_last = __hip_atomic_fetch_add(&b.done[p], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
   __syncthreads();
   if (!sh_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (tid < 8 * 28) {  // fixed-order sum: slice s holds partials s, s + 8, ... (all in flight)
     const int v = tid % 28, sl = tid / 28;
     const double* pp = b.part + (size_t)p * kMpSmallGrid * 28 + v;

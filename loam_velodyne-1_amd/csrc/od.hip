@@ -937,9 +937,13 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows_small(OdBuffers b, FeatV
   __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs], jE[6], jV[36];
   __shared__ int lm_iws[12];
   __syncthreads();
-  if (tid == 0) sh_last = atomicAdd(&b.done[p], 1) == G - 1;
+  // the done counter is an agent-scope acq_rel RMW, and the last workgroup's threads acquire at
+  // agent scope before reading the other workgroups' partials (they may sit on other XCDs)
+  if (tid == 0)
+    sh_last = __hip_atomic_fetch_add(&b.done[p], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
   __syncthreads();
   if (!sh_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // fixed-order sum of the G partials: thread (slice s, value v) sums partials s, s + 8, ... with
   // all its loads in flight at once, then the eight slice sums are added in slice order
   __shared__ double slice[8][28];

@@ -300,9 +300,22 @@ LOAM_HD float4 point_to_tobe_mapped(const MapRot& r, float4 pi) {
 }
 
 // tf::Quaternion::setRPY and tf::Matrix3x3::getRPY (double)
+// (sin and cos of one angle come from one sincos call: GCC -O2 and above merges the pair in tf's
+// inlined setRPY, and glibc >= 2.28's sincos differs from separate sin / cos in the last bit of
+// ~0.1 % of doubles — the message quaternion is published in double, so that bit is visible)
+LOAM_HD void sincos_pair(double x, double& s, double& c) {
+#ifdef __HIP_DEVICE_COMPILE__
+  sincos(x, &s, &c);
+#else
+  ::sincos(x, &s, &c);
+#endif
+}
 LOAM_HD void quat_from_rpy(double roll, double pitch, double yaw, double* q) {
   double hy = yaw * 0.5, hp = pitch * 0.5, hr = roll * 0.5;
-  double cy = cos(hy), sy = sin(hy), cp = cos(hp), sp = sin(hp), cr = cos(hr), sr = sin(hr);
+  double cy, sy, cp, sp, cr, sr;
+  sincos_pair(hy, sy, cy);
+  sincos_pair(hp, sp, cp);
+  sincos_pair(hr, sr, cr);
   q[0] = sr * cp * cy - cr * sp * sy;
   q[1] = cr * sp * cy + sr * cp * sy;
   q[2] = cr * cp * sy - sr * sp * cy;

@@ -6,6 +6,8 @@
   * ground-only sweeps (a single plane): the iteration-0 degeneracy projection fires in odometry
     (eigenvalue < 10, src/laserOdometry.cpp:770-797) and in mapping (< 100,
     src/laserMapping.cpp:927-954)
+  * Last clouds smaller than the next sweep's sharp / flat counts: the Q11 forward window
+    (src/laserOdometry.cpp:486, :598) runs to the end of CornerLast / SurfLast
   * a corner pair at one position on two rings in the Last cloud: point-to-line with l12 = 0 gives
     NaN coefficients that pass `s > 0.1 && ld2 != 0` at iterations < 5, so the NaN guard
     (src/laserOdometry.cpp:799-811, Q16) skips every update of that frame
@@ -40,7 +42,20 @@ def duplicate_corners(less_sharp, n_sharp, every=4, count=10):
     return np.array(rows, np.float32).reshape(-1, 4), len(sel)
 
 
-def run_stream(impl, sweeps, *, mapping=True, jumps=None, inject_nan_at=None, stats=True):
+def truncate_last(f, n_corner=14, n_surf=120):
+    """keep only the last n_corner lessSharp / n_surf lessFlat points (the highest rings): the next
+    sweep's CornerLast / SurfLast are then smaller than its sharp / flat counts (still above the
+    L-M gate 10 / 100, src/laserOdometry.cpp:465), so the forward ring windows of Q11, bounded by
+    cornerPointsSharpNum / surfPointsFlatNum (:486, :598), run past the Last clouds' ends — the
+    reference reads beyond the vector there; engine and oracle both clamp at |Last|"""
+    f = dict(f)
+    f["less_sharp"] = np.ascontiguousarray(f["less_sharp"][-n_corner:])
+    f["less_flat"] = np.ascontiguousarray(f["less_flat"][-n_surf:])
+    return f
+
+
+def run_stream(impl, sweeps, *, mapping=True, jumps=None, inject_nan_at=None, truncate_last_at=(),
+               stats=True):
     """scan registration -> odometry -> mapping over `sweeps` with the scenario hooks; returns one
     record per odometry call: published flags, pose, the three odometry clouds, and on mapping
     frames aft / bef / registered / surround plus the branch counters"""
@@ -53,8 +68,12 @@ def run_stream(impl, sweeps, *, mapping=True, jumps=None, inject_nan_at=None, st
         if inject_nan_at is not None and k == inject_nan_at:
             f = dict(f)
             f["less_sharp"], _ = duplicate_corners(f["less_sharp"], f["sharp"].shape[0])
+        if k in truncate_last_at:
+            f = truncate_last(f)
         pub, pose, cl, sl, full = impl.odometry(f, stamp=0.1 * k)
-        rec = {"k": k, "pub": pub, "pose": pose, "corner_last": cl, "surf_last": sl, "full_end": full}
+        rec = {"k": k, "pub": pub, "pose": pose, "corner_last": cl, "surf_last": sl, "full_end": full,
+               "n_sharp": int(f["sharp"].shape[0]), "n_flat": int(f["flat"].shape[0]),
+               "n_less_sharp": int(f["less_sharp"].shape[0]), "n_less_flat": int(f["less_flat"].shape[0])}
         if stats:
             s = impl.stats()
             rec["od_deg"], rec["od_nan"] = s["od_degenerate_steps"], s["od_nan_skips"]

@@ -106,3 +106,53 @@ def check_imu_traj(traj, tol=0.0):
 
 def test_config3_imu_oracle(oc, sg):
     check_imu_traj(_imu_stream(oc.Oracle(oc.default_config(system_delay=2)), sg))
+
+
+def config3_full_records(impl, sg, n_sweeps=220):
+    """bench.py's config-3 leg (seed 1, 220 sweeps, default configuration) through one node chain"""
+    sweeps = sg.stream_sweeps(n_sweeps, 1)
+    traj = []
+    for k, sw in enumerate(sweeps):
+        rc, f = impl.scan_registration(sw, stamp=0.1 * k)
+        if rc:
+            continue
+        pub, pose, cl, sl, full = impl.odometry(f, stamp=0.1 * k)
+        rec = {"k": k, "pub": pub, "od": pose}
+        if pub == 7:
+            a, b, reg = impl.mapping(pose, cl, sl, full, stamp=0.1 * k)
+            rec.update(aft=a, bef=b, reg_n=int(reg.shape[0]), reg=digest(reg))
+        traj.append(rec)
+    return traj
+
+
+def check_config3_full(traj, tol=0.0):
+    """every record of the 220-sweep run against the golden: poses within tol (0: bit-exact), the
+    registered cloud's digest on every mapping frame"""
+    g = G["config3_full220"]
+    assert len(traj) == len(g) == 200
+    nmap = 0
+    for r, e in zip(traj, g):
+        assert (r["k"], r["pub"]) == (e["k"], e["pub"]), (r["k"], e["k"])
+        assert np.abs(r["od"] - np.float32(e["od_sum"])).max() <= tol, (r["k"], r["od"], e["od_sum"])
+        assert ("aft" in r) == ("aft" in e), r["k"]
+        if "aft" in e:
+            nmap += 1
+            assert np.abs(r["aft"] - np.float32(e["aft"])).max() <= tol, (r["k"], r["aft"], e["aft"])
+            assert np.abs(r["bef"] - np.float32(e["bef"])).max() <= tol, r["k"]
+            assert r["reg_n"] == e["registered_count"] and r["reg"] == e["registered_sha256"], r["k"]
+    assert nmap == 100
+
+
+def test_config3_full220_oracle(oc, sg):
+    check_config3_full(config3_full_records(oc.Oracle(oc.default_config()), sg))
+
+
+def test_config5_iters_100_20_oracle(oc, sg):
+    hp, hc = sg.single_problem(2, lidar=sg.HDL64)
+    cfg = oc.default_config(n_rings=64, ring_model=1, max_points=160000, od_max_iter=100, mp_max_iter=20)
+    od, aft, st = oc.problem(hp, hc, cfg)
+    e = G["config5_problem_100_20"]
+    np.testing.assert_array_equal(od, np.float32(e["od_sum"]))
+    np.testing.assert_array_equal(aft, np.float32(e["aft"]))
+    assert (st["od_iters"], st["mp_iters"]) == (e["od_iters"], e["mp_iters"])
+    assert e["od_iters"] > 25   # the 100-iteration cap is what this config exercises

@@ -118,6 +118,19 @@ def test_nan_guard_parity(loam, oc, sg):
     assert len(hit) == 1 and hit[0]["od_nan"] == 25
 
 
+def test_q11_window_clamp_parity(loam, oc, sg):
+    """CornerLast / SurfLast smaller than the next sweep's sharp / flat counts (scenarios.truncate_last):
+    the forward windows run to the ends of the Last clouds, where engine and oracle both stop at
+    min(count, |Last|) (Q11, src/laserOdometry.cpp:486, :598)"""
+    rg, ro = _both(loam, oc, sg.stream_sweeps(12, 1), truncate_last_at=(4, 7))
+    _compare_streams(rg, ro)
+    by_k = {r["k"]: r for r in rg}
+    for k in (4, 7):
+        assert by_k[k + 1]["n_sharp"] > by_k[k]["n_less_sharp"] == 14
+        assert by_k[k + 1]["n_flat"] > by_k[k]["n_less_flat"] == 120
+        assert by_k[k + 1]["od_iters"] > 0
+
+
 @pytest.mark.parametrize("skip", [0, 2])
 def test_skip_frame_num_parity(loam, oc, sg, skip):
     rg, ro = _both(loam, oc, sg.stream_sweeps(12, 1), {"skip_frame_num": skip})

@@ -3,7 +3,8 @@ orientation = (-q.y, -q.z, q.x, q.w) of createQuaternionMsgFromRollPitchYaw(rz, 
 (src/laserOdometry.cpp:858-866, src/laserMapping.cpp:1071-1080, src/transformMaintenance.cpp:163-171),
 transformBefMapped in the twist fields (src/laserMapping.cpp:1082-1087), and the handlers' read-back
 (src/laserMapping.cpp:304-321, src/transformMaintenance.cpp:147-160,182-203).  Checked bit for bit
-against the oracle's restatement of the same tf algebra."""
+against the oracle's restatement of the same tf algebra.  (Thousands of poses: a quaternion
+built from separate sin / cos instead of the sincos pair GCC emits differs in ~0.4 % of them.)"""
 import ctypes
 
 import numpy as np
@@ -35,7 +36,7 @@ def _oracle_round_trip(oc, p):
 @pytest.mark.parametrize("kind", [0, 1, 2])
 def test_msg_from_pose_matches_oracle(loam, oc, kind):
     frames = {0: b"/laser_odom", 1: b"/aft_mapped", 2: b"/camera"}
-    for p in _poses(200):
+    for p in _poses(4000):
         bef = p[::-1].copy()
         m, t = loam.msg_from_pose(kind, p, bef if kind == 1 else None, stamp=12.5)
         np.testing.assert_array_equal(np.array(m.orientation[:]), _oracle_orientation(oc, p))
@@ -51,7 +52,7 @@ def test_msg_from_pose_matches_oracle(loam, oc, kind):
 
 def test_round_trip_matches_oracle(loam, oc):
     """publish -> receive = the oracle's pose_through_msg bit for bit; Bef passes through exactly"""
-    for p in _poses(500, seed=11):
+    for p in _poses(8000, seed=11):
         m, _ = loam.msg_from_pose(loam.MSG_AFT_MAPPED, p, p * 0.5)
         back, bef = loam.pose_from_msg(m)
         np.testing.assert_array_equal(back, _oracle_round_trip(oc, p))

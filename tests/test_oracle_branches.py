@@ -50,3 +50,17 @@ def test_skip_frame_num_cadence(oc, sg):
         solved = [r["pub"] for r in recs[1:]]
         expect = [7 if i % (skip + 1) == 0 else 1 for i in range(len(solved))]
         assert solved == expect, (skip, solved)
+
+
+def test_q11_window_past_last_cloud(oc, sg):
+    """Last clouds cut below the next sweep's sharp / flat counts: the L-M still runs (gates 10 /
+    100) with forward windows that reach the ends of CornerLast / SurfLast (Q11, clamped at |Last|,
+    src/laserOdometry.cpp:486, :598); tools/asan_suite.sh runs this under AddressSanitizer"""
+    recs = scenarios.run_stream(oc.Oracle(oc.default_config(system_delay=1)), sg.stream_sweeps(12, 1),
+                                truncate_last_at=(4, 7))
+    by_k = {r["k"]: r for r in recs}
+    for k in (4, 7):
+        cut, nxt = by_k[k], by_k[k + 1]
+        assert (cut["n_less_sharp"], cut["n_less_flat"]) == (14, 120)
+        assert nxt["n_sharp"] > 14 and nxt["n_flat"] > 120
+        assert nxt["od_iters"] > 0 and np.all(np.isfinite(nxt["pose"]))
