@@ -1242,6 +1242,7 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
   __syncthreads();
   // the done counter is an agent-scope acq_rel RMW, and the last workgroup's threads acquire at
   // agent scope before reading the other workgroups' partials (they may sit on other XCDs)
+  // (measured against a relaxed counter without the fence: config 3 1.09 vs 1.10 ms per sweep, noise)
   if (tid == 0)
     sh_last = __hip_atomic_fetch_add(&b.done[p], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
   __syncthreads();
