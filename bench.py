@@ -7,9 +7,10 @@ cur, mapping of prev into an empty map and solved for cur.  Shar
 ranges of problems per rank (seeds 1000 + global index), no collective on the data path; one
 all-gather of the poses after the timed steps.
 
-  --split weak   (default, the `value`): every rank owns --batch problems
-  --split strong (reported beside it in "strong", or as `value` when chosen): --global-batch
-                 problems in total (BASELINE config 4: 1024), global_batch / N per rank
+  --split strong (default, the `value`): --global-batch problems in total (BASELINE config 4:
+                 1024), global_batch / N per rank — a driver `--gpus N` run reports config 4 itself
+  --split weak   (reported beside it in "weak", or as `value` when chosen): every rank owns
+                 --batch problems (at N = 1 both splits are the same 1024 problems)
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--split weak|strong]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -298,7 +299,7 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1024, help="problems per GPU (weak split)")
     ap.add_argument("--global-batch", type=int, default=1024, help="problems in total (strong split)")
-    ap.add_argument("--split", choices=("weak", "strong"), default="weak", help="which split is `value`")
+    ap.add_argument("--split", choices=("weak", "strong"), default="strong", help="which split is `value`")
     ap.add_argument("--strong-leg", type=int, default=1, help="also measure the other split (0: skip)")
     ap.add_argument("--cpu-sample", type=int, default=32, help="problems in the CPU baseline sample (0: skip)")
     ap.add_argument("--cpu-reps", type=int, default=5)

@@ -430,6 +430,76 @@ LOAM_D int block_radix_sort_kv(uint32_t* ka, uint16_t* va, uint32_t* kb, uint16_
   return cur;
 }
 
+// One tile of a stable LSD radix pass through global memory (k_vg_big): thread t holds the tile's
+// items [t*E, t*E + E) (valid below n_tile) in k[].  For each valid item, rank[e] = its rank among
+// the tile's items with the same digit (key >> shift) & 15, in tile order (blocked = input order,
+// so the pass is stable); tot[d] (LDS, 16 words) = the tile's count of digit d.  The same packed
+// counters as block_radix_sort_kv.  sc: LDS scratch of (NT/64 + 1) * 8 words; n_tile < 65536.
+template <int NT, int E>
+LOAM_D void tile_rank4(const uint32_t* k, int shift, int n_tile, uint32_t* sc, uint32_t* tot, int* rank) {
+  constexpr int NW = NT / 64;
+  const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+  uint32_t meta[E];  // rank in thread | digit << 8 | valid << 12
+  uint64_t clo = 0, chi = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    meta[e] = 0;
+    if (tid * E + e < n_tile) {
+      const uint32_t d = (k[e] >> shift) & 15u;
+      const int sh = (int)(d & 7u) * 8;
+      const uint64_t c = d < 8 ? clo : chi;
+      meta[e] = (uint32_t)((c >> sh) & 255u) | (d << 8) | (1u << 12);
+      const uint64_t c2 = c + (1ull << sh);
+      if (d < 8) clo = c2; else chi = c2;
+    }
+  }
+  uint32_t p[8], inc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {  // counts of digits 2i, 2i+1 as 16-bit pairs
+    const uint64_t c = i < 4 ? clo : chi;
+    const int sh = (2 * i % 8) * 8;
+    p[i] = (uint32_t)((c >> sh) & 255u) | ((uint32_t)((c >> (sh + 8)) & 255u) << 16);
+    inc[i] = p[i];
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t t = (uint32_t)__shfl_up((int)inc[i], o, 64);
+      if (lane >= o) inc[i] += t;
+    }
+  if (lane == 63)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sc[w * 8 + i] = inc[i];
+  __syncthreads();
+  if (tid < 8) {
+    uint32_t run = 0;
+    for (int ww = 0; ww < NW; ++ww) {
+      const uint32_t t = sc[ww * 8 + tid];
+      sc[ww * 8 + tid] = run;
+      run += t;
+    }
+    tot[2 * tid] = run & 0xffffu;
+    tot[2 * tid + 1] = run >> 16;
+  }
+  __syncthreads();
+  uint32_t ex[8];  // packed exclusive prefixes of digits 2i, 2i+1 before this thread
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ex[i] = inc[i] - p[i] + sc[w * 8 + i];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    rank[e] = -1;
+    if (meta[e] >> 12) {
+      const int d = (int)((meta[e] >> 8) & 15u);
+      uint32_t x = ex[0];
+#pragma unroll
+      for (int i = 1; i < 8; ++i) x = (d >> 1) == i ? ex[i] : x;
+      rank[e] = (int)((x >> ((d & 1) * 16)) & 0xffffu) + (int)(meta[e] & 255u);
+    }
+  }
+  __syncthreads();  // sc is reused by the next call
+}
+
 LOAM_HD int next_pow2(int v) {
   int p = 1;
   while (p < v) p <<= 1;

@@ -20,7 +20,6 @@
 //  k_mp_vcopy      per valid cube: old content ++ appended points -> DS input
 //  k_mp_compact    new cube store (valid cubes downsampled, others appended) into the other pool
 //  k_mp_register   full cloud to the map frame (:1060-1063)
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <functional>
@@ -219,6 +218,7 @@ __global__ __launch_bounds__(256) void k_mp_stack(MpBuffers b, MpInput in) {
     const float4 m = loampose::point_to_map(r, a);
     out[i < nc ? i : b.capC + (i - nc)] = loampose::point_to_tobe_mapped(r, m);
   }
+  if (p == 0 && blockIdx.x == 0 && threadIdx.x == 0) { b.vg_cnt[0] = 0; b.vg_cnt[1] = 0; }  // (vg_stack's lists)
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const size_t base = (size_t)p * b.cap_stack;
     b.sseg_b[p * 2 + 0] = (int)base;
@@ -233,189 +233,16 @@ __global__ __launch_bounds__(256) void k_mp_stack(MpBuffers b, MpInput in) {
 }
 
 // ---------------------------------------------------------------- segmented VoxelGrid
-// The segmented VoxelGrid kernels run one group of G threads per segment, grid-stride over the
-// segments: G = 64 (a wave) for the many, mostly empty per-cube segments, G = 256 (the block)
-// for the few large stack segments.
-template <int G>
-struct VgGroup {
-  static constexpr int NT = G < 256 ? 256 : G;  // block size
-  int g, t;  // group index in the grid, thread index in the group
-  LOAM_D VgGroup() : g((blockIdx.x * NT + threadIdx.x) / G), t(threadIdx.x % G) {}
-  LOAM_D static int stride() { return gridDim.x * (NT / G); }
-  LOAM_D float min(float v, float* sc) {
-    if constexpr (G == 64) return wave_min_f(v);
-    else return block_reduce<NT>(v, sc, [](float a, float c) { return fminf(a, c); });
-  }
-  LOAM_D float max(float v, float* sc) {
-    if constexpr (G == 64) return wave_max_f(v);
-    else return block_reduce<NT>(v, sc, [](float a, float c) { return fmaxf(a, c); });
-  }
-  LOAM_D int excl_scan(int v, int* sc, int& total) {  // v in {0, 1}
-    if constexpr (G == 64) {
-      const uint64_t m = __ballot(v);
-      total = __popcll(m);
-      return __popcll(m & lanemask_lt());
-    } else {
-      return block_excl_scan<NT>(v, sc, total);
-    }
-  }
-};
-
-template <int G>
-__global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_params(VgJob j) {
-  __shared__ float fsc[16];
-  VgGroup<G> grp;
-  for (int s = grp.g; s < j.nseg; s += VgGroup<G>::stride()) {
-    const int b0 = j.begin[s], b1 = j.end[s];
-    int* prm = j.params + (size_t)s * 8;
-    if (b1 <= b0) {
-      if (grp.t == 0) {
-        prm[5] = 0;
-        if (j.sb24) { j.sb24[s] = 0; j.se24[s] = 0; j.sb32[s] = 0; j.se32[s] = 0; }
-      }
-      continue;
-    }
-    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
-    for (int i = b0 + grp.t; i < b1; i += G) {
-      const float4 a = j.in[i];
-      mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
-      mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
-    }
-    for (int d = 0; d < 3; ++d) {
-      mn[d] = grp.min(mn[d], fsc);
-      mx[d] = grp.max(mx[d], fsc);
-    }
-    if (grp.t == 0) {
-      const float inv = 1.0f / j.leaf[s];
-      const bool too_small = vg_leaf_too_small(mn, mx, inv);
-      int minb[3] = {0, 0, 0}, maxb[3] = {0, 0, 0};
-      if (!too_small)
-        for (int d = 0; d < 3; ++d) {
-          minb[d] = (int)floorf(mn[d] * inv);
-          maxb[d] = (int)floorf(mx[d] * inv);
-        }
-      const int divx = maxb[0] - minb[0] + 1, divy = maxb[1] - minb[1] + 1;
-      prm[0] = minb[0]; prm[1] = minb[1]; prm[2] = minb[2];
-      prm[3] = divx; prm[4] = divx * divy;
-      prm[5] = too_small ? 1 : 0;
-      const int64_t divz = (int64_t)(maxb[2] - minb[2] + 1);
-      if (!prm[5] && j.end_bit < 32 && (int64_t)divx * divy * divz > ((int64_t)1 << j.end_bit) && j.err)
-        atomicOr(&j.err[(s / j.seg_per_err) * j.err_stride], ERR_VG_BITS);
-      if (j.sb24) {
-        const bool fits = prm[5] || (int64_t)divx * divy * divz <= ((int64_t)1 << 24);
-        j.sb24[s] = fits ? b0 : 0; j.se24[s] = fits ? b1 : 0;
-        j.sb32[s] = fits ? 0 : b0; j.se32[s] = fits ? 0 : b1;
-      }
-    }
-  }
-}
-
-template <int G>
-__global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_keys(VgJob j) {
-  VgGroup<G> grp;
-  for (int s = grp.g; s < j.nseg; s += VgGroup<G>::stride()) {
-    const int b0 = j.begin[s], b1 = j.end[s];
-    if (b1 <= b0) continue;
-    const int* prm = j.params + (size_t)s * 8;
-    const float inv = 1.0f / j.leaf[s];
-    const bool pass = prm[5] != 0;
-    const int m0 = prm[0], m1 = prm[1], m2 = prm[2], mul1 = prm[3], mul2 = prm[4];
-    for (int i = b0 + grp.t; i < b1; i += G) {
-      uint32_t key = 0;
-      if (!pass) {
-        const float4 a = j.in[i];
-        const int i0 = (int)(floorf(a.x * inv) - (float)m0);
-        const int i1 = (int)(floorf(a.y * inv) - (float)m1);
-        const int i2 = (int)(floorf(a.z * inv) - (float)m2);
-        key = (uint32_t)i0 + (uint32_t)i1 * (uint32_t)mul1 + (uint32_t)i2 * (uint32_t)mul2;
-      }
-      j.keys[i] = key;
-      j.vals[i] = (uint32_t)i;
-    }
-  }
-}
-
-// one output point per run of equal keys: the float mean of x, y, z, intensity summed in sorted
-// order (the reference's VoxelGrid)
-template <int G>
-__global__ __launch_bounds__(VgGroup<G>::NT) void k_vg_reduce(VgJob j) {
-  __shared__ int isc[24];
-  __shared__ int hpos[G == 64 ? 1 : G];  // the chunk's head positions (workgroup groups)
-  __shared__ uint32_t cval[VgGroup<G>::NT];  // the chunk's sorted source indices, per group
-  VgGroup<G> grp;
-  uint32_t* gval = cval + (threadIdx.x / G) * G;
-  for (int s = grp.g; s < j.nseg; s += VgGroup<G>::stride()) {
-    const int b0 = j.begin[s], b1 = j.end[s];
-    if (b1 <= b0) {
-      if (grp.t == 0 && !j.keep_counts) j.out_count[s] = 0;
-      continue;
-    }
-    if (j.params[(size_t)s * 8 + 5]) {  // "leaf size too small": output = input
-      for (int i = b0 + grp.t; i < b1; i += G) j.out[i] = j.in[i];
-      if (grp.t == 0) j.out_count[s] = b1 - b0;
-      continue;
-    }
-    int run = 0;
-    for (int base = b0; base < b1; base += G) {
-      const int t = base + grp.t;
-      const uint32_t k = t < b1 ? j.keys_alt[t] : 0u;
-      const int head = (t < b1 && (t == b0 || j.keys_alt[t - 1] != k)) ? 1 : 0;
-      int tot;
-      gval[grp.t] = t < b1 ? j.vals_alt[t] : 0u;  // coalesced; read back by the run heads
-      if constexpr (G == 64) {
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-      }
-      const int ex = grp.excl_scan(head, isc, tot);  // (its barrier / wave sync publishes gval)
-      // a run ends at the chunk's next head; only the chunk's last run reads on past the chunk
-      int nxt = -1;
-      if constexpr (G == 64) {
-        const uint64_t hm = __ballot(head);
-        const uint64_t after = grp.t == 63 ? 0ull : hm & (~0ull << (grp.t + 1));
-        if (after) nxt = base + __ffsll((unsigned long long)after) - 1;
-      } else {
-        if (head) hpos[ex] = t;
-        __syncthreads();
-        if (head && ex + 1 < tot) nxt = hpos[ex + 1];
-      }
-      if (head) {
-        int e = nxt;
-        if (e < 0) {
-          e = min(base + G, b1);
-          while (e < b1 && j.keys_alt[e] == k) ++e;
-        }
-        float sx = 0, sy = 0, sz = 0, si = 0;
-        for (int mm = t; mm < e; mm += 4) {  // four independent gathers in flight per step
-          float4 a[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int m = min(mm + u, e - 1);
-            a[u] = j.in[m < base + G ? gval[m - base] : j.vals_alt[m]];
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (mm + u < e) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
-        }
-        const float cnt = (float)(e - t);
-        j.out[b0 + run + ex] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
-      }
-      run += tot;
-      if constexpr (G == 64) {  // gval / hpos are rewritten by the next chunk
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-      } else {
-        __syncthreads();
-      }
-    }
-    if (grp.t == 0) j.out_count[s] = run;
-  }
-}
+// PCL VoxelGrid over many segments at once: stacks (2 per instance), valid cubes (2 x
+// 125 per instance), the surround map (1).  Per segment: bbox, voxel keys, a stable sort of
+// (voxel, position) — the order of PCL's std::sort on (index, point) pairs with equal voxels in
+// input order — and one output point per voxel, the float mean of x, y, z, intensity summed in
+// sorted order.  vg_run cascades three hand-written kernels by segment size; no library sort.
 
 // Fused segmented VoxelGrid with an LDS radix sort: one workgroup per segment of at most NT*E
-// points does bbox + parameters (as k_vg_params), the voxel keys (as k_vg_keys), a stable radix
-// sort of (voxel, position) pairs over the bits the keys can differ in (the order of the stable
-// hipCUB sort), and the ordered per-voxel means (as k_vg_reduce).  Larger segments are listed in
-// big_b / big_e for the multi-kernel path.
+// points does the bbox, the voxel keys, a stable radix sort of (voxel, position) pairs over the
+// bits the keys can differ in, and the ordered per-voxel means.  Segments beyond NT*E are appended
+// to the job's big list.
 template <int NT, int E>
 __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
   constexpr int N = NT * E;
@@ -425,17 +252,18 @@ __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
   __shared__ float fsc[16];
   __shared__ int isc[24];
   const int tid = threadIdx.x;
-  for (int s = blockIdx.x; s < j.nseg; s += gridDim.x) {
+  const int nl = j.list ? *j.list_n : j.nseg;
+  for (int li = blockIdx.x; li < nl; li += gridDim.x) {
+    const int s = j.list ? j.list[li] : li;
     const int b0 = j.begin[s], b1 = j.end[s], n = b1 - b0;
-    if (n <= 0 || n > N) {
-      if (tid == 0) {
-        j.big_b[s] = n > 0 ? b0 : 0;
-        j.big_e[s] = n > 0 ? b1 : 0;
-        if (n <= 0) j.out_count[s] = 0;
-      }
+    if (n <= 0) {
+      if (tid == 0) j.out_count[s] = 0;
       continue;
     }
-    if (tid == 0) { j.big_b[s] = 0; j.big_e[s] = 0; }
+    if (n > N) {
+      if (tid == 0) j.big[atomicAdd(j.big_n, 1)] = s;
+      continue;
+    }
     const float4* in = j.in + b0;
     float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
     for (int i = tid; i < n; i += NT) {
@@ -528,71 +356,343 @@ __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
   }
 }
 
-constexpr int kVgGridCap = 16384;  // measured: 4096 / 16384 / 65536 within 0.5% of each other, 16384 best
-template <int G>
-void vg_launch_params_keys(const VgJob& j, hipStream_t st) {
-  const int grid = std::min((j.nseg + VgGroup<G>::NT / G - 1) / (VgGroup<G>::NT / G), kVgGridCap);
-  hipLaunchKernelGGL(k_vg_params<G>, dim3(grid), dim3(VgGroup<G>::NT), 0, st, j);
-  hipLaunchKernelGGL(k_vg_keys<G>, dim3(grid), dim3(VgGroup<G>::NT), 0, st, j);
-}
-template <int G>
-void vg_launch_reduce(const VgJob& j, hipStream_t st) {
-  const int grid = std::min((j.nseg + VgGroup<G>::NT / G - 1) / (VgGroup<G>::NT / G), kVgGridCap);
-  hipLaunchKernelGGL(k_vg_reduce<G>, dim3(grid), dim3(VgGroup<G>::NT), 0, st, j);
+// The same for segments of up to NT*E = 16384 points with 8 bytes of LDS per point: the voxel
+// keys stay in input order (ka[i] = key of point i) and only the 16-bit positions move between
+// the two buffers, each radix pass reading its digits through them (tile_rank4 over the whole
+// segment); the long surf stacks of VLP-16 sweeps fit it.
+template <int NT, int E>
+__global__ __launch_bounds__(NT) void k_vg_idx(VgJob j) {
+  constexpr int N = NT * E;
+  static_assert(N <= 65536, "16-bit positions");
+  __shared__ uint32_t ka[N];
+  __shared__ uint16_t va[N], vb[N];
+  __shared__ uint32_t sc[(NT / 64 + 1) * 8];
+  __shared__ uint32_t dtot[16], dbase[16];
+  __shared__ float fsc[16];
+  __shared__ int isc[24];
+  const int tid = threadIdx.x;
+  const int nl = j.list ? *j.list_n : j.nseg;
+  for (int li = blockIdx.x; li < nl; li += gridDim.x) {
+    const int s = j.list ? j.list[li] : li;
+    const int b0 = j.begin[s], b1 = j.end[s], n = b1 - b0;
+    if (n <= 0) {
+      if (tid == 0) j.out_count[s] = 0;
+      continue;
+    }
+    if (n > N) {
+      if (tid == 0) j.big[atomicAdd(j.big_n, 1)] = s;
+      continue;
+    }
+    const float4* in = j.in + b0;
+    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+    for (int i = tid; i < n; i += NT) {
+      const float4 a = in[i];
+      mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
+      mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
+    }
+    for (int d = 0; d < 3; ++d) {
+      mn[d] = block_reduce<NT>(mn[d], fsc, [](float a, float c) { return fminf(a, c); });
+      mx[d] = block_reduce<NT>(mx[d], fsc, [](float a, float c) { return fmaxf(a, c); });
+    }
+    const float inv = 1.0f / j.leaf[s];
+    if (vg_leaf_too_small(mn, mx, inv)) {  // "leaf size too small": output = input
+      for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
+      if (tid == 0) j.out_count[s] = n;
+      continue;
+    }
+    const int m0 = (int)floorf(mn[0] * inv), m1 = (int)floorf(mn[1] * inv), m2 = (int)floorf(mn[2] * inv);
+    const int divx = (int)floorf(mx[0] * inv) - m0 + 1, divy = (int)floorf(mx[1] * inv) - m1 + 1;
+    const uint32_t mul1 = (uint32_t)divx, mul2 = (uint32_t)(divx * divy);
+    uint32_t kmax = 0;
+    for (int i = tid; i < n; i += NT) {
+      const float4 a = in[i];
+      const int i0 = (int)(floorf(a.x * inv) - (float)m0);
+      const int i1 = (int)(floorf(a.y * inv) - (float)m1);
+      const int i2 = (int)(floorf(a.z * inv) - (float)m2);
+      const uint32_t key = (uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2;
+      ka[i] = key;
+      va[i] = (uint16_t)i;
+      kmax = key > kmax ? key : kmax;
+    }
+    kmax = (uint32_t)block_reduce<NT>((int)(kmax >> 1), (int*)isc, [](int a, int c) { return a > c ? a : c; });
+    const int nbits = kmax ? 33 - __clz((int)kmax) : (n > 1 ? 1 : 0);
+    int cur = 0;
+    for (int shift = 0; shift < nbits; shift += 4) {
+      const uint16_t* vs = cur ? vb : va;
+      uint16_t* vd = cur ? va : vb;
+      uint32_t k[E];
+      uint16_t v[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = tid * E + e;
+        v[e] = i < n ? vs[i] : (uint16_t)0;
+        k[e] = i < n ? ka[v[e]] : 0u;
+      }
+      int rank[E];
+      tile_rank4<NT, E>(k, shift, n, sc, dtot, rank);
+      if (tid == 0) {
+        uint32_t r = 0;
+        for (int d = 0; d < 16; ++d) { dbase[d] = r; r += dtot[d]; }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (rank[e] >= 0) vd[dbase[(k[e] >> shift) & 15u] + rank[e]] = v[e];
+      __syncthreads();
+      cur ^= 1;
+    }
+    const uint16_t* vs = cur ? vb : va;
+    // ordered per-voxel means (as k_vg_radix): thread t owns sorted positions [t E, t E + E),
+    // gathered eight at a time
+    {
+      const int i0 = tid * E;
+      int nh = 0;
+      uint32_t prev = i0 > 0 && i0 < n ? ka[vs[i0 - 1]] : 0u;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = i0 + e;
+        const uint32_t kc = i < n ? ka[vs[i]] : 0u;
+        nh += (i < n && (i == 0 || prev != kc)) ? 1 : 0;
+        prev = kc;
+      }
+      int tot;
+      int slot = block_excl_scan<NT>(nh, isc, tot);
+      bool open = false;
+      uint32_t ck = 0;
+      int cstart = 0;
+      float sx = 0, sy = 0, sz = 0, si = 0;
+      prev = i0 > 0 && i0 < n ? ka[vs[i0 - 1]] : 0u;
+#pragma unroll
+      for (int e0 = 0; e0 < E; e0 += 8) {
+        float4 a[8];
+        uint32_t kk[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + e0 + u;
+          kk[u] = i < n ? ka[vs[i]] : 0u;
+          a[u] = i < n ? in[vs[i]] : make_float4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + e0 + u;
+          if (i < n) {
+            if (i == 0 || prev != kk[u]) {
+              if (open) {
+                const float cnt = (float)(i - cstart);
+                j.out[b0 + slot++] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+              }
+              open = true;
+              ck = kk[u];
+              cstart = i;
+              sx = 0; sy = 0; sz = 0; si = 0;
+            }
+            if (open) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
+            prev = kk[u];
+          }
+        }
+      }
+      if (open) {
+        int m = min(i0 + E, n);
+        while (m < n && ka[vs[m]] == ck) {
+          const float4 b4 = in[vs[m]];
+          sx += b4.x; sy += b4.y; sz += b4.z; si += b4.w;
+          ++m;
+        }
+        const float cnt = (float)(m - cstart);
+        j.out[b0 + slot] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+      }
+      if (tid == 0) j.out_count[s] = tot;
+    }
+    __syncthreads();
+  }
 }
 
-// G = threads per segment: 64 for many mostly-empty segments, 256 / 1024 for few large ones
-// fcap: capacity (points per segment) of the fused LDS kernel — 0 (multi-kernel path only),
-// 2048 (256 threads x 8) or 12288 (1024 x 12); G: threads per segment of the multi-kernel path
-// (hipCUB segmented radix sort), which finishes the segments beyond fcap.  The fused kernel wins
-// for a few instances (streaming: one launch instead of four, no global key arrays); for large
-// batches hipCUB's multi-kernel path measured faster (both keep the stable (voxel, position) order).
-constexpr bool kVgFusedBatch = false;
-constexpr int kVgCubeCap = 12288;
-constexpr bool kVgCubeG256 = true;  // a workgroup per cube segment also in batches: a few large cubes dominate
-// finish = false: the caller guarantees every segment fits fcap (the fused launch is all)
-hipError_t vg_run(const VgJob& j0, void* tmp, size_t tmp_bytes, hipStream_t st, int G, int fcap, bool finish = true) {
+// Segments of any size (those beyond the LDS kernels), one workgroup each, taken from the job's list:
+// bbox, voxel keys into the global key array (with the digit histograms of every pass), a stable
+// LSD radix sort of (voxel, position) over the key bits through global memory — 4-bit digits, tiles
+// of NT*E items ranked in registers (tile_rank4), digit bases carried from tile to tile — and the
+// ordered per-voxel means over the sorted arrays.  Rare in VLP-16 batches (long surf stacks); the
+// HDL-64E stack and a large surround map take it.
+template <int NT, int E>
+__global__ __launch_bounds__(NT) void k_vg_big(VgJob j) {
+  constexpr int TILE = NT * E;
+  __shared__ uint32_t hist[8][16];
+  __shared__ uint32_t dbase[16], ttot[16];
+  __shared__ uint32_t sc[(NT / 64 + 1) * 8];
+  __shared__ float fsc[16];
+  __shared__ int isc[24];
+  const int tid = threadIdx.x;
+  const int nl = *j.list_n;
+  for (int li = blockIdx.x; li < nl; li += gridDim.x) {
+    const int s = j.list[li];
+    const int b0 = j.begin[s], n = j.end[s] - b0;
+    const float4* in = j.in + b0;
+    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+    for (int i = tid; i < n; i += NT) {
+      const float4 a = in[i];
+      mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
+      mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
+    }
+    for (int d = 0; d < 3; ++d) {
+      mn[d] = block_reduce<NT>(mn[d], fsc, [](float a, float c) { return fminf(a, c); });
+      mx[d] = block_reduce<NT>(mx[d], fsc, [](float a, float c) { return fmaxf(a, c); });
+    }
+    const float inv = 1.0f / j.leaf[s];
+    if (vg_leaf_too_small(mn, mx, inv)) {  // "leaf size too small": output = input
+      for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
+      if (tid == 0) j.out_count[s] = n;
+      __syncthreads();
+      continue;
+    }
+    const int m0 = (int)floorf(mn[0] * inv), m1 = (int)floorf(mn[1] * inv), m2 = (int)floorf(mn[2] * inv);
+    const int divx = (int)floorf(mx[0] * inv) - m0 + 1, divy = (int)floorf(mx[1] * inv) - m1 + 1;
+    const uint32_t mul1 = (uint32_t)divx, mul2 = (uint32_t)(divx * divy);
+    for (int i = tid; i < 8 * 16; i += NT) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    uint32_t* K = j.keys + b0;
+    uint32_t* V = j.vals + b0;
+    uint32_t* K2 = j.keys_alt + b0;
+    uint32_t* V2 = j.vals_alt + b0;
+    uint32_t kmax = 0;
+    for (int i = tid; i < n; i += NT) {
+      const float4 a = in[i];
+      const int i0 = (int)(floorf(a.x * inv) - (float)m0);
+      const int i1 = (int)(floorf(a.y * inv) - (float)m1);
+      const int i2 = (int)(floorf(a.z * inv) - (float)m2);
+      const uint32_t key = (uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2;
+      K[i] = key;
+      V[i] = (uint32_t)i;
+      kmax = key > kmax ? key : kmax;
+#pragma unroll
+      for (int p = 0; p < 8; ++p) atomicAdd(&hist[p][(key >> (4 * p)) & 15u], 1u);
+    }
+    kmax = (uint32_t)block_reduce<NT>((int)(kmax >> 1), (int*)isc, [](int a, int c) { return a > c ? a : c; });
+    const int nbits = kmax ? 33 - __clz((int)kmax) : (n > 1 ? 1 : 0);
+    int cur = 0;  // 0: the data is in (K, V)
+    for (int pass = 0; pass * 4 < nbits; ++pass) {
+      const uint32_t* ks = cur ? K2 : K;
+      const uint32_t* vs = cur ? V2 : V;
+      uint32_t* kd = cur ? K : K2;
+      uint32_t* vd = cur ? V : V2;
+      if (tid == 0) {
+        uint32_t r = 0;
+        for (int d = 0; d < 16; ++d) { dbase[d] = r; r += hist[pass][d]; }
+      }
+      __syncthreads();
+      for (int t0 = 0; t0 < n; t0 += TILE) {
+        const int nt = min(TILE, n - t0);
+        uint32_t k[E], v[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = tid * E + e;
+          k[e] = i < nt ? ks[t0 + i] : 0u;
+          v[e] = i < nt ? vs[t0 + i] : 0u;
+        }
+        int rank[E];
+        tile_rank4<NT, E>(k, 4 * pass, nt, sc, ttot, rank);
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (rank[e] >= 0) {
+            const int pos = (int)dbase[(k[e] >> (4 * pass)) & 15u] + rank[e];
+            kd[pos] = k[e];
+            vd[pos] = v[e];
+          }
+        __syncthreads();
+        if (tid < 16) dbase[tid] += ttot[tid];
+        __syncthreads();
+      }
+      cur ^= 1;
+    }
+    const uint32_t* ks = cur ? K2 : K;
+    const uint32_t* vs = cur ? V2 : V;
+    // ordered per-voxel means, tile by tile: thread t's E sorted positions, heads counted by one
+    // block scan per tile; each head sums its run in sorted order, reading on past its range
+    int outn = 0;
+    for (int t0 = 0; t0 < n; t0 += TILE) {
+      const int i0 = t0 + tid * E;
+      uint32_t kk[E];
+      int nh = 0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = i0 + e;
+        kk[e] = i < n ? ks[i] : 0u;
+        nh += (i < n && (i == 0 || (e > 0 ? kk[e - 1] : ks[i - 1]) != kk[e])) ? 1 : 0;
+      }
+      int tot;
+      int slot = outn + block_excl_scan<NT>(nh, isc, tot);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = i0 + e;
+        if (i < n && (i == 0 || (e > 0 ? kk[e - 1] : ks[i - 1]) != kk[e])) {
+          float sx = 0, sy = 0, sz = 0, si = 0;
+          int m = i;
+          while (m < n && ks[m] == kk[e]) {
+            const float4 b4 = in[vs[m]];
+            sx += b4.x; sy += b4.y; sz += b4.z; si += b4.w;
+            ++m;
+          }
+          const float cnt = (float)(m - i);
+          j.out[b0 + slot++] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+        }
+      }
+      outn += tot;
+    }
+    if (tid == 0) j.out_count[s] = outn;
+    __syncthreads();
+  }
+}
+
+// The cascade: the fused LDS kernel at cap1 points (2048: 256 threads, for the many small cube
+// segments; 12288: 1024 threads) over every segment; the segments beyond it through the 12288
+// kernel (after the 2048 one), then the rest through k_vg_big.  The list-driven launches use fixed
+// grids whose workgroups leave at once when their lists are short.  finish = false: the caller
+// knows every segment fits cap1 (streaming stacks), only the first launch is enqueued.
+// tier2_idx: the second tier is k_vg_idx (16384 points; the long surf stacks) rather than
+// k_vg_radix<1024, 12> (12288; measured faster on the 2k-12k cube segments: at batch 1024 the cubes
+// took 0.68 ms/step with it against 0.85 with k_vg_idx, the stacks 0.86 with k_vg_idx against 1.20)
+constexpr int kVgListGrid = 1024, kVgBigGrid = 256;
+hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true, bool tier2_idx = false) {
   if (j0.nseg == 0) return hipSuccess;
-  const int grid = std::min(j0.nseg, 65536);
-  VgJob j = j0;
-  if (fcap > 0) {
-    if (fcap <= 2048) hipLaunchKernelGGL((k_vg_radix<256, 8>), dim3(grid), dim3(256), 0, st, j0);
-    else hipLaunchKernelGGL((k_vg_radix<1024, 12>), dim3(grid), dim3(1024), 0, st, j0);
-    if (!finish) return hipGetLastError();
-    j.begin = j0.big_b;  // the multi-kernel path finishes what the fused kernel could not hold
-    j.end = j0.big_e;
-    j.keep_counts = 1;
+  if (!j0.zeroed) {
+    const hipError_t e = hipMemsetAsync(j0.counts, 0, 2 * sizeof(int), st);
+    if (e != hipSuccess) return e;
   }
-  if (G == 64) vg_launch_params_keys<64>(j, st);
-  else if (G == 256) vg_launch_params_keys<256>(j, st);
-  else vg_launch_params_keys<1024>(j, st);
-  size_t bytes = tmp_bytes;
-  hipError_t e;
-  if (j.sb24) {
-    e = hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
-                                                    j.nseg, j.sb24, j.se24, 0, 24, st);
-    bytes = tmp_bytes;
-    if (e == hipSuccess)
-      e = hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
-                                                      j.nseg, j.sb32, j.se32, 0, 32, st);
+  // the caller's input list (non-empty segments) is walked by a fixed grid
+  const int grid = j0.list ? std::min(j0.nseg, 8192) : std::min(j0.nseg, 65536);
+  VgJob a = j0;
+  a.big = j0.lists[0];
+  a.big_n = j0.counts;
+  int last = 0;  // the list k_vg_big takes
+  if (cap1 <= 2048) {
+    hipLaunchKernelGGL((k_vg_radix<256, 8>), dim3(grid), dim3(256), 0, st, a);
+    if (finish) {
+      VgJob b = j0;
+      b.list = j0.lists[0];
+      b.list_n = j0.counts;
+      b.big = j0.lists[1];
+      b.big_n = j0.counts + 1;
+      if (tier2_idx) hipLaunchKernelGGL((k_vg_idx<1024, 16>), dim3(std::min(j0.nseg, kVgListGrid)), dim3(1024), 0, st, b);
+      else hipLaunchKernelGGL((k_vg_radix<1024, 12>), dim3(std::min(j0.nseg, kVgListGrid)), dim3(1024), 0, st, b);
+      last = 1;
+    }
   } else {
-    e = hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, bytes, j.keys, j.keys_alt, j.vals, j.vals_alt, j.total,
-                                                    j.nseg, j.begin, j.end, 0, j.end_bit, st);
+    hipLaunchKernelGGL((k_vg_radix<1024, 12>), dim3(grid), dim3(1024), 0, st, a);
   }
-  if (e != hipSuccess) return e;
-  if (G == 64) vg_launch_reduce<64>(j, st);
-  else if (G == 256) vg_launch_reduce<256>(j, st);
-  else vg_launch_reduce<1024>(j, st);
+  if (finish) {
+    VgJob c = j0;
+    c.list = j0.lists[last];
+    c.list_n = j0.counts + last;
+    hipLaunchKernelGGL((k_vg_big<1024, 12>), dim3(std::min(j0.nseg, kVgBigGrid)), dim3(1024), 0, st, c);
+  }
   return hipGetLastError();
 }
 
-size_t vg_tmp_bytes(int total, int nseg) {
-  size_t bytes = 0;
-  if (hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                  (uint32_t*)nullptr, (uint32_t*)nullptr, total, nseg,
-                                                  (int*)nullptr, (int*)nullptr, 0, 32) != hipSuccess)
-    return 0;
-  return bytes;
+// the instance buffers' VoxelGrid scratch (sort arrays, cascade lists)
+VgJob vg_job(const MpBuffers& b) {
+  VgJob j;
+  j.keys = b.vg_k; j.keys_alt = b.vg_k2; j.vals = b.vg_v; j.vals_alt = b.vg_v2;
+  j.lists[0] = b.vg_l0; j.lists[1] = b.vg_l1; j.counts = b.vg_cnt;
+  return j;
 }
 
 // ---------------------------------------------------------------- FromMap gather
@@ -1281,6 +1381,7 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
 // host found IMU data for the odometry stamp
 __global__ void k_mp_lm_end(MpBuffers b) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p == 0) { b.vg_cnt[0] = 0; b.vg_cnt[1] = 0; b.vg_cnt[2] = 0; }  // (vg_cubes' lists)
   if (p >= b.P) return;
   const int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan]) return;
@@ -1515,6 +1616,8 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_vseg(MpBuffers b) {
     b.vseg_e[sidx] = base + (over ? 0 : n);
     b.vseg_leaf[sidx] = kind == 0 ? 0.2f : 0.4f;
     if (over && n > 0) b.istate[(size_t)p * kMpStateInts + kMiErr] |= ERR_CAP_MAP;
+    if (over || n == 0) b.vseg_cnt[sidx] = 0;  // (not in the VoxelGrid's list)
+    else b.vg_lin[atomicAdd(b.vg_cnt + 2, 1)] = sidx;
   }
 }
 
@@ -1704,18 +1807,14 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
   A(&b.sseg_cnt, (size_t)P * 2 * sizeof(int));
   A(&b.sseg_leaf, (size_t)P * 2 * sizeof(float));
   const size_t vgn = Pm > Ps ? Pm : Ps;
-  A(&b.vg_params, (size_t)P * 2 * kMaxValid * 8 * sizeof(int));
   A(&b.vg_k, vgn * sizeof(uint32_t));
   A(&b.vg_k2, vgn * sizeof(uint32_t));
   A(&b.vg_v, vgn * sizeof(uint32_t));
   A(&b.vg_v2, vgn * sizeof(uint32_t));
-  A(&b.vg_bb, (size_t)P * 2 * kMaxValid * sizeof(int));
-  A(&b.vg_split, (size_t)4 * P * 2 * kMaxValid * sizeof(int));
-  A(&b.vg_be, (size_t)P * 2 * kMaxValid * sizeof(int));
-  const size_t t1 = vg_tmp_bytes((int)vgn, P * 2 * kMaxValid), t2 = vg_tmp_bytes((int)Ps, P * 2);
-  b.cub_bytes = t1 > t2 ? t1 : t2;
-  if (t1 == 0 || t2 == 0) A.err = hipErrorInvalidValue;
-  A(&b.cub_tmp, b.cub_bytes);
+  A(&b.vg_l0, (size_t)P * 2 * kMaxValid * sizeof(int));
+  A(&b.vg_l1, (size_t)P * 2 * kMaxValid * sizeof(int));
+  A(&b.vg_lin, (size_t)P * 2 * kMaxValid * sizeof(int));
+  A(&b.vg_cnt, 3 * sizeof(int));
   A(&b.reg, (size_t)P * b.capS * sizeof(float4));
   A(&b.part, (size_t)P * kMpSmallGrid * 28 * sizeof(double));
   A(&b.rot, (size_t)P * 6 * sizeof(double));
@@ -1732,7 +1831,7 @@ void mp_free(MpBuffers& b) {
                   b.stack2, b.stack, b.nstack, b.from, b.hC_start, b.hS_start, b.h_fill, b.hC_T, b.hS_T,
                   b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.citems, b.nitems, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
-                  b.vg_params, b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_bb, b.vg_be, b.vg_split, b.cub_tmp, b.reg, b.nreg, b.part, b.done, b.rot};
+                  b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_l0, b.vg_l1, b.vg_lin, b.vg_cnt, b.reg, b.nreg, b.part, b.done, b.rot};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = MpBuffers();
@@ -1764,19 +1863,17 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   mark("k_mp_prepare");
   hipLaunchKernelGGL(k_mp_stack, dim3(16, P), dim3(256), 0, st, b, in);
   mark("k_mp_stack");
-  VgJob js;
+  VgJob js = vg_job(b);
   js.in = b.stack2; js.out = b.stack; js.begin = b.sseg_b; js.end = b.sseg_e; js.leaf = b.sseg_leaf;
-  js.out_count = b.sseg_cnt; js.params = b.vg_params; js.keys = b.vg_k; js.keys_alt = b.vg_k2;
-  js.vals = b.vg_v; js.vals_alt = b.vg_v2; js.big_b = b.vg_bb; js.big_e = b.vg_be; js.nseg = 2 * P; js.total = P * b.cap_stack;
-  if (P > 4) {  // batches: segments whose keys fit 24 bits sort in three passes, the rest in four
-    const size_t ns = (size_t)P * 2 * kMaxValid;
-    js.sb24 = b.vg_split; js.se24 = b.vg_split + ns; js.sb32 = b.vg_split + 2 * ns; js.se32 = b.vg_split + 3 * ns;
-  }
-  // two large segments per instance; when the host knows both fit the fused kernel, its
-  // multi-kernel finish (four launches over empty segment lists) is not enqueued
-  const int fcap_s = P <= 4 || kVgFusedBatch ? 12288 : 0;
-  const bool fits = fcap_s > 0 && stack_max >= 0 && stack_max <= fcap_s;
-  b.note(vg_run(js, b.cub_tmp, b.cub_bytes, st, P <= 4 ? 1024 : 256, fcap_s, !fits));
+  js.out_count = b.sseg_cnt; js.nseg = 2 * P; js.total = P * b.cap_stack;
+  // two large segments per instance (the fused 12288-point kernel); when the host knows both fit
+  // (streaming), the cascade's finish is not enqueued
+  // (k_mp_stack zeroed the cascade's list counters)
+  js.zeroed = true;
+  const bool fits = stack_max >= 0 && stack_max <= 12288;
+  // batches: the corner stacks (<= 120 points per ring) take the 2048-point kernel, the surf
+  // stacks the 12288-point one; a few instances: one 12288-point launch
+  b.note(vg_run(js, st, P <= 4 ? 12288 : 2048, !fits, /*tier2_idx=*/true));
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);
   mark("k_mp_gather");
@@ -1822,14 +1919,14 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   hipLaunchKernelGGL(k_mp_vseg, dim3(P), dim3(kMpThreads), 0, st, b);
   hipLaunchKernelGGL(k_mp_vcopy, dim3(32, P), dim3(256), 0, st, b);
   mark("k_mp_vseg_vcopy");
-  VgJob jv;
+  VgJob jv = vg_job(b);
   jv.in = b.vin; jv.out = b.vout; jv.begin = b.vseg_b; jv.end = b.vseg_e; jv.leaf = b.vseg_leaf;
-  jv.out_count = b.vseg_cnt; jv.params = b.vg_params; jv.keys = b.vg_k; jv.keys_alt = b.vg_k2;
-  jv.vals = b.vg_v; jv.vals_alt = b.vg_v2; jv.big_b = b.vg_bb; jv.big_e = b.vg_be; jv.nseg = 2 * kMaxValid * P; jv.total = P * b.map_cap;
-  // a cube spans at most 50 m: <= 252 voxels of 0.2 m per axis, keys below 2^24 (three 8-bit passes)
-  jv.end_bit = 24;
-  jv.err = b.istate + kMiErr; jv.err_stride = kMpStateInts; jv.seg_per_err = 2 * kMaxValid;
-  b.note(vg_run(jv, b.cub_tmp, b.cub_bytes, st, P <= 4 || kVgCubeG256 ? 256 : 64, P <= 4 || kVgFusedBatch ? kVgCubeCap : 0));  // 2 x 125 cube segments per instance
+  jv.out_count = b.vseg_cnt; jv.nseg = 2 * kMaxValid * P; jv.total = P * b.map_cap;
+  // only the non-empty segments, listed by k_mp_vseg (k_mp_lm_end zeroed the counters)
+  jv.list = b.vg_lin; jv.list_n = b.vg_cnt + 2; jv.zeroed = true;
+  // 2 x 125 cube segments per instance, most of them small: batches start with the 2048-point
+  // kernel (many workgroups per CU); a few instances with the 12288-point one (one launch)
+  b.note(vg_run(jv, st, P <= 4 ? 12288 : 2048));
   mark("vg_cubes");
   hipLaunchKernelGGL(k_mp_compact_table<1024>, dim3(P), dim3(1024), 0, st, b);
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);
@@ -1969,6 +2066,7 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
 // segment (leaf 0.2, downSizeFilterCorner) over vin.
 __global__ __launch_bounds__(256) void k_mp_surround(MpBuffers b) {
   const int tid = threadIdx.x;
+  if (tid == 0) { b.vg_cnt[0] = 0; b.vg_cnt[1] = 0; }  // (its VoxelGrid's lists)
   const int* ist = b.istate;
   const int* slots = slot_table(b, b.pool_cur, 0);
   const float4* pool = b.pool + (size_t)b.pool_cur * b.P * b.map_cap;
@@ -2004,11 +2102,11 @@ __global__ __launch_bounds__(256) void k_mp_surround(MpBuffers b) {
 
 int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::string& err) {
   hipLaunchKernelGGL(k_mp_surround, dim3(1), dim3(256), 0, st, b);
-  VgJob j;
+  VgJob j = vg_job(b);
   j.in = b.vin; j.out = b.vout; j.begin = b.vseg_b; j.end = b.vseg_e; j.leaf = b.vseg_leaf;
-  j.out_count = b.vseg_cnt; j.params = b.vg_params; j.keys = b.vg_k; j.keys_alt = b.vg_k2;
-  j.vals = b.vg_v; j.vals_alt = b.vg_v2; j.big_b = b.vg_bb; j.big_e = b.vg_be; j.nseg = 1; j.total = b.P * b.map_cap;
-  b.note(vg_run(j, b.cub_tmp, b.cub_bytes, st, 1024, 12288));
+  j.out_count = b.vseg_cnt; j.nseg = 1; j.total = b.P * b.map_cap;
+  j.zeroed = true;  // (by k_mp_surround)
+  b.note(vg_run(j, st, 12288));
   int cnt = 0;
   hipError_t he = hipMemcpyAsync(&cnt, b.vseg_cnt, sizeof(int), hipMemcpyDeviceToHost, st);
   if (he == hipSuccess) he = hipStreamSynchronize(st);

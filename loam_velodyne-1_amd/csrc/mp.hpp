@@ -47,19 +47,20 @@ struct VgJob {
   const int* end;
   const float* leaf;     // per segment
   int* out_count;        // per segment
-  int* params;           // [nseg][8]: minb xyz, mul1, mul2, overflow
-  uint32_t *keys, *keys_alt, *vals, *vals_alt;
+  uint32_t *keys, *keys_alt, *vals, *vals_alt;  // k_vg_big's global sort arrays (indexed like in)
   int nseg;
   int total;             // size of in / out / keys arrays
-  int* big_b = nullptr;  // [nseg] segments beyond the fused kernel's LDS capacity (else empty),
-  int* big_e = nullptr;  //        finished by the multi-kernel path
-  int keep_counts = 0;   // multi-kernel path over big_b/big_e: leave other segments' counts alone
-  int end_bit = 32;      // voxel key bits the multi-kernel sort orders; a segment whose key range
-  int* err = nullptr;    //   exceeds it raises ERR_VG_BITS in err[(s / seg_per_err) * err_stride]
-  int err_stride = 0, seg_per_err = 1;
-  // split sort (when set): k_vg_params lists each segment in sb24/se24 when its keys fit 24 bits,
-  // else in sb32/se32; vg_run sorts the two lists separately (three / four 8-bit passes)
-  int *sb24 = nullptr, *se24 = nullptr, *sb32 = nullptr, *se32 = nullptr;
+  // vg_run's cascade: lists[0] / lists[1] ([nseg] segment ids) and their lengths counts[0] / [1]
+  // (device); a kernel processes every segment, or the ids of list / *list_n, and appends the
+  // segments beyond its capacity to big / *big_n
+  int* lists[2] = {nullptr, nullptr};
+  int* counts = nullptr;   // [3]: the two lists' lengths, and the length of the caller's input list
+  // set by the caller: counts[0] / counts[1] already zeroed by an earlier kernel on the stream
+  bool zeroed = false;
+  const int* list = nullptr;
+  const int* list_n = nullptr;
+  int* big = nullptr;
+  int* big_n = nullptr;
 };
 
 struct MpBuffers {
@@ -101,12 +102,10 @@ struct MpBuffers {
   float* vseg_leaf = nullptr;
   int *sseg_b = nullptr, *sseg_e = nullptr, *sseg_cnt = nullptr;  // [P][2] stack segments
   float* sseg_leaf = nullptr;
-  int* vg_params = nullptr;
   uint32_t *vg_k = nullptr, *vg_k2 = nullptr, *vg_v = nullptr, *vg_v2 = nullptr;
-  int *vg_bb = nullptr, *vg_be = nullptr;  // [P][2][kMaxValid] big-segment ranges of vg_run
-  int* vg_split = nullptr;                 // [4][P][2][kMaxValid] split-sort segment lists of vg_run
-  void* cub_tmp = nullptr;
-  size_t cub_bytes = 0;
+  int *vg_l0 = nullptr, *vg_l1 = nullptr;  // [P][2][kMaxValid] vg_run's segment lists
+  int* vg_lin = nullptr;                   // [P][2][kMaxValid] the non-empty cube segments (k_mp_vseg)
+  int* vg_cnt = nullptr;                   // [3] the lists' lengths (vg_l0, vg_l1, vg_lin)
   float4* reg = nullptr;      // [P][capS] registered full cloud
   double* part = nullptr;     // [P][kMpSmallGrid][28] k_mp_lm_small's per-workgroup JᵀJ | Jᵀb | rows
   int* done = nullptr;        // [P] its workgroups finished (the last one runs the step)
