@@ -55,6 +55,20 @@ LOAM_HD bool vg_leaf_too_small(const float* mn, const float* mx, float inv) {
   const int64_t xy = e[0] * e[1];  // each factor <= 2^31: no overflow
   return xy > (int64_t)0x7fffffff || xy * e[2] > (int64_t)0x7fffffff;
 }
+// Per-workgroup partials handed to the last workgroup to finish (k_od_rows_small, k_mp_lm_small,
+// k_mp_iter_wide), in the form MI355X_MICROARCH.md lists as valid without a per-workgroup release:
+// each partial stored write-through (agent-scope relaxed = sc1) and drained by its wave before the
+// workgroup barrier, then ONE lane's relaxed agent-scope add on the done counter; the last
+// workgroup (told by the add's return value) acquires at agent scope once and reads the partials
+// with sc1 loads.  A __threadfence() per workgroup (L2 write-back + invalidate) cost several us each.
+LOAM_D void store_partial(double* dst, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst), __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+LOAM_D bool arrive_last(int* done, int G) {  // one lane; true for the last of G arrivals
+  return __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
+}
 LOAM_HD double dsin(float x) { return sin((double)x); }
 LOAM_HD double dcos(float x) { return cos((double)x); }
 // sin and cos of one float argument in double; on the device one ocml sincos (the same argument

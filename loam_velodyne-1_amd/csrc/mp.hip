@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_prepare(MpBuffers b, MpInput 
         sl[at(nAx - 1)] = keep;
       }
     }
-    __threadfence();
+    __threadfence_block();  // (one workgroup: the next shift's lines are other threads')
     __syncthreads();
   }
   // FOV selection (:616-672) and FromMap prefix: thread c tests cube c of the 5x5x5
@@ -1332,19 +1332,17 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
   if (tid < 28) {
     double v = red[0][tid];
     for (int ww = 1; ww < kMpQueryThreads / 64; ++ww) v += red[ww][tid];
-    b.part[((size_t)p * kMpSmallGrid + blockIdx.x) * 28 + tid] = v;
-    __threadfence();  // partials visible device-wide before this workgroup reports done
+    store_partial(&b.part[((size_t)p * kMpSmallGrid + blockIdx.x) * 28 + tid], v);
   }
   __shared__ int sh_last;
   __shared__ double slice[8][28];
   __shared__ double tot[28];
   __shared__ MpStepScratch sh;
   __syncthreads();
-  // the done counter is an agent-scope acq_rel RMW, and the last workgroup's threads acquire at
-  // agent scope before reading the other workgroups' partials (they may sit on other XCDs)
-  // (measured against a relaxed counter without the fence: config 3 1.09 vs 1.10 ms per sweep, noise)
+  // (store_partial / arrive_last: the partials are drained write-through before the counter add;
+  // the last workgroup acquires at agent scope, then reads them with sc1 loads)
   if (tid == 0)
-    sh_last = __hip_atomic_fetch_add(&b.done[p], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
+    sh_last = arrive_last(&b.done[p], G);
   __syncthreads();
   if (!sh_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
