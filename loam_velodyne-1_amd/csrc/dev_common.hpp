@@ -28,6 +28,23 @@
 #define LOAM_CHECK(cond, a, b) ((void)0)
 #endif
 
+// Phase stamps of the last-workgroup kernels (k_od_rows_small, k_mp_lm_small): compiled in only by
+// the diagnostic build (tools/build_variant.sh NAME -DLOAM_PHASES, read by tools/phase_stream.py);
+// the product build has none.  Clock: s_memrealtime (100 MHz, one counter for the whole chip, so
+// stamps of different workgroups compare).  Per launch: sum[k][0] rows = last arrival - first
+// workgroup start, [1] hand-off (arrival -> after the acquire), [2] fixed-order partial sum, [3] the
+// step (6x6 solve, eigen at iteration 0), [4] sum over workgroups of (arrival - own start), [5]
+// workgroups, [6] launches; k = 0 for the first L-M iteration, 1 for the others.
+struct PhaseAcc {
+  unsigned long long s0;
+  unsigned long long sum[2][8];
+};
+#ifdef LOAM_PHASES
+#define LOAM_PH(...) __VA_ARGS__
+#else
+#define LOAM_PH(...)
+#endif
+
 namespace loamdev {
 
 constexpr int kWave = 64;
@@ -66,6 +83,27 @@ LOAM_D void store_partial(double* dst, double v) {
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
+#ifdef LOAM_PHASES
+LOAM_D unsigned long long ph_now() { return __builtin_amdgcn_s_memrealtime(); }
+// every workgroup at its start (one lane)
+LOAM_D void ph_start(PhaseAcc* a, unsigned long long t0) { atomicMin(&a->s0, t0); }
+// every workgroup at its arrival (one lane)
+LOAM_D void ph_arrive(PhaseAcc* a, int k, unsigned long long t0, unsigned long long t1) {
+  atomicAdd(&a->sum[k][4], t1 - t0);
+  atomicAdd(&a->sum[k][5], 1ull);
+}
+// the last workgroup once its step is done (one lane): the launch's phases, then s0 reset
+LOAM_D void ph_last(PhaseAcc* a, int k, unsigned long long t1, unsigned long long t2, unsigned long long t3,
+                    unsigned long long t4) {
+  const unsigned long long s0 = __hip_atomic_load(&a->s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  atomicAdd(&a->sum[k][0], t1 - s0);
+  atomicAdd(&a->sum[k][1], t2 - t1);
+  atomicAdd(&a->sum[k][2], t3 - t2);
+  atomicAdd(&a->sum[k][3], t4 - t3);
+  atomicAdd(&a->sum[k][6], 1ull);
+  __hip_atomic_store(&a->s0, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#endif
 LOAM_D bool arrive_last(int* done, int G) {  // one lane; true for the last of G arrivals
   return __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
 }

@@ -34,6 +34,10 @@
 using namespace loamdev;
 
 namespace loam {
+#ifdef LOAM_PHASES
+__device__ PhaseAcc g_ph_mp = {~0ull, {{0}}};
+#endif
+
 
 namespace {
 
@@ -1289,6 +1293,7 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
   const int p = blockIdx.y, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan] || ist[kMiStop]) return;
+  LOAM_PH(const unsigned long long ph0 = ph_now(); if (tid == 0) ph_start(&g_ph_mp, ph0);)
   const float* st = b.state + (size_t)p * kMpStateFloats;
   __shared__ uint32_t lists[27 * kMpQueryThreads];
   __shared__ float jac[kMpQueryThreads][27];
@@ -1339,6 +1344,8 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
   __shared__ double tot[28];
   __shared__ MpStepScratch sh;
   __syncthreads();
+  LOAM_PH(const int phk = first ? 0 : 1; const unsigned long long ph1 = ph_now();
+          if (tid == 0) ph_arrive(&g_ph_mp, phk, ph0, ph1);)
   // (store_partial / arrive_last: the partials are drained write-through before the counter add;
   // the last workgroup acquires at agent scope, then reads them with sc1 loads)
   if (tid == 0)
@@ -1346,6 +1353,7 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
   __syncthreads();
   if (!sh_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  LOAM_PH(const unsigned long long ph2 = ph_now();)
   if (tid < 8 * 28) {  // fixed-order sum: slice s holds partials s, s + 8, ... (all in flight)
     const int v = tid % 28, sl = tid / 28;
     const double* pp = b.part + (size_t)p * kMpSmallGrid * 28 + v;
@@ -1369,9 +1377,11 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
     tot[tid] = v;
   }
   __syncthreads();
+  LOAM_PH(const unsigned long long ph3 = ph_now();)
   if (tid < 64) {  // the first wave
     if (tid == 0) b.done[p] = 0;
     mp_step(b, p, tot, sh);
+    LOAM_PH(const unsigned long long ph4 = ph_now(); if (tid == 0) ph_last(&g_ph_mp, phk, ph1, ph2, ph3, ph4);)
   }
 }
 
@@ -2194,3 +2204,12 @@ int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats*
 }
 
 }  // namespace loam
+
+#ifdef LOAM_PHASES
+// the phase sums of the last-workgroup kernel of this file (PhaseAcc, dev_common.hpp); diagnostic
+// build only (tools/phase_stream.py)
+extern "C" int loam_debug_phases_mp(unsigned long long* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(loam::g_ph_mp), sizeof(PhaseAcc)) == hipSuccess ? 0 : -1;
+}
+#endif

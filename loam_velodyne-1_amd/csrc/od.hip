@@ -25,6 +25,10 @@
 using namespace loamdev;
 
 namespace loam {
+#ifdef LOAM_PHASES
+__device__ PhaseAcc g_ph_od = {~0ull, {{0}}};
+#endif
+
 
 namespace {
 
@@ -890,6 +894,7 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows_small(OdBuffers b, FeatV
   const int p = blockIdx.y, it = blockIdx.z, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const int* ist = b.istate + (size_t)p * kOdStateInts;
   if (!ist[kIsActive] || ist[kIsStop]) return;
+  LOAM_PH(const unsigned long long ph0 = ph_now(); if (tid == 0) ph_start(&g_ph_od, ph0);)
   __shared__ double red[kOdWaves][28];
   __shared__ float trig[6];
   const float* st = b.state + (size_t)p * kOdStateFloats;
@@ -936,6 +941,8 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows_small(OdBuffers b, FeatV
   __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs], jE[6], jV[36];
   __shared__ int lm_iws[12];
   __syncthreads();
+  LOAM_PH(const int phk = iter == 0 ? 0 : 1; const unsigned long long ph1 = ph_now();
+          if (tid == 0) ph_arrive(&g_ph_od, phk, ph0, ph1);)
   // (store_partial / arrive_last: the partials are drained write-through before the counter add;
   // the last workgroup acquires at agent scope, then reads them with sc1 loads)
   if (tid == 0)
@@ -943,6 +950,7 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows_small(OdBuffers b, FeatV
   __syncthreads();
   if (!sh_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  LOAM_PH(const unsigned long long ph2 = ph_now();)
   // fixed-order sum of the G partials: thread (slice s, value v) sums partials s, s + 8, ... with
   // all its loads in flight at once, then the eight slice sums are added in slice order
   __shared__ double slice[8][28];
@@ -972,9 +980,11 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows_small(OdBuffers b, FeatV
     tot[tid] = v;
   }
   __syncthreads();
+  LOAM_PH(const unsigned long long ph3 = ph_now();)
   if (tid < 64) {  // the first wave
     if (tid == 0) b.done[p] = 0;
     od_step(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
+    LOAM_PH(const unsigned long long ph4 = ph_now(); if (tid == 0) ph_last(&g_ph_od, phk, ph1, ph2, ph3, ph4);)
   }
 }
 
@@ -1177,3 +1187,12 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
 }
 }  // namespace loam
 
+
+#ifdef LOAM_PHASES
+// the phase sums of the last-workgroup kernel of this file (PhaseAcc, dev_common.hpp); diagnostic
+// build only (tools/phase_stream.py)
+extern "C" int loam_debug_phases_od(unsigned long long* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(loam::g_ph_od), sizeof(PhaseAcc)) == hipSuccess ? 0 : -1;
+}
+#endif

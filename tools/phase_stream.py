@@ -1,0 +1,81 @@
+"""In-kernel phase breakdown of the sequential node chain's two last-workgroup kernels (config 3,
+seed 1, 220 sweeps): k_od_rows_small (one launch per odometry L-M iteration) and k_mp_lm_small (one
+per mapping L-M iteration).  Needs the diagnostic build:
+
+    tools/build_variant.sh phases -DLOAM_PHASES
+    LOAM_HIP_LIB=loam_velodyne-1_amd/exp/phases.so python tools/phase_stream.py [out.json]   (GPU)
+
+Per launch, in microseconds (s_memrealtime, 100 MHz; PhaseAcc in csrc/dev_common.hpp):
+  rows      first workgroup start -> last workgroup's arrival (row work + dispatch spread)
+  wg_busy   mean over workgroups of (arrival - own start)
+  handoff   last arrival -> after the agent-scope acquire
+  psum      fixed-order sum of the partials
+  step      the 6x6 solve and transform update (iteration 0: + the eigen-analysis)
+The kernel's own duration (rocprofv3) minus rows + handoff + psum + step is dispatch and drain."""
+import ctypes
+import importlib
+import json
+import os
+import sys
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+
+
+def read(lib, name):
+    buf = (ctypes.c_ulonglong * 17)()
+    if getattr(lib, name)(buf) != 0:
+        raise RuntimeError(name)
+    return list(buf)
+
+
+def summarise(a):
+    out = {}
+    for k, tag in ((0, "iter0"), (1, "iter_rest")):
+        s = a[1 + 8 * k: 1 + 8 * k + 8]
+        n = max(s[6], 1)
+        out[tag] = {"launches": s[6], "rows_us": s[0] / n / 100, "handoff_us": s[1] / n / 100,
+                    "psum_us": s[2] / n / 100, "step_us": s[3] / n / 100,
+                    "wg_busy_us": s[4] / max(s[5], 1) / 100, "wgs_per_launch": s[5] / n}
+        out[tag]["sum_us"] = sum(out[tag][x] for x in ("rows_us", "handoff_us", "psum_us", "step_us"))
+    return out
+
+
+def main():
+    if "LOAM_HIP_LIB" not in os.environ:
+        sys.exit("set LOAM_HIP_LIB to the -DLOAM_PHASES build")
+    loam = importlib.import_module("loam_velodyne-1_amd")
+    sg = importlib.import_module("loam_velodyne-1_amd.synthgen")
+    sweeps = sg.stream_sweeps(220, 1)
+    e = loam.Engine(loam.default_config())
+    lib = ctypes.CDLL(os.environ["LOAM_HIP_LIB"])
+    for name in ("loam_debug_phases_od", "loam_debug_phases_mp"):
+        getattr(lib, name).argtypes = [ctypes.c_void_p]
+    # warm-up pass (first launches, allocations), then the measured pass on a fresh engine
+    base_od, base_mp = None, None
+    for rep in range(2):
+        if rep == 1:
+            e.close()
+            e = loam.Engine(loam.default_config())
+            base_od, base_mp = read(lib, "loam_debug_phases_od"), read(lib, "loam_debug_phases_mp")
+        for k, s in enumerate(sweeps):
+            rc, f = e.scan_registration(s, stamp=0.1 * k)
+            if rc:
+                continue
+            pub, pose, cl, sl, full = e.odometry(f, stamp=0.1 * k)
+            if pub == 7:
+                e.mapping(pose, cl, sl, full, stamp=0.1 * k)
+    od = [x - y for x, y in zip(read(lib, "loam_debug_phases_od"), base_od)]
+    mp = [x - y for x, y in zip(read(lib, "loam_debug_phases_mp"), base_mp)]
+    e.close()
+    res = {"workload": "config3 sequential, 220 sweeps (seed 1), one engine, second pass",
+           "clock": "s_memrealtime 100 MHz", "k_od_rows_small": summarise(od), "k_mp_lm_small": summarise(mp)}
+    txt = json.dumps(res, indent=1)
+    print(txt)
+    if len(sys.argv) > 1:
+        with open(sys.argv[1], "w") as fh:
+            fh.write(txt + "\n")
+
+
+if __name__ == "__main__":
+    main()
