@@ -1041,14 +1041,49 @@ LOAM_HD void gemm_d(const float* A, const float* B, int m, int k, int n, float* 
     }
 }
 
+// The iteration-0 degeneracy test (:770-797 odometry, :927-954 mapping) needs the eigenvectors only
+// when the smallest eigenvalue cv::eigen reports is below the threshold: otherwise isDegenerate is
+// false and matP is never used.  cv::eigen's float Jacobi returns eigenvalues within 2.4 eps_f
+// ||A||_inf of the exact ones (measured over 20 000 normal-equation-like matrices,
+// tests/test_oracle_components.py::test_jacobi_eigen_error_bound); so when A - (thr + D) I is
+// positive definite with D = 2^-14 ||A||_inf (~512 eps_f ||A||_inf), every eigenvalue the Jacobi
+// would return is >= thr, and the branch is decided without it.  Positive definiteness: an LDL^T in
+// double whose pivots must all be positive (backward error ~1e-15 ||A||, far inside D).  NaN / inf
+// entries, and any matrix near the threshold, are not certified: the caller runs the Jacobi.
+LOAM_HD bool nondegenerate_certified(const float* A, float thr) {
+  double nrm = 0.0;
+  for (int i = 0; i < 6; ++i) {
+    double rs = 0.0;
+    for (int j = 0; j < 6; ++j) rs += fabs((double)A[i * 6 + j]);
+    nrm = rs > nrm ? rs : nrm;
+  }
+  if (!(nrm < 1e30)) return false;
+  const double shift = (double)thr + nrm * 0x1p-14;
+  double L[6][6], d[6];
+  for (int j = 0; j < 6; ++j) {
+    double dj = (double)A[j * 6 + j] - shift;
+    for (int k = 0; k < j; ++k) dj -= L[j][k] * L[j][k] * d[k];
+    if (!(dj > 0.0)) return false;
+    d[j] = dj;
+    for (int i = j + 1; i < 6; ++i) {
+      double v = (double)A[i * 6 + j];
+      for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k] * d[k];
+      L[i][j] = v / dj;
+    }
+  }
+  return true;
+}
+
 // The L-M step on a reduced normal system (shared by odometry :765-826 and mapping :922-974):
 // AtA (6x6 float), AtB (6), iteration-0 degeneracy analysis.  One lane.
 // ws: >= kLmWs floats of scratch (LDS when called from a kernel lane), iws: >= 12 ints
 constexpr int kLmWs = 36 * 6 + 6 + 14 + 6;
-// pre_E / pre_V (optional): jacobi<6>(AtA) already computed (jacobi6_wave, by the caller's wave)
+// pre_E / pre_V (optional): jacobi<6>(AtA) already computed (jacobi6_wave, by the caller's wave).
+// certified: nondegenerate_certified(AtA, eig_thresh) held, so iteration 0 sets isDegenerate = 0
+// without the eigen-analysis (matP is left as it was: it is read only when isDegenerate is set)
 LOAM_HD void lm_step(const float* AtA_in, const float* AtB_in, int iter, float eig_thresh,
                      int* isDegenerate, float* matP, float* X, float* ws, int* iws,
-                     const float* pre_E = nullptr, const float* pre_V = nullptr) {
+                     const float* pre_E = nullptr, const float* pre_V = nullptr, bool certified = false) {
   // the QR solve of every iteration works in registers (fully unrolled, constant indices); the
   // iteration-0 analysis (pivoted Jacobi / LU, data-dependent indices) in ws
   float A[36], b[6], qws[14];
@@ -1061,7 +1096,9 @@ LOAM_HD void lm_step(const float* AtA_in, const float* AtB_in, int iter, float e
   for (int i = 0; i < 36; ++i) A[i] = AtA_in[i];
   for (int i = 0; i < 6; ++i) b[i] = AtB_in[i];
   qr_solve(A, b, 6, 6, X, qws);
-  if (iter == 0) {
+  if (iter == 0 && certified) {
+    *isDegenerate = 0;
+  } else if (iter == 0) {
     if (pre_E) {
       for (int i = 0; i < 6; ++i) E[i] = pre_E[i];
       for (int i = 0; i < 36; ++i) V[i] = pre_V[i];

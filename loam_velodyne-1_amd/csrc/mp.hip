@@ -1112,12 +1112,14 @@ LOAM_D void mp_step(const MpBuffers& b, int p, const double* tot, MpStepScratch&
       }
     for (int i = 0; i < 6; ++i) sh.AtB[i] = (float)tot[21 + i];
   }
-  const bool eig = nrows >= 50 && iter == 0;
+  bool eig = nrows >= 50 && iter == 0, cert = false;
   if (eig) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    loamla::jacobi6_wave(sh.AtA, sh.jE, sh.jV);
+    cert = loamla::nondegenerate_certified(sh.AtA, 100.0f);  // every lane, the same answer
+    eig = !cert;
+    if (eig) loamla::jacobi6_wave(sh.AtA, sh.jE, sh.jV);
   }
   if (lane != 0) return;
   ist[kMiIters] = iter + 1;
@@ -1125,7 +1127,7 @@ LOAM_D void mp_step(const MpBuffers& b, int p, const double* tot, MpStepScratch&
   if (nrows >= 50) {
     int degen = ist[kMiDegen];
     loamla::lm_step(sh.AtA, sh.AtB, iter, 100.0f, &degen, st + kMpMatP, sh.X, sh.lm_ws, sh.lm_iws,
-                    eig ? sh.jE : nullptr, eig ? sh.jV : nullptr);
+                    eig ? sh.jE : nullptr, eig ? sh.jV : nullptr, cert);
     ist[kMiDegen] = degen;
     if (degen) ist[kMiDegSteps] += 1;
     for (int q = 0; q < 6; ++q) st[kMpTobe + q] += sh.X[q];

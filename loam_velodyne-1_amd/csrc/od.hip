@@ -689,16 +689,19 @@ LOAM_D void od_step(const OdBuffers& b, int p, int iter, const double* tot, floa
     }
   }
   if (nrows < 10) return;
-  const bool eig = iter == 0;
+  bool eig = iter == 0, cert = false;
   if (eig) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    loamla::jacobi6_wave(AtA, jE, jV);
+    cert = loamla::nondegenerate_certified(AtA, 10.0f);  // every lane, the same answer
+    eig = !cert;
+    if (eig) loamla::jacobi6_wave(AtA, jE, jV);
   }
   if (lane != 0) return;
   int degen = ist[kIsDegenerate];
-  loamla::lm_step(AtA, AtB, iter, 10.0f, &degen, st + kOdMatP, X, lm_ws, lm_iws, eig ? jE : nullptr, eig ? jV : nullptr);
+  loamla::lm_step(AtA, AtB, iter, 10.0f, &degen, st + kOdMatP, X, lm_ws, lm_iws, eig ? jE : nullptr, eig ? jV : nullptr,
+                  cert);
   ist[kIsDegenerate] = degen;
   if (degen) ist[kIsDegSteps] += 1;
   const bool nan = isnan(X[0]) || isnan(X[1]) || isnan(X[2]) || isnan(X[3]) || isnan(X[4]) || isnan(X[5]);

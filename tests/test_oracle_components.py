@@ -123,6 +123,92 @@ def test_jacobi_eigen(oc, n):
                 assert c > 1 - 1e-3
 
 
+def _normal_matrices(rng, count):
+    """AtA-like 6x6 float matrices (sums of weighted rows with rotation / translation columns of
+    different scales), a quarter each: generic, one direction nearly removed, one column shrunk,
+    rescaled by 1e-2..1e2"""
+    for trial in range(count):
+        m = int(rng.integers(20, 3000))
+        J = rng.standard_normal((m, 6))
+        J[:, :3] *= rng.uniform(0.1, 30)
+        w = rng.uniform(0, 1, m)
+        kind = trial % 4
+        if kind == 1:
+            d = rng.standard_normal(6)
+            d /= np.linalg.norm(d)
+            J -= np.outer(J @ d, d) * rng.uniform(0.9, 1.0)
+        elif kind == 2:
+            J[:, rng.integers(0, 6)] *= rng.uniform(1e-3, 1e-1)
+        elif kind == 3:
+            J *= rng.uniform(1e-2, 1e2)
+        A = (J * w[:, None]).T @ J
+        yield _f32((A + A.T) / 2)
+
+
+def _certified(A, thr):
+    """numpy restatement of loamla::nondegenerate_certified (csrc/dev_common.hpp)"""
+    A = A.astype(np.float64)
+    nrm = np.abs(A).sum(1).max()
+    if not nrm < 1e30:
+        return False
+    M = A - (thr + nrm * 2.0 ** -14) * np.eye(6)
+    L = np.zeros((6, 6))
+    d = np.zeros(6)
+    for j in range(6):
+        dj = M[j, j] - sum(L[j, k] * L[j, k] * d[k] for k in range(j))
+        if not dj > 0:
+            return False
+        d[j] = dj
+        for i in range(j + 1, 6):
+            L[i, j] = (M[i, j] - sum(L[i, k] * L[j, k] * d[k] for k in range(j))) / dj
+    return True
+
+
+def test_jacobi_eigen_error_bound(oc):
+    """the bound behind skipping the iteration-0 eigen-analysis when it cannot change the outcome
+    (loamla::nondegenerate_certified): cv::eigen's float Jacobi (the oracle's restatement) returns
+    eigenvalues within 2.4 eps_f ||A||_inf of the exact ones on normal-equation-like matrices; the
+    certificate's margin, 2^-14 ||A||_inf ~ 512 eps_f, must stay >= 16x the worst error seen"""
+    rng = np.random.default_rng(11)
+    worst = 0.0
+    W = np.zeros(6, np.float32)
+    V = np.zeros((6, 6), np.float32)
+    for A in _normal_matrices(rng, 4000):
+        oc.lib().oracle_jacobi(A.ctypes.data, 6, W.ctypes.data, V.ctypes.data)
+        lam = np.linalg.eigvalsh(A.astype(np.float64))
+        worst = max(worst, np.abs(np.sort(W.astype(np.float64)) - lam).max() / np.abs(A.astype(np.float64)).sum(1).max())
+    assert worst * 16 <= 2.0 ** -14, worst
+
+
+@pytest.mark.parametrize("thr", [10.0, 100.0])
+def test_nondegenerate_certificate_decides_like_jacobi(oc, thr):
+    """whenever the certificate holds, the reference's test (smallest cv::eigen eigenvalue >= thr,
+    src/laserOdometry.cpp:776-783, src/laserMapping.cpp:933-940) finds no degenerate direction;
+    matrices placed just below the threshold are not certified, and those just above only when
+    their norm leaves the margin below the gap"""
+    rng = np.random.default_rng(12)
+    W = np.zeros(6, np.float32)
+    V = np.zeros((6, 6), np.float32)
+    n_cert = 0
+    mats = list(_normal_matrices(rng, 1500))
+    below = []
+    for i, A in enumerate(mats[:300]):   # the smallest eigenvalue moved to thr * (1 +- 1e-3)
+        ev, Q = np.linalg.eigh(A.astype(np.float64))
+        ev[0] = thr * (1 + (-1e-3 if i % 2 else 1e-3))
+        mats.append(_f32(Q @ np.diag(np.sort(ev)) @ Q.T))
+        if i % 2:
+            below.append(mats[-1])
+    for A in mats:
+        oc.lib().oracle_jacobi(A.ctypes.data, 6, W.ctypes.data, V.ctypes.data)
+        if _certified(A, thr):
+            n_cert += 1
+            assert W[5] >= thr, (W, thr)
+    for A in below:
+        assert not _certified(A, thr)
+    assert n_cert > 200
+    assert not _certified(np.full((6, 6), np.nan, np.float32), thr)
+
+
 def test_lu_inverse(oc):
     rng = np.random.default_rng(5)
     for _ in range(50):
