@@ -34,10 +34,12 @@
 // stamps of different workgroups compare).  Per launch: sum[k][0] rows = last arrival - first
 // workgroup start, [1] hand-off (arrival -> after the acquire), [2] fixed-order partial sum, [3] the
 // step (6x6 solve, eigen at iteration 0), [4] sum over workgroups of (arrival - own start), [5]
-// workgroups, [6] launches; k = 0 for the first L-M iteration, 1 for the others.
+// workgroups, [6] launches; k_mp_lm_small also [7] / [8] the sum over its query waves of the 5-NN
+// search / the fit + row time, [9] those waves, [10] the last workgroup start - s0, [11] the longest
+// query wave; k = 0 for the first L-M iteration, 1 for the others.
 struct PhaseAcc {
-  unsigned long long s0;
-  unsigned long long sum[2][8];
+  unsigned long long s0, s1, s2;  // per launch: first start, last start, longest query wave
+  unsigned long long sum[2][12];
 };
 #ifdef LOAM_PHASES
 #define LOAM_PH(...) __VA_ARGS__
@@ -86,16 +88,32 @@ LOAM_D void store_partial(double* dst, double v) {
 #ifdef LOAM_PHASES
 LOAM_D unsigned long long ph_now() { return __builtin_amdgcn_s_memrealtime(); }
 // every workgroup at its start (one lane)
-LOAM_D void ph_start(PhaseAcc* a, unsigned long long t0) { atomicMin(&a->s0, t0); }
+LOAM_D void ph_start(PhaseAcc* a, unsigned long long t0) {
+  atomicMin(&a->s0, t0);
+  atomicMax(&a->s1, t0);
+}
 // every workgroup at its arrival (one lane)
 LOAM_D void ph_arrive(PhaseAcc* a, int k, unsigned long long t0, unsigned long long t1) {
   atomicAdd(&a->sum[k][4], t1 - t0);
   atomicAdd(&a->sum[k][5], 1ull);
 }
+// a query wave's search / fit times (one lane)
+LOAM_D void ph_query(PhaseAcc* a, int k, unsigned long long tnn, unsigned long long tfit) {
+  atomicAdd(&a->sum[k][7], tnn);
+  atomicAdd(&a->sum[k][8], tfit);
+  atomicAdd(&a->sum[k][9], 1ull);
+  atomicMax(&a->s2, tnn + tfit);
+}
 // the last workgroup once its step is done (one lane): the launch's phases, then s0 reset
 LOAM_D void ph_last(PhaseAcc* a, int k, unsigned long long t1, unsigned long long t2, unsigned long long t3,
                     unsigned long long t4) {
   const unsigned long long s0 = __hip_atomic_load(&a->s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long s1 = __hip_atomic_load(&a->s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long s2 = __hip_atomic_load(&a->s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  atomicAdd(&a->sum[k][10], s1 - s0);
+  atomicAdd(&a->sum[k][11], s2);
+  __hip_atomic_store(&a->s1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&a->s2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   atomicAdd(&a->sum[k][0], t1 - s0);
   atomicAdd(&a->sum[k][1], t2 - t1);
   atomicAdd(&a->sum[k][2], t3 - t2);

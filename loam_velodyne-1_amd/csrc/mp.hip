@@ -35,7 +35,7 @@ using namespace loamdev;
 
 namespace loam {
 #ifdef LOAM_PHASES
-__device__ PhaseAcc g_ph_mp = {~0ull, {{0}}};
+__device__ PhaseAcc g_ph_mp = {~0ull, 0ull, 0ull, {{0}}};
 #endif
 
 
@@ -786,7 +786,20 @@ LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t, i
   }
 }
 
+// largest batch whose mapping L-M takes the one-launch-per-iteration kernel (k_mp_lm_small)
+#ifndef LOAM_MP_SMALL_MAX
+#define LOAM_MP_SMALL_MAX 4
+#endif
+// largest batch whose k_mp_fit adds the rows and runs the step in its last workgroup (no k_mp_iter)
+#ifndef LOAM_MP_FUSED_MAX
+#define LOAM_MP_FUSED_MAX 128  // (measured at batch 128: fit + iter 0.66 -> 0.58 ms/step; at 1024 1.71 -> 2.22)
+#endif
 constexpr int kMpQueryThreads = 256;
+// lanes per query in k_mp_lm_small (streaming: the per-query search chain is the latency)
+#ifndef LOAM_MP_NN_LANES
+#define LOAM_MP_NN_LANES 8  // (config 3 sequential ms/sweep: 1 -> 0.972, 2 -> 1.009, 4 -> 0.943, 8 -> 0.933)
+#endif
+constexpr int kMpNnLanes = LOAM_MP_NN_LANES;
 // k_mp_nn workgroup size (measured k_mp_nn ms/step at batch 1024: 64 -> 3.83, 128 -> 3.81-3.86,
 // 256 -> 3.92-3.95): a workgroup's LDS is released when its slowest lane is done
 constexpr int kMpNnThreads = 128;
@@ -800,8 +813,12 @@ constexpr int kMpFitThreads = 64;
 // the lane's LDS column (stride kMpQueryThreads).  Ranges are packed start:19 | count:13; a lane
 // whose ranges do not fit falls back to knn5.
 constexpr int kNnInFlight = 8;  // measured k_mp_nn ms/step: 2 -> 4.17, 4 -> 3.95, 8 -> 3.88, 16 -> 5.33
-template <int S = kMpQueryThreads>
-LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5& t, uint32_t* lst, int& work) {
+// L > 1: one of L lanes searching the same query: every lane lists the same cells, lane `sub`
+// takes the candidates sub, sub + L, ... of the concatenated list (a crowded cell is shared too);
+// the caller merges the L partial top-5 lists (knn5_merge)
+template <int S = kMpQueryThreads, int L = 1>
+LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5& t, uint32_t* lst, int& work,
+                      int sub = 0) {
   if (T <= 0) return;
   const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
   const float gxl = q.x - (float)cx, gyl = q.y - (float)cy, gzl = q.z - (float)cz;
@@ -846,10 +863,33 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
     --left;
     return pos++;
   };
-  for (int k = 0; k < total; k += kNnInFlight) {  // independent gathers in flight per step
+  auto skip = [&](int m) {  // pass over m candidates (the other lanes' share)
+    while (m > 0) {
+      if (left == 0) {
+        const uint32_t e = lst[ci * S];
+        ++ci;
+        pos = (int)(e & ((1u << 19) - 1));
+        left = (int)(e >> 19);
+      }
+      const int s = min(m, left);
+      pos += s;
+      left -= s;
+      m -= s;
+    }
+  };
+  const int mine = L == 1 ? total : (total > sub ? (total - sub + L - 1) / L : 0);
+  if (L > 1 && mine > 0) skip(sub);  // (mine > 0: the list holds more than sub candidates)
+  for (int k = 0; k < mine; k += kNnInFlight) {  // independent gathers in flight per step
     int idx[kNnInFlight];
 #pragma unroll
-    for (int u = 0; u < kNnInFlight; ++u) idx[u] = k + u < total ? next() : idx[0];
+    for (int u = 0; u < kNnInFlight; ++u) {
+      if (k + u < mine) {
+        idx[u] = next();
+        if (L > 1 && k + u + 1 < mine) skip(L - 1);
+      } else {
+        idx[u] = idx[0];
+      }
+    }
 #ifdef LOAM_BOUNDS_CHECK
     for (int u = 0; u < kNnInFlight; ++u) LOAM_CHECK(idx[u] >= 0 && idx[u] < (1 << 19) + (1 << 13), idx[u], total);
 #endif
@@ -858,7 +898,28 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
     for (int u = 0; u < kNnInFlight; ++u) a[u] = hp[idx[u]];
 #pragma unroll
     for (int u = 0; u < kNnInFlight; ++u)
-      if (k + u < total) top5_offer(t, sqdist(a[u].x, a[u].y, a[u].z, q.x, q.y, q.z), __builtin_bit_cast(int, a[u].w));
+      if (k + u < mine) top5_offer(t, sqdist(a[u].x, a[u].y, a[u].z, q.x, q.y, q.z), __builtin_bit_cast(int, a[u].w));
+  }
+}
+
+// the L lanes of a query group (aligned, consecutive) exchange their top-5 lists in log2(L)
+// butterfly rounds; top5_offer keeps the 5 smallest (distance, index) of the union without
+// duplicates, which does not depend on the order of the offers, so every lane of the group ends
+// with the list a single lane's search over all the cells would have found
+template <int L>
+LOAM_D void knn5_merge(Top5& t) {
+#pragma unroll
+  for (int m = 1; m < L; m <<= 1) {
+    float od[5];
+    int oi[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      od[k] = __shfl_xor(t.d[k], m, 64);
+      oi[k] = __shfl_xor(t.i[k], m, 64);
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      if (oi[k] != 0x7fffffff) top5_offer(t, od[k], oi[k]);
   }
 }
 
@@ -928,9 +989,9 @@ LOAM_D MpNnCtx mp_nn_ctx(const MpBuffers& b, int p) {
   return c;
 }
 
-template <int S = kMpQueryThreads>
+template <int S = kMpQueryThreads, int L = 1>
 LOAM_D void mp_nn_query(const MpBuffers& b, const MpNnCtx& c, int q, int nsc, bool first, const loampose::MapRot& r,
-                        uint32_t* lst, float4& sel, Top5& t, int& work) {
+                        uint32_t* lst, float4& sel, Top5& t, int& work, int sub = 0) {
   const bool corner = q < nsc;
   int4* qnn = c.qnn;
   sel = loampose::point_to_map(r, c.stack[corner ? q : b.capC + (q - nsc)]);
@@ -949,11 +1010,14 @@ LOAM_D void mp_nn_query(const MpBuffers& b, const MpNnCtx& c, int q, int nsc, bo
         ++work;
       }
   }
-  if (corner) knn5_flat<S>(c.hcs, c.hcp, c.TC, sel, t, lst, work);
-  else knn5_flat<S>(c.hss, c.hsp, c.TS, sel, t, lst, work);
+  if (corner) knn5_flat<S, L>(c.hcs, c.hcp, c.TC, sel, t, lst, work, sub);
+  else knn5_flat<S, L>(c.hss, c.hsp, c.TS, sel, t, lst, work, sub);
+  if constexpr (L > 1) knn5_merge<L>(t);
   LOAM_CHECK(q < b.cap_stack && (t.i[4] == 0x7fffffff || t.i[4] < (corner ? c.nfc : c.nfs)), q, t.i[4]);
-  qnn[2 * q] = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
-  qnn[2 * q + 1] = make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0);
+  if (sub == 0) {
+    qnn[2 * q] = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
+    qnn[2 * q + 1] = make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0);
+  }
 }
 
 // jw: this lane's 27 words of LDS scratch for the 3x3 Jacobi
@@ -1050,16 +1114,15 @@ LOAM_D void mp_fit_query(const MpBuffers& b, int p, int q, int nsc, bool first, 
 }
 
 // sin / cos of the TobeMapped rotation for the rows
-LOAM_D void mp_trig(const float* st, float* trig) {
-  for (int k = 0; k < 3; ++k) {
-    trig[2 * k] = (float)dsin(st[kMpTobe + k]);
-    trig[2 * k + 1] = (float)dcos(st[kMpTobe + k]);
-  }
-}
 struct MpTrig {
   float srx, crx, sry, cry, srz, crz;
 };
 LOAM_D MpTrig mp_trig_of(const float* trig) { return {trig[0], trig[1], trig[2], trig[3], trig[4], trig[5]}; }
+// the same values from the stored rotation (rot_store: dsin / dcos of the same TobeMapped angles),
+// without the serial double sin / cos in the kernel prologue
+LOAM_D MpTrig mp_trig_of(const loampose::MapRot& r) {
+  return {(float)r.s0, (float)r.c0, (float)r.s1, (float)r.c1, (float)r.s2, (float)r.c2};
+}
 
 LOAM_D void mp_row_accum(const MpTrig& tg, float4 o, float4 c, double (&acc)[28]) {
   const float srx = tg.srx, crx = tg.crx, sry = tg.sry, cry = tg.cry, srz = tg.srz, crz = tg.crz;
@@ -1169,6 +1232,10 @@ __global__ __launch_bounds__(kMpNnThreads) __attribute__((amdgpu_waves_per_eu(5)
   }
 }
 
+// FUSED: each lane also adds its accepted row (as k_mp_lm_small does), the workgroup's fp64 partial
+// is stored write-through, and the last workgroup of the instance sums the partials in order and
+// runs the step: no k_mp_iter launch.
+template <bool FUSED>
 __global__ __launch_bounds__(kMpFitThreads) void k_mp_fit(MpBuffers b) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, tid = threadIdx.x;
@@ -1187,20 +1254,67 @@ __global__ __launch_bounds__(kMpFitThreads) void k_mp_fit(MpBuffers b) {
   const loampose::MapRot r = rot_load(b, p);
   float* jw = jac[tid];
   int nfits = 0;
+  double acc[FUSED ? 28 : 1];
+  const MpTrig tg = mp_trig_of(r);
+  if constexpr (FUSED) {
+#pragma unroll
+    for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+  }
   for (int q = blk.x * kMpFitThreads + tid; q < nq; q += gridDim.x * kMpFitThreads) {
     const bool corner = q < nsc;
     const int4 n0 = qnn[2 * q], n1 = qnn[2 * q + 1];
-    float4 sel = make_float4(0, 0, 0, 0);
-    if (n1.x != 0x7fffffff && D(__int_as_float(n1.y)) < 1.0)
-      sel = loampose::point_to_map(r, stack[corner ? q : b.capC + (q - nsc)]);
+    float4 sel = make_float4(0, 0, 0, 0), o = sel;
+    if (n1.x != 0x7fffffff && D(__int_as_float(n1.y)) < 1.0) {  // (a row needs a fit: ok implies this)
+      o = stack[corner ? q : b.capC + (q - nsc)];
+      sel = loampose::point_to_map(r, o);
+    }
     float4 cf;
     int ok;
     mp_fit_query(b, p, q, nsc, first, n0, n1, sel, jw, nfits, cf, ok);
     qok[q] = (int8_t)ok;
     qcf[q] = cf;
+    if constexpr (FUSED)
+      if (ok) mp_row_accum(tg, o, cf, acc);
   }
   nfits = wave_sum(nfits);
   if (lane_id() == 0 && nfits) atomicAdd(&ist[kMiFits], nfits);
+  if constexpr (FUSED) {
+    static_assert(kMpFitThreads == 64, "one wave per workgroup: the wave's sums are the partial");
+    const int lane = lane_id();
+    wave_reduce_scatter_28(acc);  // lanes 2v, 2v+1: the sum of value v
+    const int G = (int)gridDim.x;
+    if ((lane & 1) == 0 && (lane >> 1) < 28)
+      store_partial(&b.part[((size_t)p * kMpFitGridMax + blk.x) * 28 + (lane >> 1)], acc[0]);
+    __shared__ int sh_last;
+    __shared__ double tot[28];
+    __shared__ MpStepScratch sh;
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) sh_last = arrive_last(&b.done[p], G);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (!sh_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (lane < 28) {  // fixed order over the workgroups, eight in flight per step
+      const double* pp = b.part + (size_t)p * kMpFitGridMax * 28 + lane;
+      double v = 0.0;
+      for (int g = 0; g < G; g += 8) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          t[u] = g + u < G ? __hip_atomic_load(&pp[(size_t)(g + u) * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (g + u < G) v += t[u];
+      }
+      tot[lane] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (lane == 0) b.done[p] = 0;
+    mp_step(b, p, tot, sh);
+  }
 }
 
 namespace {
@@ -1218,21 +1332,14 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
   const int p = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan] || ist[kMiStop]) return;
-  float* st = b.state + (size_t)p * kMpStateFloats;
   __shared__ MpIterShared sh;
   const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
   const int nq = nsc + nss;
   const float4* stack = b.stack + (size_t)p * b.cap_stack;
   const int8_t* qok = b.q_ok + (size_t)p * b.cap_stack;
   const float4* qcf = b.q_cf + (size_t)p * b.cap_stack;
-  if (tid == 0)
-    for (int k = 0; k < 3; ++k) {
-      sh.trig[2 * k] = (float)dsin(st[kMpTobe + k]);
-      sh.trig[2 * k + 1] = (float)dcos(st[kMpTobe + k]);
-    }
-  __syncthreads();
-  const float srx = sh.trig[0], crx = sh.trig[1], sry = sh.trig[2], cry = sh.trig[3], srz = sh.trig[4],
-              crz = sh.trig[5];
+  const MpTrig tg = mp_trig_of(rot_load(b, p));
+  const float srx = tg.srx, crx = tg.crx, sry = tg.sry, cry = tg.cry, srz = tg.srz, crz = tg.crz;
   double acc[28];
 #pragma unroll
   for (int k = 0; k < 28; ++k) acc[k] = 0.0;
@@ -1296,39 +1403,44 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
   int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan] || ist[kMiStop]) return;
   LOAM_PH(const unsigned long long ph0 = ph_now(); if (tid == 0) ph_start(&g_ph_mp, ph0);)
-  const float* st = b.state + (size_t)p * kMpStateFloats;
   __shared__ uint32_t lists[27 * kMpQueryThreads];
   __shared__ float jac[kMpQueryThreads][27];
   __shared__ double red[kMpQueryThreads / 64][28];
-  __shared__ float trig[6];
   const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
   const int nq = nsc + nss;
   const float4* stack = b.stack + (size_t)p * b.cap_stack;
   int8_t* qok = b.q_ok + (size_t)p * b.cap_stack;
   float4* qcf = b.q_cf + (size_t)p * b.cap_stack;
   const bool first = ist[kMiIters] == 0;
-  if (tid == 0) mp_trig(st, trig);
   const loampose::MapRot r = rot_load(b, p);
   const MpNnCtx c = mp_nn_ctx(b, p);
   int work = 0, nfits = 0;  // (work: the batch kernel's profiling counter; not summed here)
-  __syncthreads();  // trig
-  const MpTrig tg = mp_trig_of(trig);
+  const MpTrig tg = mp_trig_of(r);
   double acc[28];
 #pragma unroll
   for (int k = 0; k < 28; ++k) acc[k] = 0.0;
   // each lane's row is added right after its fit (same queries, same order per lane as a
   // separate pass over the stored rows: identical sums, one reload round trip fewer)
-  for (int q = blockIdx.x * kMpQueryThreads + tid; q < nq; q += gridDim.x * kMpQueryThreads) {
+  // kMpNnLanes lanes per query: the 5-NN search split over the group, the fit and row on its first lane
+  constexpr int L = kMpNnLanes, QPB = kMpQueryThreads / L;
+  const int sub = tid % L;
+  for (int q = blockIdx.x * QPB + tid / L; q < nq; q += gridDim.x * QPB) {
+    LOAM_PH(const unsigned long long pq0 = ph_now();)
     float4 sel;
     Top5 t;
-    mp_nn_query(b, c, q, nsc, first, r, lists + tid, sel, t, work);
-    float4 cf;
-    int ok;
-    mp_fit_query(b, p, q, nsc, first, make_int4(t.i[0], t.i[1], t.i[2], t.i[3]),
-                 make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0), sel, jac[tid], nfits, cf, ok);
-    qok[q] = (int8_t)ok;
-    qcf[q] = cf;
-    if (ok) mp_row_accum(tg, stack[q < nsc ? q : b.capC + (q - nsc)], cf, acc);
+    mp_nn_query<kMpQueryThreads, L>(b, c, q, nsc, first, r, lists + tid, sel, t, work, sub);
+    LOAM_PH(asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); const unsigned long long pq1 = ph_now();)
+    float4 cf = make_float4(0, 0, 0, 0);
+    int ok = 0;
+    if (sub == 0) {
+      mp_fit_query(b, p, q, nsc, first, make_int4(t.i[0], t.i[1], t.i[2], t.i[3]),
+                   make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0), sel, jac[tid], nfits, cf, ok);
+      qok[q] = (int8_t)ok;
+      qcf[q] = cf;
+      if (ok) mp_row_accum(tg, stack[q < nsc ? q : b.capC + (q - nsc)], cf, acc);
+    }
+    LOAM_PH(asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); const unsigned long long pq2 = ph_now();
+            if (lane == 0) ph_query(&g_ph_mp, first ? 0 : 1, pq1 - pq0, pq2 - pq1);)
   }
   nfits = wave_sum(nfits);
   if (lane == 0 && nfits) atomicAdd(&ist[kMiFits], nfits);
@@ -1826,7 +1938,7 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
   A(&b.vg_lin, (size_t)P * 2 * kMaxValid * sizeof(int));
   A(&b.vg_cnt, 3 * sizeof(int));
   A(&b.reg, (size_t)P * b.capS * sizeof(float4));
-  A(&b.part, (size_t)P * kMpSmallGrid * 28 * sizeof(double));
+  A(&b.part, (size_t)P * std::max(kMpSmallGrid, kMpFitGridMax) * 28 * sizeof(double));
   A(&b.rot, (size_t)P * 6 * sizeof(double));
   A(&b.done, (size_t)P * sizeof(int));
   A(&b.nreg, (size_t)P * sizeof(int));
@@ -1906,7 +2018,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   const int gq = std::min(P >= 64 ? 24 : 64, (b.cap_stack + kMpQueryThreads - 1) / kMpQueryThreads);
   // an empty map store (the first frame after a reset) cannot run the L-M (:706): no launches
   for (int it = 0; it < (map_empty ? 0 : b.max_iter); ++it) {
-    if (P <= 4) {  // small batches: one launch per iteration
+    if (P <= LOAM_MP_SMALL_MAX) {  // small batches: one launch per iteration
       hipLaunchKernelGGL(k_mp_lm_small, dim3(kMpSmallGrid, P), dim3(kMpQueryThreads), 0, st, b);
       mark("k_mp_lm_small");
       continue;
@@ -1915,7 +2027,13 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     if (prof) hipLaunchKernelGGL(k_mp_nn<true>, dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
     else hipLaunchKernelGGL(k_mp_nn<false>, dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
     mark("k_mp_nn");
-    hipLaunchKernelGGL(k_mp_fit, dim3(gq * (kMpQueryThreads / kMpFitThreads), P), dim3(kMpFitThreads), 0, st, b);
+    const int gfit = gq * (kMpQueryThreads / kMpFitThreads);
+    if (P <= LOAM_MP_FUSED_MAX && gfit <= kMpFitGridMax) {
+      hipLaunchKernelGGL(k_mp_fit<true>, dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+      mark("k_mp_fit");
+      continue;
+    }
+    hipLaunchKernelGGL(k_mp_fit<false>, dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
     mark("k_mp_fit");
     hipLaunchKernelGGL(k_mp_iter, dim3(P), dim3(kMpThreads), 0, st, b);
     mark("k_mp_iter");

@@ -15,7 +15,8 @@ namespace loam {
 // cube grid of src/laserMapping.cpp:64-70
 constexpr int kCubeW = 21, kCubeH = 11, kCubeD = 21, kCubeNum = kCubeW * kCubeH * kCubeD;
 constexpr int kMaxValid = 125;
-constexpr int kMpSmallGrid = 64;  // workgroups per instance of the small-batch L-M iteration (multiple of 8)
+constexpr int kMpFitGridMax = 256;  // k_mp_fit<true> workgroups per instance (partials per instance)
+constexpr int kMpSmallGrid = 256;  // workgroups per instance of the small-batch L-M iteration (multiple of 8)
 
 // per-instance float state: Sum | Incre | TobeMapped | Bef | Aft | matP[36] | pointOnYAxis[3]
 constexpr int kMpSum = 0, kMpIncre = 6, kMpTobe = 12, kMpBef = 18, kMpAft = 24, kMpMatP = 30, kMpOnY = 66,

@@ -24,9 +24,18 @@
 
 using namespace loamdev;
 
+// largest batch whose odometry rows + step take the fused last-workgroup kernel (k_od_rows_small)
+#ifndef LOAM_OD_SMALL_MAX
+#define LOAM_OD_SMALL_MAX 63
+#endif
+// largest batch whose k_od_rows runs the step in its last workgroup (no k_od_step launches)
+#ifndef LOAM_OD_FUSED_MAX
+#define LOAM_OD_FUSED_MAX 0  // (measured at batch 128: rows + step 0.67 -> 0.62 ms/step, whole step unchanged; 1024 slower)
+#endif
+
 namespace loam {
 #ifdef LOAM_PHASES
-__device__ PhaseAcc g_ph_od = {~0ull, {{0}}};
+__device__ PhaseAcc g_ph_od = {~0ull, 0ull, 0ull, {{0}}};
 #endif
 
 
@@ -828,7 +837,10 @@ LOAM_D void od_trig(const float* T, float* trig) {
 // then the Jacobian of every row accumulated so far (Q12: rows of iterations 0..iter, all
 // evaluated at the current transform, :708-764) summed in fp64 into this workgroup's partial
 // JᵀJ / Jᵀb / row count; k_od_step sums the partials.  Large batches.
+// FUSED: the last workgroup of the problem to finish sums the gq partials (in k_od_step's order)
+// and runs the step itself, instead of a k_od_step launch per iteration.
 constexpr int kOdRowsWpe = 4;  // <= 128 VGPRs with two rows' loads in flight
+template <bool FUSED>
 __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdRowsWpe))) void k_od_rows(OdBuffers b, FeatView f, int last_buf, int iter) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
@@ -884,7 +896,41 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdR
   if (tid < 28) {
     double v = red[0][tid];
     for (int ww = 1; ww < kOdWaves; ++ww) v += red[ww][tid];
-    b.part[((size_t)p * b.gq + blk.x) * 28 + tid] = v;
+    if (FUSED) store_partial(&b.part[((size_t)p * b.gq + blk.x) * 28 + tid], v);
+    else b.part[((size_t)p * b.gq + blk.x) * 28 + tid] = v;
+  }
+  if constexpr (FUSED) {
+    __shared__ int sh_last;
+    __shared__ double tot[28];
+    __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs], jE[6], jV[36];
+    __shared__ int lm_iws[12];
+    __syncthreads();
+    // (store_partial / arrive_last: write-through partials, relaxed counter; the last workgroup
+    // acquires at agent scope, then reads them with sc1 loads)
+    if (tid == 0) sh_last = arrive_last(&b.done[p], b.gq);
+    __syncthreads();
+    if (!sh_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (tid < 28) {  // k_od_step's fixed order over the workgroups; eight partials in flight per step
+      double v = 0.0;
+      const double* pp = b.part + (size_t)p * b.gq * 28 + tid;
+      for (int g = 0; g < b.gq; g += 8) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          t[u] = g + u < b.gq ? __hip_atomic_load(&pp[(size_t)(g + u) * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (g + u < b.gq) v += t[u];
+      }
+      tot[tid] = v;
+    }
+    __syncthreads();
+    if (tid < 64) {  // the first wave
+      if (tid == 0) b.done[p] = 0;
+      od_step(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
+    }
   }
 }
 
@@ -1098,7 +1144,7 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   A(&b.q_cf, (size_t)P * max_iter * b.cap_q * sizeof(float4));
   A(&b.q_ok, (size_t)P * max_iter * b.cap_q * sizeof(int8_t));
   // per-workgroup partials: [P][gq][28], or [P][gq * max_iter][28] for the small-batch rows kernel
-  A(&b.part, (size_t)P * b.gq * (P < 64 ? max_iter : 1) * 28 * sizeof(double));
+  A(&b.part, (size_t)P * b.gq * (P <= LOAM_OD_SMALL_MAX ? max_iter : 1) * 28 * sizeof(double));
   A(&b.done, (size_t)P * sizeof(int));
   if (A.err != hipSuccess) {
     od_free(b);
@@ -1176,14 +1222,19 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
       }
       mark("k_od_assoc");
     }
-    if (P < 64) {  // measured: the fused step loses for large batches (its serial tail)
+    if (P <= LOAM_OD_SMALL_MAX) {  // measured: the fused step loses for large batches (its serial tail)
       hipLaunchKernelGGL(k_od_rows_small, dim3(b.gq, P, it + 1), dim3(kOdThreads), 0, st, b, f, last_buf, it);
       mark("k_od_rows");
     } else {
-      hipLaunchKernelGGL(k_od_rows, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
-      mark("k_od_rows");
-      hipLaunchKernelGGL(k_od_step, dim3(P), dim3(64), 0, st, b, it, b.gq);
-      mark("k_od_step");
+      if (P <= LOAM_OD_FUSED_MAX) {
+        hipLaunchKernelGGL(k_od_rows<true>, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+        mark("k_od_rows");
+      } else {
+        hipLaunchKernelGGL(k_od_rows<false>, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+        mark("k_od_rows");
+        hipLaunchKernelGGL(k_od_step, dim3(P), dim3(64), 0, st, b, it, b.gq);
+        mark("k_od_step");
+      }
     }
   }
   if (device_fini) hipLaunchKernelGGL(k_od_fini, dim3((P + 255) / 256), dim3(256), 0, st, b, f);

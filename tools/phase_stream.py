@@ -8,9 +8,12 @@ per mapping L-M iteration).  Needs the diagnostic build:
 Per launch, in microseconds (s_memrealtime, 100 MHz; PhaseAcc in csrc/dev_common.hpp):
   rows      first workgroup start -> last workgroup's arrival (row work + dispatch spread)
   wg_busy   mean over workgroups of (arrival - own start)
+  start_spread  last workgroup start - first workgroup start
   handoff   last arrival -> after the agent-scope acquire
   psum      fixed-order sum of the partials
   step      the 6x6 solve and transform update (iteration 0: + the eigen-analysis)
+  query_wave_nn_us / query_wave_fit_row_us (k_mp_lm_small): per query wave, the 5-NN search and
+            the fit + row, each up to its last load
 The kernel's own duration (rocprofv3) minus rows + handoff + psum + step is dispatch and drain."""
 import ctypes
 import importlib
@@ -23,7 +26,7 @@ sys.path.insert(0, ROOT)
 
 
 def read(lib, name):
-    buf = (ctypes.c_ulonglong * 17)()
+    buf = (ctypes.c_ulonglong * 27)()
     if getattr(lib, name)(buf) != 0:
         raise RuntimeError(name)
     return list(buf)
@@ -32,12 +35,18 @@ def read(lib, name):
 def summarise(a):
     out = {}
     for k, tag in ((0, "iter0"), (1, "iter_rest")):
-        s = a[1 + 8 * k: 1 + 8 * k + 8]
+        s = a[3 + 12 * k: 3 + 12 * k + 12]
         n = max(s[6], 1)
         out[tag] = {"launches": s[6], "rows_us": s[0] / n / 100, "handoff_us": s[1] / n / 100,
                     "psum_us": s[2] / n / 100, "step_us": s[3] / n / 100,
-                    "wg_busy_us": s[4] / max(s[5], 1) / 100, "wgs_per_launch": s[5] / n}
+                    "wg_busy_us": s[4] / max(s[5], 1) / 100, "wgs_per_launch": s[5] / n,
+                    "start_spread_us": s[10] / n / 100}
         out[tag]["sum_us"] = sum(out[tag][x] for x in ("rows_us", "handoff_us", "psum_us", "step_us"))
+        if s[9]:
+            out[tag]["query_wave_nn_us"] = s[7] / s[9] / 100
+            out[tag]["query_wave_fit_row_us"] = s[8] / s[9] / 100
+            out[tag]["query_waves_per_launch"] = s[9] / n
+            out[tag]["longest_query_wave_us"] = s[11] / n / 100
     return out
 
 
