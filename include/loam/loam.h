@@ -154,6 +154,23 @@ int loam_mapping(loam_ctx *ctx, double stamp, const loam_pose6 *odom_sum,
  * frame left; a LOAM_E_CAPACITY call may be repeated with more capacity). */
 int loam_mapping_surround(loam_ctx *ctx, loam_cloud_out *out, int *published);
 
+/* ---- device-resident node chain (no reference equivalent: the reference's nodes exchange ROS
+ * messages; this is the intra-process / nodelet deployment of the same three bodies) ----
+ * One sweep through loam_scan_registration -> loam_odometry -> loam_mapping (on the frames odometry
+ * publishes all three clouds, as the node graph does) on one context, the intermediate topics left
+ * in device memory: odometry reads scan registration's output buffers in place, mapping reads
+ * odometry's published CornerLast / SurfLast / full-end buffers in place.  Same kernels, same values
+ * as the three message calls; loam_mapping_surround works after it as after loam_mapping.
+ * Returns LOAM_E_NOT_READY inside system_delay.  registered: capacity 0 = not downloaded. */
+typedef struct {
+  int32_t published;          /* loam_odometry's LOAM_PUB_* flags for this sweep */
+  int32_t mapped;             /* 1 when laserMapping ran on this sweep */
+  loam_pose6 od_sum;          /* /laser_odom_to_init (transformSum), when LOAM_PUB_POSE */
+  loam_pose6 aft, bef;        /* transformAftMapped / transformBefMapped, when mapped */
+  loam_cloud_out registered;  /* /velodyne_cloud_registered, when mapped and capacity > 0 */
+} loam_chain_out;
+int loam_chain_sweep(loam_ctx *ctx, double stamp, loam_cloud_in raw, loam_chain_out *out);
+
 /* = transformMaintenance laserOdometryHandler with the last odomAftMappedHandler state.
  * Pure host function (scalar pose algebra, no kernel). */
 int loam_maintenance(const loam_pose6 *odom_sum, const loam_pose6 *bef, const loam_pose6 *aft,

@@ -92,6 +92,11 @@ STAT_BRANCH = ("od_degenerate_steps", "od_nan_skips", "mp_degenerate_steps", "mp
 STAT_WORK = ("mp_nn_candidates", "mp_nn_cells", "od_assoc_gathered", "od_assoc_boxes")
 
 
+class ChainOut(ctypes.Structure):
+    _fields_ = [("published", ctypes.c_int32), ("mapped", ctypes.c_int32), ("od_sum", Pose6),
+                ("aft", Pose6), ("bef", Pose6), ("registered", CloudOut)]
+
+
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in STAT_U64] + \
                [(n, ctypes.c_double) for n in ("ms_sr", "ms_od", "ms_mp")] + \
@@ -103,7 +108,7 @@ class Stats(ctypes.Structure):
 
 EXPORTS = ("loam_config_default", "loam_create", "loam_destroy", "loam_last_error", "loam_imu",
            "loam_scan_registration", "loam_odometry", "loam_mapping", "loam_mapping_surround",
-           "loam_maintenance",
+           "loam_maintenance", "loam_chain_sweep",
            "loam_batch_upload", "loam_batch_run", "loam_batch_sync", "loam_batch_download", "loam_get_stats",
            "loam_set_profiling", "loam_get_kernel_times", "loam_set_stream_priority",
            # include/loam/loam_bag.h: recorded-sweep ingest (rosbag v2, PointCloud2, Imu)
@@ -131,6 +136,7 @@ def lib():
         L.loam_mapping.argtypes = [PP, ctypes.c_double, P(Pose6), P(CloudOut), P(CloudOut), P(CloudOut),
                                    P(Pose6), P(Pose6), P(CloudOut)]
         L.loam_mapping_surround.argtypes = [PP, P(CloudOut), P(ctypes.c_int)]
+        L.loam_chain_sweep.argtypes = [PP, ctypes.c_double, CloudIn, P(ChainOut)]
         L.loam_maintenance.argtypes = [P(Pose6)] * 4
         L.loam_batch_upload.argtypes = [PP, ctypes.c_uint32, P(CloudIn), P(CloudIn)]
         L.loam_batch_run.argtypes = [PP]
@@ -244,6 +250,27 @@ class Engine:
                                   ctypes.byref(refs[1][0]), ctypes.byref(refs[2][0]), ctypes.byref(aft),
                                   ctypes.byref(bef), ctypes.byref(reg.c)))
         return aft.arr(), bef.arr(), reg.get()
+
+    def chain_sweep(self, raw, stamp=0.0, registered=False):
+        """one sweep through the three node bodies with the intermediate topics kept on the device
+        (loam_chain_sweep): (rc, published, od_sum, aft, bef, registered) -- aft / bef None when
+        mapping did not run on this sweep, registered None unless requested"""
+        ci, keep = _cloud_in(raw)
+        out = ChainOut()
+        reg = _Out(max(int(np.asarray(raw).shape[0]), 1)) if registered else None
+        if reg is not None:
+            out.registered = reg.c
+        rc = lib().loam_chain_sweep(self.h, stamp, ci, ctypes.byref(out))
+        if rc == LOAM_E_NOT_READY:
+            return rc, 0, None, None, None, None
+        _check(rc)
+        if not out.mapped:
+            return 0, out.published, out.od_sum.arr(), None, None, None
+        r = None
+        if reg is not None:
+            reg.c = out.registered
+            r = reg.get()
+        return 0, out.published, out.od_sum.arr(), out.aft.arr(), out.bef.arr(), r
 
     def mapping_surround(self, cap=1 << 16):
         """/laser_cloud_surround of the last mapping frame (laserMapping.cpp:1038-1058): an (n, 4)

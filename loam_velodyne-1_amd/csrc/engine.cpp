@@ -322,9 +322,14 @@ int loam_get_stats(loam_ctx* x, loam_stats* s) {
   return LOAM_OK;
 }
 
+}  // extern "C"
+
+namespace {
 // ------------------------------------------------------------------ scanRegistration
-int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_features* out) {
-  if (!x || !out) return fail(LOAM_E_INVAL, "null argument");
+// The laserCloudHandler body on ctx->sr1.  out == nullptr (the device-resident chain): the topics
+// stay in sr1 for the odometry that follows; cnt5 (sharp, lessSharp, flat, lessFlat, full counts)
+// and imu12 (/imu_trans) are returned either way.
+int sr_frame(loam_ctx* x, double stamp, const loam_cloud_in& raw, loam_features* out, int* cnt5, float* imu12) {
   if (!x->sr_inited) {  // src/scanRegistration.cpp:213-219 (Q1)
     x->sr_init_count++;
     if (x->sr_init_count >= (int)x->cfg.system_delay) x->sr_inited = true;
@@ -358,7 +363,7 @@ int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_fe
   // down on the second stream, and reach the caller's buffer on the host, while the curvature /
   // pick / VoxelGrid kernels run
   // (only when the caller's buffer holds all n points: nfull <= n can then not fail on capacity)
-  const bool early = x->st2 != nullptr && n > 0 && out->full.pts && (uint32_t)n <= out->full.capacity;
+  const bool early = out && x->st2 != nullptr && n > 0 && out->full.pts && (uint32_t)n <= out->full.capacity;
   sr_launch(b, prm, x->st, nullptr, early ? x->fork : nullptr);
   HIP_TRY(hipEventRecord(x->ev[1], x->st));
   HIP_TRY(hipGetLastError());
@@ -387,22 +392,27 @@ int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_fe
   }
   int e = 0;
   x->pin.reset();
-  if (early) {
-    out->full.count = (uint32_t)nfull;
-    if ((uint32_t)nfull > out->full.capacity) e |= fail(LOAM_E_CAPACITY, "output cloud capacity too small");
-  } else {
-    e |= copy_out(x->st, x->pin, b.full, nfull, &out->full);
+  if (out) {
+    if (early) {
+      out->full.count = (uint32_t)nfull;
+      if ((uint32_t)nfull > out->full.capacity) e |= fail(LOAM_E_CAPACITY, "output cloud capacity too small");
+    } else {
+      e |= copy_out(x->st, x->pin, b.full, nfull, &out->full);
+    }
+    e |= copy_out(x->st, x->pin, b.sharp, cnt[0], &out->sharp);
+    e |= copy_out(x->st, x->pin, b.lsharp, cnt[1], &out->less_sharp);
+    e |= copy_out(x->st, x->pin, b.flat, cnt[2], &out->flat);
+    e |= copy_out(x->st, x->pin, b.lflat, cnt[3], &out->less_flat);
+    HIP_TRY(hipStreamSynchronize(x->st));
+    x->pin.finish();
   }
-  e |= copy_out(x->st, x->pin, b.sharp, cnt[0], &out->sharp);
-  e |= copy_out(x->st, x->pin, b.lsharp, cnt[1], &out->less_sharp);
-  e |= copy_out(x->st, x->pin, b.flat, cnt[2], &out->flat);
-  e |= copy_out(x->st, x->pin, b.lflat, cnt[3], &out->less_flat);
-  HIP_TRY(hipStreamSynchronize(x->st));
-  x->pin.finish();
   // /imu_trans (:614-635)
   const float it[12] = {q->pitchStart, q->yawStart, q->rollStart, q->pitchCur, q->yawCur, q->rollCur,
                         q->shiftFSX,   q->shiftFSY, q->shiftFSZ,  q->veloFSX,  q->veloFSY, q->veloFSZ};
-  std::memcpy(out->imu_trans, it, sizeof(it));
+  if (out) std::memcpy(out->imu_trans, it, sizeof(it));
+  std::memcpy(imu12, it, sizeof(it));
+  for (int k = 0; k < 4; ++k) cnt5[k] = cnt[k];
+  cnt5[4] = nfull;
   float ms = 0;
   (void)hipEventElapsedTime(&ms, x->ev[0], x->ev[1]);
   std::memset(&x->stats, 0, sizeof(x->stats));
@@ -416,6 +426,23 @@ int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_fe
 }
 
 // ------------------------------------------------------------------ laserOdometry
+// The laserOdometry loop body on the features fv (cnt: sharp, lessSharp, flat, lessFlat, full
+// counts; imu: /imu_trans).  late_full: the full cloud is still on the host (message mode) and is
+// staged while the L-M runs; nullptr when fv's full cloud is already on the device.  nl3 (optional):
+// the published CornerLast / SurfLast / full-cloud counts, for a mapping on the device copies.
+int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu, const loam_cloud_out* late_full,
+             loam_pose6* sum_out, loam_cloud_out* corner_last, loam_cloud_out* surf_last, loam_cloud_out* full_end,
+             int* published, int* nl3);
+}  // namespace
+
+extern "C" {
+int loam_scan_registration(loam_ctx* x, double stamp, loam_cloud_in raw, loam_features* out) {
+  if (!x || !out) return fail(LOAM_E_INVAL, "null argument");
+  int cnt5[5];
+  float imu12[12];
+  return sr_frame(x, stamp, raw, out, cnt5, imu12);
+}
+
 int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6* sum_out,
                   loam_cloud_out* corner_last, loam_cloud_out* surf_last, loam_cloud_out* full_end,
                   int* published) {
@@ -424,7 +451,6 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
   HIP_TRY(hipSetDevice(x->device));
   *published = 0;
   SrBuffers& fi = x->odin;
-  OdBuffers& o = x->od1;
   const int R = x->R;
   if (in->sharp.count > (uint32_t)(kSharpPerRing * R) || in->flat.count > (uint32_t)(kFlatPerRing * R) ||
       in->less_sharp.count > (uint32_t)(kLessSharpPerRing * R))
@@ -448,16 +474,29 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
                 (int)in->less_flat.count, (int)in->full.count};
   int* mi = (int*)x->meta;  // [0..4] counts, [8..19] imu_trans, [24..] downloads below
   std::memcpy(mi, cnt, sizeof(cnt));
-  std::memcpy(mi + 8, in->imu_trans, 12 * sizeof(float));
   HIP_TRY(hipMemcpyAsync(fi.cnt, mi, 4 * sizeof(int), hipMemcpyHostToDevice, x->st));
   HIP_TRY(hipMemcpyAsync(fi.n_full, &mi[4], sizeof(int), hipMemcpyHostToDevice, x->st));
-  const FeatView fv = feat_view(fi, 0, 1);
+  return od_frame(x, feat_view(fi, 0, 1), cnt, in->imu_trans, late ? &in->full : nullptr, sum_out, corner_last,
+                  surf_last, full_end, published, nullptr);
+}
+}  // extern "C"
+
+namespace {
+int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_in, const loam_cloud_out* late_full,
+             loam_pose6* sum_out, loam_cloud_out* corner_last, loam_cloud_out* surf_last, loam_cloud_out* full_end,
+             int* published, int* nl3) {
+  *published = 0;
+  OdBuffers& o = x->od1;
+  SrBuffers& fi = x->odin;
+  int* mi = (int*)x->meta;  // [8..19] imu_trans, [24..] downloads below
+  std::memcpy(mi + 8, imu_in, 12 * sizeof(float));
+  const bool late = late_full != nullptr;
   std::memset(&x->stats, 0, sizeof(x->stats));
   // imuTransHandler (:330-351): this sweep's /imu_trans, in the state order load_imu reads
   HIP_TRY(hipMemcpyAsync(o.state + kOdImu, mi + 8, 12 * sizeof(float), hipMemcpyHostToDevice, x->st));
   if (!x->od_inited) {  // src/laserOdometry.cpp:427-456: Last = raw lessSharp / lessFlat, no L-M
     // :451-452 transformSum[0] += imuPitchStart; transformSum[2] += imuRollStart (from zero)
-    const float sum0[3] = {0.0f + in->imu_trans[0], 0.0f, 0.0f + in->imu_trans[2]};
+    const float sum0[3] = {0.0f + imu_in[0], 0.0f, 0.0f + imu_in[2]};
     HIP_TRY(hipMemcpyAsync(o.state + kOdSum, sum0, sizeof(sum0), hipMemcpyHostToDevice, x->st));
     x->od_sum[0] = sum0[0];
     x->od_sum[2] = sum0[2];
@@ -470,6 +509,7 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
     HIP_TRY(hipMemcpyAsync(nl, o.nlast, 2 * sizeof(int), hipMemcpyDeviceToHost, x->st));
     HIP_TRY(hipStreamSynchronize(x->st));
     *published = LOAM_PUB_CLOUDS;
+    if (nl3) { nl3[0] = nl[0]; nl3[1] = nl[1]; nl3[2] = 0; }
     x->pin.reset();
     int e = copy_out(x->st, x->pin, o.lastC, nl[0], corner_last) | copy_out(x->st, x->pin, o.lastS, nl[1], surf_last);
     HIP_TRY(hipStreamSynchronize(x->st));
@@ -482,7 +522,7 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
   // double trig, which a one-thread kernel took ~16 us for (the batch path keeps it on the device)
   od_solve(o, fv, cur, x->st, nullptr, /*device_fini=*/false);
   if (late) {  // late_full: host copy + DMA on the second stream, overlapping the L-M above
-    HIP_TRY(x->pin.up(x->st2, fi.full, in->full.pts, (size_t)in->full.count));
+    HIP_TRY(x->pin.up(x->st2, fi.full, late_full->pts, (size_t)late_full->count));
     HIP_TRY(hipEventRecord(x->join, x->st2));
     HIP_TRY(hipStreamWaitEvent(x->st, x->join, 0));
   }
@@ -504,7 +544,7 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
   HIP_TRY(hipStreamSynchronize(x->st));
   if (ist[kIsErr]) return fail(LOAM_E_CAPACITY, "odometry capacity exceeded");
   {  // :830-856 (k_od_fini's body, host side): transformSum from this frame's transform
-    const float* q = in->imu_trans;
+    const float* q = imu_in;
     loampose::Imu m;
     m.pitchStart = q[0]; m.yawStart = q[1]; m.rollStart = q[2];
     m.pitchLast = q[3]; m.yawLast = q[4]; m.rollLast = q[5];
@@ -523,6 +563,7 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
   if (pub) {
     x->od_frame_count = 0;
     *published |= LOAM_PUB_CLOUDS | LOAM_PUB_FULL;
+    if (nl3) { nl3[0] = nl[nxt * 2 + 0]; nl3[1] = nl[nxt * 2 + 1]; nl3[2] = nfe[nxt]; }
     x->pin.reset();
     e |= copy_out(x->st, x->pin, o.lastC + (size_t)nxt * o.P * o.capC, nl[nxt * 2 + 0], corner_last);
     e |= copy_out(x->st, x->pin, o.lastS + (size_t)nxt * o.P * o.capS, nl[nxt * 2 + 1], surf_last);
@@ -552,6 +593,9 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
   count_bytes(x->stats);
   return e ? LOAM_E_CAPACITY : LOAM_OK;
 }
+}  // namespace
+
+extern "C" {
 
 // ------------------------------------------------------------------ laserMapping
 int loam_mapping(loam_ctx* x, double stamp, const loam_pose6* odom_sum, const loam_cloud_out* corner_last,
@@ -574,6 +618,54 @@ int loam_mapping(loam_ctx* x, double stamp, const loam_pose6* odom_sum, const lo
     x->map_frame_count = 0;
     x->surround_due = true;
   }
+  return rc;
+}
+
+// ------------------------------------------------------------------ device-resident node chain
+// scanRegistration -> laserOdometry -> laserMapping on one sweep with the intermediate topics left
+// in device memory: odometry reads scanRegistration's buffers (sr1) in place and mapping reads
+// odometry's published CornerLast / SurfLast / full-end buffers in place.  The arithmetic is the
+// three node calls' own (the same kernels on the same values); only the host round trips of the
+// intermediate clouds are gone, as in an intra-process (nodelet) deployment.
+int loam_chain_sweep(loam_ctx* x, double stamp, loam_cloud_in raw, loam_chain_out* out) {
+  if (!x || !out) return fail(LOAM_E_INVAL, "null argument");
+  HIP_TRY(hipSetDevice(x->device));
+  out->published = 0;
+  out->mapped = 0;
+  int cnt5[5];
+  float imu12[12];
+  int rc = sr_frame(x, stamp, raw, nullptr, cnt5, imu12);
+  if (rc) return rc;
+  int nl3[3] = {0, 0, 0};
+  rc = od_frame(x, feat_view(x->sr1, 0, 1), cnt5, imu12, nullptr, &out->od_sum, nullptr, nullptr, nullptr,
+                &out->published, nl3);
+  if (rc) return rc;
+  if (out->published != (LOAM_PUB_POSE | LOAM_PUB_CLOUDS | LOAM_PUB_FULL)) return LOAM_OK;
+  const OdBuffers& o = x->od1;
+  const int nxt = x->od_last;  // od_frame swapped: the published Last is the current one
+  MpInput in;
+  in.corner = o.lastC + (size_t)nxt * o.P * o.capC;
+  in.surf = o.lastS + (size_t)nxt * o.P * o.capS;
+  in.full = o.fullEnd + (size_t)nxt * o.P * o.capS;
+  in.corner_stride = o.capC; in.surf_stride = o.capS; in.full_stride = o.capS;
+  in.ncorner = o.nlast + nxt * 2; in.nsurf = o.nlast + nxt * 2 + 1; in.nfull = o.nfullEnd + nxt;
+  in.ncorner_stride = in.nsurf_stride = 4; in.nfull_stride = 2;
+  in.pose = nullptr; in.pose_stride = 6;
+  float rp[2];
+  int front = 0;
+  const bool have_imu = loamimu::mp_lookup(x->mp_imu, stamp, rp[0], rp[1], front);
+  bool updated = false;
+  loam_cloud_out* reg = out->registered.capacity ? &out->registered : nullptr;
+  if (!reg) out->registered.count = 0;
+  rc = mp_stream_frame_dev(x->mp1, x->st, out->od_sum, in, nl3, &out->aft, &out->bef, reg, &x->stats, g_err,
+                           x->pin, x->meta, have_imu ? rp : nullptr, &updated);
+  if (have_imu && updated) x->mp_imu.front = front;
+  x->surround_due = false;
+  if (rc == LOAM_OK && ++x->map_frame_count >= 5) {  // :1038-1040
+    x->map_frame_count = 0;
+    x->surround_due = true;
+  }
+  if (rc == LOAM_OK) out->mapped = 1;
   return rc;
 }
 

@@ -2065,6 +2065,11 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   b.pool_cur = 1 - b.pool_cur;
 }
 
+template <typename Hook>
+int mp_stream_run(MpBuffers& b, hipStream_t st, const MpInput& in, const int* n, hipEvent_t e0, hipEvent_t e1,
+                  loam_pose6* aft, loam_pose6* bef, loam_cloud_out* registered, loam_stats* stats, std::string& err,
+                  Staging& pin, void* meta, bool* updated, Hook hook);
+
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
                     const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
                     loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, void* meta,
@@ -2119,12 +2124,64 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   in.ncorner = b.in_n; in.nsurf = b.in_n + 1; in.nfull = b.in_n + 2;
   in.ncorner_stride = in.nsurf_stride = in.nfull_stride = 3;
   in.pose = b.in_pose; in.pose_stride = 6;
-  hipError_t le = hipEventRecord(e0, st);
-  mp_frame(b, in, st, nullptr, false, [&]() {
-    if (!late || le != hipSuccess) return;
-    le = pin.up(st2, b.inF, full.pts, (size_t)n[2]);
+  return mp_stream_run(b, st, in, n, e0, e1, aft, bef, registered, stats, err, pin, meta, updated, [&]() {
+    if (!late) return hipSuccess;
+    hipError_t le = pin.up(st2, b.inF, full.pts, (size_t)n[2]);
     if (le == hipSuccess) le = hipEventRecord(ev2, st2);
     if (le == hipSuccess) le = hipStreamWaitEvent(st, ev2, 0);
+    return le;
+  });
+}
+
+// the device-resident chain (loam_chain_sweep): the clouds are already on the device (odometry's
+// published Last / full-end buffers, src, with device counts); n3: their counts on the host
+int mp_stream_frame_dev(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const MpInput& src, const int* n3,
+                        loam_pose6* aft, loam_pose6* bef, loam_cloud_out* registered, loam_stats* stats,
+                        std::string& err, Staging& pin, void* meta, const float* imu_rp, bool* updated) {
+  if (n3[0] > b.capC || n3[1] > b.capS || n3[2] > b.capS) {
+    err = "mapping input cloud exceeds capacity";
+    return LOAM_E_CAPACITY;
+  }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipError_t ce = hipEventCreate(&e0);
+  if (ce == hipSuccess) ce = hipEventCreate(&e1);
+  if (ce != hipSuccess) {
+    if (e0) (void)hipEventDestroy(e0);
+    err = std::string("mapping timing events: ") + hipGetErrorString(ce);
+    return LOAM_E_HIP;
+  }
+  int* mi = (int*)meta;  // as mp_stream_frame: [4..9] pose, [10..11] IMU (roll, pitch), [12] IMU flag
+  std::memcpy(mi + 4, &odom_sum, 6 * sizeof(float));
+  const float rp[2] = {imu_rp ? imu_rp[0] : 0.0f, imu_rp ? imu_rp[1] : 0.0f};
+  std::memcpy(mi + 10, rp, sizeof(rp));
+  mi[12] = imu_rp ? 1 : 0;
+  hipError_t ue = hipMemcpyAsync(b.in_pose, mi + 4, 6 * sizeof(float), hipMemcpyHostToDevice, st);
+  if (ue == hipSuccess) ue = hipMemcpyAsync(b.state + kMpImuRP, mi + 10, 2 * sizeof(float), hipMemcpyHostToDevice, st);
+  if (ue == hipSuccess) ue = hipMemcpyAsync(b.istate + kMiImu, mi + 12, sizeof(int), hipMemcpyHostToDevice, st);
+  if (ue != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    err = std::string("mapping upload: ") + hipGetErrorString(ue);
+    return LOAM_E_HIP;
+  }
+  MpInput in = src;
+  in.pose = b.in_pose;
+  in.pose_stride = 6;
+  return mp_stream_run(b, st, in, n3, e0, e1, aft, bef, registered, stats, err, pin, meta, updated,
+                       []() { return hipSuccess; });
+}
+
+// the frame's kernels on `in` and the downloads (both stream entry points); hook: called just
+// before k_mp_register (the late full-cloud staging); consumes e0 / e1
+template <typename Hook>
+int mp_stream_run(MpBuffers& b, hipStream_t st, const MpInput& in, const int* n, hipEvent_t e0, hipEvent_t e1,
+                  loam_pose6* aft, loam_pose6* bef, loam_cloud_out* registered, loam_stats* stats, std::string& err,
+                  Staging& pin, void* meta, bool* updated, Hook hook) {
+  int* mi = (int*)meta;
+  hipError_t le = hipEventRecord(e0, st);
+  mp_frame(b, in, st, nullptr, false, [&]() {
+    if (le != hipSuccess) return;
+    le = hook();
   }, std::max(n[0], n[1]));
   if (le == hipSuccess) le = hipEventRecord(e1, st);
   float* sf = (float*)(mi + 16);                  // kMpStateFloats

@@ -141,6 +141,11 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
                     loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, void* meta,
                     const float* imu_rp = nullptr, bool* updated = nullptr, hipStream_t st2 = nullptr,
                     hipEvent_t ev2 = nullptr);
+// the same frame on clouds already on the device (src: pointers + device counts, n3: host counts)
+int mp_stream_frame_dev(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const MpInput& src, const int* n3,
+                        loam_pose6* aft, loam_pose6* bef, loam_cloud_out* registered, loam_stats* stats,
+                        std::string& err, Staging& pin, void* meta, const float* imu_rp = nullptr,
+                        bool* updated = nullptr);
 // /laser_cloud_surround of the last streaming frame (instance 0): its 5x5x5 cube neighbourhood
 // concatenated and VoxelGrid 0.2 (src/laserMapping.cpp:1038-1058)
 int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::string& err);

@@ -7,6 +7,7 @@ reference's message conventions on the device.
              /aft_mapped_to_init, Bef and /velodyne_cloud_registered against the oracle's run
              frozen in tests/golden/oracle_golden.json["config3_full220"] — the sequential node
              chain on one context and the three-context node pipeline (pipeline.py)
+             and through loam_chain_sweep, the device-resident node chain
   config 5   bench.py latency.config5: the HDL-64E problem at the reference's 64-ring iteration
              caps 100 / 20 (bk include/loam_velodyne/common.h:31-32)
   node chain odometry -> loam_msg_from_pose(LASER_ODOM) -> loam_pose_from_msg -> loam_mapping ->
@@ -29,6 +30,45 @@ pytestmark = pytest.mark.gpu
 
 def test_config3_full220_sequential(loam, sg):
     check_config3_full(config3_full_records(loam.Engine(loam.default_config()), sg))
+
+
+def test_config3_full220_device_chain(loam, sg):
+    """the same 220 sweeps through loam_chain_sweep (intermediate topics left on the device)"""
+    e = loam.Engine(loam.default_config())
+    traj = []
+    for k, sw in enumerate(sg.stream_sweeps(220, 1)):
+        rc, pub, od, aft, bef, reg = e.chain_sweep(sw, stamp=0.1 * k, registered=True)
+        if rc:
+            continue
+        rec = {"k": k, "pub": pub, "od": od}
+        if aft is not None:
+            rec.update(aft=aft, bef=bef, reg_n=int(reg.shape[0]), reg=digest(reg))
+        traj.append(rec)
+    check_config3_full(traj)
+
+
+def test_device_chain_surround_and_counters(loam, oc, sg):
+    """loam_mapping_surround after loam_chain_sweep publishes what it publishes after the message
+    calls, and the chain leaves the same per-call counters"""
+    sweeps = sg.stream_sweeps(30, 1)
+    cfg = dict(system_delay=1)
+    a, b = loam.Engine(loam.default_config(**cfg)), loam.Engine(loam.default_config(**cfg))
+    for k, sw in enumerate(sweeps):
+        rc, f = a.scan_registration(sw, stamp=0.1 * k)
+        rc2, pub2, od2, aft2, bef2, _ = b.chain_sweep(sw, stamp=0.1 * k)
+        assert rc == rc2
+        if rc:
+            continue
+        pub, pose, cl, sl, full = a.odometry(f, stamp=0.1 * k)
+        assert pub == pub2 and np.array_equal(pose, od2), k
+        if pub == 7:
+            aft, bef, _ = a.mapping(pose, cl, sl, full, stamp=0.1 * k)
+            assert np.array_equal(aft, aft2) and np.array_equal(bef, bef2), k
+            sa, sb = a.mapping_surround(), b.mapping_surround()
+            assert (sa is None) == (sb is None), k
+            if sa is not None:
+                np.testing.assert_array_equal(sa, sb)
+            assert a.stats()["mp_iters"] == b.stats()["mp_iters"], k
 
 
 def test_config3_full220_pipelined(loam, sg):
