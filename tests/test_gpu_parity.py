@@ -263,7 +263,7 @@ def _push_out(raw, rng_m=250.0, az_deg=(0.0, 12.0)):
 
 def test_batch_stack_keys_beyond_24_bits(loam, oc, sg):
     """Batch mapping with stacks whose 0.4 m VoxelGrid spans more than 2^24 voxels (far returns on
-    the top ring): those segments take vg_run's 32-bit sort list, the others the 24-bit one."""
+    the top ring): the VoxelGrid cascade's radix passes must cover every bit the keys span."""
     prevs, curs = sg.batch_problems(8, base_seed=1300)
     for i in (0, 3, 6):
         prevs[i], n0 = _push_out(prevs[i])
