@@ -33,6 +33,12 @@ using namespace loamdev;
 #define LOAM_OD_FUSED_MAX 0  // (measured at batch 128: rows + step 0.67 -> 0.62 ms/step, whole step unchanged; 1024 slower)
 #endif
 
+// diagnostic builds: count only one phase's gathered points in od_assoc_gathered (1: the 27 cells,
+// 2: the chunk fallback beyond one cell, 3: the ring windows); 0 (product): all
+#ifndef LOAM_ASSOC_PHASE
+#define LOAM_ASSOC_PHASE 0
+#endif
+
 namespace loam {
 #ifdef LOAM_PHASES
 __device__ PhaseAcc g_ph_od = {~0ull, 0ull, 0ull, {{0}}};
@@ -116,6 +122,31 @@ LOAM_D void hash_sort(const HashJob& j, const float4* pts, int n, int T, int* st
   }
 }
 
+// the chunk boxes (min / max of x, y, z and of the ring int(intensity)) of points [0, n) in
+// kChunk-point chunks, 64 / kChunk chunks per wave step; wave w0 of nw waves
+LOAM_D void chunk_boxes(const float4* pts, int n, float4* ch, int w0, int nw) {
+  const int lane = lane_id();
+  constexpr int PER = 64 / kChunk;
+  const int nch = (n + kChunk - 1) / kChunk;
+  for (int c0 = w0 * PER; c0 < nch; c0 += nw * PER) {
+    const int c = c0 + lane / kChunk;
+    const float4 a = pts[min(c * kChunk + lane % kChunk, n - 1)];
+    const float r = (float)(int)a.w;
+    float4 lo = make_float4(a.x, a.y, a.z, r), hi = lo;
+#pragma unroll
+    for (int o = kChunk / 2; o > 0; o >>= 1) {
+      lo.x = fminf(lo.x, __shfl_xor(lo.x, o, 64)); lo.y = fminf(lo.y, __shfl_xor(lo.y, o, 64));
+      lo.z = fminf(lo.z, __shfl_xor(lo.z, o, 64)); lo.w = fminf(lo.w, __shfl_xor(lo.w, o, 64));
+      hi.x = fmaxf(hi.x, __shfl_xor(hi.x, o, 64)); hi.y = fmaxf(hi.y, __shfl_xor(hi.y, o, 64));
+      hi.z = fmaxf(hi.z, __shfl_xor(hi.z, o, 64)); hi.w = fmaxf(hi.w, __shfl_xor(hi.w, o, 64));
+    }
+    if (lane % kChunk == 0 && c < nch) {
+      ch[2 * c] = lo;
+      ch[2 * c + 1] = hi;
+    }
+  }
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_hash_build(HashJob j) {
   const int p = blockIdx.x, tid = threadIdx.x;
@@ -131,22 +162,8 @@ __global__ __launch_bounds__(NT) void k_hash_build(HashJob j) {
   if (tid == 0) j.tsize[p] = T;
   if (T <= kHashLds) hash_sort<NT, true>(j, pts, n, T, start, out, lfill, scratch);
   else hash_sort<NT, false>(j, pts, n, T, start, out, j.fill + (size_t)p * j.tmax, scratch);
-  if (j.chunks) {  // one wave per 64-point chunk of the source order
-    const int lane = lane_id(), w = tid >> 6;
-    const int nch = (n + kChunk - 1) / kChunk;
-    float4* ch = j.chunks + (size_t)p * 2 * chunks_of((int)j.pts_stride);
-    for (int c = w; c < nch; c += NT / 64) {
-      const int i = c * kChunk + lane;
-      float4 a = pts[min(i, n - 1)];
-      const float r = (float)(int)a.w;
-      const float4 lo = make_float4(wave_min_f(a.x), wave_min_f(a.y), wave_min_f(a.z), wave_min_f(r));
-      const float4 hi = make_float4(wave_max_f(a.x), wave_max_f(a.y), wave_max_f(a.z), wave_max_f(r));
-      if (lane == 0) {
-        ch[2 * c] = lo;
-        ch[2 * c + 1] = hi;
-      }
-    }
-  }
+  if (j.chunks)  // chunk boxes of the source order
+    chunk_boxes(pts, n, j.chunks + (size_t)p * 2 * chunks_of((int)j.pts_stride), tid >> 6, NT / 64);
 }
 
 // ---- the same index built by many workgroups per cloud (small batches: streaming, config 2).  One
@@ -189,22 +206,9 @@ __global__ __launch_bounds__(256) void k_hash_count(HashPair hp) {
     const uint32_t h = cell_hash(cell_of(a.x, j.inv_h), cell_of(a.y, j.inv_h), cell_of(a.z, j.inv_h)) & (T - 1);
     atomicAdd(&fill[h], 1);
   }
-  if (j.chunks) {  // chunk boxes of the source order, one wave per 64-point chunk (as k_hash_build)
-    const int lane = lane_id(), w = tid >> 6;
-    const int nch = (n + kChunk - 1) / kChunk;
-    float4* ch = j.chunks + (size_t)p * 2 * chunks_of((int)j.pts_stride);
-    for (int c = blockIdx.x * 4 + w; c < nch; c += gridDim.x * 4) {
-      const int i = c * kChunk + lane;
-      float4 a = pts[min(i, n - 1)];
-      const float r = (float)(int)a.w;
-      const float4 lo = make_float4(wave_min_f(a.x), wave_min_f(a.y), wave_min_f(a.z), wave_min_f(r));
-      const float4 hi = make_float4(wave_max_f(a.x), wave_max_f(a.y), wave_max_f(a.z), wave_max_f(r));
-      if (lane == 0) {
-        ch[2 * c] = lo;
-        ch[2 * c + 1] = hi;
-      }
-    }
-  }
+  if (j.chunks)  // chunk boxes of the source order (as k_hash_build)
+    chunk_boxes(pts, n, j.chunks + (size_t)p * 2 * chunks_of((int)j.pts_stride), blockIdx.x * 4 + (tid >> 6),
+                gridDim.x * 4);
 }
 
 // exclusive scan of the counters into start (and back into fill as the scatter's cursors)
@@ -343,7 +347,7 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
   // change a minimum)
   const int incl = wave_incl_scan(cnt);
   const int total = __shfl(incl, 63, 64);
-  wpts += total;
+  if (LOAM_ASSOC_PHASE == 0 || LOAM_ASSOC_PHASE == 1) wpts += total;
   if (lane < 32) { cells[lane] = lane < 27 ? incl - cnt : 0x7fffffff; cells[32 + lane] = b0; }
   __builtin_amdgcn_wave_barrier();
   uint64_t best = ~0ull;
@@ -375,9 +379,9 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
     while (nb) {
       const int c = k0 + __ffsll((unsigned long long)nb) - 1;
       nb &= nb - 1;
-      wpts += min(kChunk, n - c * kChunk);
+      if (LOAM_ASSOC_PHASE == 0 || LOAM_ASSOC_PHASE == 2) wpts += min(kChunk, n - c * kChunk);
       const int t = c * kChunk + lane;
-      if (t < n) {
+      if (lane < kChunk && t < n) {
         const float4 a = cloud[t];
         const float d = sqdist(a.x, a.y, a.z, q.x, q.y, q.z);
         const uint64_t key = ((uint64_t)fkey(d) << 32) | ((uint32_t)t << 8) | (uint32_t)(int)a.w;
@@ -394,19 +398,22 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
 // with d < 25.  Whole 64-point chunks whose box is >= 5 m from sel are skipped; a chunk that may
 // hold the stop is always examined.
 // bw: chunks whose box lies beyond it are skipped too (a seed's squared distance, or 25)
+#ifndef LOAM_WIN_INFLIGHT
+#define LOAM_WIN_INFLIGHT 1  // (measured k_od_assoc ms/step at batch 1024: 1 -> 2.81, 2 -> 2.80, 3 -> 3.01)
+#endif
+constexpr int kWinInFlight = LOAM_WIN_INFLIGHT;
 template <typename F>
 LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int dir, int scan, float4 sel, float bw,
                         int& wpts, int& wbox, F f) {
   const int lane = lane_id();
   // int(intensity) > scan + 2.5 (double) <=> r > scan + 2 for integers (and < scan - 2.5 <=> < scan - 2)
   auto stop_ring = [&](int r) { return dir > 0 ? r > scan + 2 : r < scan - 2; };
-  // examines points [j0 .. j0 + dir * (cnt - 1)]; true when the stop was met
-  auto run = [&](int j0, int cnt) {
-    wpts += cnt;
+  // the points [j0 .. j0 + dir * (cnt - 1)], lane k holding a = point j0 + dir * k; true when the
+  // stop was met
+  auto scan_pts = [&](int j0, int cnt, float4 a) {
+    if (LOAM_ASSOC_PHASE == 0 || LOAM_ASSOC_PHASE == 3) wpts += cnt;
     const int j = j0 + dir * lane;
     const bool inr = lane < cnt;
-    if (inr) LOAM_CHECK(j >= 0 && (dir < 0 ? j < c : j < end), j, end);
-    const float4 a = inr ? L[j] : make_float4(0, 0, 0, 0);
     const int r = (int)a.w;
     const uint64_t mb = __ballot(inr && stop_ring(r));
     const int limit = mb ? __ffsll((unsigned long long)mb) - 1 : 64;
@@ -416,6 +423,43 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
     }
     return mb != 0;
   };
+  // up to kWinInFlight of the window's needed chunks at once (their loads in flight together).  Only
+  // the last needed chunk of a 64-box step can hold the stop (it is the first box whose ring range
+  // reaches past scan +- 2), and every minimum is keyed by (distance, walk position), so taking them
+  // together visits the same points and keeps the same minima as one at a time.
+  auto run_set = [&](uint64_t& nb, int kbase, int ksign, int jofs) {
+    bool stopped = false;
+    while (nb && !stopped) {
+      int j0[kWinInFlight], cn[kWinInFlight];
+      float4 a[kWinInFlight];
+#pragma unroll
+      for (int u = 0; u < kWinInFlight; ++u) {
+        cn[u] = 0;
+        j0[u] = 0;
+        if (nb) {
+          const int kk = kbase + ksign * (__ffsll((unsigned long long)nb) - 1);
+          nb &= nb - 1;
+          j0[u] = kk * kChunk + jofs;
+          cn[u] = dir > 0 ? min(kChunk, end - kk * kChunk) : kChunk;
+        }
+        const int j = j0[u] + dir * lane;
+        if (lane < cn[u]) LOAM_CHECK(j >= 0 && (dir < 0 ? j < c : j < end), j, end);
+        a[u] = lane < cn[u] ? L[j] : make_float4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kWinInFlight; ++u)
+        if (cn[u] && !stopped) stopped = scan_pts(j0[u], cn[u], a[u]);
+    }
+    return stopped;
+  };
+  // examines points [j0 .. j0 + dir * (cnt - 1)]; true when the stop was met
+  auto run = [&](int j0, int cnt) {
+    const int j = j0 + dir * lane;
+    const bool inr = lane < cnt;
+    if (inr) LOAM_CHECK(j >= 0 && (dir < 0 ? j < c : j < end), j, end);
+    return scan_pts(j0, cnt, inr ? L[j] : make_float4(0, 0, 0, 0));
+  };
+
   if (dir > 0) {
     int j = c + 1;
     const int hend = min(end, (j + kChunk - 1) & ~(kChunk - 1));
@@ -431,12 +475,7 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
       const int limit = mc ? __ffsll((unsigned long long)mc) - 1 : 63;
       const float bd = box_d2(lo, hi, sel);
       uint64_t nb = __ballot(v && lane <= limit && bd < 25.0f && bd <= bw);
-      bool stopped = false;
-      while (nb && !stopped) {
-        const int kk = (j / kChunk) + __ffsll((unsigned long long)nb) - 1;
-        nb &= nb - 1;
-        stopped = run(kk * kChunk, min(kChunk, end - kk * kChunk));
-      }
+      run_set(nb, j / kChunk, +1, 0);
       if (mc) return;
       j += 64 * kChunk;
     }
@@ -456,12 +495,7 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
       const int limit = mc ? __ffsll((unsigned long long)mc) - 1 : 63;
       const float bd = box_d2(lo, hi, sel);
       uint64_t nb = __ballot(v && lane <= limit && bd < 25.0f && bd <= bw);
-      bool stopped = false;
-      while (nb && !stopped) {
-        const int kk = kt - (__ffsll((unsigned long long)nb) - 1);
-        nb &= nb - 1;
-        stopped = run(kk * kChunk + kChunk - 1, kChunk);
-      }
+      run_set(nb, kt, -1, kChunk - 1);
       if (mc) return;
       kt -= 64;
     }

@@ -10,7 +10,10 @@
 namespace loam {
 
 // per-problem float state: transform[6] | transformSum[6] | matP[36] | imu_trans[12]
-constexpr int kChunk = 64;  // points per chunk box
+#ifndef LOAM_OD_CHUNK
+#define LOAM_OD_CHUNK 64
+#endif
+constexpr int kChunk = LOAM_OD_CHUNK;  // points per chunk box (<= 64)
 __host__ __device__ inline int chunks_of(int cap) { return (cap + kChunk - 1) / kChunk; }
 constexpr int kOdSum = 6, kOdMatP = 12, kOdImu = 48, kOdStateFloats = 64;
 // per-problem int state

@@ -570,6 +570,9 @@ struct SelShared {
   int nsharp, nlsharp, nflat, ncand, wf, big, loff;
 };
 
+#ifndef LOAM_RINGVG_HOLD
+#define LOAM_RINGVG_HOLD 1
+#endif
 // PCL VoxelGrid 0.2 of one ring's lessFlat candidates pts[lo + cand[0..nc)) into
 // outp (capacity outcap), the whole workgroup (:575-579): bbox, (voxel, candidate) keys, sort,
 // ordered per-voxel float means.  Returns the voxel count (clamped to outcap, *err flagged).
@@ -578,10 +581,30 @@ LOAM_D int ring_vg(const float4* pts, int lo, const CandT* cand, int nc, uint64_
                    float (*red)[kSelThreads / 64], int* scratch, int* err) {
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
-  for (int t = tid; t < nc; t += kSelThreads) {
-    const float4 a = pts[lo + cand[t]];
-    mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
-    mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
+  // HOLD: the thread's candidates stay in registers from the bbox pass to the key pass (one read of
+  // the candidates from memory instead of two)
+  constexpr bool HOLD = !BIG && CAP <= 2048 && LOAM_RINGVG_HOLD;
+  constexpr int RH = HOLD ? CAP / kSelThreads : 1;
+  float4 held[RH];
+  if constexpr (HOLD) {
+#pragma unroll
+    for (int e = 0; e < RH; ++e) {
+      const int t = e * kSelThreads + tid;
+      held[e] = t < nc ? pts[lo + cand[t]] : make_float4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int e = 0; e < RH; ++e)
+      if (e * kSelThreads + tid < nc) {
+        const float4 a = held[e];
+        mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
+        mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
+      }
+  } else {
+    for (int t = tid; t < nc; t += kSelThreads) {
+      const float4 a = pts[lo + cand[t]];
+      mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
+      mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
+    }
   }
   for (int d = 0; d < 3; ++d) {
     mn[d] = wave_min_f(mn[d]);
@@ -621,7 +644,15 @@ LOAM_D int ring_vg(const float4* pts, int lo, const CandT* cand, int nc, uint64_
           const int t = base + tid;
           uint32_t idx = 0xffffffffu;
           if (t < nc) {
-            const float4 a = pts[lo + cand[t]];
+            float4 a;
+            if constexpr (HOLD) {
+              a = held[0];
+#pragma unroll
+              for (int e = 1; e < RH; ++e)
+                if (base == e * kSelThreads) a = held[e];
+            } else {
+              a = pts[lo + cand[t]];
+            }
             const int i0 = (int)(floorf(a.x * inv) - (float)minb[0]);
             const int i1 = (int)(floorf(a.y * inv) - (float)minb[1]);
             const int i2 = (int)(floorf(a.z * inv) - (float)minb[2]);
