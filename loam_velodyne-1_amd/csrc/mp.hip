@@ -726,20 +726,28 @@ struct Top5 {
   float d[5];
   int i[5];
 };
+// (distance, index) as one ordered 64-bit key: distances are >= +0, so their bits order as they do
+LOAM_D uint64_t top5_key(float d, int idx) { return ((uint64_t)__float_as_uint(d) << 32) | (uint32_t)idx; }
 LOAM_D void top5_offer(Top5& t, float d, int idx) {
-  // ascending (distance, index); a point already held (two cells in one bucket) is skipped
-  if (d > t.d[4] || (d == t.d[4] && idx > t.i[4])) return;
+  // ascending (distance, index); a point already held (a seed, or two cells in one bucket) is
+  // skipped.  Branch-free insertion: lt_k = key < K_k is monotone in k (the list is sorted), so
+  // slot k takes K_{k-1} where lt_{k-1}, the key where lt_k alone, else keeps K_k
+  const uint64_t key = top5_key(d, idx);
+  uint64_t K[5];
 #pragma unroll
-  for (int k = 0; k < 5; ++k)
-    if (t.i[k] == idx) return;
-  t.d[4] = d;
-  t.i[4] = idx;
+  for (int k = 0; k < 5; ++k) K[k] = top5_key(t.d[k], t.i[k]);
+  if (key < K[4] && key != K[0] && key != K[1] && key != K[2] && key != K[3]) {
+    const bool l0 = key < K[0], l1 = key < K[1], l2 = key < K[2], l3 = key < K[3];
+    const uint64_t n4 = l3 ? K[3] : key;
+    const uint64_t n3 = l2 ? K[2] : (l3 ? key : K[3]);
+    const uint64_t n2 = l1 ? K[1] : (l2 ? key : K[2]);
+    const uint64_t n1 = l0 ? K[0] : (l1 ? key : K[1]);
+    const uint64_t n0 = l0 ? key : K[0];
+    const uint64_t N[5] = {n0, n1, n2, n3, n4};
 #pragma unroll
-  for (int k = 4; k > 0; --k) {
-    const bool sw = t.d[k] < t.d[k - 1] || (t.d[k] == t.d[k - 1] && t.i[k] < t.i[k - 1]);
-    if (sw) {
-      float fd = t.d[k]; t.d[k] = t.d[k - 1]; t.d[k - 1] = fd;
-      int fi = t.i[k]; t.i[k] = t.i[k - 1]; t.i[k - 1] = fi;
+    for (int k = 0; k < 5; ++k) {
+      t.d[k] = __uint_as_float((uint32_t)(N[k] >> 32));
+      t.i[k] = (int)(uint32_t)N[k];
     }
   }
 }
@@ -813,6 +821,11 @@ constexpr int kMpFitThreads = 64;
 // the lane's LDS column (stride kMpQueryThreads).  Ranges are packed start:19 | count:13; a lane
 // whose ranges do not fit falls back to knn5.
 constexpr int kNnInFlight = 8;  // measured k_mp_nn ms/step: 2 -> 4.17, 4 -> 3.95, 8 -> 3.88, 16 -> 5.33
+// cells whose bucket-range loads are in flight together
+#ifndef LOAM_NN_RANGE_GROUP
+#define LOAM_NN_RANGE_GROUP 9  // (k_mp_nn ms/step at batch 1024: 1 -> 3.83, 7 -> 3.52, 9 -> 3.51, 14 -> 3.60 (spills))
+#endif
+constexpr int kNnRangeGroup = LOAM_NN_RANGE_GROUP;
 // L > 1: one of L lanes searching the same query: every lane lists the same cells, lane `sub`
 // takes the candidates sub, sub + L, ... of the concatenated list (a crowded cell is shared too);
 // the caller merges the L partial top-5 lists (knn5_merge)
@@ -826,18 +839,31 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
   const float bound = t.d[4];
   int n = 0, total = 0;
   bool fits = true;
+  // the range loads of a group of cells are all issued before any is used (a load whose count is
+  // tested in the same block is waited for at once: one dependent round trip per cell)
 #pragma unroll
-  for (int o = 0; o < 27; ++o) {
-    const int c = kCellOrder[o];
-    const int dx = c % 3 - 1, dy = (c / 3) % 3 - 1, dz = c / 9 - 1;
-    const float gx = dx < 0 ? gxl : (dx > 0 ? gxh : 0.0f);
-    const float gy = dy < 0 ? gyl : (dy > 0 ? gyh : 0.0f);
-    const float gz = dz < 0 ? gzl : (dz > 0 ? gzh : 0.0f);
-    const float bd = sqdist(gx, gy, gz, 0.0f, 0.0f, 0.0f);
-    if (bd < 1.0f && bd <= bound) {
-      const uint32_t h = cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1);
-      const int2 rg = load_pair(start + h);  // start[h], start[h + 1]: one 8-byte request
-      const int b0 = rg.x, cnt = rg.y - b0;
+  for (int g0 = 0; g0 < 27; g0 += kNnRangeGroup) {
+    int2 rg[kNnRangeGroup];
+#pragma unroll
+    for (int u = 0; u < kNnRangeGroup; ++u) {
+      const int o = g0 + u;
+      if (o >= 27) break;
+      const int c = kCellOrder[o];
+      const int dx = c % 3 - 1, dy = (c / 3) % 3 - 1, dz = c / 9 - 1;
+      const float gx = dx < 0 ? gxl : (dx > 0 ? gxh : 0.0f);
+      const float gy = dy < 0 ? gyl : (dy > 0 ? gyh : 0.0f);
+      const float gz = dz < 0 ? gzl : (dz > 0 ? gzh : 0.0f);
+      const float bd = sqdist(gx, gy, gz, 0.0f, 0.0f, 0.0f);
+      rg[u] = make_int2(0, 0);
+      if (bd < 1.0f && bd <= bound) {
+        const uint32_t h = cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1);
+        rg[u] = load_pair(start + h);  // start[h], start[h + 1]: one 8-byte request
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kNnRangeGroup; ++u) {
+      if (g0 + u >= 27) break;
+      const int b0 = rg[u].x, cnt = rg[u].y - b0;
       LOAM_CHECK(b0 >= 0 && cnt >= 0, b0, cnt);
       if (cnt > 0) {
         if (b0 >= (1 << 19) || cnt >= (1 << 13)) fits = false;
@@ -852,25 +878,24 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
     return;
   }
   work += total + (n << kWorkCellShift);
-  int ci = 0, left = 0, pos = 0;
+  // the list is walked one entry ahead: the LDS read of the next entry is issued when the current
+  // one is taken, so its latency is not on the candidate chain
+  int ci = 1, left = 0, pos = 0;
+  uint32_t nx = lst[0];
+  auto take = [&]() {
+    pos = (int)(nx & ((1u << 19) - 1));
+    left = (int)(nx >> 19);
+    nx = lst[min(ci, 26) * S];
+    ++ci;
+  };
   auto next = [&]() {  // index of the lane's next candidate
-    if (left == 0) {
-      const uint32_t e = lst[ci * S];
-      ++ci;
-      pos = (int)(e & ((1u << 19) - 1));
-      left = (int)(e >> 19);
-    }
+    if (left == 0) take();
     --left;
     return pos++;
   };
   auto skip = [&](int m) {  // pass over m candidates (the other lanes' share)
     while (m > 0) {
-      if (left == 0) {
-        const uint32_t e = lst[ci * S];
-        ++ci;
-        pos = (int)(e & ((1u << 19) - 1));
-        left = (int)(e >> 19);
-      }
+      if (left == 0) take();
       const int s = min(m, left);
       pos += s;
       left -= s;

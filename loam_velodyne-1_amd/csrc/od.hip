@@ -643,6 +643,8 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
   const int* ist = b.istate + (size_t)p * kOdStateInts;
   if (!ist[kIsActive] || ist[kIsStop]) return;
   __shared__ int cells[kAsWaves][64];
+  __shared__ float4 bq_s4[kAsWaves][64], bq_d[kAsWaves][64];
+  __shared__ int4 bq_j[kAsWaves][64];
   const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
   const float4* sel = b.sel + (size_t)p * b.cap_q;
   const size_t lp = (size_t)last_buf * b.P + p;
@@ -652,53 +654,74 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
   int* ind = b.ind + (size_t)p * 3 * b.cap_q;
   int wpts = 0, wbox = 0;  // wave-uniform work counters (loam_stats od_assoc_gathered / _boxes)
   const bool seeded = ist[kIsIters] > 0;  // ind holds this frame's previous round
-  for (int q = blk.x * kAsWaves + w; q < nq; q += gridDim.x * kAsWaves) {
-    float4 s4;
-    if constexpr (SEL) {
-      const float* st = b.state + (size_t)p * kOdStateFloats;
-      float T[6];
+  const int hCT = b.hC_T[last_buf * b.P + p], hST = b.hS_T[last_buf * b.P + p];
+  const int G = gridDim.x * kAsWaves, q0 = blk.x * kAsWaves + w;
+  // The wave's queries q0, q0 + G, ... in batches of 64: lane l first fetches query l's
+  // TransformToStart point and its seeds — the previous round's choices (ind, rounds after the
+  // first), their rings and squared distances at this round's transform — for all 64 at once
+  // (two dependent loads per batch instead of per query), staged in LDS for the per-query walks.
+  for (int i0 = 0; q0 + i0 * G < nq; i0 += 64) {
+    {
+      const int ql = q0 + (i0 + lane) * G;
+      if (ql < nq) {
+        float4 s4;
+        if constexpr (SEL) {
+          const float* st = b.state + (size_t)p * kOdStateFloats;
+          float T[6];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) T[k] = st[k];
-      const float4 po = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
-      s4 = loampose::transform_to_start(T, po);
-    } else {
-      s4 = sel[q];
+          for (int k = 0; k < 6; ++k) T[k] = st[k];
+          const float4 po = ql < nc ? f.sharp[(size_t)p * f.sharp_stride + ql] : f.flat[(size_t)p * f.flat_stride + (ql - nc)];
+          s4 = loampose::transform_to_start(T, po);
+        } else {
+          s4 = sel[ql];
+        }
+        const float4* Lc = ql < nc ? CL : SL;
+        int j[3] = {-1, -1, -1};
+        if (seeded) {
+#pragma unroll
+          for (int k = 0; k < 3; ++k) j[k] = ind[k * b.cap_q + ql];
+        }
+        float4 sp[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sp[k] = j[k] >= 0 ? Lc[j[k]] : make_float4(0, 0, 0, 0);
+        const float nnb = j[0] >= 0 ? sqdist(sp[0].x, sp[0].y, sp[0].z, s4.x, s4.y, s4.z) : 3.4e38f;
+        const float d1 = sqdist(sp[1].x, sp[1].y, sp[1].z, s4.x, s4.y, s4.z);
+        const float d2 = sqdist(sp[2].x, sp[2].y, sp[2].z, s4.x, s4.y, s4.z);
+        bq_s4[w][lane] = s4;
+        bq_j[w][lane] = make_int4(j[0], j[1], j[2], (int)sp[1].w | ((int)sp[2].w << 16));
+        bq_d[w][lane] = make_float4(nnb, d1, d2, 0.0f);
+      }
     }
-    // seeds: the previous round's choices (ind, rounds after the first), their rings and squared
-    // distances at this round's transform (lanes 0..2 load one each)
-    const bool corner = q < nc;
-    const float4* Lc = corner ? CL : SL;
-    int sj = -1;
-    float4 sp = make_float4(0, 0, 0, 0);
-    if (seeded && lane < 3) {
-      sj = ind[lane * b.cap_q + q];
-      if (sj >= 0) sp = Lc[sj];
+    __builtin_amdgcn_wave_barrier();
+    const int nb = min(64, (nq - q0 + G - 1) / G - i0);
+    for (int i = 0; i < nb; ++i) {
+      const int q = q0 + (i0 + i) * G;
+      const float4 s4 = bq_s4[w][i];
+      const int4 jj = bq_j[w][i];
+      const float4 dd = bq_d[w][i];
+      const int j1 = jj.y, j2 = jj.z, r1 = jj.w & 0xffff, r2 = jj.w >> 16;
+      const float nnb = dd.x, d1 = dd.y, d2 = dd.z;
+      int i1, i2, i3 = -1;
+      if (q < nc) {
+        const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
+        const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC, hCT, CL, ch, C, 1.0f,
+                                         1.0f, s4, nnb, cells[w], wpts, wbox);
+        wave_assoc_corner(CL, ch, min(nc, C), nn, s4, j1, r1, d1, i1, i2, wpts, wbox);
+      } else {
+        const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
+        const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS, hST, SL, ch, S, 1.0f,
+                                         1.0f, s4, nnb, cells[w], wpts, wbox);
+        wave_assoc_surf(SL, ch, min(ns, S), nn, s4, j1, r1, d1, j2, r2, d2, i1, i2, i3, wpts, wbox);
+      }
+      if (lane == 0) {
+        LOAM_CHECK(q < b.cap_q && p < b.P, q, p);
+        LOAM_CHECK(i1 < (q < nc ? C : S) && i2 < (q < nc ? C : S) && i3 < S, i1, i2);
+        ind[q] = i1;
+        ind[b.cap_q + q] = i2;
+        ind[2 * b.cap_q + q] = i3;
+      }
     }
-    const int j0 = __shfl(sj, 0, 64), j1 = __shfl(sj, 1, 64), j2 = __shfl(sj, 2, 64);
-    const float4 p0 = make_float4(__shfl(sp.x, 0, 64), __shfl(sp.y, 0, 64), __shfl(sp.z, 0, 64), __shfl(sp.w, 0, 64));
-    const float4 p1 = make_float4(__shfl(sp.x, 1, 64), __shfl(sp.y, 1, 64), __shfl(sp.z, 1, 64), __shfl(sp.w, 1, 64));
-    const float4 p2 = make_float4(__shfl(sp.x, 2, 64), __shfl(sp.y, 2, 64), __shfl(sp.z, 2, 64), __shfl(sp.w, 2, 64));
-    const float nnb = j0 >= 0 ? sqdist(p0.x, p0.y, p0.z, s4.x, s4.y, s4.z) : 3.4e38f;
-    const float d1 = sqdist(p1.x, p1.y, p1.z, s4.x, s4.y, s4.z), d2 = sqdist(p2.x, p2.y, p2.z, s4.x, s4.y, s4.z);
-    int i1, i2, i3 = -1;
-    if (corner) {
-      const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
-      const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC,
-                                       b.hC_T[last_buf * b.P + p], CL, ch, C, 1.0f, 1.0f, s4, nnb, cells[w], wpts, wbox);
-      wave_assoc_corner(CL, ch, min(nc, C), nn, s4, j1, (int)p1.w, d1, i1, i2, wpts, wbox);
-    } else {
-      const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
-      const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS,
-                                       b.hS_T[last_buf * b.P + p], SL, ch, S, 1.0f, 1.0f, s4, nnb, cells[w], wpts, wbox);
-      wave_assoc_surf(SL, ch, min(ns, S), nn, s4, j1, (int)p1.w, d1, j2, (int)p2.w, d2, i1, i2, i3, wpts, wbox);
-    }
-    if (lane == 0) {
-      LOAM_CHECK(q < b.cap_q && p < b.P, q, p);
-      LOAM_CHECK(i1 < (q < nc ? C : S) && i2 < (q < nc ? C : S) && i3 < S, i1, i2);
-      ind[q] = i1;
-      ind[b.cap_q + q] = i2;
-      ind[2 * b.cap_q + q] = i3;
-    }
+    __builtin_amdgcn_wave_barrier();
   }
   if (COUNT && lane == 0 && wpts) {
     atomicAdd((int*)&ist[kIsGathered], wpts);
