@@ -581,12 +581,16 @@ LOAM_HD uint32_t fkey(float f) { return __builtin_bit_cast(uint32_t, f); }
 LOAM_HD int32_t f2i(float f) { return __builtin_bit_cast(int32_t, f); }
 
 // ------------------------------------------------------------------ spatial hash
+// Cells are grouped in 4x4x4 blocks: the block is hashed, the cell's position in it is the low 6
+// bits.  Three consecutive cells along an axis differ mod 4, so the 27 cells around any cell fall
+// in 27 different buckets of any table of >= 64 buckets (no point is listed twice by a 3x3x3
+// search), and a neighbourhood's bucket ranges lie in a few 64-entry runs of the table.
 LOAM_HD uint32_t cell_hash(int ix, int iy, int iz) {
-  uint32_t h = (uint32_t)ix * 73856093u ^ (uint32_t)iy * 19349663u ^ (uint32_t)iz * 83492791u;
+  uint32_t h = (uint32_t)(ix >> 2) * 73856093u ^ (uint32_t)(iy >> 2) * 19349663u ^ (uint32_t)(iz >> 2) * 83492791u;
   h ^= h >> 16;
   h *= 0x7feb352du;
   h ^= h >> 15;
-  return h;
+  return (h << 6) | (uint32_t)(ix & 3) | ((uint32_t)(iy & 3) << 2) | ((uint32_t)(iz & 3) << 4);
 }
 LOAM_HD int cell_of(float v, float inv_h) { return (int)floorf(v * inv_h); }
 

@@ -728,28 +728,34 @@ struct Top5 {
 };
 // (distance, index) as one ordered 64-bit key: distances are >= +0, so their bits order as they do
 LOAM_D uint64_t top5_key(float d, int idx) { return ((uint64_t)__float_as_uint(d) << 32) | (uint32_t)idx; }
-LOAM_D void top5_offer(Top5& t, float d, int idx) {
-  // ascending (distance, index); a point already held (a seed, or two cells in one bucket) is
-  // skipped.  Branch-free insertion: lt_k = key < K_k is monotone in k (the list is sorted), so
-  // slot k takes K_{k-1} where lt_{k-1}, the key where lt_k alone, else keeps K_k
+// sorted insertion of a key below K_4 (branch-free: lt_k = key < K_k is monotone in k, so slot k
+// takes K_{k-1} where lt_{k-1}, the key where lt_k alone, else keeps K_k)
+LOAM_D void top5_insert(Top5& t, const uint64_t (&K)[5], uint64_t key) {
+  const bool l0 = key < K[0], l1 = key < K[1], l2 = key < K[2], l3 = key < K[3];
+  const uint64_t N[5] = {l0 ? key : K[0], l0 ? K[0] : (l1 ? key : K[1]), l1 ? K[1] : (l2 ? key : K[2]),
+                         l2 ? K[2] : (l3 ? key : K[3]), l3 ? K[3] : key};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    t.d[k] = __uint_as_float((uint32_t)(N[k] >> 32));
+    t.i[k] = (int)(uint32_t)N[k];
+  }
+}
+// an offer that cannot repeat a held point (the 5-NN candidate walk: every map point is listed
+// once, and a list seeded with copies of the bound B takes only keys below B)
+LOAM_D void top5_offer_new(Top5& t, float d, int idx) {
   const uint64_t key = top5_key(d, idx);
   uint64_t K[5];
 #pragma unroll
   for (int k = 0; k < 5; ++k) K[k] = top5_key(t.d[k], t.i[k]);
-  if (key < K[4] && key != K[0] && key != K[1] && key != K[2] && key != K[3]) {
-    const bool l0 = key < K[0], l1 = key < K[1], l2 = key < K[2], l3 = key < K[3];
-    const uint64_t n4 = l3 ? K[3] : key;
-    const uint64_t n3 = l2 ? K[2] : (l3 ? key : K[3]);
-    const uint64_t n2 = l1 ? K[1] : (l2 ? key : K[2]);
-    const uint64_t n1 = l0 ? K[0] : (l1 ? key : K[1]);
-    const uint64_t n0 = l0 ? key : K[0];
-    const uint64_t N[5] = {n0, n1, n2, n3, n4};
+  if (key < K[4]) top5_insert(t, K, key);
+}
+LOAM_D void top5_offer(Top5& t, float d, int idx) {
+  // ascending (distance, index); a point already held is skipped (the merge of lists)
+  const uint64_t key = top5_key(d, idx);
+  uint64_t K[5];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      t.d[k] = __uint_as_float((uint32_t)(N[k] >> 32));
-      t.i[k] = (int)(uint32_t)N[k];
-    }
-  }
+  for (int k = 0; k < 5; ++k) K[k] = top5_key(t.d[k], t.i[k]);
+  if (key < K[4] && key != K[0] && key != K[1] && key != K[2] && key != K[3]) top5_insert(t, K, key);
 }
 
 // the 27 neighbour cells (index (dx+1) + 3(dy+1) + 9(dz+1)): centre, faces, edges, corners
@@ -923,7 +929,7 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
     for (int u = 0; u < kNnInFlight; ++u) a[u] = hp[idx[u]];
 #pragma unroll
     for (int u = 0; u < kNnInFlight; ++u)
-      if (k + u < mine) top5_offer(t, sqdist(a[u].x, a[u].y, a[u].z, q.x, q.y, q.z), __builtin_bit_cast(int, a[u].w));
+      if (k + u < mine) top5_offer_new(t, sqdist(a[u].x, a[u].y, a[u].z, q.x, q.y, q.z), __builtin_bit_cast(int, a[u].w));
   }
 }
 
@@ -1020,28 +1026,45 @@ LOAM_D void mp_nn_query(const MpBuffers& b, const MpNnCtx& c, int q, int nsc, bo
   const bool corner = q < nsc;
   int4* qnn = c.qnn;
   sel = loampose::point_to_map(r, c.stack[corner ? q : b.capC + (q - nsc)]);
-#pragma unroll
-  for (int k = 0; k < 5; ++k) { t.d[k] = 3.4e38f; t.i[k] = 0x7fffffff; }
-  if (!first) {  // seed with the previous iteration's neighbours: a tight bound from the start
+  float bd = 3.4e38f;
+  int bi = 0x7fffffff;
+  if (!first) {
+    // The previous iteration's five neighbours (when they were five distinct points, n1.z) bound the
+    // search: B = the largest of their (distance, index) keys at the moved query.  The list starts
+    // as five copies of B and takes only keys below B, so it ends with the points below B — the
+    // true 5-NN whenever they lie in the searched cells, the B point itself filling the fifth place
+    // when only four lie below it (B is a real point) — and no seed needs to be offered or
+    // recognised when the walk meets it again
     const int4 n0 = qnn[2 * q], n1 = qnn[2 * q + 1];
-    const int prev[5] = {n0.x, n0.y, n0.z, n0.w, n1.x};
-    const float4* from = corner ? c.fromC : c.fromS;
+    if (n1.z) {
+      const int prev[5] = {n0.x, n0.y, n0.z, n0.w, n1.x};
+      const float4* from = corner ? c.fromC : c.fromS;
+      uint64_t B = 0;
 #pragma unroll
-    for (int k = 0; k < 5; ++k)
-      if (prev[k] != 0x7fffffff) {
+      for (int k = 0; k < 5; ++k) {
         LOAM_CHECK(prev[k] >= 0 && prev[k] < (corner ? c.nfc : c.nfs), prev[k], q);
         const float4 a = from[prev[k]];
-        top5_offer(t, sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z), prev[k]);
-        ++work;
+        const uint64_t key = top5_key(sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z), prev[k]);
+        B = key > B ? key : B;
       }
+      work += 5;
+      bd = __uint_as_float((uint32_t)(B >> 32));
+      bi = (int)(uint32_t)B;
+    }
   }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) { t.d[k] = bd; t.i[k] = bi; }
   if (corner) knn5_flat<S, L>(c.hcs, c.hcp, c.TC, sel, t, lst, work, sub);
   else knn5_flat<S, L>(c.hss, c.hsp, c.TS, sel, t, lst, work, sub);
   if constexpr (L > 1) knn5_merge<L>(t);
   LOAM_CHECK(q < b.cap_stack && (t.i[4] == 0x7fffffff || t.i[4] < (corner ? c.nfc : c.nfs)), q, t.i[4]);
   if (sub == 0) {
     qnn[2 * q] = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
-    qnn[2 * q + 1] = make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0);
+    // seeds for the next iteration only when these are five distinct map points (a rejected
+    // search can end with copies of B or sentinels; the list is sorted, so copies are adjacent)
+    const int distinct = t.i[4] != 0x7fffffff && t.i[0] != t.i[1] && t.i[1] != t.i[2] && t.i[2] != t.i[3] &&
+                         t.i[3] != t.i[4];
+    qnn[2 * q + 1] = make_int4(t.i[4], __float_as_int(t.d[4]), distinct, 0);
   }
 }
 
@@ -1908,6 +1931,7 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
   b.map_cap = map_cap;
   b.max_iter = max_iter;
   b.tmax = next_pow2(map_cap) > (1 << 20) ? (1 << 20) : next_pow2(map_cap);
+  if (b.tmax < 64) b.tmax = 64;  // >= 64 buckets: a 3x3x3 search never lists a bucket twice (cell_hash)
   b.pool_cur = 0;
   const size_t Pm = (size_t)P * map_cap, Ps = (size_t)P * b.cap_stack;
   A(&b.state, (size_t)P * kMpStateFloats * sizeof(float));
