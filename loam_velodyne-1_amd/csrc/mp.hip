@@ -829,15 +829,15 @@ constexpr int kMpFitThreads = 64;
 constexpr int kNnInFlight = 8;  // measured k_mp_nn ms/step: 2 -> 4.17, 4 -> 3.95, 8 -> 3.88, 16 -> 5.33
 // cells whose bucket-range loads are in flight together
 #ifndef LOAM_NN_RANGE_GROUP
-#define LOAM_NN_RANGE_GROUP 9  // (k_mp_nn ms/step at batch 1024: 1 -> 3.83, 7 -> 3.52, 9 -> 3.51, 14 -> 3.60 (spills))
+#define LOAM_NN_RANGE_GROUP 27  // one-word records: all 27 in flight (ms/step: 9 -> 3.11, 27 -> 3.04; 8-byte pairs: 1 -> 3.83, 9 -> 3.51)
 #endif
 constexpr int kNnRangeGroup = LOAM_NN_RANGE_GROUP;
 // L > 1: one of L lanes searching the same query: every lane lists the same cells, lane `sub`
 // takes the candidates sub, sub + L, ... of the concatenated list (a crowded cell is shared too);
 // the caller merges the L partial top-5 lists (knn5_merge)
 template <int S = kMpQueryThreads, int L = 1>
-LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5& t, uint32_t* lst, int& work,
-                      int sub = 0) {
+LOAM_D void knn5_flat(const int* start, const uint32_t* rec, const float4* hp, int T, float4 q, Top5& t,
+                      uint32_t* lst, int& work, int sub = 0) {
   if (T <= 0) return;
   const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
   const float gxl = q.x - (float)cx, gyl = q.y - (float)cy, gzl = q.z - (float)cz;
@@ -849,7 +849,7 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
   // tested in the same block is waited for at once: one dependent round trip per cell)
 #pragma unroll
   for (int g0 = 0; g0 < 27; g0 += kNnRangeGroup) {
-    int2 rg[kNnRangeGroup];
+    uint32_t rg[kNnRangeGroup];
 #pragma unroll
     for (int u = 0; u < kNnRangeGroup; ++u) {
       const int o = g0 + u;
@@ -860,22 +860,21 @@ LOAM_D void knn5_flat(const int* start, const float4* hp, int T, float4 q, Top5&
       const float gy = dy < 0 ? gyl : (dy > 0 ? gyh : 0.0f);
       const float gz = dz < 0 ? gzl : (dz > 0 ? gzh : 0.0f);
       const float bd = sqdist(gx, gy, gz, 0.0f, 0.0f, 0.0f);
-      rg[u] = make_int2(0, 0);
+      rg[u] = 0;
       if (bd < 1.0f && bd <= bound) {
         const uint32_t h = cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1);
-        rg[u] = load_pair(start + h);  // start[h], start[h + 1]: one 8-byte request
+        rg[u] = rec[h];  // the bucket's range packed in one word (hash_rec)
       }
     }
 #pragma unroll
     for (int u = 0; u < kNnRangeGroup; ++u) {
       if (g0 + u >= 27) break;
-      const int b0 = rg[u].x, cnt = rg[u].y - b0;
-      LOAM_CHECK(b0 >= 0 && cnt >= 0, b0, cnt);
-      if (cnt > 0) {
-        if (b0 >= (1 << 19) || cnt >= (1 << 13)) fits = false;
-        lst[n * S] = (uint32_t)b0 | ((uint32_t)cnt << 19);
+      const uint32_t e = rg[u];
+      if (e == kRecNone) fits = false;
+      else if (e >> 19) {
+        lst[n * S] = e;
         ++n;
-        total += cnt;
+        total += (int)(e >> 19);
       }
     }
   }
@@ -999,6 +998,7 @@ struct MpFit {
 struct MpNnCtx {
   const float4* stack;
   const int *hcs, *hss;
+  const uint32_t *hcr, *hsr;
   const float4 *hcp, *hsp, *fromC, *fromS;
   int TC, TS, nfc, nfs;
   int4* qnn;
@@ -1008,6 +1008,8 @@ LOAM_D MpNnCtx mp_nn_ctx(const MpBuffers& b, int p) {
   c.stack = b.stack + (size_t)p * b.cap_stack;
   c.hcs = b.hC_start + (size_t)p * (b.tmax + 1);
   c.hss = b.hS_start + (size_t)p * (b.tmax + 1);
+  c.hcr = b.hC_rec + (size_t)p * b.tmax;
+  c.hsr = b.hS_rec + (size_t)p * b.tmax;
   c.hcp = b.hC_pts + (size_t)p * b.map_cap;
   c.hsp = b.hS_pts + (size_t)p * b.map_cap;
   c.TC = b.hC_T[p];
@@ -1054,8 +1056,8 @@ LOAM_D void mp_nn_query(const MpBuffers& b, const MpNnCtx& c, int q, int nsc, bo
   }
 #pragma unroll
   for (int k = 0; k < 5; ++k) { t.d[k] = bd; t.i[k] = bi; }
-  if (corner) knn5_flat<S, L>(c.hcs, c.hcp, c.TC, sel, t, lst, work, sub);
-  else knn5_flat<S, L>(c.hss, c.hsp, c.TS, sel, t, lst, work, sub);
+  if (corner) knn5_flat<S, L>(c.hcs, c.hcr, c.hcp, c.TC, sel, t, lst, work, sub);
+  else knn5_flat<S, L>(c.hss, c.hsr, c.hsp, c.TS, sel, t, lst, work, sub);
   if constexpr (L > 1) knn5_merge<L>(t);
   LOAM_CHECK(q < b.cap_stack && (t.i[4] == 0x7fffffff || t.i[4] < (corner ? c.nfc : c.nfs)), q, t.i[4]);
   if (sub == 0) {
@@ -1951,6 +1953,8 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
   A(&b.from, Pm * sizeof(float4));
   A(&b.hC_start, (size_t)P * (b.tmax + 1) * sizeof(int));
   A(&b.hS_start, (size_t)P * (b.tmax + 1) * sizeof(int));
+  A(&b.hC_rec, (size_t)P * b.tmax * sizeof(uint32_t));
+  A(&b.hS_rec, (size_t)P * b.tmax * sizeof(uint32_t));
   // bucket counters: one set per cloud kind for small batches, whose two builds run together
   A(&b.h_fill, (size_t)(P <= 4 ? 2 : 1) * P * b.tmax * sizeof(int));
   A(&b.hC_T, (size_t)P * sizeof(int));
@@ -1999,7 +2003,7 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
 
 void mp_free(MpBuffers& b) {
   void* ptrs[] = {b.state, b.istate, b.slots, b.pool, b.valid, b.vpre, b.inC, b.inS, b.inF, b.in_n, b.in_pose,
-                  b.stack2, b.stack, b.nstack, b.from, b.hC_start, b.hS_start, b.h_fill, b.hC_T, b.hS_T,
+                  b.stack2, b.stack, b.nstack, b.from, b.hC_start, b.hS_start, b.hC_rec, b.hS_rec, b.h_fill, b.hC_T, b.hS_T,
                   b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.citems, b.nitems, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
                   b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_l0, b.vg_l1, b.vg_lin, b.vg_cnt, b.reg, b.nreg, b.part, b.done, b.rot};
@@ -2055,7 +2059,9 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   hc.inv_h = 1.0f;
   hc.shift = 0;  // the 5-NN search scans whole buckets: keep them to single cells
   hc.chunks = nullptr;
+  hc.rec = b.hC_rec;
   HashJob hs = hc;
+  hs.rec = b.hS_rec;
   hs.pts_off = b.nfrom; hs.pts_off_stride = 2;
   hs.count = b.nfrom + 1; hs.start = b.hS_start; hs.out = b.hS_pts; hs.tsize = b.hS_T;
   if (P <= 4) hs.fill = b.h_fill + (size_t)P * b.tmax;

@@ -84,6 +84,7 @@ struct MpBuffers {
   // FromMap + hashes
   float4* from = nullptr;     // [P][map_cap] corner then surf
   int *hC_start = nullptr, *hS_start = nullptr, *h_fill = nullptr, *hC_T = nullptr, *hS_T = nullptr;
+  uint32_t *hC_rec = nullptr, *hS_rec = nullptr;  // [P][tmax] packed bucket ranges (HashJob::rec)
   float4 *hC_pts = nullptr, *hS_pts = nullptr;   // [P][map_cap]
   int* nfrom = nullptr;       // [P][2]
   // per-query L-M outputs of the current iteration

@@ -35,6 +35,11 @@ using namespace loamdev;
 
 // diagnostic builds: count only one phase's gathered points in od_assoc_gathered (1: the 27 cells,
 // 2: the chunk fallback beyond one cell, 3: the ring windows); 0 (product): all
+// LOAM_ASSOC_SKIP (timing attribution builds only, results wrong): 1 no ring windows, 2 no chunk
+// fallback of the nearest-neighbour search, 3 neither
+#ifndef LOAM_ASSOC_SKIP
+#define LOAM_ASSOC_SKIP 0
+#endif
 #ifndef LOAM_ASSOC_PHASE
 #define LOAM_ASSOC_PHASE 0
 #endif
@@ -78,7 +83,7 @@ constexpr int kHashLds = 8192;
 // counters (read back with atomic loads: the counts were made by L2 atomics)
 template <int NT, bool LDS>
 LOAM_D void hash_sort(const HashJob& j, const float4* pts, int n, int T, int* start, float4* out, int* fill,
-                      int* scratch) {
+                      int* scratch, uint32_t* rec) {
   const int tid = threadIdx.x;
   auto ld = [&](int b) {
     if constexpr (LDS) return fill[b];
@@ -104,6 +109,7 @@ LOAM_D void hash_sort(const HashJob& j, const float4* pts, int n, int T, int* st
   for (int b = b0; b < b1; ++b) {
     const int c = ld(b);
     start[b] = run;
+    if (rec) rec[b] = hash_rec(run, c);
     if constexpr (LDS) fill[b] = run;
     else __hip_atomic_store(&fill[b], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     run += c;
@@ -160,8 +166,9 @@ __global__ __launch_bounds__(NT) void k_hash_build(HashJob j) {
   int T = next_pow2(m > 64 ? m : 64);
   if (T > j.tmax) T = j.tmax;
   if (tid == 0) j.tsize[p] = T;
-  if (T <= kHashLds) hash_sort<NT, true>(j, pts, n, T, start, out, lfill, scratch);
-  else hash_sort<NT, false>(j, pts, n, T, start, out, j.fill + (size_t)p * j.tmax, scratch);
+  uint32_t* rec = j.rec ? j.rec + (size_t)p * j.tmax : nullptr;
+  if (T <= kHashLds) hash_sort<NT, true>(j, pts, n, T, start, out, lfill, scratch, rec);
+  else hash_sort<NT, false>(j, pts, n, T, start, out, j.fill + (size_t)p * j.tmax, scratch, rec);
   if (j.chunks)  // chunk boxes of the source order
     chunk_boxes(pts, n, j.chunks + (size_t)p * 2 * chunks_of((int)j.pts_stride), tid >> 6, NT / 64);
 }
@@ -219,6 +226,7 @@ __global__ __launch_bounds__(1024) void k_hash_scan(HashPair hp) {
   const int T = hash_table_size(j, n);
   int* fill = j.fill + (size_t)p * j.tmax;
   int* start = j.start + (size_t)p * (j.tmax + 1);
+  uint32_t* rec = j.rec ? j.rec + (size_t)p * j.tmax : nullptr;
   __shared__ int scratch[32];
   const int per = (T + 1023) / 1024;
   const int b0 = tid * per, b1 = min(T, b0 + per);
@@ -251,6 +259,9 @@ __global__ __launch_bounds__(1024) void k_hash_scan(HashPair hp) {
         start[b0 + 4 * k + 1] = r.y;
         start[b0 + 4 * k + 2] = r.z;
         start[b0 + 4 * k + 3] = r.w;
+        if (rec)
+          *(uint4*)(rec + b0 + 4 * k) = make_uint4(hash_rec(r.x, v[k].x), hash_rec(r.y, v[k].y),
+                                                   hash_rec(r.z, v[k].z), hash_rec(r.w, v[k].w));
       }
     if (tid == 0) start[T] = tot;
     return;
@@ -262,6 +273,7 @@ __global__ __launch_bounds__(1024) void k_hash_scan(HashPair hp) {
   for (int b = b0; b < b1; ++b) {
     const int c = fill[b];
     start[b] = run;
+    if (rec) rec[b] = hash_rec(run, c);
     fill[b] = run;
     run += c;
   }
@@ -366,6 +378,7 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
   best = wave_min_u64(best);
   __builtin_amdgcn_wave_barrier();
   if (best != ~0ull && __uint_as_float((uint32_t)(best >> 32)) < h * h) return best;
+  if (LOAM_ASSOC_SKIP & 2) return best;
   // farther than one cell: the chunks of the whole cloud that may hold a point closer than 5 m
   best = ~0ull;
   const int nch = (n + kChunk - 1) / kChunk;
@@ -522,6 +535,7 @@ LOAM_D void wave_assoc_corner(const float4* CL, const float4* ch, int fwd_end, u
   if (!(D(d0) < 25)) return;
   const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u);
   ind1 = c;
+  if (LOAM_ASSOC_SKIP & 1) return;
   const float bw = sj >= 0 && window_member(sj, sr, c, scan, fwd_end, true, false) ? sd : 25.0f;
   uint64_t best = ~0ull;
   wave_window(CL, ch, c, fwd_end, +1, scan, sel, bw, wpts, wbox, [&](int j, int r, float d) {
@@ -554,6 +568,7 @@ LOAM_D void wave_assoc_surf(const float4* SL, const float4* ch, int fwd_end, uin
   if (!(D(d0) < 25)) return;
   const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u);
   ind1 = c;
+  if (LOAM_ASSOC_SKIP & 1) return;
   const float b2 = sj2 >= 0 && window_member(sj2, sr2, c, scan, fwd_end, false, true) ? sd2 : 25.0f;
   const float b3 = sj3 >= 0 && window_member(sj3, sr3, c, scan, fwd_end, false, false) ? sd3 : 25.0f;
   const float bw = fmaxf(b2, b3);

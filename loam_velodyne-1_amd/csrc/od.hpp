@@ -53,7 +53,13 @@ struct HashJob {
   int shift;            // T = pow2 >= count >> shift
   float4* chunks;       // optional [P][2 * chunks_of(pts_stride)]: per 64-point chunk of the source
                         // order, (min x, y, z, min ring) and (max x, y, z, max ring)
+  uint32_t* rec = nullptr;  // optional [P][tmax]: bucket b's range packed as start | count << 19
+                            // (hash_rec), kRecNone when it does not fit
 };
+constexpr uint32_t kRecNone = 0xffffffffu;
+LOAM_HD uint32_t hash_rec(int start, int count) {
+  return start < (1 << 19) && count < (1 << 13) ? (uint32_t)start | ((uint32_t)count << 19) : kRecNone;
+}
 
 struct OdBuffers {
   int P = 0, capC = 0, capS = 0, cap_q = 0, gq = 0, tC = 0, tS = 0, max_iter = 25;
