@@ -826,7 +826,17 @@ constexpr int kMpFitThreads = 64;
 // iterates max(candidates per lane) instead of the union of its lanes' cells x buckets.  `lst` =
 // the lane's LDS column (stride kMpQueryThreads).  Ranges are packed start:19 | count:13; a lane
 // whose ranges do not fit falls back to knn5.
-constexpr int kNnInFlight = 8;  // measured k_mp_nn ms/step: 2 -> 4.17, 4 -> 3.95, 8 -> 3.88, 16 -> 5.33
+#ifndef LOAM_NN_INFLIGHT
+#define LOAM_NN_INFLIGHT 8  // measured k_mp_nn ms/step: 2 -> 4.17, 4 -> 3.95, 8 -> 3.88, 16 -> 5.33
+#endif
+constexpr int kNnInFlight = LOAM_NN_INFLIGHT;
+#ifndef LOAM_NN_LIST
+#define LOAM_NN_LIST 27  // k_mp_nn list entries per lane (non-empty cells beyond it: the unlisted search)
+#endif
+constexpr int kNnListCap = LOAM_NN_LIST;
+#ifndef LOAM_NN_WPE
+#define LOAM_NN_WPE 5  // k_mp_nn waves per SIMD
+#endif
 // cells whose bucket-range loads are in flight together
 #ifndef LOAM_NN_RANGE_GROUP
 #define LOAM_NN_RANGE_GROUP 27  // one-word records: all 27 in flight (ms/step: 9 -> 3.11, 27 -> 3.04; 8-byte pairs: 1 -> 3.83, 9 -> 3.51)
@@ -835,7 +845,7 @@ constexpr int kNnRangeGroup = LOAM_NN_RANGE_GROUP;
 // L > 1: one of L lanes searching the same query: every lane lists the same cells, lane `sub`
 // takes the candidates sub, sub + L, ... of the concatenated list (a crowded cell is shared too);
 // the caller merges the L partial top-5 lists (knn5_merge)
-template <int S = kMpQueryThreads, int L = 1>
+template <int S = kMpQueryThreads, int L = 1, int CAPL = 27>
 LOAM_D void knn5_flat(const int* start, const uint32_t* rec, const float4* hp, int T, float4 q, Top5& t,
                       uint32_t* lst, int& work, int sub = 0) {
   if (T <= 0) return;
@@ -872,9 +882,13 @@ LOAM_D void knn5_flat(const int* start, const uint32_t* rec, const float4* hp, i
       const uint32_t e = rg[u];
       if (e == kRecNone) fits = false;
       else if (e >> 19) {
-        lst[n * S] = e;
-        ++n;
-        total += (int)(e >> 19);
+        if (n < CAPL) {
+          lst[n * S] = e;
+          ++n;
+          total += (int)(e >> 19);
+        } else {
+          fits = false;  // more non-empty cells than the list holds
+        }
       }
     }
   }
@@ -890,7 +904,7 @@ LOAM_D void knn5_flat(const int* start, const uint32_t* rec, const float4* hp, i
   auto take = [&]() {
     pos = (int)(nx & ((1u << 19) - 1));
     left = (int)(nx >> 19);
-    nx = lst[min(ci, 26) * S];
+    nx = lst[min(ci, CAPL - 1) * S];
     ++ci;
   };
   auto next = [&]() {  // index of the lane's next candidate
@@ -1022,7 +1036,7 @@ LOAM_D MpNnCtx mp_nn_ctx(const MpBuffers& b, int p) {
   return c;
 }
 
-template <int S = kMpQueryThreads, int L = 1>
+template <int S = kMpQueryThreads, int L = 1, int CAPL = 27>
 LOAM_D void mp_nn_query(const MpBuffers& b, const MpNnCtx& c, int q, int nsc, bool first, const loampose::MapRot& r,
                         uint32_t* lst, float4& sel, Top5& t, int& work, int sub = 0) {
   const bool corner = q < nsc;
@@ -1056,8 +1070,8 @@ LOAM_D void mp_nn_query(const MpBuffers& b, const MpNnCtx& c, int q, int nsc, bo
   }
 #pragma unroll
   for (int k = 0; k < 5; ++k) { t.d[k] = bd; t.i[k] = bi; }
-  if (corner) knn5_flat<S, L>(c.hcs, c.hcr, c.hcp, c.TC, sel, t, lst, work, sub);
-  else knn5_flat<S, L>(c.hss, c.hsr, c.hsp, c.TS, sel, t, lst, work, sub);
+  if (corner) knn5_flat<S, L, CAPL>(c.hcs, c.hcr, c.hcp, c.TC, sel, t, lst, work, sub);
+  else knn5_flat<S, L, CAPL>(c.hss, c.hsr, c.hsp, c.TS, sel, t, lst, work, sub);
   if constexpr (L > 1) knn5_merge<L>(t);
   LOAM_CHECK(q < b.cap_stack && (t.i[4] == 0x7fffffff || t.i[4] < (corner ? c.nfc : c.nfs)), q, t.i[4]);
   if (sub == 0) {
@@ -1256,14 +1270,14 @@ LOAM_D void mp_step(const MpBuffers& b, int p, const double* tot, MpStepScratch&
 // waves per SIMD (<= 96 VGPRs; the LDS lists allow five workgroups per CU).  COUNT: the profiling
 // variant that also sums its work (candidates, bucket ranges) into the frame's istate
 template <bool COUNT>
-__global__ __launch_bounds__(kMpNnThreads) __attribute__((amdgpu_waves_per_eu(5))) void k_mp_nn(MpBuffers b) {
+__global__ __launch_bounds__(kMpNnThreads) __attribute__((amdgpu_waves_per_eu(LOAM_NN_WPE))) void k_mp_nn(MpBuffers b) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, tid = threadIdx.x;
   const int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan] || ist[kMiStop]) return;
   const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
   const int nq = nsc + nss;
-  __shared__ uint32_t lists[27 * kMpNnThreads];
+  __shared__ uint32_t lists[kNnListCap * kMpNnThreads];
   uint32_t* lst = lists + tid;
   const bool first = ist[kMiIters] == 0;
   const loampose::MapRot r = rot_load(b, p);
@@ -1272,7 +1286,7 @@ __global__ __launch_bounds__(kMpNnThreads) __attribute__((amdgpu_waves_per_eu(5)
   for (int q = blk.x * kMpNnThreads + tid; q < nq; q += gridDim.x * kMpNnThreads) {
     float4 sel;
     Top5 t;
-    mp_nn_query<kMpNnThreads>(b, c, q, nsc, first, r, lst, sel, t, work);
+    mp_nn_query<kMpNnThreads, 1, kNnListCap>(b, c, q, nsc, first, r, lst, sel, t, work);
   }
   if (!COUNT) return;
   const int ncand = wave_sum(work & ((1 << kWorkCellShift) - 1)), ncell = wave_sum(work >> kWorkCellShift);

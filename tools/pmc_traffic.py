@@ -27,10 +27,17 @@ def load(path):
         k = short(r["Kernel_Name"])
         inst[k][0] += float(r["Counter_Value"])
         inst[k][1] += 1
-    # kernels with a profiling (COUNT) variant (k_mp_nn<true>, k_od_assoc<true, ...>) run it in
-    # the bench's profiling pass, whose times and work counters the roofline uses: take that one
+    # kernels with a profiling (COUNT) variant (k_mp_nn<true>, k_od_assoc<true, ...>): the variant
+    # launches in place of the plain one in the bench's profiling pass, so both are dispatches of
+    # the same launch: every dispatch of either counts, averaged together
     counted = {k.split("<")[0] for k in inst if "<true" in k}
-    inst = {k: v for k, v in inst.items() if k.split("<")[0] not in counted or "<true" in k}
+    merged = collections.defaultdict(lambda: [0.0, 0])
+    for k, (v, n) in inst.items():
+        if k.split("<")[0] in counted:
+            merged[k.split("<")[0] + "<any>"][0] += v
+            merged[k.split("<")[0] + "<any>"][1] += n
+    inst = {k: v for k, v in inst.items() if k.split("<")[0] not in counted}
+    inst.update(merged)
     agg = collections.defaultdict(lambda: [0.0, 0])
     for k, (v, n) in inst.items():
         base = k.split("<")[0]
