@@ -816,7 +816,10 @@ constexpr int kMpQueryThreads = 256;
 constexpr int kMpNnLanes = LOAM_MP_NN_LANES;
 // k_mp_nn workgroup size (measured k_mp_nn ms/step at batch 1024: 64 -> 3.83, 128 -> 3.81-3.86,
 // 256 -> 3.92-3.95): a workgroup's LDS is released when its slowest lane is done
-constexpr int kMpNnThreads = 128;
+#ifndef LOAM_NN_THREADS
+#define LOAM_NN_THREADS 128  // (round 3: 64 -> 3.00 / 0.648 ms/step at batch 1024 / 128, 128 -> 3.03 / 0.652)
+#endif
+constexpr int kMpNnThreads = LOAM_NN_THREADS;
 // k_mp_fit workgroup size (ms/step at batch 1024: 256 -> 1.27-1.29, 128 -> 1.16-1.20, 64 -> 1.17)
 constexpr int kMpFitThreads = 64;
 
