@@ -249,6 +249,26 @@ def test_batch_mapping_parity_64(loam, oc, sg):
     np.testing.assert_array_equal(aft, aft2)
 
 
+def test_batch_sparse_map_parity(loam, oc, sg):
+    """Maps built from a thinned previous sweep (every 4th return): many 5-NN searches end with the
+    fifth neighbour at >= 1 m (rejected, :719 / :826) — lists left holding copies of the bound B,
+    seeds withheld from the next iteration (q_nn distinct flag) — and the poses must still follow
+    the oracle, the same on a repeated run."""
+    prevs, curs = sg.batch_problems(16, base_seed=1400)
+    prevs = [p[::4].copy() for p in prevs]
+    e = loam.Engine()
+    e.batch_upload(prevs, curs)
+    e.batch_run()
+    od, aft, _ = e.batch_download()
+    for i in range(16):
+        od_o, aft_o, _ = oc.problem(prevs[i], curs[i])
+        assert max(np.abs(od[i] - od_o).max(), np.abs(aft[i] - aft_o).max()) <= POSE_TOL, i
+    e.batch_run()
+    od2, aft2, _ = e.batch_download()
+    np.testing.assert_array_equal(od, od2)
+    np.testing.assert_array_equal(aft, aft2)
+
+
 def _push_out(raw, rng_m=250.0, az_deg=(0.0, 12.0)):
     """top-ring returns within an azimuth block moved out to rng_m metres along their rays"""
     raw = raw.copy()
