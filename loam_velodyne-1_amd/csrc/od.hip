@@ -844,6 +844,11 @@ LOAM_D void od_row_coeff(const OdBuffers& b, const FeatView& f, int p, int q, in
   if (!ok) cf = make_float4(0, 0, 0, 0);
 }
 
+// A stored row was accepted iff its coefficient direction is not zero: od_row_coeff zeroes the
+// coefficients of a rejected row, and an accepted row's (x, y, z) is a unit normal times a weight
+// above 0.1 (or NaN / inf, which also count), so no separate flag needs to be read back
+LOAM_D bool row_ok(const float4& c) { return c.x != 0.0f || c.y != 0.0f || c.z != 0.0f; }
+
 // The coefficient-free factors of each Jacobian entry (:714-753) of a row whose raw point is po:
 // every entry is (e0)*coeff.x + (e1)*coeff.y + (e2)*coeff.z with e depending on the raw point and
 // the current transform only, evaluated in the reference's expression order
@@ -953,7 +958,7 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdR
       for (int u = 0; u < 2; ++u) {
         const int it = it0 + u;
         cv4[u] = it <= iter ? qcf[(size_t)it * b.cap_q + q] : make_float4(0, 0, 0, 0);
-        okv[u] = it <= iter ? qok[(size_t)it * b.cap_q + q] != 0 : false;
+        okv[u] = row_ok(cv4[u]);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u)
@@ -1040,7 +1045,7 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows_small(OdBuffers b, FeatV
       qok[(size_t)iter * b.cap_q + q] = (int8_t)ok;
     } else {
       c4 = qcf[(size_t)it * b.cap_q + q];
-      okit = qok[(size_t)it * b.cap_q + q] != 0;
+      okit = row_ok(c4);
     }
   }
   __syncthreads();
