@@ -92,3 +92,16 @@ def test_bench_spawns_two_ranks_gloo(sg, split):
     other = out["strong" if split == "weak" else "weak"]
     assert other["global_batch"] == 2 * other_per and other["problems_per_gpu"] == other_per
     assert out["value"] > 0 and out["roofline"]["kernel"] == "k_mp_nn"
+
+
+def test_bench_single_gpu_share_child(sg):
+    """At N = 1 the per-GPU share of 8 GPUs (global batch / 8) is timed in a child process started
+    before the parent touches the device, as one of the 8 ranks would run it; its line lands in the
+    other split's entry."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    out = _run_bench(["--steps", "2", "--warmup", "1", "--batch", "16", "--global-batch", "16", "--cpu-sample", "0",
+                      "--stream-sweeps", "0", "--latency-runs", "0", "--profile-steps", "1"], {})
+    assert out["n_gpus"] == 1 and out["config"]["global_batch"] == 16
+    share = out["weak"]["one_gpu_at_8gpu_share"]
+    assert share["problems"] == 2 and share["value"] > 0 and share["ms_per_step"] > 0
