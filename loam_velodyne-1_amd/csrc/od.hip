@@ -106,13 +106,28 @@ LOAM_D void hash_sort(const HashJob& j, const float4* pts, int n, int T, int* st
   for (int b = b0; b < b1; ++b) local += ld(b);
   int tot;
   int run = block_excl_scan<NT>(local, scratch, tot);
-  for (int b = b0; b < b1; ++b) {
-    const int c = ld(b);
-    start[b] = run;
-    if (rec) rec[b] = hash_rec(run, c);
-    if constexpr (LDS) fill[b] = run;
-    else __hip_atomic_store(&fill[b], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    run += c;
+  if constexpr (LDS) {
+    // the bucket starts into LDS, then start / rec written bucket-consecutive across the lanes
+    // (a thread's own run of buckets would make every store a 64-line scatter)
+    for (int b = b0; b < b1; ++b) {
+      const int c = fill[b];
+      fill[b] = run;
+      run += c;
+    }
+    __syncthreads();
+    for (int b = tid; b < T; b += NT) {
+      const int s0 = fill[b], s1 = b + 1 < T ? fill[b + 1] : tot;
+      start[b] = s0;
+      if (rec) rec[b] = hash_rec(s0, s1 - s0);
+    }
+  } else {
+    for (int b = b0; b < b1; ++b) {
+      const int c = ld(b);
+      start[b] = run;
+      if (rec) rec[b] = hash_rec(run, c);
+      __hip_atomic_store(&fill[b], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      run += c;
+    }
   }
   if (tid == 0) start[T] = tot;
   if (!LDS) __threadfence();
