@@ -1879,19 +1879,33 @@ __global__ __launch_bounds__(NT) void k_mp_compact_table(MpBuffers b) {
   }
   __syncthreads();
   const int x0 = tid * E, x1 = min(N, x0 + E);
-  int sum = 0, ne = 0;
-  for (int x = x0; x < x1; ++x) { sum += nn[x]; ne += nn[x] > 0 ? 1 : 0; }
-  int run, nitems;
+  int sum = 0;
+  for (int x = x0; x < x1; ++x) sum += nn[x];
+  int run;
   int off = block_excl_scan<NT>(sum, scratch, run);
-  int it = block_excl_scan<NT>(ne, scratch, nitems);
+  for (int x = x0; x < x1; ++x) {  // counts -> offsets, in LDS
+    const int c = nn[x];
+    nn[x] = off;
+    off += c;
+  }
+  __syncthreads();
+  // the table and the non-empty (kind, cube) list written (kind, cube)-consecutive across the lanes
+  // (each lane's own run of entries would scatter every store): kind | cube << 1 | (valid + 1) << 14
   int* items = b.citems + (size_t)p * 2 * kCubeNum;
-  for (int x = x0; x < x1; ++x) {
-    const int kind = x / kCubeNum, s = x % kCubeNum, n = nn[x];
-    nw[s * 4 + 2 * kind] = off;
-    nw[s * 4 + 1 + 2 * kind] = n;
-    off += n;
-    // the non-empty (kind, cube) list for the copy: kind | cube << 1 | (valid index + 1) << 14
-    if (n > 0) items[it++] = kind | (s << 1) | (((int)vidx[s] + 1) << 14);
+  int nitems = 0;
+  for (int xb = 0; xb < N; xb += NT) {
+    const int x = xb + tid;
+    int n = 0;
+    if (x < N) {
+      const int kind = x / kCubeNum, s = x % kCubeNum, o = nn[x];
+      n = (x + 1 < N ? nn[x + 1] : run) - o;
+      nw[s * 4 + 2 * kind] = o;
+      nw[s * 4 + 1 + 2 * kind] = n;
+    }
+    int tot;
+    const int ex = block_excl_scan<NT>(n > 0 ? 1 : 0, scratch, tot);
+    if (n > 0) items[nitems + ex] = (x / kCubeNum) | ((x % kCubeNum) << 1) | (((int)vidx[x % kCubeNum] + 1) << 14);
+    nitems += tot;
   }
   vpts = block_reduce<NT>(vpts, scratch, [](int a, int c) { return a + c; });
   if (tid == 0) {
