@@ -570,6 +570,10 @@ struct SelShared {
   int nsharp, nlsharp, nflat, ncand, wf, big, loff;
 };
 
+// dynamic LDS bytes added to each k_sr_ringvg workgroup (an occupancy cap for experiments)
+#ifndef LOAM_RINGVG_PAD
+#define LOAM_RINGVG_PAD 0
+#endif
 #ifndef LOAM_RINGVG_HOLD
 #define LOAM_RINGVG_HOLD 1
 #endif
@@ -1460,7 +1464,7 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
                      st, b, p);
   mark("k_sr_features");
   hipLaunchKernelGGL(k_sr_pick, dim3((b.R + kPickWaves - 1) / kPickWaves, b.S), dim3(64 * kPickWaves), 0, st, b, p);
-  hipLaunchKernelGGL(k_sr_ringvg, dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
+  hipLaunchKernelGGL(k_sr_ringvg, dim3(b.R, b.S), dim3(kSelThreads), LOAM_RINGVG_PAD, st, b, p);
   hipLaunchKernelGGL((k_sr_select<kRingCap, 1>), dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
   hipLaunchKernelGGL((k_sr_select<16, 2>), dim3(kBigSlots), dim3(kSelThreads), 0, st, b, p);
   mark("k_sr_select");
