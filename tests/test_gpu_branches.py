@@ -160,6 +160,26 @@ def test_batch_1024_parity(loam, oc, sg):
     np.testing.assert_array_equal(aft[-64:], aft2)
 
 
+def test_batch_8gpu_share_parity(loam, oc, sg):
+    """config 4's strong split on 8 GPUs: the last rank's share (problems 896..1023 of the bench's
+    batch, bench.py --split strong) as one 128-problem batch — the fused fit + rows + step mapping
+    kernel (P <= LOAM_MP_FUSED_MAX) at the exact size a rank runs; problems spread over the share
+    against the oracle, and a repeated run identical"""
+    P, r = 128, 7
+    prevs, curs = sg.batch_problems(P, base_seed=1000 + r * P)
+    e = loam.Engine()
+    e.batch_upload(prevs, curs)
+    e.batch_run()
+    od, aft, _ = e.batch_download()
+    for i in list(range(0, P, 8)) + [P - 1]:
+        od_o, aft_o, _ = oc.problem(prevs[i], curs[i])
+        assert max(np.abs(od[i] - od_o).max(), np.abs(aft[i] - aft_o).max()) <= POSE_TOL, i
+    e.batch_run()
+    od2, aft2, _ = e.batch_download()
+    np.testing.assert_array_equal(od, od2)
+    np.testing.assert_array_equal(aft, aft2)
+
+
 def test_pipeline_matches_oracle(loam, oc, sg):
     """the node pipeline (three contexts on three threads, loam_velodyne-1_amd/pipeline.py) against
     the oracle's sequential node chain: every mapping pose and registered cloud of 40 sweeps"""
