@@ -75,6 +75,11 @@ LOAM_HD float4 transform_to_end(const float* t, const Imu& m, const EndRot& e, f
   if (zero && s >= 0) {
     cx = cy = cz = 1.0;
     sx = sy = sz = 0.0;
+#ifdef LOAM_DIAG_END_NOTRIG
+  } else if (true) {  // timing diagnostic only (wrong results): the per-point trigonometry left out
+    sx = rx; sy = ry; sz = rz;
+    cx = cy = cz = 1.0;
+#endif
   } else {
     dsincos(rx, sx, cx);
     dsincos(ry, sy, cy);
