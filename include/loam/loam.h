@@ -56,7 +56,8 @@ typedef struct { float x, y, z, intensity; } loam_point;
 typedef struct { float rx, ry, rz, tx, ty, tz; } loam_pose6;
 
 /* caller-owned input cloud; x, y, z floats at byte offsets 0, 4, 8 of each record
- * (accepts 16-B PointXYZ/loam_point and 32-B PointXYZI / velodyne XYZIR records) */
+ * (accepts 16-B PointXYZ/loam_point and 32-B PointXYZI / velodyne XYZIR records); stride_bytes a
+ * multiple of 4, data at any alignment (e.g. a PointCloud2 message's own buffer, loam_pc2_cloud) */
 typedef struct { const void *data; uint32_t count; uint32_t stride_bytes; } loam_cloud_in;
 
 /* caller-owned output storage; count = points written (or required, on LOAM_E_CAPACITY) */

@@ -64,7 +64,8 @@ int loam_pc2_parse(const uint8_t *msg, uint32_t size, loam_pc2 *out);
 /* the cloud as loam_scan_registration reads it (x, y, z floats at offsets 0 / 4 / 8 of each
  * record): the message's own points when the layout already is that (no copy), else x, y, z
  * packed into scratch (capacity scratch_cap points; LOAM_E_CAPACITY with the required count in
- * out->count otherwise).  The points stay valid as long as the message / scratch does. */
+ * out->count otherwise).  The points stay valid as long as the message / scratch does; in place,
+ * they are at whatever alignment the message gives them. */
 int loam_pc2_cloud(const loam_pc2 *pc, loam_point *scratch, uint32_t scratch_cap, loam_cloud_in *out);
 
 /* parses a serialized sensor_msgs/Imu: header.stamp, orientation (x, y, z, w), linear_acceleration */

@@ -167,6 +167,10 @@ def default_config(**kw):
 
 
 def _cloud_in(a):
+    """an (n, >= 3) float array, or a ready loam_cloud_in (a strided view of caller memory, e.g. a
+    PointCloud2 message's records: rosbag.pc2_cloud_in) passed through as is"""
+    if isinstance(a, CloudIn):
+        return a, None
     a = np.ascontiguousarray(a, np.float32)
     return CloudIn(a.ctypes.data, a.shape[0], a.shape[1] * 4), a
 
@@ -186,6 +190,9 @@ def _cloud_ref(a):
 
 
 class Engine:
+    # scan_registration / chain_sweep accept a loam_cloud_in view as the raw sweep (rosbag.replay)
+    takes_cloud_in = True
+
     def __init__(self, cfg=None, device=0, cap=None):
         self.cfg = cfg or default_config()
         self.h = ctypes.c_void_p()

@@ -363,8 +363,9 @@ int loam_pc2_cloud(const loam_pc2* pc, loam_point* scratch, uint32_t scratch_cap
   if (!pc || !out) return bag_fail(LOAM_E_INVAL, "null argument");
   const uint64_t n = (uint64_t)pc->width * pc->height;
   if (n > 0xffffffffull) return bag_fail(LOAM_E_INVAL, "PointCloud2: too many points");
-  if (pc->off_x == 0 && pc->off_y == 4 && pc->off_z == 8 && ((uintptr_t)pc->data & 3) == 0 &&
-      (pc->point_step & 3) == 0) {  // the C-ABI's record layout already: hand the message over
+  // the C-ABI's record layout already: hand the message over (at any alignment: the data follows
+  // the message's variable-length header; the engine reads the records with unaligned copies)
+  if (pc->off_x == 0 && pc->off_y == 4 && pc->off_z == 8 && pc->point_step >= 12 && (pc->point_step & 3) == 0) {
     out->data = pc->data;
     out->count = (uint32_t)n;
     out->stride_bytes = pc->point_step;

@@ -80,6 +80,11 @@ LOAM_HD bool vg_leaf_too_small(const float* mn, const float* mx, float inv) {
 // workgroup barrier, then ONE lane's relaxed agent-scope add on the done counter; the last
 // workgroup (told by the add's return value) acquires at agent scope once and reads the partials
 // with sc1 loads.  A __threadfence() per workgroup (L2 write-back + invalidate) cost several us each.
+// The hand-off relies on gfx9's vmcnt counting stores as well as loads (gfx10+ counts stores in a
+// separate vscnt, where this drain would not wait for them): CDNA3 / CDNA4 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "store_partial's write-through hand-off is written for gfx942 / gfx950 (vmcnt covers stores)"
+#endif
 LOAM_D void store_partial(double* dst, double v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst), __builtin_bit_cast(unsigned long long, v),
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -108,10 +108,13 @@ int check_cloud_in(const loam_cloud_in& c, int cap) {
   return LOAM_OK;
 }
 
+// (records need not be 4-byte aligned: a PointCloud2's data follows a variable-length header in
+// the message, and loam_pc2_cloud hands it over in place)
 void pack(const loam_cloud_in& c, float4* dst) {
   const char* base = (const char*)c.data;
   for (uint32_t i = 0; i < c.count; ++i) {
-    const float* q = (const float*)(base + (size_t)i * c.stride_bytes);
+    float q[3];
+    std::memcpy(q, base + (size_t)i * c.stride_bytes, sizeof(q));
     dst[i] = make_float4(q[0], q[1], q[2], 0.0f);
   }
 }

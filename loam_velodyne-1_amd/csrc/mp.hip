@@ -5,8 +5,9 @@
 //                  quaternion round trip :304-321), cube-grid recentring (:440-614) as slot-table
 //                  shifts, FOV cube selection (:616-672), FromMap prefix.
 //  k_mp_stack      stack to map frame and back (:424-434, :683-691, Q24)
-//  vg_run          segmented PCL VoxelGrid (hipCUB segmented radix sort by voxel index; equal keys
-//                  keep input order) for the stacks (:693-701) and the valid cubes (:1018-1036)
+//  vg_run          segmented PCL VoxelGrid (a cascade of hand-written LDS / global radix-sort kernels
+//                  by voxel index; equal keys keep input order) for the stacks (:693-701) and the
+//                  valid cubes (:1018-1036)
 //  k_mp_gather     FromMap = valid cubes concatenated (:674-681), then voxel-hashed (k_hash_build)
 //  k_mp_nn         one L-M iteration's 5-NN (:714-719, :821-826) for every instance at once, lane
 //                  per stack point: exact 5-NN through the 1 m hash (any point within the 1 m
@@ -820,6 +821,14 @@ constexpr int kMpNnLanes = LOAM_MP_NN_LANES;
 #define LOAM_NN_THREADS 128  // (round 3: 64 -> 3.00 / 0.648 ms/step at batch 1024 / 128, 128 -> 3.03 / 0.652)
 #endif
 constexpr int kMpNnThreads = LOAM_NN_THREADS;
+// lanes per query of k_mp_nn for batches of at most LOAM_NN_LANES_MAXP problems
+#ifndef LOAM_NN_BATCH_LANES
+#define LOAM_NN_BATCH_LANES 1
+#endif
+#ifndef LOAM_NN_LANES_MAXP
+#define LOAM_NN_LANES_MAXP 256
+#endif
+constexpr int kNnBatchLanes = LOAM_NN_BATCH_LANES;
 // k_mp_fit workgroup size (ms/step at batch 1024: 256 -> 1.27-1.29, 128 -> 1.16-1.20, 64 -> 1.17)
 constexpr int kMpFitThreads = 64;
 
@@ -1272,8 +1281,8 @@ LOAM_D void mp_step(const MpBuffers& b, int p, const double* tot, MpStepScratch&
 // batch kernels.  k_mp_nn: small and register-light so many waves hide the gather latency; five
 // waves per SIMD (<= 96 VGPRs; the LDS lists allow five workgroups per CU).  COUNT: the profiling
 // variant that also sums its work (candidates, bucket ranges) into the frame's istate
-template <bool COUNT>
-__global__ __launch_bounds__(kMpNnThreads) __attribute__((amdgpu_waves_per_eu(LOAM_NN_WPE))) void k_mp_nn(MpBuffers b) {
+template <bool COUNT, int L>
+__global__ __launch_bounds__(kMpNnThreads) __attribute__((amdgpu_waves_per_eu(L > 1 ? 4 : LOAM_NN_WPE))) void k_mp_nn(MpBuffers b) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, tid = threadIdx.x;
   const int* ist = b.istate + (size_t)p * kMpStateInts;
@@ -1286,12 +1295,17 @@ __global__ __launch_bounds__(kMpNnThreads) __attribute__((amdgpu_waves_per_eu(LO
   const loampose::MapRot r = rot_load(b, p);
   const MpNnCtx c = mp_nn_ctx(b, p);
   int work = 0;  // work counter (loam_stats mp_nn_candidates / mp_nn_cells), packed as in knn5
-  for (int q = blk.x * kMpNnThreads + tid; q < nq; q += gridDim.x * kMpNnThreads) {
+  // L lanes per query (aligned groups): the candidates strided over the group, the partial top-5
+  // lists merged (knn5_merge); the group's first lane stores the result
+  constexpr int QPB = kMpNnThreads / L;
+  const int sub = tid % L;
+  for (int q = blk.x * QPB + tid / L; q < nq; q += gridDim.x * QPB) {
     float4 sel;
     Top5 t;
-    mp_nn_query<kMpNnThreads, 1, kNnListCap>(b, c, q, nsc, first, r, lst, sel, t, work);
+    mp_nn_query<kMpNnThreads, L, kNnListCap>(b, c, q, nsc, first, r, lst, sel, t, work, sub);
   }
   if (!COUNT) return;
+  if (sub != 0) work = 0;  // (every lane of a group counted the group's whole list)
   const int ncand = wave_sum(work & ((1 << kWorkCellShift) - 1)), ncell = wave_sum(work >> kWorkCellShift);
   if (lane_id() == 0 && ncand) {
     atomicAdd((int*)&ist[kMiNnCand], ncand);
@@ -1362,19 +1376,25 @@ __global__ __launch_bounds__(kMpFitThreads) void k_mp_fit(MpBuffers b) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     if (!sh_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (lane < 28) {  // fixed order over the workgroups, eight in flight per step
-      const double* pp = b.part + (size_t)p * kMpFitGridMax * 28 + lane;
-      double v = 0.0;
-      for (int g = 0; g < G; g += 8) {
-        double t[8];
+    {  // fixed order over the workgroups: lane (half h, value v) sums half h of the partials in
+       // order, sixteen loads in flight per round, then the two halves are added in order
+      const int v = lane % 28, h = lane / 28, G2 = (G + 1) / 2;
+      const int g0 = h == 0 ? 0 : G2, g1 = h == 0 ? G2 : G;
+      const double* pp = b.part + (size_t)p * kMpFitGridMax * 28 + v;
+      double sum = 0.0;
+      if (h < 2) {
+        for (int g = g0; g < g1; g += 16) {
+          double t[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          t[u] = g + u < G ? __hip_atomic_load(&pp[(size_t)(g + u) * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+          for (int u = 0; u < 16; ++u)
+            t[u] = g + u < g1 ? __hip_atomic_load(&pp[(size_t)(g + u) * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (g + u < G) v += t[u];
+          for (int u = 0; u < 16; ++u)
+            if (g + u < g1) sum += t[u];
+        }
       }
-      tot[lane] = v;
+      const double upper = __shfl_down(sum, 28, 64);
+      if (lane < 28) tot[lane] = sum + upper;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -2076,7 +2096,8 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   // (streaming), the cascade's finish is not enqueued
   // (k_mp_stack zeroed the cascade's list counters)
   js.zeroed = true;
-  const bool fits = stack_max >= 0 && stack_max <= 12288;
+  // (the cascade's first kernel takes 12288 points for a few instances, 2048 for batches)
+  const bool fits = stack_max >= 0 && stack_max <= (P <= 4 ? 12288 : 2048);
   // batches: the corner stacks (<= 120 points per ring) take the 2048-point kernel, the surf
   // stacks the 12288-point one; a few instances: one 12288-point launch
   b.note(vg_run(js, st, P <= 4 ? 12288 : 2048, !fits, /*tier2_idx=*/true));
@@ -2110,8 +2131,14 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
       continue;
     }
     const int gnn = gq * (kMpQueryThreads / kMpNnThreads);
-    if (prof) hipLaunchKernelGGL(k_mp_nn<true>, dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
-    else hipLaunchKernelGGL(k_mp_nn<false>, dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
+    if (P <= LOAM_NN_LANES_MAXP && kNnBatchLanes > 1) {  // shares of a few hundred problems: the slowest wave is the launch
+      if (prof) hipLaunchKernelGGL((k_mp_nn<true, kNnBatchLanes>), dim3(gnn * kNnBatchLanes, P), dim3(kMpNnThreads), 0, st, b);
+      else hipLaunchKernelGGL((k_mp_nn<false, kNnBatchLanes>), dim3(gnn * kNnBatchLanes, P), dim3(kMpNnThreads), 0, st, b);
+    } else if (prof) {
+      hipLaunchKernelGGL((k_mp_nn<true, 1>), dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
+    } else {
+      hipLaunchKernelGGL((k_mp_nn<false, 1>), dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
+    }
     mark("k_mp_nn");
     const int gfit = gq * (kMpQueryThreads / kMpFitThreads);
     if (P <= LOAM_MP_FUSED_MAX && gfit <= kMpFitGridMax) {

@@ -113,7 +113,7 @@ struct MpBuffers {
   int* done = nullptr;        // [P] its workgroups finished (the last one runs the step)
   double* rot = nullptr;      // [P][6] cos / sin of the TobeMapped rotation (rot_store in mp.hip)
   int* nreg = nullptr;
-  hipError_t sticky = hipSuccess;  // first failed library call of the launch sequences (hipCUB)
+  hipError_t sticky = hipSuccess;  // first failed HIP call of the launch sequences
   void note(hipError_t e) {
     if (sticky == hipSuccess) sticky = e;
   }

@@ -28,6 +28,13 @@ using namespace loamdev;
 #ifndef LOAM_OD_SMALL_MAX
 #define LOAM_OD_SMALL_MAX 63
 #endif
+// batches whose association rounds run their iterations in one workgroup per problem (k_od_lm)
+#ifndef LOAM_OD_LM_MIN
+#define LOAM_OD_LM_MIN 1
+#endif
+#ifndef LOAM_OD_LM_MAX
+#define LOAM_OD_LM_MAX 0
+#endif
 // largest batch whose k_od_rows runs the step in its last workgroup (no k_od_step launches)
 #ifndef LOAM_OD_FUSED_MAX
 #define LOAM_OD_FUSED_MAX 0  // (measured at batch 128: rows + step 0.67 -> 0.62 ms/step, whole step unchanged; 1024 slower)
@@ -42,6 +49,9 @@ using namespace loamdev;
 #endif
 #ifndef LOAM_ASSOC_PHASE
 #define LOAM_ASSOC_PHASE 0
+#endif
+#if (LOAM_ASSOC_SKIP != 0 || LOAM_ASSOC_PHASE != 0) && !defined(LOAM_EXPERIMENT_BUILD)
+#error "LOAM_ASSOC_SKIP / LOAM_ASSOC_PHASE are diagnostic (wrong results / partial counters): tools/build_variant.sh only"
 #endif
 
 namespace loam {
@@ -809,21 +819,16 @@ LOAM_D void od_step(const OdBuffers& b, int p, int iter, const double* tot, floa
   if (D(dR) < 0.1 && D(dT) < 0.1) ist[kIsStop] = 1;
 }
 
-// The residual + weight of query q at this iteration (:530-583 corner, :653-694 surf) against its
-// association; a rejected correspondence is a zero coefficient (it then adds exact zeros).
-LOAM_D void od_row_coeff(const OdBuffers& b, const FeatView& f, int p, int q, int nc, size_t lp, int iter,
-                         const float* T, float4 po, float4& cf, int& ok) {
+// The residual + weight of a query at this iteration (:530-583 corner, :653-694 surf) from its
+// raw point and its associated Last points (t1, t2 and, for a surface query, t3; has: the
+// association found them); a rejected correspondence is a zero coefficient (it then adds exact zeros).
+LOAM_D void od_coeff_from(int iter, const float* T, float4 po, bool corner, bool has, float4 t1, float4 t2,
+                          float4 t3, float4& cf, int& ok) {
   const float4 s4 = loampose::transform_to_start(T, po);
-  const int* ind = b.ind + (size_t)p * 3 * b.cap_q;
-  const int i1 = ind[q], i2 = ind[b.cap_q + q], i3 = ind[2 * b.cap_q + q];
-  LOAM_CHECK(q < b.cap_q && iter < b.max_iter, q, iter);
-  LOAM_CHECK(i1 < b.nlast[(p * 2 + (int)(lp / (size_t)b.P)) * 2 + (q < nc ? 0 : 1)], i1, q);
   ok = 0;
   cf = make_float4(0, 0, 0, 0);
-  if (q < nc) {
-    if (i2 >= 0) {
-      const float4* CL = b.lastC + lp * b.capC;
-      const float4 t1 = CL[i1], t2 = CL[i2];
+  if (corner) {
+    if (has) {
       const float x0 = s4.x, y0 = s4.y, z0 = s4.z;
       const float x1 = t1.x, y1 = t1.y, z1 = t1.z, x2 = t2.x, y2 = t2.y, z2 = t2.z;
       const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
@@ -840,9 +845,7 @@ LOAM_D void od_row_coeff(const OdBuffers& b, const FeatView& f, int p, int q, in
       cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
       ok = (D(sw) > 0.1 && ld2 != 0) ? 1 : 0;
     }
-  } else if (i2 >= 0 && i3 >= 0) {
-    const float4* SL = b.lastS + lp * b.capS;
-    const float4 t1 = SL[i1], t2 = SL[i2], t3 = SL[i3];
+  } else if (has) {
     float pa = (t2.y - t1.y) * (t3.z - t1.z) - (t3.y - t1.y) * (t2.z - t1.z);
     float pb = (t2.z - t1.z) * (t3.x - t1.x) - (t3.z - t1.z) * (t2.x - t1.x);
     float pc = (t2.x - t1.x) * (t3.y - t1.y) - (t3.x - t1.x) * (t2.y - t1.y);
@@ -857,6 +860,37 @@ LOAM_D void od_row_coeff(const OdBuffers& b, const FeatView& f, int p, int q, in
     ok = (D(sw) > 0.1 && pd2 != 0) ? 1 : 0;
   }
   if (!ok) cf = make_float4(0, 0, 0, 0);
+}
+
+// query q's associated Last points (od_coeff_from's t1, t2, t3, has)
+LOAM_D bool od_assoc_pts(const OdBuffers& b, int p, int q, int nc, size_t lp, float4& t1, float4& t2, float4& t3) {
+  const int* ind = b.ind + (size_t)p * 3 * b.cap_q;
+  const int i1 = ind[q], i2 = ind[b.cap_q + q], i3 = ind[2 * b.cap_q + q];
+  LOAM_CHECK(q < b.cap_q, q, p);
+  LOAM_CHECK(i1 < b.nlast[(p * 2 + (int)(lp / (size_t)b.P)) * 2 + (q < nc ? 0 : 1)], i1, q);
+  t1 = t2 = t3 = make_float4(0, 0, 0, 0);
+  if (q < nc) {
+    if (i2 < 0) return false;
+    const float4* CL = b.lastC + lp * b.capC;
+    t1 = CL[i1];
+    t2 = CL[i2];
+    return true;
+  }
+  if (i2 < 0 || i3 < 0) return false;
+  const float4* SL = b.lastS + lp * b.capS;
+  t1 = SL[i1];
+  t2 = SL[i2];
+  t3 = SL[i3];
+  return true;
+}
+
+// The residual + weight of query q at this iteration against its association
+LOAM_D void od_row_coeff(const OdBuffers& b, const FeatView& f, int p, int q, int nc, size_t lp, int iter,
+                         const float* T, float4 po, float4& cf, int& ok) {
+  LOAM_CHECK(iter < b.max_iter, q, iter);
+  float4 t1, t2, t3;
+  const bool has = od_assoc_pts(b, p, q, nc, lp, t1, t2, t3);
+  od_coeff_from(iter, T, po, q < nc, has, t1, t2, t3, cf, ok);
 }
 
 // A stored row was accepted iff its coefficient direction is not zero: od_row_coeff zeroes the
@@ -1154,8 +1188,170 @@ __global__ __launch_bounds__(64) void k_od_step(OdBuffers b, int iter, int gq) {
   od_step(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
 }
 
+// One association round's iterations (it0 .. it0 + 4, Q10) of a problem in one workgroup, the 6x6
+// step between them on its first wave: no launch, grid-wide drain or partial hand-off per iteration
+// (at the 8-GPU share the k_od_rows + k_od_step pair cost ~20 us per iteration, mostly latency).
+// Lane q < nq owns query q: its raw point and associated Last points are loaded once per round, and
+// each iteration it stores its new row (:530-583, :653-694).  The Q12 re-evaluation of every stored
+// row at the current transform is spread evenly over the workgroup: lane t sums the rows
+// [t R / NT, (t + 1) R / NT) of R = nq (iter + 1) in (query, iteration) order, recomputing the J
+// factors when its query changes; the fp64 sums are reduced in a fixed order (wave butterflies, then
+// the waves in order).  Needs nq <= NT.
+constexpr int kOdLmThreads = 1024;
+#ifndef LOAM_OD_LM_INFLIGHT
+#define LOAM_OD_LM_INFLIGHT 4
+#endif
+constexpr int kOdLmRowsInFlight = LOAM_OD_LM_INFLIGHT;
+constexpr int kOdJf = 17;  // floats of OdJf
+// dynamic LDS of k_od_lm: per query its raw point and associated Last points (4 float4; t1.w: the
+// association holds) and the J factors at the current transform (17 floats)
+inline size_t od_lm_lds(int cap_q) { return (size_t)cap_q * (4 * sizeof(float4) + kOdJf * sizeof(float)); }
+LOAM_D void od_jf_store(float* d, int s, const OdJf& e) {
+  d[0] = e.e00; d[s] = e.e01; d[2 * s] = e.e02; d[3 * s] = e.e10; d[4 * s] = e.e12; d[5 * s] = e.e20;
+  d[6 * s] = e.e21; d[7 * s] = e.e22; d[8 * s] = e.e30; d[9 * s] = e.e31; d[10 * s] = e.e32; d[11 * s] = e.e40;
+  d[12 * s] = e.e41; d[13 * s] = e.e42; d[14 * s] = e.e50; d[15 * s] = e.e51; d[16 * s] = e.e52;
+}
+LOAM_D OdJf od_jf_load(const float* d, int s) {
+  OdJf e;
+  e.e00 = d[0]; e.e01 = d[s]; e.e02 = d[2 * s]; e.e10 = d[3 * s]; e.e12 = d[4 * s]; e.e20 = d[5 * s];
+  e.e21 = d[6 * s]; e.e22 = d[7 * s]; e.e30 = d[8 * s]; e.e31 = d[9 * s]; e.e32 = d[10 * s]; e.e40 = d[11 * s];
+  e.e41 = d[12 * s]; e.e42 = d[13 * s]; e.e50 = d[14 * s]; e.e51 = d[15 * s]; e.e52 = d[16 * s];
+  return e;
+}
+// the step out of line: its solver's registers are not live beside the row loop's
+__device__ __noinline__ void od_step_call(const OdBuffers& b, int p, int iter, const double* tot, float* AtA, float* AtB,
+                                          float* X, float* lm_ws, int* lm_iws, float* jE, float* jV) {
+  od_step(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
+}
+__global__ __launch_bounds__(kOdLmThreads) void k_od_lm(OdBuffers b, FeatView f, int last_buf, int it0) {
+  const int p = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  int* ist = b.istate + (size_t)p * kOdStateInts;
+  if (!ist[kIsActive] || ist[kIsStop]) return;
+  constexpr int NW = kOdLmThreads / 64;
+  __shared__ double red[NW][28];
+  __shared__ double tot[28];
+  __shared__ float Tsh[6], trig[6];
+  __shared__ int stop_sh;
+  __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs], jE[6], jV[36];
+  __shared__ int lm_iws[12];
+  extern __shared__ float4 od_lm_dyn[];
+  const int CQ = b.cap_q;
+  float4* qpts = od_lm_dyn;                  // [4][CQ]
+  float* jf = (float*)(od_lm_dyn + 4 * CQ);  // [17][CQ]
+  float* st = b.state + (size_t)p * kOdStateFloats;
+  if (tid < 6) {  // the transform, and od_trig's sin / cos of its angles one per lane
+    Tsh[tid] = st[tid];
+    const float a = st[tid >> 1];
+    trig[tid] = (float)((tid & 1) ? dcos(a) : dsin(a));
+  }
+  const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
+  const size_t lp = (size_t)last_buf * b.P + p;
+  float4* qcf = b.q_cf + (size_t)p * b.max_iter * CQ;
+  int8_t* qok = b.q_ok + (size_t)p * b.max_iter * CQ;
+  if (tid < nq) {
+    float4 t1, t2, t3;
+    const bool has = od_assoc_pts(b, p, tid, nc, lp, t1, t2, t3);
+    t1.w = has ? 1.0f : 0.0f;
+    qpts[tid] = tid < nc ? f.sharp[(size_t)p * f.sharp_stride + tid] : f.flat[(size_t)p * f.flat_stride + (tid - nc)];
+    qpts[CQ + tid] = t1;
+    qpts[2 * CQ + tid] = t2;
+    qpts[3 * CQ + tid] = t3;
+  }
+  __syncthreads();
+  const int it_end = min(it0 + 5, b.max_iter);
+  for (int iter = it0; iter < it_end; ++iter) {
+    LOAM_PH(const unsigned long long pt0 = ph_now();)
+    // lane q: the new row and its query's J factors at the current transform
+    if (tid < nq) {
+      float T[6], tg[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        T[k] = Tsh[k];
+        tg[k] = trig[k];
+      }
+      const float4 po = qpts[tid], t1 = qpts[CQ + tid];
+      float4 cf;
+      int ok;
+      od_coeff_from(iter, T, po, tid < nc, t1.w != 0.0f, t1, qpts[2 * CQ + tid], qpts[3 * CQ + tid], cf, ok);
+      qcf[(size_t)iter * CQ + tid] = cf;
+      qok[(size_t)iter * CQ + tid] = (int8_t)ok;
+      const OdJf e = od_jfactors(tg, T, po);
+      od_jf_store(jf + tid, CQ, e);
+    }
+    __syncthreads();
+    LOAM_PH(const unsigned long long pt1 = ph_now();)
+    double acc[28];
+#pragma unroll
+    for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+    const int n_it = iter + 1, R = nq * n_it;
+    int r = (int)((long long)tid * R / kOdLmThreads);
+    const int r1 = (int)((long long)(tid + 1) * R / kOdLmThreads);
+    int qq = r / n_it, it = r - qq * n_it, qe = -1;
+    OdJf e;
+    for (; r < r1; r += kOdLmRowsInFlight) {
+      // the next rows' coefficients, all loads in flight together
+      float4 cv[kOdLmRowsInFlight];
+      int qv[kOdLmRowsInFlight];
+#pragma unroll
+      for (int u = 0; u < kOdLmRowsInFlight; ++u) {
+        qv[u] = qq;
+        cv[u] = r + u < r1 ? qcf[(size_t)it * CQ + qq] : make_float4(0, 0, 0, 0);
+        if (++it == n_it) { it = 0; ++qq; }
+      }
+#pragma unroll
+      for (int u = 0; u < kOdLmRowsInFlight; ++u) {
+        if (r + u < r1) {
+          if (qv[u] != qe) {
+            qe = qv[u];
+            e = od_jf_load(jf + qe, CQ);
+          }
+          od_row_accum(e, cv[u], row_ok(cv[u]), acc);
+        }
+      }
+    }
+    wave_reduce_scatter_28(acc);
+    if ((lane & 1) == 0 && (lane >> 1) < 28) red[w][lane >> 1] = acc[0];
+    __syncthreads();
+    LOAM_PH(const unsigned long long pt2 = ph_now();)
+    if (tid < 28) {
+      double v = red[0][tid];
+#pragma unroll
+      for (int ww = 1; ww < NW; ++ww) v += red[ww][tid];
+      tot[tid] = v;
+    }
+    __syncthreads();
+    LOAM_PH(const unsigned long long pt3 = ph_now();)
+    if (tid < 64) {  // the first wave: the step (od_step writes the state; lane 0 reads its own writes)
+      od_step_call(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
+      if (tid == 0) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) Tsh[k] = st[k];
+        stop_sh = ist[kIsStop];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (tid < 6) {
+        const float a = Tsh[tid >> 1];
+        trig[tid] = (float)((tid & 1) ? dcos(a) : dsin(a));
+      }
+    }
+    __syncthreads();
+    LOAM_PH(if (tid == 0) {
+      const unsigned long long pt4 = ph_now();
+      atomicAdd(&g_ph_od.sum[1][0], pt1 - pt0);
+      atomicAdd(&g_ph_od.sum[1][1], pt2 - pt1);
+      atomicAdd(&g_ph_od.sum[1][2], pt3 - pt2);
+      atomicAdd(&g_ph_od.sum[1][3], pt4 - pt3);
+      atomicAdd(&g_ph_od.sum[1][4], (unsigned long long)(iter + 1));
+      atomicAdd(&g_ph_od.sum[1][6], 1ull);
+    })
+    if (stop_sh) break;
+  }
+}
+
 // pose accumulation (:830-856) for every problem
-__global__ void k_od_fini(OdBuffers b, FeatView f) {
+__global__ __launch_bounds__(64) void k_od_fini(OdBuffers b, FeatView f) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= b.P) return;
   float* st = b.state + (size_t)p * kOdStateFloats;
@@ -1299,6 +1495,9 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
   const int P = b.P;
   auto mark = [&](const char* n) { if (prof) prof->mark(n); };
   hipLaunchKernelGGL(k_od_begin, dim3((P + 255) / 256), dim3(256), 0, st, b, f);
+  // batches up to LOAM_OD_LM_MAX problems: each association round's iterations in one k_od_lm
+  // workgroup per problem (the queries must fit its lanes)
+  const bool lm_round = P >= LOAM_OD_LM_MIN && P <= LOAM_OD_LM_MAX && b.cap_q <= kOdLmThreads;
   for (int it = 0; it < b.max_iter; ++it) {
     if (it % 5 == 0) {  // Q10
       // one wave per query when the batch is small (streaming: TransformToStart in the wave), 64
@@ -1313,6 +1512,12 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
         else hipLaunchKernelGGL((k_od_assoc<false, true>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
       }
       mark("k_od_assoc");
+      if (lm_round) {  // the round's iterations in one workgroup per problem
+        hipLaunchKernelGGL(k_od_lm, dim3(P), dim3(kOdLmThreads), od_lm_lds(b.cap_q), st, b, f, last_buf, it);
+        mark("k_od_lm");
+        it += 4;
+        continue;
+      }
     }
     if (P <= LOAM_OD_SMALL_MAX) {  // measured: the fused step loses for large batches (its serial tail)
       hipLaunchKernelGGL(k_od_rows_small, dim3(b.gq, P, it + 1), dim3(kOdThreads), 0, st, b, f, last_buf, it);
@@ -1329,7 +1534,7 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
       }
     }
   }
-  if (device_fini) hipLaunchKernelGGL(k_od_fini, dim3((P + 255) / 256), dim3(256), 0, st, b, f);
+  if (device_fini) hipLaunchKernelGGL(k_od_fini, dim3((P + 63) / 64), dim3(64), 0, st, b, f);
 }
 }  // namespace loam
 

@@ -9,6 +9,10 @@
 #ifndef LOAM_POSE_MATH_HPP
 #define LOAM_POSE_MATH_HPP
 
+#if defined(LOAM_DIAG_END_NOTRIG) && !defined(LOAM_EXPERIMENT_BUILD)
+#error "LOAM_DIAG_END_NOTRIG is a timing diagnostic (wrong results): tools/build_variant.sh only"
+#endif
+
 #include "dev_common.hpp"
 
 namespace loampose {

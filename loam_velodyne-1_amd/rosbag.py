@@ -62,13 +62,19 @@ class Bag:
         self.close()
 
     def __iter__(self):
+        for topic, type_, stamp, data, size in self.views():
+            yield topic, type_, stamp, ctypes.string_at(data, size)
+
+    def views(self):
+        """(topic, type, stamp, address, size) per message record, in file order, without copying:
+        the address points into the reader's buffer and is valid until the next message is read"""
         m = BagMsg()
         while True:
             rc = _bag_lib().loam_bag_next(self.h, ctypes.byref(m))
             if rc == LOAM_BAG_END:
                 return
             _check(rc)
-            yield m.topic.decode(), m.type.decode(), m.stamp, ctypes.string_at(m.data, m.size)
+            yield m.topic.decode(), m.type.decode(), m.stamp, m.data, m.size
 
 
 def parse_pc2(payload):
@@ -86,10 +92,24 @@ def parse_pc2(payload):
         raw = np.frombuffer(ctypes.string_at(ci.data, n * ci.stride_bytes), np.uint8).reshape(n, ci.stride_bytes)
         pts = np.zeros((n, 4), np.float32)
         pts[:, :3] = raw[:, :12].copy().view(np.float32).reshape(n, 3)
-        if pc.off_intensity >= 0:
+        if 0 <= pc.off_intensity and pc.off_intensity + 4 <= ci.stride_bytes:
             o = pc.off_intensity
             pts[:, 3] = raw[:, o:o + 4].copy().view(np.float32).reshape(n)
     return pc.stamp, pts, pc
+
+
+def pc2_cloud_in(data, size):
+    """sensor_msgs/PointCloud2 at (address, size) -> (header stamp, loam_cloud_in, keep-alive): the
+    message's own records handed over by stride when x, y, z sit at 0 / 4 / 8 (the velodyne layout,
+    src/scanRegistration.cpp:225-229 reads exactly those), else packed into a scratch array that the
+    keep-alive holds"""
+    pc = Pc2()
+    _check(_bag_lib().loam_pc2_parse(data, size, ctypes.byref(pc)))
+    n = pc.width * pc.height
+    scratch = np.zeros((max(n, 1), 4), np.float32)
+    ci = CloudIn()
+    _check(_bag_lib().loam_pc2_cloud(ctypes.byref(pc), scratch.ctypes.data, n, ctypes.byref(ci)))
+    return pc.stamp, ci, (scratch if ci.data == scratch.ctypes.data else None)
 
 
 def parse_imu(payload):
@@ -105,16 +125,23 @@ def parse_imu(payload):
 def replay(path, engine, cloud_topic="/velodyne_points", imu_topic="/imu/data", max_sweeps=None):
     """Feeds a bag through the node path of one engine context: /imu/data -> loam_imu, every cloud
     -> scan registration -> odometry -> mapping on the frames odometry publishes (Q20).  Returns
-    dict(odometry=[(stamp, pose6)], mapping=[(stamp, aft pose6)], sweeps=int)."""
+    dict(odometry=[(stamp, pose6)], mapping=[(stamp, aft pose6)], sweeps=int).
+    A checker engine without `takes_cloud_in` (the CPU oracle) gets the cloud decoded into an
+    (n, 4) array instead; the product engine reads the message's records in place (zero-copy:
+    the scan registration's upload is the only copy of the points)."""
     odo, mapped, n = [], [], 0
-    for topic, _type, _t, payload in Bag(path):
+    zero_copy = getattr(engine, "takes_cloud_in", False)
+    for topic, _type, _t, data, size in Bag(path).views():
         if topic == imu_topic:
-            stamp, q, a = parse_imu(payload)
+            stamp, q, a = parse_imu(ctypes.string_at(data, size))
             engine.imu(stamp, q, a)
         elif topic == cloud_topic:
-            stamp, pts, _pc = parse_pc2(payload)
+            if zero_copy:
+                stamp, cloud, _keep = pc2_cloud_in(data, size)
+            else:
+                stamp, cloud, _pc = parse_pc2(ctypes.string_at(data, size))
             n += 1
-            rc, f = engine.scan_registration(pts, stamp=stamp)
+            rc, f = engine.scan_registration(cloud, stamp=stamp)
             if rc != LOAM_OK:
                 continue  # inside systemDelay (Q1)
             pub, pose, cl, sl, full = engine.odometry(f, stamp=stamp)

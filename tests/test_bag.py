@@ -68,6 +68,65 @@ def test_pointcloud2_other_layout_packed(rb):
     np.testing.assert_array_equal(pts, p)
 
 
+def _pc2_by_spec(pts, sec, nsec, frame="velodyne"):
+    """sensor_msgs/PointCloud2 serialized from the ROS1 message definition itself (not through
+    tests/bagwriter.py): Header {uint32 seq, time stamp (uint32 sec, nsec), string frame_id},
+    uint32 height, width, PointField[] {string name, uint32 offset, uint8 datatype (7 = FLOAT32,
+    4 = UINT16), uint32 count}, bool is_bigendian, uint32 point_step, row_step, uint8[] data,
+    bool is_dense; little-endian, strings and arrays length-prefixed with a uint32.  Velodyne layout:
+    x, y, z, pad, intensity at 16, ring (uint16) at 20, point_step 32."""
+    import struct
+    def string(t):
+        return struct.pack("<I", len(t)) + t.encode()
+    fields = [("x", 0, 7), ("y", 4, 7), ("z", 8, 7), ("intensity", 16, 7), ("ring", 20, 4)]
+    n = pts.shape[0]
+    rec = np.zeros((n, 32), np.uint8)
+    rec[:, 0:12] = np.ascontiguousarray(pts[:, :3], "<f4").view(np.uint8).reshape(n, 12)
+    rec[:, 16:20] = np.ascontiguousarray(pts[:, 3], "<f4").view(np.uint8).reshape(n, 4)
+    rec[:, 20:22] = (np.arange(n) % 16).astype("<u2").view(np.uint8).reshape(n, 2)
+    out = struct.pack("<III", 7, sec, nsec) + string(frame) + struct.pack("<II", 1, n)
+    out += struct.pack("<I", len(fields)) + b"".join(string(nm) + struct.pack("<IBI", o, dt, 1) for nm, o, dt in fields)
+    out += struct.pack("<BII", 0, 32, 32 * n) + struct.pack("<I", 32 * n) + rec.tobytes() + struct.pack("<B", 0)
+    return out
+
+
+def test_pointcloud2_wire_format_by_spec(rb):
+    """the reader against a message packed straight from the ROS1 PointCloud2 definition"""
+    p = _cloud(8, n=321, nan=5)
+    m = _pc2_by_spec(p, 1234, 500000000)
+    stamp, pts, pc = rb.parse_pc2(m)
+    assert stamp == 1234.5
+    assert (pc.width, pc.height, pc.point_step, pc.row_step) == (321, 1, 32, 32 * 321)
+    assert (pc.off_x, pc.off_y, pc.off_z, pc.off_intensity, pc.off_ring) == (0, 4, 8, 16, 20)
+    assert (pc.is_bigendian, pc.is_dense) == (0, 0)
+    np.testing.assert_array_equal(pts, p)
+
+
+def test_pc2_cloud_in_reads_message_in_place(rb, tmp_path):
+    """rosbag.pc2_cloud_in (the replay path): a velodyne-layout cloud is handed over as a strided
+    view of the bag reader's own message buffer (no copy), another layout packed into scratch"""
+    import ctypes
+    p, q = _cloud(9, n=500, nan=3), _cloud(10, n=200)
+    path = tmp_path / "z.bag"
+    bw.write_bag(path, [("/velodyne_points", "sensor_msgs/PointCloud2", 1.0, _pc2_by_spec(p, 1, 0)),
+                        ("/velodyne_points", "sensor_msgs/PointCloud2", 2.0, bw.pointcloud2(q, 2.0, layout="shuffled"))],
+                 chunk_messages=1, compression="lz4")
+    seen = 0
+    for _topic, _ty, _st, data, size in rb.Bag(path).views():
+        stamp, ci, keep = rb.pc2_cloud_in(data, size)
+        ref = p if seen == 0 else q
+        assert ci.count == ref.shape[0]
+        if seen == 0:
+            assert keep is None and ci.stride_bytes == 32 and data <= ci.data < data + size
+        else:
+            assert keep is not None and ci.data == keep.ctypes.data and ci.stride_bytes == 16
+        raw = np.frombuffer(ctypes.string_at(ci.data, ci.count * ci.stride_bytes), np.uint8)
+        xyz = raw.reshape(ci.count, ci.stride_bytes)[:, :12].copy().view(np.float32)
+        np.testing.assert_array_equal(xyz, ref[:, :3])
+        seen += 1
+    assert seen == 2
+
+
 def test_pointcloud2_rejects_non_float32_xyz(rb, loam):
     with pytest.raises(loam.LoamError) as e:
         rb.parse_pc2(bw.pointcloud2(_cloud(5, n=10), 1.0, layout="xyz_f64"))

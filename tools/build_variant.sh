@@ -7,7 +7,7 @@ name=$1; shift
 D="$ROOT/loam_velodyne-1_amd"
 mkdir -p "$D/exp/$name.obj"
 for f in sr.hip od.hip mp.hip engine.cpp bag.cpp msg.cpp; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wno-unused-function "$@" \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wno-unused-function -DLOAM_EXPERIMENT_BUILD "$@" \
     -x hip -c "$D/csrc/$f" -o "$D/exp/$name.obj/$f.o" &
 done
 wait
