@@ -107,6 +107,65 @@ LIMITED_BY = {"k_mp_nn": "latency (dependent gathers)", "k_od_assoc": "latency (
               "k_sr_select": "latency (serial greedy picks)", "k_mp_fit": "latency (gathers + VALU)"}
 
 
+def rooflines(st, st_prof, ktimes, psteps, ms_per_step, traffic_file="traffic.json"):
+    """(roofline of the dominant kernel, every kernel's, the whole step's, ms per step per kernel)
+    from one workload's work counters (st: the timed steps; st_prof: the profiling pass, whose
+    search-kernel counters kernel_bytes needs) and its per-kernel HIP-event times (ktimes: name ->
+    (total ms, launches) over psteps steps)"""
+    # roofline of the dominant kernel: bytes per launch / average launch duration
+    kb = kernel_bytes(st_prof)
+    alg_kb = algorithmic_bytes(st_prof)
+    priced = {k: v for k, v in ktimes.items() if k in alg_kb}
+    dom = max(priced.items(), key=lambda kv: kv[1][0])[0] if priced else None
+    roof = None
+    if dom:
+        tot_ms, launches = ktimes[dom]
+        avg_ms = tot_ms / max(launches, 1)
+        launches_per_step = launches / psteps
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", traffic_file)
+        if os.path.exists(tpath):
+            try:
+                traffic = json.load(open(tpath)).get(dom)
+            except Exception:
+                traffic = None
+        alg_launch = alg_kb[dom] / launches_per_step
+        achieved = alg_launch / (avg_ms * 1e-3) / 1e9
+        roof = {"kernel": dom, "bound": "hbm", "limited_by": LIMITED_BY.get(dom, "hbm"),
+                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic, "avg_launch_ms": avg_ms, "bytes_per_launch": alg_launch,
+                "bytes_model": "algorithmic bytes, SURVEY.md §8(d) per-unit figure x units (bench.algorithmic_bytes)"}
+        if traffic:
+            roof["traffic_gbs"] = traffic / (avg_ms * 1e-3) / 1e9
+            roof["traffic_frac"] = roof["traffic_gbs"] / HBM_PEAK_GBS
+        if dom in SEARCH_KERNELS:
+            # what the search actually reads (candidate cells, window points, chunk boxes), from the
+            # work counters: L2-resident gathers, priced against the chip's L2 gather rate
+            g_launch = kb[dom] / launches_per_step
+            g = g_launch / (avg_ms * 1e-3) / 1e9
+            roof["gathered"] = {"bytes_per_launch": g_launch, "achieved_gbs": g,
+                                "l2_gather_peak": L2_GATHER_PEAK_GBS, "l2_frac": g / L2_GATHER_PEAK_GBS}
+    stage_ms = {k: round(v[0] / psteps, 4) for k, v in sorted(ktimes.items())}
+    roof_all = {}
+    for k, nbytes in alg_kb.items():
+        if k in ktimes and ktimes[k][0] > 0:
+            sec = ktimes[k][0] / psteps * 1e-3
+            gbs = nbytes / sec / 1e9  # algorithmic bytes per step / s per step
+            roof_all[k] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                           "ms_per_step": round(ktimes[k][0] / psteps, 4),
+                           "bytes_per_step": int(nbytes), "limited_by": LIMITED_BY.get(k, "hbm")}
+            if k in SEARCH_KERNELS:
+                ggbs = kb[k] / sec / 1e9
+                roof_all[k]["gathered"] = {"bytes_per_step": int(kb[k]), "achieved_gbs": round(ggbs, 1),
+                                           "l2_frac": round(ggbs / L2_GATHER_PEAK_GBS, 4)}
+    # the whole pipeline against HBM: SURVEY.md §8(d)'s algorithmic bytes per step / step time
+    alg = int(st["bytes_sr"] + st["bytes_od"] + st["bytes_mp"])
+    pipeline = {"algorithmic_bytes_per_step": alg, "achieved_gbs": alg / (ms_per_step * 1e-3) / 1e9,
+                "frac": alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "kernel_busy_ms_per_step": round(sum(v[0] for v in ktimes.values()) / psteps, 4) if ktimes else None}
+    return roof, roof_all, pipeline, stage_ms
+
+
 def stream_leg(loam, sg, n_sweeps, n_cpu, stages=3, priority="default"):
     """Config 3 (streaming, seed 1): scan registration -> odometry -> mapping on every published
     frame, one sweep at a time on one GPU context, next to the CPU oracle on the first sweeps."""
@@ -222,10 +281,11 @@ class pinned_core:
         os.sched_setaffinity(0, self.old)
 
 
-def cpu_leg(oc, prevs, curs, od, aft, n_sample, reps):
+def cpu_leg(oc, prevs, curs, od, aft, n_sample, reps, ocfg=None):
     """The oracle (single-thread C++ restatement), pinned to one core, over a bounded sample of the
     batch's problems spread across it: 1 warm-up run, then the median of `reps` runs (BASELINE.md
-    §2).  Also checks the engine's poses of the sampled problems against the oracle."""
+    §2).  Also checks the engine's poses of the sampled problems against the oracle.  ocfg: the
+    oracle's configuration (default: the VLP-16 one)"""
     B = len(prevs)
     idx = sorted(set(int(round(v)) for v in np.linspace(0, B - 1, min(n_sample, B))))
     times = []
@@ -233,7 +293,8 @@ def cpu_leg(oc, prevs, curs, od, aft, n_sample, reps):
     with pinned_core() as core:
         for r in range(reps + 1):
             a = time.perf_counter()
-            outs = [oc.problem(prevs[i], curs[i]) for i in idx]
+            outs = [oc.problem(prevs[i], curs[i]) if ocfg is None else oc.problem(prevs[i], curs[i], ocfg)
+                    for i in idx]
             t = time.perf_counter() - a
             if r == 0:
                 for i, (od_o, aft_o, _) in zip(idx, outs):
@@ -257,6 +318,53 @@ def cpu_leg(oc, prevs, curs, od, aft, n_sample, reps):
                      f"{med:.2f} s per run (runs: {', '.join(f'{t:.2f}' for t in times)})"}
     parity = {"problems_checked": len(idx), "max_abs_err_odometry": err_od, "max_abs_err_mapping": err_mp}
     return cpu, parity
+
+
+# config 5 (BASELINE.json: dense HDL-64E sweeps, the HBM roofline stress) with the reference's
+# 64-ring settings: linear ring model, 100 odometry / 20 mapping iterations
+# (bk include/loam_velodyne/common.h:26-32, src/scanRegistration.cpp:268-275)
+DENSE_CFG = dict(n_rings=64, max_points=160000, od_max_iter=100, mp_max_iter=20)
+DENSE_SEED = 5000
+
+
+def dense_batch_leg(loam, sg, B, steps, warmup, profile_steps, cpu_sample, cpu_reps, device=0):
+    """Config 5 as a batch: B independent HDL-64E problems (seeds DENSE_SEED + i, ~131k points per
+    sweep, 64 rings) through the same step as config 4 — enough sweeps in flight to load the chip,
+    which one 131k-point problem does not.  Inputs resident in HBM; its own roofline (dominant kernel
+    and whole step), CPU oracle sample and parity."""
+    prevs, curs = sg.batch_problems(B, base_seed=DENSE_SEED, lidar=sg.HDL64)
+    eng = loam.Engine(loam.default_config(ring_model=loam.RING_LINEAR, **DENSE_CFG), device=device)
+    eng.batch_upload(prevs, curs)
+    elapsed = timed(eng, steps, warmup, None, "cpu")
+    od, aft, st = eng.batch_download()
+    ms = elapsed / steps * 1e3
+    ktimes, st_prof = {}, st
+    if profile_steps > 0:
+        eng.set_profiling(True)
+        for _ in range(profile_steps):
+            eng.batch_run()
+        _, _, st_prof = eng.batch_download()
+        ktimes = eng.kernel_times()
+        eng.set_profiling(False)
+    eng.close()
+    roof, roof_all, pipeline, stage_ms = rooflines(st, st_prof, ktimes, max(profile_steps, 1), ms,
+                                                   traffic_file="traffic_config5.json")
+    out = {"config": f"config5 batch: {B} HDL-64E problems (seeds {DENSE_SEED}..{DENSE_SEED + B - 1}, 64 rings, "
+                     "linear ring model, 100 / 20 iterations), inputs resident",
+           "problems": B, "points_per_sweep_mean": float(np.mean([len(c) for c in curs])),
+           "value": B * steps / elapsed, "unit": "scans/s", "ms_per_step": ms, "steps": steps, "warmup": warmup,
+           "roofline": roof, "roofline_kernels": roof_all, "pipeline": pipeline, "kernel_ms_per_step": stage_ms,
+           "workload_stats": {"od_iters_mean": st["od_iters"] / B, "mp_iters_mean": st["mp_iters"] / B,
+                              "mp_stack_mean": st["mp_stack"] / B, "od_queries_mean": st["od_queries"] / B}}
+    if cpu_sample > 0 and not os.environ.get("LOAM_BENCH_ENGINE"):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_ctypes as oc
+        cpu, parity = cpu_leg(oc, prevs, curs, od, aft, cpu_sample, cpu_reps,
+                              ocfg=oc.default_config(ring_model=1, **DENSE_CFG))
+        out["cpu_baseline"] = cpu
+        out["parity"] = parity
+        out["speedup_vs_cpu"] = out["value"] / cpu["value"]
+    return out
 
 
 def engine_factory():
@@ -329,6 +437,9 @@ def main(argv=None):
     ap.add_argument("--stream-sweeps", type=int, default=220, help="config-3 streaming leg (0: skip)")
     ap.add_argument("--stream-cpu-sweeps", type=int, default=60)
     ap.add_argument("--latency-runs", type=int, default=50, help="config-2 warm latency leg (0: skip)")
+    ap.add_argument("--dense-batch", type=int, default=64, help="config-5 batched HDL-64E leg: problems (0: skip)")
+    ap.add_argument("--dense-steps", type=int, default=5)
+    ap.add_argument("--dense-cpu-sample", type=int, default=2)
     ap.add_argument("--share-only", type=int, default=0, help=argparse.SUPPRESS)
     argv = sys.argv[1:] if argv is None else argv
     args = ap.parse_args(argv)
@@ -439,39 +550,7 @@ def main(argv=None):
     value = world * B * args.steps / elapsed
     psteps = max(args.profile_steps, 1)
 
-    # roofline of the dominant kernel: bytes per launch / average launch duration
-    kb = kernel_bytes(st_prof)
-    alg_kb = algorithmic_bytes(st_prof)
-    priced = {k: v for k, v in ktimes.items() if k in alg_kb}
-    dom = max(priced.items(), key=lambda kv: kv[1][0])[0] if priced else None
-    roof = None
-    if dom:
-        tot_ms, launches = ktimes[dom]
-        avg_ms = tot_ms / max(launches, 1)
-        launches_per_step = launches / psteps
-        traffic = None
-        tpath = os.path.join(ROOT, "profiles", "traffic.json")
-        if os.path.exists(tpath):
-            try:
-                traffic = json.load(open(tpath)).get(dom)
-            except Exception:
-                traffic = None
-        alg_launch = alg_kb[dom] / launches_per_step
-        achieved = alg_launch / (avg_ms * 1e-3) / 1e9
-        roof = {"kernel": dom, "bound": "hbm", "limited_by": LIMITED_BY.get(dom, "hbm"),
-                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic, "avg_launch_ms": avg_ms, "bytes_per_launch": alg_launch,
-                "bytes_model": "algorithmic bytes, SURVEY.md §8(d) per-unit figure x units (bench.algorithmic_bytes)"}
-        if traffic:
-            roof["traffic_gbs"] = traffic / (avg_ms * 1e-3) / 1e9
-            roof["traffic_frac"] = roof["traffic_gbs"] / HBM_PEAK_GBS
-        if dom in SEARCH_KERNELS:
-            # what the search actually reads (candidate cells, window points, chunk boxes), from the
-            # work counters: L2-resident gathers, priced against the chip's L2 gather rate
-            g_launch = kb[dom] / launches_per_step
-            g = g_launch / (avg_ms * 1e-3) / 1e9
-            roof["gathered"] = {"bytes_per_launch": g_launch, "achieved_gbs": g,
-                                "l2_gather_peak": L2_GATHER_PEAK_GBS, "l2_frac": g / L2_GATHER_PEAK_GBS}
+    roof, roof_all, pipeline, stage_ms = rooflines(st, st_prof, ktimes, psteps, ms_per_step)
 
     # CPU baseline: the oracle on a bounded sample, N=1 only
     cpu = parity = None
@@ -479,25 +558,6 @@ def main(argv=None):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_ctypes as oc
         cpu, parity = cpu_leg(oc, main_leg["prevs"], main_leg["curs"], od, aft, args.cpu_sample, args.cpu_reps)
-
-    stage_ms = {k: round(v[0] / psteps, 4) for k, v in sorted(ktimes.items())}
-    roof_all = {}
-    for k, nbytes in alg_kb.items():
-        if k in ktimes and ktimes[k][0] > 0:
-            sec = ktimes[k][0] / psteps * 1e-3
-            gbs = nbytes / sec / 1e9  # algorithmic bytes per step / s per step
-            roof_all[k] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-                           "ms_per_step": round(ktimes[k][0] / psteps, 4),
-                           "bytes_per_step": int(nbytes), "limited_by": LIMITED_BY.get(k, "hbm")}
-            if k in SEARCH_KERNELS:
-                ggbs = kb[k] / sec / 1e9
-                roof_all[k]["gathered"] = {"bytes_per_step": int(kb[k]), "achieved_gbs": round(ggbs, 1),
-                                           "l2_frac": round(ggbs / L2_GATHER_PEAK_GBS, 4)}
-    # the whole pipeline against HBM: SURVEY.md §8(d)'s algorithmic bytes per step / step time
-    alg = int(st["bytes_sr"] + st["bytes_od"] + st["bytes_mp"])
-    pipeline = {"algorithmic_bytes_per_step": alg, "achieved_gbs": alg / (ms_per_step * 1e-3) / 1e9,
-                "frac": alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "kernel_busy_ms_per_step": round(sum(v[0] for v in ktimes.values()) / psteps, 4) if ktimes else None}
 
     stream = latency = None
     if world == 1 and not os.environ.get("LOAM_BENCH_ENGINE"):
@@ -533,6 +593,11 @@ def main(argv=None):
                                              "inputs resident")
             dense["points_per_sweep"] = int(len(prob[1]))
             latency["config5"] = with_cpu(dense, *prob, ocfg=lambda oc: oc.default_config(ring_model=1, **dense_cfg))
+    dense = None
+    if world == 1 and args.dense_batch > 0 and not os.environ.get("LOAM_BENCH_ENGINE"):
+        loam = importlib.import_module("loam_velodyne-1_amd")
+        dense = dense_batch_leg(loam, sg, args.dense_batch, args.dense_steps, 2, min(args.profile_steps, 2),
+                                args.dense_cpu_sample if args.cpu_sample > 0 else 0, 3, device=local)
     out = {
         "metric": METRIC,
         "value": value,
@@ -558,6 +623,7 @@ def main(argv=None):
         "kernel_ms_per_step": stage_ms,
         "single_stream": stream,
         "latency": latency,
+        "dense_batch": dense,
         "gathered": {"problems": int(gathered.shape[0]),
                      "sha1": hashlib.sha1(np.ascontiguousarray(gathered, np.float32).tobytes()).hexdigest()}
         if gathered is not None else None,

@@ -9,7 +9,8 @@ reference's message conventions on the device.
              chain on one context and the three-context node pipeline (pipeline.py)
              and through loam_chain_sweep, the device-resident node chain
   config 5   bench.py latency.config5: the HDL-64E problem at the reference's 64-ring iteration
-             caps 100 / 20 (bk include/loam_velodyne/common.h:31-32)
+             caps 100 / 20 (bk include/loam_velodyne/common.h:31-32); bench.py dense_batch: 64
+             such problems as one batch
   node chain odometry -> loam_msg_from_pose(LASER_ODOM) -> loam_pose_from_msg -> loam_mapping ->
              loam_msg_from_pose(AFT_MAPPED, Bef in the twist) -> loam_pose_from_msg ->
              loam_maintenance -> loam_msg_from_pose(INTEGRATED), against the oracle's chain
@@ -95,6 +96,30 @@ def test_config5_iters_100_20(loam, sg):
     np.testing.assert_array_equal(od[0], np.float32(g["od_sum"]))
     np.testing.assert_array_equal(aft[0], np.float32(g["aft"]))
     assert (st["od_iters"], st["mp_iters"]) == (g["od_iters"], g["mp_iters"]) and g["od_iters"] > 25
+
+
+def test_config5_batch_parity(loam, oc, sg):
+    """config 5 as bench.py's dense_batch leg runs it: a batch of HDL-64E problems (seeds 5000 + i,
+    64 rings, 160k capacity, 100 / 20 iterations) through the batch kernels, which a single problem
+    does not reach (P >= 64 launch shapes: k_od_sel + k_od_assoc, batch VoxelGrid cascade); problems
+    spread over the batch against the oracle, and a repeated run identical"""
+    P = 64
+    kw = dict(n_rings=64, max_points=160000, od_max_iter=100, mp_max_iter=20)
+    prevs, curs = sg.batch_problems(P, base_seed=5000, lidar=sg.HDL64)
+    e = loam.Engine(loam.default_config(ring_model=loam.RING_LINEAR, **kw))
+    e.batch_upload(prevs, curs)
+    e.batch_run()
+    od, aft, st = e.batch_download()
+    assert np.all(np.isfinite(od)) and np.all(np.isfinite(aft)) and st["od_iters"] > 25 * P
+    ocfg = oc.default_config(ring_model=1, **kw)
+    for i in (0, 21, P - 1):
+        od_o, aft_o, _ = oc.problem(prevs[i], curs[i], ocfg)
+        np.testing.assert_array_equal(od[i], od_o)
+        np.testing.assert_array_equal(aft[i], aft_o)
+    e.batch_run()
+    od2, aft2, _ = e.batch_download()
+    np.testing.assert_array_equal(od, od2)
+    np.testing.assert_array_equal(aft, aft2)
 
 
 def _msg_chain_engine(loam, sweeps):
