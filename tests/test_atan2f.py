@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_device_atan2f_is_glibc(tmp_path):
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     exe = str(tmp_path / "atan2f_check")
-    subprocess.run([hipcc, "-O2", "-ffp-contract=off", "-o", exe, os.path.join(ROOT, "tests", "atan2f_check.cpp")],
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-O2", "-ffp-contract=off", "-o", exe, os.path.join(ROOT, "tests", "atan2f_check.cpp")],
                    check=True, capture_output=True)
     n, bad = map(int, subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split())
     assert n == 4000000 and bad == 0

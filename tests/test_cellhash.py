@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_cell_hash_separates_neighbourhoods(tmp_path):
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     exe = str(tmp_path / "cellhash_check")
-    subprocess.run([hipcc, "-O2", "-o", exe, os.path.join(ROOT, "tests", "cellhash_check.cpp")], check=True,
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-O2", "-o", exe, os.path.join(ROOT, "tests", "cellhash_check.cpp")], check=True,
                    capture_output=True)
     checked, collisions = map(int, subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split())
     assert checked == 3000000 and collisions == 0

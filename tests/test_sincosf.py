@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_device_sincosf_is_glibc(tmp_path):
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     exe = str(tmp_path / "sincosf_check")
-    subprocess.run([hipcc, "-O2", "-ffp-contract=off", "-fno-builtin", "-o", exe,
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-O2", "-ffp-contract=off", "-fno-builtin", "-o", exe,
                     os.path.join(ROOT, "tests", "sincosf_check.cpp")], check=True, capture_output=True)
     # every 61st float of |x| < 120, both signs (the full sweep, step 3, is 0 mismatches too)
     n, bs, bc = map(int, subprocess.run([exe, "61"], check=True, capture_output=True, text=True).stdout.split())
