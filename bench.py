@@ -367,15 +367,32 @@ def dense_batch_leg(loam, sg, B, steps, warmup, profile_steps, cpu_sample, cpu_r
     return out
 
 
-def engine_factory():
+def engine_factory(tune=None):
     """the engine under measurement: libloam_hip.so through its ctypes binding.  LOAM_BENCH_ENGINE
     ("module:attr") substitutes a stand-in for the harness tests on CPU-only machines (gloo);
-    it is never set for a measurement."""
+    it is never set for a measurement.  tune: {key: value} launch choices (loam_set_tuning), for A/B
+    runs of the same library."""
     spec = os.environ.get("LOAM_BENCH_ENGINE")
     if spec:
         mod, attr = spec.split(":")
         return getattr(importlib.import_module(mod), attr)
-    return importlib.import_module("loam_velodyne-1_amd").Engine
+    E = importlib.import_module("loam_velodyne-1_amd").Engine
+    if not tune:
+        return E
+
+    def make(*a, **k):
+        e = E(*a, **k)
+        e.set_tuning(**tune)
+        return e
+    return make
+
+
+def parse_tune(items):
+    out = {}
+    for it in items or []:
+        k, v = it.split("=")
+        out[k.strip()] = int(v)
+    return out
 
 
 def timed(eng, steps, warmup, dist, sync_dev):
@@ -440,14 +457,16 @@ def main(argv=None):
     ap.add_argument("--dense-batch", type=int, default=64, help="config-5 batched HDL-64E leg: problems (0: skip)")
     ap.add_argument("--dense-steps", type=int, default=5)
     ap.add_argument("--dense-cpu-sample", type=int, default=2)
+    ap.add_argument("--tune", action="append", default=[], help="key=value launch choice (loam_set_tuning), repeatable")
     ap.add_argument("--share-only", type=int, default=0, help=argparse.SUPPRESS)
     argv = sys.argv[1:] if argv is None else argv
     args = ap.parse_args(argv)
+    tune = parse_tune(args.tune)
 
     if args.share_only:  # child: the 8-GPU share timed alone in a fresh process, as one rank runs it
         first, B8 = shard(0, 8, args.batch, "strong", args.global_batch)
         prevs, curs = importlib.import_module("loam_velodyne-1_amd.synthgen").batch_problems(B8, base_seed=BASE_SEED + first)
-        e8 = engine_factory()(device=0)
+        e8 = engine_factory(tune)(device=0)
         e8.batch_upload(prevs, curs)
         el = timed(e8, args.steps, args.warmup, None, "cpu")
         e8.close()
@@ -481,12 +500,13 @@ def main(argv=None):
         # in this process after the batch-1024 leg it measured ~10 % slower)
         out = subprocess.run([sys.executable, os.path.abspath(__file__), "--share-only", "1", "--steps", str(args.steps),
                               "--warmup", str(args.warmup), "--batch", str(args.batch),
-                              "--global-batch", str(args.global_batch)], capture_output=True, text=True)
+                              "--global-batch", str(args.global_batch)] + [f"--tune={t}" for t in args.tune],
+                             capture_output=True, text=True)
         if out.returncode != 0:
             raise SystemExit(f"8-GPU share child failed ({out.returncode}): {out.stderr[-2000:]}")
         share8 = json.loads(out.stdout.strip().splitlines()[-1])
 
-    Engine = engine_factory()
+    Engine = engine_factory(tune)
     sg = importlib.import_module("loam_velodyne-1_amd.synthgen")
 
     def leg(split):
@@ -613,7 +633,7 @@ def main(argv=None):
         "data": "synthetic (seeded VLP-16 ray-cast sweeps, random planes+edges scenes; bags unavailable offline)",
         "config": {"workload": "config4: independent VLP-16 problems (SR prev+cur, odometry L-M, mapping L-M)",
                    "problems_per_gpu": B, "global_batch": world * B, "points_per_sweep": 28800,
-                   "split": args.split, "parallelism": f"shard{world}"},
+                   "split": args.split, "parallelism": f"shard{world}", **({"tuning": tune} if tune else {})},
         "roofline": roof,
         "roofline_kernels": roof_all,
         "pipeline": pipeline,

@@ -194,6 +194,13 @@ int loam_batch_download(loam_ctx *ctx, loam_pose6 *od_sum, loam_pose6 *aft, loam
  * contexts share one GPU.  Waits for the context's queued work, then replaces its streams. */
 int loam_set_stream_priority(loam_ctx *ctx, int priority);
 
+/* launch-shape choices of the batch / streaming L-M loops by batch size (no reference equivalent):
+ * key = one of od_small_max, od_lm_min, od_lm_max, od_fused_max, mp_small_max, mp_fused_max,
+ * nn_lanes, nn_lanes_maxp, od_assoc_wg (loam_velodyne-1_amd/csrc/engine.hpp, struct Tuning).  Every
+ * choice computes the same results; the defaults are the measured fastest.  LOAM_E_INVAL for an
+ * unknown key or a value out of range.  Takes effect from the next call. */
+int loam_set_tuning(loam_ctx *ctx, const char *key, long long value);
+
 /* last-call statistics of a context (stage device times, counts, algorithmic bytes) */
 int loam_get_stats(loam_ctx *ctx, loam_stats *stats);
 

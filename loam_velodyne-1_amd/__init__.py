@@ -110,7 +110,7 @@ EXPORTS = ("loam_config_default", "loam_create", "loam_destroy", "loam_last_erro
            "loam_scan_registration", "loam_odometry", "loam_mapping", "loam_mapping_surround",
            "loam_maintenance", "loam_chain_sweep",
            "loam_batch_upload", "loam_batch_run", "loam_batch_sync", "loam_batch_download", "loam_get_stats",
-           "loam_set_profiling", "loam_get_kernel_times", "loam_set_stream_priority",
+           "loam_set_profiling", "loam_get_kernel_times", "loam_set_stream_priority", "loam_set_tuning",
            # include/loam/loam_bag.h: recorded-sweep ingest (rosbag v2, PointCloud2, Imu)
            "loam_bag_open", "loam_bag_close", "loam_bag_next", "loam_pc2_parse", "loam_pc2_cloud",
            "loam_imu_parse",
@@ -143,6 +143,7 @@ def lib():
         L.loam_batch_sync.argtypes = [PP]
         L.loam_set_profiling.argtypes = [PP, ctypes.c_int]
         L.loam_set_stream_priority.argtypes = [PP, ctypes.c_int]
+        L.loam_set_tuning.argtypes = [PP, ctypes.c_char_p, ctypes.c_longlong]
         L.loam_get_kernel_times.argtypes = [PP, ctypes.c_char_p, ctypes.c_uint32]
         L.loam_batch_download.argtypes = [PP, P(Pose6), P(Pose6), P(Stats)]
         L.loam_get_stats.argtypes = [PP, P(Stats)]
@@ -313,6 +314,12 @@ class Engine:
     def set_stream_priority(self, priority):
         """> 0 highest, 0 normal, < 0 lowest device stream priority for this context's streams"""
         _check(lib().loam_set_stream_priority(self.h, int(priority)))
+
+    def set_tuning(self, **kv):
+        """launch-shape choices by batch size (include/loam/loam.h loam_set_tuning), e.g.
+        set_tuning(od_lm_max=128); every choice computes the same results"""
+        for k, v in kv.items():
+            _check(lib().loam_set_tuning(self.h, k.encode(), int(v)))
 
     def set_profiling(self, on):
         _check(lib().loam_set_profiling(self.h, 1 if on else 0))

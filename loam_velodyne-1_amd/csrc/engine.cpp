@@ -97,6 +97,7 @@ struct loam_ctx {
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipStream_t st2 = nullptr;                 // batch: mapping frame 1 beside the odometry solve
   hipEvent_t fork = nullptr, join = nullptr;
+  Tuning tune;                               // launch choices by batch size (loam_set_tuning)
 };
 
 namespace {
@@ -232,6 +233,7 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   if (he == hipSuccess) he = sr_alloc(x->odin, 1, x->cap, x->R);
   if (he == hipSuccess) he = od_alloc(x->od1, 1, x->R, x->cap, (int)c.od_max_iter);
   if (he == hipSuccess) he = mp_alloc(x->mp1, 1, x->R, x->cap, (int)c.map_capacity, (int)c.mp_max_iter);
+  x->od1.tune = x->mp1.tune = x->tune;
   if (he == hipSuccess) he = hipMalloc(&x->sr_imu_dev, sizeof(loamimu::SrQueue));
   if (he != hipSuccess) x->sr_imu_dev = nullptr;
   if (he == hipSuccess) he = hipHostMalloc((void**)&x->meta, 8192, hipHostMallocDefault);
@@ -296,6 +298,16 @@ int loam_set_stream_priority(loam_ctx* x, int priority) {
   x->st2 = st2;
   x->pin.streams[0] = st;
   x->pin.streams[1] = st2;
+  return LOAM_OK;
+}
+
+int loam_set_tuning(loam_ctx* x, const char* key, long long value) {
+  if (!x || !key) return fail(LOAM_E_INVAL, "null argument");
+  Tuning t = x->tune;
+  if (!t.set(key, value)) return fail(LOAM_E_INVAL, std::string("unknown tuning key or value out of range: ") + key);
+  x->tune = t;
+  x->od1.tune = x->odb.tune = t;
+  x->mp1.tune = x->mpb.tune = t;
   return LOAM_OK;
 }
 
@@ -741,6 +753,8 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
     }
     x->P = (int)n;
   }
+  x->odb.tune = x->tune;
+  x->mpb.tune = x->tune;
   std::vector<float4> h((size_t)x->cap);
   std::vector<int> counts(2 * n);
   for (uint32_t i = 0; i < n; ++i)

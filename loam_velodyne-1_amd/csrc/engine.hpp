@@ -31,6 +31,38 @@ constexpr int kRingCap = 4096;      // max ring span (points) handled in LDS by 
 constexpr int kBigSlots = 8;        // workgroups (scratch slots) of the global-memory selection
 constexpr int kSharpPerRing = 12, kLessSharpPerRing = 120, kFlatPerRing = 24;
 
+// Launch-shape choices of the L-M loops by batch size (P = problems of the launch).  Defaults are
+// the measured best; loam_set_tuning changes them per context, so that every
+// path stays reachable by the parity tests and A/B measurements need no rebuild.
+struct Tuning {
+  int od_small_max = 63;   // k_od_rows_small (a workgroup per (queries, stored iteration)) for P <= this
+  int od_lm_min = 1;       // k_od_lm (an association round's 5 iterations in one workgroup per problem)
+  int od_lm_max = 0;       //   for od_lm_min <= P <= od_lm_max
+  int od_fused_max = 0;    // k_od_rows<true> (step in the last workgroup) for P <= this, else + k_od_step
+  int mp_small_max = 4;    // k_mp_lm_small (5-NN + fit + rows + step in one launch) for P <= this
+  int mp_fused_max = 128;  // k_mp_fit<true> (rows + step in its last workgroup) for P <= this, else + k_mp_iter
+  int nn_lanes = 1;        // lanes per query of the batch 5-NN (1, 2, 4) ...
+  int nn_lanes_maxp = 256; //   for P <= this
+  int od_assoc_wg = 64;    // k_od_assoc query waves (workgroups) per problem (batches, P >= 64)
+  // key = value (loam_set_tuning); false for an unknown key or a value out of range
+  bool set(const char* key, long long v) {
+    struct K { const char* n; int* f; long long lo, hi; };
+    const K ks[] = {{"od_small_max", &od_small_max, 0, 1 << 20}, {"od_lm_min", &od_lm_min, 1, 1 << 20},
+                    {"od_lm_max", &od_lm_max, 0, 1 << 20}, {"od_fused_max", &od_fused_max, 0, 1 << 20},
+                    {"mp_small_max", &mp_small_max, 0, 1 << 20}, {"mp_fused_max", &mp_fused_max, 0, 1 << 20},
+                    {"nn_lanes", &nn_lanes, 1, 4}, {"nn_lanes_maxp", &nn_lanes_maxp, 0, 1 << 20},
+                    {"od_assoc_wg", &od_assoc_wg, 1, 1024}};
+    for (const K& k : ks)
+      if (std::strcmp(key, k.n) == 0) {
+        if (v < k.lo || v > k.hi) return false;
+        if (k.f == &nn_lanes && v == 3) return false;
+        *k.f = (int)v;
+        return true;
+      }
+    return false;
+  }
+};
+
 // Scan-registration buffers for S sweeps of capacity `cap` points each (index s*cap + i).
 struct SrBuffers {
   int S = 0, cap = 0, R = 0;

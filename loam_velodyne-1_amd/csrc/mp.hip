@@ -801,14 +801,9 @@ LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t, i
   }
 }
 
-// largest batch whose mapping L-M takes the one-launch-per-iteration kernel (k_mp_lm_small)
-#ifndef LOAM_MP_SMALL_MAX
-#define LOAM_MP_SMALL_MAX 4
-#endif
-// largest batch whose k_mp_fit adds the rows and runs the step in its last workgroup (no k_mp_iter)
-#ifndef LOAM_MP_FUSED_MAX
-#define LOAM_MP_FUSED_MAX 128  // (measured at batch 128: fit + iter 0.66 -> 0.58 ms/step; at 1024 1.71 -> 2.22)
-#endif
+// batch-size launch choices (k_mp_lm_small, k_mp_fit<true>, lanes per query of k_mp_nn): the
+// context's Tuning (engine.hpp), MpBuffers::tune.  (k_mp_fit<true> measured at batch 128: fit + iter
+// 0.66 -> 0.58 ms/step; at 1024 1.71 -> 2.22.)
 constexpr int kMpQueryThreads = 256;
 // lanes per query in k_mp_lm_small (streaming: the per-query search chain is the latency)
 #ifndef LOAM_MP_NN_LANES
@@ -821,14 +816,6 @@ constexpr int kMpNnLanes = LOAM_MP_NN_LANES;
 #define LOAM_NN_THREADS 128  // (round 3: 64 -> 3.00 / 0.648 ms/step at batch 1024 / 128, 128 -> 3.03 / 0.652)
 #endif
 constexpr int kMpNnThreads = LOAM_NN_THREADS;
-// lanes per query of k_mp_nn for batches of at most LOAM_NN_LANES_MAXP problems
-#ifndef LOAM_NN_BATCH_LANES
-#define LOAM_NN_BATCH_LANES 1
-#endif
-#ifndef LOAM_NN_LANES_MAXP
-#define LOAM_NN_LANES_MAXP 256
-#endif
-constexpr int kNnBatchLanes = LOAM_NN_BATCH_LANES;
 // k_mp_fit workgroup size (ms/step at batch 1024: 256 -> 1.27-1.29, 128 -> 1.16-1.20, 64 -> 1.17)
 constexpr int kMpFitThreads = 64;
 
@@ -2125,15 +2112,20 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   const int gq = std::min(P >= 64 ? 24 : 64, (b.cap_stack + kMpQueryThreads - 1) / kMpQueryThreads);
   // an empty map store (the first frame after a reset) cannot run the L-M (:706): no launches
   for (int it = 0; it < (map_empty ? 0 : b.max_iter); ++it) {
-    if (P <= LOAM_MP_SMALL_MAX) {  // small batches: one launch per iteration
+    if (P <= b.tune.mp_small_max) {  // small batches: one launch per iteration
       hipLaunchKernelGGL(k_mp_lm_small, dim3(kMpSmallGrid, P), dim3(kMpQueryThreads), 0, st, b);
       mark("k_mp_lm_small");
       continue;
     }
     const int gnn = gq * (kMpQueryThreads / kMpNnThreads);
-    if (P <= LOAM_NN_LANES_MAXP && kNnBatchLanes > 1) {  // shares of a few hundred problems: the slowest wave is the launch
-      if (prof) hipLaunchKernelGGL((k_mp_nn<true, kNnBatchLanes>), dim3(gnn * kNnBatchLanes, P), dim3(kMpNnThreads), 0, st, b);
-      else hipLaunchKernelGGL((k_mp_nn<false, kNnBatchLanes>), dim3(gnn * kNnBatchLanes, P), dim3(kMpNnThreads), 0, st, b);
+    // L lanes per query for shares of a few hundred problems (the slowest wave is the launch)
+    const int L = P <= b.tune.nn_lanes_maxp ? b.tune.nn_lanes : 1;
+    if (L == 4) {
+      if (prof) hipLaunchKernelGGL((k_mp_nn<true, 4>), dim3(gnn * 4, P), dim3(kMpNnThreads), 0, st, b);
+      else hipLaunchKernelGGL((k_mp_nn<false, 4>), dim3(gnn * 4, P), dim3(kMpNnThreads), 0, st, b);
+    } else if (L == 2) {
+      if (prof) hipLaunchKernelGGL((k_mp_nn<true, 2>), dim3(gnn * 2, P), dim3(kMpNnThreads), 0, st, b);
+      else hipLaunchKernelGGL((k_mp_nn<false, 2>), dim3(gnn * 2, P), dim3(kMpNnThreads), 0, st, b);
     } else if (prof) {
       hipLaunchKernelGGL((k_mp_nn<true, 1>), dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
     } else {
@@ -2141,7 +2133,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     }
     mark("k_mp_nn");
     const int gfit = gq * (kMpQueryThreads / kMpFitThreads);
-    if (P <= LOAM_MP_FUSED_MAX && gfit <= kMpFitGridMax) {
+    if (P <= b.tune.mp_fused_max && gfit <= kMpFitGridMax) {
       hipLaunchKernelGGL(k_mp_fit<true>, dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
       mark("k_mp_fit");
       continue;

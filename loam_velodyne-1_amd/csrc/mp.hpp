@@ -113,6 +113,7 @@ struct MpBuffers {
   int* done = nullptr;        // [P] its workgroups finished (the last one runs the step)
   double* rot = nullptr;      // [P][6] cos / sin of the TobeMapped rotation (rot_store in mp.hip)
   int* nreg = nullptr;
+  Tuning tune;                // host-side launch choices (mp_frame)
   hipError_t sticky = hipSuccess;  // first failed HIP call of the launch sequences
   void note(hipError_t e) {
     if (sticky == hipSuccess) sticky = e;

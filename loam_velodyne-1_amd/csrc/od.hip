@@ -24,21 +24,10 @@
 
 using namespace loamdev;
 
-// largest batch whose odometry rows + step take the fused last-workgroup kernel (k_od_rows_small)
-#ifndef LOAM_OD_SMALL_MAX
-#define LOAM_OD_SMALL_MAX 63
-#endif
-// batches whose association rounds run their iterations in one workgroup per problem (k_od_lm)
-#ifndef LOAM_OD_LM_MIN
-#define LOAM_OD_LM_MIN 1
-#endif
-#ifndef LOAM_OD_LM_MAX
-#define LOAM_OD_LM_MAX 0
-#endif
-// largest batch whose k_od_rows runs the step in its last workgroup (no k_od_step launches)
-#ifndef LOAM_OD_FUSED_MAX
-#define LOAM_OD_FUSED_MAX 0  // (measured at batch 128: rows + step 0.67 -> 0.62 ms/step, whole step unchanged; 1024 slower)
-#endif
+// batch-size launch choices (k_od_rows_small / k_od_lm / k_od_rows<true> / k_od_assoc grid): the
+// context's Tuning (engine.hpp), OdBuffers::tune
+// (measured at batch 128: k_od_rows<true> rows + step 0.67 -> 0.62 ms/step, whole step unchanged;
+// 1024 slower)
 
 // diagnostic builds: count only one phase's gathered points in od_assoc_gathered (1: the 27 cells,
 // 2: the chunk fallback beyond one cell, 3: the ring windows); 0 (product): all
@@ -1432,7 +1421,7 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   A(&b.q_cf, (size_t)P * max_iter * b.cap_q * sizeof(float4));
   A(&b.q_ok, (size_t)P * max_iter * b.cap_q * sizeof(int8_t));
   // per-workgroup partials: [P][gq][28], or [P][gq * max_iter][28] for the small-batch rows kernel
-  A(&b.part, (size_t)P * b.gq * (P <= LOAM_OD_SMALL_MAX ? max_iter : 1) * 28 * sizeof(double));
+  A(&b.part, (size_t)P * b.gq * max_iter * 28 * sizeof(double));  // (k_od_rows_small: per stored iteration)
   A(&b.done, (size_t)P * sizeof(int));
   if (A.err != hipSuccess) {
     od_free(b);
@@ -1495,14 +1484,15 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
   const int P = b.P;
   auto mark = [&](const char* n) { if (prof) prof->mark(n); };
   hipLaunchKernelGGL(k_od_begin, dim3((P + 255) / 256), dim3(256), 0, st, b, f);
-  // batches up to LOAM_OD_LM_MAX problems: each association round's iterations in one k_od_lm
+  // batches of tune.od_lm_min .. od_lm_max problems: each association round's iterations in one k_od_lm
   // workgroup per problem (the queries must fit its lanes)
-  const bool lm_round = P >= LOAM_OD_LM_MIN && P <= LOAM_OD_LM_MAX && b.cap_q <= kOdLmThreads;
+  const Tuning& tn = b.tune;
+  const bool lm_round = P >= tn.od_lm_min && P <= tn.od_lm_max && b.cap_q <= kOdLmThreads;
   for (int it = 0; it < b.max_iter; ++it) {
     if (it % 5 == 0) {  // Q10
       // one wave per query when the batch is small (streaming: TransformToStart in the wave), 64
       // waves per problem otherwise (the queries transformed by k_od_sel first)
-      const int ga = P >= 64 ? 16 * kOdWaves / kAsWaves : (b.cap_q + kAsWaves - 1) / kAsWaves;  // (8 / 32 / 64 measured slower)
+      const int ga = P >= 64 ? tn.od_assoc_wg : (b.cap_q + kAsWaves - 1) / kAsWaves;  // (8 / 32 / 64 measured slower)
       if (P >= 64) {
         hipLaunchKernelGGL(k_od_sel, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f);
         if (prof) hipLaunchKernelGGL((k_od_assoc<true, false>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
@@ -1519,11 +1509,11 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
         continue;
       }
     }
-    if (P <= LOAM_OD_SMALL_MAX) {  // measured: the fused step loses for large batches (its serial tail)
+    if (P <= tn.od_small_max) {  // measured: the fused step loses for large batches (its serial tail)
       hipLaunchKernelGGL(k_od_rows_small, dim3(b.gq, P, it + 1), dim3(kOdThreads), 0, st, b, f, last_buf, it);
       mark("k_od_rows");
     } else {
-      if (P <= LOAM_OD_FUSED_MAX) {
+      if (P <= tn.od_fused_max) {
         hipLaunchKernelGGL(k_od_rows<true>, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         mark("k_od_rows");
       } else {

@@ -86,6 +86,7 @@ struct OdBuffers {
   int8_t* q_ok = nullptr;     // [P][max_iter][cap_q] accepted flags
   double* part = nullptr;     // [P][gq][28] per-workgroup JᵀJ | Jᵀb | rows
   int* done = nullptr;        // [P] workgroups of k_od_rows finished (the last one runs the step)
+  Tuning tune;                // host-side launch choices (od_solve)
 };
 
 // both clouds' indexes: a workgroup per cloud for batches, a grid per cloud for P <= 4

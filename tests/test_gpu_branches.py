@@ -202,3 +202,55 @@ def test_pipeline_matches_oracle(loam, oc, sg):
         assert np.abs(aft - aft_o).max() <= POSE_TOL, (i, aft, aft_o)
         assert np.abs(bef - bef_o).max() <= POSE_TOL, i
         _cloud_eq(reg, reg_o, f"registered@{i}")
+
+
+_SHARE = {}
+
+
+def _share_run(loam, sg, **tune):
+    P, r = 128, 7
+    if "inputs" not in _SHARE:
+        _SHARE["inputs"] = sg.batch_problems(P, base_seed=1000 + r * P)
+    prevs, curs = _SHARE["inputs"]
+    e = loam.Engine()
+    e.set_tuning(**tune)
+    e.batch_upload(prevs, curs)
+    e.batch_run()
+    od, aft, st = e.batch_download()
+    e.close()
+    return od, aft, st
+
+
+@pytest.mark.parametrize("tune", [
+    {"od_fused_max": 128},                   # k_od_rows<true>: the step in the rows' last workgroup
+    {"od_lm_max": 128},                      # k_od_lm: an association round in one workgroup per problem
+    {"od_small_max": 128},                   # k_od_rows_small: a workgroup per (queries, stored iteration)
+    {"mp_fused_max": 0},                     # k_mp_fit<false> + k_mp_iter
+    {"mp_small_max": 128},                   # k_mp_lm_small: one launch per mapping iteration
+    {"nn_lanes": 2}, {"nn_lanes": 4},        # k_mp_nn<., L>: L lanes per query, merged 5-lists
+    {"od_assoc_wg": 16},                     # fewer association waves per problem (queries looped)
+], ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
+def test_launch_choices_at_8gpu_share(loam, oc, sg, tune):
+    """every launch shape the engine can pick by batch size (include/loam/loam.h loam_set_tuning),
+    forced at the 8-GPU share: the poses equal the default shapes' bit for bit, and a few problems
+    equal the oracle"""
+    if "default" not in _SHARE:
+        _SHARE["default"] = _share_run(loam, sg)
+    od0, aft0, st0 = _SHARE["default"]
+    od, aft, st = _share_run(loam, sg, **tune)
+    np.testing.assert_array_equal(od, od0)
+    np.testing.assert_array_equal(aft, aft0)
+    assert st["od_iters"] == st0["od_iters"] and st["mp_iters"] == st0["mp_iters"]
+    prevs, curs = _SHARE["inputs"]
+    for i in (0, 77, 127):
+        od_o, aft_o, _ = oc.problem(prevs[i], curs[i])
+        assert max(np.abs(od[i] - od_o).max(), np.abs(aft[i] - aft_o).max()) <= POSE_TOL, i
+
+
+def test_tuning_rejects_unknown(loam):
+    e = loam.Engine()
+    with pytest.raises(Exception):
+        e.set_tuning(no_such_key=1)
+    with pytest.raises(Exception):
+        e.set_tuning(nn_lanes=3)
+    e.close()
