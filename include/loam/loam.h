@@ -110,6 +110,9 @@ typedef struct {
   uint64_t mp_nn_cells;         /* hash bucket ranges the 5-NN read */
   uint64_t od_assoc_gathered;   /* Last-cloud points the association loaded (cells, fallback, windows) */
   uint64_t od_assoc_boxes;      /* 64-point chunk boxes the association loaded */
+  uint64_t mp_nn_lds_blocks;    /* query blocks of the LDS-staged 5-NN (tuning nn_lds; profiling pass) */
+  uint64_t mp_nn_lds_fit;       /*   of them whose buckets fit the LDS set and point buffer */
+  uint64_t mp_nn_lds_staged;    /*   queries searched from LDS */
 } loam_stats;
 
 typedef struct loam_ctx loam_ctx;

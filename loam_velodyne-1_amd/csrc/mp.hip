@@ -986,6 +986,9 @@ __global__ void k_mp_lm_begin(MpBuffers b) {
   ist[kMiDegSteps] = 0;
   ist[kMiNnCand] = 0;
   ist[kMiNnCells] = 0;
+  ist[kMiLdsBlocks] = 0;
+  ist[kMiLdsFit] = 0;
+  ist[kMiLdsStaged] = 0;
 }
 
 // One L-M iteration's correspondences (:714-877), lane per stack point (corner, then surf), in
@@ -1476,6 +1479,14 @@ __global__ __launch_bounds__(kNnLdsThreads) void k_mp_nn_lds(MpBuffers b) {
         knn5(c.hss, c.hsp, c.TS, sel, t, work);
       }
       mp_nn_store(c, q, t);
+    }
+    if (COUNT) {
+      const int ns = wave_sum((act && staged && fit) ? 1 : 0);
+      if (lane_id() == 0 && ns) atomicAdd((int*)&ist[kMiLdsStaged], ns);
+      if (tid == 0) {
+        atomicAdd((int*)&ist[kMiLdsBlocks], 1);
+        if (fit) atomicAdd((int*)&ist[kMiLdsFit], 1);
+      }
     }
     __syncthreads();
   }
@@ -2670,6 +2681,9 @@ int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats*
       stats->mp_grid_shifts += (uint64_t)q[kMiShifts];
       stats->mp_nn_candidates += (uint64_t)(uint32_t)q[kMiNnCand];
       stats->mp_nn_cells += (uint64_t)(uint32_t)q[kMiNnCells];
+      stats->mp_nn_lds_blocks += (uint64_t)(uint32_t)q[kMiLdsBlocks];
+      stats->mp_nn_lds_fit += (uint64_t)(uint32_t)q[kMiLdsFit];
+      stats->mp_nn_lds_staged += (uint64_t)(uint32_t)q[kMiLdsStaged];
     }
   }
   return LOAM_OK;

@@ -27,8 +27,9 @@ enum { kMiCenW = 0, kMiCenH, kMiCenD, kMiDegen, kMiNValid, kMiIters, kMiRows, kM
        kMiShifts,    // cube-grid slab shifts of this frame's recentring (the reference's passes)
        kMiNnCand,    // map points the 5-NN evaluated this frame (seeds included)
        kMiNnCells,   // hash bucket ranges the 5-NN read this frame
-       kMpStateInts = 24 };
-static_assert(kMiNnCells < kMpStateInts, "istate layout");
+       kMiLdsBlocks, kMiLdsFit, kMiLdsStaged,  // k_mp_nn_lds<COUNT>: blocks, blocks staged, queries staged
+       kMpStateInts = 28 };
+static_assert(kMiLdsStaged < kMpStateInts, "istate layout");
 
 // one mapping frame's inputs for every instance (device pointers)
 struct MpInput {

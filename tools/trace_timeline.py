@@ -16,9 +16,10 @@ import re
 
 
 def short(name):
-    n = re.sub(r"\(.*$", "", name)          # drop the argument list
+    n = name.replace("(anonymous namespace)::", "")
+    n = re.sub(r"\(.*$", "", n)             # drop the argument list
     n = re.sub(r"^void ", "", n)
-    n = re.sub(r"^loam::(\(anonymous namespace\)::)?", "", n)
+    n = re.sub(r"^loam::", "", n)
     return n.strip()
 
 
