@@ -2315,7 +2315,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
       mark("k_mp_lm_small");
       continue;
     }
-    const int gnn = gq * (kMpQueryThreads / kMpNnThreads);
+    const int gnn = b.tune.nn_wg > 0 ? b.tune.nn_wg : gq * (kMpQueryThreads / kMpNnThreads);
     // L lanes per query for shares of a few hundred problems (the slowest wave is the launch)
     const int L = P <= b.tune.nn_lanes_maxp ? b.tune.nn_lanes : 1;
     if (b.tune.nn_lds) {  // the block's cells staged in LDS (k_mp_nn_lds: 256 queries per workgroup)
@@ -2333,7 +2333,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
       hipLaunchKernelGGL((k_mp_nn<false, 1>), dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
     }
     mark("k_mp_nn");
-    const int gfit = gq * (kMpQueryThreads / kMpFitThreads);
+    const int gfit = b.tune.fit_wg > 0 ? std::min(b.tune.fit_wg, kMpFitGridMax) : gq * (kMpQueryThreads / kMpFitThreads);
     if (P <= b.tune.mp_fused_max && gfit <= kMpFitGridMax) {
       hipLaunchKernelGGL(k_mp_fit<true>, dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
       mark("k_mp_fit");

@@ -955,8 +955,10 @@ LOAM_D void od_trig(const float* T, float* trig) {
 // FUSED: the last workgroup of the problem to finish sums the gq partials (in k_od_step's order)
 // and runs the step itself, instead of a k_od_step launch per iteration.
 constexpr int kOdRowsWpe = 4;  // <= 128 VGPRs with two rows' loads in flight
-template <bool FUSED>
-__global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdRowsWpe))) void k_od_rows(OdBuffers b, FeatView f, int last_buf, int iter) {
+// INF: stored rows whose loads are in flight together per lane step (2 for large batches, where
+// occupancy hides the chain; more for small ones, where the lane's chain of iter + 1 loads is the time)
+template <bool FUSED, int INF>
+__global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(INF > 2 ? 2 : kOdRowsWpe))) void k_od_rows(OdBuffers b, FeatView f, int last_buf, int iter) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const int* ist = b.istate + (size_t)p * kOdStateInts;
@@ -988,18 +990,18 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdR
   for (int k = 0; k < 28; ++k) acc[k] = 0.0;
   if (q < nq) {
     const OdJf e = od_jfactors(trig, T, po);
-    // the stored rows two iterations at a time (their loads in flight together), summed in order
-    for (int it0 = 0; it0 <= iter; it0 += 2) {
-      float4 cv4[2];
-      bool okv[2];
+    // the stored rows INF iterations at a time (their loads in flight together), summed in order
+    for (int it0 = 0; it0 <= iter; it0 += INF) {
+      float4 cv4[INF];
+      bool okv[INF];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < INF; ++u) {
         const int it = it0 + u;
         cv4[u] = it <= iter ? qcf[(size_t)it * b.cap_q + q] : make_float4(0, 0, 0, 0);
         okv[u] = row_ok(cv4[u]);
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < INF; ++u)
         if (it0 + u <= iter) od_row_accum(e, cv4[u], okv[u], acc);
     }
   }
@@ -1513,11 +1515,14 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
       hipLaunchKernelGGL(k_od_rows_small, dim3(b.gq, P, it + 1), dim3(kOdThreads), 0, st, b, f, last_buf, it);
       mark("k_od_rows");
     } else {
+      const bool deep = P <= tn.od_rows_deep_max;  // more stored rows' loads in flight per lane
       if (P <= tn.od_fused_max) {
-        hipLaunchKernelGGL(k_od_rows<true>, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+        if (deep) hipLaunchKernelGGL((k_od_rows<true, 8>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+        else hipLaunchKernelGGL((k_od_rows<true, 2>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         mark("k_od_rows");
       } else {
-        hipLaunchKernelGGL(k_od_rows<false>, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+        if (deep) hipLaunchKernelGGL((k_od_rows<false, 8>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+        else hipLaunchKernelGGL((k_od_rows<false, 2>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         mark("k_od_rows");
         hipLaunchKernelGGL(k_od_step, dim3(P), dim3(64), 0, st, b, it, b.gq);
         mark("k_od_step");
