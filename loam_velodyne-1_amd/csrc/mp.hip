@@ -1501,6 +1501,52 @@ __global__ __launch_bounds__(kNnLdsThreads) void k_mp_nn_lds(MpBuffers b) {
 // FUSED: each lane also adds its accepted row (as k_mp_lm_small does), the workgroup's fp64 partial
 // is stored write-through, and the last workgroup of the instance sums the partials in order and
 // runs the step: no k_mp_iter launch.
+// the fused step of one-wave workgroups (k_mp_fit<true>, k_mp_nnfit<true>): the wave's row sums as
+// this workgroup's partial (write-through), and the last workgroup of the instance to arrive sums
+// the G partials in workgroup order and runs the step
+LOAM_D void mp_partial_and_step(const MpBuffers& b, int p, int wg, int G, double (&acc)[28]) {
+  static_assert(kMpFitThreads == 64, "one wave per workgroup: the wave's sums are the partial");
+  const int lane = lane_id();
+  wave_reduce_scatter_28(acc);  // lanes 2v, 2v+1: the sum of value v
+  if ((lane & 1) == 0 && (lane >> 1) < 28)
+    store_partial(&b.part[((size_t)p * kMpFitGridMax + wg) * 28 + (lane >> 1)], acc[0]);
+  __shared__ int sh_last;
+  __shared__ double tot[28];
+  __shared__ MpStepScratch sh;
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) sh_last = arrive_last(&b.done[p], G);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (!sh_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  {  // fixed order over the workgroups: lane (half h, value v) sums half h of the partials in
+     // order, sixteen loads in flight per round, then the two halves are added in order
+    const int v = lane % 28, h = lane / 28, G2 = (G + 1) / 2;
+    const int g0 = h == 0 ? 0 : G2, g1 = h == 0 ? G2 : G;
+    const double* pp = b.part + (size_t)p * kMpFitGridMax * 28 + v;
+    double sum = 0.0;
+    if (h < 2) {
+      for (int g = g0; g < g1; g += 16) {
+        double t[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          t[u] = g + u < g1 ? __hip_atomic_load(&pp[(size_t)(g + u) * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (g + u < g1) sum += t[u];
+      }
+    }
+    const double upper = __shfl_down(sum, 28, 64);
+    if (lane < 28) tot[lane] = sum + upper;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (lane == 0) b.done[p] = 0;
+  mp_step(b, p, tot, sh);
+}
+
 template <bool FUSED>
 __global__ __launch_bounds__(kMpFitThreads) void k_mp_fit(MpBuffers b) {
   const XcdBlock blk = xcd_block();
@@ -1544,49 +1590,74 @@ __global__ __launch_bounds__(kMpFitThreads) void k_mp_fit(MpBuffers b) {
   }
   nfits = wave_sum(nfits);
   if (lane_id() == 0 && nfits) atomicAdd(&ist[kMiFits], nfits);
+  if constexpr (FUSED) mp_partial_and_step(b, p, blk.x, (int)gridDim.x, acc);
+}
+
+// One mapping L-M iteration's correspondences in one launch (small batches): lane per query, the
+// 5-NN search (mp_nn_query, k_mp_nn's) then the fit and row (mp_fit_query, k_mp_fit's) — the fit
+// needs only the lane's own five neighbours — in one-wave workgroups whose 27-entry candidate
+// lists and 27-word Jacobi scratch share one LDS array (the wave's search is over before its fits
+// begin).  Same query -> lane mapping and row order as k_mp_fit, so the sums are k_mp_fit's.
+// FUSED: the partial + last-workgroup step of k_mp_fit<true>.  COUNT: the work counters.
+template <bool FUSED, bool COUNT>
+__global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(FUSED ? 2 : 4))) void k_mp_nnfit(MpBuffers b) {
+  constexpr int NT = kMpFitThreads;
+  static_assert(NT == 64, "the list / scratch sharing needs one wave per workgroup");
+  const XcdBlock blk = xcd_block();
+  const int p = blk.y, tid = threadIdx.x;
+  int* ist = b.istate + (size_t)p * kMpStateInts;
+  if (!ist[kMiLmRan] || ist[kMiStop]) return;
+  const bool first = ist[kMiIters] == 0;
+  __shared__ uint32_t lds[kNnListCap * NT];  // candidate lists (column tid, stride NT) / Jacobi rows
+  const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
+  const int nq = nsc + nss;
+  int8_t* qok = b.q_ok + (size_t)p * b.cap_stack;
+  float4* qcf = b.q_cf + (size_t)p * b.cap_stack;
+  const loampose::MapRot r = rot_load(b, p);
+  const MpNnCtx c = mp_nn_ctx(b, p);
+  const MpTrig tg = mp_trig_of(r);
+  float* jw = (float*)lds + tid * 27;
+  int nfits = 0, work = 0;
+  double acc[FUSED ? 28 : 1];
   if constexpr (FUSED) {
-    static_assert(kMpFitThreads == 64, "one wave per workgroup: the wave's sums are the partial");
-    const int lane = lane_id();
-    wave_reduce_scatter_28(acc);  // lanes 2v, 2v+1: the sum of value v
-    const int G = (int)gridDim.x;
-    if ((lane & 1) == 0 && (lane >> 1) < 28)
-      store_partial(&b.part[((size_t)p * kMpFitGridMax + blk.x) * 28 + (lane >> 1)], acc[0]);
-    __shared__ int sh_last;
-    __shared__ double tot[28];
-    __shared__ MpStepScratch sh;
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) sh_last = arrive_last(&b.done[p], G);
+#pragma unroll
+    for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+  }
+  for (int q0 = blk.x * NT; q0 < nq; q0 += gridDim.x * NT) {  // (wave-uniform trip count)
+    const int q = q0 + tid;
+    float4 sel = make_float4(0, 0, 0, 0);
+    Top5 t;
+    if (q < nq) mp_nn_query<NT, 1, kNnListCap>(b, c, q, nsc, first, r, lds + tid, sel, t, work);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_wave_barrier();  // every lane's list reads are done before the scratch reuse
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (!sh_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    {  // fixed order over the workgroups: lane (half h, value v) sums half h of the partials in
-       // order, sixteen loads in flight per round, then the two halves are added in order
-      const int v = lane % 28, h = lane / 28, G2 = (G + 1) / 2;
-      const int g0 = h == 0 ? 0 : G2, g1 = h == 0 ? G2 : G;
-      const double* pp = b.part + (size_t)p * kMpFitGridMax * 28 + v;
-      double sum = 0.0;
-      if (h < 2) {
-        for (int g = g0; g < g1; g += 16) {
-          double t[16];
-#pragma unroll
-          for (int u = 0; u < 16; ++u)
-            t[u] = g + u < g1 ? __hip_atomic_load(&pp[(size_t)(g + u) * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-#pragma unroll
-          for (int u = 0; u < 16; ++u)
-            if (g + u < g1) sum += t[u];
-        }
-      }
-      const double upper = __shfl_down(sum, 28, 64);
-      if (lane < 28) tot[lane] = sum + upper;
+    if (q < nq) {
+      const bool corner = q < nsc;
+      const int4 n0 = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
+      const int4 n1 = make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0);
+      float4 o = make_float4(0, 0, 0, 0), cf;
+      if (n1.x != 0x7fffffff && D(t.d[4]) < 1.0) o = c.stack[corner ? q : b.capC + (q - nsc)];
+      int ok;
+      mp_fit_query(b, p, q, nsc, first, n0, n1, sel, jw, nfits, cf, ok);
+      qok[q] = (int8_t)ok;
+      qcf[q] = cf;
+      if constexpr (FUSED)
+        if (ok) mp_row_accum(tg, o, cf, acc);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_wave_barrier();  // the fits' scratch is free before the next lists
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (lane == 0) b.done[p] = 0;
-    mp_step(b, p, tot, sh);
   }
+  nfits = wave_sum(nfits);
+  if (lane_id() == 0 && nfits) atomicAdd(&ist[kMiFits], nfits);
+  if (COUNT) {
+    const int ncand = wave_sum(work & ((1 << kWorkCellShift) - 1)), ncell = wave_sum(work >> kWorkCellShift);
+    if (lane_id() == 0 && ncand) {
+      atomicAdd(&ist[kMiNnCand], ncand);
+      atomicAdd(&ist[kMiNnCells], ncell);
+    }
+  }
+  if constexpr (FUSED) mp_partial_and_step(b, p, blk.x, (int)gridDim.x, acc);
 }
 
 namespace {
@@ -2315,6 +2386,20 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
       mark("k_mp_lm_small");
       continue;
     }
+    const int gfit = b.tune.fit_wg > 0 ? std::min(b.tune.fit_wg, kMpFitGridMax) : gq * (kMpQueryThreads / kMpFitThreads);
+    if (P <= b.tune.nnfit_max && gfit <= kMpFitGridMax) {  // search + fit (+ step) in one launch
+      const bool fused = P <= b.tune.mp_fused_max;
+      if (fused && prof) hipLaunchKernelGGL((k_mp_nnfit<true, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+      else if (fused) hipLaunchKernelGGL((k_mp_nnfit<true, false>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+      else if (prof) hipLaunchKernelGGL((k_mp_nnfit<false, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+      else hipLaunchKernelGGL((k_mp_nnfit<false, false>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+      mark("k_mp_nnfit");
+      if (!fused) {
+        hipLaunchKernelGGL(k_mp_iter, dim3(P), dim3(kMpThreads), 0, st, b);
+        mark("k_mp_iter");
+      }
+      continue;
+    }
     const int gnn = b.tune.nn_wg > 0 ? b.tune.nn_wg : gq * (kMpQueryThreads / kMpNnThreads);
     // L lanes per query for shares of a few hundred problems (the slowest wave is the launch)
     const int L = P <= b.tune.nn_lanes_maxp ? b.tune.nn_lanes : 1;
@@ -2333,7 +2418,6 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
       hipLaunchKernelGGL((k_mp_nn<false, 1>), dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
     }
     mark("k_mp_nn");
-    const int gfit = b.tune.fit_wg > 0 ? std::min(b.tune.fit_wg, kMpFitGridMax) : gq * (kMpQueryThreads / kMpFitThreads);
     if (P <= b.tune.mp_fused_max && gfit <= kMpFitGridMax) {
       hipLaunchKernelGGL(k_mp_fit<true>, dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
       mark("k_mp_fit");

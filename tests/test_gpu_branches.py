@@ -232,6 +232,8 @@ def _share_run(loam, sg, **tune):
     {"nn_lds": 1},                           # k_mp_nn_lds: the workgroup's map cells staged in LDS
     {"od_rows_deep_max": 128},               # k_od_rows<., 8>: eight stored rows' loads in flight
     {"od_rows_deep_max": 128, "od_fused_max": 128},
+    {"nnfit_max": 128},                      # k_mp_nnfit<true>: 5-NN + fit + rows + step in one launch
+    {"nnfit_max": 128, "mp_fused_max": 0},   # k_mp_nnfit<false> + k_mp_iter
 ], ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_launch_choices_at_8gpu_share(loam, oc, sg, tune):
     """every launch shape the engine can pick by batch size (include/loam/loam.h loam_set_tuning),
