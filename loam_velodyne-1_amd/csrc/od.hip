@@ -185,6 +185,12 @@ __global__ __launch_bounds__(NT) void k_hash_build(HashJob j) {
   else hash_sort<NT, false>(j, pts, n, T, start, out, j.fill + (size_t)p * j.tmax, scratch, rec);
   if (j.chunks)  // chunk boxes of the source order
     chunk_boxes(pts, n, j.chunks + (size_t)p * 2 * chunks_of((int)j.pts_stride), tid >> 6, NT / 64);
+  if (j.mono) {  // rings non-decreasing in index order (one flag per cloud: no atomics)
+    bool bad = false;
+    for (int i = tid + 1; i < n; i += NT) bad |= (int)pts[i].w < (int)pts[i - 1].w;
+    bad = __syncthreads_or(bad);
+    if (tid == 0) j.mono[(size_t)p * j.mono_stride] = bad ? 0 : 1;
+  }
 }
 
 // ---- the same index built by many workgroups per cloud (small batches: streaming, config 2).  One
@@ -210,7 +216,10 @@ __global__ __launch_bounds__(256) void k_hash_zero(HashPair hp) {
   const HashJob& j = hp.j[blockIdx.z];
   const int p = blockIdx.y;
   const int T = hash_table_size(j, hash_count_of(j, p));
-  if (blockIdx.x == 0 && threadIdx.x == 0) j.tsize[p] = T;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    j.tsize[p] = T;
+    if (j.mono) j.mono[(size_t)p * j.mono_stride] = 1;  // (k_hash_count clears it on a ring drop)
+  }
   int* fill = j.fill + (size_t)p * j.tmax;
   for (int b = blockIdx.x * 256 + threadIdx.x; b < T; b += gridDim.x * 256) fill[b] = 0;
 }
@@ -230,6 +239,11 @@ __global__ __launch_bounds__(256) void k_hash_count(HashPair hp) {
   if (j.chunks)  // chunk boxes of the source order (as k_hash_build)
     chunk_boxes(pts, n, j.chunks + (size_t)p * 2 * chunks_of((int)j.pts_stride), blockIdx.x * 4 + (tid >> 6),
                 gridDim.x * 4);
+  if (j.mono) {
+    bool bad = false;
+    for (int i = blockIdx.x * 256 + tid + 1; i < n; i += gridDim.x * 256) bad |= (int)pts[i].w < (int)pts[i - 1].w;
+    if (bad) j.mono[(size_t)p * j.mono_stride] = 0;
+  }
 }
 
 // exclusive scan of the counters into start (and back into fill as the scatter's cursors)
@@ -343,6 +357,21 @@ LOAM_D float box_d2(const float4& lo, const float4& hi, const float4& s) {
   return sqdist(gx, gy, gz, 0.0f, 0.0f, 0.0f);
 }
 
+// j (ring r) belongs to the window set of a query whose nearest point is c (ring scan): the points
+// the forward walk c+1 .. fwd_end-1 and the backward walk c-1 .. 0 visit before their stops, of the
+// wanted category (corner: the other rings; surf: same = the same / lower ring forward and the same /
+// higher ring backward, else the other rings).  Exact for a ring-monotone cloud (HashJob::mono),
+// where every point of rings scan - 2 .. scan + 2 on the walk's side precedes the stop.
+LOAM_D bool window_member(int j, int r, int c, int scan, int fwd_end, bool corner, bool same) {
+  if (j > c) return j < fwd_end && r <= scan + 2 && (corner ? r > scan : (same ? r <= scan : r > scan));
+  return j < c && r >= scan - 2 && (corner ? r < scan : (same ? r >= scan : r < scan));
+}
+
+// bounds of the window minima known before the walks (squared distances of members, or 25)
+struct WinBound {
+  float same = 25.0f, other = 25.0f;
+};
+
 // exact nearest neighbour of q among the hashed cloud (wave-cooperative), as far as it matters:
 // returns the packed (float distance bits << 32 | index << 8 | ring) minimum (ties on the index,
 // as before: the ring is a function of the point), or ~0 when no point lies
@@ -351,8 +380,12 @@ LOAM_D float box_d2(const float4& lo, const float4& hi, const float4& s) {
 // boxes of the whole cloud closer than 5 m.  `cells` = per-wave LDS scratch of 64 ints.
 // bound: the squared distance of a known point of the cloud (a seed), or above 25: cells and chunks
 // whose box lies beyond it cannot hold the minimum (which is <= the seed's) and are skipped
+// kind 0 / 1 (corner / surf, 1 m cells only; -1: none) with mono: when the nearest point lies in the
+// 27 cells, the cells' points that belong to its window sets (window_member, fwd_end) bound the
+// window minima (wb): a chunk beyond such a member cannot hold the minimum.
 LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const float4* cloud, const float4* ch,
-                             int n, float h, float inv_h, float4 q, float bound, int* cells, int& wpts, int& wbox) {
+                             int n, float h, float inv_h, float4 q, float bound, int* cells, int& wpts, int& wbox,
+                             int kind = -1, int fwd_end = 0, bool mono = false, WinBound* wb = nullptr) {
   const int lane = lane_id();
   const int cx = cell_of(q.x, inv_h), cy = cell_of(q.y, inv_h), cz = cell_of(q.z, inv_h);
   int bucket = -1, b0 = 0, cnt = 0;
@@ -377,13 +410,18 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
   if (lane < 32) { cells[lane] = lane < 27 ? incl - cnt : 0x7fffffff; cells[32 + lane] = b0; }
   __builtin_amdgcn_wave_barrier();
   uint64_t best = ~0ull;
-  for (int t = lane; t < total; t += 64) {
+  auto cand = [&](int t) {
     int k = 0;  // last cell whose prefix is <= t (binary search over 32 entries)
 #pragma unroll
     for (int step = 16; step > 0; step >>= 1)
       if (cells[k + step] <= t) k += step;
     LOAM_CHECK(cells[32 + k] + (t - cells[k]) < n && cells[32 + k] >= 0, cells[32 + k] + (t - cells[k]), n);
-    const float4 a = hp[cells[32 + k] + (t - cells[k])];
+    return hp[cells[32 + k] + (t - cells[k])];
+  };
+  float4 a0 = make_float4(0, 0, 0, 0);  // the lane's first candidate, kept for the window bounds
+  for (int t = lane; t < total; t += 64) {
+    const float4 a = cand(t);
+    if (t == lane) a0 = a;
     const float d = sqdist(a.x, a.y, a.z, q.x, q.y, q.z);
     const uint32_t tag = (uint32_t)__float_as_int(a.w);  // index | ring << 24
     const uint64_t key = ((uint64_t)fkey(d) << 32) | ((tag & 0xffffffu) << 8) | (tag >> 24);
@@ -391,7 +429,28 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
   }
   best = wave_min_u64(best);
   __builtin_amdgcn_wave_barrier();
-  if (best != ~0ull && __uint_as_float((uint32_t)(best >> 32)) < h * h) return best;
+  if (best != ~0ull && __uint_as_float((uint32_t)(best >> 32)) < h * h) {
+    if (kind >= 0 && mono && D(__uint_as_float((uint32_t)(best >> 32))) < 25) {
+      const int c = (int)((uint32_t)best >> 8), scan = (int)((uint32_t)best & 255u);
+      float ms = 3.4e38f, mo = 3.4e38f;
+      for (int t = lane; t < total; t += 64) {
+        const float4 a = t == lane ? a0 : cand(t);
+        const uint32_t tag = (uint32_t)__float_as_int(a.w);
+        const int j = (int)(tag & 0xffffffu), r = (int)(tag >> 24);
+        const float d = sqdist(a.x, a.y, a.z, q.x, q.y, q.z);
+        if (kind == 0) {
+          if (window_member(j, r, c, scan, fwd_end, true, false)) mo = fminf(mo, d);
+        } else if (window_member(j, r, c, scan, fwd_end, false, true)) {
+          ms = fminf(ms, d);
+        } else if (window_member(j, r, c, scan, fwd_end, false, false)) {
+          mo = fminf(mo, d);
+        }
+      }
+      wb->same = fminf(wb->same, wave_min_f(ms));
+      wb->other = fminf(wb->other, wave_min_f(mo));
+    }
+    return best;
+  }
   if (LOAM_ASSOC_SKIP & 2) return best;
   // farther than one cell: the chunks of the whole cloud that may hold a point closer than 5 m
   best = ~0ull;
@@ -424,14 +483,16 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
 // lies beyond scan +- 2.5.  `f(j, a, d)` is called by the lane holding point j (before the stop)
 // with d < 25.  Whole 64-point chunks whose box is >= 5 m from sel are skipped; a chunk that may
 // hold the stop is always examined.
-// bw: chunks whose box lies beyond it are skipped too (a seed's squared distance, or 25)
+// bs / bo: bounds of the same-ring / other-ring minima (squared distances of known members, or 25;
+// bs < 0: no same-ring minimum is taken, the corner walk): a chunk is needed only when its box may
+// beat the bound of a category its ring range [lo.w, hi.w] can hold
 #ifndef LOAM_WIN_INFLIGHT
 #define LOAM_WIN_INFLIGHT 1  // (measured k_od_assoc ms/step at batch 1024: 1 -> 2.81, 2 -> 2.80, 3 -> 3.01)
 #endif
 constexpr int kWinInFlight = LOAM_WIN_INFLIGHT;
 template <typename F>
-LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int dir, int scan, float4 sel, float bw,
-                        int& wpts, int& wbox, F f) {
+LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int dir, int scan, float4 sel, float bs,
+                        float bo, int& wpts, int& wbox, F f) {
   const int lane = lane_id();
   // int(intensity) > scan + 2.5 (double) <=> r > scan + 2 for integers (and < scan - 2.5 <=> < scan - 2)
   auto stop_ring = [&](int r) { return dir > 0 ? r > scan + 2 : r < scan - 2; };
@@ -501,7 +562,9 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
       const uint64_t mc = __ballot(v && stop_ring((int)hi.w));
       const int limit = mc ? __ffsll((unsigned long long)mc) - 1 : 63;
       const float bd = box_d2(lo, hi, sel);
-      uint64_t nb = __ballot(v && lane <= limit && bd < 25.0f && bd <= bw);
+      // forward: the same category is ring <= scan, the other ring > scan
+      const bool need = bd < 25.0f && ((bd <= bs && (int)lo.w <= scan) || (bd <= bo && (int)hi.w > scan));
+      uint64_t nb = __ballot(v && lane <= limit && need);
       run_set(nb, j / kChunk, +1, 0);
       if (mc) return;
       j += 64 * kChunk;
@@ -521,7 +584,9 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
       const uint64_t mc = __ballot(v && stop_ring((int)lo.w));
       const int limit = mc ? __ffsll((unsigned long long)mc) - 1 : 63;
       const float bd = box_d2(lo, hi, sel);
-      uint64_t nb = __ballot(v && lane <= limit && bd < 25.0f && bd <= bw);
+      // backward: the same category is ring >= scan, the other ring < scan
+      const bool need = bd < 25.0f && ((bd <= bs && (int)hi.w >= scan) || (bd <= bo && (int)lo.w < scan));
+      uint64_t nb = __ballot(v && lane <= limit && need);
       run_set(nb, kt, -1, kChunk - 1);
       if (mc) return;
       kt -= 64;
@@ -535,13 +600,12 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
 // now (sj < 0: none).  When it belongs to this round's window set (the sets are ring ranges of the
 // ring-major Last cloud, see wave_window) it bounds the window minimum, so chunks beyond it are
 // skipped; the minimum itself is still taken over every point the walk visits.
-LOAM_D bool window_member(int j, int r, int c, int scan, int fwd_end, bool corner, bool same) {
-  if (j > c) return j < fwd_end && r <= scan + 2 && (corner ? r > scan : (same ? r <= scan : r > scan));
-  return j < c && r >= scan - 2 && (corner ? r < scan : (same ? r >= scan : r < scan));
-}
 
+// wb: bounds from the nearest neighbour's cells (wave_hash_nn); mono: the cloud is ring-monotone,
+// without which no bound is used (window_member would not be exact)
 LOAM_D void wave_assoc_corner(const float4* CL, const float4* ch, int fwd_end, uint64_t nn, float4 sel,
-                              int sj, int sr, float sd, int& ind1, int& ind2, int& wpts, int& wbox) {
+                              int sj, int sr, float sd, const WinBound& wb, bool mono, int& ind1, int& ind2,
+                              int& wpts, int& wbox) {
   ind1 = -1;
   ind2 = -1;
   if (nn == ~0ull) return;
@@ -550,15 +614,16 @@ LOAM_D void wave_assoc_corner(const float4* CL, const float4* ch, int fwd_end, u
   const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u);
   ind1 = c;
   if (LOAM_ASSOC_SKIP & 1) return;
-  const float bw = sj >= 0 && window_member(sj, sr, c, scan, fwd_end, true, false) ? sd : 25.0f;
+  const float bw = !mono ? 25.0f
+                         : fminf(wb.other, sj >= 0 && window_member(sj, sr, c, scan, fwd_end, true, false) ? sd : 25.0f);
   uint64_t best = ~0ull;
-  wave_window(CL, ch, c, fwd_end, +1, scan, sel, bw, wpts, wbox, [&](int j, int r, float d) {
+  wave_window(CL, ch, c, fwd_end, +1, scan, sel, -1.0f, bw, wpts, wbox, [&](int j, int r, float d) {
     if (r > scan) {
       const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)(j - c - 1);
       best = key < best ? key : best;
     }
   });
-  wave_window(CL, ch, c, fwd_end, -1, scan, sel, bw, wpts, wbox, [&](int j, int r, float d) {
+  wave_window(CL, ch, c, fwd_end, -1, scan, sel, -1.0f, bw, wpts, wbox, [&](int j, int r, float d) {
     if (r < scan) {
       const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)((1u << 30) + (c - 1 - j));
       best = key < best ? key : best;
@@ -574,7 +639,7 @@ LOAM_D void wave_assoc_corner(const float4* CL, const float4* ch, int fwd_end, u
 // surface association (:590-650): closest, the best of the same / lower ring (min2) and of the
 // higher rings (min3) in the forward window; mirrored in the backward window.
 LOAM_D void wave_assoc_surf(const float4* SL, const float4* ch, int fwd_end, uint64_t nn, float4 sel,
-                            int sj2, int sr2, float sd2, int sj3, int sr3, float sd3,
+                            int sj2, int sr2, float sd2, int sj3, int sr3, float sd3, const WinBound& wb, bool mono,
                             int& ind1, int& ind2, int& ind3, int& wpts, int& wbox) {
   ind1 = ind2 = ind3 = -1;
   if (nn == ~0ull) return;
@@ -583,16 +648,18 @@ LOAM_D void wave_assoc_surf(const float4* SL, const float4* ch, int fwd_end, uin
   const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u);
   ind1 = c;
   if (LOAM_ASSOC_SKIP & 1) return;
-  const float b2 = sj2 >= 0 && window_member(sj2, sr2, c, scan, fwd_end, false, true) ? sd2 : 25.0f;
-  const float b3 = sj3 >= 0 && window_member(sj3, sr3, c, scan, fwd_end, false, false) ? sd3 : 25.0f;
-  const float bw = fmaxf(b2, b3);
+  float b2 = 25.0f, b3 = 25.0f;
+  if (mono) {
+    b2 = fminf(wb.same, sj2 >= 0 && window_member(sj2, sr2, c, scan, fwd_end, false, true) ? sd2 : 25.0f);
+    b3 = fminf(wb.other, sj3 >= 0 && window_member(sj3, sr3, c, scan, fwd_end, false, false) ? sd3 : 25.0f);
+  }
   uint64_t best2 = ~0ull, best3 = ~0ull;
-  wave_window(SL, ch, c, fwd_end, +1, scan, sel, bw, wpts, wbox, [&](int j, int r, float d) {
+  wave_window(SL, ch, c, fwd_end, +1, scan, sel, b2, b3, wpts, wbox, [&](int j, int r, float d) {
     const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)(j - c - 1);
     if (r <= scan) best2 = key < best2 ? key : best2;
     else best3 = key < best3 ? key : best3;
   });
-  wave_window(SL, ch, c, fwd_end, -1, scan, sel, bw, wpts, wbox, [&](int j, int r, float d) {
+  wave_window(SL, ch, c, fwd_end, -1, scan, sel, b2, b3, wpts, wbox, [&](int j, int r, float d) {
     const uint64_t key = ((uint64_t)fkey(d) << 32) | (uint32_t)((1u << 30) + (c - 1 - j));
     if (r >= scan) best2 = key < best2 ? key : best2;
     else best3 = key < best3 ? key : best3;
@@ -684,6 +751,7 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
   int wpts = 0, wbox = 0;  // wave-uniform work counters (loam_stats od_assoc_gathered / _boxes)
   const bool seeded = ist[kIsIters] > 0;  // ind holds this frame's previous round
   const int hCT = b.hC_T[last_buf * b.P + p], hST = b.hS_T[last_buf * b.P + p];
+  const bool monoC = b.mono[lp * 2 + 0] != 0, monoS = b.mono[lp * 2 + 1] != 0;
   const int G = gridDim.x * kAsWaves, q0 = blk.x * kAsWaves + w;
   // The wave's queries q0, q0 + G, ... in batches of 64: lane l first fetches query l's
   // TransformToStart point and its seeds — the previous round's choices (ind, rounds after the
@@ -731,16 +799,17 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
       const int j1 = jj.y, j2 = jj.z, r1 = jj.w & 0xffff, r2 = jj.w >> 16;
       const float nnb = dd.x, d1 = dd.y, d2 = dd.z;
       int i1, i2, i3 = -1;
+      WinBound wb;
       if (q < nc) {
         const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
         const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC, hCT, CL, ch, C, 1.0f,
-                                         1.0f, s4, nnb, cells[w], wpts, wbox);
-        wave_assoc_corner(CL, ch, min(nc, C), nn, s4, j1, r1, d1, i1, i2, wpts, wbox);
+                                         1.0f, s4, nnb, cells[w], wpts, wbox, 0, min(nc, C), monoC, &wb);
+        wave_assoc_corner(CL, ch, min(nc, C), nn, s4, j1, r1, d1, wb, monoC, i1, i2, wpts, wbox);
       } else {
         const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
         const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS, hST, SL, ch, S, 1.0f,
-                                         1.0f, s4, nnb, cells[w], wpts, wbox);
-        wave_assoc_surf(SL, ch, min(ns, S), nn, s4, j1, r1, d1, j2, r2, d2, i1, i2, i3, wpts, wbox);
+                                         1.0f, s4, nnb, cells[w], wpts, wbox, 1, min(ns, S), monoS, &wb);
+        wave_assoc_surf(SL, ch, min(ns, S), nn, s4, j1, r1, d1, j2, r2, d2, wb, monoS, i1, i2, i3, wpts, wbox);
       }
       if (lane == 0) {
         LOAM_CHECK(q < b.cap_q && p < b.P, q, p);
@@ -1425,6 +1494,7 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   // per-workgroup partials: [P][gq][28], or [P][gq * max_iter][28] for the small-batch rows kernel
   A(&b.part, (size_t)P * b.gq * max_iter * 28 * sizeof(double));  // (k_od_rows_small: per stored iteration)
   A(&b.done, (size_t)P * sizeof(int));
+  A(&b.mono, (size_t)2 * P * 2 * sizeof(int));
   if (A.err != hipSuccess) {
     od_free(b);
     return A.err;
@@ -1443,7 +1513,7 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
 void od_free(OdBuffers& b) {
   void* ptrs[] = {b.state, b.istate, b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
-                  b.ind, b.sel, b.q_cf, b.q_ok, b.part, b.done};
+                  b.ind, b.sel, b.q_cf, b.q_ok, b.part, b.done, b.mono};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = OdBuffers();
@@ -1466,7 +1536,10 @@ void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
   jc.inv_h = 1.0f;
   jc.shift = 1;
   jc.chunks = b.cC + (size_t)buf * b.P * 2 * chunks_of(b.capC);
+  jc.mono = b.mono + (size_t)buf * b.P * 2;
+  jc.mono_stride = 2;
   HashJob js = jc;
+  js.mono = jc.mono + 1;
   js.pts = b.lastS + (size_t)buf * b.P * b.capS;
   js.pts_stride = b.capS;
   js.count = b.nlast + buf * 2 + 1;

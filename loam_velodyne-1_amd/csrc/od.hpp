@@ -55,6 +55,8 @@ struct HashJob {
                         // order, (min x, y, z, min ring) and (max x, y, z, max ring)
   uint32_t* rec = nullptr;  // optional [P][tmax]: bucket b's range packed as start | count << 19
                             // (hash_rec), kRecNone when it does not fit
+  int* mono = nullptr;      // optional: mono[p * mono_stride] = 1 when the cloud's rings int(w) never
+  int mono_stride = 1;      // decrease in index order (the association's window bounds rely on it)
 };
 constexpr uint32_t kRecNone = 0xffffffffu;
 LOAM_HD uint32_t hash_rec(int start, int count) {
@@ -86,6 +88,7 @@ struct OdBuffers {
   int8_t* q_ok = nullptr;     // [P][max_iter][cap_q] accepted flags
   double* part = nullptr;     // [P][gq][28] per-workgroup JᵀJ | Jᵀb | rows
   int* done = nullptr;        // [P] workgroups of k_od_rows finished (the last one runs the step)
+  int* mono = nullptr;        // [2][P][2] Last corner / surf of each buffer ring-monotone (HashJob::mono)
   Tuning tune;                // host-side launch choices (od_solve)
 };
 
