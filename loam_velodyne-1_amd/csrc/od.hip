@@ -799,16 +799,18 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
       const int j1 = jj.y, j2 = jj.z, r1 = jj.w & 0xffff, r2 = jj.w >> 16;
       const float nnb = dd.x, d1 = dd.y, d2 = dd.z;
       int i1, i2, i3 = -1;
+      // the cells' window bounds in the first round only (later rounds have their seeds: the extra
+      // pass over the cells cost more than the chunks it saved there)
       WinBound wb;
       if (q < nc) {
         const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
         const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC, hCT, CL, ch, C, 1.0f,
-                                         1.0f, s4, nnb, cells[w], wpts, wbox, 0, min(nc, C), monoC, &wb);
+                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded ? -1 : 0, min(nc, C), monoC, &wb);
         wave_assoc_corner(CL, ch, min(nc, C), nn, s4, j1, r1, d1, wb, monoC, i1, i2, wpts, wbox);
       } else {
         const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
         const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS, hST, SL, ch, S, 1.0f,
-                                         1.0f, s4, nnb, cells[w], wpts, wbox, 1, min(ns, S), monoS, &wb);
+                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded ? -1 : 1, min(ns, S), monoS, &wb);
         wave_assoc_surf(SL, ch, min(ns, S), nn, s4, j1, r1, d1, j2, r2, d2, wb, monoS, i1, i2, i3, wpts, wbox);
       }
       if (lane == 0) {
