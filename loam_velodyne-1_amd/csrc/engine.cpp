@@ -98,6 +98,17 @@ struct loam_ctx {
   hipStream_t st2 = nullptr;                 // batch: mapping frame 1 beside the odometry solve
   hipEvent_t fork = nullptr, join = nullptr;
   Tuning tune;                               // launch choices by batch size (loam_set_tuning)
+  // tune.graph: the batch step captured once as a HIP graph (for this P / these buffers) and replayed
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t graph_exec = nullptr;
+  int graph_P = 0;
+  void drop_graph() {
+    if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+    if (graph) (void)hipGraphDestroy(graph);
+    graph_exec = nullptr;
+    graph = nullptr;
+    graph_P = 0;
+  }
 };
 
 namespace {
@@ -270,6 +281,7 @@ void loam_destroy(loam_ctx* x) {
   for (auto& e : x->ev)
     if (e) (void)hipEventDestroy(e);
   if (x->st2) (void)hipStreamSynchronize(x->st2);
+  x->drop_graph();
   if (x->fork) (void)hipEventDestroy(x->fork);
   if (x->join) (void)hipEventDestroy(x->join);
   if (x->st2) (void)hipStreamDestroy(x->st2);
@@ -306,6 +318,8 @@ int loam_set_tuning(loam_ctx* x, const char* key, long long value) {
   Tuning t = x->tune;
   if (!t.set(key, value)) return fail(LOAM_E_INVAL, std::string("unknown tuning key or value out of range: ") + key);
   x->tune = t;
+  if (x->st) (void)hipStreamSynchronize(x->st);
+  x->drop_graph();  // (captured with the old choices)
   x->od1.tune = x->odb.tune = t;
   x->mp1.tune = x->mpb.tune = t;
   return LOAM_OK;
@@ -737,6 +751,7 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
   if ((int)n != x->P) {
     HIP_TRY(hipStreamSynchronize(x->st));
     if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
+    x->drop_graph();  // (its kernels' arguments name the old buffers)
     sr_free(x->srb);
     od_free(x->odb);
     mp_free(x->mpb);
@@ -769,18 +784,20 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
   return LOAM_OK;
 }
 
-int loam_batch_run(loam_ctx* x) {
-  if (!x || x->P == 0) return fail(LOAM_E_INVAL, "no batch uploaded");
-  HIP_TRY(hipSetDevice(x->device));
+namespace {
+// one batch step's device work on x->st (+ x->st2 for mapping frame 1); timing events only when
+// `events` (a captured graph records none: its stage times are not split)
+hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   const int P = x->P;
   OdBuffers& o = x->odb;
-  Prof* pf = x->prof.on ? &x->prof : nullptr;
-  HIP_TRY(hipEventRecord(x->ev[0], x->st));
+  hipError_t e = hipSuccess;
+  auto T = [&](hipError_t r) { if (e == hipSuccess) e = r; };
+  if (events) T(hipEventRecord(x->ev[0], x->st));
   x->prof.begin(x->st);
   sr_launch(x->srb, sr_params(x), x->st, pf);
-  HIP_TRY(hipEventRecord(x->ev[1], x->st));
-  HIP_TRY(hipMemsetAsync(o.state, 0, (size_t)P * kOdStateFloats * sizeof(float), x->st));
-  HIP_TRY(hipMemsetAsync(o.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st));
+  if (events) T(hipEventRecord(x->ev[1], x->st));
+  T(hipMemsetAsync(o.state, 0, (size_t)P * kOdStateFloats * sizeof(float), x->st));
+  T(hipMemsetAsync(o.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st));
   const FeatView fprev = feat_view(x->srb, 0, 2), fcur = feat_view(x->srb, 1, 2);
   // odometry seeded from prev as a solved zero-increment frame, then one loop body on cur
   hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fprev, 0, 1, 1);
@@ -793,24 +810,57 @@ int loam_batch_run(loam_ctx* x) {
   // keeps one stream so that its per-kernel event times stay attributable.
   const bool overlap = x->st2 && !pf;
   if (overlap) {
-    HIP_TRY(hipEventRecord(x->fork, x->st));
-    HIP_TRY(hipStreamWaitEvent(x->st2, x->fork, 0));
+    T(hipEventRecord(x->fork, x->st));
+    T(hipStreamWaitEvent(x->st2, x->fork, 0));
     mp_batch_frame1(x->mpb, o, x->st2, nullptr);
-    HIP_TRY(hipEventRecord(x->join, x->st2));
+    T(hipEventRecord(x->join, x->st2));
   }
   od_solve(o, fcur, 0, x->st, pf);
   hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, 1, 2, 1);
   x->prof.mark("k_od_end");
-  HIP_TRY(hipEventRecord(x->ev[2], x->st));
+  if (events) T(hipEventRecord(x->ev[2], x->st));
   // mapping: (frame 1 unless overlapped) then cur with the odometry pose
   if (overlap) {
-    HIP_TRY(hipStreamWaitEvent(x->st, x->join, 0));
+    T(hipStreamWaitEvent(x->st, x->join, 0));
   } else {
     mp_batch_frame1(x->mpb, o, x->st, pf);
   }
   mp_batch_frame2(x->mpb, o, x->st, pf);
+  if (events) T(hipEventRecord(x->ev[3], x->st));
+  T(hipGetLastError());
+  return e;
+}
+}  // namespace
+
+int loam_batch_run(loam_ctx* x) {
+  if (!x || x->P == 0) return fail(LOAM_E_INVAL, "no batch uploaded");
+  HIP_TRY(hipSetDevice(x->device));
+  Prof* pf = x->prof.on ? &x->prof : nullptr;
+  if (!x->tune.graph || pf) {
+    HIP_TRY(batch_enqueue(x, pf, true));
+    return LOAM_OK;
+  }
+  // graph replay: captured on the first call for this batch (the kernels' arguments are the
+  // batch's buffers, which stay put until the next loam_batch_upload of another size)
+  if (!x->graph_exec || x->graph_P != x->P) {
+    x->drop_graph();
+    HIP_TRY(hipStreamBeginCapture(x->st, hipStreamCaptureModeThreadLocal));
+    const hipError_t ce = batch_enqueue(x, nullptr, false);
+    hipGraph_t g = nullptr;
+    const hipError_t ee = hipStreamEndCapture(x->st, &g);
+    if (ce != hipSuccess || ee != hipSuccess) {
+      if (g) (void)hipGraphDestroy(g);
+      return fail(LOAM_E_HIP, std::string("batch graph capture: ") + hipGetErrorString(ce != hipSuccess ? ce : ee));
+    }
+    x->graph = g;
+    HIP_TRY(hipGraphInstantiate(&x->graph_exec, g, nullptr, nullptr, 0));
+    x->graph_P = x->P;
+  }
+  HIP_TRY(hipEventRecord(x->ev[0], x->st));
+  HIP_TRY(hipEventRecord(x->ev[1], x->st));
+  HIP_TRY(hipEventRecord(x->ev[2], x->st));
+  HIP_TRY(hipGraphLaunch(x->graph_exec, x->st));
   HIP_TRY(hipEventRecord(x->ev[3], x->st));
-  HIP_TRY(hipGetLastError());
   return LOAM_OK;
 }
 

@@ -49,6 +49,7 @@ struct Tuning {
   int nn_wg = 0;           // k_mp_nn workgroups per problem (0: one pass over a VLP-16 stack)
   int fit_wg = 0;          // k_mp_fit workgroups per problem (0: likewise)
   int nnfit_max = 0;       // k_mp_nnfit (5-NN + fit in one launch per iteration) for P <= this
+  int graph = 0;           // loam_batch_run replays the step as a captured HIP graph
   // key = value (loam_set_tuning); false for an unknown key or a value out of range
   bool set(const char* key, long long v) {
     struct K { const char* n; int* f; long long lo, hi; };
@@ -58,7 +59,8 @@ struct Tuning {
                     {"nn_lanes", &nn_lanes, 1, 4}, {"nn_lanes_maxp", &nn_lanes_maxp, 0, 1 << 20},
                     {"od_assoc_wg", &od_assoc_wg, 1, 1024}, {"nn_lds", &nn_lds, 0, 1},
                     {"od_rows_deep_max", &od_rows_deep_max, 0, 1 << 20}, {"nn_wg", &nn_wg, 0, 4096},
-                    {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20}};
+                    {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20},
+                    {"graph", &graph, 0, 1}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {
         if (v < k.lo || v > k.hi) return false;

@@ -215,7 +215,8 @@ def _share_run(loam, sg, **tune):
     e = loam.Engine()
     e.set_tuning(**tune)
     e.batch_upload(prevs, curs)
-    e.batch_run()
+    for _ in range(2 if tune.get("graph") else 1):  # (a graph: its capture, then a replay)
+        e.batch_run()
     od, aft, st = e.batch_download()
     e.close()
     return od, aft, st
@@ -234,6 +235,7 @@ def _share_run(loam, sg, **tune):
     {"od_rows_deep_max": 128, "od_fused_max": 128},
     {"nnfit_max": 128},                      # k_mp_nnfit<true>: 5-NN + fit + rows + step in one launch
     {"nnfit_max": 128, "mp_fused_max": 0},   # k_mp_nnfit<false> + k_mp_iter
+    {"graph": 1},                            # the step captured as a HIP graph and replayed
 ], ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_launch_choices_at_8gpu_share(loam, oc, sg, tune):
     """every launch shape the engine can pick by batch size (include/loam/loam.h loam_set_tuning),
