@@ -83,10 +83,14 @@ def kernel_bytes(st):
         "k_mp_fit": 129 * st["mp_stack_iters"] + 144 * st["mp_fits"],
         # per query-iteration: accept flag, stack point and coefficient read back for JtJ
         "k_mp_iter": 33 * st["mp_stack_iters"],
+        # the search and the fit in one launch: k_mp_nn's and k_mp_fit's bytes less the fit's read of
+        # the 5-NN the search just found (32 B per query-iteration, kept in registers)
+        "k_mp_nnfit": (80 + 129 - 32) * st["mp_stack_iters"] + 8 * st["mp_nn_cells"] + 16 * st["mp_nn_candidates"]
+                      + 144 * st["mp_fits"],
     }
 
 
-SEARCH_KERNELS = ("k_mp_nn", "k_od_assoc")
+SEARCH_KERNELS = ("k_mp_nn", "k_mp_nnfit", "k_od_assoc")
 
 
 def algorithmic_bytes(st):
@@ -97,6 +101,8 @@ def algorithmic_bytes(st):
     Last point once (16 B (C + S), B_OD)."""
     alg = dict(kernel_bytes(st))
     alg["k_mp_nn"] = 96 * st["mp_stack_iters"]
+    # k_mp_nnfit: the search's 96 B plus the fit's own bytes (k_mp_fit's less the 5-NN read back)
+    alg["k_mp_nnfit"] = (96 + 129 - 32) * st["mp_stack_iters"] + 144 * st["mp_fits"]
     alg["k_od_assoc"] = 16 * st["od_assoc_points"]
     return alg
 
@@ -104,6 +110,7 @@ def algorithmic_bytes(st):
 # what bounds each kernel in practice: the roofline is priced against HBM, but the
 # search kernels are limited by dependent gathers, not bandwidth
 LIMITED_BY = {"k_mp_nn": "latency (dependent gathers)", "k_od_assoc": "latency (dependent gathers)",
+              "k_mp_nnfit": "latency (dependent gathers, then the fit's VALU)",
               "k_sr_select": "latency (serial greedy picks)", "k_mp_fit": "latency (gathers + VALU)"}
 
 

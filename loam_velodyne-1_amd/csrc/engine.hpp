@@ -40,7 +40,9 @@ struct Tuning {
   int od_lm_max = 0;       //   for od_lm_min <= P <= od_lm_max
   int od_fused_max = 0;    // k_od_rows<true> (step in the last workgroup) for P <= this, else + k_od_step
   int mp_small_max = 4;    // k_mp_lm_small (5-NN + fit + rows + step in one launch) for P <= this
-  int mp_fused_max = 128;  // k_mp_fit<true> (rows + step in its last workgroup) for P <= this, else + k_mp_iter
+  int mp_fused_max = 0;    // the fit kernel (k_mp_fit<true> / k_mp_nnfit<true>) adds the rows and runs the
+                           // step in its last workgroup for P <= this, else k_mp_iter (round 4: with
+                           // k_mp_nnfit the separate k_mp_iter measured faster at 128 and 1024)
   int nn_lanes = 1;        // lanes per query of the batch 5-NN (1, 2, 4) ...
   int nn_lanes_maxp = 256; //   for P <= this
   int od_assoc_wg = 64;    // k_od_assoc query waves (workgroups) per problem (batches, P >= 64)
@@ -48,7 +50,8 @@ struct Tuning {
   int od_rows_deep_max = 0;  // k_od_rows with 8 (not 2) stored rows' loads in flight for P <= this
   int nn_wg = 0;           // k_mp_nn workgroups per problem (0: one pass over a VLP-16 stack)
   int fit_wg = 0;          // k_mp_fit workgroups per problem (0: likewise)
-  int nnfit_max = 0;       // k_mp_nnfit (5-NN + fit in one launch per iteration) for P <= this
+  int nnfit_max = 1 << 20; // k_mp_nnfit (5-NN + fit in one launch per iteration) for P <= this (round 4:
+                           // 3.32 -> 3.26-3.27 ms/step at 128, 16.02 -> 15.94 at 1024 with k_mp_iter)
   int graph = 0;           // loam_batch_run replays the step as a captured HIP graph
   // key = value (loam_set_tuning); false for an unknown key or a value out of range
   bool set(const char* key, long long v) {
