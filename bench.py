@@ -466,6 +466,7 @@ def main(argv=None):
     ap.add_argument("--dense-cpu-sample", type=int, default=2)
     ap.add_argument("--tune", action="append", default=[], help="key=value launch choice (loam_set_tuning), repeatable")
     ap.add_argument("--share-only", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--dense-only", type=int, default=0, help="run only the config-5 batched leg (profiling)")
     argv = sys.argv[1:] if argv is None else argv
     args = ap.parse_args(argv)
     tune = parse_tune(args.tune)
@@ -478,6 +479,13 @@ def main(argv=None):
         el = timed(e8, args.steps, args.warmup, None, "cpu")
         e8.close()
         print(json.dumps({"problems": B8, "value": B8 * args.steps / el, "ms_per_step": el / args.steps * 1e3}))
+        return
+
+    if args.dense_only:  # the config-5 batched leg alone (rocprof passes of tools/profile.sh)
+        loam = importlib.import_module("loam_velodyne-1_amd")
+        sg = importlib.import_module("loam_velodyne-1_amd.synthgen")
+        print(json.dumps(dense_batch_leg(loam, sg, args.dense_batch, args.dense_steps, 2, args.profile_steps,
+                                         args.dense_cpu_sample if args.cpu_sample > 0 else 0, 3)))
         return
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
