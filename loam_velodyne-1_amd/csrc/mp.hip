@@ -1504,12 +1504,12 @@ __global__ __launch_bounds__(kNnLdsThreads) void k_mp_nn_lds(MpBuffers b) {
 // the fused step of one-wave workgroups (k_mp_fit<true>, k_mp_nnfit<true>): the wave's row sums as
 // this workgroup's partial (write-through), and the last workgroup of the instance to arrive sums
 // the G partials in workgroup order and runs the step
-LOAM_D void mp_partial_and_step(const MpBuffers& b, int p, int wg, int G, double (&acc)[28]) {
+// red: the wave's sums reduce-scattered (wave_reduce_scatter_28: lanes 2v, 2v+1 hold value v)
+LOAM_D void mp_store_partial_and_step(const MpBuffers& b, int p, int wg, int G, double red) {
   static_assert(kMpFitThreads == 64, "one wave per workgroup: the wave's sums are the partial");
   const int lane = lane_id();
-  wave_reduce_scatter_28(acc);  // lanes 2v, 2v+1: the sum of value v
   if ((lane & 1) == 0 && (lane >> 1) < 28)
-    store_partial(&b.part[((size_t)p * kMpFitGridMax + wg) * 28 + (lane >> 1)], acc[0]);
+    store_partial(&b.part[((size_t)p * kMpFitGridMax + wg) * 28 + (lane >> 1)], red);
   __shared__ int sh_last;
   __shared__ double tot[28];
   __shared__ MpStepScratch sh;
@@ -1545,6 +1545,10 @@ LOAM_D void mp_partial_and_step(const MpBuffers& b, int p, int wg, int G, double
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   if (lane == 0) b.done[p] = 0;
   mp_step(b, p, tot, sh);
+}
+LOAM_D void mp_partial_and_step(const MpBuffers& b, int p, int wg, int G, double (&acc)[28]) {
+  wave_reduce_scatter_28(acc);  // lanes 2v, 2v+1: the sum of value v
+  mp_store_partial_and_step(b, p, wg, G, acc[0]);
 }
 
 template <bool FUSED>
@@ -1600,7 +1604,7 @@ __global__ __launch_bounds__(kMpFitThreads) void k_mp_fit(MpBuffers b) {
 // begin).  Same query -> lane mapping and row order as k_mp_fit, so the sums are k_mp_fit's.
 // FUSED: the partial + last-workgroup step of k_mp_fit<true>.  COUNT: the work counters.
 template <bool FUSED, bool COUNT>
-__global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(FUSED ? 2 : 4))) void k_mp_nnfit(MpBuffers b) {
+__global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(FUSED ? 3 : 4))) void k_mp_nnfit(MpBuffers b) {
   constexpr int NT = kMpFitThreads;
   static_assert(NT == 64, "the list / scratch sharing needs one wave per workgroup");
   const XcdBlock blk = xcd_block();
@@ -1618,14 +1622,14 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(F
   const MpTrig tg = mp_trig_of(r);
   float* jw = (float*)lds + tid * 27;
   int nfits = 0, work = 0;
-  double acc[FUSED ? 28 : 1];
-  if constexpr (FUSED) {
-#pragma unroll
-    for (int k = 0; k < 28; ++k) acc[k] = 0.0;
-  }
+  // FUSED: the rows of each pass over the queries are reduce-scattered over the wave at once (no
+  // 28 fp64 sums live across the search), the passes' sums added in pass order (one pass per lane
+  // for a VLP-16 stack: the same sums as k_mp_fit<true>)
+  double red = 0.0;
   for (int q0 = blk.x * NT; q0 < nq; q0 += gridDim.x * NT) {  // (wave-uniform trip count)
     const int q = q0 + tid;
-    float4 sel = make_float4(0, 0, 0, 0);
+    float4 sel = make_float4(0, 0, 0, 0), row_o = sel, row_c = sel;
+    bool row_ok = false;
     Top5 t;
     if (q < nq) mp_nn_query<NT, 1, kNnListCap>(b, c, q, nsc, first, r, lds + tid, sel, t, work);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1641,8 +1645,19 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(F
       mp_fit_query(b, p, q, nsc, first, n0, n1, sel, jw, nfits, cf, ok);
       qok[q] = (int8_t)ok;
       qcf[q] = cf;
-      if constexpr (FUSED)
-        if (ok) mp_row_accum(tg, o, cf, acc);
+      if constexpr (FUSED) {
+        row_ok = ok != 0;
+        row_o = o;
+        row_c = cf;
+      }
+    }
+    if constexpr (FUSED) {  // (outside the branch: every lane takes part in the shuffles)
+      double acc[28];
+#pragma unroll
+      for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+      if (row_ok) mp_row_accum(tg, row_o, row_c, acc);
+      wave_reduce_scatter_28(acc);
+      red += acc[0];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();  // the fits' scratch is free before the next lists
@@ -1657,7 +1672,7 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(F
       atomicAdd(&ist[kMiNnCells], ncell);
     }
   }
-  if constexpr (FUSED) mp_partial_and_step(b, p, blk.x, (int)gridDim.x, acc);
+  if constexpr (FUSED) mp_store_partial_and_step(b, p, blk.x, (int)gridDim.x, red);
 }
 
 namespace {
