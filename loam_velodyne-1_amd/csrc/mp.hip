@@ -1677,7 +1677,7 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(F
 
 namespace {
 struct MpIterShared {
-  double red[kMpWaves][28];
+  double red[16][28];  // (up to 1024 threads)
   double tot[28];
   float trig[6];
   MpStepScratch step;
@@ -1686,7 +1686,9 @@ struct MpIterShared {
 
 // the normal equations of the accepted rows (:879-974) and the 6x6 step, one workgroup per
 // instance; rows = the accepted correspondences of this iteration, in stack order
-__global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
+// NT threads per instance: 256 for large batches, 1024 for small ones (a shorter row chain per lane)
+template <int NT>
+__global__ __launch_bounds__(NT) void k_mp_iter(MpBuffers b) {
   const int p = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan] || ist[kMiStop]) return;
@@ -1702,12 +1704,12 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
 #pragma unroll
   for (int k = 0; k < 28; ++k) acc[k] = 0.0;
   // four rows' loads in flight per step; the rows are still summed in the lane's q order
-  for (int q0 = tid; q0 < nq; q0 += 4 * kMpThreads) {  // :897-921
+  for (int q0 = tid; q0 < nq; q0 += 4 * NT) {  // :897-921
     int8_t okv[4];
     float4 ov[4], cv4[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int q = q0 + u * kMpThreads;
+      const int q = q0 + u * NT;
       okv[u] = q < nq ? qok[q] : (int8_t)0;
       ov[u] = q < nq ? stack[q < nsc ? q : b.capC + (q - nsc)] : make_float4(0, 0, 0, 0);
       cv4[u] = q < nq ? qcf[q] : make_float4(0, 0, 0, 0);
@@ -1744,7 +1746,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_iter(MpBuffers b) {
   __syncthreads();
   if (tid < 28) {
     double v = sh.red[0][tid];
-    for (int ww = 1; ww < kMpWaves; ++ww) v += sh.red[ww][tid];
+    for (int ww = 1; ww < NT / 64; ++ww) v += sh.red[ww][tid];
     sh.tot[tid] = v;
   }
   __syncthreads();
@@ -2410,7 +2412,8 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
       else hipLaunchKernelGGL((k_mp_nnfit<false, false>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
       mark("k_mp_nnfit");
       if (!fused) {
-        hipLaunchKernelGGL(k_mp_iter, dim3(P), dim3(kMpThreads), 0, st, b);
+        if (P <= b.tune.mp_iter_wide_max) hipLaunchKernelGGL(k_mp_iter<1024>, dim3(P), dim3(1024), 0, st, b);
+        else hipLaunchKernelGGL(k_mp_iter<kMpThreads>, dim3(P), dim3(kMpThreads), 0, st, b);
         mark("k_mp_iter");
       }
       continue;
@@ -2440,7 +2443,8 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     }
     hipLaunchKernelGGL(k_mp_fit<false>, dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
     mark("k_mp_fit");
-    hipLaunchKernelGGL(k_mp_iter, dim3(P), dim3(kMpThreads), 0, st, b);
+    if (P <= b.tune.mp_iter_wide_max) hipLaunchKernelGGL(k_mp_iter<1024>, dim3(P), dim3(1024), 0, st, b);
+    else hipLaunchKernelGGL(k_mp_iter<kMpThreads>, dim3(P), dim3(kMpThreads), 0, st, b);
     mark("k_mp_iter");
   }
   hipLaunchKernelGGL(k_mp_lm_end, dim3((P + 255) / 256), dim3(256), 0, st, b);

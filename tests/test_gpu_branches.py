@@ -237,6 +237,7 @@ def _share_run(loam, sg, **tune):
     {"od_rows_deep_max": 128, "od_fused_max": 128},
     {"mp_fused_max": 128},                   # k_mp_nnfit<true>: 5-NN + fit + rows + step in one launch
     {"graph": 1},                            # the step captured as a HIP graph and replayed
+    {"mp_iter_wide_max": 128},               # k_mp_iter<1024>
 ], ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_launch_choices_at_8gpu_share(loam, oc, sg, tune):
     """every launch shape the engine can pick by batch size (include/loam/loam.h loam_set_tuning),
