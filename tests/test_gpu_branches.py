@@ -226,8 +226,8 @@ def _share_run(loam, sg, **tune):
     {"od_fused_max": 128},                   # k_od_rows<true>: the step in the rows' last workgroup
     {"od_lm_max": 128},                      # k_od_lm: an association round in one workgroup per problem
     {"od_small_max": 128},                   # k_od_rows_small: a workgroup per (queries, stored iteration)
-    {"nnfit_max": 0, "mp_fused_max": 128},   # k_mp_nn + k_mp_fit<true> (round 3's shapes)
-    {"nnfit_max": 0},                        # k_mp_nn + k_mp_fit<false> + k_mp_iter
+    {"nnfit_max": 0},                        # k_mp_nn + k_mp_fit<true> (round 3's shapes)
+    {"nnfit_max": 0, "mp_fused_max": 0},     # k_mp_nn + k_mp_fit<false> + k_mp_iter
     {"mp_small_max": 128},                   # k_mp_lm_small: one launch per mapping iteration
     {"nnfit_max": 0, "nn_lanes": 2},         # k_mp_nn<., L>: L lanes per query, merged 5-lists
     {"nnfit_max": 0, "nn_lanes": 4},
@@ -235,9 +235,9 @@ def _share_run(loam, sg, **tune):
     {"nnfit_max": 0, "nn_lds": 1},           # k_mp_nn_lds: the workgroup's map cells staged in LDS
     {"od_rows_deep_max": 128},               # k_od_rows<., 8>: eight stored rows' loads in flight
     {"od_rows_deep_max": 128, "od_fused_max": 128},
-    {"mp_fused_max": 128},                   # k_mp_nnfit<true>: 5-NN + fit + rows + step in one launch
+    {"mp_fused_max": 0},                     # k_mp_nnfit<false> + k_mp_iter
     {"graph": 1},                            # the step captured as a HIP graph and replayed
-    {"mp_iter_wide_max": 128},               # k_mp_iter<1024>
+    {"mp_fused_max": 0, "mp_iter_wide_max": 128},  # k_mp_iter<1024>
 ], ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_launch_choices_at_8gpu_share(loam, oc, sg, tune):
     """every launch shape the engine can pick by batch size (include/loam/loam.h loam_set_tuning),
