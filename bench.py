@@ -459,7 +459,7 @@ def main(argv=None):
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--profile-steps", type=int, default=3)
     ap.add_argument("--stream-sweeps", type=int, default=220, help="config-3 streaming leg (0: skip)")
-    ap.add_argument("--stream-cpu-sweeps", type=int, default=60)
+    ap.add_argument("--stream-cpu-sweeps", type=int, default=220, help="CPU oracle over the same sweeps as the GPU legs")
     ap.add_argument("--latency-runs", type=int, default=50, help="config-2 warm latency leg (0: skip)")
     ap.add_argument("--dense-batch", type=int, default=64, help="config-5 batched HDL-64E leg: problems (0: skip)")
     ap.add_argument("--dense-steps", type=int, default=5)
