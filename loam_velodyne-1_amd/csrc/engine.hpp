@@ -54,6 +54,7 @@ struct Tuning {
                            // 3.32 -> 3.26-3.27 ms/step at 128, 16.02 -> 15.94 at 1024 with k_mp_iter)
   int graph = 0;           // loam_batch_run replays the step as a captured HIP graph
   int mp_iter_wide_max = 0;  // k_mp_iter in 1024-thread (not 256) workgroups for P <= this
+  int vg_merge = 0;        // the cubes' VoxelGrid merges an old sorted prefix with the appended tail
   // key = value (loam_set_tuning); false for an unknown key or a value out of range
   bool set(const char* key, long long v) {
     struct K { const char* n; int* f; long long lo, hi; };
@@ -64,7 +65,8 @@ struct Tuning {
                     {"od_assoc_wg", &od_assoc_wg, 1, 1024}, {"nn_lds", &nn_lds, 0, 1},
                     {"od_rows_deep_max", &od_rows_deep_max, 0, 1 << 20}, {"nn_wg", &nn_wg, 0, 4096},
                     {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20},
-                    {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20}};
+                    {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20},
+                    {"vg_merge", &vg_merge, 0, 1}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {
         if (v < k.lo || v > k.hi) return false;

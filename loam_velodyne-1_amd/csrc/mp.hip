@@ -260,6 +260,7 @@ __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
   const int nl = j.list ? *j.list_n : j.nseg;
   for (int li = blockIdx.x; li < nl; li += gridDim.x) {
     const int s = j.list ? j.list[li] : li;
+    if (j.skip && j.skip[s]) continue;  // (written by k_vg_merge; only the cascade's first kernel sees it)
     const int b0 = j.begin[s], b1 = j.end[s], n = b1 - b0;
     if (n <= 0) {
       if (tid == 0) j.out_count[s] = 0;
@@ -643,6 +644,168 @@ __global__ __launch_bounds__(NT) void k_vg_big(VgJob j) {
       outn += tot;
     }
     if (tid == 0) j.out_count[s] = outn;
+    __syncthreads();
+  }
+}
+
+// Incremental VoxelGrid of a cube segment (:1018-1036) whose first nold points are the cube's
+// previous VoxelGrid output and whose tail is this frame's appended points.  A VoxelGrid output
+// lists one point per voxel in voxel order; when the old points' voxel keys (under this segment's
+// bounding box: the order of absolute grid cells (k, j, i) does not depend on it) are strictly
+// increasing, the stable (voxel, position) sort of the whole segment is the merge of the old points
+// with the sorted tail, old first within a voxel (they precede the tail in input order).  So only the
+// tail is sorted (LDS bitonic, <= NEW points), and each output voxel sums its members in input
+// order: its old point, then its tail points — the same float sums as the full sort.  Segments whose
+// old keys are not strictly increasing (a cube appended to without a VoxelGrid since, or a mean
+// rounded into a neighbouring voxel), whose keys exceed the cascade's 24 sorted bits, or whose box
+// is "too small" are left to the cascade (skip[s] = 0).
+constexpr int kVgMergeMin = 2048, kVgMergeNew = 4096;
+template <int NT, int NEW>
+__global__ __launch_bounds__(NT) void k_vg_merge(VgJob j) {
+  static_assert((NEW & (NEW - 1)) == 0 && NEW % NT == 0, "bitonic sort / scan layout");
+  __shared__ uint64_t nk[NEW];      // tail (key << 32 | tail position), sorted
+  __shared__ uint32_t nhk[NEW];     // keys of the tail's voxels that hold no old point, ascending
+  __shared__ uint16_t nhp[NEW];     //   and their first entry in nk
+  __shared__ float fsc[16];
+  __shared__ int isc[24];
+  const int tid = threadIdx.x;
+  const int nl = *j.mlist_n;
+  for (int li = blockIdx.x; li < nl; li += gridDim.x) {
+    const int s = j.mlist[li];
+    const int b0 = j.begin[s], n = j.end[s] - b0, nold = j.nold[s], nnew = n - nold;
+    const float4* in = j.in + b0;
+    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+    for (int i = tid; i < n; i += NT) {
+      const float4 a = in[i];
+      mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
+      mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
+    }
+    for (int d = 0; d < 3; ++d) {
+      mn[d] = block_reduce<NT>(mn[d], fsc, [](float a, float c) { return fminf(a, c); });
+      mx[d] = block_reduce<NT>(mx[d], fsc, [](float a, float c) { return fmaxf(a, c); });
+    }
+    const float inv = 1.0f / j.leaf[s];
+    if (vg_leaf_too_small(mn, mx, inv)) {  // (the cascade copies it)
+      if (tid == 0) j.skip[s] = 0;
+      continue;
+    }
+    const int m0 = (int)floorf(mn[0] * inv), m1 = (int)floorf(mn[1] * inv), m2 = (int)floorf(mn[2] * inv);
+    const int divx = (int)floorf(mx[0] * inv) - m0 + 1, divy = (int)floorf(mx[1] * inv) - m1 + 1;
+    const uint32_t mul1 = (uint32_t)divx, mul2 = (uint32_t)(divx * divy);
+    auto key_of = [&](const float4& a) {
+      const int i0 = (int)(floorf(a.x * inv) - (float)m0);
+      const int i1 = (int)(floorf(a.y * inv) - (float)m1);
+      const int i2 = (int)(floorf(a.z * inv) - (float)m2);
+      return (uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2;
+    };
+    // the old keys (global scratch, the segment's range of the sort arrays) and their order check
+    uint32_t* K = j.keys + b0;
+    bool bad = false;
+    for (int i = tid; i < nold; i += NT) {
+      const uint32_t k = key_of(in[i]);
+      K[i] = k;
+      bad |= k >= (1u << 24);
+    }
+    // the tail's (key, position), padded to a power of two for the sort
+    int P2 = 1;
+    while (P2 < nnew) P2 <<= 1;
+    for (int t = tid; t < P2; t += NT) {
+      uint64_t e = ~0ull;
+      if (t < nnew) {
+        const uint32_t k = key_of(in[nold + t]);
+        bad |= k >= (1u << 24);
+        e = ((uint64_t)k << 32) | (uint32_t)t;
+      }
+      nk[t] = e;
+    }
+    __syncthreads();
+    for (int i = tid + 1; i < nold; i += NT) bad |= K[i] <= K[i - 1];
+    if (__syncthreads_or(bad)) {
+      if (tid == 0) j.skip[s] = 0;
+      continue;
+    }
+    if (P2 > 1) block_bitonic_sort<NT>(nk, P2);
+    __syncthreads();
+    // lower_bound of key k in the old keys (global, ascending)
+    auto old_lb = [&](uint32_t k) {
+      int lo = 0, hi = nold;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (K[mid] < k) lo = mid + 1; else hi = mid;
+      }
+      return lo;
+    };
+    // the tail's voxels that hold no old point, compacted in key order (NEW / NT entries per thread)
+    constexpr int PT = NEW / NT;
+    int fl[PT], cntf = 0;
+#pragma unroll
+    for (int u = 0; u < PT; ++u) {
+      const int t = tid * PT + u;
+      fl[u] = 0;
+      if (t < nnew) {
+        const uint32_t k = (uint32_t)(nk[t] >> 32);
+        if (t == 0 || (uint32_t)(nk[t - 1] >> 32) != k) {
+          const int at = old_lb(k);
+          fl[u] = (at == nold || K[at] != k) ? 1 : 0;
+        }
+      }
+      cntf += fl[u];
+    }
+    int m = 0;
+    int r = block_excl_scan<NT>(cntf, isc, m);
+#pragma unroll
+    for (int u = 0; u < PT; ++u)
+      if (fl[u]) {
+        const int t = tid * PT + u;
+        nhk[r] = (uint32_t)(nk[t] >> 32);
+        nhp[r] = (uint16_t)t;
+        ++r;
+      }
+    __syncthreads();
+    // sums of a voxel's tail members from tail entry e on (sorted: input order within the voxel)
+    auto add_tail = [&](int e, uint32_t k, float& sx, float& sy, float& sz, float& si, int& c) {
+      for (; e < nnew && (uint32_t)(nk[e] >> 32) == k; ++e) {
+        const float4 a = in[nold + (int)(uint32_t)nk[e]];
+        sx += a.x; sy += a.y; sz += a.z; si += a.w;
+        ++c;
+      }
+    };
+    // old voxels: slot = i + (tail-only voxels before it); members = the old point, then its tail run
+    for (int i = tid; i < nold; i += NT) {
+      const uint32_t k = K[i];
+      int lo = 0, hi = m;  // tail-only voxels with a smaller key
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (nhk[mid] < k) lo = mid + 1; else hi = mid;
+      }
+      const int slot = i + lo;
+      int e0 = 0, e1 = nnew;  // first tail entry with key >= k
+      while (e0 < e1) {
+        const int mid = (e0 + e1) >> 1;
+        if ((uint32_t)(nk[mid] >> 32) < k) e0 = mid + 1; else e1 = mid;
+      }
+      const float4 a = in[i];
+      float sx = 0, sy = 0, sz = 0, si = 0;
+      sx += a.x; sy += a.y; sz += a.z; si += a.w;
+      int c = 1;
+      add_tail(e0, k, sx, sy, sz, si, c);
+      const float cnt = (float)c;
+      j.out[b0 + slot] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+    }
+    // tail-only voxels: slot = r + (old voxels before it)
+    for (int q = tid; q < m; q += NT) {
+      const uint32_t k = nhk[q];
+      const int slot = q + old_lb(k);
+      float sx = 0, sy = 0, sz = 0, si = 0;
+      int c = 0;
+      add_tail(nhp[q], k, sx, sy, sz, si, c);
+      const float cnt = (float)c;
+      j.out[b0 + slot] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+    }
+    if (tid == 0) {
+      j.out_count[s] = nold + m;
+      j.skip[s] = 1;
+    }
     __syncthreads();
   }
 }
@@ -1863,7 +2026,7 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
 // host found IMU data for the odometry stamp
 __global__ void k_mp_lm_end(MpBuffers b) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p == 0) { b.vg_cnt[0] = 0; b.vg_cnt[1] = 0; b.vg_cnt[2] = 0; }  // (vg_cubes' lists)
+  if (p == 0) { b.vg_cnt[0] = 0; b.vg_cnt[1] = 0; b.vg_cnt[2] = 0; b.vg_cnt[3] = 0; }  // (vg_cubes' lists)
   if (p >= b.P) return;
   const int* ist = b.istate + (size_t)p * kMpStateInts;
   if (!ist[kMiLmRan]) return;
@@ -2080,10 +2243,11 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_vseg(MpBuffers b) {
   const int* ac = b.app_cnt + (size_t)p * kCubeNum * 2;
   __shared__ int scratch[16];
   const int kind = tid / kMaxValid, v = tid % kMaxValid;
-  int n = 0;
+  int n = 0, nold = 0;
   if (tid < 2 * kMaxValid && v < nv) {
     const int ind = b.valid[(size_t)p * kMaxValid + v];
-    n = slots[ind * 4 + 1 + 2 * kind] + ac[ind * 2 + kind];
+    nold = slots[ind * 4 + 1 + 2 * kind];
+    n = nold + ac[ind * 2 + kind];
   }
   int tot;
   const int ex = block_excl_scan<kMpThreads>(n, scratch, tot);
@@ -2098,8 +2262,16 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_vseg(MpBuffers b) {
     b.vseg_e[sidx] = base + (over ? 0 : n);
     b.vseg_leaf[sidx] = kind == 0 ? 0.2f : 0.4f;
     if (over && n > 0) b.istate[(size_t)p * kMpStateInts + kMiErr] |= ERR_CAP_MAP;
-    if (over || n == 0) b.vseg_cnt[sidx] = 0;  // (not in the VoxelGrid's list)
-    else b.vg_lin[atomicAdd(b.vg_cnt + 2, 1)] = sidx;
+    b.vseg_nold[sidx] = nold;
+    b.vseg_skip[sidx] = 0;
+    if (over || n == 0) {
+      b.vseg_cnt[sidx] = 0;  // (not in the VoxelGrid's list)
+    } else {
+      b.vg_lin[atomicAdd(b.vg_cnt + 2, 1)] = sidx;
+      // long segments with a short appended tail: the incremental VoxelGrid may take them
+      if (b.tune.vg_merge && n > kVgMergeMin && nold > 0 && n - nold <= kVgMergeNew)
+        b.vg_mlist[atomicAdd(b.vg_cnt + 3, 1)] = sidx;
+    }
   }
 }
 
@@ -2313,7 +2485,10 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
   A(&b.vg_l0, (size_t)P * 2 * kMaxValid * sizeof(int));
   A(&b.vg_l1, (size_t)P * 2 * kMaxValid * sizeof(int));
   A(&b.vg_lin, (size_t)P * 2 * kMaxValid * sizeof(int));
-  A(&b.vg_cnt, 3 * sizeof(int));
+  A(&b.vg_cnt, 4 * sizeof(int));
+  A(&b.vg_mlist, (size_t)P * 2 * kMaxValid * sizeof(int));
+  A(&b.vseg_nold, (size_t)P * 2 * kMaxValid * sizeof(int));
+  A(&b.vseg_skip, (size_t)P * 2 * kMaxValid * sizeof(int));
   A(&b.reg, (size_t)P * b.capS * sizeof(float4));
   A(&b.part, (size_t)P * std::max(kMpSmallGrid, kMpFitGridMax) * 28 * sizeof(double));
   A(&b.rot, (size_t)P * 6 * sizeof(double));
@@ -2330,7 +2505,8 @@ void mp_free(MpBuffers& b) {
                   b.stack2, b.stack, b.nstack, b.from, b.hC_start, b.hS_start, b.hC_rec, b.hS_rec, b.h_fill, b.hC_T, b.hS_T,
                   b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.citems, b.nitems, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
-                  b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_l0, b.vg_l1, b.vg_lin, b.vg_cnt, b.reg, b.nreg, b.part, b.done, b.rot};
+                  b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_l0, b.vg_l1, b.vg_lin, b.vg_cnt, b.reg, b.nreg, b.part, b.done, b.rot,
+                  b.vg_mlist, b.vseg_nold, b.vseg_skip};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = MpBuffers();
@@ -2461,6 +2637,10 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   jv.out_count = b.vseg_cnt; jv.nseg = 2 * kMaxValid * P; jv.total = P * b.map_cap;
   // only the non-empty segments, listed by k_mp_vseg (k_mp_lm_end zeroed the counters)
   jv.list = b.vg_lin; jv.list_n = b.vg_cnt + 2; jv.zeroed = true;
+  if (b.tune.vg_merge) {  // long cube segments with a short tail first (k_vg_merge), the rest by the cascade
+    jv.nold = b.vseg_nold; jv.mlist = b.vg_mlist; jv.mlist_n = b.vg_cnt + 3; jv.skip = b.vseg_skip;
+    hipLaunchKernelGGL((k_vg_merge<1024, kVgMergeNew>), dim3(std::min(2 * kMaxValid * P, 1024)), dim3(1024), 0, st, jv);
+  }
   // 2 x 125 cube segments per instance, most of them small: batches start with the 2048-point
   // kernel (many workgroups per CU); a few instances with the 12288-point one (one launch)
   b.note(vg_run(jv, st, P <= 4 ? 12288 : 2048));

@@ -63,6 +63,13 @@ struct VgJob {
   const int* list_n = nullptr;
   int* big = nullptr;
   int* big_n = nullptr;
+  // incremental cube VoxelGrid (k_vg_merge): per segment the count of its leading points that are the
+  // cube's previous VoxelGrid output, the candidate list, and the per-segment "done" flags the
+  // cascade's first kernel skips
+  const int* nold = nullptr;
+  const int* mlist = nullptr;
+  const int* mlist_n = nullptr;
+  int* skip = nullptr;
 };
 
 struct MpBuffers {
@@ -108,7 +115,10 @@ struct MpBuffers {
   uint32_t *vg_k = nullptr, *vg_k2 = nullptr, *vg_v = nullptr, *vg_v2 = nullptr;
   int *vg_l0 = nullptr, *vg_l1 = nullptr;  // [P][2][kMaxValid] vg_run's segment lists
   int* vg_lin = nullptr;                   // [P][2][kMaxValid] the non-empty cube segments (k_mp_vseg)
-  int* vg_cnt = nullptr;                   // [3] the lists' lengths (vg_l0, vg_l1, vg_lin)
+  int* vg_cnt = nullptr;                   // [4] the lists' lengths (vg_l0, vg_l1, vg_lin, vg_mlist)
+  int* vg_mlist = nullptr;                 // [P][2][kMaxValid] cube segments k_vg_merge may take
+  int* vseg_nold = nullptr;                // [P][2][kMaxValid] leading points from the cube's last DS
+  int* vseg_skip = nullptr;                // [P][2][kMaxValid] 1: k_vg_merge wrote the segment
   float4* reg = nullptr;      // [P][capS] registered full cloud
   double* part = nullptr;     // [P][kMpSmallGrid][28] k_mp_lm_small's per-workgroup JᵀJ | Jᵀb | rows
   int* done = nullptr;        // [P] its workgroups finished (the last one runs the step)

@@ -48,6 +48,24 @@ def test_config3_full220_device_chain(loam, sg):
     check_config3_full(traj)
 
 
+def test_config3_full220_vg_merge(loam, sg):
+    """the 220 sweeps through loam_chain_sweep with the incremental cube VoxelGrid (k_vg_merge: the
+    map grows, so its cubes' old sorted prefixes are long): every pose and registered cloud as the
+    golden run"""
+    e = loam.Engine(loam.default_config())
+    e.set_tuning(vg_merge=1)
+    traj = []
+    for k, sw in enumerate(sg.stream_sweeps(220, 1)):
+        rc, pub, od, aft, bef, reg = e.chain_sweep(sw, stamp=0.1 * k, registered=True)
+        if rc:
+            continue
+        rec = {"k": k, "pub": pub, "od": od}
+        if aft is not None:
+            rec.update(aft=aft, bef=bef, reg_n=int(reg.shape[0]), reg=digest(reg))
+        traj.append(rec)
+    check_config3_full(traj)
+
+
 def test_device_chain_surround_and_counters(loam, oc, sg):
     """loam_mapping_surround after loam_chain_sweep publishes what it publishes after the message
     calls, and the chain leaves the same per-call counters"""
