@@ -659,13 +659,14 @@ __global__ __launch_bounds__(NT) void k_vg_big(VgJob j) {
 // old keys are not strictly increasing (a cube appended to without a VoxelGrid since, or a mean
 // rounded into a neighbouring voxel), whose keys exceed the cascade's 24 sorted bits, or whose box
 // is "too small" are left to the cascade (skip[s] = 0).
-constexpr int kVgMergeMin = 2048, kVgMergeNew = 4096;
+// (segments beyond the cascade's LDS tiers, which k_vg_big would sort through global memory; the
+// LDS tiers measured faster than the merge on 2k-12k segments)
+constexpr int kVgMergeMin = 12288, kVgMergeNew = 8192;
 template <int NT, int NEW>
 __global__ __launch_bounds__(NT) void k_vg_merge(VgJob j) {
-  static_assert((NEW & (NEW - 1)) == 0 && NEW % NT == 0, "bitonic sort / scan layout");
+  static_assert((NEW & (NEW - 1)) == 0 && NEW % NT == 0 && NEW <= 65536, "bitonic sort / scan layout");
   __shared__ uint64_t nk[NEW];      // tail (key << 32 | tail position), sorted
-  __shared__ uint32_t nhk[NEW];     // keys of the tail's voxels that hold no old point, ascending
-  __shared__ uint16_t nhp[NEW];     //   and their first entry in nk
+  __shared__ uint16_t nhp[NEW];     // first entry in nk of each tail voxel that holds no old point
   __shared__ float fsc[16];
   __shared__ int isc[24];
   const int tid = threadIdx.x;
@@ -757,7 +758,6 @@ __global__ __launch_bounds__(NT) void k_vg_merge(VgJob j) {
     for (int u = 0; u < PT; ++u)
       if (fl[u]) {
         const int t = tid * PT + u;
-        nhk[r] = (uint32_t)(nk[t] >> 32);
         nhp[r] = (uint16_t)t;
         ++r;
       }
@@ -776,7 +776,7 @@ __global__ __launch_bounds__(NT) void k_vg_merge(VgJob j) {
       int lo = 0, hi = m;  // tail-only voxels with a smaller key
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (nhk[mid] < k) lo = mid + 1; else hi = mid;
+        if ((uint32_t)(nk[nhp[mid]] >> 32) < k) lo = mid + 1; else hi = mid;
       }
       const int slot = i + lo;
       int e0 = 0, e1 = nnew;  // first tail entry with key >= k
@@ -794,7 +794,7 @@ __global__ __launch_bounds__(NT) void k_vg_merge(VgJob j) {
     }
     // tail-only voxels: slot = r + (old voxels before it)
     for (int q = tid; q < m; q += NT) {
-      const uint32_t k = nhk[q];
+      const uint32_t k = (uint32_t)(nk[nhp[q]] >> 32);
       const int slot = q + old_lb(k);
       float sx = 0, sy = 0, sz = 0, si = 0;
       int c = 0;
