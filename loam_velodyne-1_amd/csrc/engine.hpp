@@ -55,6 +55,8 @@ struct Tuning {
   int graph = 0;           // loam_batch_run replays the step as a captured HIP graph
   int mp_iter_wide_max = 0;  // k_mp_iter in 1024-thread (not 256) workgroups for P <= this
   int vg_merge = 0;        // the cubes' VoxelGrid merges an old sorted prefix with the appended tail
+  int mp_late_iter = 0;    // mapping iterations >= this (0: none) take k_mp_nn<mp_late_lanes> + k_mp_fit
+  int mp_late_lanes = 4;
   // key = value (loam_set_tuning); false for an unknown key or a value out of range
   bool set(const char* key, long long v) {
     struct K { const char* n; int* f; long long lo, hi; };
@@ -66,11 +68,12 @@ struct Tuning {
                     {"od_rows_deep_max", &od_rows_deep_max, 0, 1 << 20}, {"nn_wg", &nn_wg, 0, 4096},
                     {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20},
                     {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20},
-                    {"vg_merge", &vg_merge, 0, 1}};
+                    {"vg_merge", &vg_merge, 0, 1}, {"mp_late_iter", &mp_late_iter, 0, 1000},
+                    {"mp_late_lanes", &mp_late_lanes, 1, 4}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {
         if (v < k.lo || v > k.hi) return false;
-        if (k.f == &nn_lanes && v == 3) return false;
+        if ((k.f == &nn_lanes || k.f == &mp_late_lanes) && v == 3) return false;
         *k.f = (int)v;
         return true;
       }
