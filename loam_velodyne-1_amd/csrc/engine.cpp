@@ -800,7 +800,8 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   T(hipMemsetAsync(o.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st));
   const FeatView fprev = feat_view(x->srb, 0, 2), fcur = feat_view(x->srb, 1, 2);
   // odometry seeded from prev as a solved zero-increment frame, then one loop body on cur
-  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fprev, 0, 1, 1);
+  // (the full clouds' TransformToEnd happens in mapping's registration kernel, mp_batch_frame*)
+  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fprev, 0, 1, 0);
   x->prof.mark("k_od_end_seed");
   od_build_hashes(o, 0, x->st);
   x->prof.mark("k_hash_build_last");
@@ -812,20 +813,20 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   if (overlap) {
     T(hipEventRecord(x->fork, x->st));
     T(hipStreamWaitEvent(x->st2, x->fork, 0));
-    mp_batch_frame1(x->mpb, o, x->st2, nullptr);
+    mp_batch_frame1(x->mpb, o, fprev, x->st2, nullptr);
     T(hipEventRecord(x->join, x->st2));
   }
   od_solve(o, fcur, 0, x->st, pf);
-  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, 1, 2, 1);
+  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, 1, 2, 0);
   x->prof.mark("k_od_end");
   if (events) T(hipEventRecord(x->ev[2], x->st));
   // mapping: (frame 1 unless overlapped) then cur with the odometry pose
   if (overlap) {
     T(hipStreamWaitEvent(x->st, x->join, 0));
   } else {
-    mp_batch_frame1(x->mpb, o, x->st, pf);
+    mp_batch_frame1(x->mpb, o, fprev, x->st, pf);
   }
-  mp_batch_frame2(x->mpb, o, x->st, pf);
+  mp_batch_frame2(x->mpb, o, fcur, x->st, pf);
   if (events) T(hipEventRecord(x->ev[3], x->st));
   T(hipGetLastError());
   return e;

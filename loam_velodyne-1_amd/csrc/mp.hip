@@ -2412,8 +2412,27 @@ __global__ __launch_bounds__(256) void k_mp_register(MpBuffers b, MpInput in) {
   const int p = blockIdx.y;
   const loampose::MapRot r = rot_load(b, p);
   const int n = min(in.nfull[p * in.nfull_stride], b.capS);
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
-    b.reg[(size_t)p * b.capS + i] = loampose::point_to_map(r, in.full[(size_t)p * in.full_stride + i]);
+  if (in.end_mode) {  // odometry's TransformToEnd of the raw cloud first (k_od_end's, :875-891)
+    float t[6] = {0, 0, 0, 0, 0, 0};
+    loampose::Imu imu = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (in.end_mode == 2) {
+      const float* st = in.end_state + (size_t)p * kOdStateFloats;
+      for (int k = 0; k < 6; ++k) t[k] = st[k];
+      const float* q = st + kOdImu;
+      imu.pitchStart = q[0]; imu.yawStart = q[1]; imu.rollStart = q[2];
+      imu.pitchLast = q[3]; imu.yawLast = q[4]; imu.rollLast = q[5];
+      imu.shiftX = q[6]; imu.shiftY = q[7]; imu.shiftZ = q[8];
+      imu.veloX = q[9]; imu.veloY = q[10]; imu.veloZ = q[11];
+    }
+    const loampose::EndRot er = loampose::end_rot(t, imu);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+      const float4 a = loampose::transform_to_end(t, imu, er, in.full[(size_t)p * in.full_stride + i], in.end_mode == 1);
+      b.reg[(size_t)p * b.capS + i] = loampose::point_to_map(r, a);
+    }
+  } else {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+      b.reg[(size_t)p * b.capS + i] = loampose::point_to_map(r, in.full[(size_t)p * in.full_stride + i]);
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) b.nreg[p] = n;
 }
 
@@ -2907,34 +2926,36 @@ int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::s
 
 // frame 1 of the batch problem: reset, then prev (Last[0], fullEnd[0]) into the empty store at
 // the zero pose.  Reads only what the odometry seeding wrote, so it may run beside od_solve.
-void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof) {
+void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, const FeatView& fprev, hipStream_t st, Prof* prof) {
   b.note(mp_reset(b, st));
   if (prof) prof->mark("mp_reset");
   MpInput in;
-  in.corner = od.lastC; in.surf = od.lastS; in.full = od.fullEnd;
-  in.corner_stride = od.capC; in.surf_stride = od.capS; in.full_stride = od.capS;
-  in.ncorner = od.nlast + 0; in.nsurf = od.nlast + 1; in.nfull = od.nfullEnd + 0;
-  in.ncorner_stride = 4; in.nsurf_stride = 4; in.nfull_stride = 2;
+  in.corner = od.lastC; in.surf = od.lastS;
+  in.corner_stride = od.capC; in.surf_stride = od.capS;
+  in.ncorner = od.nlast + 0; in.nsurf = od.nlast + 1;
+  in.ncorner_stride = 4; in.nsurf_stride = 4;
+  // the full cloud: prev's raw one, TransformToEnd with the zero transform in k_mp_register
+  in.full = fprev.full; in.full_stride = fprev.full_stride;
+  in.nfull = fprev.nfull_p; in.nfull_stride = fprev.nfull_stride;
+  in.end_mode = 1;
   in.pose = nullptr; in.pose_stride = 0;
   mp_frame(b, in, st, prof, /*map_empty=*/true);
 }
 
 // frame 2: cur (Last[1], fullEnd[1]) with the odometry transformSum
-void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof) {
+void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, const FeatView& fcur, hipStream_t st, Prof* prof) {
   MpInput in;
   in.corner = od.lastC + (size_t)od.P * od.capC;
   in.surf = od.lastS + (size_t)od.P * od.capS;
-  in.full = od.fullEnd + (size_t)od.P * od.capS;
-  in.corner_stride = od.capC; in.surf_stride = od.capS; in.full_stride = od.capS;
-  in.ncorner = od.nlast + 2; in.nsurf = od.nlast + 3; in.nfull = od.nfullEnd + 1;
-  in.ncorner_stride = 4; in.nsurf_stride = 4; in.nfull_stride = 2;
+  in.corner_stride = od.capC; in.surf_stride = od.capS;
+  in.ncorner = od.nlast + 2; in.nsurf = od.nlast + 3;
+  in.ncorner_stride = 4; in.nsurf_stride = 4;
+  // the full cloud: cur's raw one, TransformToEnd with the solved transform in k_mp_register
+  in.full = fcur.full; in.full_stride = fcur.full_stride;
+  in.nfull = fcur.nfull_p; in.nfull_stride = fcur.nfull_stride;
+  in.end_state = od.state; in.end_mode = 2;
   in.pose = od.state + kOdSum; in.pose_stride = kOdStateFloats;
   mp_frame(b, in, st, prof);
-}
-
-void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof) {
-  mp_batch_frame1(b, od, st, prof);
-  mp_batch_frame2(b, od, st, prof);
 }
 
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err) {

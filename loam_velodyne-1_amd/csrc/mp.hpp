@@ -39,6 +39,11 @@ struct MpInput {
   int ncorner_stride, nsurf_stride, nfull_stride;
   const float* pose;   // transformSum of the odometry message (nullptr = zero pose)
   int pose_stride;
+  // the batch path: `full` is the raw ring-sorted cloud, and k_mp_register applies odometry's
+  // TransformToEnd itself (end_mode 1: zero transform, 2: the transform in end_state, OdBuffers
+  // state layout), so the full cloud is neither written to nor read back from fullEnd
+  const float* end_state = nullptr;
+  int end_mode = 0;
 };
 
 // segmented PCL VoxelGrid job (segment s: input in[begin[s] .. end[s]), output out[begin[s] ..))
@@ -162,9 +167,9 @@ int mp_stream_frame_dev(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum
 // /laser_cloud_surround of the last streaming frame (instance 0): its 5x5x5 cube neighbourhood
 // concatenated and VoxelGrid 0.2 (src/laserMapping.cpp:1038-1058)
 int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::string& err);
-void mp_batch_run(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof = nullptr);
-void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof = nullptr);
-void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, hipStream_t st, Prof* prof = nullptr);
+// fprev / fcur: the scan registration outputs whose full clouds the frames register
+void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, const FeatView& fprev, hipStream_t st, Prof* prof = nullptr);
+void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, const FeatView& fcur, hipStream_t st, Prof* prof = nullptr);
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err);
 
 }  // namespace loam
