@@ -54,7 +54,8 @@ struct Tuning {
                            // 3.32 -> 3.26-3.27 ms/step at 128, 16.02 -> 15.94 at 1024 with k_mp_iter)
   int graph = 0;           // loam_batch_run replays the step as a captured HIP graph
   int mp_iter_wide_max = 0;  // k_mp_iter in 1024-thread (not 256) workgroups for P <= this
-  int vg_merge = 0;        // the cubes' VoxelGrid merges an old sorted prefix with the appended tail
+  int vg_merge = 1;        // the cubes' VoxelGrid merges an old sorted prefix with the appended tail
+                           // (k_vg_merge; config 3's big cubes: 95 -> 50 us per mapping frame)
   int mp_late_iter = 0;    // mapping iterations >= this (0: none) take k_mp_nn<mp_late_lanes> + k_mp_fit
   int mp_late_lanes = 4;
   // key = value (loam_set_tuning); false for an unknown key or a value out of range

@@ -48,12 +48,12 @@ def test_config3_full220_device_chain(loam, sg):
     check_config3_full(traj)
 
 
-def test_config3_full220_vg_merge(loam, sg):
-    """the 220 sweeps through loam_chain_sweep with the incremental cube VoxelGrid (k_vg_merge: the
-    map grows, so its cubes' old sorted prefixes are long): every pose and registered cloud as the
-    golden run"""
+def test_config3_full220_no_vg_merge(loam, sg):
+    """the 220 sweeps through loam_chain_sweep without the incremental cube VoxelGrid (k_vg_merge,
+    the default, takes the growing map's big cubes; here the cascade sorts them): every pose and
+    registered cloud as the golden run"""
     e = loam.Engine(loam.default_config())
-    e.set_tuning(vg_merge=1)
+    e.set_tuning(vg_merge=0)
     traj = []
     for k, sw in enumerate(sg.stream_sweeps(220, 1)):
         rc, pub, od, aft, bef, reg = e.chain_sweep(sw, stamp=0.1 * k, registered=True)

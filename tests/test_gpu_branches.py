@@ -238,7 +238,7 @@ def _share_run(loam, sg, **tune):
     {"mp_fused_max": 0},                     # k_mp_nnfit<false> + k_mp_iter
     {"graph": 1},                            # the step captured as a HIP graph and replayed
     {"mp_fused_max": 0, "mp_iter_wide_max": 128},  # k_mp_iter<1024>
-    {"vg_merge": 1},                         # k_vg_merge: the cubes' old sorted prefix merged with the tail
+    {"vg_merge": 0},                         # the cube VoxelGrid cascade alone (no k_vg_merge)
 ], ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_launch_choices_at_8gpu_share(loam, oc, sg, tune):
     """every launch shape the engine can pick by batch size (include/loam/loam.h loam_set_tuning),
