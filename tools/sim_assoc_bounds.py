@@ -1,6 +1,8 @@
 """CPU simulation (numpy + the oracle) of the odometry association windows' first round on config-4
 problems: points the chunk walk visits per query with the 5 m bound, with the bound from the nearest
 neighbour's 27 cells, and with per-category pruning.  Diagnostic; run from the repo root."""
+import sys
+import numpy as np
 import os; R=os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0,R); sys.path.insert(0,os.path.join(R,'oracle'))
 import importlib
 sg=importlib.import_module('loam_velodyne-1_amd.synthgen')

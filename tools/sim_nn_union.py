@@ -1,6 +1,8 @@
 """CPU estimate (numpy + the oracle) of how many distinct map points the 27-cell neighbourhoods of
 64 / 128 / 256 consecutive stack points hold against their summed candidates (the reuse an LDS-staged
 5-NN could buy).  Diagnostic; run from the repo root."""
+import sys
+import numpy as np
 import os; R=os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0,R); sys.path.insert(0,os.path.join(R,'oracle'))
 import importlib
 sg=importlib.import_module('loam_velodyne-1_amd.synthgen')
