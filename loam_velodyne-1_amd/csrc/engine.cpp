@@ -61,6 +61,8 @@ FeatView feat_view(const SrBuffers& b, int first, int step) {
 
 }  // namespace
 
+constexpr size_t kMetaBytes = 8192, kMetaSumSlot = kMetaBytes - 64;  // (loam_ctx::meta)
+
 struct loam_ctx {
   loam_config cfg;
   int device = 0;
@@ -91,7 +93,15 @@ struct loam_ctx {
   MpBuffers mpb;
   std::vector<float4> stage;
   Staging pin;                  // pinned staging of the node calls' host clouds
-  char* meta = nullptr;         // pinned scratch (8 KB) for the node calls' small D2H / H2D copies
+  // pinned scratch (8 KB) for the node calls' small D2H / H2D copies, as ints:
+  //   scan registration  [0] n, [1..4] feature counts, [5] nfull, [6] error bits
+  //   odometry           [0..4] counts, [8..19] imu_trans, [24..27] init-frame Last counts,
+  //                      [32 ..) state (kOdStateFloats), istate, nlast (4), nfullEnd (2) downloads
+  //   mapping            [0..2] counts, [4..9] pose, [10..11] IMU roll / pitch, [12] IMU flag,
+  //                      [16 ..) state (kMpStateFloats), istate, nreg downloads (mp.hip)
+  //   kMetaSumSlot       odometry's transformSum written back to the device (an async H2D that
+  //                      may still be pending when the next phase reuses the areas above)
+  char* meta = nullptr;
   loam_stats stats;
   Prof prof;
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -247,7 +257,7 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   x->od1.tune = x->mp1.tune = x->tune;
   if (he == hipSuccess) he = hipMalloc(&x->sr_imu_dev, sizeof(loamimu::SrQueue));
   if (he != hipSuccess) x->sr_imu_dev = nullptr;
-  if (he == hipSuccess) he = hipHostMalloc((void**)&x->meta, 8192, hipHostMallocDefault);
+  if (he == hipSuccess) he = hipHostMalloc((void**)&x->meta, kMetaBytes, hipHostMallocDefault);
   if (he != hipSuccess) x->meta = nullptr;
   x->sr_imu = new loamimu::SrQueue();
   std::memset(x->sr_imu, 0, sizeof(loamimu::SrQueue));
@@ -583,8 +593,9 @@ int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_i
     ist[kIsQueries] = ist[kIsAssoc] * (cnt[0] + cnt[2]);
     // keep the device copy of transformSum current (it is seeded only on the init frame): the
     // host result goes back from the pinned state block, ordered before the next frame's kernels
-    std::memcpy(st + kOdSum, x->od_sum, sizeof(loam_pose6));
-    HIP_TRY(hipMemcpyAsync(o.state + kOdSum, st + kOdSum, sizeof(loam_pose6), hipMemcpyHostToDevice, x->st));
+    float* slot = (float*)(x->meta + kMetaSumSlot);  // (its own slot: see loam_ctx::meta)
+    std::memcpy(slot, x->od_sum, sizeof(loam_pose6));
+    HIP_TRY(hipMemcpyAsync(o.state + kOdSum, slot, sizeof(loam_pose6), hipMemcpyHostToDevice, x->st));
   }
   if (sum_out) std::memcpy(sum_out, x->od_sum, sizeof(loam_pose6));
   *published = LOAM_PUB_POSE;
