@@ -106,7 +106,7 @@ struct loam_ctx {
   Prof prof;
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipStream_t st2 = nullptr;                 // batch: mapping frame 1 beside the odometry solve
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, fork2 = nullptr, join2 = nullptr;
   Tuning tune;                               // launch choices by batch size (loam_set_tuning)
   // tune.graph: the batch step captured once as a HIP graph (for this P / these buffers) and replayed
   hipGraph_t graph = nullptr;
@@ -246,6 +246,8 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   x->pin.streams[1] = x->st2;
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->fork, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->join, hipEventDisableTiming);
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&x->fork2, hipEventDisableTiming);
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&x->join2, hipEventDisableTiming);
   if (he != hipSuccess) {
     loam_destroy(x);
     return fail(LOAM_E_HIP, std::string("event creation failed: ") + hipGetErrorString(he));
@@ -294,6 +296,8 @@ void loam_destroy(loam_ctx* x) {
   x->drop_graph();
   if (x->fork) (void)hipEventDestroy(x->fork);
   if (x->join) (void)hipEventDestroy(x->join);
+  if (x->fork2) (void)hipEventDestroy(x->fork2);
+  if (x->join2) (void)hipEventDestroy(x->join2);
   if (x->st2) (void)hipStreamDestroy(x->st2);
   if (x->st) (void)hipStreamDestroy(x->st);
   delete x;
@@ -827,9 +831,18 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
     mp_batch_frame1(x->mpb, o, fprev, x->st2, nullptr);
     T(hipEventRecord(x->join, x->st2));
   }
-  od_solve(o, fcur, 0, x->st, pf);
+  // the pose accumulation (k_od_fini, one serial double-trig chain per problem) beside
+  // TransformToEnd on the second stream: both only read the solved transform
+  od_solve(o, fcur, 0, x->st, pf, /*device_fini=*/!overlap);
+  if (overlap) {
+    T(hipEventRecord(x->fork2, x->st));
+    T(hipStreamWaitEvent(x->st2, x->fork2, 0));
+    od_fini(o, fcur, x->st2);
+    T(hipEventRecord(x->join2, x->st2));
+  }
   hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, 1, 2, 0);
   x->prof.mark("k_od_end");
+  if (overlap) T(hipStreamWaitEvent(x->st, x->join2, 0));
   if (events) T(hipEventRecord(x->ev[2], x->st));
   // mapping: (frame 1 unless overlapped) then cur with the odometry pose
   if (overlap) {

@@ -366,29 +366,13 @@ __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
 // keys stay in input order (ka[i] = key of point i) and only the 16-bit positions move between
 // the two buffers, each radix pass reading its digits through them (tile_rank4 over the whole
 // segment); the long surf stacks of VLP-16 sweeps fit it.
+// one segment of k_vg_idx with E positions per thread (the layout is blocked: thread t owns
+// positions [t E, t E + E)), so a segment of n points keeps ceil(n / E) threads busy: the kernel
+// picks the smallest E of 4 / 8 / 16 that holds it (a 5k-point surf stack: 625 busy threads, not 313)
 template <int NT, int E>
-__global__ __launch_bounds__(NT) void k_vg_idx(VgJob j) {
-  constexpr int N = NT * E;
-  static_assert(N <= 65536, "16-bit positions");
-  __shared__ uint32_t ka[N];
-  __shared__ uint16_t va[N], vb[N];
-  __shared__ uint32_t sc[(NT / 64 + 1) * 8];
-  __shared__ uint32_t dtot[16], dbase[16];
-  __shared__ float fsc[16];
-  __shared__ int isc[24];
+__device__ __noinline__ void vg_idx_segment(const VgJob& j, int s, int b0, int n, uint32_t* ka, uint16_t* va, uint16_t* vb,
+                           uint32_t* sc, uint32_t* dtot, uint32_t* dbase, float* fsc, int* isc) {
   const int tid = threadIdx.x;
-  const int nl = j.list ? *j.list_n : j.nseg;
-  for (int li = blockIdx.x; li < nl; li += gridDim.x) {
-    const int s = j.list ? j.list[li] : li;
-    const int b0 = j.begin[s], b1 = j.end[s], n = b1 - b0;
-    if (n <= 0) {
-      if (tid == 0) j.out_count[s] = 0;
-      continue;
-    }
-    if (n > N) {
-      if (tid == 0) j.big[atomicAdd(j.big_n, 1)] = s;
-      continue;
-    }
     const float4* in = j.in + b0;
     float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
     for (int i = tid; i < n; i += NT) {
@@ -404,7 +388,7 @@ __global__ __launch_bounds__(NT) void k_vg_idx(VgJob j) {
     if (vg_leaf_too_small(mn, mx, inv)) {  // "leaf size too small": output = input
       for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
       if (tid == 0) j.out_count[s] = n;
-      continue;
+      return;
     }
     const int m0 = (int)floorf(mn[0] * inv), m1 = (int)floorf(mn[1] * inv), m2 = (int)floorf(mn[2] * inv);
     const int divx = (int)floorf(mx[0] * inv) - m0 + 1, divy = (int)floorf(mx[1] * inv) - m1 + 1;
@@ -509,6 +493,34 @@ __global__ __launch_bounds__(NT) void k_vg_idx(VgJob j) {
       }
       if (tid == 0) j.out_count[s] = tot;
     }
+}
+
+template <int NT, int E>
+__global__ __launch_bounds__(NT) void k_vg_idx(VgJob j) {
+  constexpr int N = NT * E;
+  static_assert(N <= 65536, "16-bit positions");
+  __shared__ uint32_t ka[N];
+  __shared__ uint16_t va[N], vb[N];
+  __shared__ uint32_t sc[(NT / 64 + 1) * 8];
+  __shared__ uint32_t dtot[16], dbase[16];
+  __shared__ float fsc[16];
+  __shared__ int isc[24];
+  const int tid = threadIdx.x;
+  const int nl = j.list ? *j.list_n : j.nseg;
+  for (int li = blockIdx.x; li < nl; li += gridDim.x) {
+    const int s = j.list ? j.list[li] : li;
+    const int b0 = j.begin[s], b1 = j.end[s], n = b1 - b0;
+    if (n <= 0) {
+      if (tid == 0) j.out_count[s] = 0;
+      continue;
+    }
+    if (n > N) {
+      if (tid == 0) j.big[atomicAdd(j.big_n, 1)] = s;
+      continue;
+    }
+    if (E >= 16 && n <= NT * 4) vg_idx_segment<NT, 4>(j, s, b0, n, ka, va, vb, sc, dtot, dbase, fsc, isc);
+    else if (E >= 16 && n <= NT * 8) vg_idx_segment<NT, 8>(j, s, b0, n, ka, va, vb, sc, dtot, dbase, fsc, isc);
+    else vg_idx_segment<NT, E>(j, s, b0, n, ka, va, vb, sc, dtot, dbase, fsc, isc);
     __syncthreads();
   }
 }
@@ -2661,7 +2673,8 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   jv.list = b.vg_lin; jv.list_n = b.vg_cnt + 2; jv.zeroed = true;
   if (b.tune.vg_merge) {  // long cube segments with a short tail first (k_vg_merge), the rest by the cascade
     jv.nold = b.vseg_nold; jv.mlist = b.vg_mlist; jv.mlist_n = b.vg_cnt + 3; jv.skip = b.vseg_skip;
-    hipLaunchKernelGGL((k_vg_merge<1024, kVgMergeNew>), dim3(std::min(2 * kMaxValid * P, 1024)), dim3(1024), 0, st, jv);
+    // (its segments are rare: a small grid whose workgroups leave at once when the list is short)
+    hipLaunchKernelGGL((k_vg_merge<1024, kVgMergeNew>), dim3(std::min(2 * kMaxValid * P, 32)), dim3(1024), 0, st, jv);
   }
   // 2 x 125 cube segments per instance, most of them small: batches start with the 2048-point
   // kernel (many workgroups per CU); a few instances with the 12288-point one (one launch)

@@ -1606,6 +1606,10 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
   }
   if (device_fini) hipLaunchKernelGGL(k_od_fini, dim3((P + 63) / 64), dim3(64), 0, st, b, f);
 }
+
+void od_fini(const OdBuffers& b, const FeatView& f, hipStream_t st) {
+  hipLaunchKernelGGL(k_od_fini, dim3((b.P + 63) / 64), dim3(64), 0, st, b, f);
+}
 }  // namespace loam
 
 

@@ -106,6 +106,8 @@ void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st);
 // device_fini: the pose accumulation (k_od_fini) on the device; the streaming path does it on the host
 void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t st, Prof* prof = nullptr,
               bool device_fini = true);
+// the pose accumulation alone (k_od_fini), for a caller that runs it beside TransformToEnd
+void od_fini(const OdBuffers& b, const FeatView& f, hipStream_t st);
 
 }  // namespace loam
 
