@@ -1570,7 +1570,7 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
       // one wave per query when the batch is small (streaming: TransformToStart in the wave), 64
       // waves per problem otherwise (the queries transformed by k_od_sel first)
       const int ga = P >= 64 ? tn.od_assoc_wg : (b.cap_q + kAsWaves - 1) / kAsWaves;  // (8 / 32 / 64 measured slower)
-      if (P >= 64) {
+      if (P >= tn.od_sel_min) {
         hipLaunchKernelGGL(k_od_sel, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f);
         if (prof) hipLaunchKernelGGL((k_od_assoc<true, false>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
         else hipLaunchKernelGGL((k_od_assoc<false, false>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
