@@ -850,7 +850,11 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   } else {
     mp_batch_frame1(x->mpb, o, fprev, x->st, pf);
   }
-  mp_batch_frame2(x->mpb, o, fcur, x->st, pf);
+  // (frame 1 is done: the second stream is free for frame 2's independent branches)
+  SideStream side;
+  side.st = x->st2;
+  side.fork[0] = x->fork; side.join[0] = x->join; side.fork[1] = x->fork2; side.join[1] = x->join2;
+  mp_batch_frame2(x->mpb, o, fcur, x->st, pf, overlap ? &side : nullptr);
   if (events) T(hipEventRecord(x->ev[3], x->st));
   T(hipGetLastError());
   return e;

@@ -2562,7 +2562,7 @@ hipError_t mp_reset(MpBuffers& b, hipStream_t st) {
 }
 
 void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool map_empty,
-              const std::function<void()>& before_register, int stack_max) {
+              const std::function<void()>& before_register, int stack_max, const SideStream* side) {
   const int P = b.P;
   auto mark = [&](const char* n) { if (prof) prof->mark(n); };
   hipLaunchKernelGGL(k_mp_prepare, dim3(P), dim3(kMpThreads), 0, st, b, in);
@@ -2579,8 +2579,15 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   // (the cascade's first kernel takes 12288 points for a few instances, 2048 for batches)
   const bool fits = stack_max >= 0 && stack_max <= (P <= 4 ? 12288 : 2048);
   // batches: the corner stacks (<= 120 points per ring) take the 2048-point kernel, the surf
-  // stacks the 12288-point one; a few instances: one 12288-point launch
-  b.note(vg_run(js, st, P <= 4 ? 12288 : 2048, !fits, /*tier2_idx=*/true));
+  // stacks the 12288-point one; a few instances: one 12288-point launch.  With a side stream it
+  // runs there, beside the FromMap gather and the map hash builds (which read only the store)
+  const bool fork = side && !prof && !map_empty;
+  if (fork) {
+    b.note(hipEventRecord(side->fork[0], st));
+    b.note(hipStreamWaitEvent(side->st, side->fork[0], 0));
+  }
+  b.note(vg_run(js, fork ? side->st : st, P <= 4 ? 12288 : 2048, !fits, /*tier2_idx=*/true));
+  if (fork) b.note(hipEventRecord(side->join[0], side->st));
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);
   mark("k_mp_gather");
@@ -2599,6 +2606,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   if (P <= 4) hs.fill = b.h_fill + (size_t)P * b.tmax;
   hash_build_pair(hc, hs, P, st, false);
   mark("k_hash_build_map");
+  if (fork) b.note(hipStreamWaitEvent(st, side->join[0], 0));
   hipLaunchKernelGGL(k_mp_lm_begin, dim3((P + 255) / 256), dim3(256), 0, st, b);
   // workgroups per instance: all the stack's queries at once for a few instances; for large
   // batches about one pass over a VLP-16 stack (bigger stacks loop), fewer idle workgroups
@@ -2658,6 +2666,15 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     mark("k_mp_iter");
   }
   hipLaunchKernelGGL(k_mp_lm_end, dim3((P + 255) / 256), dim3(256), 0, st, b);
+  // the registration reads only the final pose and the full cloud: beside the insertion with a
+  // side stream (the batch: no before_register hook)
+  const bool reg_side = fork && !before_register;
+  if (reg_side) {
+    b.note(hipEventRecord(side->fork[1], st));
+    b.note(hipStreamWaitEvent(side->st, side->fork[1], 0));
+    hipLaunchKernelGGL(k_mp_register, dim3(16, P), dim3(256), 0, side->st, b, in);
+    b.note(hipEventRecord(side->join[1], side->st));
+  }
   // insertion + per-valid-cube downsampling into the other pool
   // a few instances: 1024 threads per instance (the per-instance serial parts are the cost)
   // 1024 threads per instance also for batches (k_mp_insert 0.40 -> 0.25 ms/step at batch 1024 against 256)
@@ -2684,8 +2701,12 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);
   mark("k_mp_compact");
   if (before_register) before_register();
-  hipLaunchKernelGGL(k_mp_register, dim3(16, P), dim3(256), 0, st, b, in);
-  mark("k_mp_register");
+  if (reg_side) {
+    b.note(hipStreamWaitEvent(st, side->join[1], 0));
+  } else {
+    hipLaunchKernelGGL(k_mp_register, dim3(16, P), dim3(256), 0, st, b, in);
+    mark("k_mp_register");
+  }
   b.pool_cur = 1 - b.pool_cur;
 }
 
@@ -2956,7 +2977,8 @@ void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, const FeatView& fprev, h
 }
 
 // frame 2: cur (Last[1], fullEnd[1]) with the odometry transformSum
-void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, const FeatView& fcur, hipStream_t st, Prof* prof) {
+void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, const FeatView& fcur, hipStream_t st, Prof* prof,
+                     const SideStream* side) {
   MpInput in;
   in.corner = od.lastC + (size_t)od.P * od.capC;
   in.surf = od.lastS + (size_t)od.P * od.capS;
@@ -2968,7 +2990,7 @@ void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, const FeatView& fcur, hi
   in.nfull = fcur.nfull_p; in.nfull_stride = fcur.nfull_stride;
   in.end_state = od.state; in.end_mode = 2;
   in.pose = od.state + kOdSum; in.pose_stride = kOdStateFloats;
-  mp_frame(b, in, st, prof);
+  mp_frame(b, in, st, prof, false, nullptr, -1, side);
 }
 
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err) {

@@ -150,8 +150,16 @@ hipError_t mp_reset(MpBuffers& b, hipStream_t st);
 // before_register: called once every kernel before k_mp_register is enqueued (the streaming path
 // stages the full cloud there); stack_max: the largest stack segment (corner or surf input count)
 // when the host knows it, else -1
+// side: an idle second stream (and two fork / join event pairs) for the frame's independent
+// branches: the stack VoxelGrid beside the FromMap gather + hash builds, and the registration of the
+// full cloud beside the map insertion / per-cube VoxelGrid
+struct SideStream {
+  hipStream_t st = nullptr;
+  hipEvent_t fork[2] = {nullptr, nullptr}, join[2] = {nullptr, nullptr};
+};
 void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof = nullptr, bool map_empty = false,
-              const std::function<void()>& before_register = nullptr, int stack_max = -1);
+              const std::function<void()>& before_register = nullptr, int stack_max = -1,
+              const SideStream* side = nullptr);
 // imu_rp: the IMU (roll, pitch) transformUpdate blends in (nullptr = no IMU); *updated = whether
 // transformUpdate ran (the caller then commits its IMU queue pointer)
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
@@ -169,7 +177,8 @@ int mp_stream_frame_dev(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum
 int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::string& err);
 // fprev / fcur: the scan registration outputs whose full clouds the frames register
 void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, const FeatView& fprev, hipStream_t st, Prof* prof = nullptr);
-void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, const FeatView& fcur, hipStream_t st, Prof* prof = nullptr);
+void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, const FeatView& fcur, hipStream_t st, Prof* prof = nullptr,
+                     const SideStream* side = nullptr);
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err);
 
 }  // namespace loam
