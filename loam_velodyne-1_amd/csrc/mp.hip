@@ -452,18 +452,19 @@ __device__ __noinline__ void vg_idx_segment(const VgJob& j, int s, int b0, int n
       int cstart = 0;
       float sx = 0, sy = 0, sz = 0, si = 0;
       prev = i0 > 0 && i0 < n ? ka[vs[i0 - 1]] : 0u;
+      constexpr int G = E < 8 ? E : 8;  // gathers in flight (the thread's E positions only)
 #pragma unroll
-      for (int e0 = 0; e0 < E; e0 += 8) {
-        float4 a[8];
-        uint32_t kk[8];
+      for (int e0 = 0; e0 < E; e0 += G) {
+        float4 a[G];
+        uint32_t kk[G];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < G; ++u) {
           const int i = i0 + e0 + u;
           kk[u] = i < n ? ka[vs[i]] : 0u;
           a[u] = i < n ? in[vs[i]] : make_float4(0, 0, 0, 0);
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < G; ++u) {
           const int i = i0 + e0 + u;
           if (i < n) {
             if (i == 0 || prev != kk[u]) {
