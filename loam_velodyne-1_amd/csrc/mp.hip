@@ -519,8 +519,8 @@ __global__ __launch_bounds__(NT) void k_vg_idx(VgJob j) {
       if (tid == 0) j.big[atomicAdd(j.big_n, 1)] = s;
       continue;
     }
-    if (E >= 16 && n <= NT * 4) vg_idx_segment<NT, 4>(j, s, b0, n, ka, va, vb, sc, dtot, dbase, fsc, isc);
-    else if (E >= 16 && n <= NT * 8) vg_idx_segment<NT, 8>(j, s, b0, n, ka, va, vb, sc, dtot, dbase, fsc, isc);
+    if (j.adapt && E >= 16 && n <= NT * 4) vg_idx_segment<NT, 4>(j, s, b0, n, ka, va, vb, sc, dtot, dbase, fsc, isc);
+    else if (j.adapt && E >= 16 && n <= NT * 8) vg_idx_segment<NT, 8>(j, s, b0, n, ka, va, vb, sc, dtot, dbase, fsc, isc);
     else vg_idx_segment<NT, E>(j, s, b0, n, ka, va, vb, sc, dtot, dbase, fsc, isc);
     __syncthreads();
   }
@@ -2577,6 +2577,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   // (streaming), the cascade's finish is not enqueued
   // (k_mp_stack zeroed the cascade's list counters)
   js.zeroed = true;
+  js.adapt = b.tune.vg_idx_adapt != 0;
   // (the cascade's first kernel takes 12288 points for a few instances, 2048 for batches)
   const bool fits = stack_max >= 0 && stack_max <= (P <= 4 ? 12288 : 2048);
   // batches: the corner stacks (<= 120 points per ring) take the 2048-point kernel, the surf
