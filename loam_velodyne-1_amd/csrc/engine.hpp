@@ -56,7 +56,6 @@ struct Tuning {
   int mp_iter_wide_max = 0;  // k_mp_iter in 1024-thread (not 256) workgroups for P <= this
   int vg_merge = 1;        // the cubes' VoxelGrid merges an old sorted prefix with the appended tail
                            // (k_vg_merge; config 3's big cubes: 95 -> 50 us per mapping frame)
-  int vg_idx_adapt = 0;    // k_vg_idx with 4 / 8 / 16 positions per thread by segment size (else 16)
   int od_sel_min = 64;     // TransformToStart of the queries as its own launch (k_od_sel) for P >= this,
                            // else inside the association wave (k_od_assoc<., true>)
   int mp_late_iter = 0;    // mapping iterations >= this (0: none) take k_mp_nn<mp_late_lanes> + k_mp_fit
@@ -73,8 +72,7 @@ struct Tuning {
                     {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20},
                     {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20},
                     {"vg_merge", &vg_merge, 0, 1}, {"mp_late_iter", &mp_late_iter, 0, 1000},
-                    {"mp_late_lanes", &mp_late_lanes, 1, 4}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
-                    {"vg_idx_adapt", &vg_idx_adapt, 0, 1}};
+                    {"mp_late_lanes", &mp_late_lanes, 1, 4}, {"od_sel_min", &od_sel_min, 1, 1 << 20}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {
         if (v < k.lo || v > k.hi) return false;

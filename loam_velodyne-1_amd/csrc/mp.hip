@@ -366,11 +366,11 @@ __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
 // keys stay in input order (ka[i] = key of point i) and only the 16-bit positions move between
 // the two buffers, each radix pass reading its digits through them (tile_rank4 over the whole
 // segment); the long surf stacks of VLP-16 sweeps fit it.
-// one segment of k_vg_idx with E positions per thread (the layout is blocked: thread t owns
-// positions [t E, t E + E)), so a segment of n points keeps ceil(n / E) threads busy: the kernel
-// picks the smallest E of 4 / 8 / 16 that holds it (a 5k-point surf stack: 625 busy threads, not 313)
+// one segment of k_vg_idx with E positions per thread (blocked: thread t owns positions [t E, t E + E)).
+// (Round 4: choosing E = 4 / 8 / 16 by segment size, so that a 5k-point stack keeps 625 threads busy
+// instead of 313, measured equal at batch 128 and 1024.)
 template <int NT, int E>
-__device__ __noinline__ void vg_idx_segment(const VgJob& j, int s, int b0, int n, uint32_t* ka, uint16_t* va, uint16_t* vb,
+__device__ __forceinline__ void vg_idx_segment(const VgJob& j, int s, int b0, int n, uint32_t* ka, uint16_t* va, uint16_t* vb,
                            uint32_t* sc, uint32_t* dtot, uint32_t* dbase, float* fsc, int* isc) {
   const int tid = threadIdx.x;
     const float4* in = j.in + b0;
@@ -519,9 +519,7 @@ __global__ __launch_bounds__(NT) void k_vg_idx(VgJob j) {
       if (tid == 0) j.big[atomicAdd(j.big_n, 1)] = s;
       continue;
     }
-    if (j.adapt && E >= 16 && n <= NT * 4) vg_idx_segment<NT, 4>(j, s, b0, n, ka, va, vb, sc, dtot, dbase, fsc, isc);
-    else if (j.adapt && E >= 16 && n <= NT * 8) vg_idx_segment<NT, 8>(j, s, b0, n, ka, va, vb, sc, dtot, dbase, fsc, isc);
-    else vg_idx_segment<NT, E>(j, s, b0, n, ka, va, vb, sc, dtot, dbase, fsc, isc);
+    vg_idx_segment<NT, E>(j, s, b0, n, ka, va, vb, sc, dtot, dbase, fsc, isc);
     __syncthreads();
   }
 }
@@ -2577,7 +2575,6 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   // (streaming), the cascade's finish is not enqueued
   // (k_mp_stack zeroed the cascade's list counters)
   js.zeroed = true;
-  js.adapt = b.tune.vg_idx_adapt != 0;
   // (the cascade's first kernel takes 12288 points for a few instances, 2048 for batches)
   const bool fits = stack_max >= 0 && stack_max <= (P <= 4 ? 12288 : 2048);
   // batches: the corner stacks (<= 120 points per ring) take the 2048-point kernel, the surf

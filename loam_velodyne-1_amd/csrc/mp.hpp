@@ -75,7 +75,6 @@ struct VgJob {
   const int* mlist = nullptr;
   const int* mlist_n = nullptr;
   int* skip = nullptr;
-  bool adapt = false;  // k_vg_idx: positions per thread by segment size (Tuning::vg_idx_adapt)
 };
 
 struct MpBuffers {
