@@ -58,8 +58,6 @@ struct Tuning {
                            // (k_vg_merge; config 3's big cubes: 95 -> 50 us per mapping frame)
   int od_sel_min = 64;     // TransformToStart of the queries as its own launch (k_od_sel) for P >= this,
                            // else inside the association wave (k_od_assoc<., true>)
-  int mp_late_iter = 0;    // mapping iterations >= this (0: none) take k_mp_nn<mp_late_lanes> + k_mp_fit
-  int mp_late_lanes = 4;
   // key = value (loam_set_tuning); false for an unknown key or a value out of range
   bool set(const char* key, long long v) {
     struct K { const char* n; int* f; long long lo, hi; };
@@ -71,12 +69,11 @@ struct Tuning {
                     {"od_rows_deep_max", &od_rows_deep_max, 0, 1 << 20}, {"nn_wg", &nn_wg, 0, 4096},
                     {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20},
                     {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20},
-                    {"vg_merge", &vg_merge, 0, 1}, {"mp_late_iter", &mp_late_iter, 0, 1000},
-                    {"mp_late_lanes", &mp_late_lanes, 1, 4}, {"od_sel_min", &od_sel_min, 1, 1 << 20}};
+                    {"vg_merge", &vg_merge, 0, 1}, {"od_sel_min", &od_sel_min, 1, 1 << 20}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {
         if (v < k.lo || v > k.hi) return false;
-        if ((k.f == &nn_lanes || k.f == &mp_late_lanes) && v == 3) return false;
+        if (k.f == &nn_lanes && v == 3) return false;
         *k.f = (int)v;
         return true;
       }

@@ -2618,10 +2618,9 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
       continue;
     }
     const int gfit = b.tune.fit_wg > 0 ? std::min(b.tune.fit_wg, kMpFitGridMax) : gq * (kMpQueryThreads / kMpFitThreads);
-    // late iterations (few instances still running: the launch is one instance's query chain) may
-    // split each query's candidates over mp_late_lanes lanes instead
-    const bool late = b.tune.mp_late_iter > 0 && it >= b.tune.mp_late_iter;
-    if (!late && P <= b.tune.nnfit_max && gfit <= kMpFitGridMax) {  // search + fit (+ step) in one launch
+    // (round 4: the late iterations, when few instances still run, with 2 / 4 lanes per query
+    // through k_mp_nn<L> measured slower at P = 128: 3.15 -> 3.22 / 3.29 ms/step)
+    if (P <= b.tune.nnfit_max && gfit <= kMpFitGridMax) {  // search + fit (+ step) in one launch
       const bool fused = P <= b.tune.mp_fused_max;
       if (fused && prof) hipLaunchKernelGGL((k_mp_nnfit<true, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
       else if (fused) hipLaunchKernelGGL((k_mp_nnfit<true, false>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
@@ -2637,7 +2636,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     }
     const int gnn = b.tune.nn_wg > 0 ? b.tune.nn_wg : gq * (kMpQueryThreads / kMpNnThreads);
     // L lanes per query for shares of a few hundred problems (the slowest wave is the launch)
-    const int L = late ? b.tune.mp_late_lanes : (P <= b.tune.nn_lanes_maxp ? b.tune.nn_lanes : 1);
+    const int L = P <= b.tune.nn_lanes_maxp ? b.tune.nn_lanes : 1;
     if (b.tune.nn_lds) {  // the block's cells staged in LDS (k_mp_nn_lds: 256 queries per workgroup)
       if (prof) hipLaunchKernelGGL(k_mp_nn_lds<true>, dim3(gq, P), dim3(kNnLdsThreads), 0, st, b);
       else hipLaunchKernelGGL(k_mp_nn_lds<false>, dim3(gq, P), dim3(kNnLdsThreads), 0, st, b);
