@@ -83,10 +83,13 @@ def kernel_bytes(st):
         "k_mp_fit": 129 * st["mp_stack_iters"] + 144 * st["mp_fits"],
         # per query-iteration: accept flag, stack point and coefficient read back for JtJ
         "k_mp_iter": 33 * st["mp_stack_iters"],
-        # the search and the fit in one launch: k_mp_nn's and k_mp_fit's bytes less the fit's read of
-        # the 5-NN the search just found (32 B per query-iteration, kept in registers)
-        "k_mp_nnfit": (80 + 129 - 32) * st["mp_stack_iters"] + 8 * st["mp_nn_cells"] + 16 * st["mp_nn_candidates"]
-                      + 144 * st["mp_fits"],
+        # the search and the fit in one launch, one 64-B record per query (last 5-NN + its fit): per
+        # query-iteration the stack point (16 B), the record's 5-NN read and written (32 + 32 B), its
+        # fit read (32 B, an upper bound: only reused fits are read) and the row written (17 B); per
+        # refit the 5 neighbours (80 B) and the fit written (32 B) less the fit read; the search's
+        # 8 B per bucket range and 16 B per map point evaluated (seeds included)
+        "k_mp_nnfit": 129 * st["mp_stack_iters"] + 8 * st["mp_nn_cells"] + 16 * st["mp_nn_candidates"]
+                      + 80 * st["mp_fits"],
     }
 
 
@@ -101,8 +104,9 @@ def algorithmic_bytes(st):
     Last point once (16 B (C + S), B_OD)."""
     alg = dict(kernel_bytes(st))
     alg["k_mp_nn"] = 96 * st["mp_stack_iters"]
-    # k_mp_nnfit: the search's 96 B plus the fit's own bytes (k_mp_fit's less the 5-NN read back)
-    alg["k_mp_nnfit"] = (96 + 129 - 32) * st["mp_stack_iters"] + 144 * st["mp_fits"]
+    # k_mp_nnfit: the search's 96 B, the record (32 B read + 32 B written, 32 B fit read) and the
+    # row (17 B); per refit the fit written (32 B)
+    alg["k_mp_nnfit"] = (96 + 96 + 17) * st["mp_stack_iters"] + 32 * st["mp_fits"]
     alg["k_od_assoc"] = 16 * st["od_assoc_points"]
     return alg
 

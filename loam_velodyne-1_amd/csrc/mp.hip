@@ -1212,8 +1212,10 @@ LOAM_D MpNnCtx mp_nn_ctx(const MpBuffers& b, int p) {
   return c;
 }
 
-// the list's start: five copies of the seed bound B (see mp_nn_query), or sentinels
-LOAM_D void mp_nn_seed(const MpNnCtx& c, int q, bool corner, bool first, float4 sel, Top5& t, int& work) {
+// the list's start: five copies of the seed bound B (see mp_nn_query), or sentinels; n0 / n1: the
+// previous iteration's ordered 5-NN (i0..i3 | i4, -, distinct) when !first
+LOAM_D void mp_nn_seed_from(const MpNnCtx& c, int q, bool corner, bool first, int4 n0, int4 n1, float4 sel, Top5& t,
+                            int& work) {
   float bd = 3.4e38f;
   int bi = 0x7fffffff;
   if (!first) {
@@ -1223,7 +1225,6 @@ LOAM_D void mp_nn_seed(const MpNnCtx& c, int q, bool corner, bool first, float4 
     // true 5-NN whenever they lie in the searched cells, the B point itself filling the fifth place
     // when only four lie below it (B is a real point) — and no seed needs to be offered or
     // recognised when the walk meets it again
-    const int4 n0 = c.qnn[2 * q], n1 = c.qnn[2 * q + 1];
     if (n1.z) {
       const int prev[5] = {n0.x, n0.y, n0.z, n0.w, n1.x};
       const float4* from = corner ? c.fromC : c.fromS;
@@ -1244,13 +1245,21 @@ LOAM_D void mp_nn_seed(const MpNnCtx& c, int q, bool corner, bool first, float4 
   for (int k = 0; k < 5; ++k) { t.d[k] = bd; t.i[k] = bi; }
 }
 
+LOAM_D void mp_nn_seed(const MpNnCtx& c, int q, bool corner, bool first, float4 sel, Top5& t, int& work) {
+  int4 n0 = make_int4(0, 0, 0, 0), n1 = n0;
+  if (!first) { n0 = c.qnn[2 * q]; n1 = c.qnn[2 * q + 1]; }
+  mp_nn_seed_from(c, q, corner, first, n0, n1, sel, t, work);
+}
+
+// the seeds for the next iteration only when the list holds five distinct map points (a rejected
+// search can end with copies of B or sentinels; the list is sorted, so copies are adjacent)
+LOAM_D int top5_distinct(const Top5& t) {
+  return t.i[4] != 0x7fffffff && t.i[0] != t.i[1] && t.i[1] != t.i[2] && t.i[2] != t.i[3] && t.i[3] != t.i[4];
+}
+
 LOAM_D void mp_nn_store(const MpNnCtx& c, int q, const Top5& t) {
   c.qnn[2 * q] = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
-  // seeds for the next iteration only when these are five distinct map points (a rejected
-  // search can end with copies of B or sentinels; the list is sorted, so copies are adjacent)
-  const int distinct = t.i[4] != 0x7fffffff && t.i[0] != t.i[1] && t.i[1] != t.i[2] && t.i[2] != t.i[3] &&
-                       t.i[3] != t.i[4];
-  c.qnn[2 * q + 1] = make_int4(t.i[4], __float_as_int(t.d[4]), distinct, 0);
+  c.qnn[2 * q + 1] = make_int4(t.i[4], __float_as_int(t.d[4]), top5_distinct(t), 0);
 }
 
 template <int S = kMpQueryThreads, int L = 1, int CAPL = 27>
@@ -1264,6 +1273,79 @@ LOAM_D void mp_nn_query(const MpBuffers& b, const MpNnCtx& c, int q, int nsc, bo
   if constexpr (L > 1) knn5_merge<L>(t);
   LOAM_CHECK(q < b.cap_stack && (t.i[4] == 0x7fffffff || t.i[4] < (corner ? c.nfc : c.nfs)), q, t.i[4]);
   if (sub == 0) mp_nn_store(c, q, t);
+}
+
+// the line (corner: PCA of the 5 neighbours, 3x3 Jacobi, :721-760) or plane (surf: 5x3 QR, :828-850)
+// through the ordered 5-NN points nb; jw: this lane's 27 words of LDS scratch for the Jacobi
+LOAM_D void mp_fit_compute(bool corner, const float4 (&nb)[5], float* jw, float4& g0, float4& g1) {
+  if (corner) {  // :721-760
+    float cx = 0, cy = 0, cz = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { cx += nb[k].x; cy += nb[k].y; cz += nb[k].z; }
+    cx /= 5; cy /= 5; cz /= 5;
+    float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const float ax = nb[k].x - cx, ay = nb[k].y - cy, az = nb[k].z - cz;
+      a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
+      a22 += ay * ay; a23 += ay * az; a33 += az * az;
+    }
+    a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
+    float* A1 = jw;
+    float* D1 = jw + 9;
+    float* V1 = jw + 12;
+    int* iws = (int*)(jw + 21);
+    A1[0] = a11; A1[1] = a12; A1[2] = a13; A1[3] = a12; A1[4] = a22;
+    A1[5] = a23; A1[6] = a13; A1[7] = a23; A1[8] = a33;
+    loamla::jacobi<3>(A1, D1, V1, iws);
+    const bool valid = D1[0] > 3 * D1[1];
+    g0 = make_float4((float)(D(cx) + 0.1 * D(V1[0])), (float)(D(cy) + 0.1 * D(V1[1])),
+                     (float)(D(cz) + 0.1 * D(V1[2])), valid ? 1.0f : 0.0f);
+    g1 = make_float4((float)(D(cx) - 0.1 * D(V1[0])), (float)(D(cy) - 0.1 * D(V1[1])),
+                     (float)(D(cz) - 0.1 * D(V1[2])), 0.0f);
+  } else {  // :828-850
+    float A0[15], B0[5] = {-1, -1, -1, -1, -1}, X0[3], ws[14];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { A0[k * 3 + 0] = nb[k].x; A0[k * 3 + 1] = nb[k].y; A0[k * 3 + 2] = nb[k].z; }
+    loamla::qr_solve(A0, B0, 5, 3, X0, ws);
+    float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
+    const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
+    pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+    bool planeValid = true;
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      if (fabs(D(pa * nb[k].x + pb * nb[k].y + pc * nb[k].z + pd)) > 0.2) planeValid = false;
+    g0 = make_float4(pa, pb, pc, pd);
+    g1 = make_float4(planeValid ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f);
+  }
+}
+
+// the weighted residual of the mapped point sel against a fit (:762-816 corner, :852-874 surf)
+LOAM_D void mp_fit_residual(bool corner, float4 g0, float4 g1, float4 sel, float4& cf, int& ok) {
+  ok = 0;
+  cf = make_float4(0, 0, 0, 0);
+  if (corner && g0.w != 0.0f) {  // :762-816
+    const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
+    const float x1 = g0.x, y1 = g0.y, z1 = g0.z, x2 = g1.x, y2 = g1.y, z2 = g1.z;
+    const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
+    const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
+    const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
+    const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
+    const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
+    const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
+    const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
+    const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
+    const float ld2 = a012 / l12;
+    const float sw = (float)(1 - 0.9 * fabs(D(ld2)));
+    cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
+    ok = D(sw) > 0.1 ? 1 : 0;
+  } else if (!corner && g1.x != 0.0f) {  // :852-874
+    const float pa = g0.x, pb = g0.y, pc = g0.z, pd = g0.w;
+    const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
+    const float sw = (float)(1 - 0.9 * fabs(D(pd2)) / sqrt(sqrt(D(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z))));
+    cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
+    ok = D(sw) > 0.1 ? 1 : 0;
+  }
 }
 
 // jw: this lane's 27 words of LDS scratch for the 3x3 Jacobi
@@ -1288,70 +1370,10 @@ LOAM_D void mp_fit_query(const MpBuffers& b, int p, int q, int nsc, bool first, 
       }
       f.n0 = n0;
       f.n1 = make_int4(n1.x, 0, 0, 0);
-      if (corner) {  // :721-760
-        float cx = 0, cy = 0, cz = 0;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) { cx += nb[k].x; cy += nb[k].y; cz += nb[k].z; }
-        cx /= 5; cy /= 5; cz /= 5;
-        float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          const float ax = nb[k].x - cx, ay = nb[k].y - cy, az = nb[k].z - cz;
-          a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
-          a22 += ay * ay; a23 += ay * az; a33 += az * az;
-        }
-        a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
-        float* A1 = jw;
-        float* D1 = jw + 9;
-        float* V1 = jw + 12;
-        int* iws = (int*)(jw + 21);
-        A1[0] = a11; A1[1] = a12; A1[2] = a13; A1[3] = a12; A1[4] = a22;
-        A1[5] = a23; A1[6] = a13; A1[7] = a23; A1[8] = a33;
-        loamla::jacobi<3>(A1, D1, V1, iws);
-        const bool valid = D1[0] > 3 * D1[1];
-        f.g0 = make_float4((float)(D(cx) + 0.1 * D(V1[0])), (float)(D(cy) + 0.1 * D(V1[1])),
-                           (float)(D(cz) + 0.1 * D(V1[2])), valid ? 1.0f : 0.0f);
-        f.g1 = make_float4((float)(D(cx) - 0.1 * D(V1[0])), (float)(D(cy) - 0.1 * D(V1[1])),
-                           (float)(D(cz) - 0.1 * D(V1[2])), 0.0f);
-      } else {  // :828-850
-        float A0[15], B0[5] = {-1, -1, -1, -1, -1}, X0[3], ws[14];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) { A0[k * 3 + 0] = nb[k].x; A0[k * 3 + 1] = nb[k].y; A0[k * 3 + 2] = nb[k].z; }
-        loamla::qr_solve(A0, B0, 5, 3, X0, ws);
-        float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
-        const float ps = (float)sqrt(D(pa * pa + pb * pb + pc * pc));
-        pa /= ps; pb /= ps; pc /= ps; pd /= ps;
-        bool planeValid = true;
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-          if (fabs(D(pa * nb[k].x + pb * nb[k].y + pc * nb[k].z + pd)) > 0.2) planeValid = false;
-        f.g0 = make_float4(pa, pb, pc, pd);
-        f.g1 = make_float4(planeValid ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f);
-      }
+      mp_fit_compute(corner, nb, jw, f.g0, f.g1);
       qfit[q] = f;
     }
-    if (corner && f.g0.w != 0.0f) {  // :762-816
-      const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
-      const float x1 = f.g0.x, y1 = f.g0.y, z1 = f.g0.z, x2 = f.g1.x, y2 = f.g1.y, z2 = f.g1.z;
-      const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
-      const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
-      const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
-      const float a012 = (float)sqrt(D(m11 * m11 + m22 * m22 + m33 * m33));
-      const float l12 = (float)sqrt(D((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2)));
-      const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
-      const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
-      const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
-      const float ld2 = a012 / l12;
-      const float sw = (float)(1 - 0.9 * fabs(D(ld2)));
-      cf = make_float4(sw * la, sw * lb, sw * lc, sw * ld2);
-      ok = D(sw) > 0.1 ? 1 : 0;
-    } else if (!corner && f.g1.x != 0.0f) {  // :852-874
-      const float pa = f.g0.x, pb = f.g0.y, pc = f.g0.z, pd = f.g0.w;
-      const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
-      const float sw = (float)(1 - 0.9 * fabs(D(pd2)) / sqrt(sqrt(D(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z))));
-      cf = make_float4(sw * pa, sw * pb, sw * pc, sw * pd2);
-      ok = D(sw) > 0.1 ? 1 : 0;
-    }
+    mp_fit_residual(corner, f.g0, f.g1, sel, cf, ok);
   } else if (first) {
     // no fit this iteration: drop a fit left by an earlier frame (whose map indices name other
     // points) so that a later iteration cannot take it for this frame's
@@ -1800,36 +1822,67 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(F
   // 28 fp64 sums live across the search), the passes' sums added in pass order (one pass per lane
   // for a VLP-16 stack: the same sums as k_mp_fit<true>)
   double red = 0.0;
+  // one record per query (MpFit in q_fit): the 5-NN of the last iteration (i0..i3 | i4, d4 bits,
+  // distinct, fit valid) and the fit made for them — the seeds and the reuse test in one read
+  MpFit* qrec = (MpFit*)b.q_fit + (size_t)p * b.cap_stack;
   for (int q0 = blk.x * NT; q0 < nq; q0 += gridDim.x * NT) {  // (wave-uniform trip count)
     const int q = q0 + tid;
-    float4 sel = make_float4(0, 0, 0, 0), row_o = sel, row_c = sel;
+    const bool corner = q < nsc;
+    float4 sel = make_float4(0, 0, 0, 0), o = sel, cf = sel;
+    int4 r0 = make_int4(-1, -1, -1, -1), r1 = make_int4(0, 0, 0, 0);
     bool row_ok = false;
     Top5 t;
-    if (q < nq) mp_nn_query<NT, 1, kNnListCap>(b, c, q, nsc, first, r, lds + tid, sel, t, work);
+    if (q < nq) {
+      o = c.stack[corner ? q : b.capC + (q - nsc)];
+      if (!first) { r0 = qrec[q].n0; r1 = qrec[q].n1; }
+      sel = loampose::point_to_map(r, o);
+      mp_nn_seed_from(c, q, corner, first, r0, r1, sel, t, work);
+      if (corner) knn5_flat<NT, 1, kNnListCap>(c.hcs, c.hcr, c.hcp, c.TC, sel, t, lds + tid, work, 0);
+      else knn5_flat<NT, 1, kNnListCap>(c.hss, c.hsr, c.hsp, c.TS, sel, t, lds + tid, work, 0);
+      LOAM_CHECK(q < b.cap_stack && (t.i[4] == 0x7fffffff || t.i[4] < (corner ? c.nfc : c.nfs)), q, t.i[4]);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();  // every lane's list reads are done before the scratch reuse
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     if (q < nq) {
-      const bool corner = q < nsc;
       const int4 n0 = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
-      const int4 n1 = make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0);
-      float4 o = make_float4(0, 0, 0, 0), cf;
-      if (n1.x != 0x7fffffff && D(t.d[4]) < 1.0) o = c.stack[corner ? q : b.capC + (q - nsc)];
-      int ok;
-      mp_fit_query(b, p, q, nsc, first, n0, n1, sel, jw, nfits, cf, ok);
+      // the stored fit is this list's when the list is unchanged and the fit was made (a fit is
+      // a function of the five map points alone: reusing it is bit-identical to refitting)
+      bool valid = !first && r1.w && r0.x == n0.x && r0.y == n0.y && r0.z == n0.z && r0.w == n0.w &&
+                   r1.x == t.i[4];
+      int ok = 0;
+      if (t.i[4] != 0x7fffffff && D(t.d[4]) < 1.0) {  // :719, :826
+        float4 g0, g1;
+        if (valid) {
+          g0 = qrec[q].g0;
+          g1 = qrec[q].g1;
+        } else {
+          ++nfits;
+          const float4* from = corner ? c.fromC : c.fromS;
+          float4 nb[5];
+#pragma unroll
+          for (int k = 0; k < 5; ++k) {
+            LOAM_CHECK(t.i[k] >= 0 && t.i[k] < (corner ? c.nfc : c.nfs), t.i[k], q);
+            nb[k] = from[t.i[k]];
+          }
+          mp_fit_compute(corner, nb, jw, g0, g1);
+          qrec[q].g0 = g0;
+          qrec[q].g1 = g1;
+          valid = true;
+        }
+        mp_fit_residual(corner, g0, g1, sel, cf, ok);
+      }
+      qrec[q].n0 = n0;
+      qrec[q].n1 = make_int4(t.i[4], __float_as_int(t.d[4]), top5_distinct(t), valid ? 1 : 0);
       qok[q] = (int8_t)ok;
       qcf[q] = cf;
-      if constexpr (FUSED) {
-        row_ok = ok != 0;
-        row_o = o;
-        row_c = cf;
-      }
+      row_ok = ok != 0;
     }
     if constexpr (FUSED) {  // (outside the branch: every lane takes part in the shuffles)
       double acc[28];
 #pragma unroll
       for (int k = 0; k < 28; ++k) acc[k] = 0.0;
-      if (row_ok) mp_row_accum(tg, row_o, row_c, acc);
+      if (row_ok) mp_row_accum(tg, o, cf, acc);
       wave_reduce_scatter_28(acc);
       red += acc[0];
     }

@@ -105,6 +105,7 @@ struct MpBuffers {
   float4* q_cf = nullptr;     // [P][cap_stack]
   int4* q_nn = nullptr;       // [P][cap_stack][2] this iteration's ordered 5-NN (i0..i3 | i4, d4 bits)
   float4* q_fit = nullptr;    // [P][cap_stack][4] MpFit: the 5-NN a line / plane was fitted to + the fit
+                              // (k_mp_nnfit: the last iteration's 5-NN, d4, distinct, fit-valid + the fit)
   // insertion / per-cube downsampling
   int* app_cnt = nullptr;     // [P][kCubeNum][2] appended points per cube
   int* citems = nullptr;      // [P][2 * kCubeNum] non-empty (kind, cube, valid index) of the new store
