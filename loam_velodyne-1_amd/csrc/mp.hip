@@ -43,7 +43,6 @@ __device__ PhaseAcc g_ph_mp = {~0ull, 0ull, 0ull, {{0}}};
 namespace {
 
 constexpr int kMpThreads = 256;
-constexpr int kMpWaves = kMpThreads / 64;
 
 LOAM_D int cube_of(float v, int cen) {  // :446-452, :983-989
   int c = (int)((D(v) + 25.0) / 50.0) + cen;
@@ -1392,9 +1391,9 @@ LOAM_D MpTrig mp_trig_of(const loampose::MapRot& r) {
   return {(float)r.s0, (float)r.c0, (float)r.s1, (float)r.c1, (float)r.s2, (float)r.c2};
 }
 
-LOAM_D void mp_row_accum(const MpTrig& tg, float4 o, float4 c, double (&acc)[28]) {
+// the accepted row's J (:897-921): a[0..5] and b = -coefficient.w
+LOAM_D void mp_row_jac(const MpTrig& tg, float4 o, float4 c, float (&a)[6], float& bb) {
   const float srx = tg.srx, crx = tg.crx, sry = tg.sry, cry = tg.cry, srz = tg.srz, crz = tg.crz;
-  float a[6];
   a[0] = (crx * sry * srz * o.x + crx * crz * sry * o.y - srx * sry * o.z) * c.x +
          (-srx * srz * o.x - crz * srx * o.y - crx * o.z) * c.y +
          (crx * cry * srz * o.x + crx * cry * crz * o.y - cry * srx * o.z) * c.z;
@@ -1406,7 +1405,12 @@ LOAM_D void mp_row_accum(const MpTrig& tg, float4 o, float4 c, double (&acc)[28]
   a[3] = c.x;
   a[4] = c.y;
   a[5] = c.z;
-  const float bb = -c.w;
+  bb = -c.w;
+}
+
+LOAM_D void mp_row_accum(const MpTrig& tg, float4 o, float4 c, double (&acc)[28]) {
+  float a[6], bb;
+  mp_row_jac(tg, o, c, a, bb);
   int k = 0;
 #pragma unroll
   for (int i = 0; i < 6; ++i)
@@ -1799,8 +1803,11 @@ __global__ __launch_bounds__(kMpFitThreads) void k_mp_fit(MpBuffers b) {
 // lists and 27-word Jacobi scratch share one LDS array (the wave's search is over before its fits
 // begin).  Same query -> lane mapping and row order as k_mp_fit, so the sums are k_mp_fit's.
 // FUSED: the partial + last-workgroup step of k_mp_fit<true>.  COUNT: the work counters.
+#ifndef LOAM_NNFIT_WPE
+#define LOAM_NNFIT_WPE 4
+#endif
 template <bool FUSED, bool COUNT>
-__global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(FUSED ? 3 : 4))) void k_mp_nnfit(MpBuffers b) {
+__global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(LOAM_NNFIT_WPE))) void k_mp_nnfit(MpBuffers b) {
   constexpr int NT = kMpFitThreads;
   static_assert(NT == 64, "the list / scratch sharing needs one wave per workgroup");
   const XcdBlock blk = xcd_block();
@@ -1822,6 +1829,24 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(F
   // 28 fp64 sums live across the search), the passes' sums added in pass order (one pass per lane
   // for a VLP-16 stack: the same sums as k_mp_fit<true>)
   double red = 0.0;
+  // FUSED: lane 2t's term t of the 28 sums (JᵀJ upper triangle row-major, Jᵀb, rows) as the
+  // product of row entries term_x * term_y (mp_row_accum's order; entry 7 = 1 per accepted row)
+  int term_x = -1, term_y = -1;
+  if (FUSED && (tid & 1) == 0 && (tid >> 1) < 28) {
+    const int t = tid >> 1;
+    if (t < 21) {
+      int i = 0, r0 = t;
+      while (r0 >= 6 - i) { r0 -= 6 - i; ++i; }
+      term_x = i;
+      term_y = i + r0;
+    } else if (t < 27) {
+      term_x = t - 21;
+      term_y = 6;
+    } else {
+      term_x = 7;
+      term_y = 7;
+    }
+  }
   // one record per query (MpFit in q_fit): the 5-NN of the last iteration (i0..i3 | i4, d4 bits,
   // distinct, fit valid) and the fit made for them — the seeds and the reuse test in one read
   MpFit* qrec = (MpFit*)b.q_fit + (size_t)p * b.cap_stack;
@@ -1878,13 +1903,29 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(F
       qcf[q] = cf;
       row_ok = ok != 0;
     }
-    if constexpr (FUSED) {  // (outside the branch: every lane takes part in the shuffles)
-      double acc[28];
+    if constexpr (FUSED) {  // (outside the branch: every lane takes part)
+      // the pass's rows through LDS (8 floats per lane: J, b, 1 when accepted, else zeros), then
+      // lane 2t sums term t over the wave's rows in query order: no 28 fp64 sums per lane
+      float a6[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0f;
+      if (row_ok) mp_row_jac(tg, o, cf, a6, bb);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();  // the fits' scratch reads are done
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      float* rw = (float*)lds + tid * 8;
 #pragma unroll
-      for (int k = 0; k < 28; ++k) acc[k] = 0.0;
-      if (row_ok) mp_row_accum(tg, o, cf, acc);
-      wave_reduce_scatter_28(acc);
-      red += acc[0];
+      for (int k = 0; k < 6; ++k) rw[k] = a6[k];
+      rw[6] = bb;
+      rw[7] = row_ok ? 1.0f : 0.0f;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (term_x >= 0) {
+        const float* rows = (const float*)lds;
+        double s = 0.0;
+#pragma unroll 16
+        for (int l = 0; l < NT; ++l) s = loamla::dmac(s, rows[l * 8 + term_x], rows[l * 8 + term_y]);
+        red += s;
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();  // the fits' scratch is free before the next lists
