@@ -58,6 +58,9 @@ struct Tuning {
                            // (k_vg_merge; config 3's big cubes: 95 -> 50 us per mapping frame)
   int od_sel_min = 64;     // TransformToStart of the queries as its own launch (k_od_sel) for P >= this,
                            // else inside the association wave (k_od_assoc<., true>)
+  int od_win_mono = 3;     // association rounds whose ring windows on ring-monotone Last clouds take the
+                           // index-range search (wave_window_mono) instead of the walks: bit 0 the
+                           // first (unseeded) round, bit 1 the seeded ones
   // key = value (loam_set_tuning); false for an unknown key or a value out of range
   bool set(const char* key, long long v) {
     struct K { const char* n; int* f; long long lo, hi; };
@@ -69,7 +72,8 @@ struct Tuning {
                     {"od_rows_deep_max", &od_rows_deep_max, 0, 1 << 20}, {"nn_wg", &nn_wg, 0, 4096},
                     {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20},
                     {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20},
-                    {"vg_merge", &vg_merge, 0, 1}, {"od_sel_min", &od_sel_min, 1, 1 << 20}};
+                    {"vg_merge", &vg_merge, 0, 1}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
+                    {"od_win_mono", &od_win_mono, 0, 3}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {
         if (v < k.lo || v > k.hi) return false;

@@ -143,27 +143,43 @@ LOAM_D void hash_sort(const HashJob& j, const float4* pts, int n, int T, int* st
 }
 
 // the chunk boxes (min / max of x, y, z and of the ring int(intensity)) of points [0, n) in
-// kChunk-point chunks, 64 / kChunk chunks per wave step; wave w0 of nw waves
+// CHK-point chunks, 64 / CHK chunks per wave step; wave w0 of nw waves
+template <int CHK = kChunk>
 LOAM_D void chunk_boxes(const float4* pts, int n, float4* ch, int w0, int nw) {
   const int lane = lane_id();
-  constexpr int PER = 64 / kChunk;
-  const int nch = (n + kChunk - 1) / kChunk;
+  constexpr int PER = 64 / CHK;
+  const int nch = (n + CHK - 1) / CHK;
   for (int c0 = w0 * PER; c0 < nch; c0 += nw * PER) {
-    const int c = c0 + lane / kChunk;
-    const float4 a = pts[min(c * kChunk + lane % kChunk, n - 1)];
+    const int c = c0 + lane / CHK;
+    const float4 a = pts[min(c * CHK + lane % CHK, n - 1)];
     const float r = (float)(int)a.w;
     float4 lo = make_float4(a.x, a.y, a.z, r), hi = lo;
 #pragma unroll
-    for (int o = kChunk / 2; o > 0; o >>= 1) {
+    for (int o = CHK / 2; o > 0; o >>= 1) {
       lo.x = fminf(lo.x, __shfl_xor(lo.x, o, 64)); lo.y = fminf(lo.y, __shfl_xor(lo.y, o, 64));
       lo.z = fminf(lo.z, __shfl_xor(lo.z, o, 64)); lo.w = fminf(lo.w, __shfl_xor(lo.w, o, 64));
       hi.x = fmaxf(hi.x, __shfl_xor(hi.x, o, 64)); hi.y = fmaxf(hi.y, __shfl_xor(hi.y, o, 64));
       hi.z = fmaxf(hi.z, __shfl_xor(hi.z, o, 64)); hi.w = fmaxf(hi.w, __shfl_xor(hi.w, o, 64));
     }
-    if (lane % kChunk == 0 && c < nch) {
+    if (lane % CHK == 0 && c < nch) {
       ch[2 * c] = lo;
       ch[2 * c + 1] = hi;
     }
+  }
+}
+
+// the ring start table of a ring-monotone cloud (HashJob::rstart): point i (of threads t0, t0 + nt,
+// ...) opens the rings above its predecessor's up to its own; the last point closes the rest
+LOAM_D void ring_starts(const HashJob& j, const float4* pts, int n, int p, int t0, int nt) {
+  int* rs = j.rstart + (size_t)p * j.rstart_stride;
+  auto ring = [&](int i) { return min(max((int)pts[i].w, 0), kRingTab - 1); };
+  if (n == 0 && t0 < kRingTab)
+    for (int r = t0; r < kRingTab; r += nt) rs[r] = 0;
+  for (int i = t0; i < n; i += nt) {
+    const int r = ring(i), rp = i > 0 ? ring(i - 1) : -1;
+    for (int rr = rp + 1; rr <= r; ++rr) rs[rr] = i;
+    if (i == n - 1)
+      for (int rr = r + 1; rr < kRingTab; ++rr) rs[rr] = n;
   }
 }
 
@@ -185,12 +201,14 @@ __global__ __launch_bounds__(NT) void k_hash_build(HashJob j) {
   else hash_sort<NT, false>(j, pts, n, T, start, out, j.fill + (size_t)p * j.tmax, scratch, rec);
   if (j.chunks)  // chunk boxes of the source order
     chunk_boxes(pts, n, j.chunks + (size_t)p * 2 * chunks_of((int)j.pts_stride), tid >> 6, NT / 64);
+  if (j.fine) chunk_boxes<kSub>(pts, n, j.fine + (size_t)p * 2 * subs_of((int)j.pts_stride), tid >> 6, NT / 64);
   if (j.mono) {  // rings non-decreasing in index order (one flag per cloud: no atomics)
     bool bad = false;
     for (int i = tid + 1; i < n; i += NT) bad |= (int)pts[i].w < (int)pts[i - 1].w;
     bad = __syncthreads_or(bad);
     if (tid == 0) j.mono[(size_t)p * j.mono_stride] = bad ? 0 : 1;
   }
+  if (j.rstart) ring_starts(j, pts, n, p, tid, NT);
 }
 
 // ---- the same index built by many workgroups per cloud (small batches: streaming, config 2).  One
@@ -239,11 +257,15 @@ __global__ __launch_bounds__(256) void k_hash_count(HashPair hp) {
   if (j.chunks)  // chunk boxes of the source order (as k_hash_build)
     chunk_boxes(pts, n, j.chunks + (size_t)p * 2 * chunks_of((int)j.pts_stride), blockIdx.x * 4 + (tid >> 6),
                 gridDim.x * 4);
+  if (j.fine)
+    chunk_boxes<kSub>(pts, n, j.fine + (size_t)p * 2 * subs_of((int)j.pts_stride), blockIdx.x * 4 + (tid >> 6),
+                      gridDim.x * 4);
   if (j.mono) {
     bool bad = false;
     for (int i = blockIdx.x * 256 + tid + 1; i < n; i += gridDim.x * 256) bad |= (int)pts[i].w < (int)pts[i - 1].w;
     if (bad) j.mono[(size_t)p * j.mono_stride] = 0;
   }
+  if (j.rstart) ring_starts(j, pts, n, p, blockIdx.x * 256 + tid, gridDim.x * 256);
 }
 
 // exclusive scan of the counters into start (and back into fill as the scatter's cursors)
@@ -594,6 +616,125 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
   }
 }
 
+// The ring windows of a ring-monotone Last cloud (HashJob::mono) as index ranges: the walks of
+// :486-523 / :598-645 from the nearest point c (ring scan) visit, before their stops, exactly the points
+// of [rs[scan - 2], c) backward and (c, min(fwd_end, rs[scan + 3])) forward, and a point's category is
+// its ring: the same ring (surf min2: j > c ring <= scan, j < c ring >= scan) is [rs[scan], rs[scan + 1]),
+// the rest are the other rings (corner, surf min3).  Each minimum is keyed by (distance, walk
+// position) like the walks', so it is found by visiting the window's kSub-point sub-chunks (64 / kSub
+// per wave step, in index order) while their boxes may still hold a point at or below a wanted
+// category's bound — the previous round's choice when it is a member, the cells' members (wb, first
+// round), then the minima so far: exact, in a few wave steps.
+// fb: the cloud's kSub-point sub-chunk boxes; rs: its ring start table (LDS).  want_same: the surf min2 category is taken (corner: no).
+// best2 / best3 in and out: the keys ((distance bits << 32) | walk position), ~0 for none; keys at
+// or above 25 m² never count (:491, :602).
+#ifndef LOAM_WIN_TIGHTEN
+#define LOAM_WIN_TIGHTEN 0  // bounds tightened after every wave step: 0 never (the seeds' / cells' only),
+#endif                      // 1 always, 2 in the first (unseeded) round
+
+LOAM_D void wave_window_mono(const float4* L, const float4* fb, const int* rs, int c, int scan, int fwd_end,
+                             float4 sel, bool want_same, const WinBound& wb, bool tighten, uint64_t& best2,
+                             uint64_t& best3, int& wpts, int& wbox) {
+  constexpr int PER = 64 / kSub;            // sub-chunks visited per wave step
+  constexpr int BPL = kSub == 16 ? 2 : 1;   // boxes per lane per box step
+  const int lane = lane_id();
+  const int w0 = rs[max(scan - 2, 0)], rs0 = rs[scan], rs1 = rs[scan + 1];
+  const int w1 = max(min(fwd_end, rs[min(scan + 3, kRingTab - 1)]), c + 1);
+  // the lane's keys (reduced once at the end) and the categories' distance bounds (wave-uniform):
+  // the seeds', the cells' (wb), 25
+  uint64_t k2 = best2, k3 = best3;
+  float d2 = fminf(wb.same, __uint_as_float((uint32_t)(best2 >> 32)));
+  float d3 = fminf(wb.other, __uint_as_float((uint32_t)(best3 >> 32)));
+  d2 = fminf(d2, 25.0f);
+  d3 = fminf(d3, 25.0f);
+  const int k0 = w0 / kSub, k1 = (w1 - 1) / kSub;  // sub-chunks overlapping [w0, w1)
+  for (int g = k0; g <= k1; g += 64 * BPL) {
+    wbox += min(64 * BPL, k1 - g + 1);
+    float bd[BPL];
+    bool hs[BPL], ho[BPL];
+    uint64_t live[BPL];
+#pragma unroll
+    for (int u = 0; u < BPL; ++u) {
+      const int k = g + u * 64 + lane;
+      bd[u] = 3.4e38f;
+      hs[u] = ho[u] = false;
+      if (k <= k1) {
+        bd[u] = box_d2(fb[2 * k], fb[2 * k + 1], sel);
+        const int lo = max(k * kSub, w0), hi = min(k * kSub + kSub, w1);
+        hs[u] = want_same && max(lo, rs0) < min(hi, rs1);
+        ho[u] = lo < rs0 || hi > rs1;
+      }
+      live[u] = ~0ull;
+    }
+    while (true) {
+      // the boxes that may still hold a point at or below a wanted category's bound
+      bool any = false;
+#pragma unroll
+      for (int u = 0; u < BPL; ++u) {
+        live[u] &= __ballot((hs[u] && bd[u] <= d2) || (ho[u] && bd[u] <= d3));
+        any |= live[u] != 0;
+      }
+      if (!any) break;
+      // the first PER of them in index order; lane l visits point l % kSub of pick l / kSub
+      int mine = -1, npick = 0;
+#pragma unroll
+      for (int s = 0; s < PER; ++s) {
+        int pk = -1;
+#pragma unroll
+        for (int u = 0; u < BPL; ++u)
+          if (pk < 0 && live[u]) {
+            pk = u * 64 + __ffsll((unsigned long long)live[u]) - 1;
+            live[u] &= live[u] - 1;
+          }
+        if (pk >= 0) ++npick;
+        if (lane / kSub == s) mine = pk;
+      }
+      if (LOAM_ASSOC_PHASE == 0 || LOAM_ASSOC_PHASE == 3) wpts += npick * kSub;
+      float ds = 3.4e38f, dot = 3.4e38f;
+      const int j = (g + mine) * kSub + lane % kSub;
+      if (mine >= 0 && j >= w0 && j < w1 && j != c) {
+        const float4 a = L[j];
+        const float d = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
+        const uint32_t pos = j > c ? (uint32_t)(j - c - 1) : (1u << 30) + (uint32_t)(c - 1 - j);
+        const uint64_t key = ((uint64_t)fkey(d) << 32) | pos;
+        if (j >= rs0 && j < rs1) {
+          if (want_same) {
+            k2 = key < k2 ? key : k2;
+            ds = d;
+          }
+        } else {
+          k3 = key < k3 ? key : k3;
+          dot = d;
+        }
+      }
+      if (tighten) {
+        if (want_same) d2 = fminf(d2, wave_min_f(ds));
+        d3 = fminf(d3, wave_min_f(dot));
+      }
+    }
+  }
+  const uint64_t kNone = (uint64_t)fkey(25.0f) << 32;  // keys below this have d < 25 (:491, :602)
+  best2 = want_same ? wave_min_u64(k2) : ~0ull;
+  best3 = wave_min_u64(k3);
+  if (best2 >= kNone) best2 = ~0ull;
+  if (best3 >= kNone) best3 = ~0ull;
+}
+
+// a seed's key in wave_window_mono's categories (~0 when j is not in the wanted one or d >= 25)
+LOAM_D uint64_t mono_seed_key(const int* rs, int c, int scan, int fwd_end, int j, float d, bool same) {
+  if (j < 0 || j == c || !(D(d) < 25)) return ~0ull;
+  const int w0 = rs[max(scan - 2, 0)], rs0 = rs[scan], rs1 = rs[scan + 1];
+  const int w1 = max(min(fwd_end, rs[min(scan + 3, kRingTab - 1)]), c + 1);
+  if (j < w0 || j >= w1 || (j >= rs0 && j < rs1) != same) return ~0ull;
+  const uint32_t pos = j > c ? (uint32_t)(j - c - 1) : (1u << 30) + (uint32_t)(c - 1 - j);
+  return ((uint64_t)fkey(d) << 32) | pos;
+}
+
+LOAM_D int mono_decode(int c, uint64_t k) {
+  const uint32_t o = (uint32_t)k;
+  return o >= (1u << 30) ? c - 1 - (int)(o - (1u << 30)) : c + 1 + (int)o;
+}
+
 // corner association (:478-527): closest (kd NN, sqDis < 25) and the best point of an adjacent
 // ring in the index window.  fwd_end = min(cornerPointsSharpNum, C) (Q11).
 // A seed (sj, sd): the previous association round's choice for this query and its squared distance
@@ -750,8 +891,17 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
   int* ind = b.ind + (size_t)p * 3 * b.cap_q;
   int wpts = 0, wbox = 0;  // wave-uniform work counters (loam_stats od_assoc_gathered / _boxes)
   const bool seeded = ist[kIsIters] > 0;  // ind holds this frame's previous round
+  const bool use_mono = (b.tune.od_win_mono & (seeded ? 2 : 1)) != 0;
+  const bool tight = LOAM_WIN_TIGHTEN == 1 || (LOAM_WIN_TIGHTEN == 2 && !seeded);
   const int hCT = b.hC_T[last_buf * b.P + p], hST = b.hS_T[last_buf * b.P + p];
   const bool monoC = b.mono[lp * 2 + 0] != 0, monoS = b.mono[lp * 2 + 1] != 0;
+  __shared__ int rsC[kRingTab], rsS[kRingTab];  // the ring start tables (ring-monotone clouds)
+  static_assert(kAsWaves == 1, "the ring tables are loaded by the workgroup's one wave");
+  for (int r = lane; r < kRingTab; r += 64) {
+    rsC[r] = b.rstart[lp * 2 * kRingTab + r];
+    rsS[r] = b.rstart[lp * 2 * kRingTab + kRingTab + r];
+  }
+  __builtin_amdgcn_wave_barrier();
   const int G = gridDim.x * kAsWaves, q0 = blk.x * kAsWaves + w;
   // The wave's queries q0, q0 + G, ... in batches of 64: lane l first fetches query l's
   // TransformToStart point and its seeds — the previous round's choices (ind, rounds after the
@@ -802,7 +952,33 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
       // the cells' window bounds in the first round only (later rounds have their seeds: the extra
       // pass over the cells cost more than the chunks it saved there)
       WinBound wb;
-      if (q < nc) {
+      if (q < nc && monoC && use_mono) {
+        const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
+        const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC, hCT, CL, ch, C, 1.0f,
+                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded ? -1 : 0, min(nc, C), true, &wb);
+        i1 = i2 = -1;
+        if (nn != ~0ull && D(__uint_as_float((uint32_t)(nn >> 32))) < 25) {
+          const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u), fe = min(nc, C);
+          i1 = c;
+          uint64_t k2 = ~0ull, k3 = mono_seed_key(rsC, c, scan, fe, j1, d1, false);
+          wave_window_mono(CL, b.fC + lp * 2 * subs_of(b.capC), rsC, c, scan, fe, s4, false, wb, tight, k2, k3, wpts, wbox);
+          if (k3 != ~0ull) i2 = mono_decode(c, k3);
+        }
+      } else if (q >= nc && monoS && use_mono) {
+        const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
+        const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS, hST, SL, ch, S, 1.0f,
+                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded ? -1 : 1, min(ns, S), true, &wb);
+        i1 = i2 = -1;
+        if (nn != ~0ull && D(__uint_as_float((uint32_t)(nn >> 32))) < 25) {
+          const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u), fe = min(ns, S);
+          i1 = c;
+          uint64_t k2 = mono_seed_key(rsS, c, scan, fe, j1, d1, true);
+          uint64_t k3 = mono_seed_key(rsS, c, scan, fe, j2, d2, false);
+          wave_window_mono(SL, b.fS + lp * 2 * subs_of(b.capS), rsS, c, scan, fe, s4, true, wb, tight, k2, k3, wpts, wbox);
+          if (k2 != ~0ull) i2 = mono_decode(c, k2);
+          if (k3 != ~0ull) i3 = mono_decode(c, k3);
+        }
+      } else if (q < nc) {
         const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
         const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC, hCT, CL, ch, C, 1.0f,
                                          1.0f, s4, nnb, cells[w], wpts, wbox, seeded ? -1 : 0, min(nc, C), monoC, &wb);
@@ -1488,6 +1664,8 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   A(&b.hC_T, (size_t)2 * P * sizeof(int));
   A(&b.cC, (size_t)2 * P * 2 * chunks_of(b.capC) * sizeof(float4));
   A(&b.cS, (size_t)2 * P * 2 * chunks_of(b.capS) * sizeof(float4));
+  A(&b.fC, (size_t)2 * P * 2 * subs_of(b.capC) * sizeof(float4));
+  A(&b.fS, (size_t)2 * P * 2 * subs_of(b.capS) * sizeof(float4));
   A(&b.hS_T, (size_t)2 * P * sizeof(int));
   A(&b.ind, (size_t)P * 3 * b.cap_q * sizeof(int));
   A(&b.sel, (size_t)P * b.cap_q * sizeof(float4));
@@ -1497,6 +1675,7 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   A(&b.part, (size_t)P * b.gq * max_iter * 28 * sizeof(double));  // (k_od_rows_small: per stored iteration)
   A(&b.done, (size_t)P * sizeof(int));
   A(&b.mono, (size_t)2 * P * 2 * sizeof(int));
+  A(&b.rstart, (size_t)2 * P * 2 * kRingTab * sizeof(int));
   if (A.err != hipSuccess) {
     od_free(b);
     return A.err;
@@ -1515,7 +1694,7 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
 void od_free(OdBuffers& b) {
   void* ptrs[] = {b.state, b.istate, b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
-                  b.ind, b.sel, b.q_cf, b.q_ok, b.part, b.done, b.mono};
+                  b.ind, b.sel, b.q_cf, b.q_ok, b.part, b.done, b.mono, b.rstart, b.fC, b.fS};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = OdBuffers();
@@ -1538,10 +1717,14 @@ void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
   jc.inv_h = 1.0f;
   jc.shift = 1;
   jc.chunks = b.cC + (size_t)buf * b.P * 2 * chunks_of(b.capC);
+  jc.fine = b.fC + (size_t)buf * b.P * 2 * subs_of(b.capC);
   jc.mono = b.mono + (size_t)buf * b.P * 2;
   jc.mono_stride = 2;
+  jc.rstart = b.rstart + (size_t)buf * b.P * 2 * kRingTab;
+  jc.rstart_stride = 2 * kRingTab;
   HashJob js = jc;
   js.mono = jc.mono + 1;
+  js.rstart = jc.rstart + kRingTab;
   js.pts = b.lastS + (size_t)buf * b.P * b.capS;
   js.pts_stride = b.capS;
   js.count = b.nlast + buf * 2 + 1;
@@ -1551,6 +1734,7 @@ void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
   js.tsize = b.hS_T + buf * b.P;
   js.tmax = b.tS;
   js.chunks = b.cS + (size_t)buf * b.P * 2 * chunks_of(b.capS);
+  js.fine = b.fS + (size_t)buf * b.P * 2 * subs_of(b.capS);
   hash_build_pair(jc, js, b.P, st, true);
 }
 

@@ -15,6 +15,13 @@ namespace loam {
 #endif
 constexpr int kChunk = LOAM_OD_CHUNK;  // points per chunk box (<= 64)
 __host__ __device__ inline int chunks_of(int cap) { return (cap + kChunk - 1) / kChunk; }
+// the association's best-first ring windows (ring-monotone clouds) visit kSub-point sub-chunks
+#ifndef LOAM_WIN_SUB
+#define LOAM_WIN_SUB 32
+#endif
+constexpr int kSub = LOAM_WIN_SUB;
+static_assert(kSub == 16 || kSub == 32 || kSub == 64, "sub-chunks of 16, 32 or 64 points");
+__host__ __device__ inline int subs_of(int cap) { return (cap + kSub - 1) / kSub; }
 constexpr int kOdSum = 6, kOdMatP = 12, kOdImu = 48, kOdStateFloats = 64;
 // per-problem int state
 enum { kIsDegenerate = 0, kIsCornerLastNum, kIsSurfLastNum, kIsIters, kIsAssoc, kIsRows, kIsQueries,
@@ -53,11 +60,15 @@ struct HashJob {
   int shift;            // T = pow2 >= count >> shift
   float4* chunks;       // optional [P][2 * chunks_of(pts_stride)]: per 64-point chunk of the source
                         // order, (min x, y, z, min ring) and (max x, y, z, max ring)
+  float4* fine = nullptr;   // optional [P][2 * subs_of(pts_stride)]: the same boxes per kSub-point sub-chunk
   uint32_t* rec = nullptr;  // optional [P][tmax]: bucket b's range packed as start | count << 19
                             // (hash_rec), kRecNone when it does not fit
   int* mono = nullptr;      // optional: mono[p * mono_stride] = 1 when the cloud's rings int(w) never
   int mono_stride = 1;      // decrease in index order (the association's window bounds rely on it)
+  int* rstart = nullptr;    // optional [P][rstart_stride]: rstart[r] = first index whose ring int(w) >= r
+  int rstart_stride = 0;    // (r in [0, kRingTab), n when none; meaningful for a ring-monotone cloud only)
 };
+constexpr int kRingTab = 66;  // rings 0..63 (n_rings <= 64) and two past the last
 constexpr uint32_t kRecNone = 0xffffffffu;
 LOAM_HD uint32_t hash_rec(int start, int count) {
   return start < (1 << 19) && count < (1 << 13) ? (uint32_t)start | ((uint32_t)count << 19) : kRecNone;
@@ -82,6 +93,8 @@ struct OdBuffers {
   int* hS_T = nullptr;      // [2][P]
   float4* cC = nullptr;     // [2][P][2 * chunks_of(capC)] chunk boxes of Last corner
   float4* cS = nullptr;     // [2][P][2 * chunks_of(capS)] chunk boxes of Last surf
+  float4* fC = nullptr;     // [2][P][2 * subs_of(capC)] sub-chunk boxes of Last corner (HashJob::fine)
+  float4* fS = nullptr;     // [2][P][2 * subs_of(capS)] sub-chunk boxes of Last surf
   float4* sel = nullptr;      // [P][cap_q] queries at the current transform (association rounds)
   int* ind = nullptr;         // [P][3][cap_q] association of every query (refreshed every 5th iteration)
   float4* q_cf = nullptr;     // [P][max_iter][cap_q] coefficients (zero when rejected)
@@ -89,6 +102,7 @@ struct OdBuffers {
   double* part = nullptr;     // [P][gq][28] per-workgroup JᵀJ | Jᵀb | rows
   int* done = nullptr;        // [P] workgroups of k_od_rows finished (the last one runs the step)
   int* mono = nullptr;        // [2][P][2] Last corner / surf of each buffer ring-monotone (HashJob::mono)
+  int* rstart = nullptr;      // [2][P][2][kRingTab] their ring start tables (HashJob::rstart)
   Tuning tune;                // host-side launch choices (od_solve)
 };
 

@@ -240,6 +240,9 @@ def _share_run(loam, sg, **tune):
     {"mp_fused_max": 0, "mp_iter_wide_max": 128},  # k_mp_iter<1024>
     {"vg_merge": 0},                         # the cube VoxelGrid cascade alone (no k_vg_merge)
     {"od_sel_min": 1024},                    # TransformToStart inside the association wave
+    {"od_win_mono": 3},                      # index-range ring windows (ring-monotone clouds)
+    {"od_win_mono": 1},
+    {"od_win_mono": 2},
 ], ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_launch_choices_at_8gpu_share(loam, oc, sg, tune):
     """every launch shape the engine can pick by batch size (include/loam/loam.h loam_set_tuning),
