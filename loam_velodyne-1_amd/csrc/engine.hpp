@@ -60,7 +60,9 @@ struct Tuning {
                            // else inside the association wave (k_od_assoc<., true>)
   int od_win_mono = 3;     // association rounds whose ring windows on ring-monotone Last clouds take the
                            // index-range search (wave_window_mono) instead of the walks: bit 0 the
-                           // first (unseeded) round, bit 1 the seeded ones
+                           // first (unseeded) round, bit 1 the seeded ones (round 4, 1024 problems:
+                           // k_od_assoc 2.76 -> 2.42 ms/step with both)
+  int od_win_mono_min = 2; // ... for P >= this (config 3's chain, P = 1: 0.733 -> 0.743 ms/sweep with them)
   // key = value (loam_set_tuning); false for an unknown key or a value out of range
   bool set(const char* key, long long v) {
     struct K { const char* n; int* f; long long lo, hi; };
@@ -73,7 +75,7 @@ struct Tuning {
                     {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20},
                     {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20},
                     {"vg_merge", &vg_merge, 0, 1}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
-                    {"od_win_mono", &od_win_mono, 0, 3}};
+                    {"od_win_mono", &od_win_mono, 0, 3}, {"od_win_mono_min", &od_win_mono_min, 1, 1 << 20}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {
         if (v < k.lo || v > k.hi) return false;

@@ -891,7 +891,7 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
   int* ind = b.ind + (size_t)p * 3 * b.cap_q;
   int wpts = 0, wbox = 0;  // wave-uniform work counters (loam_stats od_assoc_gathered / _boxes)
   const bool seeded = ist[kIsIters] > 0;  // ind holds this frame's previous round
-  const bool use_mono = (b.tune.od_win_mono & (seeded ? 2 : 1)) != 0;
+  const bool use_mono = b.P >= b.tune.od_win_mono_min && (b.tune.od_win_mono & (seeded ? 2 : 1)) != 0;
   const bool tight = LOAM_WIN_TIGHTEN == 1 || (LOAM_WIN_TIGHTEN == 2 && !seeded);
   const int hCT = b.hC_T[last_buf * b.P + p], hST = b.hS_T[last_buf * b.P + p];
   const bool monoC = b.mono[lp * 2 + 0] != 0, monoS = b.mono[lp * 2 + 1] != 0;

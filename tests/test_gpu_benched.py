@@ -48,12 +48,14 @@ def test_config3_full220_device_chain(loam, sg):
     check_config3_full(traj)
 
 
-def test_config3_full220_no_vg_merge(loam, sg):
-    """the 220 sweeps through loam_chain_sweep without the incremental cube VoxelGrid (k_vg_merge,
-    the default, takes the growing map's big cubes; here the cascade sorts them): every pose and
+@pytest.mark.parametrize("tune", [{"vg_merge": 0}, {"od_win_mono_min": 1}], ids=["no_vg_merge", "win_mono"])
+def test_config3_full220_tuned(loam, sg, tune):
+    """the 220 sweeps through loam_chain_sweep with a non-default launch choice: the cascade instead of
+    the incremental cube VoxelGrid (k_vg_merge, the default, takes the growing map's big cubes); the
+    association's index-range ring windows (batch default) on the streaming path.  Every pose and
     registered cloud as the golden run"""
     e = loam.Engine(loam.default_config())
-    e.set_tuning(vg_merge=0)
+    e.set_tuning(**tune)
     traj = []
     for k, sw in enumerate(sg.stream_sweeps(220, 1)):
         rc, pub, od, aft, bef, reg = e.chain_sweep(sw, stamp=0.1 * k, registered=True)
