@@ -903,6 +903,87 @@ LOAM_HD void jacobi(float* A, float* W, float* V, int* iws) {
   }
 }
 
+// jacobi<3> in registers, bit-identical: only the upper triangle (a01, a02, a12) and the diagonal
+// (W) are read by jacobi<N>, and for N = 3 the pivot (k, l) is one of three pairs, so every step is a
+// select over the three cases with the same operations in the same order (the row / column maxima
+// tracking, the rotation, the final descending sort).  A: row-major 3x3 (symmetric; not modified).
+LOAM_HD void jacobi3_reg(const float* A, float* W, float* V) {
+  const float eps = 1.1920928955078125e-07f;
+  float a01 = A[1], a02 = A[2], a12 = A[5];
+  float w0 = A[0], w1 = A[4], w2 = A[8];
+  float v00 = 1, v01 = 0, v02 = 0, v10 = 0, v11 = 1, v12 = 0, v20 = 0, v21 = 0, v22 = 1;
+  // indR[0] in {1, 2}: the first maximum of |a01|, |a02|; indR[1] = 2; indC[1] = 0; indC[2] in {0, 1}
+  int r0 = fabsf(a01) < fabsf(a02) ? 2 : 1, c2 = fabsf(a02) < fabsf(a12) ? 1 : 0;
+  for (int iters = 0; iters < 3 * 3 * 30; ++iters) {
+    // pivot scan (jacobi<N>: rows k < N - 1 by indR, then columns i >= 1 by indC, strict <)
+    int k = 0, l = r0;
+    float mv = fabsf(r0 == 1 ? a01 : a02);
+    if (mv < fabsf(a12)) { mv = fabsf(a12); k = 1; l = 2; }  // row 1: indR[1] = 2
+    if (mv < fabsf(a01)) { mv = fabsf(a01); k = 0; l = 1; }  // column 1: indC[1] = 0
+    {
+      const float val = fabsf(c2 == 0 ? a02 : a12);           // column 2: indC[2]
+      if (mv < val) { mv = val; k = c2; l = 2; }
+    }
+    const bool p01 = k == 0 && l == 1, p02 = k == 0 && l == 2;  // else (1, 2)
+    const float p = p01 ? a01 : (p02 ? a02 : a12);
+    if (fabsf(p) <= eps) break;
+    const float wk = k == 0 ? w0 : w1, wl = l == 1 ? w1 : w2;
+    float y = (float)((wl - wk) * 0.5);
+    float t = fabsf(y) + hypot_cv(p, y);
+    float s = hypot_cv(p, t);
+    const float c = t / s;
+    s = p / s;
+    t = (p / t) * p;
+    if (y < 0) { s = -s; t = -t; }
+    // A[k][l] = 0; W[k] -= t; W[l] += t
+    if (p01) a01 = 0;
+    if (p02) a02 = 0;
+    if (!p01 && !p02) a12 = 0;
+    if (k == 0) w0 -= t; else w1 -= t;
+    if (l == 1) w1 += t; else w2 += t;
+    // the one off-diagonal pair the rotation touches: (0, 1) -> (a02, a12) [i > l]; (0, 2) ->
+    // (a01, a12) [k < i < l]; (1, 2) -> (a01, a02) [i < k]
+    {
+      const float x0 = p01 ? a02 : a01, x1 = p02 || p01 ? a12 : a02;
+      const float n0 = x0 * c - x1 * s, n1 = x0 * s + x1 * c;
+      if (p01) { a02 = n0; a12 = n1; }
+      else if (p02) { a01 = n0; a12 = n1; }
+      else { a01 = n0; a02 = n1; }
+    }
+    // eigenvector rows k and l
+    {
+      const float k0 = k == 0 ? v00 : v10, k1 = k == 0 ? v01 : v11, k2 = k == 0 ? v02 : v12;
+      const float l0 = l == 1 ? v10 : v20, l1 = l == 1 ? v11 : v21, l2 = l == 1 ? v12 : v22;
+      const float nk0 = k0 * c - l0 * s, nl0 = k0 * s + l0 * c;
+      const float nk1 = k1 * c - l1 * s, nl1 = k1 * s + l1 * c;
+      const float nk2 = k2 * c - l2 * s, nl2 = k2 * s + l2 * c;
+      if (k == 0) { v00 = nk0; v01 = nk1; v02 = nk2; } else { v10 = nk0; v11 = nk1; v12 = nk2; }
+      if (l == 1) { v10 = nl0; v11 = nl1; v12 = nl2; } else { v20 = nl0; v21 = nl1; v22 = nl2; }
+    }
+    // the maxima of rows / columns k and l (jacobi<N> refreshes indR[idx] for idx < N - 1 and
+    // indC[idx] for idx > 0; indR[1] and indC[1] are fixed for N = 3)
+    if (k == 0) r0 = fabsf(a01) < fabsf(a02) ? 2 : 1;
+    if (l == 2) c2 = fabsf(a02) < fabsf(a12) ? 1 : 0;
+  }
+  // descending selection sort with the eigenvector rows (jacobi<N>'s order)
+  auto swap_rows = [](float& wa, float& wb, float& a0, float& a1, float& a2, float& b0, float& b1, float& b2) {
+    float q = wa; wa = wb; wb = q;
+    q = a0; a0 = b0; b0 = q;
+    q = a1; a1 = b1; b1 = q;
+    q = a2; a2 = b2; b2 = q;
+  };
+  {
+    int m = 0;
+    if (w0 < w1) m = 1;
+    if ((m == 0 ? w0 : w1) < w2) m = 2;
+    if (m == 1) swap_rows(w0, w1, v00, v01, v02, v10, v11, v12);
+    if (m == 2) swap_rows(w0, w2, v00, v01, v02, v20, v21, v22);
+  }
+  if (w1 < w2) swap_rows(w1, w2, v10, v11, v12, v20, v21, v22);
+  W[0] = w0; W[1] = w1; W[2] = w2;
+  V[0] = v00; V[1] = v01; V[2] = v02; V[3] = v10; V[4] = v11; V[5] = v12; V[6] = v20; V[7] = v21; V[8] = v22;
+}
+
 // jacobi<6> by one whole wave (all 64 lanes active), bit-identical: lane 6r + c (< 36) holds
 // A[r][c] and V[r][c] in registers, lanes 0..5 hold W and the tracked row / column maxima (indR,
 // indC).  A rotation's element pairs are disjoint, so every affected lane updates at once from its

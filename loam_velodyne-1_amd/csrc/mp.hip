@@ -1290,13 +1290,10 @@ LOAM_D void mp_fit_compute(bool corner, const float4 (&nb)[5], float* jw, float4
       a22 += ay * ay; a23 += ay * az; a33 += az * az;
     }
     a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
-    float* A1 = jw;
-    float* D1 = jw + 9;
-    float* V1 = jw + 12;
-    int* iws = (int*)(jw + 21);
-    A1[0] = a11; A1[1] = a12; A1[2] = a13; A1[3] = a12; A1[4] = a22;
-    A1[5] = a23; A1[6] = a13; A1[7] = a23; A1[8] = a33;
-    loamla::jacobi<3>(A1, D1, V1, iws);
+    (void)jw;
+    const float A1[9] = {a11, a12, a13, a12, a22, a23, a13, a23, a33};
+    float D1[3], V1[9];
+    loamla::jacobi3_reg(A1, D1, V1);  // (bit-identical to jacobi<3>: tests/test_jacobi3.py)
     const bool valid = D1[0] > 3 * D1[1];
     g0 = make_float4((float)(D(cx) + 0.1 * D(V1[0])), (float)(D(cy) + 0.1 * D(V1[1])),
                      (float)(D(cz) + 0.1 * D(V1[2])), valid ? 1.0f : 0.0f);
