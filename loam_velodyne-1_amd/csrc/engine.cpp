@@ -61,7 +61,7 @@ FeatView feat_view(const SrBuffers& b, int first, int step) {
 
 }  // namespace
 
-constexpr size_t kMetaBytes = 8192, kMetaSumSlot = kMetaBytes - 64;  // (loam_ctx::meta)
+constexpr size_t kMetaBytes = 8192;  // (loam_ctx::meta)
 
 struct loam_ctx {
   loam_config cfg;
@@ -93,15 +93,15 @@ struct loam_ctx {
   MpBuffers mpb;
   std::vector<float4> stage;
   Staging pin;                  // pinned staging of the node calls' host clouds
-  // pinned scratch (8 KB) for the node calls' small D2H / H2D copies, as ints:
-  //   scan registration  [0] n, [1..4] feature counts, [5] nfull, [6] error bits
-  //   odometry           [0..4] counts, [8..19] imu_trans, [24..27] init-frame Last counts,
-  //                      [32 ..) state (kOdStateFloats), istate, nlast (4), nfullEnd (2) downloads
-  //   mapping            [0..2] counts, [4..9] pose, [10..11] IMU roll / pitch, [12] IMU flag,
-  //                      [16 ..) state (kMpStateFloats), istate, nreg downloads (mp.hip)
-  //   kMetaSumSlot       odometry's transformSum written back to the device (an async H2D that
-  //                      may still be pending when the next phase reuses the areas above)
+  // pinned scratch (8 KB) for the node calls' host-side small values, as ints:
+  //   odometry           [8..19] imu_trans, [24..27]
+  //                      init-frame Last counts (downloaded), [32 ..) the host copy of the
+  //                      state / istate / nlast / nfullEnd download (from xb)
+  // Every other small transfer of a node call goes through k_xfer (xfer.hpp): host values in its
+  // arguments, device values into xb (scan registration, odometry and mapping regions)
   char* meta = nullptr;
+  XferBuf xb;          // mapped, coherent host block for k_xfer's downloads (xfer.hpp regions)
+  StreamIo io() { StreamIo s; s.meta = meta; s.xb = xb; s.e0 = ev[4]; s.e1 = ev[5]; return s; }
   loam_stats stats;
   Prof prof;
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -132,11 +132,17 @@ int check_cloud_in(const loam_cloud_in& c, int cap) {
 
 // (records need not be 4-byte aligned: a PointCloud2's data follows a variable-length header in
 // the message, and loam_pc2_cloud hands it over in place)
-void pack(const loam_cloud_in& c, float4* dst) {
+// points [i0, i1) of c into dst[i0 ..) as float4 (w is not read by the device: a 16-byte stride
+// is copied as is)
+void pack(const loam_cloud_in& c, float4* dst, size_t i0, size_t i1) {
   const char* base = (const char*)c.data;
-  for (uint32_t i = 0; i < c.count; ++i) {
+  if (c.stride_bytes == 16) {
+    std::memcpy(dst + i0, base + i0 * 16, (i1 - i0) * 16);
+    return;
+  }
+  for (size_t i = i0; i < i1; ++i) {
     float q[3];
-    std::memcpy(q, base + (size_t)i * c.stride_bytes, sizeof(q));
+    std::memcpy(q, base + i * c.stride_bytes, sizeof(q));
     dst[i] = make_float4(q[0], q[1], q[2], 0.0f);
   }
 }
@@ -261,6 +267,9 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   if (he != hipSuccess) x->sr_imu_dev = nullptr;
   if (he == hipSuccess) he = hipHostMalloc((void**)&x->meta, kMetaBytes, hipHostMallocDefault);
   if (he != hipSuccess) x->meta = nullptr;
+  if (he == hipSuccess) he = hipHostMalloc((void**)&x->xb.h, kXferBytes, hipHostMallocCoherent | hipHostMallocMapped);
+  if (he != hipSuccess) x->xb.h = nullptr;
+  if (he == hipSuccess) he = hipHostGetDevicePointer((void**)&x->xb.d, x->xb.h, 0);
   x->sr_imu = new loamimu::SrQueue();
   std::memset(x->sr_imu, 0, sizeof(loamimu::SrQueue));
   x->sr_imu->last = -1;
@@ -288,6 +297,7 @@ void loam_destroy(loam_ctx* x) {
   mp_free(x->mpb);
   if (x->sr_imu_dev) (void)hipFree(x->sr_imu_dev);
   if (x->meta) (void)hipHostFree(x->meta);
+  if (x->xb.h) (void)hipHostFree(x->xb.h);
   x->pin.release();
   delete x->sr_imu;
   for (auto& e : x->ev)
@@ -387,12 +397,19 @@ int sr_frame(loam_ctx* x, double stamp, const loam_cloud_in& raw, loam_features*
   HIP_TRY(x->pin.reserve((size_t)2 * n, x->st));
   float4* praw = x->pin.buf;  // the sweep packed straight into pinned memory
   float4* pfull = x->pin.buf + n;  // the early download of the full cloud (below)
-  pack(raw, praw);
   x->pin.off = (size_t)2 * n;
-  int* mi = (int*)x->meta;  // [0] n, [1..4] counts, [5] nfull, [6] err
-  mi[0] = n;
-  if (n) HIP_TRY(hipMemcpyAsync(b.raw, praw, (size_t)n * sizeof(float4), hipMemcpyHostToDevice, x->st));
-  HIP_TRY(hipMemcpyAsync(b.raw_n, &mi[0], sizeof(int), hipMemcpyHostToDevice, x->st));
+  // packed in chunks, each chunk's DMA overlapping the packing of the next
+  constexpr size_t kPackChunk = 8192;
+  for (size_t i0 = 0; i0 < (size_t)n; i0 += kPackChunk) {
+    const size_t i1 = std::min((size_t)n, i0 + kPackChunk);
+    pack(raw, praw, i0, i1);
+    HIP_TRY(hipMemcpyAsync(b.raw + i0, praw + i0, (i1 - i0) * sizeof(float4), hipMemcpyHostToDevice, x->st));
+  }
+  {
+    Xfer xp;
+    xp.put(b.raw_n, &n, sizeof(int));
+    xfer_launch(xp, x->st);
+  }
   SrParams prm = sr_params(x);
   loamimu::SrQueue* q = x->sr_imu;
   const size_t tail = offsetof(loamimu::SrQueue, front);  // pointers, Start, Cur, FromStart
@@ -418,9 +435,16 @@ int sr_frame(loam_ctx* x, double stamp, const loam_cloud_in& raw, loam_features*
   if (q->last >= 0)
     HIP_TRY(hipMemcpyAsync((char*)q + tail, (const char*)x->sr_imu_dev + tail, sizeof(*q) - tail,
                            hipMemcpyDeviceToHost, x->st));
-  HIP_TRY(hipMemcpyAsync(&mi[1], b.cnt, 4 * sizeof(int), hipMemcpyDeviceToHost, x->st));
-  HIP_TRY(hipMemcpyAsync(&mi[5], b.n_full, sizeof(int), hipMemcpyDeviceToHost, x->st));
-  HIP_TRY(hipMemcpyAsync(&mi[6], b.err, sizeof(int), hipMemcpyDeviceToHost, x->st));
+  // [1..4] counts, [5] nfull, [6] err into the mapped host block, one launch
+  const int* mi = (const int*)(x->xb.h + kXferSr) - 1;
+  {
+    Xfer xg;
+    xg.get(x->xb.d + kXferSr, b.cnt, 4 * sizeof(int));
+    xg.get(x->xb.d + kXferSr + 16, b.n_full, sizeof(int));
+    xg.get(x->xb.d + kXferSr + 20, b.err, sizeof(int));
+    xfer_launch(xg, x->st);
+  }
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(x->st));
   int cnt[4] = {mi[1], mi[2], mi[3], mi[4]};
   const int nfull = mi[5];
@@ -515,10 +539,13 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
     return rc;
   int cnt[5] = {(int)in->sharp.count, (int)in->less_sharp.count, (int)in->flat.count,
                 (int)in->less_flat.count, (int)in->full.count};
-  int* mi = (int*)x->meta;  // [0..4] counts, [8..19] imu_trans, [24..] downloads below
-  std::memcpy(mi, cnt, sizeof(cnt));
-  HIP_TRY(hipMemcpyAsync(fi.cnt, mi, 4 * sizeof(int), hipMemcpyHostToDevice, x->st));
-  HIP_TRY(hipMemcpyAsync(fi.n_full, &mi[4], sizeof(int), hipMemcpyHostToDevice, x->st));
+  {
+    Xfer xp;
+    xp.put(fi.cnt, cnt, 4 * sizeof(int));
+    xp.put(fi.n_full, &cnt[4], sizeof(int));
+    xfer_launch(xp, x->st);
+    HIP_TRY(hipGetLastError());
+  }
   return od_frame(x, feat_view(fi, 0, 1), cnt, in->imu_trans, late ? &in->full : nullptr, sum_out, corner_last,
                   surf_last, full_end, published, nullptr);
 }
@@ -536,7 +563,11 @@ int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_i
   const bool late = late_full != nullptr;
   std::memset(&x->stats, 0, sizeof(x->stats));
   // imuTransHandler (:330-351): this sweep's /imu_trans, in the state order load_imu reads
-  HIP_TRY(hipMemcpyAsync(o.state + kOdImu, mi + 8, 12 * sizeof(float), hipMemcpyHostToDevice, x->st));
+  {
+    Xfer xp;
+    xp.put(o.state + kOdImu, mi + 8, 12 * sizeof(float));
+    xfer_launch(xp, x->st);
+  }
   if (!x->od_inited) {  // src/laserOdometry.cpp:427-456: Last = raw lessSharp / lessFlat, no L-M
     // :451-452 transformSum[0] += imuPitchStart; transformSum[2] += imuRollStart (from zero)
     const float sum0[3] = {0.0f + imu_in[0], 0.0f, 0.0f + imu_in[2]};
@@ -576,15 +607,25 @@ int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_i
   HIP_TRY(hipEventRecord(x->ev[1], x->st));
   HIP_TRY(hipGetLastError());
   x->od_last = nxt;
+  // state (kOdStateFloats), istate (kOdStateInts), nlast (4), nfullEnd (2) into the mapped host
+  // block in one launch, then copied out (the host edits st / ist below)
+  static_assert(kXferOd + 4 * (kOdStateFloats + kOdStateInts + 6) <= kXferMp, "odometry transfer region");
+  {
+    Xfer xg;
+    char* d = x->xb.d + kXferOd;
+    xg.get(d, o.state, kOdStateFloats * sizeof(float));
+    xg.get(d + 4 * kOdStateFloats, o.istate, kOdStateInts * sizeof(int));
+    xg.get(d + 4 * (kOdStateFloats + kOdStateInts), o.nlast, 4 * sizeof(int));
+    xg.get(d + 4 * (kOdStateFloats + kOdStateInts + 4), o.nfullEnd, 2 * sizeof(int));
+    xfer_launch(xg, x->st);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(x->st));
   float* st = (float*)(mi + 32);                  // kOdStateFloats
   int* ist = mi + 32 + kOdStateFloats;             // kOdStateInts
   int* nl = ist + kOdStateInts;                    // 4
   int* nfe = nl + 4;                               // 2
-  HIP_TRY(hipMemcpyAsync(st, o.state, kOdStateFloats * sizeof(float), hipMemcpyDeviceToHost, x->st));
-  HIP_TRY(hipMemcpyAsync(ist, o.istate, kOdStateInts * sizeof(int), hipMemcpyDeviceToHost, x->st));
-  HIP_TRY(hipMemcpyAsync(nl, o.nlast, 4 * sizeof(int), hipMemcpyDeviceToHost, x->st));
-  HIP_TRY(hipMemcpyAsync(nfe, o.nfullEnd, 2 * sizeof(int), hipMemcpyDeviceToHost, x->st));
-  HIP_TRY(hipStreamSynchronize(x->st));
+  std::memcpy(st, x->xb.h + kXferOd, 4 * (kOdStateFloats + kOdStateInts + 6));
   if (ist[kIsErr]) return fail(LOAM_E_CAPACITY, "odometry capacity exceeded");
   {  // :830-856 (k_od_fini's body, host side): transformSum from this frame's transform
     const float* q = imu_in;
@@ -596,10 +637,11 @@ int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_i
     loampose::accumulate_pose(st, m, x->od_sum);
     ist[kIsQueries] = ist[kIsAssoc] * (cnt[0] + cnt[2]);
     // keep the device copy of transformSum current (it is seeded only on the init frame): the
-    // host result goes back from the pinned state block, ordered before the next frame's kernels
-    float* slot = (float*)(x->meta + kMetaSumSlot);  // (its own slot: see loam_ctx::meta)
-    std::memcpy(slot, x->od_sum, sizeof(loam_pose6));
-    HIP_TRY(hipMemcpyAsync(o.state + kOdSum, slot, sizeof(loam_pose6), hipMemcpyHostToDevice, x->st));
+    // host result goes back in k_xfer's arguments, ordered before the next frame's kernels
+    Xfer xp;
+    xp.put(o.state + kOdSum, x->od_sum, sizeof(loam_pose6));
+    xfer_launch(xp, x->st);
+    HIP_TRY(hipGetLastError());
   }
   if (sum_out) std::memcpy(sum_out, x->od_sum, sizeof(loam_pose6));
   *published = LOAM_PUB_POSE;
@@ -654,7 +696,7 @@ int loam_mapping(loam_ctx* x, double stamp, const loam_pose6* odom_sum, const lo
   const bool have_imu = loamimu::mp_lookup(x->mp_imu, stamp, rp[0], rp[1], front);
   bool updated = false;
   const int rc = mp_stream_frame(x->mp1, x->st, *odom_sum, *corner_last, *surf_last, *full_end, aft, bef,
-                                 registered, &x->stats, g_err, x->pin, x->meta, have_imu ? rp : nullptr, &updated,
+                                 registered, &x->stats, g_err, x->pin, x->io(), have_imu ? rp : nullptr, &updated,
                                  x->st2, x->join);
   if (have_imu && updated) x->mp_imu.front = front;  // the pointer walk happens inside transformUpdate
   x->surround_due = false;
@@ -702,7 +744,7 @@ int loam_chain_sweep(loam_ctx* x, double stamp, loam_cloud_in raw, loam_chain_ou
   loam_cloud_out* reg = out->registered.capacity ? &out->registered : nullptr;
   if (!reg) out->registered.count = 0;
   rc = mp_stream_frame_dev(x->mp1, x->st, out->od_sum, in, nl3, &out->aft, &out->bef, reg, &x->stats, g_err,
-                           x->pin, x->meta, have_imu ? rp : nullptr, &updated);
+                           x->pin, x->io(), have_imu ? rp : nullptr, &updated);
   if (have_imu && updated) x->mp_imu.front = front;
   x->surround_due = false;
   if (rc == LOAM_OK && ++x->map_frame_count >= 5) {  // :1038-1040
@@ -790,7 +832,7 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
   for (uint32_t i = 0; i < n; ++i)
     for (int k = 0; k < 2; ++k) {
       const loam_cloud_in& c = k == 0 ? prev[i] : cur[i];
-      pack(c, h.data());
+      pack(c, h.data(), 0, c.count);
       counts[2 * i + k] = (int)c.count;
       HIP_TRY(hipMemcpy(x->srb.raw + (size_t)(2 * i + k) * x->cap, h.data(), (size_t)c.count * sizeof(float4),
                         hipMemcpyHostToDevice));
@@ -966,3 +1008,16 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
 }
 
 }  // extern "C"
+
+namespace loam {
+__global__ __launch_bounds__(256) void k_xfer(Xfer x) {
+  for (int e = 0; e < x.n; ++e) {
+    uint32_t* d = x.dst[e];
+    const uint32_t* s = x.src[e];
+    for (int w = threadIdx.x; w < x.words[e]; w += 256) d[w] = s ? s[w] : x.imm[x.imm_off[e] + w];
+  }
+}
+void xfer_launch(const Xfer& x, hipStream_t st) {
+  if (x.n) hipLaunchKernelGGL(k_xfer, dim3(1), dim3(256), 0, st, x);
+}
+}  // namespace loam

@@ -40,9 +40,10 @@ struct Tuning {
   int od_lm_max = 0;       //   for od_lm_min <= P <= od_lm_max
   int od_fused_max = 0;    // k_od_rows<true> (step in the last workgroup) for P <= this, else + k_od_step
   int mp_small_max = 4;    // k_mp_lm_small (5-NN + fit + rows + step in one launch) for P <= this
-  int mp_fused_max = 128;  // the fit kernel (k_mp_fit<true> / k_mp_nnfit<true>) adds the rows and runs the
-                           // step in its last workgroup for P <= this, else k_mp_iter (round 4, with
-                           // k_mp_nnfit: 128 problems 3.25 -> 3.16 ms/step fused; 1024: 15.73 -> 16.32)
+  int mp_fused_max = 1 << 20;  // the fit kernel (k_mp_fit<true> / k_mp_nnfit<true>) adds the rows and runs
+                           // the step in its last workgroup for P <= this, else k_mp_iter (round 4, with
+                           // k_mp_nnfit: 128 problems 3.25 -> 3.16 ms/step fused; 1024: 15.73 -> 16.32
+                           // with the register reduce-scatter, 15.31 -> 15.23 with the LDS row sums)
   int nn_lanes = 1;        // lanes per query of the batch 5-NN (1, 2, 4) ...
   int nn_lanes_maxp = 256; //   for P <= this
   int od_assoc_wg = 64;    // k_od_assoc query waves (workgroups) per problem (batches, P >= 64)

@@ -2800,13 +2800,13 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
 }
 
 template <typename Hook>
-int mp_stream_run(MpBuffers& b, hipStream_t st, const MpInput& in, const int* n, hipEvent_t e0, hipEvent_t e1,
-                  loam_pose6* aft, loam_pose6* bef, loam_cloud_out* registered, loam_stats* stats, std::string& err,
-                  Staging& pin, void* meta, bool* updated, Hook hook);
+int mp_stream_run(MpBuffers& b, hipStream_t st, const MpInput& in, const int* n, loam_pose6* aft, loam_pose6* bef,
+                  loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, const StreamIo& io,
+                  bool* updated, Hook hook);
 
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
                     const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
-                    loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, void* meta,
+                    loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, const StreamIo& io,
                     const float* imu_rp, bool* updated, hipStream_t st2, hipEvent_t ev2) {
   if (corner.count > (uint32_t)b.capC || surf.count > (uint32_t)b.capS || full.count > (uint32_t)b.capS) {
     err = "mapping input cloud exceeds capacity";
@@ -2816,17 +2816,9 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
     err = "mapping input cloud pts is null";
     return LOAM_E_INVAL;
   }
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  hipError_t ce = hipEventCreate(&e0);
-  if (ce == hipSuccess) ce = hipEventCreate(&e1);
-  if (ce != hipSuccess) {
-    if (e0) (void)hipEventDestroy(e0);
-    err = std::string("mapping timing events: ") + hipGetErrorString(ce);
-    return LOAM_E_HIP;
-  }
-  // host inputs through the pinned arena / scratch: [0..2] counts, [4..9] pose, [10..11] IMU
-  // (roll, pitch), [12] IMU flag; downloads below from [16]
-  int* mi = (int*)meta;
+  // host inputs: [0..2] counts, [4..9] pose, [10..11] IMU (roll, pitch), [12] IMU flag, to the
+  // device in one k_xfer launch; downloads through io.xb (mp_stream_run)
+  int mi[16];
   int* n = mi;
   n[0] = (int)corner.count; n[1] = (int)surf.count; n[2] = (int)full.count;
   std::memcpy(mi + 4, &odom_sum, 6 * sizeof(float));
@@ -2842,13 +2834,16 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   // overlap the frame's kernels (enqueued just before k_mp_register)
   const bool late = st2 != nullptr && n[2] > 0;
   if (ue == hipSuccess && !late) ue = pin.up(st, b.inF, full.pts, (size_t)n[2]);
-  if (ue == hipSuccess) ue = hipMemcpyAsync(b.in_n, n, 3 * sizeof(int), hipMemcpyHostToDevice, st);
-  if (ue == hipSuccess) ue = hipMemcpyAsync(b.in_pose, mi + 4, 6 * sizeof(float), hipMemcpyHostToDevice, st);
-  if (ue == hipSuccess) ue = hipMemcpyAsync(b.state + kMpImuRP, mi + 10, 2 * sizeof(float), hipMemcpyHostToDevice, st);
-  if (ue == hipSuccess) ue = hipMemcpyAsync(b.istate + kMiImu, mi + 12, sizeof(int), hipMemcpyHostToDevice, st);
+  if (ue == hipSuccess) {
+    Xfer xp;
+    xp.put(b.in_n, n, 3 * sizeof(int));
+    xp.put(b.in_pose, mi + 4, 6 * sizeof(float));
+    xp.put(b.state + kMpImuRP, mi + 10, 2 * sizeof(float));
+    xp.put(b.istate + kMiImu, mi + 12, sizeof(int));
+    xfer_launch(xp, st);
+    ue = hipGetLastError();
+  }
   if (ue != hipSuccess) {
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     err = std::string("mapping upload: ") + hipGetErrorString(ue);
     return LOAM_E_HIP;
   }
@@ -2858,7 +2853,7 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
   in.ncorner = b.in_n; in.nsurf = b.in_n + 1; in.nfull = b.in_n + 2;
   in.ncorner_stride = in.nsurf_stride = in.nfull_stride = 3;
   in.pose = b.in_pose; in.pose_stride = 6;
-  return mp_stream_run(b, st, in, n, e0, e1, aft, bef, registered, stats, err, pin, meta, updated, [&]() {
+  return mp_stream_run(b, st, in, n, aft, bef, registered, stats, err, pin, io, updated, [&]() {
     if (!late) return hipSuccess;
     hipError_t le = pin.up(st2, b.inF, full.pts, (size_t)n[2]);
     if (le == hipSuccess) le = hipEventRecord(ev2, st2);
@@ -2871,65 +2866,62 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
 // published Last / full-end buffers, src, with device counts); n3: their counts on the host
 int mp_stream_frame_dev(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const MpInput& src, const int* n3,
                         loam_pose6* aft, loam_pose6* bef, loam_cloud_out* registered, loam_stats* stats,
-                        std::string& err, Staging& pin, void* meta, const float* imu_rp, bool* updated) {
+                        std::string& err, Staging& pin, const StreamIo& io, const float* imu_rp, bool* updated) {
   if (n3[0] > b.capC || n3[1] > b.capS || n3[2] > b.capS) {
     err = "mapping input cloud exceeds capacity";
     return LOAM_E_CAPACITY;
   }
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  hipError_t ce = hipEventCreate(&e0);
-  if (ce == hipSuccess) ce = hipEventCreate(&e1);
-  if (ce != hipSuccess) {
-    if (e0) (void)hipEventDestroy(e0);
-    err = std::string("mapping timing events: ") + hipGetErrorString(ce);
-    return LOAM_E_HIP;
-  }
-  int* mi = (int*)meta;  // as mp_stream_frame: [4..9] pose, [10..11] IMU (roll, pitch), [12] IMU flag
-  std::memcpy(mi + 4, &odom_sum, 6 * sizeof(float));
+  // as mp_stream_frame: the pose, the IMU (roll, pitch) and flag in one k_xfer launch
   const float rp[2] = {imu_rp ? imu_rp[0] : 0.0f, imu_rp ? imu_rp[1] : 0.0f};
-  std::memcpy(mi + 10, rp, sizeof(rp));
-  mi[12] = imu_rp ? 1 : 0;
-  hipError_t ue = hipMemcpyAsync(b.in_pose, mi + 4, 6 * sizeof(float), hipMemcpyHostToDevice, st);
-  if (ue == hipSuccess) ue = hipMemcpyAsync(b.state + kMpImuRP, mi + 10, 2 * sizeof(float), hipMemcpyHostToDevice, st);
-  if (ue == hipSuccess) ue = hipMemcpyAsync(b.istate + kMiImu, mi + 12, sizeof(int), hipMemcpyHostToDevice, st);
+  const int flag = imu_rp ? 1 : 0;
+  Xfer xp;
+  xp.put(b.in_pose, &odom_sum, 6 * sizeof(float));
+  xp.put(b.state + kMpImuRP, rp, sizeof(rp));
+  xp.put(b.istate + kMiImu, &flag, sizeof(int));
+  xfer_launch(xp, st);
+  const hipError_t ue = hipGetLastError();
   if (ue != hipSuccess) {
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     err = std::string("mapping upload: ") + hipGetErrorString(ue);
     return LOAM_E_HIP;
   }
   MpInput in = src;
   in.pose = b.in_pose;
   in.pose_stride = 6;
-  return mp_stream_run(b, st, in, n3, e0, e1, aft, bef, registered, stats, err, pin, meta, updated,
+  return mp_stream_run(b, st, in, n3, aft, bef, registered, stats, err, pin, io, updated,
                        []() { return hipSuccess; });
 }
 
 // the frame's kernels on `in` and the downloads (both stream entry points); hook: called just
-// before k_mp_register (the late full-cloud staging); consumes e0 / e1
+// before k_mp_register (the late full-cloud staging)
 template <typename Hook>
-int mp_stream_run(MpBuffers& b, hipStream_t st, const MpInput& in, const int* n, hipEvent_t e0, hipEvent_t e1,
-                  loam_pose6* aft, loam_pose6* bef, loam_cloud_out* registered, loam_stats* stats, std::string& err,
-                  Staging& pin, void* meta, bool* updated, Hook hook) {
-  int* mi = (int*)meta;
+int mp_stream_run(MpBuffers& b, hipStream_t st, const MpInput& in, const int* n, loam_pose6* aft, loam_pose6* bef,
+                  loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, const StreamIo& io,
+                  bool* updated, Hook hook) {
+  const hipEvent_t e0 = io.e0, e1 = io.e1;
   hipError_t le = hipEventRecord(e0, st);
   mp_frame(b, in, st, nullptr, false, [&]() {
     if (le != hipSuccess) return;
     le = hook();
   }, std::max(n[0], n[1]));
   if (le == hipSuccess) le = hipEventRecord(e1, st);
-  float* sf = (float*)(mi + 16);                  // kMpStateFloats
-  int* si = mi + 16 + kMpStateFloats;             // kMpStateInts
-  int* pnreg = si + kMpStateInts;
-  hipError_t he = hipMemcpyAsync(sf, b.state, kMpStateFloats * sizeof(float), hipMemcpyDeviceToHost, st);
-  if (he == hipSuccess) he = hipMemcpyAsync(si, b.istate, kMpStateInts * sizeof(int), hipMemcpyDeviceToHost, st);
-  if (he == hipSuccess) he = hipMemcpyAsync(pnreg, b.nreg, sizeof(int), hipMemcpyDeviceToHost, st);
+  // state (kMpStateFloats), istate (kMpStateInts), nreg into the mapped host block, one launch
+  static_assert(kXferMp + 4 * (kMpStateFloats + kMpStateInts + 1) <= kXferBytes, "mapping transfer region");
+  const float* sf = (const float*)(io.xb.h + kXferMp);
+  const int* si = (const int*)(io.xb.h + kXferMp) + kMpStateFloats;
+  const int* pnreg = si + kMpStateInts;
+  {
+    Xfer xg;
+    char* d = io.xb.d + kXferMp;
+    xg.get(d, b.state, kMpStateFloats * sizeof(float));
+    xg.get(d + kMpStateFloats * 4, b.istate, kMpStateInts * sizeof(int));
+    xg.get(d + (kMpStateFloats + kMpStateInts) * 4, b.nreg, sizeof(int));
+    xfer_launch(xg, st);
+  }
+  hipError_t he = hipGetLastError();
   if (he == hipSuccess) he = hipStreamSynchronize(st);
   const int nreg = *pnreg;
   float ms = 0;
   (void)hipEventElapsedTime(&ms, e0, e1);
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   if (he == hipSuccess) he = b.take_error();
   if (he == hipSuccess) he = le;
   if (he != hipSuccess) {

@@ -8,6 +8,7 @@
 #include <string>
 
 #include "engine.hpp"
+#include "xfer.hpp"
 #include "od.hpp"
 
 namespace loam {
@@ -165,13 +166,13 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof = null
 // transformUpdate ran (the caller then commits its IMU queue pointer)
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
                     const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
-                    loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, void* meta,
+                    loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, const StreamIo& io,
                     const float* imu_rp = nullptr, bool* updated = nullptr, hipStream_t st2 = nullptr,
                     hipEvent_t ev2 = nullptr);
 // the same frame on clouds already on the device (src: pointers + device counts, n3: host counts)
 int mp_stream_frame_dev(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const MpInput& src, const int* n3,
                         loam_pose6* aft, loam_pose6* bef, loam_cloud_out* registered, loam_stats* stats,
-                        std::string& err, Staging& pin, void* meta, const float* imu_rp = nullptr,
+                        std::string& err, Staging& pin, const StreamIo& io, const float* imu_rp = nullptr,
                         bool* updated = nullptr);
 // /laser_cloud_surround of the last streaming frame (instance 0): its 5x5x5 cube neighbourhood
 // concatenated and VoxelGrid 0.2 (src/laserMapping.cpp:1038-1058)
