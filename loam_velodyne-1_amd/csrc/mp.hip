@@ -671,7 +671,8 @@ __global__ __launch_bounds__(NT) void k_vg_big(VgJob j) {
 // is "too small" are left to the cascade (skip[s] = 0).
 // (segments beyond the cascade's LDS tiers, which k_vg_big would sort through global memory; the
 // LDS tiers measured faster than the merge on 2k-12k segments)
-constexpr int kVgMergeMin = 12288, kVgMergeNew = 8192;
+// (Tuning::vg_merge_min: 12288 by default, the largest LDS tier)
+constexpr int kVgMergeNew = 8192;
 template <int NT, int NEW>
 __global__ __launch_bounds__(NT) void k_vg_merge(VgJob j) {
   static_assert((NEW & (NEW - 1)) == 0 && NEW % NT == 0 && NEW <= 65536, "bitonic sort / scan layout");
@@ -2371,7 +2372,7 @@ __global__ __launch_bounds__(kMpThreads) void k_mp_vseg(MpBuffers b) {
     } else {
       b.vg_lin[atomicAdd(b.vg_cnt + 2, 1)] = sidx;
       // long segments with a short appended tail: the incremental VoxelGrid may take them
-      if (b.tune.vg_merge && n > kVgMergeMin && nold > 0 && n - nold <= kVgMergeNew)
+      if (b.tune.vg_merge && n > b.tune.vg_merge_min && nold > 0 && n - nold <= kVgMergeNew)
         b.vg_mlist[atomicAdd(b.vg_cnt + 3, 1)] = sidx;
     }
   }

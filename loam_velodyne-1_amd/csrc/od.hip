@@ -1188,12 +1188,6 @@ LOAM_D void od_row_accum(const OdJf& e, float4 c4, bool okit, double (&acc)[28])
   acc[27] += okit ? 1.0 : 0.0;
 }
 
-LOAM_D void od_trig(const float* T, float* trig) {
-  for (int k = 0; k < 3; ++k) {
-    trig[2 * k] = (float)dsin(1 * T[k]);
-    trig[2 * k + 1] = (float)dcos(1 * T[k]);
-  }
-}
 
 // one iteration's rows (lane per query): this iteration's residual + weight stored at [iter][q];
 // then the Jacobian of every row accumulated so far (Q12: rows of iterations 0..iter, all
@@ -1216,7 +1210,10 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(INF 
   float T[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) T[k] = st[k];
-  if (tid == 0) od_trig(T, trig);
+  if (tid < 6) {  // the angles' double sin / cos as floats, one per lane (trig[2k], trig[2k + 1]: sin, cos of T[k])
+    const float ang = st[tid >> 1];
+    trig[tid] = (float)((tid & 1) ? dcos(ang) : dsin(ang));
+  }
   const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
   const int q = blk.x * kOdThreads + tid;
   const size_t lp = (size_t)last_buf * b.P + p;
@@ -1314,7 +1311,10 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows_small(OdBuffers b, FeatV
   float T[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) T[k] = st[k];
-  if (tid == 0) od_trig(T, trig);
+  if (tid < 6) {  // the angles' double sin / cos as floats, one per lane (trig[2k], trig[2k + 1]: sin, cos of T[k])
+    const float ang = st[tid >> 1];
+    trig[tid] = (float)((tid & 1) ? dcos(ang) : dsin(ang));
+  }
   const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
   const int q = blockIdx.x * kOdThreads + tid;
   const size_t lp = (size_t)last_buf * b.P + p;
@@ -1477,7 +1477,7 @@ __global__ __launch_bounds__(kOdLmThreads) void k_od_lm(OdBuffers b, FeatView f,
   float4* qpts = od_lm_dyn;                  // [4][CQ]
   float* jf = (float*)(od_lm_dyn + 4 * CQ);  // [17][CQ]
   float* st = b.state + (size_t)p * kOdStateFloats;
-  if (tid < 6) {  // the transform, and od_trig's sin / cos of its angles one per lane
+  if (tid < 6) {  // the transform, and the double sin / cos of its angles one per lane
     Tsh[tid] = st[tid];
     const float a = st[tid >> 1];
     trig[tid] = (float)((tid & 1) ? dcos(a) : dsin(a));
