@@ -652,7 +652,11 @@ def main(argv=None):
         "data": "synthetic (seeded VLP-16 ray-cast sweeps, random planes+edges scenes; bags unavailable offline)",
         "config": {"workload": "config4: independent VLP-16 problems (SR prev+cur, odometry L-M, mapping L-M)",
                    "problems_per_gpu": B, "global_batch": world * B, "points_per_sweep": 28800,
-                   "split": args.split, "parallelism": f"shard{world}", **({"tuning": tune} if tune else {})},
+                   "split": args.split, "parallelism": f"shard{world}",
+                   "step_overlap": ("each step enqueues the next step's scan registration on a third stream "
+                                    "(tuning sr_ahead, P >= 64); the K timed steps include K scan "
+                                    "registrations (loam_batch_sync waits for the one enqueued ahead)"),
+                   **({"tuning": tune} if tune else {})},
         "roofline": roof,
         "roofline_kernels": roof_all,
         "pipeline": pipeline,

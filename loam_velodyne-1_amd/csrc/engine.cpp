@@ -89,6 +89,22 @@ struct loam_ctx {
   // batch (config 4)
   int P = 0;
   SrBuffers srb;
+  // tune.sr_ahead: the next step's scan registration runs one step ahead on st3, into the other of
+  // two buffer sets, as soon as the step that last read that set has finished (step_done); the
+  // step that consumes it waits on sr_done.  The raw sweeps are uploaded into both sets.
+  SrBuffers srb2;
+  hipStream_t st3 = nullptr;
+  hipEvent_t sr_done = nullptr, step_done[2] = {nullptr, nullptr};
+  bool step_done_rec[2] = {false, false};
+  int sr_idx = 0;         // the set the next step reads
+  bool sr_ready = false;  // its scan registration is already enqueued (st3, sr_done)
+  int srb_last = 0;       // the set of the last enqueued step (loam_batch_download)
+  SrBuffers& srbuf(int i) { return i ? srb2 : srb; }
+  void reset_ahead() {    // (after draining st3)
+    sr_ready = false;
+    sr_idx = srb_last = 0;
+    step_done_rec[0] = step_done_rec[1] = false;
+  }
   OdBuffers odb;
   MpBuffers mpb;
   std::vector<float4> stage;
@@ -248,6 +264,10 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   for (auto& e : x->ev)
     if (he == hipSuccess) he = hipEventCreate(&e);
   if (he == hipSuccess && hipStreamCreateWithFlags(&x->st2, hipStreamNonBlocking) != hipSuccess) x->st2 = nullptr;
+  if (he == hipSuccess && hipStreamCreateWithFlags(&x->st3, hipStreamNonBlocking) != hipSuccess) x->st3 = nullptr;
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&x->sr_done, hipEventDisableTiming);
+  for (auto& e : x->step_done)
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
   x->pin.streams[0] = x->st;
   x->pin.streams[1] = x->st2;
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->fork, hipEventDisableTiming);
@@ -288,11 +308,13 @@ void loam_destroy(loam_ctx* x) {
   if (!x) return;
   (void)hipSetDevice(x->device);
   if (x->st) (void)hipStreamSynchronize(x->st);
+  if (x->st3) (void)hipStreamSynchronize(x->st3);
   sr_free(x->sr1);
   sr_free(x->odin);
   od_free(x->od1);
   mp_free(x->mp1);
   sr_free(x->srb);
+  sr_free(x->srb2);
   od_free(x->odb);
   mp_free(x->mpb);
   if (x->sr_imu_dev) (void)hipFree(x->sr_imu_dev);
@@ -308,6 +330,10 @@ void loam_destroy(loam_ctx* x) {
   if (x->join) (void)hipEventDestroy(x->join);
   if (x->fork2) (void)hipEventDestroy(x->fork2);
   if (x->join2) (void)hipEventDestroy(x->join2);
+  if (x->sr_done) (void)hipEventDestroy(x->sr_done);
+  for (auto& e : x->step_done)
+    if (e) (void)hipEventDestroy(e);
+  if (x->st3) (void)hipStreamDestroy(x->st3);
   if (x->st2) (void)hipStreamDestroy(x->st2);
   if (x->st) (void)hipStreamDestroy(x->st);
   delete x;
@@ -322,6 +348,7 @@ int loam_set_stream_priority(loam_ctx* x, int priority) {
   // drain the old streams first: a failure here leaves the context on its old streams, unchanged
   HIP_TRY(hipStreamSynchronize(x->st));
   if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
+  if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));
   hipStream_t st = nullptr, st2 = nullptr;
   HIP_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio));
   if (hipStreamCreateWithPriority(&st2, hipStreamNonBlocking, prio) != hipSuccess) {
@@ -343,6 +370,7 @@ int loam_set_tuning(loam_ctx* x, const char* key, long long value) {
   if (!t.set(key, value)) return fail(LOAM_E_INVAL, std::string("unknown tuning key or value out of range: ") + key);
   x->tune = t;
   if (x->st) (void)hipStreamSynchronize(x->st);
+  if (x->st3) (void)hipStreamSynchronize(x->st3);
   x->drop_graph();  // (captured with the old choices)
   x->od1.tune = x->odb.tune = t;
   x->mp1.tune = x->mpb.tune = t;
@@ -805,20 +833,26 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
     if (!rc) rc = check_cloud_in(cur[i], x->cap);
     if (rc) return rc;
   }
+  // (a step ahead may still read the raw sweeps or write its buffer set)
+  HIP_TRY(hipStreamSynchronize(x->st));
+  if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));
+  x->reset_ahead();
   if ((int)n != x->P) {
-    HIP_TRY(hipStreamSynchronize(x->st));
     if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
     x->drop_graph();  // (its kernels' arguments name the old buffers)
     sr_free(x->srb);
+    sr_free(x->srb2);
     od_free(x->odb);
     mp_free(x->mpb);
     x->P = 0;  // no batch until every buffer of the new size exists
     hipError_t he = sr_alloc(x->srb, 2 * (int)n, x->cap, x->R);
+    if (he == hipSuccess) he = sr_alloc(x->srb2, 2 * (int)n, x->cap, x->R);
     if (he == hipSuccess) he = od_alloc(x->odb, (int)n, x->R, x->cap, (int)x->cfg.od_max_iter);
     if (he == hipSuccess)
       he = mp_alloc(x->mpb, (int)n, x->R, x->cap, mp_batch_map_capacity(x->cap), (int)x->cfg.mp_max_iter);
     if (he != hipSuccess) {
       sr_free(x->srb);
+      sr_free(x->srb2);
       od_free(x->odb);
       mp_free(x->mpb);
       return fail(LOAM_E_NOMEM, std::string("batch allocation failed: ") + hipGetErrorString(he));
@@ -838,6 +872,9 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
                         hipMemcpyHostToDevice));
     }
   HIP_TRY(hipMemcpy(x->srb.raw_n, counts.data(), counts.size() * sizeof(int), hipMemcpyHostToDevice));
+  // the second set's raw sweeps (tune.sr_ahead)
+  HIP_TRY(hipMemcpy(x->srb2.raw, x->srb.raw, (size_t)2 * n * x->cap * sizeof(float4), hipMemcpyDeviceToDevice));
+  HIP_TRY(hipMemcpy(x->srb2.raw_n, x->srb.raw_n, counts.size() * sizeof(int), hipMemcpyDeviceToDevice));
   return LOAM_OK;
 }
 
@@ -849,13 +886,21 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   OdBuffers& o = x->odb;
   hipError_t e = hipSuccess;
   auto T = [&](hipError_t r) { if (e == hipSuccess) e = r; };
+  // scan registration of this step: already enqueued one step ahead (st3), or here
+  const int idx = x->sr_idx;
+  SrBuffers& sb = x->srbuf(idx);
   if (events) T(hipEventRecord(x->ev[0], x->st));
   x->prof.begin(x->st);
-  sr_launch(x->srb, sr_params(x), x->st, pf);
+  if (x->sr_ready) {
+    T(hipStreamWaitEvent(x->st, x->sr_done, 0));
+    x->sr_ready = false;
+  } else {
+    sr_launch(sb, sr_params(x), x->st, pf);
+  }
   if (events) T(hipEventRecord(x->ev[1], x->st));
   T(hipMemsetAsync(o.state, 0, (size_t)P * kOdStateFloats * sizeof(float), x->st));
   T(hipMemsetAsync(o.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st));
-  const FeatView fprev = feat_view(x->srb, 0, 2), fcur = feat_view(x->srb, 1, 2);
+  const FeatView fprev = feat_view(sb, 0, 2), fcur = feat_view(sb, 1, 2);
   // odometry seeded from prev as a solved zero-increment frame, then one loop body on cur
   // (the full clouds' TransformToEnd happens in mapping's registration kernel, mp_batch_frame*)
   hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fprev, 0, 1, 0);
@@ -898,6 +943,19 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   side.fork[0] = x->fork; side.join[0] = x->join; side.fork[1] = x->fork2; side.join[1] = x->join2;
   mp_batch_frame2(x->mpb, o, fcur, x->st, pf, overlap ? &side : nullptr);
   if (events) T(hipEventRecord(x->ev[3], x->st));
+  x->srb_last = idx;
+  // the next step's scan registration into the other set, once the step that last read it is done
+  // (not in a captured graph, whose replays would all reuse one set, nor in the profiling pass)
+  if (x->st3 && x->tune.sr_ahead > 0 && P >= x->tune.sr_ahead && events && !pf) {
+    T(hipEventRecord(x->step_done[idx], x->st));
+    x->step_done_rec[idx] = true;
+    const int nx = 1 - idx;
+    if (x->step_done_rec[nx]) T(hipStreamWaitEvent(x->st3, x->step_done[nx], 0));
+    sr_launch(x->srbuf(nx), sr_params(x), x->st3, nullptr);
+    T(hipEventRecord(x->sr_done, x->st3));
+    x->sr_ready = true;
+    x->sr_idx = nx;
+  }
   T(hipGetLastError());
   return e;
 }
@@ -939,6 +997,8 @@ int loam_batch_sync(loam_ctx* x) {
   if (!x) return fail(LOAM_E_INVAL, "null argument");
   HIP_TRY(hipSetDevice(x->device));
   HIP_TRY(hipStreamSynchronize(x->st));
+  // (a step's work includes the scan registration it enqueued for the next step)
+  if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));
   return LOAM_OK;
 }
 
@@ -951,9 +1011,9 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
   std::vector<int> ist((size_t)P * kOdStateInts), srerr(2 * P), cnt(8 * P), nfull(2 * P), nl(4 * P);
   HIP_TRY(hipMemcpy(st.data(), x->odb.state, st.size() * sizeof(float), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(ist.data(), x->odb.istate, ist.size() * sizeof(int), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(srerr.data(), x->srb.err, srerr.size() * sizeof(int), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(cnt.data(), x->srb.cnt, cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(nfull.data(), x->srb.n_full, nfull.size() * sizeof(int), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(srerr.data(), x->srbuf(x->srb_last).err, srerr.size() * sizeof(int), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(cnt.data(), x->srbuf(x->srb_last).cnt, cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(nfull.data(), x->srbuf(x->srb_last).n_full, nfull.size() * sizeof(int), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(nl.data(), x->odb.nlast, nl.size() * sizeof(int), hipMemcpyDeviceToHost));
   for (int i = 0; i < 2 * P; ++i) {
     int rc = sr_errors(srerr[i]);
@@ -973,7 +1033,7 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
   int raw_n[2];
   (void)raw_n;
   std::vector<int> rn(2 * P);
-  HIP_TRY(hipMemcpy(rn.data(), x->srb.raw_n, rn.size() * sizeof(int), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(rn.data(), x->srbuf(x->srb_last).raw_n, rn.size() * sizeof(int), hipMemcpyDeviceToHost));
   for (int i = 0; i < 2 * P; ++i) s.n_raw += rn[i];
   for (int i = 0; i < P; ++i) {
     const int* q = &ist[(size_t)i * kOdStateInts];

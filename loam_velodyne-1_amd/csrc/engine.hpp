@@ -58,6 +58,12 @@ struct Tuning {
   int vg_merge = 1;        // the cubes' VoxelGrid merges an old sorted prefix with the appended tail
                            // (k_vg_merge; config 3's big cubes: 95 -> 50 us per mapping frame)
   int vg_merge_min = 12288;  // ... for segments of more than this many points
+  int sr_ahead = 64;       // for P >= this (0: never), loam_batch_run enqueues the next step's scan
+                           // registration one step ahead (a second buffer set, a third stream), where
+                           // it overlaps this step's latency-bound odometry / mapping launches.  A
+                           // throughput choice for batches of independent problems: a one-problem
+                           // latency (config 2) would count the next problem's work ahead of time
+                           // (round 4: 128 problems 3.04 -> 2.90 ms/step, 1024: 15.12 -> 14.96)
   int od_sel_min = 64;     // TransformToStart of the queries as its own launch (k_od_sel) for P >= this,
                            // else inside the association wave (k_od_assoc<., true>)
   int od_win_mono = 3;     // association rounds whose ring windows on ring-monotone Last clouds take the
@@ -76,7 +82,8 @@ struct Tuning {
                     {"od_rows_deep_max", &od_rows_deep_max, 0, 1 << 20}, {"nn_wg", &nn_wg, 0, 4096},
                     {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20},
                     {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20},
-                    {"vg_merge", &vg_merge, 0, 1}, {"vg_merge_min", &vg_merge_min, 0, 1 << 20}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
+                    {"vg_merge", &vg_merge, 0, 1}, {"vg_merge_min", &vg_merge_min, 0, 1 << 20},
+                    {"sr_ahead", &sr_ahead, 0, 1 << 20}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
                     {"od_win_mono", &od_win_mono, 0, 3}, {"od_win_mono_min", &od_win_mono_min, 1, 1 << 20}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {

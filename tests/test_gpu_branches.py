@@ -215,7 +215,9 @@ def _share_run(loam, sg, **tune):
     e = loam.Engine()
     e.set_tuning(**tune)
     e.batch_upload(prevs, curs)
-    for _ in range(2 if tune.get("graph") else 1):  # (a graph: its capture, then a replay)
+    # (a graph: its capture, then a replay; a step ahead: both buffer sets, each step consuming the
+    # scan registration its predecessor enqueued)
+    for _ in range(3 if tune.get("sr_ahead") else 2 if tune.get("graph") else 1):
         e.batch_run()
     od, aft, st = e.batch_download()
     e.close()
@@ -244,6 +246,7 @@ def _share_run(loam, sg, **tune):
     {"od_win_mono": 1},
     {"od_win_mono": 2},
     {"od_win_mono": 0},
+    {"sr_ahead": 1},                         # scan registration one step ahead (runs twice)
 ], ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_launch_choices_at_8gpu_share(loam, oc, sg, tune):
     """every launch shape the engine can pick by batch size (include/loam/loam.h loam_set_tuning),
