@@ -95,6 +95,7 @@ struct loam_ctx {
   SrBuffers srb2;
   hipStream_t st3 = nullptr;
   hipEvent_t sr_done = nullptr, step_done[2] = {nullptr, nullptr};
+  hipEvent_t ahead_at = nullptr;  // the point of this step after which it may start (tune.sr_ahead_at)
   bool step_done_rec[2] = {false, false};
   int sr_idx = 0;         // the set the next step reads
   bool sr_ready = false;  // its scan registration is already enqueued (st3, sr_done)
@@ -266,6 +267,7 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   if (he == hipSuccess && hipStreamCreateWithFlags(&x->st2, hipStreamNonBlocking) != hipSuccess) x->st2 = nullptr;
   if (he == hipSuccess && hipStreamCreateWithFlags(&x->st3, hipStreamNonBlocking) != hipSuccess) x->st3 = nullptr;
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->sr_done, hipEventDisableTiming);
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&x->ahead_at, hipEventDisableTiming);
   for (auto& e : x->step_done)
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
   x->pin.streams[0] = x->st;
@@ -331,6 +333,7 @@ void loam_destroy(loam_ctx* x) {
   if (x->fork2) (void)hipEventDestroy(x->fork2);
   if (x->join2) (void)hipEventDestroy(x->join2);
   if (x->sr_done) (void)hipEventDestroy(x->sr_done);
+  if (x->ahead_at) (void)hipEventDestroy(x->ahead_at);
   for (auto& e : x->step_done)
     if (e) (void)hipEventDestroy(e);
   if (x->st3) (void)hipStreamDestroy(x->st3);
@@ -901,12 +904,19 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   T(hipMemsetAsync(o.state, 0, (size_t)P * kOdStateFloats * sizeof(float), x->st));
   T(hipMemsetAsync(o.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st));
   const FeatView fprev = feat_view(sb, 0, 2), fcur = feat_view(sb, 1, 2);
+  const bool ahead = x->st3 && x->tune.sr_ahead > 0 && P >= x->tune.sr_ahead && events && !pf;
+  const int ahead_at = x->tune.sr_ahead_at >= 0 ? x->tune.sr_ahead_at : (P <= 256 ? 2 : 1);
+  auto ahead_point = [&](int at) {
+    if (ahead && ahead_at == at) T(hipEventRecord(x->ahead_at, x->st));
+  };
+  ahead_point(0);
   // odometry seeded from prev as a solved zero-increment frame, then one loop body on cur
   // (the full clouds' TransformToEnd happens in mapping's registration kernel, mp_batch_frame*)
   hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fprev, 0, 1, 0);
   x->prof.mark("k_od_end_seed");
   od_build_hashes(o, 0, x->st);
   x->prof.mark("k_hash_build_last");
+  ahead_point(1);
   // mapping frame 1 (prev into an empty map at the origin) reads only the seeding's Last[0] /
   // fullEnd[0]: it runs on a second stream beside the odometry solve, whose L-M iterations are
   // chains of small latency-bound launches that leave most of the chip idle.  The profiling pass
@@ -937,6 +947,7 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   } else {
     mp_batch_frame1(x->mpb, o, fprev, x->st, pf);
   }
+  ahead_point(2);
   // (frame 1 is done: the second stream is free for frame 2's independent branches)
   SideStream side;
   side.st = x->st2;
@@ -946,11 +957,12 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   x->srb_last = idx;
   // the next step's scan registration into the other set, once the step that last read it is done
   // (not in a captured graph, whose replays would all reuse one set, nor in the profiling pass)
-  if (x->st3 && x->tune.sr_ahead > 0 && P >= x->tune.sr_ahead && events && !pf) {
+  if (ahead) {
     T(hipEventRecord(x->step_done[idx], x->st));
     x->step_done_rec[idx] = true;
     const int nx = 1 - idx;
     if (x->step_done_rec[nx]) T(hipStreamWaitEvent(x->st3, x->step_done[nx], 0));
+    T(hipStreamWaitEvent(x->st3, x->ahead_at, 0));
     sr_launch(x->srbuf(nx), sr_params(x), x->st3, nullptr);
     T(hipEventRecord(x->sr_done, x->st3));
     x->sr_ready = true;

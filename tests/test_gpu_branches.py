@@ -246,7 +246,8 @@ def _share_run(loam, sg, **tune):
     {"od_win_mono": 1},
     {"od_win_mono": 2},
     {"od_win_mono": 0},
-    {"sr_ahead": 1},                         # scan registration one step ahead (runs twice)
+    {"sr_ahead": 1},                         # scan registration one step ahead (three steps)
+    {"sr_ahead": 1, "sr_ahead_at": 0},
 ], ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_launch_choices_at_8gpu_share(loam, oc, sg, tune):
     """every launch shape the engine can pick by batch size (include/loam/loam.h loam_set_tuning),
