@@ -96,6 +96,10 @@ struct loam_ctx {
   hipStream_t st3 = nullptr;
   hipEvent_t sr_done = nullptr, step_done[2] = {nullptr, nullptr};
   hipEvent_t ahead_at = nullptr;  // the point of this step after which it may start (tune.sr_ahead_at)
+  // ... followed by the next step's odometry seed (Last[0] and its hashes, into the other istate
+  // set), once this step's second mapping frame begins (the odometry no longer reads Last[0])
+  hipEvent_t seed_at = nullptr, seed_done = nullptr;
+  bool seed_ready = false;
   bool step_done_rec[2] = {false, false};
   int sr_idx = 0;         // the set the next step reads
   bool sr_ready = false;  // its scan registration is already enqueued (st3, sr_done)
@@ -103,6 +107,7 @@ struct loam_ctx {
   SrBuffers& srbuf(int i) { return i ? srb2 : srb; }
   void reset_ahead() {    // (after draining st3)
     sr_ready = false;
+    seed_ready = false;
     sr_idx = srb_last = 0;
     step_done_rec[0] = step_done_rec[1] = false;
   }
@@ -268,6 +273,8 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   if (he == hipSuccess && hipStreamCreateWithFlags(&x->st3, hipStreamNonBlocking) != hipSuccess) x->st3 = nullptr;
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->sr_done, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->ahead_at, hipEventDisableTiming);
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_at, hipEventDisableTiming);
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_done, hipEventDisableTiming);
   for (auto& e : x->step_done)
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
   x->pin.streams[0] = x->st;
@@ -334,6 +341,8 @@ void loam_destroy(loam_ctx* x) {
   if (x->join2) (void)hipEventDestroy(x->join2);
   if (x->sr_done) (void)hipEventDestroy(x->sr_done);
   if (x->ahead_at) (void)hipEventDestroy(x->ahead_at);
+  if (x->seed_at) (void)hipEventDestroy(x->seed_at);
+  if (x->seed_done) (void)hipEventDestroy(x->seed_done);
   for (auto& e : x->step_done)
     if (e) (void)hipEventDestroy(e);
   if (x->st3) (void)hipStreamDestroy(x->st3);
@@ -901,8 +910,8 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
     sr_launch(sb, sr_params(x), x->st, pf);
   }
   if (events) T(hipEventRecord(x->ev[1], x->st));
+  o.istate = o.istate_set[idx];  // (this step's; the kernels take the buffers by value)
   T(hipMemsetAsync(o.state, 0, (size_t)P * kOdStateFloats * sizeof(float), x->st));
-  T(hipMemsetAsync(o.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st));
   const FeatView fprev = feat_view(sb, 0, 2), fcur = feat_view(sb, 1, 2);
   const bool ahead = x->st3 && x->tune.sr_ahead > 0 && P >= x->tune.sr_ahead && events && !pf;
   const int ahead_at = x->tune.sr_ahead_at >= 0 ? x->tune.sr_ahead_at : (P <= 256 ? 2 : 1);
@@ -912,10 +921,16 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   ahead_point(0);
   // odometry seeded from prev as a solved zero-increment frame, then one loop body on cur
   // (the full clouds' TransformToEnd happens in mapping's registration kernel, mp_batch_frame*)
-  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fprev, 0, 1, 0);
-  x->prof.mark("k_od_end_seed");
-  od_build_hashes(o, 0, x->st);
-  x->prof.mark("k_hash_build_last");
+  if (x->seed_ready) {  // enqueued one step ahead (st3, seed_done)
+    T(hipStreamWaitEvent(x->st, x->seed_done, 0));
+    x->seed_ready = false;
+  } else {
+    T(hipMemsetAsync(o.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st));
+    hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fprev, 0, 1, 0);
+    x->prof.mark("k_od_end_seed");
+    od_build_hashes(o, 0, x->st);
+    x->prof.mark("k_hash_build_last");
+  }
   ahead_point(1);
   // mapping frame 1 (prev into an empty map at the origin) reads only the seeding's Last[0] /
   // fullEnd[0]: it runs on a second stream beside the odometry solve, whose L-M iterations are
@@ -948,6 +963,7 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
     mp_batch_frame1(x->mpb, o, fprev, x->st, pf);
   }
   ahead_point(2);
+  if (ahead) T(hipEventRecord(x->seed_at, x->st));
   // (frame 1 is done: the second stream is free for frame 2's independent branches)
   SideStream side;
   side.st = x->st2;
@@ -967,6 +983,17 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
     T(hipEventRecord(x->sr_done, x->st3));
     x->sr_ready = true;
     x->sr_idx = nx;
+    // the next step's odometry seed: Last[0] / its hashes are free once this step's odometry is
+    // done (the second mapping frame reads Last[1] and the state only); its counts go to the other
+    // istate set, which the next step reads
+    T(hipStreamWaitEvent(x->st3, x->seed_at, 0));
+    OdBuffers on = o;
+    on.istate = o.istate_set[nx];
+    T(hipMemsetAsync(on.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st3));
+    hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st3, on, feat_view(x->srbuf(nx), 0, 2), 0, 1, 0);
+    od_build_hashes(on, 0, x->st3);
+    T(hipEventRecord(x->seed_done, x->st3));
+    x->seed_ready = true;
   }
   T(hipGetLastError());
   return e;
@@ -1019,6 +1046,7 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
   HIP_TRY(hipSetDevice(x->device));
   const int P = x->P;
   HIP_TRY(hipStreamSynchronize(x->st));
+  if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));  // (the work enqueued ahead rewrites Last[0] alike)
   std::vector<float> st((size_t)P * kOdStateFloats);
   std::vector<int> ist((size_t)P * kOdStateInts), srerr(2 * P), cnt(8 * P), nfull(2 * P), nl(4 * P);
   HIP_TRY(hipMemcpy(st.data(), x->odb.state, st.size() * sizeof(float), hipMemcpyDeviceToHost));

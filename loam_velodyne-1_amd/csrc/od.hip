@@ -1649,7 +1649,9 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   b.tC = next_pow2(b.capC);
   b.tS = next_pow2(b.capS) > 65536 ? 65536 : next_pow2(b.capS);
   A(&b.state, (size_t)P * kOdStateFloats * sizeof(float));
-  A(&b.istate, (size_t)P * kOdStateInts * sizeof(int));
+  A(&b.istate_set[0], (size_t)P * kOdStateInts * sizeof(int));
+  A(&b.istate_set[1], (size_t)P * kOdStateInts * sizeof(int));
+  b.istate = b.istate_set[0];
   A(&b.lastC, (size_t)2 * P * b.capC * sizeof(float4));
   A(&b.lastS, (size_t)2 * P * b.capS * sizeof(float4));
   A(&b.fullEnd, (size_t)2 * P * b.capS * sizeof(float4));
@@ -1682,7 +1684,8 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   }
   if (A.err == hipSuccess) A.err = hipMemset(b.done, 0, (size_t)P * sizeof(int));
   if (A.err == hipSuccess) A.err = hipMemset(b.state, 0, (size_t)P * kOdStateFloats * sizeof(float));
-  if (A.err == hipSuccess) A.err = hipMemset(b.istate, 0, (size_t)P * kOdStateInts * sizeof(int));
+  for (int k = 0; k < 2; ++k)
+    if (A.err == hipSuccess) A.err = hipMemset(b.istate_set[k], 0, (size_t)P * kOdStateInts * sizeof(int));
   if (A.err == hipSuccess) A.err = hipMemset(b.nlast, 0, (size_t)P * 4 * sizeof(int));
   if (A.err == hipSuccess) A.err = hipMemset(b.nfullEnd, 0, (size_t)P * 2 * sizeof(int));
   if (A.err == hipSuccess) A.err = hipMemset(b.hC_T, 0, (size_t)2 * P * sizeof(int));
@@ -1692,7 +1695,7 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
 }
 
 void od_free(OdBuffers& b) {
-  void* ptrs[] = {b.state, b.istate, b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
+  void* ptrs[] = {b.state, b.istate_set[0], b.istate_set[1], b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
                   b.ind, b.sel, b.q_cf, b.q_ok, b.part, b.done, b.mono, b.rstart, b.fC, b.fS};
   for (void* q : ptrs)
