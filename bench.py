@@ -653,9 +653,11 @@ def main(argv=None):
         "config": {"workload": "config4: independent VLP-16 problems (SR prev+cur, odometry L-M, mapping L-M)",
                    "problems_per_gpu": B, "global_batch": world * B, "points_per_sweep": 28800,
                    "split": args.split, "parallelism": f"shard{world}",
-                   "step_overlap": ("each step enqueues the next step's scan registration on a third stream "
-                                    "(tuning sr_ahead, P >= 64); the K timed steps include K scan "
-                                    "registrations (loam_batch_sync waits for the one enqueued ahead)"),
+                   "step_overlap": ("consecutive steps run as a software pipeline (tuning step_pipe, P >= 64): "
+                                    "step k's odometry beside step k-1's mapping, step k+1's scan "
+                                    "registration + odometry seed enqueued ahead; the K timed steps "
+                                    "contain exactly K of each stage (loam_batch_sync waits for all "
+                                    "streams, including the stage enqueued ahead)"),
                    **({"tuning": tune} if tune else {})},
         "roofline": roof,
         "roofline_kernels": roof_all,

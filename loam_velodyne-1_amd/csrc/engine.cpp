@@ -100,14 +100,22 @@ struct loam_ctx {
   // set), once this step's second mapping frame begins (the odometry no longer reads Last[0])
   hipEvent_t seed_at = nullptr, seed_done = nullptr;
   bool seed_ready = false;
+  // tune.step_pipe: consecutive steps overlap — the odometry of a step (st) beside the mapping of the
+  // previous one (st4), the scan registration + seed of the next (st3); hand-offs by events (batch_enqueue_pipe)
+  hipStream_t st4 = nullptr;
+  hipEvent_t od_done = nullptr, mp1_done = nullptr, inputs_read = nullptr, a_start = nullptr, b_last = nullptr;
+  hipEvent_t mp_done[2] = {nullptr, nullptr};
+  bool mp_done_rec[2] = {false, false}, inputs_read_rec = false, b_used = false;
   bool step_done_rec[2] = {false, false};
   int sr_idx = 0;         // the set the next step reads
   bool sr_ready = false;  // its scan registration is already enqueued (st3, sr_done)
   int srb_last = 0;       // the set of the last enqueued step (loam_batch_download)
   SrBuffers& srbuf(int i) { return i ? srb2 : srb; }
-  void reset_ahead() {    // (after draining st3)
+  void reset_ahead() {    // (after draining st3 / st4)
     sr_ready = false;
     seed_ready = false;
+    mp_done_rec[0] = mp_done_rec[1] = false;
+    inputs_read_rec = b_used = false;
     sr_idx = srb_last = 0;
     step_done_rec[0] = step_done_rec[1] = false;
   }
@@ -274,6 +282,9 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->sr_done, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->ahead_at, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_at, hipEventDisableTiming);
+  if (he == hipSuccess && hipStreamCreateWithFlags(&x->st4, hipStreamNonBlocking) != hipSuccess) x->st4 = nullptr;
+  for (hipEvent_t* e : {&x->od_done, &x->mp1_done, &x->inputs_read, &x->a_start, &x->b_last, &x->mp_done[0], &x->mp_done[1]})
+    if (he == hipSuccess) he = hipEventCreateWithFlags(e, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_done, hipEventDisableTiming);
   for (auto& e : x->step_done)
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -318,6 +329,7 @@ void loam_destroy(loam_ctx* x) {
   (void)hipSetDevice(x->device);
   if (x->st) (void)hipStreamSynchronize(x->st);
   if (x->st3) (void)hipStreamSynchronize(x->st3);
+  if (x->st4) (void)hipStreamSynchronize(x->st4);
   sr_free(x->sr1);
   sr_free(x->odin);
   od_free(x->od1);
@@ -342,6 +354,9 @@ void loam_destroy(loam_ctx* x) {
   if (x->sr_done) (void)hipEventDestroy(x->sr_done);
   if (x->ahead_at) (void)hipEventDestroy(x->ahead_at);
   if (x->seed_at) (void)hipEventDestroy(x->seed_at);
+  for (hipEvent_t e : {x->od_done, x->mp1_done, x->inputs_read, x->a_start, x->b_last, x->mp_done[0], x->mp_done[1]})
+    if (e) (void)hipEventDestroy(e);
+  if (x->st4) (void)hipStreamDestroy(x->st4);
   if (x->seed_done) (void)hipEventDestroy(x->seed_done);
   for (auto& e : x->step_done)
     if (e) (void)hipEventDestroy(e);
@@ -361,6 +376,7 @@ int loam_set_stream_priority(loam_ctx* x, int priority) {
   HIP_TRY(hipStreamSynchronize(x->st));
   if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
   if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));
+  if (x->st4) HIP_TRY(hipStreamSynchronize(x->st4));
   hipStream_t st = nullptr, st2 = nullptr;
   HIP_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio));
   if (hipStreamCreateWithPriority(&st2, hipStreamNonBlocking, prio) != hipSuccess) {
@@ -382,7 +398,10 @@ int loam_set_tuning(loam_ctx* x, const char* key, long long value) {
   if (!t.set(key, value)) return fail(LOAM_E_INVAL, std::string("unknown tuning key or value out of range: ") + key);
   x->tune = t;
   if (x->st) (void)hipStreamSynchronize(x->st);
+  if (x->st2) (void)hipStreamSynchronize(x->st2);
   if (x->st3) (void)hipStreamSynchronize(x->st3);
+  if (x->st4) (void)hipStreamSynchronize(x->st4);
+  x->reset_ahead();
   x->drop_graph();  // (captured with the old choices)
   x->od1.tune = x->odb.tune = t;
   x->mp1.tune = x->mpb.tune = t;
@@ -847,7 +866,9 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
   }
   // (a step ahead may still read the raw sweeps or write its buffer set)
   HIP_TRY(hipStreamSynchronize(x->st));
+  if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
   if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));
+  if (x->st4) HIP_TRY(hipStreamSynchronize(x->st4));
   x->reset_ahead();
   if ((int)n != x->P) {
     if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
@@ -903,6 +924,10 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   SrBuffers& sb = x->srbuf(idx);
   if (events) T(hipEventRecord(x->ev[0], x->st));
   x->prof.begin(x->st);
+  if (x->b_used) {  // a pipelined step's mapping may still run on st4 (batch_enqueue_pipe)
+    T(hipStreamWaitEvent(x->st, x->b_last, 0));
+    x->b_used = false;
+  }
   if (x->sr_ready) {
     T(hipStreamWaitEvent(x->st, x->sr_done, 0));
     x->sr_ready = false;
@@ -911,6 +936,7 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   }
   if (events) T(hipEventRecord(x->ev[1], x->st));
   o.istate = o.istate_set[idx];  // (this step's; the kernels take the buffers by value)
+  o.state = o.state_set[idx];
   T(hipMemsetAsync(o.state, 0, (size_t)P * kOdStateFloats * sizeof(float), x->st));
   const FeatView fprev = feat_view(sb, 0, 2), fcur = feat_view(sb, 1, 2);
   const bool ahead = x->st3 && x->tune.sr_ahead > 0 && P >= x->tune.sr_ahead && events && !pf;
@@ -998,12 +1024,100 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   T(hipGetLastError());
   return e;
 }
+// The scan registration of the step reading buffer set i and its odometry seed (Last[0], its
+// hashes, the counts in istate set i), on st3.  Waits: the set's previous step is done with it
+// (mp_done[i]: its mapping, the last reader), and Last[0] is free (od_done / mp1_done of the step
+// before, passed as `free_last`).
+hipError_t enqueue_ahead(loam_ctx* x, int i, bool free_last) {
+  const int P = x->P;
+  OdBuffers on = x->odb;
+  hipError_t e = hipSuccess;
+  auto T = [&](hipError_t r) { if (e == hipSuccess) e = r; };
+  if (x->mp_done_rec[i]) T(hipStreamWaitEvent(x->st3, x->mp_done[i], 0));
+  T(hipStreamWaitEvent(x->st3, x->a_start, 0));  // (whatever ran on st before this call)
+  sr_launch(x->srbuf(i), sr_params(x), x->st3, nullptr);
+  T(hipEventRecord(x->sr_done, x->st3));
+  if (free_last) {
+    T(hipStreamWaitEvent(x->st3, x->od_done, 0));
+    T(hipStreamWaitEvent(x->st3, x->mp1_done, 0));
+  }
+  on.istate = on.istate_set[i];
+  T(hipMemsetAsync(on.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st3));
+  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st3, on, feat_view(x->srbuf(i), 0, 2), 0, 1, 0);
+  od_build_hashes(on, 0, x->st3);
+  T(hipEventRecord(x->seed_done, x->st3));
+  x->sr_ready = x->seed_ready = true;
+  return e;
+}
+
+// One batch step as a stage of a software pipeline over consecutive steps (tune.step_pipe):
+//   st3  scan registration + odometry seed of step k + 1 (enqueue_ahead)
+//   st   odometry of step k (L-M, pose accumulation, TransformToEnd of Last[1])
+//   st4  mapping of step k: frame 1 (needs the seed), frame 2 (needs the odometry), side branches on st2
+// so the odometry of step k + 1 runs beside the mapping of step k.  Buffers shared between steps:
+// the SR set and the odometry state / istate sets alternate; Last[0] is rewritten by the next seed
+// only after this step's odometry and frame 1 (od_done, mp1_done); Last[1] by the next odometry only
+// after this step's frame 2 has read it (inputs_read).  Every step does the same work as
+// batch_enqueue's; loam_batch_sync waits for all four streams.
+hipError_t batch_enqueue_pipe(loam_ctx* x) {
+  const int P = x->P;
+  OdBuffers& o = x->odb;
+  hipError_t e = hipSuccess;
+  auto T = [&](hipError_t r) { if (e == hipSuccess) e = r; };
+  const int idx = x->sr_idx, nx = 1 - idx;
+  SrBuffers& sb = x->srbuf(idx);
+  T(hipEventRecord(x->a_start, x->st));
+  T(hipEventRecord(x->ev[0], x->st));
+  if (!x->sr_ready || !x->seed_ready) T(enqueue_ahead(x, idx, false));
+  x->sr_ready = x->seed_ready = false;
+  const FeatView fprev = feat_view(sb, 0, 2), fcur = feat_view(sb, 1, 2);
+  // odometry (st)
+  o.istate = o.istate_set[idx];
+  o.state = o.state_set[idx];
+  T(hipStreamWaitEvent(x->st, x->sr_done, 0));
+  T(hipStreamWaitEvent(x->st, x->seed_done, 0));
+  T(hipEventRecord(x->ev[1], x->st));
+  T(hipMemsetAsync(o.state, 0, (size_t)P * kOdStateFloats * sizeof(float), x->st));
+  od_solve(o, fcur, 0, x->st, nullptr, /*device_fini=*/true);
+  if (x->inputs_read_rec) T(hipStreamWaitEvent(x->st, x->inputs_read, 0));  // (the last frame 2 read Last[1])
+  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, 1, 2, 0);
+  T(hipEventRecord(x->od_done, x->st));
+  T(hipEventRecord(x->ev[2], x->st));
+  // mapping (st4): frame 1 once the seed (and this call's earlier work on st) is there, frame 2 once
+  // the odometry is
+  T(hipStreamWaitEvent(x->st4, x->a_start, 0));
+  T(hipStreamWaitEvent(x->st4, x->seed_done, 0));
+  mp_batch_frame1(x->mpb, o, fprev, x->st4, nullptr);
+  T(hipEventRecord(x->mp1_done, x->st4));
+  T(hipStreamWaitEvent(x->st4, x->od_done, 0));
+  SideStream side;
+  side.st = x->st2;
+  side.fork[0] = x->fork; side.join[0] = x->join; side.fork[1] = x->fork2; side.join[1] = x->join2;
+  side.inputs_read = x->inputs_read;
+  mp_batch_frame2(x->mpb, o, fcur, x->st4, nullptr, &side);
+  x->inputs_read_rec = true;
+  T(hipEventRecord(x->mp_done[idx], x->st4));
+  x->mp_done_rec[idx] = true;
+  T(hipEventRecord(x->b_last, x->st4));
+  x->b_used = true;
+  T(hipEventRecord(x->ev[3], x->st4));
+  x->srb_last = idx;
+  // the next step's scan registration + seed (st3)
+  T(enqueue_ahead(x, nx, true));
+  x->sr_idx = nx;
+  T(hipGetLastError());
+  return e;
+}
 }  // namespace
 
 int loam_batch_run(loam_ctx* x) {
   if (!x || x->P == 0) return fail(LOAM_E_INVAL, "no batch uploaded");
   HIP_TRY(hipSetDevice(x->device));
   Prof* pf = x->prof.on ? &x->prof : nullptr;
+  if (!pf && !x->tune.graph && x->st2 && x->st3 && x->st4 && x->tune.step_pipe > 0 && x->P >= x->tune.step_pipe) {
+    HIP_TRY(batch_enqueue_pipe(x));
+    return LOAM_OK;
+  }
   if (!x->tune.graph || pf) {
     HIP_TRY(batch_enqueue(x, pf, true));
     return LOAM_OK;
@@ -1036,7 +1150,10 @@ int loam_batch_sync(loam_ctx* x) {
   if (!x) return fail(LOAM_E_INVAL, "null argument");
   HIP_TRY(hipSetDevice(x->device));
   HIP_TRY(hipStreamSynchronize(x->st));
-  // (a step's work includes the scan registration it enqueued for the next step)
+  // (a step's work includes its mapping on st4 and the scan registration it enqueued for the next
+  // step on st3)
+  if (x->st4) HIP_TRY(hipStreamSynchronize(x->st4));
+  if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
   if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));
   return LOAM_OK;
 }
@@ -1046,6 +1163,8 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
   HIP_TRY(hipSetDevice(x->device));
   const int P = x->P;
   HIP_TRY(hipStreamSynchronize(x->st));
+  if (x->st4) HIP_TRY(hipStreamSynchronize(x->st4));
+  if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
   if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));  // (the work enqueued ahead rewrites Last[0] alike)
   std::vector<float> st((size_t)P * kOdStateFloats);
   std::vector<int> ist((size_t)P * kOdStateInts), srerr(2 * P), cnt(8 * P), nfull(2 * P), nl(4 * P);

@@ -64,6 +64,10 @@ struct Tuning {
                            // throughput choice for batches of independent problems: a one-problem
                            // latency (config 2) would count the next problem's work ahead of time
                            // (round 4: 128 problems 3.04 -> 2.90 ms/step, 1024: 15.12 -> 14.96)
+  int step_pipe = 64;      // for P >= this (0: never): consecutive loam_batch_run steps as a software
+                           // pipeline (the odometry of a step beside the mapping of the previous one;
+                           // batch_enqueue_pipe), which supersedes sr_ahead (round 4: 128 problems
+                           // 2.75 -> 2.37 ms/step, 1024: 14.56 -> 14.25)
   int sr_ahead_at = -1;    // ... starting after this point of the current step: 0 its start, 1 the
                            // odometry seed's hashes, 2 the second mapping frame; -1: 2 for P <= 256,
                            // else 1 (round 4: 128 problems 2.91 / 2.91 / 2.82 ms/step for 0 / 1 / 2;
@@ -87,7 +91,8 @@ struct Tuning {
                     {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20},
                     {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20},
                     {"vg_merge", &vg_merge, 0, 1}, {"vg_merge_min", &vg_merge_min, 0, 1 << 20},
-                    {"sr_ahead", &sr_ahead, 0, 1 << 20}, {"sr_ahead_at", &sr_ahead_at, -1, 2}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
+                    {"sr_ahead", &sr_ahead, 0, 1 << 20}, {"sr_ahead_at", &sr_ahead_at, -1, 2},
+                    {"step_pipe", &step_pipe, 0, 1 << 20}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
                     {"od_win_mono", &od_win_mono, 0, 3}, {"od_win_mono_min", &od_win_mono_min, 1, 1 << 20}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {

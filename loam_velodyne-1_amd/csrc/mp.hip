@@ -2660,6 +2660,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   mark("k_mp_prepare");
   hipLaunchKernelGGL(k_mp_stack, dim3(16, P), dim3(256), 0, st, b, in);
   mark("k_mp_stack");
+  if (side && side->inputs_read) b.note(hipEventRecord(side->inputs_read, st));  // (in.corner / in.surf read)
   VgJob js = vg_job(b);
   js.in = b.stack2; js.out = b.stack; js.begin = b.sseg_b; js.end = b.sseg_e; js.leaf = b.sseg_leaf;
   js.out_count = b.sseg_cnt; js.nseg = 2 * P; js.total = P * b.cap_stack;

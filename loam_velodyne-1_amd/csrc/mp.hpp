@@ -158,6 +158,7 @@ hipError_t mp_reset(MpBuffers& b, hipStream_t st);
 struct SideStream {
   hipStream_t st = nullptr;
   hipEvent_t fork[2] = {nullptr, nullptr}, join[2] = {nullptr, nullptr};
+  hipEvent_t inputs_read = nullptr;  // optional: recorded once the frame has read its input clouds
 };
 void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof = nullptr, bool map_empty = false,
               const std::function<void()>& before_register = nullptr, int stack_max = -1,

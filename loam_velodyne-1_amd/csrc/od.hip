@@ -1648,7 +1648,9 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   b.gq = (b.cap_q + kOdThreads - 1) / kOdThreads;
   b.tC = next_pow2(b.capC);
   b.tS = next_pow2(b.capS) > 65536 ? 65536 : next_pow2(b.capS);
-  A(&b.state, (size_t)P * kOdStateFloats * sizeof(float));
+  A(&b.state_set[0], (size_t)P * kOdStateFloats * sizeof(float));
+  A(&b.state_set[1], (size_t)P * kOdStateFloats * sizeof(float));
+  b.state = b.state_set[0];
   A(&b.istate_set[0], (size_t)P * kOdStateInts * sizeof(int));
   A(&b.istate_set[1], (size_t)P * kOdStateInts * sizeof(int));
   b.istate = b.istate_set[0];
@@ -1683,7 +1685,8 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
     return A.err;
   }
   if (A.err == hipSuccess) A.err = hipMemset(b.done, 0, (size_t)P * sizeof(int));
-  if (A.err == hipSuccess) A.err = hipMemset(b.state, 0, (size_t)P * kOdStateFloats * sizeof(float));
+  for (int k = 0; k < 2; ++k)
+    if (A.err == hipSuccess) A.err = hipMemset(b.state_set[k], 0, (size_t)P * kOdStateFloats * sizeof(float));
   for (int k = 0; k < 2; ++k)
     if (A.err == hipSuccess) A.err = hipMemset(b.istate_set[k], 0, (size_t)P * kOdStateInts * sizeof(int));
   if (A.err == hipSuccess) A.err = hipMemset(b.nlast, 0, (size_t)P * 4 * sizeof(int));
@@ -1695,7 +1698,7 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
 }
 
 void od_free(OdBuffers& b) {
-  void* ptrs[] = {b.state, b.istate_set[0], b.istate_set[1], b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
+  void* ptrs[] = {b.state_set[0], b.state_set[1], b.istate_set[0], b.istate_set[1], b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
                   b.ind, b.sel, b.q_cf, b.q_ok, b.part, b.done, b.mono, b.rstart, b.fC, b.fS};
   for (void* q : ptrs)

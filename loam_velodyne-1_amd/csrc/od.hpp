@@ -76,7 +76,8 @@ LOAM_HD uint32_t hash_rec(int start, int count) {
 
 struct OdBuffers {
   int P = 0, capC = 0, capS = 0, cap_q = 0, gq = 0, tC = 0, tS = 0, max_iter = 25;
-  float* state = nullptr;   // [P][kOdStateFloats]
+  float* state = nullptr;   // [P][kOdStateFloats] (one of state_set: batches alternate per step)
+  float* state_set[2] = {nullptr, nullptr};
   int* istate = nullptr;    // [P][kOdStateInts] (one of istate_set: batches alternate per step)
   int* istate_set[2] = {nullptr, nullptr};
   float4* lastC = nullptr;  // [2][P][capC]

@@ -217,7 +217,7 @@ def _share_run(loam, sg, **tune):
     e.batch_upload(prevs, curs)
     # (a graph: its capture, then a replay; a step ahead: both buffer sets, each step consuming the
     # scan registration its predecessor enqueued)
-    for _ in range(3 if tune.get("sr_ahead") else 2 if tune.get("graph") else 1):
+    for _ in range(3 if tune.get("sr_ahead") or tune.get("step_pipe") else 2 if tune.get("graph") else 1):
         e.batch_run()
     od, aft, st = e.batch_download()
     e.close()
@@ -248,6 +248,8 @@ def _share_run(loam, sg, **tune):
     {"od_win_mono": 0},
     {"sr_ahead": 1},                         # scan registration one step ahead (three steps)
     {"sr_ahead": 1, "sr_ahead_at": 0},
+    {"step_pipe": 1},                        # steps as a software pipeline (three steps)
+    {"step_pipe": 1, "sr_ahead": 0},
 ], ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_launch_choices_at_8gpu_share(loam, oc, sg, tune):
     """every launch shape the engine can pick by batch size (include/loam/loam.h loam_set_tuning),
