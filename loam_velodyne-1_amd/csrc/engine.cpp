@@ -278,11 +278,9 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   for (auto& e : x->ev)
     if (he == hipSuccess) he = hipEventCreate(&e);
   if (he == hipSuccess && hipStreamCreateWithFlags(&x->st2, hipStreamNonBlocking) != hipSuccess) x->st2 = nullptr;
-  if (he == hipSuccess && hipStreamCreateWithFlags(&x->st3, hipStreamNonBlocking) != hipSuccess) x->st3 = nullptr;
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->sr_done, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->ahead_at, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_at, hipEventDisableTiming);
-  if (he == hipSuccess && hipStreamCreateWithFlags(&x->st4, hipStreamNonBlocking) != hipSuccess) x->st4 = nullptr;
   for (hipEvent_t* e : {&x->od_done, &x->mp1_done, &x->inputs_read, &x->a_start, &x->b_last, &x->mp_done[0], &x->mp_done[1]})
     if (he == hipSuccess) he = hipEventCreateWithFlags(e, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_done, hipEventDisableTiming);
@@ -864,6 +862,11 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
     if (!rc) rc = check_cloud_in(cur[i], x->cap);
     if (rc) return rc;
   }
+  // the batch's extra streams, created with the first batch only: a streaming context keeps two
+  // (GPU_MAX_HW_QUEUES hardware queues per process are shared by every context's streams; the node
+  // pipeline's three contexts measured 0.44 -> 0.59 ms/sweep with four streams each)
+  if (!x->st3 && hipStreamCreateWithFlags(&x->st3, hipStreamNonBlocking) != hipSuccess) x->st3 = nullptr;
+  if (!x->st4 && hipStreamCreateWithFlags(&x->st4, hipStreamNonBlocking) != hipSuccess) x->st4 = nullptr;
   // (a step ahead may still read the raw sweeps or write its buffer set)
   HIP_TRY(hipStreamSynchronize(x->st));
   if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
