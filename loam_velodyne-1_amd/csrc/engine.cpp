@@ -278,6 +278,13 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   for (auto& e : x->ev)
     if (he == hipSuccess) he = hipEventCreate(&e);
   if (he == hipSuccess && hipStreamCreateWithFlags(&x->st2, hipStreamNonBlocking) != hipSuccess) x->st2 = nullptr;
+  // the batch pipeline's streams, created here with the first two: streams take the process's
+  // GPU_MAX_HW_QUEUES hardware queues in creation order, and the four created together measured
+  // 2.42 ms/step at the 8-GPU share against 3.13 when st3 / st4 came with the first batch (two
+  // stages then shared a queue).  A context that never runs batches drops them (tuning
+  // batch_streams = 0, the node pipeline's contexts), leaving the queues to the other contexts.
+  if (he == hipSuccess && hipStreamCreateWithFlags(&x->st3, hipStreamNonBlocking) != hipSuccess) x->st3 = nullptr;
+  if (he == hipSuccess && hipStreamCreateWithFlags(&x->st4, hipStreamNonBlocking) != hipSuccess) x->st4 = nullptr;
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->sr_done, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->ahead_at, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_at, hipEventDisableTiming);
@@ -400,6 +407,14 @@ int loam_set_tuning(loam_ctx* x, const char* key, long long value) {
   if (x->st3) (void)hipStreamSynchronize(x->st3);
   if (x->st4) (void)hipStreamSynchronize(x->st4);
   x->reset_ahead();
+  if (!t.batch_streams) {  // (the batch then runs on st / st2 alone)
+    if (x->st3) (void)hipStreamDestroy(x->st3);
+    if (x->st4) (void)hipStreamDestroy(x->st4);
+    x->st3 = x->st4 = nullptr;
+  } else {
+    if (!x->st3 && hipStreamCreateWithFlags(&x->st3, hipStreamNonBlocking) != hipSuccess) x->st3 = nullptr;
+    if (!x->st4 && hipStreamCreateWithFlags(&x->st4, hipStreamNonBlocking) != hipSuccess) x->st4 = nullptr;
+  }
   x->drop_graph();  // (captured with the old choices)
   x->od1.tune = x->odb.tune = t;
   x->mp1.tune = x->mpb.tune = t;
@@ -862,11 +877,6 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
     if (!rc) rc = check_cloud_in(cur[i], x->cap);
     if (rc) return rc;
   }
-  // the batch's extra streams, created with the first batch only: a streaming context keeps two
-  // (GPU_MAX_HW_QUEUES hardware queues per process are shared by every context's streams; the node
-  // pipeline's three contexts measured 0.44 -> 0.59 ms/sweep with four streams each)
-  if (!x->st3 && hipStreamCreateWithFlags(&x->st3, hipStreamNonBlocking) != hipSuccess) x->st3 = nullptr;
-  if (!x->st4 && hipStreamCreateWithFlags(&x->st4, hipStreamNonBlocking) != hipSuccess) x->st4 = nullptr;
   // (a step ahead may still read the raw sweeps or write its buffer set)
   HIP_TRY(hipStreamSynchronize(x->st));
   if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));

