@@ -480,7 +480,7 @@ int sr_frame(loam_ctx* x, double stamp, const loam_cloud_in& raw, loam_features*
   {
     Xfer xp;
     xp.put(b.raw_n, &n, sizeof(int));
-    xfer_launch(xp, x->st);
+    HIP_TRY(xfer_launch(xp, x->st));
   }
   SrParams prm = sr_params(x);
   loamimu::SrQueue* q = x->sr_imu;
@@ -514,7 +514,7 @@ int sr_frame(loam_ctx* x, double stamp, const loam_cloud_in& raw, loam_features*
     xg.get(x->xb.d + kXferSr, b.cnt, 4 * sizeof(int));
     xg.get(x->xb.d + kXferSr + 16, b.n_full, sizeof(int));
     xg.get(x->xb.d + kXferSr + 20, b.err, sizeof(int));
-    xfer_launch(xg, x->st);
+    HIP_TRY(xfer_launch(xg, x->st));
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(x->st));
@@ -615,7 +615,7 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
     Xfer xp;
     xp.put(fi.cnt, cnt, 4 * sizeof(int));
     xp.put(fi.n_full, &cnt[4], sizeof(int));
-    xfer_launch(xp, x->st);
+    HIP_TRY(xfer_launch(xp, x->st));
     HIP_TRY(hipGetLastError());
   }
   return od_frame(x, feat_view(fi, 0, 1), cnt, in->imu_trans, late ? &in->full : nullptr, sum_out, corner_last,
@@ -638,7 +638,7 @@ int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_i
   {
     Xfer xp;
     xp.put(o.state + kOdImu, mi + 8, 12 * sizeof(float));
-    xfer_launch(xp, x->st);
+    HIP_TRY(xfer_launch(xp, x->st));
   }
   if (!x->od_inited) {  // src/laserOdometry.cpp:427-456: Last = raw lessSharp / lessFlat, no L-M
     // :451-452 transformSum[0] += imuPitchStart; transformSum[2] += imuRollStart (from zero)
@@ -689,7 +689,7 @@ int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_i
     xg.get(d + 4 * kOdStateFloats, o.istate, kOdStateInts * sizeof(int));
     xg.get(d + 4 * (kOdStateFloats + kOdStateInts), o.nlast, 4 * sizeof(int));
     xg.get(d + 4 * (kOdStateFloats + kOdStateInts + 4), o.nfullEnd, 2 * sizeof(int));
-    xfer_launch(xg, x->st);
+    HIP_TRY(xfer_launch(xg, x->st));
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(x->st));
@@ -712,7 +712,7 @@ int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_i
     // host result goes back in k_xfer's arguments, ordered before the next frame's kernels
     Xfer xp;
     xp.put(o.state + kOdSum, x->od_sum, sizeof(loam_pose6));
-    xfer_launch(xp, x->st);
+    HIP_TRY(xfer_launch(xp, x->st));
     HIP_TRY(hipGetLastError());
   }
   if (sum_out) std::memcpy(sum_out, x->od_sum, sizeof(loam_pose6));
@@ -1249,7 +1249,9 @@ __global__ __launch_bounds__(256) void k_xfer(Xfer x) {
     for (int w = threadIdx.x; w < x.words[e]; w += 256) d[w] = s ? s[w] : x.imm[x.imm_off[e] + w];
   }
 }
-void xfer_launch(const Xfer& x, hipStream_t st) {
+hipError_t xfer_launch(const Xfer& x, hipStream_t st) {
+  if (x.overflow) return hipErrorInvalidValue;
   if (x.n) hipLaunchKernelGGL(k_xfer, dim3(1), dim3(256), 0, st, x);
+  return hipGetLastError();
 }
 }  // namespace loam

@@ -2842,8 +2842,7 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
     xp.put(b.in_pose, mi + 4, 6 * sizeof(float));
     xp.put(b.state + kMpImuRP, mi + 10, 2 * sizeof(float));
     xp.put(b.istate + kMiImu, mi + 12, sizeof(int));
-    xfer_launch(xp, st);
-    ue = hipGetLastError();
+    ue = xfer_launch(xp, st);
   }
   if (ue != hipSuccess) {
     err = std::string("mapping upload: ") + hipGetErrorString(ue);
@@ -2880,8 +2879,7 @@ int mp_stream_frame_dev(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum
   xp.put(b.in_pose, &odom_sum, 6 * sizeof(float));
   xp.put(b.state + kMpImuRP, rp, sizeof(rp));
   xp.put(b.istate + kMiImu, &flag, sizeof(int));
-  xfer_launch(xp, st);
-  const hipError_t ue = hipGetLastError();
+  const hipError_t ue = xfer_launch(xp, st);
   if (ue != hipSuccess) {
     err = std::string("mapping upload: ") + hipGetErrorString(ue);
     return LOAM_E_HIP;
@@ -2917,7 +2915,7 @@ int mp_stream_run(MpBuffers& b, hipStream_t st, const MpInput& in, const int* n,
     xg.get(d, b.state, kMpStateFloats * sizeof(float));
     xg.get(d + kMpStateFloats * 4, b.istate, kMpStateInts * sizeof(int));
     xg.get(d + (kMpStateFloats + kMpStateInts) * 4, b.nreg, sizeof(int));
-    xfer_launch(xg, st);
+    le = le == hipSuccess ? xfer_launch(xg, st) : le;
   }
   hipError_t he = hipGetLastError();
   if (he == hipSuccess) he = hipStreamSynchronize(st);

@@ -16,6 +16,7 @@ namespace loam {
 struct Xfer {
   static constexpr int kMax = 8, kImm = 64;
   int n = 0, nimm = 0;
+  bool overflow = false;  // an entry did not fit: xfer_launch refuses the whole transfer
   uint32_t* dst[kMax];
   const uint32_t* src[kMax];  // nullptr: a put from imm
   int words[kMax], imm_off[kMax];
@@ -23,7 +24,10 @@ struct Xfer {
   // device words <- host bytes (a multiple of 4), copied into the launch's arguments now
   bool put(void* dev, const void* host, int nbytes) {
     const int w = nbytes / 4;
-    if (n == kMax || nimm + w > kImm) return false;
+    if (n == kMax || nimm + w > kImm || nbytes % 4) {
+      overflow = true;
+      return false;
+    }
     dst[n] = (uint32_t*)dev;
     src[n] = nullptr;
     words[n] = w;
@@ -35,7 +39,10 @@ struct Xfer {
   }
   // mapped host words (the device address of the context's host block) <- device bytes
   bool get(void* host_dev, const void* dev, int nbytes) {
-    if (n == kMax) return false;
+    if (n == kMax || nbytes % 4) {
+      overflow = true;
+      return false;
+    }
     dst[n] = (uint32_t*)host_dev;
     src[n] = (const uint32_t*)dev;
     words[n] = nbytes / 4;
@@ -51,7 +58,8 @@ struct XferBuf {
   char* d = nullptr;
 };
 
-void xfer_launch(const Xfer& x, hipStream_t st);
+// hipErrorInvalidValue (nothing launched) when an entry did not fit, else the launch's error
+hipError_t xfer_launch(const Xfer& x, hipStream_t st);
 
 // what a streaming node call needs beyond its buffers: the pinned scratch (meta), the mapped host
 // block (xb; regions: scan registration [0, 64), odometry [64, 512), mapping [512, 1024) bytes) and
