@@ -628,6 +628,11 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
 // fb: the cloud's kSub-point sub-chunk boxes; rs: its ring start table (LDS).  want_same: the surf min2 category is taken (corner: no).
 // best2 / best3 in and out: the keys ((distance bits << 32) | walk position), ~0 for none; keys at
 // or above 25 m² never count (:491, :602).
+#ifndef LOAM_WIN_WB
+#define LOAM_WIN_WB 0  // the first round's window bounds from the nearest neighbour's cells (wave_hash_nn):
+                       // its second pass over the cells cost more than the sub-chunks it saved
+                       // (k_od_assoc at 1024: 2.42 with, 2.35 without)
+#endif
 #ifndef LOAM_WIN_TIGHTEN
 #define LOAM_WIN_TIGHTEN 0  // bounds tightened after every wave step: 0 never (the seeds' / cells' only),
 #endif                      // 1 always, 2 in the first (unseeded) round
@@ -955,7 +960,7 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
       if (q < nc && monoC && use_mono) {
         const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
         const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC, hCT, CL, ch, C, 1.0f,
-                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded ? -1 : 0, min(nc, C), true, &wb);
+                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded || !LOAM_WIN_WB ? -1 : 0, min(nc, C), true, &wb);
         i1 = i2 = -1;
         if (nn != ~0ull && D(__uint_as_float((uint32_t)(nn >> 32))) < 25) {
           const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u), fe = min(nc, C);
@@ -967,7 +972,7 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
       } else if (q >= nc && monoS && use_mono) {
         const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
         const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS, hST, SL, ch, S, 1.0f,
-                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded ? -1 : 1, min(ns, S), true, &wb);
+                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded || !LOAM_WIN_WB ? -1 : 1, min(ns, S), true, &wb);
         i1 = i2 = -1;
         if (nn != ~0ull && D(__uint_as_float((uint32_t)(nn >> 32))) < 25) {
           const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u), fe = min(ns, S);

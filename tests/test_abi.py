@@ -82,3 +82,19 @@ def test_stats_layout_matches_header(loam, oc):
     po = [("uint64_t" if t is ctypes.c_uint64 else "double", n) for n, t in oc.Stats._fields_]
     assert py == names
     assert po == names
+
+
+def test_tuning_keys_documented():
+    """every launch choice loam_set_tuning accepts (engine.hpp Tuning::set's table) is listed in the
+    C-ABI header's documentation of loam_set_tuning"""
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hpp = open(os.path.join(root, "loam_velodyne-1_amd", "csrc", "engine.hpp")).read()
+    table = hpp[hpp.index("const K ks[] = {"):]
+    table = table[:table.index("};")]
+    keys = set(re.findall(r'\{"([a-z0-9_]+)", &', table))
+    hdr = open(os.path.join(root, "include", "loam", "loam.h")).read()
+    doc = hdr[:hdr.index("int loam_set_tuning(")]
+    doc = doc[doc.rindex("/*"):]
+    words = set(re.findall(r"\b[a-z_0-9]+\b", doc))
+    assert len(keys) >= 20 and keys <= words, sorted(keys - words)
