@@ -199,7 +199,7 @@ int loam_set_stream_priority(loam_ctx *ctx, int priority);
 
 /* launch-shape choices of the batch / streaming L-M loops by batch size (no reference equivalent):
  * key = one of od_small_max, od_lm_min, od_lm_max, od_fused_max, mp_small_max, mp_fused_max,
- * nn_lanes, nn_lanes_maxp, od_assoc_wg, nn_lds, od_rows_deep_max, nn_wg, fit_wg, nnfit_max, graph, mp_iter_wide_max, vg_merge, vg_merge_min, sr_ahead, sr_ahead_at, step_pipe, batch_streams, od_sel_min, od_win_mono, od_win_mono_min (loam_velodyne-1_amd/csrc/engine.hpp, struct Tuning).  Every
+ * nn_lanes, nn_lanes_maxp, od_assoc_wg, nn_lds, od_rows_deep_max, nn_wg, fit_wg, nnfit_max, graph, mp_iter_wide_max, vg_merge, vg_merge_min, sr_ahead, sr_ahead_at, step_pipe, batch_streams, pipe_mp_sets, od_sel_min, od_win_mono, od_win_mono_min (loam_velodyne-1_amd/csrc/engine.hpp, struct Tuning).  Every
  * choice computes the same results; the defaults are the measured fastest.  LOAM_E_INVAL for an
  * unknown key or a value out of range.  Takes effect from the next call. */
 int loam_set_tuning(loam_ctx *ctx, const char *key, long long value);

@@ -111,6 +111,9 @@ struct loam_ctx {
   bool sr_ready = false;  // its scan registration is already enqueued (st3, sr_done)
   int srb_last = 0;       // the set of the last enqueued step (loam_batch_download)
   SrBuffers& srbuf(int i) { return i ? srb2 : srb; }
+  MpBuffers mpb2;         // the second mapping set: the step pipeline's steps alternate (mpbuf)
+  MpBuffers& mpbuf(int i) { return i ? mpb2 : mpb; }
+  int mp_last = 0;        // the mapping set of the last enqueued step (loam_batch_download)
   void reset_ahead() {    // (after draining st3 / st4)
     sr_ready = false;
     seed_ready = false;
@@ -343,6 +346,7 @@ void loam_destroy(loam_ctx* x) {
   sr_free(x->srb2);
   od_free(x->odb);
   mp_free(x->mpb);
+  mp_free(x->mpb2);
   if (x->sr_imu_dev) (void)hipFree(x->sr_imu_dev);
   if (x->meta) (void)hipHostFree(x->meta);
   if (x->xb.h) (void)hipHostFree(x->xb.h);
@@ -417,7 +421,7 @@ int loam_set_tuning(loam_ctx* x, const char* key, long long value) {
   }
   x->drop_graph();  // (captured with the old choices)
   x->od1.tune = x->odb.tune = t;
-  x->mp1.tune = x->mpb.tune = t;
+  x->mp1.tune = x->mpb.tune = x->mpb2.tune = t;
   return LOAM_OK;
 }
 
@@ -890,23 +894,27 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
     sr_free(x->srb2);
     od_free(x->odb);
     mp_free(x->mpb);
+    mp_free(x->mpb2);
     x->P = 0;  // no batch until every buffer of the new size exists
     hipError_t he = sr_alloc(x->srb, 2 * (int)n, x->cap, x->R);
     if (he == hipSuccess) he = sr_alloc(x->srb2, 2 * (int)n, x->cap, x->R);
     if (he == hipSuccess) he = od_alloc(x->odb, (int)n, x->R, x->cap, (int)x->cfg.od_max_iter);
     if (he == hipSuccess)
       he = mp_alloc(x->mpb, (int)n, x->R, x->cap, mp_batch_map_capacity(x->cap), (int)x->cfg.mp_max_iter);
+    if (he == hipSuccess)
+      he = mp_alloc(x->mpb2, (int)n, x->R, x->cap, mp_batch_map_capacity(x->cap), (int)x->cfg.mp_max_iter);
     if (he != hipSuccess) {
       sr_free(x->srb);
       sr_free(x->srb2);
       od_free(x->odb);
       mp_free(x->mpb);
+      mp_free(x->mpb2);
       return fail(LOAM_E_NOMEM, std::string("batch allocation failed: ") + hipGetErrorString(he));
     }
     x->P = (int)n;
   }
   x->odb.tune = x->tune;
-  x->mpb.tune = x->tune;
+  x->mpb.tune = x->mpb2.tune = x->tune;
   std::vector<float4> h((size_t)x->cap);
   std::vector<int> counts(2 * n);
   for (uint32_t i = 0; i < n; ++i)
@@ -937,8 +945,9 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   SrBuffers& sb = x->srbuf(idx);
   if (events) T(hipEventRecord(x->ev[0], x->st));
   x->prof.begin(x->st);
-  if (x->b_used) {  // a pipelined step's mapping may still run on st4 (batch_enqueue_pipe)
-    T(hipStreamWaitEvent(x->st, x->b_last, 0));
+  if (x->b_used) {  // pipelined steps' mappings may still run on st4 / st2 (batch_enqueue_pipe)
+    for (int i = 0; i < 2; ++i)
+      if (x->mp_done_rec[i]) T(hipStreamWaitEvent(x->st, x->mp_done[i], 0));
     x->b_used = false;
   }
   if (x->sr_ready) {
@@ -979,7 +988,7 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   if (overlap) {
     T(hipEventRecord(x->fork, x->st));
     T(hipStreamWaitEvent(x->st2, x->fork, 0));
-    mp_batch_frame1(x->mpb, o, fprev, x->st2, nullptr);
+    mp_batch_frame1(x->mpbuf(idx), o, fprev, x->st2, nullptr);
     T(hipEventRecord(x->join, x->st2));
   }
   // the pose accumulation (k_od_fini, one serial double-trig chain per problem) beside
@@ -999,7 +1008,7 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   if (overlap) {
     T(hipStreamWaitEvent(x->st, x->join, 0));
   } else {
-    mp_batch_frame1(x->mpb, o, fprev, x->st, pf);
+    mp_batch_frame1(x->mpbuf(idx), o, fprev, x->st, pf);
   }
   ahead_point(2);
   if (ahead) T(hipEventRecord(x->seed_at, x->st));
@@ -1007,7 +1016,8 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   SideStream side;
   side.st = x->st2;
   side.fork[0] = x->fork; side.join[0] = x->join; side.fork[1] = x->fork2; side.join[1] = x->join2;
-  mp_batch_frame2(x->mpb, o, fcur, x->st, pf, overlap ? &side : nullptr);
+  mp_batch_frame2(x->mpbuf(idx), o, fcur, x->st, pf, overlap ? &side : nullptr);
+  x->mp_last = idx;
   if (events) T(hipEventRecord(x->ev[3], x->st));
   x->srb_last = idx;
   // the next step's scan registration into the other set, once the step that last read it is done
@@ -1096,24 +1106,29 @@ hipError_t batch_enqueue_pipe(loam_ctx* x) {
   hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, 1, 2, 0);
   T(hipEventRecord(x->od_done, x->st));
   T(hipEventRecord(x->ev[2], x->st));
-  // mapping (st4): frame 1 once the seed (and this call's earlier work on st) is there, frame 2 once
-  // the odometry is
-  T(hipStreamWaitEvent(x->st4, x->a_start, 0));
-  T(hipStreamWaitEvent(x->st4, x->seed_done, 0));
-  mp_batch_frame1(x->mpb, o, fprev, x->st4, nullptr);
-  T(hipEventRecord(x->mp1_done, x->st4));
-  T(hipStreamWaitEvent(x->st4, x->od_done, 0));
+  // mapping: frame 1 once the seed (and this call's earlier work on st) is there, frame 2 once the
+  // odometry is.  tune.pipe_mp_sets = 2: the steps alternate between two mapping sets on st4 / st2,
+  // so the next step's frame 1 runs beside this step's frame 2 (no side branches then); 1: one set
+  // on st4, frame 2's independent branches on st2
+  const bool two = x->tune.pipe_mp_sets == 2;
+  hipStream_t ms = two && idx ? x->st2 : x->st4;
+  MpBuffers& mb = two ? x->mpbuf(idx) : x->mpb;
+  T(hipStreamWaitEvent(ms, x->a_start, 0));
+  T(hipStreamWaitEvent(ms, x->seed_done, 0));
+  mp_batch_frame1(mb, o, fprev, ms, nullptr);
+  T(hipEventRecord(x->mp1_done, ms));
+  T(hipStreamWaitEvent(ms, x->od_done, 0));
   SideStream side;
-  side.st = x->st2;
+  side.st = two ? nullptr : x->st2;
   side.fork[0] = x->fork; side.join[0] = x->join; side.fork[1] = x->fork2; side.join[1] = x->join2;
   side.inputs_read = x->inputs_read;
-  mp_batch_frame2(x->mpb, o, fcur, x->st4, nullptr, &side);
+  mp_batch_frame2(mb, o, fcur, ms, nullptr, &side);
   x->inputs_read_rec = true;
-  T(hipEventRecord(x->mp_done[idx], x->st4));
+  T(hipEventRecord(x->mp_done[idx], ms));
   x->mp_done_rec[idx] = true;
-  T(hipEventRecord(x->b_last, x->st4));
   x->b_used = true;
-  T(hipEventRecord(x->ev[3], x->st4));
+  x->mp_last = two ? idx : 0;
+  T(hipEventRecord(x->ev[3], ms));
   x->srb_last = idx;
   // the next step's scan registration + seed (st3)
   T(enqueue_ahead(x, nx, true));
@@ -1195,7 +1210,7 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
     for (int i = 0; i < P; ++i) std::memcpy(&od_sum[i], &st[(size_t)i * kOdStateFloats + kOdSum], sizeof(loam_pose6));
   loam_stats s;
   std::memset(&s, 0, sizeof(s));
-  int rc = mp_batch_download(x->mpb, x->st, aft, &s, g_err);
+  int rc = mp_batch_download(x->mpbuf(x->mp_last), x->st, aft, &s, g_err);
   if (rc) return rc;
   for (int i = 0; i < 2 * P; ++i) {
     s.n_ring += nfull[i];

@@ -68,6 +68,9 @@ struct Tuning {
                            // pipeline (the odometry of a step beside the mapping of the previous one;
                            // batch_enqueue_pipe), which supersedes sr_ahead (round 4: 128 problems
                            // 2.75 -> 2.37 ms/step, 1024: 14.56 -> 14.25)
+  int pipe_mp_sets = 2;    // the step pipeline's mapping: 1 one set (st4, side branches on st2), 2 two sets
+                           // alternating on st4 / st2 (the next frame 1 beside this frame 2; round 4:
+                           // 128 problems 2.37 -> 2.20 ms/step, 1024: 14.23 -> 14.03)
   int batch_streams = 1;   // the context keeps the batch pipeline's two extra streams (0: drops them)
   int sr_ahead_at = -1;    // ... starting after this point of the current step: 0 its start, 1 the
                            // odometry seed's hashes, 2 the second mapping frame; -1: 2 for P <= 256,
@@ -93,7 +96,8 @@ struct Tuning {
                     {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20},
                     {"vg_merge", &vg_merge, 0, 1}, {"vg_merge_min", &vg_merge_min, 0, 1 << 20},
                     {"sr_ahead", &sr_ahead, 0, 1 << 20}, {"sr_ahead_at", &sr_ahead_at, -1, 2},
-                    {"step_pipe", &step_pipe, 0, 1 << 20}, {"batch_streams", &batch_streams, 0, 1}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
+                    {"step_pipe", &step_pipe, 0, 1 << 20}, {"batch_streams", &batch_streams, 0, 1},
+                    {"pipe_mp_sets", &pipe_mp_sets, 1, 2}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
                     {"od_win_mono", &od_win_mono, 0, 3}, {"od_win_mono_min", &od_win_mono_min, 1, 1 << 20}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {

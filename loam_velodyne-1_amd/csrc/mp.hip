@@ -2673,7 +2673,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   // batches: the corner stacks (<= 120 points per ring) take the 2048-point kernel, the surf
   // stacks the 12288-point one; a few instances: one 12288-point launch.  With a side stream it
   // runs there, beside the FromMap gather and the map hash builds (which read only the store)
-  const bool fork = side && !prof && !map_empty;
+  const bool fork = side && side->st && !prof && !map_empty;
   if (fork) {
     b.note(hipEventRecord(side->fork[0], st));
     b.note(hipStreamWaitEvent(side->st, side->fork[0], 0));

@@ -250,6 +250,7 @@ def _share_run(loam, sg, **tune):
     {"sr_ahead": 1, "sr_ahead_at": 0},
     {"step_pipe": 1},                        # steps as a software pipeline (three steps)
     {"step_pipe": 1, "sr_ahead": 0},
+    {"step_pipe": 1, "pipe_mp_sets": 1},     # one mapping set, frame 2's side branches on st2
 ], ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_launch_choices_at_8gpu_share(loam, oc, sg, tune):
     """every launch shape the engine can pick by batch size (include/loam/loam.h loam_set_tuning),
