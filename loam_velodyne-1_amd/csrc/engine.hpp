@@ -38,7 +38,8 @@ struct Tuning {
   int od_small_max = 63;   // k_od_rows_small (a workgroup per (queries, stored iteration)) for P <= this
   int od_lm_min = 1;       // k_od_lm (an association round's 5 iterations in one workgroup per problem)
   int od_lm_max = 0;       //   for od_lm_min <= P <= od_lm_max
-  int od_fused_max = 0;    // k_od_rows<true> (step in the last workgroup) for P <= this, else + k_od_step
+  int od_fused_max = 128;  // k_od_rows<true> (step in the last workgroup) for P <= this, else + k_od_step
+                           // (round 4, in the step pipeline: 128 problems 2.19 -> 2.14 ms/step; 1024 slower)
   int mp_small_max = 4;    // k_mp_lm_small (5-NN + fit + rows + step in one launch) for P <= this
   int mp_fused_max = 1 << 20;  // the fit kernel (k_mp_fit<true> / k_mp_nnfit<true>) adds the rows and runs
                            // the step in its last workgroup for P <= this, else k_mp_iter (round 4, with

@@ -225,7 +225,7 @@ def _share_run(loam, sg, **tune):
 
 
 @pytest.mark.parametrize("tune", [
-    {"od_fused_max": 128},                   # k_od_rows<true>: the step in the rows' last workgroup
+    {"od_fused_max": 0},                     # k_od_rows<false> + k_od_step (the default above 128)
     {"od_lm_max": 128},                      # k_od_lm: an association round in one workgroup per problem
     {"od_small_max": 128},                   # k_od_rows_small: a workgroup per (queries, stored iteration)
     {"nnfit_max": 0},                        # k_mp_nn + k_mp_fit<true> (round 3's shapes)
