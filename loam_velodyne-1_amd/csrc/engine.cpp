@@ -104,6 +104,7 @@ struct loam_ctx {
   // previous one (st4), the scan registration + seed of the next (st3); hand-offs by events (batch_enqueue_pipe)
   hipStream_t st4 = nullptr;
   hipEvent_t od_done = nullptr, mp1_done = nullptr, inputs_read = nullptr, a_start = nullptr, b_last = nullptr;
+  hipEvent_t mp1_read = nullptr;  // frame 1 has read Last[0] (after its k_mp_stack)
   hipEvent_t mp_done[2] = {nullptr, nullptr};
   bool mp_done_rec[2] = {false, false}, inputs_read_rec = false, b_used = false;
   bool step_done_rec[2] = {false, false};
@@ -291,7 +292,8 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->sr_done, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->ahead_at, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_at, hipEventDisableTiming);
-  for (hipEvent_t* e : {&x->od_done, &x->mp1_done, &x->inputs_read, &x->a_start, &x->b_last, &x->mp_done[0], &x->mp_done[1]})
+  for (hipEvent_t* e : {&x->od_done, &x->mp1_done, &x->inputs_read, &x->a_start, &x->b_last, &x->mp_done[0], &x->mp_done[1],
+                        &x->mp1_read})
     if (he == hipSuccess) he = hipEventCreateWithFlags(e, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_done, hipEventDisableTiming);
   for (auto& e : x->step_done)
@@ -363,7 +365,8 @@ void loam_destroy(loam_ctx* x) {
   if (x->sr_done) (void)hipEventDestroy(x->sr_done);
   if (x->ahead_at) (void)hipEventDestroy(x->ahead_at);
   if (x->seed_at) (void)hipEventDestroy(x->seed_at);
-  for (hipEvent_t e : {x->od_done, x->mp1_done, x->inputs_read, x->a_start, x->b_last, x->mp_done[0], x->mp_done[1]})
+  for (hipEvent_t e : {x->od_done, x->mp1_done, x->inputs_read, x->a_start, x->b_last, x->mp_done[0], x->mp_done[1],
+                       x->mp1_read})
     if (e) (void)hipEventDestroy(e);
   if (x->st4) (void)hipStreamDestroy(x->st4);
   if (x->seed_done) (void)hipEventDestroy(x->seed_done);
@@ -1049,7 +1052,7 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
 }
 // The scan registration of the step reading buffer set i and its odometry seed (Last[0], its
 // hashes, the counts in istate set i), on st3.  Waits: the set's previous step is done with it
-// (mp_done[i]: its mapping, the last reader), and Last[0] is free (od_done / mp1_done of the step
+// (mp_done[i]: its mapping, the last reader), and Last[0] is free (od_done / mp1_read of the step
 // before, passed as `free_last`).
 hipError_t enqueue_ahead(loam_ctx* x, int i, bool free_last) {
   const int P = x->P;
@@ -1060,9 +1063,9 @@ hipError_t enqueue_ahead(loam_ctx* x, int i, bool free_last) {
   T(hipStreamWaitEvent(x->st3, x->a_start, 0));  // (whatever ran on st before this call)
   sr_launch(x->srbuf(i), sr_params(x), x->st3, nullptr);
   T(hipEventRecord(x->sr_done, x->st3));
-  if (free_last) {
+  if (free_last) {  // Last[0] read by this step's odometry and frame 1 (its k_mp_stack)
     T(hipStreamWaitEvent(x->st3, x->od_done, 0));
-    T(hipStreamWaitEvent(x->st3, x->mp1_done, 0));
+    T(hipStreamWaitEvent(x->st3, x->mp1_read, 0));
   }
   on.istate = on.istate_set[i];
   T(hipMemsetAsync(on.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st3));
@@ -1115,7 +1118,9 @@ hipError_t batch_enqueue_pipe(loam_ctx* x) {
   MpBuffers& mb = two ? x->mpbuf(idx) : x->mpb;
   T(hipStreamWaitEvent(ms, x->a_start, 0));
   T(hipStreamWaitEvent(ms, x->seed_done, 0));
-  mp_batch_frame1(mb, o, fprev, ms, nullptr);
+  SideStream side1;  // (no branches: only the event once Last[0] is read)
+  side1.inputs_read = x->mp1_read;
+  mp_batch_frame1(mb, o, fprev, ms, nullptr, &side1);
   T(hipEventRecord(x->mp1_done, ms));
   T(hipStreamWaitEvent(ms, x->od_done, 0));
   SideStream side;

@@ -3041,7 +3041,8 @@ int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::s
 
 // frame 1 of the batch problem: reset, then prev (Last[0], fullEnd[0]) into the empty store at
 // the zero pose.  Reads only what the odometry seeding wrote, so it may run beside od_solve.
-void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, const FeatView& fprev, hipStream_t st, Prof* prof) {
+void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, const FeatView& fprev, hipStream_t st, Prof* prof,
+                     const SideStream* side) {
   b.note(mp_reset(b, st));
   if (prof) prof->mark("mp_reset");
   MpInput in;
@@ -3054,7 +3055,7 @@ void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, const FeatView& fprev, h
   in.nfull = fprev.nfull_p; in.nfull_stride = fprev.nfull_stride;
   in.end_mode = 1;
   in.pose = nullptr; in.pose_stride = 0;
-  mp_frame(b, in, st, prof, /*map_empty=*/true);
+  mp_frame(b, in, st, prof, /*map_empty=*/true, nullptr, -1, side);
 }
 
 // frame 2: cur (Last[1], fullEnd[1]) with the odometry transformSum

@@ -179,7 +179,9 @@ int mp_stream_frame_dev(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum
 // concatenated and VoxelGrid 0.2 (src/laserMapping.cpp:1038-1058)
 int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::string& err);
 // fprev / fcur: the scan registration outputs whose full clouds the frames register
-void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, const FeatView& fprev, hipStream_t st, Prof* prof = nullptr);
+// side: only its inputs_read event is used (the frame runs on st alone)
+void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, const FeatView& fprev, hipStream_t st, Prof* prof = nullptr,
+                     const SideStream* side = nullptr);
 void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, const FeatView& fcur, hipStream_t st, Prof* prof = nullptr,
                      const SideStream* side = nullptr);
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err);
