@@ -338,6 +338,7 @@ void loam_destroy(loam_ctx* x) {
   if (!x) return;
   (void)hipSetDevice(x->device);
   if (x->st) (void)hipStreamSynchronize(x->st);
+  if (x->st2) (void)hipStreamSynchronize(x->st2);  // (a pipelined step's mapping set runs there)
   if (x->st3) (void)hipStreamSynchronize(x->st3);
   if (x->st4) (void)hipStreamSynchronize(x->st4);
   sr_free(x->sr1);
