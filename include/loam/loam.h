@@ -184,7 +184,11 @@ int loam_maintenance(const loam_pose6 *odom_sum, const loam_pose6 *bef, const lo
  * problem i = scan registration of (prev_i, cur_i), odometry seeded from prev_i and solved on
  * cur_i, mapping of prev_i into an empty map then solved for cur_i.
  * upload copies the host sweeps into device memory; run executes every problem on the device
- * with all inputs resident in HBM; download copies the poses back. */
+ * with all inputs resident in HBM; download copies the poses back.  run only enqueues: for
+ * n >= 64 (tunings step_pipe / sr_ahead) consecutive runs overlap as a software pipeline — a run's
+ * odometry beside the previous run's mapping, the next run's scan registration and odometry seed
+ * enqueued ahead (they re-run the same uploaded problems) — and sync waits for all of it.  download
+ * returns the last run's results. */
 int loam_batch_upload(loam_ctx *ctx, uint32_t n, const loam_cloud_in *prev,
                       const loam_cloud_in *cur);
 int loam_batch_run(loam_ctx *ctx);
