@@ -1080,12 +1080,13 @@ hipError_t enqueue_ahead(loam_ctx* x, int i, bool free_last) {
 // One batch step as a stage of a software pipeline over consecutive steps (tune.step_pipe):
 //   st3  scan registration + odometry seed of step k + 1 (enqueue_ahead)
 //   st   odometry of step k (L-M, pose accumulation, TransformToEnd of Last[1])
-//   st4  mapping of step k: frame 1 (needs the seed), frame 2 (needs the odometry), side branches on st2
+//   st4 / st2  mapping of step k: frame 1 (needs the seed), frame 2 (needs the odometry); with two
+//        mapping sets (tune.pipe_mp_sets = 2) the steps alternate between st4 and st2
 // so the odometry of step k + 1 runs beside the mapping of step k.  Buffers shared between steps:
-// the SR set and the odometry state / istate sets alternate; Last[0] is rewritten by the next seed
-// only after this step's odometry and frame 1 (od_done, mp1_done); Last[1] by the next odometry only
-// after this step's frame 2 has read it (inputs_read).  Every step does the same work as
-// batch_enqueue's; loam_batch_sync waits for all four streams.
+// the SR set, the odometry state / istate sets and the mapping sets alternate; Last[0] is rewritten
+// by the next seed only after this step's odometry and frame 1 have read it (od_done, mp1_read);
+// Last[1] by the next odometry only after this step's frame 2 has read it (inputs_read).  Every step
+// does the same work as batch_enqueue's; loam_batch_sync waits for all four streams.
 hipError_t batch_enqueue_pipe(loam_ctx* x) {
   const int P = x->P;
   OdBuffers& o = x->odb;
