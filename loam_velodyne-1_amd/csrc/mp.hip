@@ -2574,7 +2574,7 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
   A(&b.hC_rec, (size_t)P * b.tmax * sizeof(uint32_t));
   A(&b.hS_rec, (size_t)P * b.tmax * sizeof(uint32_t));
   // bucket counters: one set per cloud kind for small batches, whose two builds run together
-  A(&b.h_fill, (size_t)(P <= 4 ? 2 : 1) * P * b.tmax * sizeof(int));
+  A(&b.h_fill, (size_t)2 * P * b.tmax * sizeof(int));  // (corner, surf: built concurrently)
   A(&b.hC_T, (size_t)P * sizeof(int));
   A(&b.hS_T, (size_t)P * sizeof(int));
   A(&b.hC_pts, Pm * sizeof(float4));
@@ -2695,7 +2695,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   hs.rec = b.hS_rec;
   hs.pts_off = b.nfrom; hs.pts_off_stride = 2;
   hs.count = b.nfrom + 1; hs.start = b.hS_start; hs.out = b.hS_pts; hs.tsize = b.hS_T;
-  if (P <= 4) hs.fill = b.h_fill + (size_t)P * b.tmax;
+  hs.fill = b.h_fill + (size_t)P * b.tmax;  // (the two indexes are built in one launch / concurrently)
   hash_build_pair(hc, hs, P, st, false);
   mark("k_hash_build_map");
   if (fork) b.note(hipStreamWaitEvent(st, side->join[0], 0));

@@ -183,8 +183,14 @@ LOAM_D void ring_starts(const HashJob& j, const float4* pts, int n, int p, int t
   }
 }
 
+struct HashPair {
+  HashJob j[2];
+};
+
+// both clouds' indexes in one launch: blockIdx.y selects the job (the two are independent)
 template <int NT>
-__global__ __launch_bounds__(NT) void k_hash_build(HashJob j) {
+__global__ __launch_bounds__(NT) void k_hash_build(HashPair hp) {
+  const HashJob& j = hp.j[blockIdx.y];
   const int p = blockIdx.x, tid = threadIdx.x;
   const int n = *(const int*)((const char*)j.count + (size_t)p * j.count_stride_bytes);
   const float4* pts = j.pts + (size_t)p * j.pts_stride + (j.pts_off ? j.pts_off[p * j.pts_off_stride] : 0);
@@ -216,9 +222,6 @@ __global__ __launch_bounds__(NT) void k_hash_build(HashJob j) {
 // bucket counters, counts with global atomics, one workgroup scans, and the grid scatters.  The
 // order of points inside a bucket differs from the single-workgroup build (both are atomic
 // orders); no consumer depends on it (every search breaks ties on the source index).
-struct HashPair {
-  HashJob j[2];
-};
 constexpr int kHashGrid = 32;  // workgroups per cloud
 
 LOAM_D int hash_table_size(const HashJob& j, int n) {
@@ -349,13 +352,11 @@ __global__ __launch_bounds__(256) void k_hash_scatter(HashPair hp) {
 
 void hash_build_pair(const HashJob& a, const HashJob& b, int P, hipStream_t st, bool wide) {
   if (P > 4) {  // batches: a workgroup per cloud fills the chip
-    if (wide) {
-      hipLaunchKernelGGL(k_hash_build<1024>, dim3(P), dim3(1024), 0, st, a);
-      hipLaunchKernelGGL(k_hash_build<1024>, dim3(P), dim3(1024), 0, st, b);
-    } else {
-      hipLaunchKernelGGL(k_hash_build<512>, dim3(P), dim3(512), 0, st, a);
-      hipLaunchKernelGGL(k_hash_build<512>, dim3(P), dim3(512), 0, st, b);
-    }
+    HashPair hp;
+    hp.j[0] = a;
+    hp.j[1] = b;
+    if (wide) hipLaunchKernelGGL(k_hash_build<1024>, dim3(P, 2), dim3(1024), 0, st, hp);
+    else hipLaunchKernelGGL(k_hash_build<512>, dim3(P, 2), dim3(512), 0, st, hp);
     return;
   }
   HashPair hp;
