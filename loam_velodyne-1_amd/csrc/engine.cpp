@@ -103,10 +103,16 @@ struct loam_ctx {
   // tune.step_pipe: consecutive steps overlap — the odometry of a step (st) beside the mapping of the
   // previous one (st4), the scan registration + seed of the next (st3); hand-offs by events (batch_enqueue_pipe)
   hipStream_t st4 = nullptr;
-  hipEvent_t od_done = nullptr, mp1_done = nullptr, inputs_read = nullptr, a_start = nullptr, b_last = nullptr;
-  hipEvent_t mp1_read = nullptr;  // frame 1 has read Last[0] (after its k_mp_stack)
+  hipEvent_t od_done = nullptr, mp1_done = nullptr, a_start = nullptr, b_last = nullptr;
+  hipEvent_t mp1_read = nullptr;  // frame 1 has read Last[s] (after its k_mp_stack)
+  hipEvent_t inputs_read[2] = {nullptr, nullptr};  // frame 2 of the steps reading SR set i has read Last[e]
   hipEvent_t mp_done[2] = {nullptr, nullptr};
-  bool mp_done_rec[2] = {false, false}, inputs_read_rec = false, b_used = false;
+  bool mp_done_rec[2] = {false, false}, inputs_read_rec[2] = {false, false}, b_used = false;
+  // the Last buffers (OdBuffers, kOdBufs of them) of the next step: its seed's (od_s, the odometry's
+  // Last) and its TransformToEnd's (od_e, frame 2's input).  The step pipeline rotates (s, e) ->
+  // (3 - s - e, s), so the next seed writes the buffer no running step reads and never waits for the
+  // odometry; batch_enqueue keeps them.  od_s_last: the seed buffer of the last enqueued step.
+  int od_s = 0, od_e = 1, od_s_last = 0;
   bool step_done_rec[2] = {false, false};
   int sr_idx = 0;         // the set the next step reads
   bool sr_ready = false;  // its scan registration is already enqueued (st3, sr_done)
@@ -119,7 +125,7 @@ struct loam_ctx {
     sr_ready = false;
     seed_ready = false;
     mp_done_rec[0] = mp_done_rec[1] = false;
-    inputs_read_rec = b_used = false;
+    inputs_read_rec[0] = inputs_read_rec[1] = b_used = false;
     sr_idx = srb_last = 0;
     step_done_rec[0] = step_done_rec[1] = false;
   }
@@ -292,8 +298,8 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->sr_done, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->ahead_at, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_at, hipEventDisableTiming);
-  for (hipEvent_t* e : {&x->od_done, &x->mp1_done, &x->inputs_read, &x->a_start, &x->b_last, &x->mp_done[0], &x->mp_done[1],
-                        &x->mp1_read})
+  for (hipEvent_t* e : {&x->od_done, &x->mp1_done, &x->inputs_read[0], &x->inputs_read[1], &x->a_start, &x->b_last,
+                        &x->mp_done[0], &x->mp_done[1], &x->mp1_read})
     if (he == hipSuccess) he = hipEventCreateWithFlags(e, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_done, hipEventDisableTiming);
   for (auto& e : x->step_done)
@@ -366,8 +372,8 @@ void loam_destroy(loam_ctx* x) {
   if (x->sr_done) (void)hipEventDestroy(x->sr_done);
   if (x->ahead_at) (void)hipEventDestroy(x->ahead_at);
   if (x->seed_at) (void)hipEventDestroy(x->seed_at);
-  for (hipEvent_t e : {x->od_done, x->mp1_done, x->inputs_read, x->a_start, x->b_last, x->mp_done[0], x->mp_done[1],
-                       x->mp1_read})
+  for (hipEvent_t e : {x->od_done, x->mp1_done, x->inputs_read[0], x->inputs_read[1], x->a_start, x->b_last,
+                       x->mp_done[0], x->mp_done[1], x->mp1_read})
     if (e) (void)hipEventDestroy(e);
   if (x->st4) (void)hipStreamDestroy(x->st4);
   if (x->seed_done) (void)hipEventDestroy(x->seed_done);
@@ -687,7 +693,8 @@ int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_i
   HIP_TRY(hipEventRecord(x->ev[1], x->st));
   HIP_TRY(hipGetLastError());
   x->od_last = nxt;
-  // state (kOdStateFloats), istate (kOdStateInts), nlast (4), nfullEnd (2) into the mapped host
+  // state (kOdStateFloats), istate (kOdStateInts), nlast (4: problem 0's buffers 0 and 1, the two the
+  // streaming path alternates), nfullEnd (2) into the mapped host
   // block in one launch, then copied out (the host edits st / ist below)
   static_assert(kXferOd + 4 * (kOdStateFloats + kOdStateInts + 6) <= kXferMp, "odometry transfer region");
   {
@@ -815,7 +822,7 @@ int loam_chain_sweep(loam_ctx* x, double stamp, loam_cloud_in raw, loam_chain_ou
   in.full = o.fullEnd + (size_t)nxt * o.P * o.capS;
   in.corner_stride = o.capC; in.surf_stride = o.capS; in.full_stride = o.capS;
   in.ncorner = o.nlast + nxt * 2; in.nsurf = o.nlast + nxt * 2 + 1; in.nfull = o.nfullEnd + nxt;
-  in.ncorner_stride = in.nsurf_stride = 4; in.nfull_stride = 2;
+  in.ncorner_stride = in.nsurf_stride = 2 * kOdBufs; in.nfull_stride = kOdBufs;
   in.pose = nullptr; in.pose_stride = 6;
   float rp[2];
   int front = 0;
@@ -947,6 +954,8 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   // scan registration of this step: already enqueued one step ahead (st3), or here
   const int idx = x->sr_idx;
   SrBuffers& sb = x->srbuf(idx);
+  const int ls = x->od_s, le = x->od_e;  // (Last buffers: the seed's, TransformToEnd's)
+  x->od_s_last = ls;
   if (events) T(hipEventRecord(x->ev[0], x->st));
   x->prof.begin(x->st);
   if (x->b_used) {  // pipelined steps' mappings may still run on st4 / st2 (batch_enqueue_pipe)
@@ -978,33 +987,32 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
     x->seed_ready = false;
   } else {
     T(hipMemsetAsync(o.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st));
-    hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fprev, 0, 1, 0);
+    hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fprev, ls, 1, 0);
     x->prof.mark("k_od_end_seed");
-    od_build_hashes(o, 0, x->st);
+    od_build_hashes(o, ls, x->st);
     x->prof.mark("k_hash_build_last");
   }
   ahead_point(1);
-  // mapping frame 1 (prev into an empty map at the origin) reads only the seeding's Last[0] /
-  // fullEnd[0]: it runs on a second stream beside the odometry solve, whose L-M iterations are
+  // mapping frame 1 (prev into an empty map at the origin) reads only the seeding's Last[s]: it runs on a second stream beside the odometry solve, whose L-M iterations are
   // chains of small latency-bound launches that leave most of the chip idle.  The profiling pass
   // keeps one stream so that its per-kernel event times stay attributable.
   const bool overlap = x->st2 && !pf;
   if (overlap) {
     T(hipEventRecord(x->fork, x->st));
     T(hipStreamWaitEvent(x->st2, x->fork, 0));
-    mp_batch_frame1(x->mpbuf(idx), o, fprev, x->st2, nullptr);
+    mp_batch_frame1(x->mpbuf(idx), o, ls, fprev, x->st2, nullptr);
     T(hipEventRecord(x->join, x->st2));
   }
   // the pose accumulation (k_od_fini, one serial double-trig chain per problem) beside
   // TransformToEnd on the second stream: both only read the solved transform
-  od_solve(o, fcur, 0, x->st, pf, /*device_fini=*/!overlap);
+  od_solve(o, fcur, ls, x->st, pf, /*device_fini=*/!overlap);
   if (overlap) {
     T(hipEventRecord(x->fork2, x->st));
     T(hipStreamWaitEvent(x->st2, x->fork2, 0));
     od_fini(o, fcur, x->st2);
     T(hipEventRecord(x->join2, x->st2));
   }
-  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, 1, 2, 0);
+  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, le, 2, 0);
   x->prof.mark("k_od_end");
   if (overlap) T(hipStreamWaitEvent(x->st, x->join2, 0));
   if (events) T(hipEventRecord(x->ev[2], x->st));
@@ -1012,7 +1020,7 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   if (overlap) {
     T(hipStreamWaitEvent(x->st, x->join, 0));
   } else {
-    mp_batch_frame1(x->mpbuf(idx), o, fprev, x->st, pf);
+    mp_batch_frame1(x->mpbuf(idx), o, ls, fprev, x->st, pf);
   }
   ahead_point(2);
   if (ahead) T(hipEventRecord(x->seed_at, x->st));
@@ -1020,7 +1028,7 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   SideStream side;
   side.st = x->st2;
   side.fork[0] = x->fork; side.join[0] = x->join; side.fork[1] = x->fork2; side.join[1] = x->join2;
-  mp_batch_frame2(x->mpbuf(idx), o, fcur, x->st, pf, overlap ? &side : nullptr);
+  mp_batch_frame2(x->mpbuf(idx), o, le, fcur, x->st, pf, overlap ? &side : nullptr);
   x->mp_last = idx;
   if (events) T(hipEventRecord(x->ev[3], x->st));
   x->srb_last = idx;
@@ -1036,26 +1044,27 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
     T(hipEventRecord(x->sr_done, x->st3));
     x->sr_ready = true;
     x->sr_idx = nx;
-    // the next step's odometry seed: Last[0] / its hashes are free once this step's odometry is
-    // done (the second mapping frame reads Last[1] and the state only); its counts go to the other
+    // the next step's odometry seed: Last[s] / its hashes are free once this step's odometry is
+    // done (the second mapping frame reads Last[e] and the state only); its counts go to the other
     // istate set, which the next step reads
     T(hipStreamWaitEvent(x->st3, x->seed_at, 0));
     OdBuffers on = o;
     on.istate = o.istate_set[nx];
     T(hipMemsetAsync(on.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st3));
-    hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st3, on, feat_view(x->srbuf(nx), 0, 2), 0, 1, 0);
-    od_build_hashes(on, 0, x->st3);
+    hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st3, on, feat_view(x->srbuf(nx), 0, 2), ls, 1, 0);
+    od_build_hashes(on, ls, x->st3);
     T(hipEventRecord(x->seed_done, x->st3));
     x->seed_ready = true;
   }
   T(hipGetLastError());
   return e;
 }
-// The scan registration of the step reading buffer set i and its odometry seed (Last[0], its
+// The scan registration of the step reading buffer set i and its odometry seed (Last[ls], its
 // hashes, the counts in istate set i), on st3.  Waits: the set's previous step is done with it
-// (mp_done[i]: its mapping, the last reader), and Last[0] is free (od_done / mp1_read of the step
-// before, passed as `free_last`).
-hipError_t enqueue_ahead(loam_ctx* x, int i, bool free_last) {
+// (mp_done[i]: its mapping, the last reader, after that step's odometry), and, when `free_last` is
+// recorded, Last[ls]'s last reader: frame 2 of the step before the current one (the rotation of
+// batch_enqueue_pipe leaves Last[ls] to no running step's odometry or frame 1).
+hipError_t enqueue_ahead(loam_ctx* x, int i, int ls, hipEvent_t free_last) {
   const int P = x->P;
   OdBuffers on = x->odb;
   hipError_t e = hipSuccess;
@@ -1064,14 +1073,11 @@ hipError_t enqueue_ahead(loam_ctx* x, int i, bool free_last) {
   T(hipStreamWaitEvent(x->st3, x->a_start, 0));  // (whatever ran on st before this call)
   sr_launch(x->srbuf(i), sr_params(x), x->st3, nullptr);
   T(hipEventRecord(x->sr_done, x->st3));
-  if (free_last) {  // Last[0] read by this step's odometry and frame 1 (its k_mp_stack)
-    T(hipStreamWaitEvent(x->st3, x->od_done, 0));
-    T(hipStreamWaitEvent(x->st3, x->mp1_read, 0));
-  }
+  if (free_last) T(hipStreamWaitEvent(x->st3, free_last, 0));
   on.istate = on.istate_set[i];
   T(hipMemsetAsync(on.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st3));
-  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st3, on, feat_view(x->srbuf(i), 0, 2), 0, 1, 0);
-  od_build_hashes(on, 0, x->st3);
+  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st3, on, feat_view(x->srbuf(i), 0, 2), ls, 1, 0);
+  od_build_hashes(on, ls, x->st3);
   T(hipEventRecord(x->seed_done, x->st3));
   x->sr_ready = x->seed_ready = true;
   return e;
@@ -1079,25 +1085,30 @@ hipError_t enqueue_ahead(loam_ctx* x, int i, bool free_last) {
 
 // One batch step as a stage of a software pipeline over consecutive steps (tune.step_pipe):
 //   st3  scan registration + odometry seed of step k + 1 (enqueue_ahead)
-//   st   odometry of step k (L-M, pose accumulation, TransformToEnd of Last[1])
-//   st4 / st2  mapping of step k: frame 1 (needs the seed), frame 2 (needs the odometry); with two
-//        mapping sets (tune.pipe_mp_sets = 2) the steps alternate between st4 and st2
-// so the odometry of step k + 1 runs beside the mapping of step k.  Buffers shared between steps:
-// the SR set, the odometry state / istate sets and the mapping sets alternate; Last[0] is rewritten
-// by the next seed only after this step's odometry and frame 1 have read it (od_done, mp1_read);
-// Last[1] by the next odometry only after this step's frame 2 has read it (inputs_read).  Every step
-// does the same work as batch_enqueue's; loam_batch_sync waits for all four streams.
+//   st   odometry of step k (L-M against Last[s], pose accumulation, TransformToEnd into Last[e])
+//   st4 / st2  mapping of step k: frame 1 (reads Last[s]), frame 2 (reads Last[e], after the
+//        odometry); with two mapping sets (tune.pipe_mp_sets = 2) the steps alternate st4 / st2
+// so the odometry of step k + 1 runs beside the mapping of step k and the seed of step k + 2 beside
+// both.  Buffers shared between steps: the SR set, the odometry state / istate sets and the mapping
+// sets alternate; the three Last buffers rotate (s, e) -> (3 - s - e, s): step k + 1 seeds the one
+// step k - 1's frame 2 read last (inputs_read of that parity), and step k + 1's TransformToEnd
+// rewrites step k's Last[s] once frame 1 of step k has read it (mp1_read; the odometry of step k is
+// ahead on st).  Every step does the same work as batch_enqueue's; loam_batch_sync waits for all
+// four streams.
 hipError_t batch_enqueue_pipe(loam_ctx* x) {
   const int P = x->P;
   OdBuffers& o = x->odb;
   hipError_t e = hipSuccess;
   auto T = [&](hipError_t r) { if (e == hipSuccess) e = r; };
   const int idx = x->sr_idx, nx = 1 - idx;
+  const int ls = x->od_s, le = x->od_e, lf = kOdBufs - ls - le;
+  static_assert(kOdBufs == 3, "the rotation takes three Last buffers");
   SrBuffers& sb = x->srbuf(idx);
   T(hipEventRecord(x->a_start, x->st));
   T(hipEventRecord(x->ev[0], x->st));
-  if (!x->sr_ready || !x->seed_ready) T(enqueue_ahead(x, idx, false));
+  if (!x->sr_ready || !x->seed_ready) T(enqueue_ahead(x, idx, ls, nullptr));
   x->sr_ready = x->seed_ready = false;
+  x->od_s_last = ls;
   const FeatView fprev = feat_view(sb, 0, 2), fcur = feat_view(sb, 1, 2);
   // odometry (st)
   o.istate = o.istate_set[idx];
@@ -1106,9 +1117,11 @@ hipError_t batch_enqueue_pipe(loam_ctx* x) {
   T(hipStreamWaitEvent(x->st, x->seed_done, 0));
   T(hipEventRecord(x->ev[1], x->st));
   T(hipMemsetAsync(o.state, 0, (size_t)P * kOdStateFloats * sizeof(float), x->st));
-  od_solve(o, fcur, 0, x->st, nullptr, /*device_fini=*/true);
-  if (x->inputs_read_rec) T(hipStreamWaitEvent(x->st, x->inputs_read, 0));  // (the last frame 2 read Last[1])
-  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, 1, 2, 0);
+  od_solve(o, fcur, ls, x->st, nullptr, /*device_fini=*/true);
+  // Last[le] was the previous step's Last[s]: its frame 1 has read it (its odometry is ahead on st);
+  // before that, frame 2 of the step before read it, which the previous seed waited for
+  if (x->b_used) T(hipStreamWaitEvent(x->st, x->mp1_read, 0));
+  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, le, 2, 0);
   T(hipEventRecord(x->od_done, x->st));
   T(hipEventRecord(x->ev[2], x->st));
   // mapping: frame 1 once the seed (and this call's earlier work on st) is there, frame 2 once the
@@ -1120,25 +1133,28 @@ hipError_t batch_enqueue_pipe(loam_ctx* x) {
   MpBuffers& mb = two ? x->mpbuf(idx) : x->mpb;
   T(hipStreamWaitEvent(ms, x->a_start, 0));
   T(hipStreamWaitEvent(ms, x->seed_done, 0));
-  SideStream side1;  // (no branches: only the event once Last[0] is read)
+  SideStream side1;  // (no branches: only the event once Last[ls] is read)
   side1.inputs_read = x->mp1_read;
-  mp_batch_frame1(mb, o, fprev, ms, nullptr, &side1);
+  mp_batch_frame1(mb, o, ls, fprev, ms, nullptr, &side1);
   T(hipEventRecord(x->mp1_done, ms));
   T(hipStreamWaitEvent(ms, x->od_done, 0));
   SideStream side;
   side.st = two ? nullptr : x->st2;
   side.fork[0] = x->fork; side.join[0] = x->join; side.fork[1] = x->fork2; side.join[1] = x->join2;
-  side.inputs_read = x->inputs_read;
-  mp_batch_frame2(mb, o, fcur, ms, nullptr, &side);
-  x->inputs_read_rec = true;
+  side.inputs_read = x->inputs_read[idx];
+  mp_batch_frame2(mb, o, le, fcur, ms, nullptr, &side);
   T(hipEventRecord(x->mp_done[idx], ms));
   x->mp_done_rec[idx] = true;
   x->b_used = true;
   x->mp_last = two ? idx : 0;
   T(hipEventRecord(x->ev[3], ms));
   x->srb_last = idx;
-  // the next step's scan registration + seed (st3)
-  T(enqueue_ahead(x, nx, true));
+  // the next step's scan registration + seed (st3) into Last[lf], which frame 2 of the previous
+  // step (SR set nx) read last
+  T(enqueue_ahead(x, nx, lf, x->inputs_read_rec[nx] ? x->inputs_read[nx] : nullptr));
+  x->inputs_read_rec[idx] = true;
+  x->od_s = lf;
+  x->od_e = ls;
   x->sr_idx = nx;
   T(hipGetLastError());
   return e;
@@ -1202,7 +1218,7 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
   if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
   if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));  // (the work enqueued ahead rewrites Last[0] alike)
   std::vector<float> st((size_t)P * kOdStateFloats);
-  std::vector<int> ist((size_t)P * kOdStateInts), srerr(2 * P), cnt(8 * P), nfull(2 * P), nl(4 * P);
+  std::vector<int> ist((size_t)P * kOdStateInts), srerr(2 * P), cnt(8 * P), nfull(2 * P), nl((size_t)kOdBufs * 2 * P);
   HIP_TRY(hipMemcpy(st.data(), x->odb.state, st.size() * sizeof(float), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(ist.data(), x->odb.istate, ist.size() * sizeof(int), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(srerr.data(), x->srbuf(x->srb_last).err, srerr.size() * sizeof(int), hipMemcpyDeviceToHost));
@@ -1229,6 +1245,7 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
   std::vector<int> rn(2 * P);
   HIP_TRY(hipMemcpy(rn.data(), x->srbuf(x->srb_last).raw_n, rn.size() * sizeof(int), hipMemcpyDeviceToHost));
   for (int i = 0; i < 2 * P; ++i) s.n_raw += rn[i];
+  const int ls = x->od_s_last;  // (the last step's Last[s]; every step reads the same counts)
   for (int i = 0; i < P; ++i) {
     const int* q = &ist[(size_t)i * kOdStateInts];
     if (q[kIsErr]) return fail(LOAM_E_CAPACITY, "odometry capacity exceeded");
@@ -1243,9 +1260,10 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
     const uint64_t nq = q[kIsAssoc] ? (uint64_t)(q[kIsQueries] / q[kIsAssoc]) : 0, it = (uint64_t)q[kIsIters];
     s.od_query_iters += nq * it;
     s.od_row_evals += nq * it * (it + 1) / 2;
-    s.od_corner_last += nl[i * 4 + 0];
-    s.od_surf_last += nl[i * 4 + 1];
-    s.od_assoc_points += (uint64_t)q[kIsAssoc] * (nl[i * 4 + 0] + nl[i * 4 + 1]);
+    const int* n = &nl[((size_t)i * kOdBufs + ls) * 2];
+    s.od_corner_last += n[0];
+    s.od_surf_last += n[1];
+    s.od_assoc_points += (uint64_t)q[kIsAssoc] * (n[0] + n[1]);
   }
   count_bytes(s);
   x->prof.collect();

@@ -3039,17 +3039,18 @@ int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::s
   return LOAM_OK;
 }
 
-// frame 1 of the batch problem: reset, then prev (Last[0], fullEnd[0]) into the empty store at
+// frame 1 of the batch problem: reset, then prev (the seed's Last[buf]) into the empty store at
 // the zero pose.  Reads only what the odometry seeding wrote, so it may run beside od_solve.
-void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, const FeatView& fprev, hipStream_t st, Prof* prof,
+void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, int buf, const FeatView& fprev, hipStream_t st, Prof* prof,
                      const SideStream* side) {
   b.note(mp_reset(b, st));
   if (prof) prof->mark("mp_reset");
   MpInput in;
-  in.corner = od.lastC; in.surf = od.lastS;
+  in.corner = od.lastC + (size_t)buf * od.P * od.capC;
+  in.surf = od.lastS + (size_t)buf * od.P * od.capS;
   in.corner_stride = od.capC; in.surf_stride = od.capS;
-  in.ncorner = od.nlast + 0; in.nsurf = od.nlast + 1;
-  in.ncorner_stride = 4; in.nsurf_stride = 4;
+  in.ncorner = od.nlast + buf * 2; in.nsurf = od.nlast + buf * 2 + 1;
+  in.ncorner_stride = 2 * kOdBufs; in.nsurf_stride = 2 * kOdBufs;
   // the full cloud: prev's raw one, TransformToEnd with the zero transform in k_mp_register
   in.full = fprev.full; in.full_stride = fprev.full_stride;
   in.nfull = fprev.nfull_p; in.nfull_stride = fprev.nfull_stride;
@@ -3058,15 +3059,15 @@ void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, const FeatView& fprev, h
   mp_frame(b, in, st, prof, /*map_empty=*/true, nullptr, -1, side);
 }
 
-// frame 2: cur (Last[1], fullEnd[1]) with the odometry transformSum
-void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, const FeatView& fcur, hipStream_t st, Prof* prof,
+// frame 2: cur (TransformToEnd's Last[buf]) with the odometry transformSum
+void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, int buf, const FeatView& fcur, hipStream_t st, Prof* prof,
                      const SideStream* side) {
   MpInput in;
-  in.corner = od.lastC + (size_t)od.P * od.capC;
-  in.surf = od.lastS + (size_t)od.P * od.capS;
+  in.corner = od.lastC + (size_t)buf * od.P * od.capC;
+  in.surf = od.lastS + (size_t)buf * od.P * od.capS;
   in.corner_stride = od.capC; in.surf_stride = od.capS;
-  in.ncorner = od.nlast + 2; in.nsurf = od.nlast + 3;
-  in.ncorner_stride = 4; in.nsurf_stride = 4;
+  in.ncorner = od.nlast + buf * 2; in.nsurf = od.nlast + buf * 2 + 1;
+  in.ncorner_stride = 2 * kOdBufs; in.nsurf_stride = 2 * kOdBufs;
   // the full cloud: cur's raw one, TransformToEnd with the solved transform in k_mp_register
   in.full = fcur.full; in.full_stride = fcur.full_stride;
   in.nfull = fcur.nfull_p; in.nfull_stride = fcur.nfull_stride;

@@ -178,12 +178,13 @@ int mp_stream_frame_dev(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum
 // /laser_cloud_surround of the last streaming frame (instance 0): its 5x5x5 cube neighbourhood
 // concatenated and VoxelGrid 0.2 (src/laserMapping.cpp:1038-1058)
 int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::string& err);
+// buf: the odometry's Last buffer the frame reads (frame 1: the seed's, frame 2: TransformToEnd's)
 // fprev / fcur: the scan registration outputs whose full clouds the frames register
 // side: only its inputs_read event is used (the frame runs on st alone)
-void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, const FeatView& fprev, hipStream_t st, Prof* prof = nullptr,
-                     const SideStream* side = nullptr);
-void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, const FeatView& fcur, hipStream_t st, Prof* prof = nullptr,
-                     const SideStream* side = nullptr);
+void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, int buf, const FeatView& fprev, hipStream_t st,
+                     Prof* prof = nullptr, const SideStream* side = nullptr);
+void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, int buf, const FeatView& fcur, hipStream_t st,
+                     Prof* prof = nullptr, const SideStream* side = nullptr);
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err);
 
 }  // namespace loam

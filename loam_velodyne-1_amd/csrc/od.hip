@@ -891,7 +891,7 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
   const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
   const float4* sel = b.sel + (size_t)p * b.cap_q;
   const size_t lp = (size_t)last_buf * b.P + p;
-  const int C = b.nlast[(p * 2 + last_buf) * 2 + 0], S = b.nlast[(p * 2 + last_buf) * 2 + 1];
+  const int C = b.nlast[(p * kOdBufs + last_buf) * 2 + 0], S = b.nlast[(p * kOdBufs + last_buf) * 2 + 1];
   const float4* CL = b.lastC + lp * b.capC;
   const float4* SL = b.lastS + lp * b.capS;
   int* ind = b.ind + (size_t)p * 3 * b.cap_q;
@@ -1109,7 +1109,7 @@ LOAM_D bool od_assoc_pts(const OdBuffers& b, int p, int q, int nc, size_t lp, fl
   const int* ind = b.ind + (size_t)p * 3 * b.cap_q;
   const int i1 = ind[q], i2 = ind[b.cap_q + q], i3 = ind[2 * b.cap_q + q];
   LOAM_CHECK(q < b.cap_q, q, p);
-  LOAM_CHECK(i1 < b.nlast[(p * 2 + (int)(lp / (size_t)b.P)) * 2 + (q < nc ? 0 : 1)], i1, q);
+  LOAM_CHECK(i1 < b.nlast[(p * kOdBufs + (int)(lp / (size_t)b.P)) * 2 + (q < nc ? 0 : 1)], i1, q);
   t1 = t2 = t3 = make_float4(0, 0, 0, 0);
   if (q < nc) {
     if (i2 < 0) return false;
@@ -1632,9 +1632,9 @@ __global__ __launch_bounds__(256) void k_od_end(OdBuffers b, FeatView f, int dst
     *o = mode == 0 ? a : loampose::transform_to_end(t, imu, er, a, mode == 1);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    b.nlast[(p * 2 + dst) * 2 + 0] = cl;
-    b.nlast[(p * 2 + dst) * 2 + 1] = cf;
-    b.nfullEnd[p * 2 + dst] = cu;
+    b.nlast[(p * kOdBufs + dst) * 2 + 0] = cl;
+    b.nlast[(p * kOdBufs + dst) * 2 + 1] = cf;
+    b.nfullEnd[p * kOdBufs + dst] = cu;
     if (mode != 0) {  // laserCloudCornerLastNum / SurfLastNum (:901-902); the init frame leaves 0 (Q8)
       b.istate[(size_t)p * kOdStateInts + kIsCornerLastNum] = cl;
       b.istate[(size_t)p * kOdStateInts + kIsSurfLastNum] = cf;
@@ -1660,23 +1660,23 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   A(&b.istate_set[0], (size_t)P * kOdStateInts * sizeof(int));
   A(&b.istate_set[1], (size_t)P * kOdStateInts * sizeof(int));
   b.istate = b.istate_set[0];
-  A(&b.lastC, (size_t)2 * P * b.capC * sizeof(float4));
-  A(&b.lastS, (size_t)2 * P * b.capS * sizeof(float4));
-  A(&b.fullEnd, (size_t)2 * P * b.capS * sizeof(float4));
-  A(&b.nlast, (size_t)P * 4 * sizeof(int));
-  A(&b.nfullEnd, (size_t)P * 2 * sizeof(int));
-  A(&b.hC_start, (size_t)2 * P * (b.tC + 1) * sizeof(int));
-  A(&b.hS_start, (size_t)2 * P * (b.tS + 1) * sizeof(int));
+  A(&b.lastC, (size_t)kOdBufs * P * b.capC * sizeof(float4));
+  A(&b.lastS, (size_t)kOdBufs * P * b.capS * sizeof(float4));
+  A(&b.fullEnd, (size_t)kOdBufs * P * b.capS * sizeof(float4));
+  A(&b.nlast, (size_t)P * kOdBufs * 2 * sizeof(int));
+  A(&b.nfullEnd, (size_t)P * kOdBufs * sizeof(int));
+  A(&b.hC_start, (size_t)kOdBufs * P * (b.tC + 1) * sizeof(int));
+  A(&b.hS_start, (size_t)kOdBufs * P * (b.tS + 1) * sizeof(int));
   A(&b.hC_fill, (size_t)P * b.tC * sizeof(int));
   A(&b.hS_fill, (size_t)P * b.tS * sizeof(int));
-  A(&b.hC_pts, (size_t)2 * P * b.capC * sizeof(float4));
-  A(&b.hS_pts, (size_t)2 * P * b.capS * sizeof(float4));
-  A(&b.hC_T, (size_t)2 * P * sizeof(int));
-  A(&b.cC, (size_t)2 * P * 2 * chunks_of(b.capC) * sizeof(float4));
-  A(&b.cS, (size_t)2 * P * 2 * chunks_of(b.capS) * sizeof(float4));
-  A(&b.fC, (size_t)2 * P * 2 * subs_of(b.capC) * sizeof(float4));
-  A(&b.fS, (size_t)2 * P * 2 * subs_of(b.capS) * sizeof(float4));
-  A(&b.hS_T, (size_t)2 * P * sizeof(int));
+  A(&b.hC_pts, (size_t)kOdBufs * P * b.capC * sizeof(float4));
+  A(&b.hS_pts, (size_t)kOdBufs * P * b.capS * sizeof(float4));
+  A(&b.hC_T, (size_t)kOdBufs * P * sizeof(int));
+  A(&b.cC, (size_t)kOdBufs * P * 2 * chunks_of(b.capC) * sizeof(float4));
+  A(&b.cS, (size_t)kOdBufs * P * 2 * chunks_of(b.capS) * sizeof(float4));
+  A(&b.fC, (size_t)kOdBufs * P * 2 * subs_of(b.capC) * sizeof(float4));
+  A(&b.fS, (size_t)kOdBufs * P * 2 * subs_of(b.capS) * sizeof(float4));
+  A(&b.hS_T, (size_t)kOdBufs * P * sizeof(int));
   A(&b.ind, (size_t)P * 3 * b.cap_q * sizeof(int));
   A(&b.sel, (size_t)P * b.cap_q * sizeof(float4));
   A(&b.q_cf, (size_t)P * max_iter * b.cap_q * sizeof(float4));
@@ -1684,8 +1684,8 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   // per-workgroup partials: [P][gq][28], or [P][gq * max_iter][28] for the small-batch rows kernel
   A(&b.part, (size_t)P * b.gq * max_iter * 28 * sizeof(double));  // (k_od_rows_small: per stored iteration)
   A(&b.done, (size_t)P * sizeof(int));
-  A(&b.mono, (size_t)2 * P * 2 * sizeof(int));
-  A(&b.rstart, (size_t)2 * P * 2 * kRingTab * sizeof(int));
+  A(&b.mono, (size_t)kOdBufs * P * 2 * sizeof(int));
+  A(&b.rstart, (size_t)kOdBufs * P * 2 * kRingTab * sizeof(int));
   if (A.err != hipSuccess) {
     od_free(b);
     return A.err;
@@ -1695,10 +1695,10 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
     if (A.err == hipSuccess) A.err = hipMemset(b.state_set[k], 0, (size_t)P * kOdStateFloats * sizeof(float));
   for (int k = 0; k < 2; ++k)
     if (A.err == hipSuccess) A.err = hipMemset(b.istate_set[k], 0, (size_t)P * kOdStateInts * sizeof(int));
-  if (A.err == hipSuccess) A.err = hipMemset(b.nlast, 0, (size_t)P * 4 * sizeof(int));
-  if (A.err == hipSuccess) A.err = hipMemset(b.nfullEnd, 0, (size_t)P * 2 * sizeof(int));
-  if (A.err == hipSuccess) A.err = hipMemset(b.hC_T, 0, (size_t)2 * P * sizeof(int));
-  if (A.err == hipSuccess) A.err = hipMemset(b.hS_T, 0, (size_t)2 * P * sizeof(int));
+  if (A.err == hipSuccess) A.err = hipMemset(b.nlast, 0, (size_t)P * kOdBufs * 2 * sizeof(int));
+  if (A.err == hipSuccess) A.err = hipMemset(b.nfullEnd, 0, (size_t)P * kOdBufs * sizeof(int));
+  if (A.err == hipSuccess) A.err = hipMemset(b.hC_T, 0, (size_t)kOdBufs * P * sizeof(int));
+  if (A.err == hipSuccess) A.err = hipMemset(b.hS_T, 0, (size_t)kOdBufs * P * sizeof(int));
   if (A.err != hipSuccess) od_free(b);
   return A.err;
 }
@@ -1720,7 +1720,7 @@ void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
   jc.pts_off = nullptr;
   jc.pts_off_stride = 0;
   jc.count = b.nlast + buf * 2 + 0;
-  jc.count_stride_bytes = 4 * sizeof(int);
+  jc.count_stride_bytes = 2 * kOdBufs * sizeof(int);
   jc.start = b.hC_start + (size_t)buf * b.P * (b.tC + 1);
   jc.fill = b.hC_fill;
   jc.out = b.hC_pts + (size_t)buf * b.P * b.capC;

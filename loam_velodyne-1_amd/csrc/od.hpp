@@ -74,37 +74,41 @@ LOAM_HD uint32_t hash_rec(int start, int count) {
   return start < (1 << 19) && count < (1 << 13) ? (uint32_t)start | ((uint32_t)count << 19) : kRecNone;
 }
 
+// Last-cloud buffers (Last corner / surf, fullEnd, their counts, hashes, boxes, flags): the streaming
+// path alternates two, the batch step pipeline rotates three (the seed's, TransformToEnd's, a free one)
+constexpr int kOdBufs = 3;
+
 struct OdBuffers {
   int P = 0, capC = 0, capS = 0, cap_q = 0, gq = 0, tC = 0, tS = 0, max_iter = 25;
   float* state = nullptr;   // [P][kOdStateFloats] (one of state_set: batches alternate per step)
   float* state_set[2] = {nullptr, nullptr};
   int* istate = nullptr;    // [P][kOdStateInts] (one of istate_set: batches alternate per step)
   int* istate_set[2] = {nullptr, nullptr};
-  float4* lastC = nullptr;  // [2][P][capC]
-  float4* lastS = nullptr;  // [2][P][capS]
-  float4* fullEnd = nullptr;  // [2][P][capS]
-  int* nlast = nullptr;     // [P][2][2]
-  int* nfullEnd = nullptr;  // [P][2]
-  int* hC_start = nullptr;  // [2][P][tC+1]
-  int* hS_start = nullptr;  // [2][P][tS+1]
+  float4* lastC = nullptr;  // [kOdBufs][P][capC]
+  float4* lastS = nullptr;  // [kOdBufs][P][capS]
+  float4* fullEnd = nullptr;  // [kOdBufs][P][capS]
+  int* nlast = nullptr;     // [P][kOdBufs][2]
+  int* nfullEnd = nullptr;  // [P][kOdBufs]
+  int* hC_start = nullptr;  // [kOdBufs][P][tC+1]
+  int* hS_start = nullptr;  // [kOdBufs][P][tS+1]
   int* hC_fill = nullptr;   // [P][tC]
   int* hS_fill = nullptr;   // [P][tS]
-  float4* hC_pts = nullptr; // [2][P][capC]
-  float4* hS_pts = nullptr; // [2][P][capS]
-  int* hC_T = nullptr;      // [2][P]
-  int* hS_T = nullptr;      // [2][P]
-  float4* cC = nullptr;     // [2][P][2 * chunks_of(capC)] chunk boxes of Last corner
-  float4* cS = nullptr;     // [2][P][2 * chunks_of(capS)] chunk boxes of Last surf
-  float4* fC = nullptr;     // [2][P][2 * subs_of(capC)] sub-chunk boxes of Last corner (HashJob::fine)
-  float4* fS = nullptr;     // [2][P][2 * subs_of(capS)] sub-chunk boxes of Last surf
+  float4* hC_pts = nullptr; // [kOdBufs][P][capC]
+  float4* hS_pts = nullptr; // [kOdBufs][P][capS]
+  int* hC_T = nullptr;      // [kOdBufs][P]
+  int* hS_T = nullptr;      // [kOdBufs][P]
+  float4* cC = nullptr;     // [kOdBufs][P][2 * chunks_of(capC)] chunk boxes of Last corner
+  float4* cS = nullptr;     // [kOdBufs][P][2 * chunks_of(capS)] chunk boxes of Last surf
+  float4* fC = nullptr;     // [kOdBufs][P][2 * subs_of(capC)] sub-chunk boxes of Last corner (HashJob::fine)
+  float4* fS = nullptr;     // [kOdBufs][P][2 * subs_of(capS)] sub-chunk boxes of Last surf
   float4* sel = nullptr;      // [P][cap_q] queries at the current transform (association rounds)
   int* ind = nullptr;         // [P][3][cap_q] association of every query (refreshed every 5th iteration)
   float4* q_cf = nullptr;     // [P][max_iter][cap_q] coefficients (zero when rejected)
   int8_t* q_ok = nullptr;     // [P][max_iter][cap_q] accepted flags
   double* part = nullptr;     // [P][gq][28] per-workgroup JᵀJ | Jᵀb | rows
   int* done = nullptr;        // [P] workgroups of k_od_rows finished (the last one runs the step)
-  int* mono = nullptr;        // [2][P][2] Last corner / surf of each buffer ring-monotone (HashJob::mono)
-  int* rstart = nullptr;      // [2][P][2][kRingTab] their ring start tables (HashJob::rstart)
+  int* mono = nullptr;        // [kOdBufs][P][2] Last corner / surf of each buffer ring-monotone (HashJob::mono)
+  int* rstart = nullptr;      // [kOdBufs][P][2][kRingTab] their ring start tables (HashJob::rstart)
   Tuning tune;                // host-side launch choices (od_solve)
 };
 
