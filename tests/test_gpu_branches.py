@@ -276,3 +276,33 @@ def test_tuning_rejects_unknown(loam):
     with pytest.raises(Exception):
         e.set_tuning(nn_lanes=3)
     e.close()
+
+
+def test_pipeline_rotation_then_sequential(loam, oc, sg):
+    """the step pipeline's three Last buffers through a whole rotation and one more step (four
+    pipelined steps: (s, e) = (0, 1), (2, 0), (1, 2), (0, 1)), then sequential steps (step_pipe 0)
+    on the buffers the rotation left, on the one context: every download equals a one-step run,
+    the Last-cloud counts in the stats included (they are read from the last step's seed buffer)"""
+    if "default" not in _SHARE:
+        _SHARE["default"] = _share_run(loam, sg)
+    od0, aft0, st0 = _SHARE["default"]
+    prevs, curs = _SHARE["inputs"]
+    e = loam.Engine()
+    e.set_tuning(step_pipe=1)
+    e.batch_upload(prevs, curs)
+    for n in (1, 2, 3, 4, 5):
+        e.batch_run()
+        od, aft, st = e.batch_download()
+        np.testing.assert_array_equal(od, od0)
+        np.testing.assert_array_equal(aft, aft0)
+        for k in ("od_iters", "mp_iters", "od_corner_last", "od_surf_last", "od_assoc_points"):
+            assert st[k] == st0[k], (n, k)
+    e.set_tuning(step_pipe=0)  # (drains the streams; the rotated (s, e) stay)
+    for n in range(2):
+        e.batch_run()
+        od, aft, st = e.batch_download()
+        np.testing.assert_array_equal(od, od0)
+        np.testing.assert_array_equal(aft, aft0)
+        for k in ("od_iters", "mp_iters", "od_corner_last", "od_surf_last", "od_assoc_points"):
+            assert st[k] == st0[k], ("sequential", n, k)
+    e.close()
