@@ -73,8 +73,10 @@ def kernel_bytes(st):
                       + 32 * st["od_assoc_boxes"],
         # per iteration: every stored row's coefficient (16 B) + accept flag (1 B) read back (Q12:
         # all rows so far re-evaluated at the current transform), the query point read (16 B) and
-        # its coefficient + flag written (17 B)
-        "k_od_rows": 17 * st["od_row_evals"] + 33 * st["od_query_iters"],
+        # its coefficient + flag written (17 B); with the per-query moments (tuning od_moments_min,
+        # st["od_moments"]) the query point (16 B) and its ten fp64 moments read and written (160 B)
+        "k_od_rows": (176 * st["od_query_iters"] if st.get("od_moments")
+                      else 17 * st["od_row_evals"] + 33 * st["od_query_iters"]),
         # per query-iteration: stack point read, ordered 5-NN written and last iteration's read
         # (16 + 32 + 32 B); 8 B per bucket range and 16 B per map point evaluated (seeds included)
         "k_mp_nn": 80 * st["mp_stack_iters"] + 8 * st["mp_nn_cells"] + 16 * st["mp_nn_candidates"],
@@ -98,15 +100,18 @@ SEARCH_KERNELS = ("k_mp_nn", "k_mp_nnfit", "k_od_assoc")
 
 def algorithmic_bytes(st):
     """SURVEY.md §8(d)'s algorithmic bytes per kernel and step: what the kernel must read and write
-    at minimum.  Equal to kernel_bytes except for the two search kernels, whose algorithmic cost is
-    the query and its answer, not the candidates the search visits: k_mp_nn = per query-iteration
-    the stack point and its 5 neighbours (16 + 80 B, B_MP); k_od_assoc = per association round every
-    Last point once (16 B (C + S), B_OD)."""
+    at minimum.  Equal to kernel_bytes for the streaming kernels.  The search and mapping L-M
+    kernels are priced by B_MP's / B_OD's per-unit terms, not by the candidates the search visits or
+    the engine's own caches (the MpFit record): k_mp_nn = per query-iteration the stack point and
+    its 5 neighbours (16 + 80 B); k_mp_fit = per accepted row 64 B (the row written and read back,
+    B_MP's 64 r_k); k_mp_nnfit = both (96 B per query-iteration + 64 B per row; the mapping rows'
+    counter mp_rows_sum); k_mp_iter's row reads are part of those 64 B, so it is not priced on its
+    own; k_od_assoc = per association round every Last point once (16 B (C + S), B_OD)."""
     alg = dict(kernel_bytes(st))
     alg["k_mp_nn"] = 96 * st["mp_stack_iters"]
-    # k_mp_nnfit: the search's 96 B, the record (32 B read + 32 B written, 32 B fit read) and the
-    # row (17 B); per refit the fit written (32 B)
-    alg["k_mp_nnfit"] = (96 + 96 + 17) * st["mp_stack_iters"] + 32 * st["mp_fits"]
+    alg["k_mp_fit"] = 64 * st["mp_rows_sum"]
+    alg["k_mp_nnfit"] = 96 * st["mp_stack_iters"] + 64 * st["mp_rows_sum"]
+    alg.pop("k_mp_iter")
     alg["k_od_assoc"] = 16 * st["od_assoc_points"]
     return alg
 
@@ -149,6 +154,8 @@ def rooflines(st, st_prof, ktimes, psteps, ms_per_step, traffic_file="traffic.js
         if traffic:
             roof["traffic_gbs"] = traffic / (avg_ms * 1e-3) / 1e9
             roof["traffic_frac"] = roof["traffic_gbs"] / HBM_PEAK_GBS
+            # HBM bytes (PMC, profiles/traffic*.json) per algorithmic byte: > 1 = re-reads / engine caches
+            roof["traffic_over_algorithmic"] = traffic / alg_launch
         if dom in SEARCH_KERNELS:
             # what the search actually reads (candidate cells, window points, chunk boxes), from the
             # work counters: L2-resident gathers, priced against the chip's L2 gather rate
@@ -175,6 +182,15 @@ def rooflines(st, st_prof, ktimes, psteps, ms_per_step, traffic_file="traffic.js
                 "frac": alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "kernel_busy_ms_per_step": round(sum(v[0] for v in ktimes.values()) / psteps, 4) if ktimes else None}
     return roof, roof_all, pipeline, stage_ms
+
+
+def uses_moments(eng, P):
+    """whether the engine's odometry keeps the stored rows as per-query moments at batch size P
+    (tuning od_moments_min; the rows kernel's byte model depends on it)"""
+    get = getattr(eng, "get_tuning", None)
+    if get is None:
+        return False
+    return P > get("od_small_max") and P >= get("od_moments_min")
 
 
 def stream_leg(loam, sg, n_sweeps, n_cpu, stages=3, priority="default"):
@@ -338,13 +354,15 @@ DENSE_CFG = dict(n_rings=64, max_points=160000, od_max_iter=100, mp_max_iter=20)
 DENSE_SEED = 5000
 
 
-def dense_batch_leg(loam, sg, B, steps, warmup, profile_steps, cpu_sample, cpu_reps, device=0):
+def dense_batch_leg(loam, sg, B, steps, warmup, profile_steps, cpu_sample, cpu_reps, device=0, tune=None):
     """Config 5 as a batch: B independent HDL-64E problems (seeds DENSE_SEED + i, ~131k points per
     sweep, 64 rings) through the same step as config 4 — enough sweeps in flight to load the chip,
     which one 131k-point problem does not.  Inputs resident in HBM; its own roofline (dominant kernel
     and whole step), CPU oracle sample and parity."""
     prevs, curs = sg.batch_problems(B, base_seed=DENSE_SEED, lidar=sg.HDL64)
     eng = loam.Engine(loam.default_config(ring_model=loam.RING_LINEAR, **DENSE_CFG), device=device)
+    if tune:
+        eng.set_tuning(**tune)
     eng.batch_upload(prevs, curs)
     elapsed = timed(eng, steps, warmup, None, "cpu")
     od, aft, st = eng.batch_download()
@@ -357,6 +375,7 @@ def dense_batch_leg(loam, sg, B, steps, warmup, profile_steps, cpu_sample, cpu_r
         _, _, st_prof = eng.batch_download()
         ktimes = eng.kernel_times()
         eng.set_profiling(False)
+    st["od_moments"] = st_prof["od_moments"] = uses_moments(eng, B)
     eng.close()
     roof, roof_all, pipeline, stage_ms = rooflines(st, st_prof, ktimes, max(profile_steps, 1), ms,
                                                    traffic_file="traffic_config5.json")
@@ -489,7 +508,7 @@ def main(argv=None):
         loam = importlib.import_module("loam_velodyne-1_amd")
         sg = importlib.import_module("loam_velodyne-1_amd.synthgen")
         print(json.dumps(dense_batch_leg(loam, sg, args.dense_batch, args.dense_steps, 2, args.profile_steps,
-                                         args.dense_cpu_sample if args.cpu_sample > 0 else 0, 3)))
+                                         args.dense_cpu_sample if args.cpu_sample > 0 else 0, 3, tune=tune)))
         return
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -589,6 +608,7 @@ def main(argv=None):
     value = world * B * args.steps / elapsed
     psteps = max(args.profile_steps, 1)
 
+    st["od_moments"] = st_prof["od_moments"] = uses_moments(eng, B)
     roof, roof_all, pipeline, stage_ms = rooflines(st, st_prof, ktimes, psteps, ms_per_step)
 
     # CPU baseline: the oracle on a bounded sample, N=1 only
@@ -636,7 +656,7 @@ def main(argv=None):
     if world == 1 and args.dense_batch > 0 and not os.environ.get("LOAM_BENCH_ENGINE"):
         loam = importlib.import_module("loam_velodyne-1_amd")
         dense = dense_batch_leg(loam, sg, args.dense_batch, args.dense_steps, 2, min(args.profile_steps, 2),
-                                args.dense_cpu_sample if args.cpu_sample > 0 else 0, 3, device=local)
+                                args.dense_cpu_sample if args.cpu_sample > 0 else 0, 3, device=local, tune=tune)
     out = {
         "metric": METRIC,
         "value": value,

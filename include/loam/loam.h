@@ -16,8 +16,9 @@
  *                              equivalent: one problem = the bodies above composed)
  *
  * Conventions: no C++ types cross the boundary; all host storage is caller-owned and never
- * retained after a call; a context owns its device memory, one HIP device and one stream; a
- * context is not thread-safe, distinct contexts may run concurrently.  Every function returns
+ * retained after a call; a context owns its device memory, one HIP device and its HIP streams
+ * (the node bodies run on one; a batch step spreads over up to four, loam_batch_sync drains them
+ * all); a context is not thread-safe, distinct contexts may run concurrently.  Every function returns
  * LOAM_OK (0) or a negative LOAM_E_* code; loam_last_error() describes the last failure on the
  * calling thread.  LOAM_E_CAPACITY writes the required size back into the cloud's `count`.
  */
@@ -203,10 +204,14 @@ int loam_set_stream_priority(loam_ctx *ctx, int priority);
 
 /* launch-shape choices of the batch / streaming L-M loops by batch size (no reference equivalent):
  * key = one of od_small_max, od_lm_min, od_lm_max, od_fused_max, mp_small_max, mp_fused_max,
- * nn_lanes, nn_lanes_maxp, od_assoc_wg, nn_lds, od_rows_deep_max, nn_wg, fit_wg, nnfit_max, graph, mp_iter_wide_max, vg_merge, vg_merge_min, sr_ahead, sr_ahead_at, step_pipe, batch_streams, pipe_mp_sets, od_sel_min, od_win_mono, od_win_mono_min (loam_velodyne-1_amd/csrc/engine.hpp, struct Tuning).  Every
- * choice computes the same results; the defaults are the measured fastest.  LOAM_E_INVAL for an
- * unknown key or a value out of range.  Takes effect from the next call. */
+ * nn_lanes, nn_lanes_maxp, od_assoc_wg, nn_lds, od_rows_deep_max, nn_wg, fit_wg, nnfit_max, graph, mp_iter_wide_max, vg_merge, vg_merge_min, sr_ahead, sr_ahead_at, step_pipe, batch_streams, pipe_mp_sets, od_sel_min, od_win_mono, od_win_mono_min, od_moments_min (loam_velodyne-1_amd/csrc/engine.hpp, struct
+ * Tuning).  Every choice computes the same results bit for bit except od_moments_min (the odometry's
+ * stored rows as per-query fp64 moments: within the north star's 1e-4 of the reference);
+ * the defaults are the measured fastest.  LOAM_E_INVAL for an unknown key or a value out of range.
+ * Takes effect from the next call (waits for the context's queued work). */
 int loam_set_tuning(loam_ctx *ctx, const char *key, long long value);
+/* the current value of a launch choice (LOAM_E_INVAL for an unknown key) */
+int loam_get_tuning(loam_ctx *ctx, const char *key, long long *value);
 
 /* last-call statistics of a context (stage device times, counts, algorithmic bytes) */
 int loam_get_stats(loam_ctx *ctx, loam_stats *stats);

@@ -112,6 +112,7 @@ EXPORTS = ("loam_config_default", "loam_create", "loam_destroy", "loam_last_erro
            "loam_maintenance", "loam_chain_sweep",
            "loam_batch_upload", "loam_batch_run", "loam_batch_sync", "loam_batch_download", "loam_get_stats",
            "loam_set_profiling", "loam_get_kernel_times", "loam_set_stream_priority", "loam_set_tuning",
+           "loam_get_tuning",
            # include/loam/loam_bag.h: recorded-sweep ingest (rosbag v2, PointCloud2, Imu)
            "loam_bag_open", "loam_bag_close", "loam_bag_next", "loam_pc2_parse", "loam_pc2_cloud",
            "loam_imu_parse",
@@ -145,6 +146,7 @@ def lib():
         L.loam_set_profiling.argtypes = [PP, ctypes.c_int]
         L.loam_set_stream_priority.argtypes = [PP, ctypes.c_int]
         L.loam_set_tuning.argtypes = [PP, ctypes.c_char_p, ctypes.c_longlong]
+        L.loam_get_tuning.argtypes = [PP, ctypes.c_char_p, P(ctypes.c_longlong)]
         L.loam_get_kernel_times.argtypes = [PP, ctypes.c_char_p, ctypes.c_uint32]
         L.loam_batch_download.argtypes = [PP, P(Pose6), P(Pose6), P(Stats)]
         L.loam_get_stats.argtypes = [PP, P(Stats)]
@@ -266,7 +268,8 @@ class Engine:
         mapping did not run on this sweep, registered None unless requested"""
         ci, keep = _cloud_in(raw)
         out = ChainOut()
-        reg = _Out(max(int(np.asarray(raw).shape[0]), 1)) if registered else None
+        # (the registered cloud has one point per input point: a CloudIn view carries its count)
+        reg = _Out(max(int(ci.count), 1)) if registered else None
         if reg is not None:
             out.registered = reg.c
         rc = lib().loam_chain_sweep(self.h, stamp, ci, ctypes.byref(out))
@@ -321,6 +324,12 @@ class Engine:
         set_tuning(od_lm_max=128); every choice computes the same results"""
         for k, v in kv.items():
             _check(lib().loam_set_tuning(self.h, k.encode(), int(v)))
+
+    def get_tuning(self, key):
+        """the current value of a launch choice (include/loam/loam.h loam_get_tuning)"""
+        v = ctypes.c_longlong(0)
+        _check(lib().loam_get_tuning(self.h, key.encode(), ctypes.byref(v)))
+        return int(v.value)
 
     def set_profiling(self, on):
         _check(lib().loam_set_profiling(self.h, 1 if on else 0))

@@ -148,6 +148,7 @@ struct loam_ctx {
   hipStream_t st2 = nullptr;                 // batch: mapping frame 1 beside the odometry solve
   hipEvent_t fork = nullptr, join = nullptr, fork2 = nullptr, join2 = nullptr;
   Tuning tune;                               // launch choices by batch size (loam_set_tuning)
+  int prio = 0;                              // HIP priority of the context's streams (loam_set_stream_priority)
   // tune.graph: the batch step captured once as a HIP graph (for this P / these buffers) and replayed
   hipGraph_t graph = nullptr;
   hipGraphExec_t graph_exec = nullptr;
@@ -396,18 +397,30 @@ int loam_set_stream_priority(loam_ctx* x, int priority) {
   if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
   if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));
   if (x->st4) HIP_TRY(hipStreamSynchronize(x->st4));
-  hipStream_t st = nullptr, st2 = nullptr;
-  HIP_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio));
-  if (hipStreamCreateWithPriority(&st2, hipStreamNonBlocking, prio) != hipSuccess) {
-    (void)hipStreamDestroy(st);
+  // all of the context's streams at the new priority, created in loam_create's order (st, st2, st3,
+  // st4: streams take the process's hardware queues in creation order); the batch pipeline's two
+  // only when the context keeps them (tuning batch_streams)
+  const bool batch = x->st3 != nullptr || x->st4 != nullptr;
+  hipStream_t ns[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipError_t he = hipSuccess;
+  for (int i = 0; i < (batch ? 4 : 2) && he == hipSuccess; ++i)
+    he = hipStreamCreateWithPriority(&ns[i], hipStreamNonBlocking, prio);
+  if (he != hipSuccess) {
+    for (hipStream_t s : ns)
+      if (s) (void)hipStreamDestroy(s);
     return fail(LOAM_E_HIP, "hipStreamCreateWithPriority failed (context keeps its old streams)");
   }
-  if (x->st2) (void)hipStreamDestroy(x->st2);
-  (void)hipStreamDestroy(x->st);
-  x->st = st;
-  x->st2 = st2;
-  x->pin.streams[0] = st;
-  x->pin.streams[1] = st2;
+  for (hipStream_t s : {x->st, x->st2, x->st3, x->st4})
+    if (s) (void)hipStreamDestroy(s);
+  x->st = ns[0];
+  x->st2 = ns[1];
+  x->st3 = ns[2];
+  x->st4 = ns[3];
+  x->prio = prio;
+  x->reset_ahead();
+  x->drop_graph();  // (captured on the old streams)
+  x->pin.streams[0] = x->st;
+  x->pin.streams[1] = x->st2;
   return LOAM_OK;
 }
 
@@ -415,23 +428,32 @@ int loam_set_tuning(loam_ctx* x, const char* key, long long value) {
   if (!x || !key) return fail(LOAM_E_INVAL, "null argument");
   Tuning t = x->tune;
   if (!t.set(key, value)) return fail(LOAM_E_INVAL, std::string("unknown tuning key or value out of range: ") + key);
+  // (the streams below are created on the context's device, whatever device is current)
+  HIP_TRY(hipSetDevice(x->device));
+  HIP_TRY(hipStreamSynchronize(x->st));
+  if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
+  if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));
+  if (x->st4) HIP_TRY(hipStreamSynchronize(x->st4));
   x->tune = t;
-  if (x->st) (void)hipStreamSynchronize(x->st);
-  if (x->st2) (void)hipStreamSynchronize(x->st2);
-  if (x->st3) (void)hipStreamSynchronize(x->st3);
-  if (x->st4) (void)hipStreamSynchronize(x->st4);
   x->reset_ahead();
   if (!t.batch_streams) {  // (the batch then runs on st / st2 alone)
     if (x->st3) (void)hipStreamDestroy(x->st3);
     if (x->st4) (void)hipStreamDestroy(x->st4);
     x->st3 = x->st4 = nullptr;
   } else {
-    if (!x->st3 && hipStreamCreateWithFlags(&x->st3, hipStreamNonBlocking) != hipSuccess) x->st3 = nullptr;
-    if (!x->st4 && hipStreamCreateWithFlags(&x->st4, hipStreamNonBlocking) != hipSuccess) x->st4 = nullptr;
+    // (at the context's stream priority, as loam_set_stream_priority creates them)
+    if (!x->st3) HIP_TRY(hipStreamCreateWithPriority(&x->st3, hipStreamNonBlocking, x->prio));
+    if (!x->st4) HIP_TRY(hipStreamCreateWithPriority(&x->st4, hipStreamNonBlocking, x->prio));
   }
   x->drop_graph();  // (captured with the old choices)
   x->od1.tune = x->odb.tune = t;
   x->mp1.tune = x->mpb.tune = x->mpb2.tune = t;
+  return LOAM_OK;
+}
+
+int loam_get_tuning(loam_ctx* x, const char* key, long long* value) {
+  if (!x || !key || !value) return fail(LOAM_E_INVAL, "null argument");
+  if (!x->tune.get(key, value)) return fail(LOAM_E_INVAL, std::string("unknown tuning key: ") + key);
   return LOAM_OK;
 }
 
@@ -907,13 +929,11 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
     mp_free(x->mpb);
     mp_free(x->mpb2);
     x->P = 0;  // no batch until every buffer of the new size exists
+    // (the second SR / mapping sets only when a mode that alternates them runs: ensure_second_sets)
     hipError_t he = sr_alloc(x->srb, 2 * (int)n, x->cap, x->R);
-    if (he == hipSuccess) he = sr_alloc(x->srb2, 2 * (int)n, x->cap, x->R);
     if (he == hipSuccess) he = od_alloc(x->odb, (int)n, x->R, x->cap, (int)x->cfg.od_max_iter);
     if (he == hipSuccess)
       he = mp_alloc(x->mpb, (int)n, x->R, x->cap, mp_batch_map_capacity(x->cap), (int)x->cfg.mp_max_iter);
-    if (he == hipSuccess)
-      he = mp_alloc(x->mpb2, (int)n, x->R, x->cap, mp_batch_map_capacity(x->cap), (int)x->cfg.mp_max_iter);
     if (he != hipSuccess) {
       sr_free(x->srb);
       sr_free(x->srb2);
@@ -937,11 +957,36 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
                         hipMemcpyHostToDevice));
     }
   HIP_TRY(hipMemcpy(x->srb.raw_n, counts.data(), counts.size() * sizeof(int), hipMemcpyHostToDevice));
-  // the second set's raw sweeps (tune.sr_ahead)
-  HIP_TRY(hipMemcpy(x->srb2.raw, x->srb.raw, (size_t)2 * n * x->cap * sizeof(float4), hipMemcpyDeviceToDevice));
-  HIP_TRY(hipMemcpy(x->srb2.raw_n, x->srb.raw_n, counts.size() * sizeof(int), hipMemcpyDeviceToDevice));
+  if (x->srb2.S) {  // the second set's raw sweeps (tune.sr_ahead / step_pipe)
+    HIP_TRY(hipMemcpy(x->srb2.raw, x->srb.raw, (size_t)2 * n * x->cap * sizeof(float4), hipMemcpyDeviceToDevice));
+    HIP_TRY(hipMemcpy(x->srb2.raw_n, x->srb.raw_n, counts.size() * sizeof(int), hipMemcpyDeviceToDevice));
+  }
   return LOAM_OK;
 }
+
+namespace {
+// The second scan-registration set and the second mapping set, which only the modes that alternate
+// the sets between steps use (tune.sr_ahead, tune.step_pipe): allocated on the first step that
+// needs them, the uploaded raw sweeps copied from the first set.  The sets of the batch are then
+// kept until an upload of another size.
+int ensure_second_sets(loam_ctx* x) {
+  if (x->srb2.S) return LOAM_OK;
+  const int P = x->P;
+  hipError_t he = sr_alloc(x->srb2, 2 * P, x->cap, x->R);
+  if (he == hipSuccess)
+    he = mp_alloc(x->mpb2, P, x->R, x->cap, mp_batch_map_capacity(x->cap), (int)x->cfg.mp_max_iter);
+  if (he != hipSuccess) {
+    sr_free(x->srb2);
+    mp_free(x->mpb2);
+    return fail(LOAM_E_NOMEM, std::string("second batch set allocation failed: ") + hipGetErrorString(he));
+  }
+  x->mpb2.tune = x->tune;
+  // (the raw sweeps are only read by the kernels, so the first set's may be copied while steps run)
+  HIP_TRY(hipMemcpy(x->srb2.raw, x->srb.raw, (size_t)2 * P * x->cap * sizeof(float4), hipMemcpyDeviceToDevice));
+  HIP_TRY(hipMemcpy(x->srb2.raw_n, x->srb.raw_n, (size_t)2 * P * sizeof(int), hipMemcpyDeviceToDevice));
+  return LOAM_OK;
+}
+}  // namespace
 
 namespace {
 // one batch step's device work on x->st (+ x->st2 for mapping frame 1); timing events only when
@@ -1165,7 +1210,13 @@ int loam_batch_run(loam_ctx* x) {
   if (!x || x->P == 0) return fail(LOAM_E_INVAL, "no batch uploaded");
   HIP_TRY(hipSetDevice(x->device));
   Prof* pf = x->prof.on ? &x->prof : nullptr;
-  if (!pf && !x->tune.graph && x->st2 && x->st3 && x->st4 && x->tune.step_pipe > 0 && x->P >= x->tune.step_pipe) {
+  const bool pipe = !pf && !x->tune.graph && x->st2 && x->st3 && x->st4 && x->tune.step_pipe > 0 && x->P >= x->tune.step_pipe;
+  const bool ahead = !pf && !x->tune.graph && x->st3 && x->tune.sr_ahead > 0 && x->P >= x->tune.sr_ahead;
+  if (pipe || ahead) {
+    const int rc = ensure_second_sets(x);
+    if (rc) return rc;
+  }
+  if (pipe) {
     HIP_TRY(batch_enqueue_pipe(x));
     return LOAM_OK;
   }
@@ -1206,6 +1257,8 @@ int loam_batch_sync(loam_ctx* x) {
   if (x->st4) HIP_TRY(hipStreamSynchronize(x->st4));
   if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
   if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));
+  // launch errors of either mapping set (the step pipeline alternates them), reported by this call
+  for (int i = 0; i < 2; ++i) HIP_TRY(x->mpbuf(i).take_error());
   return LOAM_OK;
 }
 
@@ -1233,6 +1286,9 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
     for (int i = 0; i < P; ++i) std::memcpy(&od_sum[i], &st[(size_t)i * kOdStateFloats + kOdSum], sizeof(loam_pose6));
   loam_stats s;
   std::memset(&s, 0, sizeof(s));
+  // (a launch error recorded on the other mapping set during an earlier pipelined step fails this
+  // call too, not a later unrelated one)
+  HIP_TRY(x->mpbuf(1 - x->mp_last).take_error());
   int rc = mp_batch_download(x->mpbuf(x->mp_last), x->st, aft, &s, g_err);
   if (rc) return rc;
   for (int i = 0; i < 2 * P; ++i) {

@@ -84,8 +84,17 @@ struct Tuning {
                            // first (unseeded) round, bit 1 the seeded ones (round 4, 1024 problems:
                            // k_od_assoc 2.76 -> 2.42 ms/step with both)
   int od_win_mono_min = 2; // ... for P >= this (config 3's chain, P = 1: 0.733 -> 0.743 ms/sweep with them)
-  // key = value (loam_set_tuning); false for an unknown key or a value out of range
-  bool set(const char* key, long long v) {
+  int od_moments_min = 64; // for P >= this (and P > od_small_max), k_od_rows keeps each query's
+                           // stored rows (Q12) as fp64 moments instead of re-evaluating them every
+                           // iteration: O(queries) per iteration, not bit-identical, within 1e-4 of the
+                           // reference on every benched problem (round 5: config 5
+                           // k_od_rows 4.50 -> 2.49 ms/step, 1024 problems 1.37 -> 1.03)
+  // key = value (loam_set_tuning); false for an unknown key or a value out of range.  get: the
+  // current value of a key (loam_get_tuning); false for an unknown key
+  bool get(const char* key, long long* v) {
+    return set(key, 0, v);
+  }
+  bool set(const char* key, long long v, long long* read = nullptr) {
     struct K { const char* n; int* f; long long lo, hi; };
     const K ks[] = {{"od_small_max", &od_small_max, 0, 1 << 20}, {"od_lm_min", &od_lm_min, 1, 1 << 20},
                     {"od_lm_max", &od_lm_max, 0, 1 << 20}, {"od_fused_max", &od_fused_max, 0, 1 << 20},
@@ -99,9 +108,14 @@ struct Tuning {
                     {"sr_ahead", &sr_ahead, 0, 1 << 20}, {"sr_ahead_at", &sr_ahead_at, -1, 2},
                     {"step_pipe", &step_pipe, 0, 1 << 20}, {"batch_streams", &batch_streams, 0, 1},
                     {"pipe_mp_sets", &pipe_mp_sets, 1, 2}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
-                    {"od_win_mono", &od_win_mono, 0, 3}, {"od_win_mono_min", &od_win_mono_min, 1, 1 << 20}};
+                    {"od_win_mono", &od_win_mono, 0, 3}, {"od_win_mono_min", &od_win_mono_min, 1, 1 << 20},
+                    {"od_moments_min", &od_moments_min, 1, 1 << 30}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {
+        if (read) {
+          *read = *k.f;
+          return true;
+        }
         if (v < k.lo || v > k.hi) return false;
         if (k.f == &nn_lanes && v == 3) return false;
         *k.f = (int)v;

@@ -1194,6 +1194,50 @@ LOAM_D void od_row_accum(const OdJf& e, float4 c4, bool okit, double (&acc)[28])
   acc[27] += okit ? 1.0 : 0.0;
 }
 
+// Q12 as per-query moments (tuning od_moments_min; NOT bit-identical to the reference, which rounds each
+// J entry to float: within the north star's 1e-4).  Every stored row of query q has
+// the same raw point (pointOri, :709-712), so at the current transform row r's J is E_q c_r, E_q the
+// 6x3 coefficient-free factors (od_jfactors) and c_r the row's (coeff.x, y, z); B_r = -0.05 d2_r.
+// Hence the rows' JᵀJ = E_q M_q E_qᵀ and Jᵀb = E_q m_q with M_q = Σ_r c_r c_rᵀ, m_q = Σ_r c_r B_r
+// (products of floats, exact in fp64) kept per query across the iterations: O(queries) per
+// iteration instead of O(rows), and a rejected row (zero coefficient) still adds nothing.
+constexpr int kOdMom = 10;  // Mxx Mxy Mxz Myy Myz Mzz | mx my mz | accepted rows
+LOAM_D void od_mom_add(double (&m)[kOdMom], float4 c4) {
+  const float bb = (float)(-0.05 * D(c4.w));
+  m[0] = loamla::dmac(m[0], c4.x, c4.x);
+  m[1] = loamla::dmac(m[1], c4.x, c4.y);
+  m[2] = loamla::dmac(m[2], c4.x, c4.z);
+  m[3] = loamla::dmac(m[3], c4.y, c4.y);
+  m[4] = loamla::dmac(m[4], c4.y, c4.z);
+  m[5] = loamla::dmac(m[5], c4.z, c4.z);
+  m[6] = loamla::dmac(m[6], c4.x, bb);
+  m[7] = loamla::dmac(m[7], c4.y, bb);
+  m[8] = loamla::dmac(m[8], c4.z, bb);
+  m[9] += row_ok(c4) ? 1.0 : 0.0;
+}
+// the query's JᵀJ (21) | Jᵀb (6) | rows (1) from its moments at the current factors e
+LOAM_D void od_mom_accum(const OdJf& e, const double (&m)[kOdMom], double (&acc)[28]) {
+  // E rows in od_row_accum's signs (a[1] has no y term)
+  const double E[6][3] = {{e.e00, e.e01, e.e02}, {e.e10, 0.0, e.e12},   {e.e20, e.e21, e.e22},
+                          {e.e30, e.e31, -e.e32}, {e.e40, -e.e41, -e.e42}, {e.e50, -e.e51, -e.e52}};
+  // (no rounding order to match here: fused multiply-adds throughout)
+  auto dot3 = [](double a0, double a1, double a2, double b0, double b1, double b2) {
+    return __builtin_fma(a0, b0, __builtin_fma(a1, b1, a2 * b2));
+  };
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    // F = E_i M (M symmetric)
+    const double f0 = dot3(E[i][0], E[i][1], E[i][2], m[0], m[1], m[2]);
+    const double f1 = dot3(E[i][0], E[i][1], E[i][2], m[1], m[3], m[4]);
+    const double f2 = dot3(E[i][0], E[i][1], E[i][2], m[2], m[4], m[5]);
+#pragma unroll
+    for (int jj = i; jj < 6; ++jj) { acc[k] = dot3(f0, f1, f2, E[jj][0], E[jj][1], E[jj][2]); ++k; }
+    acc[21 + i] = dot3(E[i][0], E[i][1], E[i][2], m[6], m[7], m[8]);
+  }
+  acc[27] = m[9];
+}
+
 
 // one iteration's rows (lane per query): this iteration's residual + weight stored at [iter][q];
 // then the Jacobian of every row accumulated so far (Q12: rows of iterations 0..iter, all
@@ -1204,7 +1248,9 @@ LOAM_D void od_row_accum(const OdJf& e, float4 c4, bool okit, double (&acc)[28])
 constexpr int kOdRowsWpe = 4;  // <= 128 VGPRs with two rows' loads in flight
 // INF: stored rows whose loads are in flight together per lane step (2 for large batches, where
 // occupancy hides the chain; more for small ones, where the lane's chain of iter + 1 loads is the time)
-template <bool FUSED, int INF>
+// MOM: the stored rows as the query's fp64 moments (od_mom_add / od_mom_accum; tuning od_moments_min)
+// instead of re-evaluating each (INF unused)
+template <bool FUSED, int INF, bool MOM = false>
 __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(INF > 2 ? 2 : kOdRowsWpe))) void k_od_rows(OdBuffers b, FeatView f, int last_buf, int iter) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
@@ -1226,6 +1272,26 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(INF 
   float4* qcf = b.q_cf + (size_t)p * b.max_iter * b.cap_q;
   int8_t* qok = b.q_ok + (size_t)p * b.max_iter * b.cap_q;
   float4 po = make_float4(0, 0, 0, 0);
+  double acc[28];
+#pragma unroll
+  for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+  if constexpr (MOM) {
+    double m[kOdMom];
+    if (q < nq) {
+      po = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
+      float4 cf;
+      int ok;
+      od_row_coeff(b, f, p, q, nc, lp, iter, T, po, cf, ok);
+      double* mq = b.mom + (size_t)p * kOdMom * b.cap_q + q;  // [P][kOdMom][cap_q]
+#pragma unroll
+      for (int k = 0; k < kOdMom; ++k) m[k] = iter == 0 ? 0.0 : mq[(size_t)k * b.cap_q];
+      od_mom_add(m, cf);
+#pragma unroll
+      for (int k = 0; k < kOdMom; ++k) mq[(size_t)k * b.cap_q] = m[k];
+    }
+    __syncthreads();  // trig
+    if (q < nq) od_mom_accum(od_jfactors(trig, T, po), m, acc);
+  } else {
   if (q < nq) {
     po = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
     float4 cf;
@@ -1235,9 +1301,6 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(INF 
     qok[(size_t)iter * b.cap_q + q] = (int8_t)ok;
   }
   __syncthreads();
-  double acc[28];
-#pragma unroll
-  for (int k = 0; k < 28; ++k) acc[k] = 0.0;
   if (q < nq) {
     const OdJf e = od_jfactors(trig, T, po);
     // the stored rows INF iterations at a time (their loads in flight together), summed in order
@@ -1254,6 +1317,7 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(INF 
       for (int u = 0; u < INF; ++u)
         if (it0 + u <= iter) od_row_accum(e, cv4[u], okv[u], acc);
     }
+  }
   }
   // wave sums of the 28 values as a butterfly reduce-scatter (32 shuffles instead of 28 x 6);
   // lanes 2v, 2v+1 end with the sum of value v
@@ -1681,6 +1745,7 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   A(&b.sel, (size_t)P * b.cap_q * sizeof(float4));
   A(&b.q_cf, (size_t)P * max_iter * b.cap_q * sizeof(float4));
   A(&b.q_ok, (size_t)P * max_iter * b.cap_q * sizeof(int8_t));
+  A(&b.mom, (size_t)P * kOdMom * b.cap_q * sizeof(double));
   // per-workgroup partials: [P][gq][28], or [P][gq * max_iter][28] for the small-batch rows kernel
   A(&b.part, (size_t)P * b.gq * max_iter * 28 * sizeof(double));  // (k_od_rows_small: per stored iteration)
   A(&b.done, (size_t)P * sizeof(int));
@@ -1706,7 +1771,7 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
 void od_free(OdBuffers& b) {
   void* ptrs[] = {b.state_set[0], b.state_set[1], b.istate_set[0], b.istate_set[1], b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
-                  b.ind, b.sel, b.q_cf, b.q_ok, b.part, b.done, b.mono, b.rstart, b.fC, b.fS};
+                  b.ind, b.sel, b.q_cf, b.q_ok, b.mom, b.part, b.done, b.mono, b.rstart, b.fC, b.fS};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = OdBuffers();
@@ -1787,12 +1852,15 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
       mark("k_od_rows");
     } else {
       const bool deep = P <= tn.od_rows_deep_max;  // more stored rows' loads in flight per lane
+      const bool mom = P >= tn.od_moments_min;     // the stored rows as per-query moments (not bit-exact)
       if (P <= tn.od_fused_max) {
-        if (deep) hipLaunchKernelGGL((k_od_rows<true, 8>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+        if (mom) hipLaunchKernelGGL((k_od_rows<true, 2, true>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+        else if (deep) hipLaunchKernelGGL((k_od_rows<true, 8>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         else hipLaunchKernelGGL((k_od_rows<true, 2>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         mark("k_od_rows");
       } else {
-        if (deep) hipLaunchKernelGGL((k_od_rows<false, 8>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+        if (mom) hipLaunchKernelGGL((k_od_rows<false, 2, true>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+        else if (deep) hipLaunchKernelGGL((k_od_rows<false, 8>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         else hipLaunchKernelGGL((k_od_rows<false, 2>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         mark("k_od_rows");
         hipLaunchKernelGGL(k_od_step, dim3(P), dim3(64), 0, st, b, it, b.gq);

@@ -105,6 +105,7 @@ struct OdBuffers {
   int* ind = nullptr;         // [P][3][cap_q] association of every query (refreshed every 5th iteration)
   float4* q_cf = nullptr;     // [P][max_iter][cap_q] coefficients (zero when rejected)
   int8_t* q_ok = nullptr;     // [P][max_iter][cap_q] accepted flags
+  double* mom = nullptr;      // [P][10][cap_q] per-query fp64 moments of the stored rows (tuning od_moments)
   double* part = nullptr;     // [P][gq][28] per-workgroup JᵀJ | Jᵀb | rows
   int* done = nullptr;        // [P] workgroups of k_od_rows finished (the last one runs the step)
   int* mono = nullptr;        // [kOdBufs][P][2] Last corner / surf of each buffer ring-monotone (HashJob::mono)

@@ -164,6 +164,30 @@ def test_truncated_bag(rb, loam, tmp_path):
 
 
 @pytest.mark.gpu
+def test_chain_sweep_cloud_in_registered(loam, sg):
+    """loam_chain_sweep fed a loam_cloud_in view (32-B velodyne records, as rosbag.pc2_cloud_in hands
+    them over) with the registered cloud requested: the same poses and registered clouds as the
+    array path (the registered cloud is sized from the view's count)"""
+    sweeps = sg.stream_sweeps(8, 1)
+    cfg = loam.default_config(system_delay=1)
+    a, b = loam.Engine(cfg), loam.Engine(cfg)
+    mapped = 0
+    for k, s in enumerate(sweeps):
+        rec = np.zeros((s.shape[0], 8), np.float32)  # x, y, z, pad, intensity, ring, pad, pad
+        rec[:, :3] = s[:, :3]
+        ci = loam.CloudIn(rec.ctypes.data, rec.shape[0], 32)
+        ra = a.chain_sweep(s, stamp=0.1 * k, registered=True)
+        rb_ = b.chain_sweep(ci, stamp=0.1 * k, registered=True)
+        assert ra[:2] == rb_[:2], k
+        for x, y in zip(ra[2:], rb_[2:]):
+            assert (x is None) == (y is None), k
+            if x is not None:
+                np.testing.assert_array_equal(x, y)
+        mapped += ra[3] is not None
+    assert mapped >= 3
+
+
+@pytest.mark.gpu
 def test_replay_matches_array_path(rb, loam, sg, tmp_path):
     """Config 3 sweeps written to a bag (velodyne layout, bz2 chunks) and replayed: the same poses as
     feeding the arrays to the node path directly (the ingest is lossless)."""

@@ -18,7 +18,8 @@ reference's message conventions on the device.
              src/transformMaintenance.cpp:147-203)
 
 Poses bit-exact (tolerance 0.0, tighter than the north-star 1e-4 m / 1e-4 rad), registered clouds
-by SHA-256 of their float32 bytes."""
+by SHA-256 of their float32 bytes; the config-5 batch (P = 64 >= od_moments_min: the odometry's stored
+rows as per-query moments) within the north star's 1e-4."""
 import importlib
 
 import numpy as np
@@ -132,10 +133,11 @@ def test_config5_batch_parity(loam, oc, sg):
     od, aft, st = e.batch_download()
     assert np.all(np.isfinite(od)) and np.all(np.isfinite(aft)) and st["od_iters"] > 25 * P
     ocfg = oc.default_config(ring_model=1, **kw)
+    # (the batch default keeps the odometry's stored rows as per-query moments: north-star tolerance;
+    # the bit-exact row re-evaluation is checked on all 64 problems in test_gpu_moments.py)
     for i in (0, 21, P - 1):
         od_o, aft_o, _ = oc.problem(prevs[i], curs[i], ocfg)
-        np.testing.assert_array_equal(od[i], od_o)
-        np.testing.assert_array_equal(aft[i], aft_o)
+        assert max(np.abs(od[i] - od_o).max(), np.abs(aft[i] - aft_o).max()) <= 1e-4, i
     e.batch_run()
     od2, aft2, _ = e.batch_download()
     np.testing.assert_array_equal(od, od2)

@@ -205,6 +205,7 @@ def test_pipeline_matches_oracle(loam, oc, sg):
 
 
 _SHARE = {}
+EXACT_ROWS = 1 << 30  # tuning od_moments_min: no batch size keeps the odometry rows as moments
 
 
 def _share_run(loam, sg, **tune):
@@ -213,7 +214,9 @@ def _share_run(loam, sg, **tune):
         _SHARE["inputs"] = sg.batch_problems(P, base_seed=1000 + r * P)
     prevs, curs = _SHARE["inputs"]
     e = loam.Engine()
-    e.set_tuning(**tune)
+    # (the row re-evaluation of the reference, so that every launch choice is compared bit for bit;
+    # the per-query moments' own launch choices: test_gpu_moments.py)
+    e.set_tuning(**{"od_moments_min": EXACT_ROWS, **tune})
     e.batch_upload(prevs, curs)
     # (a graph: its capture, then a replay; a step ahead: both buffer sets, each step consuming the
     # scan registration its predecessor enqueued)
@@ -288,7 +291,7 @@ def test_pipeline_rotation_then_sequential(loam, oc, sg):
     od0, aft0, st0 = _SHARE["default"]
     prevs, curs = _SHARE["inputs"]
     e = loam.Engine()
-    e.set_tuning(step_pipe=1)
+    e.set_tuning(step_pipe=1, od_moments_min=EXACT_ROWS)
     e.batch_upload(prevs, curs)
     for n in (1, 2, 3, 4, 5):
         e.batch_run()
