@@ -447,6 +447,44 @@ def timed(eng, steps, warmup, dist, sync_dev):
     return elapsed
 
 
+def fed_leg(Engine, sg, prevs, curs, steps, warmup, device):
+    """Batches arriving over time: each step's sweeps handed over from host memory with
+    loam_batch_feed (pack into pinned staging + PCIe copy on the pipeline's stream, inside the timed
+    region), alternating two distinct batches of the same size, so no step re-runs the previous
+    step's inputs; and the resident batch with the step pipeline off (step_pipe = sr_ahead = 0:
+    each step's stages in sequence, no work enqueued ahead).  Reported beside the metric, which
+    times the resident batch through the pipeline."""
+    B = len(prevs)
+    prevs2, curs2 = sg.batch_problems(B, base_seed=BASE_SEED + 100000)
+    out = {}
+    eng = Engine(device=device)
+    eng.batch_upload(prevs, curs)
+    fb = [eng.prepare_batch(prevs, curs), eng.prepare_batch(prevs2, curs2)]
+    for k in range(warmup):
+        eng.batch_feed(fb[k % 2])
+        eng.batch_run()
+    eng.sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        eng.batch_feed(fb[k % 2])
+        eng.batch_run()
+    eng.sync()
+    el = time.perf_counter() - t0
+    eng.close()
+    out["fed_from_host"] = {"value": B * steps / el, "ms_per_step": el / steps * 1e3, "problems": B,
+                            "note": "every step's sweeps fed from host memory (loam_batch_feed: pack + "
+                                    "PCIe copy inside the timed region), two distinct batches alternating"}
+    e2 = Engine(device=device)
+    e2.set_tuning(step_pipe=0, sr_ahead=0)
+    e2.batch_upload(prevs, curs)
+    el2 = timed(e2, steps, warmup, None, "cpu")
+    e2.close()
+    out["unpipelined"] = {"value": B * steps / el2, "ms_per_step": el2 / steps * 1e3, "problems": B,
+                          "note": "inputs resident, step_pipe = sr_ahead = 0: no stage of a step "
+                                  "overlaps another step's"}
+    return out
+
+
 def gather_poses(dist, od, aft, world, dev):
     """the one collective of the sharded path: every rank's (odometry, mapping) poses, in global
     problem order (RCCL all-gather on GPUs)"""
@@ -488,6 +526,7 @@ def main(argv=None):
     ap.add_argument("--dense-steps", type=int, default=5)
     ap.add_argument("--dense-cpu-sample", type=int, default=2)
     ap.add_argument("--tune", action="append", default=[], help="key=value launch choice (loam_set_tuning), repeatable")
+    ap.add_argument("--fed-leg", type=int, default=1, help="fed-from-host and unpipelined legs at N = 1 (0: skip)")
     ap.add_argument("--share-only", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--dense-only", type=int, default=0, help="run only the config-5 batched leg (profiling)")
     argv = sys.argv[1:] if argv is None else argv
@@ -576,6 +615,10 @@ def main(argv=None):
 
     eng, B, elapsed, st = main_leg["eng"], main_leg["B"], main_leg["elapsed"], main_leg["st"]
     od, aft = main_leg["od"], main_leg["aft"]
+
+    fed = None
+    if args.fed_leg and world == 1 and not os.environ.get("LOAM_BENCH_ENGINE"):
+        fed = fed_leg(Engine, sg, main_leg["prevs"], main_leg["curs"], args.steps, args.warmup, local)
 
     # host-buffer rate: the same batch handed over from host memory, upload + one step
     a = time.perf_counter()
@@ -677,7 +720,9 @@ def main(argv=None):
                                     "step k's odometry beside step k-1's mapping, step k+1's scan "
                                     "registration + odometry seed enqueued ahead; the K timed steps "
                                     "contain exactly K of each stage (loam_batch_sync waits for all "
-                                    "streams, including the stage enqueued ahead)"),
+                                    "streams, including the stage enqueued ahead); the timed steps re-run "
+                                    "the resident batch — arriving_batches gives fresh batches fed from "
+                                    "the host each step and the pipeline-off rate"),
                    **({"tuning": tune} if tune else {})},
         "roofline": roof,
         "roofline_kernels": roof_all,
@@ -686,6 +731,7 @@ def main(argv=None):
         "parity": parity,
         "strong" if args.split == "weak" else "weak": other,
         "kernel_ms_per_step": stage_ms,
+        "arriving_batches": fed,
         "single_stream": stream,
         "latency": latency,
         "dense_batch": dense,

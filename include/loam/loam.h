@@ -114,6 +114,7 @@ typedef struct {
   uint64_t mp_nn_lds_blocks;    /* query blocks of the LDS-staged 5-NN (tuning nn_lds; profiling pass) */
   uint64_t mp_nn_lds_fit;       /*   of them whose buckets fit the LDS set and point buffer */
   uint64_t mp_nn_lds_staged;    /*   queries searched from LDS */
+  uint64_t od_assoc_settled;    /* association queries settled by their certificate (tuning od_assoc_cert) */
 } loam_stats;
 
 typedef struct loam_ctx loam_ctx;
@@ -188,11 +189,20 @@ int loam_maintenance(const loam_pose6 *odom_sum, const loam_pose6 *bef, const lo
  * with all inputs resident in HBM; download copies the poses back.  run only enqueues: for
  * n >= 64 (tunings step_pipe / sr_ahead) consecutive runs overlap as a software pipeline — a run's
  * odometry beside the previous run's mapping, the next run's scan registration and odometry seed
- * enqueued ahead (they re-run the same uploaded problems) — and sync waits for all of it.  download
- * returns the last run's results. */
+ * enqueued ahead (they re-run the same uploaded problems, unless loam_batch_feed supplies each run's
+ * sweeps) — and sync waits for all of it.  download returns the last run's results. */
 int loam_batch_upload(loam_ctx *ctx, uint32_t n, const loam_cloud_in *prev,
                       const loam_cloud_in *cur);
 int loam_batch_run(loam_ctx *ctx);
+/* the sweeps of the NEXT loam_batch_run: n independent problems of the uploaded batch size (a new
+ * batch arriving over time).  In the step pipeline (n >= tuning step_pipe) the sweeps are copied from
+ * pinned staging into the scan-registration set that step reads, on the pipeline's own stream behind
+ * that set's previous reader, and that step's scan registration + odometry seed are enqueued there
+ * at once, so fresh batches overlap the running steps; a fed context no longer re-runs the resident
+ * sweeps ahead (a run without a feed re-runs that set's last sweeps).  Otherwise (sequential steps)
+ * the same as loam_batch_upload.  The call packs the sweeps on the calling thread and returns once
+ * the copies are enqueued; the caller's buffers are free on return. */
+int loam_batch_feed(loam_ctx *ctx, uint32_t n, const loam_cloud_in *prev, const loam_cloud_in *cur);
 int loam_batch_sync(loam_ctx *ctx);   /* waits for the work enqueued by loam_batch_run */
 int loam_batch_download(loam_ctx *ctx, loam_pose6 *od_sum, loam_pose6 *aft, loam_stats *stats);
 
@@ -204,7 +214,8 @@ int loam_set_stream_priority(loam_ctx *ctx, int priority);
 
 /* launch-shape choices of the batch / streaming L-M loops by batch size (no reference equivalent):
  * key = one of od_small_max, od_lm_min, od_lm_max, od_fused_max, mp_small_max, mp_fused_max,
- * nn_lanes, nn_lanes_maxp, od_assoc_wg, nn_lds, od_rows_deep_max, nn_wg, fit_wg, nnfit_max, graph, mp_iter_wide_max, vg_merge, vg_merge_min, sr_ahead, sr_ahead_at, step_pipe, batch_streams, pipe_mp_sets, od_sel_min, od_win_mono, od_win_mono_min, od_moments_min (loam_velodyne-1_amd/csrc/engine.hpp, struct
+ * nn_lanes, nn_lanes_maxp, od_assoc_wg, nn_lds, od_rows_deep_max, nn_wg, fit_wg, nnfit_max, graph, mp_iter_wide_max, vg_merge, vg_merge_min, sr_ahead, sr_ahead_at, step_pipe, batch_streams, pipe_mp_sets, od_sel_min, od_win_mono, od_win_mono_min, od_moments_min, od_lm_mom_min, od_lm_mom_max,
+ * od_assoc_half_min, od_assoc_cert (loam_velodyne-1_amd/csrc/engine.hpp, struct
  * Tuning).  Every choice computes the same results bit for bit except od_moments_min (the odometry's
  * stored rows as per-query fp64 moments: within the north star's 1e-4 of the reference);
  * the defaults are the measured fastest.  LOAM_E_INVAL for an unknown key or a value out of range.

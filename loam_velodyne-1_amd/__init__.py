@@ -90,7 +90,7 @@ STAT_U64 = ("n_raw", "n_ring", "n_sharp", "n_less_sharp", "n_flat", "n_less_flat
 
 STAT_BRANCH = ("od_degenerate_steps", "od_nan_skips", "mp_degenerate_steps", "mp_grid_shifts")
 STAT_WORK = ("mp_nn_candidates", "mp_nn_cells", "od_assoc_gathered", "od_assoc_boxes",
-             "mp_nn_lds_blocks", "mp_nn_lds_fit", "mp_nn_lds_staged")
+             "mp_nn_lds_blocks", "mp_nn_lds_fit", "mp_nn_lds_staged", "od_assoc_settled")
 
 
 class ChainOut(ctypes.Structure):
@@ -110,7 +110,7 @@ class Stats(ctypes.Structure):
 EXPORTS = ("loam_config_default", "loam_create", "loam_destroy", "loam_last_error", "loam_imu",
            "loam_scan_registration", "loam_odometry", "loam_mapping", "loam_mapping_surround",
            "loam_maintenance", "loam_chain_sweep",
-           "loam_batch_upload", "loam_batch_run", "loam_batch_sync", "loam_batch_download", "loam_get_stats",
+           "loam_batch_upload", "loam_batch_feed", "loam_batch_run", "loam_batch_sync", "loam_batch_download", "loam_get_stats",
            "loam_set_profiling", "loam_get_kernel_times", "loam_set_stream_priority", "loam_set_tuning",
            "loam_get_tuning",
            # include/loam/loam_bag.h: recorded-sweep ingest (rosbag v2, PointCloud2, Imu)
@@ -141,6 +141,7 @@ def lib():
         L.loam_chain_sweep.argtypes = [PP, ctypes.c_double, CloudIn, P(ChainOut)]
         L.loam_maintenance.argtypes = [P(Pose6)] * 4
         L.loam_batch_upload.argtypes = [PP, ctypes.c_uint32, P(CloudIn), P(CloudIn)]
+        L.loam_batch_feed.argtypes = [PP, ctypes.c_uint32, P(CloudIn), P(CloudIn)]
         L.loam_batch_run.argtypes = [PP]
         L.loam_batch_sync.argtypes = [PP]
         L.loam_set_profiling.argtypes = [PP, ctypes.c_int]
@@ -297,7 +298,10 @@ class Engine:
         return out.get() if pub.value else None
 
     # --- config 4
-    def batch_upload(self, prevs, curs):
+    @staticmethod
+    def prepare_batch(prevs, curs):
+        """the loam_cloud_in arrays of a batch (kept with the arrays they view), built once for
+        repeated batch_feed calls"""
         n = len(prevs)
         keep = []
         a = (CloudIn * n)()
@@ -306,8 +310,18 @@ class Engine:
             a[i], k1 = _cloud_in(prevs[i])
             b[i], k2 = _cloud_in(curs[i])
             keep += [k1, k2]
+        return n, a, b, keep
+
+    def batch_upload(self, prevs, curs):
+        n, a, b, _keep = self.prepare_batch(prevs, curs)
         _check(lib().loam_batch_upload(self.h, n, a, b))
         self.n = n
+
+    def batch_feed(self, prevs, curs=None):
+        """the sweeps of the next batch_run (loam_batch_feed): (prevs, curs) lists, or a
+        prepare_batch result as the only argument"""
+        n, a, b, _keep = prevs if curs is None else self.prepare_batch(prevs, curs)
+        _check(lib().loam_batch_feed(self.h, n, a, b))
 
     def batch_run(self):
         _check(lib().loam_batch_run(self.h))

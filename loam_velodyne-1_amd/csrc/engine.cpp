@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/loam/loam.h"
@@ -121,6 +122,24 @@ struct loam_ctx {
   MpBuffers mpb2;         // the second mapping set: the step pipeline's steps alternate (mpbuf)
   MpBuffers& mpbuf(int i) { return i ? mpb2 : mpb; }
   int mp_last = 0;        // the mapping set of the last enqueued step (loam_batch_download)
+  // loam_batch_feed: each pipelined step's sweeps arrive from the host through the SR set the step
+  // reads (copied on st3 behind that set's previous reader, then its scan registration + seed
+  // there); a fed context enqueues nothing ahead at the end of a run (the feed does)
+  bool fed = false;
+  float4* feed_pin[2] = {nullptr, nullptr};  // pinned staging per SR set, [2P][cap]
+  int* feed_n[2] = {nullptr, nullptr};       // pinned sweep sizes per SR set, [2P]
+  hipEvent_t feed_copied[2] = {nullptr, nullptr};
+  bool feed_rec[2] = {false, false};
+  void free_feed() {
+    for (int i = 0; i < 2; ++i) {
+      if (feed_rec[i]) (void)hipEventSynchronize(feed_copied[i]);
+      if (feed_pin[i]) (void)hipHostFree(feed_pin[i]);
+      if (feed_n[i]) (void)hipHostFree(feed_n[i]);
+      feed_pin[i] = nullptr;
+      feed_n[i] = nullptr;
+      feed_rec[i] = false;
+    }
+  }
   void reset_ahead() {    // (after draining st3 / st4)
     sr_ready = false;
     seed_ready = false;
@@ -305,6 +324,8 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_done, hipEventDisableTiming);
   for (auto& e : x->step_done)
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (auto& e : x->feed_copied)
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
   x->pin.streams[0] = x->st;
   x->pin.streams[1] = x->st2;
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->fork, hipEventDisableTiming);
@@ -357,6 +378,9 @@ void loam_destroy(loam_ctx* x) {
   od_free(x->odb);
   mp_free(x->mpb);
   mp_free(x->mpb2);
+  x->free_feed();
+  for (auto& e : x->feed_copied)
+    if (e) (void)hipEventDestroy(e);
   if (x->sr_imu_dev) (void)hipFree(x->sr_imu_dev);
   if (x->meta) (void)hipHostFree(x->meta);
   if (x->xb.h) (void)hipHostFree(x->xb.h);
@@ -920,9 +944,11 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
   if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));
   if (x->st4) HIP_TRY(hipStreamSynchronize(x->st4));
   x->reset_ahead();
+  x->fed = false;
   if ((int)n != x->P) {
     if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
     x->drop_graph();  // (its kernels' arguments name the old buffers)
+    x->free_feed();   // (sized for the old batch)
     sr_free(x->srb);
     sr_free(x->srb2);
     od_free(x->odb);
@@ -965,6 +991,25 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
 }
 
 namespace {
+// sweeps [s0, s1) of a batch (sweep 2i = prev[i], 2i + 1 = cur[i]) packed into dst at stride cap,
+// their sizes into n; several host threads for a large batch (the pack is a memory copy per sweep)
+void pack_batch(const loam_cloud_in* prev, const loam_cloud_in* cur, uint32_t nprob, int cap, float4* dst, int* n) {
+  const size_t S = 2 * (size_t)nprob;
+  auto run = [&](size_t s0, size_t s1) {
+    for (size_t s = s0; s < s1; ++s) {
+      const loam_cloud_in& c = (s & 1) ? cur[s / 2] : prev[s / 2];
+      pack(c, dst + s * (size_t)cap, 0, c.count);
+      n[s] = (int)c.count;
+    }
+  };
+  const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  const size_t nt = S >= 64 ? hw : 1;
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; ++t) th.emplace_back(run, S * t / nt, S * (t + 1) / nt);
+  run(0, S / nt);
+  for (auto& t : th) t.join();
+}
+
 // The second scan-registration set and the second mapping set, which only the modes that alternate
 // the sets between steps use (tune.sr_ahead, tune.step_pipe): allocated on the first step that
 // needs them, the uploaded raw sweeps copied from the first set.  The sets of the batch are then
@@ -1151,7 +1196,10 @@ hipError_t batch_enqueue_pipe(loam_ctx* x) {
   SrBuffers& sb = x->srbuf(idx);
   T(hipEventRecord(x->a_start, x->st));
   T(hipEventRecord(x->ev[0], x->st));
-  if (!x->sr_ready || !x->seed_ready) T(enqueue_ahead(x, idx, ls, nullptr));
+  // (not enqueued ahead: the first pipelined step, or a fed context's step without a feed, which
+  // re-runs the set's resident sweeps; Last[ls]'s last reader as for the trailing call below)
+  if (!x->sr_ready || !x->seed_ready)
+    T(enqueue_ahead(x, idx, ls, x->inputs_read_rec[idx] ? x->inputs_read[idx] : nullptr));
   x->sr_ready = x->seed_ready = false;
   x->od_s_last = ls;
   const FeatView fprev = feat_view(sb, 0, 2), fcur = feat_view(sb, 1, 2);
@@ -1195,8 +1243,9 @@ hipError_t batch_enqueue_pipe(loam_ctx* x) {
   T(hipEventRecord(x->ev[3], ms));
   x->srb_last = idx;
   // the next step's scan registration + seed (st3) into Last[lf], which frame 2 of the previous
-  // step (SR set nx) read last
-  T(enqueue_ahead(x, nx, lf, x->inputs_read_rec[nx] ? x->inputs_read[nx] : nullptr));
+  // step (SR set nx) read last; a fed context's next loam_batch_feed enqueues them instead, after
+  // copying its sweeps into set nx
+  if (!x->fed) T(enqueue_ahead(x, nx, lf, x->inputs_read_rec[nx] ? x->inputs_read[nx] : nullptr));
   x->inputs_read_rec[idx] = true;
   x->od_s = lf;
   x->od_e = ls;
@@ -1245,6 +1294,53 @@ int loam_batch_run(loam_ctx* x) {
   HIP_TRY(hipEventRecord(x->ev[2], x->st));
   HIP_TRY(hipGraphLaunch(x->graph_exec, x->st));
   HIP_TRY(hipEventRecord(x->ev[3], x->st));
+  return LOAM_OK;
+}
+
+int loam_batch_feed(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const loam_cloud_in* cur) {
+  if (!x || !prev || !cur || n == 0) return fail(LOAM_E_INVAL, "bad batch arguments");
+  if (x->P == 0 || (int)n != x->P)
+    return fail(LOAM_E_INVAL, "loam_batch_feed: n must equal the uploaded batch size (loam_batch_upload first)");
+  HIP_TRY(hipSetDevice(x->device));
+  for (uint32_t i = 0; i < n; ++i) {
+    int rc = check_cloud_in(prev[i], x->cap);
+    if (!rc) rc = check_cloud_in(cur[i], x->cap);
+    if (rc) return rc;
+  }
+  const int P = x->P;
+  const bool pipe = !x->prof.on && !x->tune.graph && x->st2 && x->st3 && x->st4 && x->tune.step_pipe > 0 &&
+                    P >= x->tune.step_pipe;
+  if (!pipe) {  // sequential steps: the next step's sweeps replace the resident ones (as an upload)
+    return loam_batch_upload(x, n, prev, cur);
+  }
+  int rc = ensure_second_sets(x);
+  if (rc) return rc;
+  const int i = x->sr_idx;  // the set the next step reads
+  if (x->sr_ready || x->seed_ready) {
+    // (enqueued ahead on the set's resident sweeps by a run before the context was fed: discarded,
+    // the feed's scan registration rewrites the set)
+    HIP_TRY(hipStreamSynchronize(x->st3));
+    x->sr_ready = x->seed_ready = false;
+  }
+  const size_t per = (size_t)2 * P * x->cap;
+  if (!x->feed_pin[i]) {
+    HIP_TRY(hipHostMalloc((void**)&x->feed_pin[i], per * sizeof(float4), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&x->feed_n[i], (size_t)2 * P * sizeof(int), hipHostMallocDefault));
+  }
+  if (x->feed_rec[i]) HIP_TRY(hipEventSynchronize(x->feed_copied[i]));  // (the staging's last copy is out)
+  pack_batch(prev, cur, n, x->cap, x->feed_pin[i], x->feed_n[i]);
+  SrBuffers& sb = x->srbuf(i);
+  // behind the set's last reader (the step that used it: its mapping, after its scan registration)
+  if (x->mp_done_rec[i]) HIP_TRY(hipStreamWaitEvent(x->st3, x->mp_done[i], 0));
+  for (int s = 0; s < 2 * P; ++s)
+    if (x->feed_n[i][s] > 0)
+      HIP_TRY(hipMemcpyAsync(sb.raw + (size_t)s * x->cap, x->feed_pin[i] + (size_t)s * x->cap,
+                             (size_t)x->feed_n[i][s] * sizeof(float4), hipMemcpyHostToDevice, x->st3));
+  HIP_TRY(hipMemcpyAsync(sb.raw_n, x->feed_n[i], (size_t)2 * P * sizeof(int), hipMemcpyHostToDevice, x->st3));
+  HIP_TRY(hipEventRecord(x->feed_copied[i], x->st3));
+  x->feed_rec[i] = true;
+  HIP_TRY(enqueue_ahead(x, i, x->od_s, x->inputs_read_rec[i] ? x->inputs_read[i] : nullptr));
+  x->fed = true;
   return LOAM_OK;
 }
 
@@ -1313,6 +1409,7 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
     s.od_nan_skips += (uint64_t)q[kIsNanSkips];
     s.od_assoc_gathered += (uint64_t)(uint32_t)q[kIsGathered];
     s.od_assoc_boxes += (uint64_t)(uint32_t)q[kIsBoxes];
+    s.od_assoc_settled += (uint64_t)(uint32_t)q[kIsCert];
     const uint64_t nq = q[kIsAssoc] ? (uint64_t)(q[kIsQueries] / q[kIsAssoc]) : 0, it = (uint64_t)q[kIsIters];
     s.od_query_iters += nq * it;
     s.od_row_evals += nq * it * (it + 1) / 2;

@@ -84,6 +84,12 @@ struct Tuning {
                            // first (unseeded) round, bit 1 the seeded ones (round 4, 1024 problems:
                            // k_od_assoc 2.76 -> 2.42 ms/step with both)
   int od_win_mono_min = 2; // ... for P >= this (config 3's chain, P = 1: 0.733 -> 0.743 ms/sweep with them)
+  int od_assoc_half_min = 1 << 30;  // k_od_assoc with two queries per wave (half_hash_nn /
+                           // half_window_mono) for P >= this (with k_od_sel: P >= od_sel_min)
+  int od_assoc_cert = 0;   // association queries of the seeded rounds settled by their last full search's
+                           // certificate when it still separates every choice from its rivals (exact)
+  int od_lm_mom_min = 1;   // with the moments: k_od_lm_mom (an association round's 5 iterations in one
+  int od_lm_mom_max = 0;   //   workgroup per problem) for od_lm_mom_min <= P <= od_lm_mom_max
   int od_moments_min = 64; // for P >= this (and P > od_small_max), k_od_rows keeps each query's
                            // stored rows (Q12) as fp64 moments instead of re-evaluating them every
                            // iteration: O(queries) per iteration, not bit-identical, within 1e-4 of the
@@ -109,7 +115,9 @@ struct Tuning {
                     {"step_pipe", &step_pipe, 0, 1 << 20}, {"batch_streams", &batch_streams, 0, 1},
                     {"pipe_mp_sets", &pipe_mp_sets, 1, 2}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
                     {"od_win_mono", &od_win_mono, 0, 3}, {"od_win_mono_min", &od_win_mono_min, 1, 1 << 20},
-                    {"od_moments_min", &od_moments_min, 1, 1 << 30}};
+                    {"od_moments_min", &od_moments_min, 1, 1 << 30}, {"od_lm_mom_min", &od_lm_mom_min, 1, 1 << 20},
+                    {"od_lm_mom_max", &od_lm_mom_max, 0, 1 << 20},
+                    {"od_assoc_half_min", &od_assoc_half_min, 1, 1 << 30}, {"od_assoc_cert", &od_assoc_cert, 0, 1}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {
         if (read) {

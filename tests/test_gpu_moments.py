@@ -72,6 +72,23 @@ def test_moments_config5_all_64(loam, oc, sg):
     _check(loam, prevs, curs, cfg, _oracle_all(oc, prevs, curs, oc.default_config(ring_model=1, **DENSE)))
 
 
+@pytest.mark.parametrize("P,seed,dense", [(128, 1896, False), (64, 5000, True)], ids=["share128", "config5"])
+def test_moments_round_kernel(loam, oc, sg, P, seed, dense):
+    """k_od_lm_mom (an association round's five iterations in one workgroup per problem, the rows as
+    moments; tuning od_lm_mom_max) at the 8-GPU share and on config 5's 2304-query HDL-64E problems
+    (144 KB of LDS per workgroup): every problem within the north star of the oracle"""
+    kw = dict(lidar=sg.HDL64) if dense else {}
+    prevs, curs = sg.batch_problems(P, base_seed=seed, **kw)
+    cfg = loam.default_config(ring_model=loam.RING_LINEAR, **DENSE) if dense else None
+    ocfg = oc.default_config(ring_model=1, **DENSE) if dense else None
+    od_o, aft_o, iters_o = _oracle_all(oc, prevs, curs, ocfg)
+    od, aft, st = _run(loam, prevs, curs, cfg, od_lm_mom_max=1 << 20)
+    e_od, e_mp = np.abs(od - od_o).max(), np.abs(aft - aft_o).max()
+    print(f"k_od_lm_mom P={P}: max |d odometry| {e_od:.3g}, |d mapping| {e_mp:.3g}, "
+          f"iterations {st['od_iters']} vs {iters_o}")
+    assert e_od <= TOL and e_mp <= TOL
+
+
 def test_moments_8gpu_share_fused(loam, oc, sg):
     """the share (P = 128): the moments in the fused rows kernel (step in the last workgroup) and
     through the step pipeline (three steps), against the oracle"""
