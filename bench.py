@@ -193,10 +193,16 @@ def uses_moments(eng, P):
     return P > get("od_small_max") and P >= get("od_moments_min")
 
 
-def stream_leg(loam, sg, n_sweeps, n_cpu, stages=3, priority="default"):
+def stream_leg(loam, sg, n_sweeps, n_cpu, stages=3, priority="default", tune=None):
     """Config 3 (streaming, seed 1): scan registration -> odometry -> mapping on every published
     frame, one sweep at a time on one GPU context, next to the CPU oracle on the first sweeps."""
     sweeps = sg.stream_sweeps(n_sweeps, 1)
+
+    def Eng(cfg=None):  # (tune: launch choices of the A/B runs)
+        e = loam.Engine(cfg)
+        if tune:
+            e.set_tuning(**tune)
+        return e
 
     def run(impl, sw):
         poses, n, t = [], 0, 0.0
@@ -211,9 +217,9 @@ def stream_leg(loam, sg, n_sweeps, n_cpu, stages=3, priority="default"):
             t += time.perf_counter() - a
         return np.array(poses), n, t
 
-    warm = loam.Engine(loam.default_config(system_delay=1))
+    warm = Eng(loam.default_config(system_delay=1))
     run(warm, sweeps[:6])
-    pg, ng, tg = run(loam.Engine(loam.default_config()), sweeps)
+    pg, ng, tg = run(Eng(loam.default_config()), sweeps)
     out = {"config": f"config3: VLP-16 stream (seed 1), {n_sweeps} sweeps, systemDelay 20, mapping every 2nd frame",
            "sweeps_processed": ng, "scans_per_s": ng / tg, "ms_per_sweep": 1e3 * tg / max(ng, 1),
            "mode": "sequential: one thread calls the three node bodies in turn on one context (per-sweep latency)"}
@@ -232,9 +238,9 @@ def stream_leg(loam, sg, n_sweeps, n_cpu, stages=3, priority="default"):
             t += time.perf_counter() - a
         return np.array(poses), n, t
 
-    warm_c = loam.Engine(loam.default_config(system_delay=1))
+    warm_c = Eng(loam.default_config(system_delay=1))
     run_chain(warm_c, sweeps[:6])
-    pc, nc, tc_ = run_chain(loam.Engine(loam.default_config()), sweeps)
+    pc, nc, tc_ = run_chain(Eng(loam.default_config()), sweeps)
     out["device_chain"] = {"mode": "sequential, intermediate topics left on the device (loam_chain_sweep)",
                            "sweeps_processed": nc, "scans_per_s": nc / tc_, "ms_per_sweep": 1e3 * tc_ / max(nc, 1),
                            "max_abs_err_vs_sequential": float(np.abs(pc - pg).max()) if pc.shape == pg.shape else None}
@@ -242,12 +248,12 @@ def stream_leg(loam, sg, n_sweeps, n_cpu, stages=3, priority="default"):
     # the same sweeps through the node pipeline (loam_velodyne-1_amd/pipeline.py): one context and
     # one thread per node, as the reference's node processes run; outputs must equal the sequential run
     pl_mod = importlib.import_module("loam_velodyne-1_amd.pipeline")
-    warm_pl = pl_mod.NodePipeline(loam.Engine, loam.default_config(system_delay=1), stages=stages)
+    warm_pl = pl_mod.NodePipeline(Eng, loam.default_config(system_delay=1), stages=stages)
     warm_pl.run(sweeps[:6])
     warm_pl.close()
     if priority == "default":
         priority = pl_mod.NodePipeline.DEFAULT_PRIORITY
-    pl = pl_mod.NodePipeline(loam.Engine, loam.default_config(), stages=stages, priority=priority)
+    pl = pl_mod.NodePipeline(Eng, loam.default_config(), stages=stages, priority=priority)
     a = time.perf_counter()
     res, n_pl = pl.run(sweeps)
     t_pl = time.perf_counter() - a
@@ -665,7 +671,7 @@ def main(argv=None):
     if world == 1 and not os.environ.get("LOAM_BENCH_ENGINE"):
         loam = importlib.import_module("loam_velodyne-1_amd")
         if args.stream_sweeps > 0:
-            stream = stream_leg(loam, sg, args.stream_sweeps, args.stream_cpu_sweeps)
+            stream = stream_leg(loam, sg, args.stream_sweeps, args.stream_cpu_sweeps, tune=tune)
         if args.latency_runs > 0:
             def with_cpu(lat, p0, c0, od0, aft0, ocfg=None):
                 """the pinned oracle on the same problem: median of 3 after a warm-up, and the parity"""

@@ -206,6 +206,108 @@ LOAM_D int wave_incl_scan(int v) {
   return v;
 }
 
+// ---- cross-lane without the LDS crossbar (gfx950): DPP row operations fused into the VALU op,
+// and v_permlane16_swap / v_permlane32_swap for the 16- and 32-lane exchanges.  __shfl_xor /
+// __shfl_up compile to ds_bpermute_b32: an address VGPR, an LDS round trip and a wait per step
+// (214 of them in the association kernel).  The _x forms below take an identity `old` for the
+// lanes a DPP read cannot reach; they are meant for call sites where the whole wave (or, for the
+// half forms, the whole 32-lane half) is active.  Only order-free operations (min, max, integer
+// sums / scans) are offered, so results are bit-identical to the shuffle forms.
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E;         // quad_perm [1,0,3,2] / [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141, kDppRor8 = 0x128; // row_half_mirror (8 lanes), row_ror:8 (= xor 8)
+constexpr int kDppShr1 = 0x111, kDppShr2 = 0x112, kDppShr3 = 0x113, kDppShr4 = 0x114, kDppShr8 = 0x118;
+constexpr int kDppBcast15 = 0x142, kDppBcast31 = 0x143;
+template <int CTRL, int ROW = 0xf, int BANK = 0xf>
+LOAM_D uint32_t dpp_u32(uint32_t old, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROW, BANK, false);
+}
+// v and its partner lane l ^ 16 (first) / l ^ 32 (second) in one swap: min / max take both
+LOAM_D uint32_t min_x16(uint32_t v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return r[0] < r[1] ? r[0] : r[1];
+}
+LOAM_D uint32_t min_x32(uint32_t v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return r[0] < r[1] ? r[0] : r[1];
+}
+// the value of lane (l ^ m) for a wave-uniform m in {1, 2, 4, 8, 16, 32} (others: __shfl_xor),
+// bit-identical to __shfl_xor(v, m, 64) with the whole wave active
+LOAM_D uint32_t xor_u32(uint32_t v, int m) {
+  switch (m) {
+    case 1: return dpp_u32<kDppXor1>(v, v);
+    case 2: return dpp_u32<kDppXor2>(v, v);
+    case 4: {  // banks 0 / 2 of each row read lane + 4 (row_shl:4), banks 1 / 3 lane - 4 (row_shr:4)
+      const uint32_t t = dpp_u32<0x104, 0xf, 0x5>(v, v);
+      return dpp_u32<kDppShr4, 0xf, 0xa>(t, v);
+    }
+    case 8: return dpp_u32<kDppRor8>(v, v);
+    case 16: {
+      const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+      return (__lane_id() & 16) ? r[0] : r[1];
+    }
+    case 32: {
+      const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+      return (__lane_id() & 32) ? r[0] : r[1];
+    }
+    default: return (uint32_t)__shfl_xor((int)v, m, 64);
+  }
+}
+LOAM_D double xor_f64(double v, int m) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint64_t r = ((uint64_t)xor_u32((uint32_t)(u >> 32), m) << 32) | xor_u32((uint32_t)u, m);
+  return __builtin_bit_cast(double, r);
+}
+// min over the 32-lane half (HALF) or the wave
+template <bool HALF = false>
+LOAM_D uint32_t wave_min_u32_x(uint32_t v) {
+  v = min(v, dpp_u32<kDppXor1>(~0u, v));
+  v = min(v, dpp_u32<kDppXor2>(~0u, v));
+  v = min(v, dpp_u32<kDppHalfMirror>(~0u, v));
+  v = min(v, dpp_u32<kDppRor8>(~0u, v));
+  v = min_x16(v);
+  if constexpr (!HALF) v = min_x32(v);
+  return v;
+}
+// 64-bit keys: the high words' minimum, then the low words' among the lanes holding it
+template <bool HALF = false>
+LOAM_D uint64_t wave_min_u64_x(uint64_t v) {
+  const uint32_t hi = wave_min_u32_x<HALF>((uint32_t)(v >> 32));
+  const uint32_t lo = wave_min_u32_x<HALF>((uint32_t)(v >> 32) == hi ? (uint32_t)v : ~0u);
+  return ((uint64_t)hi << 32) | lo;
+}
+// float minimum (fminf semantics on non-NaN values: -0 and +0 compare equal either way)
+template <bool HALF = false>
+LOAM_D float wave_min_f_x(float v) {
+  constexpr uint32_t kInf = 0x7f800000u;
+  v = fminf(v, __uint_as_float(dpp_u32<kDppXor1>(kInf, __float_as_uint(v))));
+  v = fminf(v, __uint_as_float(dpp_u32<kDppXor2>(kInf, __float_as_uint(v))));
+  v = fminf(v, __uint_as_float(dpp_u32<kDppHalfMirror>(kInf, __float_as_uint(v))));
+  v = fminf(v, __uint_as_float(dpp_u32<kDppRor8>(kInf, __float_as_uint(v))));
+  {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fminf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  }
+  if constexpr (!HALF) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fminf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  }
+  return v;
+}
+// inclusive prefix sum over the wave (HALF: over each 32-lane half), the row-shift / row-broadcast
+// ladder: lanes beyond a row's start read 0
+template <bool HALF = false>
+LOAM_D int wave_incl_scan_x(int v) {
+  const uint32_t u = (uint32_t)v;
+  uint32_t s = u + dpp_u32<kDppShr1>(0u, u);
+  s += dpp_u32<kDppShr2>(0u, u);
+  s += dpp_u32<kDppShr3>(0u, u);
+  s += dpp_u32<kDppShr4, 0xf, 0xe>(0u, s);   // lanes 4..15 of each row
+  s += dpp_u32<kDppShr8, 0xf, 0xc>(0u, s);   // lanes 8..15
+  s += dpp_u32<kDppBcast15, 0xa, 0xf>(0u, s); // rows 1 and 3: + lane 15 of rows 0 / 2
+  if constexpr (!HALF) s += dpp_u32<kDppBcast31, 0xc, 0xf>(0u, s);  // rows 2, 3: + lane 31
+  return (int)s;
+}
+
 LOAM_D int wave_incl_max(int v) {
   for (int o = 1; o < 64; o <<= 1) {
     int w = __shfl_up(v, o, 64);
@@ -280,10 +382,10 @@ LOAM_D void wave_reduce_scatter_28(double (&a)[28]) {
     for (int k = 0; k < h; ++k) {
       const double send = upper ? v[k] : v[h + k];
       const double keep = upper ? v[h + k] : v[k];
-      v[k] = keep + __shfl_xor(send, 2 * h, 64);
+      v[k] = keep + xor_f64(send, 2 * h);
     }
   }
-  a[0] = v[0] + __shfl_xor(v[0], 1, 64);
+  a[0] = v[0] + xor_f64(v[0], 1);
 }
 
 // ------------------------------------------------------------------ LDS bitonic sort (ascending)
@@ -320,6 +422,8 @@ LOAM_D void block_bitonic_sort(uint64_t* k, int n64) {
 // barrier per stage for the plain LDS network.  k is the LDS scratch of those stages and receives
 // the sorted keys.  The initial placement of a key is irrelevant (a sort is a permutation), so the
 // loads are coalesced.
+// (the register sorts' runtime strides: ds_bpermute; xor_u32's switch per exchange measured slower
+// there, k_sr_select 1.55 -> 2.53 ms/step at batch 1024)
 LOAM_D uint64_t shfl_xor_u64(uint64_t v, int m) {
   const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
   return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;

@@ -2236,7 +2236,7 @@ __global__ __launch_bounds__(NT) void k_mp_insert(MpBuffers b, int* slot_of, int
       int rank = 0;
       while (m) {
         const int leader = __ffsll((unsigned long long)m) - 1;
-        const int il = __shfl(id, leader, 64);
+        const int il = __builtin_amdgcn_readlane(id, leader);
         const uint64_t mm = __ballot(v && id == il);
         const int basecnt = wcnt[w][il];
         if (v && id == il) rank = basecnt + __popcll(mm & lanemask_lt());
@@ -2282,7 +2282,7 @@ __global__ __launch_bounds__(NT) void k_mp_insert(MpBuffers b, int* slot_of, int
       int rank = 0;
       while (m) {
         const int leader = __ffsll((unsigned long long)m) - 1;
-        const int kl = __shfl(key, leader, 64);
+        const int kl = __builtin_amdgcn_readlane(key, leader);
         const uint64_t mm = __ballot(v && key == kl);
         const int basecnt = cnt[kl & 1][kl >> 1];
         if (v && key == kl) rank = basecnt + __popcll(mm & lanemask_lt());

@@ -434,8 +434,8 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
   }
   // (two of the 27 cells may share a bucket: its points are then offered twice, which does not
   // change a minimum)
-  const int incl = wave_incl_scan(cnt);
-  const int total = __shfl(incl, 63, 64);
+  const int incl = wave_incl_scan_x(cnt);
+  const int total = __builtin_amdgcn_readlane(incl, 63);
   if (LOAM_ASSOC_PHASE == 0 || LOAM_ASSOC_PHASE == 1) wpts += total;
   if (lane < 32) { cells[lane] = lane < 27 ? incl - cnt : 0x7fffffff; cells[32 + lane] = b0; }
   __builtin_amdgcn_wave_barrier();
@@ -462,14 +462,14 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
     best = key < best ? key : best;
   }
   const uint64_t lbest = best;
-  best = wave_min_u64(best);
+  best = wave_min_u64_x(best);
   __builtin_amdgcn_wave_barrier();
   if (cert_l) {
     *cert_l = 0.0f;
     if (best != ~0ull && __uint_as_float((uint32_t)(best >> 32)) < 1.0f) {
-      const uint64_t sec = wave_min_u64(lbest == best ? second : lbest);
+      const uint64_t sec = wave_min_u64_x(lbest == best ? second : lbest);
       const float ds = sec == ~0ull ? 3.4e38f : __uint_as_float((uint32_t)(sec >> 32));
-      *cert_l = fminf(fminf(ds, wave_min_f(skip_bd)), 1.0f);
+      *cert_l = fminf(fminf(ds, wave_min_f_x(skip_bd)), 1.0f);
     }
   }
   if (best != ~0ull && __uint_as_float((uint32_t)(best >> 32)) < h * h) {
@@ -489,8 +489,8 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
           mo = fminf(mo, d);
         }
       }
-      wb->same = fminf(wb->same, wave_min_f(ms));
-      wb->other = fminf(wb->other, wave_min_f(mo));
+      wb->same = fminf(wb->same, wave_min_f_x(ms));
+      wb->other = fminf(wb->other, wave_min_f_x(mo));
     }
     return best;
   }
@@ -518,7 +518,7 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
       }
     }
   }
-  return wave_min_u64(best);
+  return wave_min_u64_x(best);
 }
 
 // One direction of a ring-window scan (:486-523 / :598-645) over the cloud L from c (exclusive):
@@ -745,8 +745,8 @@ LOAM_D void wave_window_mono(const float4* L, const float4* fb, const int* rs, i
         }
       }
       if (tighten) {
-        if (want_same) d2 = fminf(d2, wave_min_f(ds));
-        d3 = fminf(d3, wave_min_f(dot));
+        if (want_same) d2 = fminf(d2, wave_min_f_x(ds));
+        d3 = fminf(d3, wave_min_f_x(dot));
       }
     }
   }
@@ -755,16 +755,16 @@ LOAM_D void wave_window_mono(const float4* L, const float4* fb, const int* rs, i
     // the minimum's runner-up over the wave (lanes holding the minimum offer their second key), or
     // the minimum itself when it does not count (>= 25 m²: then every member is a rival of "none")
     auto lower = [&](uint64_t k, uint64_t sk, float fl) {
-      const uint64_t m = wave_min_u64(k);
-      const uint64_t r = m >= kNone ? m : wave_min_u64(k == m ? sk : k);
+      const uint64_t m = wave_min_u64_x(k);
+      const uint64_t r = m >= kNone ? m : wave_min_u64_x(k == m ? sk : k);
       const float dr = r == ~0ull ? 3.4e38f : __uint_as_float((uint32_t)(r >> 32));
-      return fminf(dr, wave_min_f(fl));
+      return fminf(dr, wave_min_f_x(fl));
     };
     cert[0] = want_same ? lower(k2, s2, f2) : 0.0f;
     cert[1] = lower(k3, s3, f3);
   }
-  best2 = want_same ? wave_min_u64(k2) : ~0ull;
-  best3 = wave_min_u64(k3);
+  best2 = want_same ? wave_min_u64_x(k2) : ~0ull;
+  best3 = wave_min_u64_x(k3);
   if (best2 >= kNone) best2 = ~0ull;
   if (best3 >= kNone) best3 = ~0ull;
 }
@@ -794,23 +794,6 @@ LOAM_D int mono_decode(int c, uint64_t k) {
 static_assert(kSub <= 32, "half-wave windows take kSub <= 32 point sub-chunks");
 LOAM_D int half_lane() { return lane_id() & 31; }
 LOAM_D uint32_t half_bits(uint64_t m) { return (uint32_t)(m >> (lane_id() & 32)); }
-LOAM_D uint64_t half_min_u64(uint64_t v) {
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) {
-    const uint64_t w = __shfl_xor(v, o, 64);
-    v = w < v ? w : v;
-  }
-  return v;
-}
-LOAM_D int half_incl_scan(int v) {
-  const int hl = half_lane();
-#pragma unroll
-  for (int o = 1; o < 32; o <<= 1) {
-    const int w = __shfl_up(v, o, 32);
-    if (hl >= o) v += w;
-  }
-  return v;
-}
 
 // wave_hash_nn (1 m cells, no window bounds) over the half's 32 lanes; cells: the half's 64 ints of LDS
 LOAM_D uint64_t half_hash_nn(const int* start, const float4* hp, int T, const float4* cloud, const float4* ch,
@@ -831,7 +814,7 @@ LOAM_D uint64_t half_hash_nn(const int* start, const float4* hp, int T, const fl
       LOAM_CHECK(b0 >= 0 && cnt >= 0 && b0 + cnt <= n, b0, cnt);
     }
   }
-  const int incl = half_incl_scan(cnt);
+  const int incl = wave_incl_scan_x<true>(cnt);
   const int total = __shfl(incl, (lane_id() & 32) + 31, 64);
   if (LOAM_ASSOC_PHASE == 0 || LOAM_ASSOC_PHASE == 1) wpts += total;
   cells[hl] = hl < 27 ? incl - cnt : 0x7fffffff;
@@ -850,7 +833,7 @@ LOAM_D uint64_t half_hash_nn(const int* start, const float4* hp, int T, const fl
     const uint64_t key = ((uint64_t)fkey(d) << 32) | ((tag & 0xffffffu) << 8) | (tag >> 24);
     best = key < best ? key : best;
   }
-  best = half_min_u64(best);
+  best = wave_min_u64_x<true>(best);
   __builtin_amdgcn_wave_barrier();
   if ((best != ~0ull && __uint_as_float((uint32_t)(best >> 32)) < 1.0f) || (LOAM_ASSOC_SKIP & 2)) return best;
   // farther than one cell: the chunks of the whole cloud that may hold a point closer than 5 m
@@ -878,7 +861,7 @@ LOAM_D uint64_t half_hash_nn(const int* start, const float4* hp, int T, const fl
       }
     }
   }
-  return half_min_u64(best);
+  return wave_min_u64_x<true>(best);
 }
 
 // wave_window_mono (no tightening) over the half's 32 lanes: 32 / kSub sub-chunks per step, the
@@ -941,8 +924,8 @@ LOAM_D void half_window_mono(const float4* L, const float4* fb, const int* rs, i
     }
   }
   const uint64_t kNone = (uint64_t)fkey(25.0f) << 32;
-  best2 = want_same ? half_min_u64(k2) : ~0ull;
-  best3 = half_min_u64(k3);
+  best2 = want_same ? wave_min_u64_x<true>(k2) : ~0ull;
+  best3 = wave_min_u64_x<true>(k3);
   if (best2 >= kNone) best2 = ~0ull;
   if (best3 >= kNone) best3 = ~0ull;
 }
@@ -982,7 +965,7 @@ LOAM_D void wave_assoc_corner(const float4* CL, const float4* ch, int fwd_end, u
       best = key < best ? key : best;
     }
   });
-  best = wave_min_u64(best);
+  best = wave_min_u64_x(best);
   if (best != ~0ull) {
     const uint32_t o = (uint32_t)best;
     ind2 = o >= (1u << 30) ? c - 1 - (int)(o - (1u << 30)) : c + 1 + (int)o;
@@ -1017,8 +1000,8 @@ LOAM_D void wave_assoc_surf(const float4* SL, const float4* ch, int fwd_end, uin
     if (r >= scan) best2 = key < best2 ? key : best2;
     else best3 = key < best3 ? key : best3;
   });
-  best2 = wave_min_u64(best2);
-  best3 = wave_min_u64(best3);
+  best2 = wave_min_u64_x(best2);
+  best3 = wave_min_u64_x(best3);
   auto decode = [c](uint64_t k) {
     const uint32_t o = (uint32_t)k;
     return o >= (1u << 30) ? c - 1 - (int)(o - (1u << 30)) : c + 1 + (int)o;

@@ -218,7 +218,7 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_sort(SrBuffers b, SrPara
     uint64_t mval = __ballot(valid);
     while (mval) {
       const int leader = __ffsll((unsigned long long)mval) - 1;
-      const int rl = __shfl(sid, leader, 64);
+      const int rl = __builtin_amdgcn_readlane(sid, leader);
       const uint64_t mm = __ballot(valid && sid == rl);
       if (valid && sid == rl) rank = __popcll(mm & lanemask_lt());
       if (lane == leader) sh_wcnt[w][rl] = __popcll(mm);
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_scatter(SrBuffers b, SrP
     uint64_t mval = __ballot(valid);
     while (mval) {
       const int leader = __ffsll((unsigned long long)mval) - 1;
-      const int rl = __shfl(sid[e], leader, 64);
+      const int rl = __builtin_amdgcn_readlane(sid[e], leader);
       const uint64_t mm = __ballot(valid && sid[e] == rl);
       if (valid && sid[e] == rl) rank[e] = __popcll(mm & lanemask_lt());
       if (lane == leader) sh_wcnt[rl][e * kW + w] = __popcll(mm);
@@ -857,7 +857,7 @@ LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, 
         }
         pk[ind - wlo] |= 1;
       }
-      mark_neighbours(n, __shfl(ind, f, 64), pk, wlo);
+      mark_neighbours(n, __builtin_amdgcn_readlane(ind, f), pk, wlo);
       __threadfence_block();
       __builtin_amdgcn_wave_barrier();
       remaining &= ~((2ull << f) - 1ull);
@@ -884,7 +884,7 @@ LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, 
         }
       }
     }
-    best = wave_min_u64(best);
+    best = wave_min_u64_x(best);
     if (best == ~0ull) break;
     const int ind = lo + (int)(uint32_t)best;
     if (lane == 0) {
@@ -1050,7 +1050,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
             }
             pk[ind - wlo] |= 1;
           }
-          mark_neighbours(n, __shfl(ind, f, 64), pk, wlo);
+          mark_neighbours(n, __builtin_amdgcn_readlane(ind, f), pk, wlo);
           __threadfence_block();
           __builtin_amdgcn_wave_barrier();
           remaining &= ~((2ull << f) - 1ull);
@@ -1079,7 +1079,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
           smallest++;
           if (smallest >= 4) { done = true; break; }
           if (lane == f) pk[ind - wlo] |= 1;
-          mark_neighbours(n, __shfl(ind, f, 64), pk, wlo);
+          mark_neighbours(n, __builtin_amdgcn_readlane(ind, f), pk, wlo);
           __threadfence_block();
           __builtin_amdgcn_wave_barrier();
           remaining &= ~((2ull << f) - 1ull);
@@ -1177,7 +1177,7 @@ LOAM_D int sweep_route(const SrBuffers& b, int s, int R, int n, int cap, int* se
     // predecessor of r in the insertion sort's order (start ascending, ring index on ties)
     int pst = 0, pidx = -1, phi = -100000;  // -100000: the walk's initial prev_hi
     for (int k = 0; k < R; ++k) {
-      const int ks = __shfl(lo, k, 64), kh = __shfl(hi, k, 64);
+      const int ks = __builtin_amdgcn_readlane(lo, k), kh = __builtin_amdgcn_readlane(hi, k);
       const bool before = (ks < lo || (ks == lo && k < r));
       if (((am >> k) & 1) && before && (pidx < 0 || ks > pst || (ks == pst && k > pidx))) {
         pst = ks;
