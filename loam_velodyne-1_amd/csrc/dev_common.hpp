@@ -424,6 +424,8 @@ LOAM_D void block_bitonic_sort(uint64_t* k, int n64) {
 // loads are coalesced.
 // (the register sorts' runtime strides: ds_bpermute; xor_u32's switch per exchange measured slower
 // there, k_sr_select 1.55 -> 2.53 ms/step at batch 1024)
+// (DPP / permlane stages here measured slower than ds_bpermute: k_sr_select 1.54 -> 1.65 ms/step at
+// batch 1024 with a switch per stage in the wave sorts, 2.53 with one per exchange)
 LOAM_D uint64_t shfl_xor_u64(uint64_t v, int m) {
   const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
   return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
