@@ -1672,6 +1672,135 @@ __global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(INF 
   }
 }
 
+// The rows launch of the per-query moments (tuning od_moments_min; k_od_rows<., ., true>'s sums)
+// shaped for latency: a launch is a few dependent global round trips per lane, so the independent
+// loads (the problem's flags, transform and counts, the query's moments and round data) are issued
+// together ahead of the early return, and a query's associated Last points are gathered through ind
+// only in the first iteration of an association round (Q10), which keeps them in b.qa for the
+// round's other four (one round trip instead of two).  Sums in k_od_rows' order: the same bits.
+template <bool FUSED>
+__global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdRowsWpe))) void k_od_rows_mom(OdBuffers b, FeatView f, int last_buf, int iter) {
+  const XcdBlock blk = xcd_block();
+  const int p = blk.y, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int* ist = b.istate + (size_t)p * kOdStateInts;
+  const float* st = b.state + (size_t)p * kOdStateFloats;
+  const int q = blk.x * kOdThreads + tid;
+  const bool inq = q < b.cap_q, first = iter % 5 == 0;
+  // round trip 1: everything that depends on q and p only
+  const int active = ist[kIsActive], stop = ist[kIsStop];
+  const int nc = f.count(p, 0), ns = f.count(p, 2);
+  float T[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) T[k] = st[k];
+  double* mq = b.mom + (size_t)p * kOdMom * b.cap_q + q;  // [P][kOdMom][cap_q]
+  float4* qa = b.qa + ((size_t)p * b.cap_q + q) * 3;     // [P][cap_q][3]
+  double m[kOdMom];
+#pragma unroll
+  for (int k = 0; k < kOdMom; ++k) m[k] = iter > 0 && inq ? mq[(size_t)k * b.cap_q] : 0.0;
+  float4 t1 = make_float4(0, 0, 0, 0), t2 = t1, t3 = t1;
+  int i1 = -1, i2 = -1, i3 = -1;
+  if (inq) {
+    if (first) {
+      const int* ind = b.ind + (size_t)p * 3 * b.cap_q;
+      i1 = ind[q];
+      i2 = ind[b.cap_q + q];
+      i3 = ind[2 * b.cap_q + q];
+    } else {
+      t1 = qa[0];
+      t2 = qa[1];
+      t3 = qa[2];
+    }
+  }
+  if (!active || stop) return;
+  __shared__ double red[kOdWaves][28];
+  __shared__ float trig[6];
+  if (tid < 6) {  // the angles' double sin / cos as floats, one per lane (trig[2k], trig[2k + 1]: sin, cos of T[k])
+    const float ang = T[tid >> 1];
+    trig[tid] = (float)((tid & 1) ? dcos(ang) : dsin(ang));
+  }
+  const int nq = nc + ns;
+  float4 po = make_float4(0, 0, 0, 0);
+  double acc[28];
+#pragma unroll
+  for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+  if (q < nq) {
+    // round trip 2: the raw point (its cloud by nc) and, in a round's first iteration, the points
+    po = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
+    if (first) {  // od_assoc_pts; t1.w: the association holds
+      const size_t lp = (size_t)last_buf * b.P + p;
+      bool has;
+      if (q < nc) {
+        has = i2 >= 0;
+        if (has) {
+          const float4* CL = b.lastC + lp * b.capC;
+          t1 = CL[i1];
+          t2 = CL[i2];
+        }
+      } else {
+        has = i2 >= 0 && i3 >= 0;
+        if (has) {
+          const float4* SL = b.lastS + lp * b.capS;
+          t1 = SL[i1];
+          t2 = SL[i2];
+          t3 = SL[i3];
+        }
+      }
+      t1.w = has ? 1.0f : 0.0f;
+      qa[0] = t1;
+      qa[1] = t2;
+      qa[2] = t3;
+    }
+    float4 cf;
+    int ok;
+    od_coeff_from(iter, T, po, q < nc, t1.w != 0.0f, t1, t2, t3, cf, ok);
+    od_mom_add(m, cf);
+#pragma unroll
+    for (int k = 0; k < kOdMom; ++k) mq[(size_t)k * b.cap_q] = m[k];
+  }
+  __syncthreads();  // trig
+  if (q < nq) od_mom_accum(od_jfactors(trig, T, po), m, acc);
+  wave_reduce_scatter_28(acc);
+  if ((lane & 1) == 0 && (lane >> 1) < 28) red[w][lane >> 1] = acc[0];
+  __syncthreads();
+  if (tid < 28) {
+    double v = red[0][tid];
+    for (int ww = 1; ww < kOdWaves; ++ww) v += red[ww][tid];
+    if (FUSED) store_partial(&b.part[((size_t)p * b.gq + blk.x) * 28 + tid], v);
+    else b.part[((size_t)p * b.gq + blk.x) * 28 + tid] = v;
+  }
+  if constexpr (FUSED) {
+    __shared__ int sh_last;
+    __shared__ double tot[28];
+    __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs], jE[6], jV[36];
+    __shared__ int lm_iws[12];
+    __syncthreads();
+    if (tid == 0) sh_last = arrive_last(&b.done[p], b.gq);
+    __syncthreads();
+    if (!sh_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (tid < 28) {  // k_od_step's fixed order over the workgroups; eight partials in flight per step
+      double v = 0.0;
+      const double* pp = b.part + (size_t)p * b.gq * 28 + tid;
+      for (int g = 0; g < b.gq; g += 8) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          t[u] = g + u < b.gq ? __hip_atomic_load(&pp[(size_t)(g + u) * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (g + u < b.gq) v += t[u];
+      }
+      tot[tid] = v;
+    }
+    __syncthreads();
+    if (tid < 64) {  // the first wave
+      if (tid == 0) b.done[p] = 0;
+      od_step(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
+    }
+  }
+}
+
 // Small batches (streaming, config 2): a workgroup per (256 queries, stored iteration) pair, each
 // lane one row, so the Q12 re-evaluation of every stored row is one load deep instead of a chain
 // of (iter + 1) per lane; the workgroups of the current iteration compute and store the new
@@ -2154,6 +2283,7 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   A(&b.q_ok, (size_t)P * max_iter * b.cap_q * sizeof(int8_t));
   A(&b.mom, (size_t)P * kOdMom * b.cap_q * sizeof(double));
   A(&b.cert, (size_t)P * b.cap_q * 2 * sizeof(float4));
+  A(&b.qa, (size_t)P * b.cap_q * 3 * sizeof(float4));
   // per-workgroup partials: [P][gq][28], or [P][gq * max_iter][28] for the small-batch rows kernel
   A(&b.part, (size_t)P * b.gq * max_iter * 28 * sizeof(double));  // (k_od_rows_small: per stored iteration)
   A(&b.done, (size_t)P * sizeof(int));
@@ -2179,7 +2309,7 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
 void od_free(OdBuffers& b) {
   void* ptrs[] = {b.state_set[0], b.state_set[1], b.istate_set[0], b.istate_set[1], b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
-                  b.ind, b.sel, b.q_cf, b.q_ok, b.mom, b.cert, b.part, b.done, b.mono, b.rstart, b.fC, b.fS};
+                  b.ind, b.sel, b.q_cf, b.q_ok, b.mom, b.cert, b.qa, b.part, b.done, b.mono, b.rstart, b.fC, b.fS};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = OdBuffers();
@@ -2294,12 +2424,12 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
       const bool deep = P <= tn.od_rows_deep_max;  // more stored rows' loads in flight per lane
       const bool mom = P >= tn.od_moments_min;     // the stored rows as per-query moments (not bit-exact)
       if (P <= tn.od_fused_max) {
-        if (mom) hipLaunchKernelGGL((k_od_rows<true, 2, true>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+        if (mom) hipLaunchKernelGGL((k_od_rows_mom<true>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         else if (deep) hipLaunchKernelGGL((k_od_rows<true, 8>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         else hipLaunchKernelGGL((k_od_rows<true, 2>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         mark("k_od_rows");
       } else {
-        if (mom) hipLaunchKernelGGL((k_od_rows<false, 2, true>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
+        if (mom) hipLaunchKernelGGL((k_od_rows_mom<false>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         else if (deep) hipLaunchKernelGGL((k_od_rows<false, 8>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         else hipLaunchKernelGGL((k_od_rows<false, 2>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         mark("k_od_rows");

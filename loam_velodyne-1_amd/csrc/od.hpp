@@ -108,6 +108,7 @@ struct OdBuffers {
   int8_t* q_ok = nullptr;     // [P][max_iter][cap_q] accepted flags
   float4* cert = nullptr;     // [P][cap_q][2] association certificates: the query point of the last full
                               // search and its rivals' distance bounds (k_od_assoc, tuning od_assoc_cert)
+  float4* qa = nullptr;       // [P][cap_q][3] a query's associated Last points for its round (k_od_rows_mom)
   double* mom = nullptr;      // [P][10][cap_q] per-query fp64 moments of the stored rows (tuning od_moments)
   double* part = nullptr;     // [P][gq][28] per-workgroup JᵀJ | Jᵀb | rows
   int* done = nullptr;        // [P] workgroups of k_od_rows finished (the last one runs the step)
