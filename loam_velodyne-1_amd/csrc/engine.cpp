@@ -1328,14 +1328,20 @@ int loam_batch_feed(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const lo
     HIP_TRY(hipHostMalloc((void**)&x->feed_n[i], (size_t)2 * P * sizeof(int), hipHostMallocDefault));
   }
   if (x->feed_rec[i]) HIP_TRY(hipEventSynchronize(x->feed_copied[i]));  // (the staging's last copy is out)
-  pack_batch(prev, cur, n, x->cap, x->feed_pin[i], x->feed_n[i]);
   SrBuffers& sb = x->srbuf(i);
   // behind the set's last reader (the step that used it: its mapping, after its scan registration)
   if (x->mp_done_rec[i]) HIP_TRY(hipStreamWaitEvent(x->st3, x->mp_done[i], 0));
-  for (int s = 0; s < 2 * P; ++s)
-    if (x->feed_n[i][s] > 0)
-      HIP_TRY(hipMemcpyAsync(sb.raw + (size_t)s * x->cap, x->feed_pin[i] + (size_t)s * x->cap,
-                             (size_t)x->feed_n[i][s] * sizeof(float4), hipMemcpyHostToDevice, x->st3));
+  // packed in chunks of problems, each chunk's copies enqueued before the next is packed, so the
+  // host packing overlaps the DMA of the chunk before
+  constexpr uint32_t kFeedChunk = 64;
+  for (uint32_t c0 = 0; c0 < n; c0 += kFeedChunk) {
+    const uint32_t nc = std::min(kFeedChunk, n - c0);
+    pack_batch(prev + c0, cur + c0, nc, x->cap, x->feed_pin[i] + (size_t)2 * c0 * x->cap, x->feed_n[i] + 2 * c0);
+    for (uint32_t s = 2 * c0; s < 2 * (c0 + nc); ++s)
+      if (x->feed_n[i][s] > 0)
+        HIP_TRY(hipMemcpyAsync(sb.raw + (size_t)s * x->cap, x->feed_pin[i] + (size_t)s * x->cap,
+                               (size_t)x->feed_n[i][s] * sizeof(float4), hipMemcpyHostToDevice, x->st3));
+  }
   HIP_TRY(hipMemcpyAsync(sb.raw_n, x->feed_n[i], (size_t)2 * P * sizeof(int), hipMemcpyHostToDevice, x->st3));
   HIP_TRY(hipEventRecord(x->feed_copied[i], x->st3));
   x->feed_rec[i] = true;

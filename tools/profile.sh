@@ -7,10 +7,10 @@
 #   kt128/          kernel trace of the 8-GPU share (128 problems; tools/trace_timeline.py)
 #   dkt/, dfetch/, dwrite/  the same for the config-5 batched leg alone (--dense-only)
 R=$GRAFT_REPO_ROOT
-TAG=${1:-r04}
+TAG=${1:-r05}
 O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
-Q="--cpu-sample 0 --latency-runs 0 --strong-leg 0 --stream-sweeps 0 --dense-batch 0"
+Q="--cpu-sample 0 --latency-runs 0 --strong-leg 0 --stream-sweeps 0 --dense-batch 0 --fed-leg 0"
 D="--dense-only 1 --dense-batch 64 --cpu-sample 0"
 cd $R && timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err && \
 export TMPDIR=/tmp && cd /tmp && \
