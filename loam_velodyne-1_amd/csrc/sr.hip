@@ -808,17 +808,48 @@ LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, 
 #pragma unroll
     for (int k = 0; k < SR; ++k) cr[k] = crin[k];
   }
+  if constexpr (SR > 0) {
+    // The sharp walk (:476-522) takes the points with curvature > 0.1 from the top of the stable
+    // ascending sort: by (curvature, position) descending, skipping a marked point, until the 21st
+    // pick.  Marks only grow, so its next pick is always the largest (curvature bits, position) key
+    // among the unmarked candidates: repeated wave arg-max over the segment's register-held
+    // curvatures, no sort (the flat pass below is the same walk from the bottom).
+    pre();
+    int largest = 0;
+    for (;;) {
+      uint64_t nkey = ~0ull;  // complemented keys: the minimum is the largest key
+#pragma unroll
+      for (int k = 0; k < SR; ++k) {
+        const int t = sp + k * 64 + lane;
+        if (t <= ep && D(cr[k]) > 0.1 && (pk[lo + t - wlo] & 1) == 0) {
+          const uint64_t key = ~(((uint64_t)fkey(cr[k]) << 32) | (uint32_t)t);
+          nkey = key < nkey ? key : nkey;
+        }
+      }
+      nkey = wave_min_u64_x(nkey);
+      if (nkey == ~0ull) break;
+      largest++;
+      if (largest > 20) break;
+      const int ind = lo + (int)(uint32_t)~nkey;
+      if (lane == 0) {
+        if (largest <= 2) {
+          lab[ind - wlo] = 2;
+          picks[nsharp++] = ind;
+          picks[kSharpPerRing + nlsharp++] = ind;
+        } else {
+          lab[ind - wlo] = 1;
+          picks[kSharpPerRing + nlsharp++] = ind;
+        }
+        pk[ind - wlo] |= 1;
+      }
+      mark_neighbours(n, ind, pk, wlo);
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
   // points with curvature > 0.1, as (curvature bits, position): ascending = the stable sort's order
   int m = 0;
   if constexpr (SR > 0) {
-#pragma unroll
-    for (int k = 0; k < SR; ++k) {
-      const int t = sp + k * 64 + lane;
-      const bool e = t <= ep && D(cr[k]) > 0.1;
-      const uint64_t bm = __ballot(e);
-      if (e) list[m + __popcll(bm & lanemask_lt())] = ((uint64_t)fkey(cr[k]) << 32) | (uint32_t)t;
-      m += __popcll(bm);
-    }
   } else {
     for (int base = sp; base <= ep; base += 64) {
       const int t = base + lane;
@@ -828,13 +859,13 @@ LOAM_D void select_segment_fast(int n, int lo, int sp, int ep, const float* cv, 
       m += __popcll(bm);
     }
   }
-  pre();
+  if constexpr (SR == 0) pre();
   __threadfence_block();
   __builtin_amdgcn_wave_barrier();
-  if (m > 1) wave_sort_u64(list, m);
+  if (SR == 0 && m > 1) wave_sort_u64(list, m);
   int largest = 0;
   bool done = false;
-  for (int base = m - 1; base >= 0 && !done; base -= 64) {  // from the largest curvature down
+  for (int base = m - 1; SR == 0 && base >= 0 && !done; base -= 64) {  // from the largest curvature down
     const int k = base - lane;
     const bool elig = k >= 0;
     const int ind = elig ? lo + (int)(uint32_t)list[k] : 0;
