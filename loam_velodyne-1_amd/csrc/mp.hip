@@ -1435,6 +1435,16 @@ LOAM_D void mp_step(const MpBuffers& b, int p, const double* tot, MpStepScratch&
   float* st = b.state + (size_t)p * kMpStateFloats;
   const int iter = ist[kMiIters];
   const int nrows = (int)tot[27];
+  // lane 0's global reads of the step, issued together up front (round trips on the serial chain)
+  int c_rows = 0, degen = 0, c_deg = 0;
+  float T[6] = {0, 0, 0, 0, 0, 0};
+  if (lane == 0) {
+    c_rows = ist[kMiRows];
+    degen = ist[kMiDegen];
+    c_deg = ist[kMiDegSteps];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) T[q] = st[kMpTobe + q];
+  }
   if (nrows >= 50 && lane == 0) {
     int k = 0;
     for (int i = 0; i < 6; ++i)
@@ -1456,19 +1466,22 @@ LOAM_D void mp_step(const MpBuffers& b, int p, const double* tot, MpStepScratch&
   }
   if (lane != 0) return;
   ist[kMiIters] = iter + 1;
-  ist[kMiRows] += nrows;
+  ist[kMiRows] = c_rows + nrows;
   if (nrows >= 50) {
-    int degen = ist[kMiDegen];
     loamla::lm_step(sh.AtA, sh.AtB, iter, 100.0f, &degen, st + kMpMatP, sh.X, sh.lm_ws, sh.lm_iws,
                     eig ? sh.jE : nullptr, eig ? sh.jV : nullptr, cert);
     ist[kMiDegen] = degen;
-    if (degen) ist[kMiDegSteps] += 1;
-    for (int q = 0; q < 6; ++q) st[kMpTobe + q] += sh.X[q];
-    rot_store(b, p, st + kMpTobe);
+    if (degen) ist[kMiDegSteps] = c_deg + 1;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      T[q] = T[q] + sh.X[q];
+      st[kMpTobe + q] = T[q];
+    }
+    rot_store(b, p, T);
     const float dR = loamla::delta_r(sh.X), dT = loamla::delta_t(sh.X);
     if (D(dR) < 0.05 && D(dT) < 0.05) ist[kMiStop] = 1;
   }
-  if (ist[kMiIters] >= b.max_iter) ist[kMiStop] = 1;
+  if (iter + 1 >= b.max_iter) ist[kMiStop] = 1;
 }
 }  // namespace
 

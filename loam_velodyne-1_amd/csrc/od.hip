@@ -1328,10 +1328,21 @@ LOAM_D void od_step(const OdBuffers& b, int p, int iter, const double* tot, floa
   int* ist = b.istate + (size_t)p * kOdStateInts;
   float* st = b.state + (size_t)p * kOdStateFloats;
   const int nrows = (int)tot[27];
+  // lane 0's global reads of the step, issued together up front (each is a round trip on the
+  // problem's serial chain): the counters it updates and the transform
+  int c_rows = 0, degen = 0, c_deg = 0, c_nan = 0;
+  float T[6] = {0, 0, 0, 0, 0, 0};
   if (lane == 0) {
+    const int c_assoc = ist[kIsAssoc];
+    c_rows = ist[kIsRows];
+    degen = ist[kIsDegenerate];
+    c_deg = ist[kIsDegSteps];
+    c_nan = ist[kIsNanSkips];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) T[q] = st[q];
     ist[kIsIters] = iter + 1;
-    if (iter % 5 == 0) ist[kIsAssoc] += 1;
-    ist[kIsRows] += nrows;
+    if (iter % 5 == 0) ist[kIsAssoc] = c_assoc + 1;
+    ist[kIsRows] = c_rows + nrows;
     if (nrows >= 10) {  // :697-700
       int k = 0;
       for (int i = 0; i < 6; ++i)
@@ -1354,16 +1365,15 @@ LOAM_D void od_step(const OdBuffers& b, int p, int iter, const double* tot, floa
     if (eig) loamla::jacobi6_wave(AtA, jE, jV);
   }
   if (lane != 0) return;
-  int degen = ist[kIsDegenerate];
   loamla::lm_step(AtA, AtB, iter, 10.0f, &degen, st + kOdMatP, X, lm_ws, lm_iws, eig ? jE : nullptr, eig ? jV : nullptr,
                   cert);
   ist[kIsDegenerate] = degen;
-  if (degen) ist[kIsDegSteps] += 1;
+  if (degen) ist[kIsDegSteps] = c_deg + 1;
   const bool nan = isnan(X[0]) || isnan(X[1]) || isnan(X[2]) || isnan(X[3]) || isnan(X[4]) || isnan(X[5]);
   if (!nan)  // Q16
-    for (int q = 0; q < 6; ++q) st[q] += X[q];
+    for (int q = 0; q < 6; ++q) st[q] = T[q] + X[q];
   else
-    ist[kIsNanSkips] += 1;
+    ist[kIsNanSkips] = c_nan + 1;
   const float dR = loamla::delta_r(X), dT = loamla::delta_t(X);
   if (D(dR) < 0.1 && D(dT) < 0.1) ist[kIsStop] = 1;
 }
