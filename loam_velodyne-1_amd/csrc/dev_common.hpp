@@ -1295,21 +1295,130 @@ constexpr int kLmWs = 36 * 6 + 6 + 14 + 6;
 // pre_E / pre_V (optional): jacobi<6>(AtA) already computed (jacobi6_wave, by the caller's wave).
 // certified: nondegenerate_certified(AtA, eig_thresh) held, so iteration 0 sets isDegenerate = 0
 // without the eigen-analysis (matP is left as it was: it is read only when isDegenerate is set)
+LOAM_HD void lm_step_tail(const float* AtA_in, int iter, float eig_thresh, int* isDegenerate, float* matP, float* X,
+                          float* ws, int* iws, const float* pre_E, const float* pre_V, bool certified);
 LOAM_HD void lm_step(const float* AtA_in, const float* AtB_in, int iter, float eig_thresh,
                      int* isDegenerate, float* matP, float* X, float* ws, int* iws,
                      const float* pre_E = nullptr, const float* pre_V = nullptr, bool certified = false) {
   // the QR solve of every iteration works in registers (fully unrolled, constant indices); the
   // iteration-0 analysis (pivoted Jacobi / LU, data-dependent indices) in ws
   float A[36], b[6], qws[14];
+  for (int i = 0; i < 36; ++i) A[i] = AtA_in[i];
+  for (int i = 0; i < 6; ++i) b[i] = AtB_in[i];
+  qr_solve(A, b, 6, 6, X, qws);
+  lm_step_tail(AtA_in, iter, eig_thresh, isDegenerate, matP, X, ws, iws, pre_E, pre_V, certified);
+}
+
+// qr_solve(A, b, 6, 6, x) by one whole wave (all 64 lanes active), bit-identical to the one-lane
+// solve: lane c < 6 holds column c of A in registers, lane 6 holds b.  Per Householder step l the
+// column's norm and reflector stay one serial chain (uniform values, as in the one-lane code), but
+// the divisions v[i] / nrm and v[i] / v[0] run one per lane, and every column's dot product and
+// update (lanes l..5) run at once; b's step l (the one-lane code's second loop, which reads only
+// column l's stored reflector and h[l], final after step l) runs on lane 6 beside them.  The back
+// substitution is the serial chain on broadcast values.  The one-lane solve was ~1 200 dependent
+// instructions (~3 us per L-M step on the streaming path); A (row-major 36) and b are read from
+// memory, x is returned to every lane.
+LOAM_D bool qr_solve6_wave(const float* A_in, const float* b_in, float (&x)[6]) {
+  const int lane = __lane_id();
+  const float eps = 1.1920928955078125e-07f * 10;
+  const bool isb = lane == 6;
+  float col[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) col[i] = lane < 6 ? A_in[i * 6 + (lane < 6 ? lane : 0)] : (isb ? b_in[i] : 0.0f);
+#pragma unroll
+  for (int l = 0; l < 6; ++l) {
+    const int len = 6 - l;
+    float s[6];
+#pragma unroll
+    for (int i = 0; i < len; ++i) s[i] = wl_read(col[l + i], l);
+    float nrm = 0.0f;
+#pragma unroll
+    for (int i = 0; i < len; ++i) nrm += s[i] * s[i];
+    const float v0 = s[0];
+    s[0] = s[0] + sgn1(s[0]) * sqrtf(nrm);
+    nrm = sqrtf(nrm + s[0] * s[0] - v0 * v0);
+    float mine = s[0];
+#pragma unroll
+    for (int i = 1; i < len; ++i)
+      if (lane == i) mine = s[i];
+    const float myv = mine / nrm;  // lane i: v[i] /= nrm
+    float v[6], vp[6];
+#pragma unroll
+    for (int i = 0; i < len; ++i) v[i] = wl_read(myv, i);
+    const float mys = myv / v[0];  // lane i >= 1: the stored A[(l + i) n + l] = v[i] / v[0]
+    vp[0] = 1.0f;
+#pragma unroll
+    for (int i = 1; i < len; ++i) vp[i] = wl_read(mys, i);
+    const float h = v[0] * v[0];
+    // columns j >= l: dot = sum v[i] A[l + i][j], A -= 2 v[i] dot; b (lane 6, with the stored
+    // reflector vp and h[l]): b -= 2 vp[i] dot h
+    float dot = 0.0f;
+#pragma unroll
+    for (int i = 0; i < len; ++i) dot += (isb ? vp[i] : v[i]) * col[l + i];
+    if ((lane >= l && lane < 6) || isb) {
+#pragma unroll
+      for (int i = 0; i < len; ++i) {
+        float u = 2 * (isb ? vp[i] : v[i]) * dot;
+        if (isb) u = u * h;
+        col[l + i] -= u;
+      }
+    }
+    if (lane == l) {
+#pragma unroll
+      for (int i = 1; i < len; ++i) col[l + i] = vp[i];
+    }
+  }
+  float R[6][6], bb[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    bb[i] = wl_read(col[i], 6);
+#pragma unroll
+    for (int j = i; j < 6; ++j) R[i][j] = wl_read(col[i], j);
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+#pragma unroll
+    for (int j = 5; j > i; --j) bb[i] -= bb[j] * R[i][j];
+    if (fabsf(R[i][i]) < eps) {
+#pragma unroll
+      for (int q = 0; q < 6; ++q) x[q] = 0.0f;
+      return false;
+    }
+    bb[i] /= R[i][i];
+  }
+#pragma unroll
+  for (int q = 0; q < 6; ++q) x[q] = bb[q];
+  return true;
+}
+
+// lm_step by one whole wave: the QR solve wave-parallel (qr_solve6_wave), the rest on lane 0 (the
+// other lanes return; the caller's lane 0 continues with X)
+LOAM_D void lm_step_wave(const float* AtA_in, const float* AtB_in, int iter, float eig_thresh, int* isDegenerate,
+                         float* matP, float* X, float* ws, int* iws, const float* pre_E = nullptr,
+                         const float* pre_V = nullptr, bool certified = false) {
+#ifdef LOAM_QR_ONE_LANE  // (experiment builds: the one-lane solve, for A/B)
+  if (__lane_id() != 0) return;
+  lm_step(AtA_in, AtB_in, iter, eig_thresh, isDegenerate, matP, X, ws, iws, pre_E, pre_V, certified);
+  return;
+#endif
+  float x[6];
+  qr_solve6_wave(AtA_in, AtB_in, x);
+  if (__lane_id() != 0) return;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) X[q] = x[q];
+  lm_step_tail(AtA_in, iter, eig_thresh, isDegenerate, matP, X, ws, iws, pre_E, pre_V, certified);
+}
+
+// lm_step after the QR solve (X holds the solution): the iteration-0 degeneracy analysis and the
+// projection of a degenerate step
+LOAM_HD void lm_step_tail(const float* AtA_in, int iter, float eig_thresh, int* isDegenerate, float* matP, float* X,
+                          float* ws, int* iws, const float* pre_E, const float* pre_V, bool certified) {
   float* A2 = ws + 42;      // 36
   float* V = ws + 78;       // 36
   float* V2 = ws + 114;     // 36
   float* Vi = ws + 150;     // 36
   float* E = ws + 186;      // 6
   float* tmp = ws + 192;    // 36 (LU rhs) / 14 (QR) / 6 (X2)
-  for (int i = 0; i < 36; ++i) A[i] = AtA_in[i];
-  for (int i = 0; i < 6; ++i) b[i] = AtB_in[i];
-  qr_solve(A, b, 6, 6, X, qws);
   if (iter == 0 && certified) {
     *isDegenerate = 0;
   } else if (iter == 0) {

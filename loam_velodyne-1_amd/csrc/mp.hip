@@ -1455,21 +1455,25 @@ LOAM_D void mp_step(const MpBuffers& b, int p, const double* tot, MpStepScratch&
       }
     for (int i = 0; i < 6; ++i) sh.AtB[i] = (float)tot[21 + i];
   }
-  bool eig = nrows >= 50 && iter == 0, cert = false;
-  if (eig) {
+  const bool solve = nrows >= 50;  // (uniform)
+  bool eig = solve && iter == 0, cert = false;
+  if (solve) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_wave_barrier();  // lane 0's AtA / AtB, for the wave
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    cert = loamla::nondegenerate_certified(sh.AtA, 100.0f);  // every lane, the same answer
-    eig = !cert;
-    if (eig) loamla::jacobi6_wave(sh.AtA, sh.jE, sh.jV);
+    if (eig) {
+      cert = loamla::nondegenerate_certified(sh.AtA, 100.0f);  // every lane, the same answer
+      eig = !cert;
+      if (eig) loamla::jacobi6_wave(sh.AtA, sh.jE, sh.jV);
+    }
+    // the QR solve by the whole wave; lane 0 goes on with X
+    loamla::lm_step_wave(sh.AtA, sh.AtB, iter, 100.0f, &degen, st + kMpMatP, sh.X, sh.lm_ws, sh.lm_iws,
+                         eig ? sh.jE : nullptr, eig ? sh.jV : nullptr, cert);
   }
   if (lane != 0) return;
   ist[kMiIters] = iter + 1;
   ist[kMiRows] = c_rows + nrows;
-  if (nrows >= 50) {
-    loamla::lm_step(sh.AtA, sh.AtB, iter, 100.0f, &degen, st + kMpMatP, sh.X, sh.lm_ws, sh.lm_iws,
-                    eig ? sh.jE : nullptr, eig ? sh.jV : nullptr, cert);
+  if (solve) {
     ist[kMiDegen] = degen;
     if (degen) ist[kMiDegSteps] = c_deg + 1;
 #pragma unroll

@@ -1355,18 +1355,19 @@ LOAM_D void od_step(const OdBuffers& b, int p, int iter, const double* tot, floa
     }
   }
   if (nrows < 10) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();  // lane 0's AtA / AtB, for the wave
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   bool eig = iter == 0, cert = false;
   if (eig) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     cert = loamla::nondegenerate_certified(AtA, 10.0f);  // every lane, the same answer
     eig = !cert;
     if (eig) loamla::jacobi6_wave(AtA, jE, jV);
   }
+  // the QR solve by the whole wave; lane 0 goes on with X
+  loamla::lm_step_wave(AtA, AtB, iter, 10.0f, &degen, st + kOdMatP, X, lm_ws, lm_iws, eig ? jE : nullptr,
+                       eig ? jV : nullptr, cert);
   if (lane != 0) return;
-  loamla::lm_step(AtA, AtB, iter, 10.0f, &degen, st + kOdMatP, X, lm_ws, lm_iws, eig ? jE : nullptr, eig ? jV : nullptr,
-                  cert);
   ist[kIsDegenerate] = degen;
   if (degen) ist[kIsDegSteps] = c_deg + 1;
   const bool nan = isnan(X[0]) || isnan(X[1]) || isnan(X[2]) || isnan(X[3]) || isnan(X[4]) || isnan(X[5]);

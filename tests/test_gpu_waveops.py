@@ -16,3 +16,14 @@ def test_cross_lane_primitives():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_wave_qr_solve_bitexact():
+    """loamla::qr_solve6_wave (the L-M step's 6x6 QR solve by a whole wave) equals the one-lane
+    qr_solve bit for bit on 32768 systems (normal equations at several scales, rank-deficient,
+    general, NaN / inf entries; a NaN matches a NaN)."""
+    exe = os.path.join(ROOT, "tools", "mb", "qr_wave_check")
+    assert os.path.exists(exe), "build first (make -C loam_velodyne-1_amd)"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
