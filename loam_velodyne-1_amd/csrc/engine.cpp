@@ -22,6 +22,51 @@
 #include "od.hpp"
 #include "pose_math.hpp"
 
+#ifdef LOAM_PIPE_TRACE
+// Diagnostic builds only (tools/build_variant.sh NAME -DLOAM_PIPE_TRACE): device timestamps of the
+// step pipeline's stages (events recorded on the stage's stream), printed by loam_batch_sync as
+// "step stage start_us end_us" relative to the first event, to see which hand-off paces the steps.
+namespace {
+struct PipeTrace {
+  struct Mark { int step; const char* stage; hipEvent_t a, b; };
+  std::vector<Mark> marks;
+  int step = 0;
+  void begin(const char* stage, hipStream_t st) {
+    Mark m{step, stage, nullptr, nullptr};
+    (void)hipEventCreate(&m.a);
+    (void)hipEventCreate(&m.b);
+    (void)hipEventRecord(m.a, st);
+    marks.push_back(m);
+  }
+  void end(const char* stage, hipStream_t st) {
+    for (auto it = marks.rbegin(); it != marks.rend(); ++it)
+      if (!std::strcmp(it->stage, stage) && it->step == step) { (void)hipEventRecord(it->b, st); return; }
+  }
+  void dump() {
+    if (marks.empty()) return;
+    for (auto& m : marks) {
+      float a = 0, b = 0;
+      if (!m.a || !m.b) continue;
+      (void)hipEventElapsedTime(&a, marks[0].a, m.a);
+      (void)hipEventElapsedTime(&b, marks[0].a, m.b);
+      std::fprintf(stderr, "PIPE %d %s %.1f %.1f\n", m.step, m.stage, 1e3 * a, 1e3 * b);
+    }
+    for (auto& m : marks) {
+      if (m.a) (void)hipEventDestroy(m.a);
+      if (m.b) (void)hipEventDestroy(m.b);
+    }
+    marks.clear();
+  }
+};
+PipeTrace g_pt;
+}  // namespace
+#define PT_BEGIN(s, st) g_pt.begin(s, st)
+#define PT_END(s, st) g_pt.end(s, st)
+#else
+#define PT_BEGIN(s, st) ((void)0)
+#define PT_END(s, st) ((void)0)
+#endif
+
 using namespace loam;
 
 namespace {
@@ -830,7 +875,7 @@ int loam_mapping(loam_ctx* x, double stamp, const loam_pose6* odom_sum, const lo
   bool updated = false;
   const int rc = mp_stream_frame(x->mp1, x->st, *odom_sum, *corner_last, *surf_last, *full_end, aft, bef,
                                  registered, &x->stats, g_err, x->pin, x->io(), have_imu ? rp : nullptr, &updated,
-                                 x->st2, x->join);
+                                 x->st2, x->join, x->tune.mp_defer ? x->st2 : nullptr);
   if (have_imu && updated) x->mp_imu.front = front;  // the pointer walk happens inside transformUpdate
   x->surround_due = false;
   if (rc == LOAM_OK && ++x->map_frame_count >= 5) {  // :1038-1040
@@ -877,7 +922,7 @@ int loam_chain_sweep(loam_ctx* x, double stamp, loam_cloud_in raw, loam_chain_ou
   loam_cloud_out* reg = out->registered.capacity ? &out->registered : nullptr;
   if (!reg) out->registered.count = 0;
   rc = mp_stream_frame_dev(x->mp1, x->st, out->od_sum, in, nl3, &out->aft, &out->bef, reg, &x->stats, g_err,
-                           x->pin, x->io(), have_imu ? rp : nullptr, &updated);
+                           x->pin, x->io(), have_imu ? rp : nullptr, &updated, x->tune.mp_defer ? x->st2 : nullptr);
   if (have_imu && updated) x->mp_imu.front = front;
   x->surround_due = false;
   if (rc == LOAM_OK && ++x->map_frame_count >= 5) {  // :1038-1040
@@ -1161,7 +1206,9 @@ hipError_t enqueue_ahead(loam_ctx* x, int i, int ls, hipEvent_t free_last) {
   auto T = [&](hipError_t r) { if (e == hipSuccess) e = r; };
   if (x->mp_done_rec[i]) T(hipStreamWaitEvent(x->st3, x->mp_done[i], 0));
   T(hipStreamWaitEvent(x->st3, x->a_start, 0));  // (whatever ran on st before this call)
+  PT_BEGIN("sr", x->st3);
   sr_launch(x->srbuf(i), sr_params(x), x->st3, nullptr);
+  PT_END("sr", x->st3);
   T(hipEventRecord(x->sr_done, x->st3));
   if (free_last) T(hipStreamWaitEvent(x->st3, free_last, 0));
   on.istate = on.istate_set[i];
@@ -1209,12 +1256,14 @@ hipError_t batch_enqueue_pipe(loam_ctx* x) {
   T(hipStreamWaitEvent(x->st, x->sr_done, 0));
   T(hipStreamWaitEvent(x->st, x->seed_done, 0));
   T(hipEventRecord(x->ev[1], x->st));
+  PT_BEGIN("od", x->st);
   T(hipMemsetAsync(o.state, 0, (size_t)P * kOdStateFloats * sizeof(float), x->st));
   od_solve(o, fcur, ls, x->st, nullptr, /*device_fini=*/true);
   // Last[le] was the previous step's Last[s]: its frame 1 has read it (its odometry is ahead on st);
   // before that, frame 2 of the step before read it, which the previous seed waited for
   if (x->b_used) T(hipStreamWaitEvent(x->st, x->mp1_read, 0));
   hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, le, 2, 0);
+  PT_END("od", x->st);
   T(hipEventRecord(x->od_done, x->st));
   T(hipEventRecord(x->ev[2], x->st));
   // mapping: frame 1 once the seed (and this call's earlier work on st) is there, frame 2 once the
@@ -1228,14 +1277,21 @@ hipError_t batch_enqueue_pipe(loam_ctx* x) {
   T(hipStreamWaitEvent(ms, x->seed_done, 0));
   SideStream side1;  // (no branches: only the event once Last[ls] is read)
   side1.inputs_read = x->mp1_read;
+  PT_BEGIN("mp1", ms);
   mp_batch_frame1(mb, o, ls, fprev, ms, nullptr, &side1);
+  PT_END("mp1", ms);
   T(hipEventRecord(x->mp1_done, ms));
   T(hipStreamWaitEvent(ms, x->od_done, 0));
+  PT_BEGIN("mp2", ms);
   SideStream side;
   side.st = two ? nullptr : x->st2;
   side.fork[0] = x->fork; side.join[0] = x->join; side.fork[1] = x->fork2; side.join[1] = x->join2;
   side.inputs_read = x->inputs_read[idx];
   mp_batch_frame2(mb, o, le, fcur, ms, nullptr, &side);
+  PT_END("mp2", ms);
+#ifdef LOAM_PIPE_TRACE
+  ++g_pt.step;
+#endif
   T(hipEventRecord(x->mp_done[idx], ms));
   x->mp_done_rec[idx] = true;
   x->b_used = true;
@@ -1361,6 +1417,9 @@ int loam_batch_sync(loam_ctx* x) {
   if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));
   // launch errors of either mapping set (the step pipeline alternates them), reported by this call
   for (int i = 0; i < 2; ++i) HIP_TRY(x->mpbuf(i).take_error());
+#ifdef LOAM_PIPE_TRACE
+  g_pt.dump();
+#endif
   return LOAM_OK;
 }
 

@@ -90,6 +90,9 @@ struct Tuning {
                            // certificate when it still separates every choice from its rivals (exact)
   int od_lm_mom_min = 1;   // with the moments: k_od_lm_mom (an association round's 5 iterations in one
   int od_lm_mom_max = 0;   //   workgroup per problem) for od_lm_mom_min <= P <= od_lm_mom_max
+  int mp_defer = 1;        // streaming mapping frames run the map update (insertion, per-cube VoxelGrid,
+                           // compaction) on the second stream after the L-M: the pose and registered cloud
+                           // are downloaded without waiting for it; the next frame waits for it first
   int od_moments_min = 64; // for P >= this (and P > od_small_max), k_od_rows keeps each query's
                            // stored rows (Q12) as fp64 moments instead of re-evaluating them every
                            // iteration: O(queries) per iteration, not bit-identical, within 1e-4 of the
@@ -102,7 +105,7 @@ struct Tuning {
   }
   bool set(const char* key, long long v, long long* read = nullptr) {
     struct K { const char* n; int* f; long long lo, hi; };
-    const K ks[] = {{"od_small_max", &od_small_max, 0, 1 << 20}, {"od_lm_min", &od_lm_min, 1, 1 << 20},
+    const K ks[] = {{"od_small_max", &od_small_max, 0, 1 << 20}, {"mp_defer", &mp_defer, 0, 1}, {"od_lm_min", &od_lm_min, 1, 1 << 20},
                     {"od_lm_max", &od_lm_max, 0, 1 << 20}, {"od_fused_max", &od_fused_max, 0, 1 << 20},
                     {"mp_small_max", &mp_small_max, 0, 1 << 20}, {"mp_fused_max", &mp_fused_max, 0, 1 << 20},
                     {"nn_lanes", &nn_lanes, 1, 4}, {"nn_lanes_maxp", &nn_lanes_maxp, 0, 1 << 20},

@@ -2646,8 +2646,11 @@ void mp_free(MpBuffers& b) {
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
                   b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_l0, b.vg_l1, b.vg_lin, b.vg_cnt, b.reg, b.nreg, b.part, b.done, b.rot,
                   b.vg_mlist, b.vseg_nold, b.vseg_skip};
+  if (b.upd_pending && b.upd_done) (void)hipEventSynchronize(b.upd_done);
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
+  if (b.upd_fork) (void)hipEventDestroy(b.upd_fork);
+  if (b.upd_done) (void)hipEventDestroy(b.upd_done);
   b = MpBuffers();
 }
 
@@ -2659,6 +2662,7 @@ __global__ void k_mp_reset(MpBuffers b) {
 }
 
 hipError_t mp_reset(MpBuffers& b, hipStream_t st) {
+  mp_wait_update(b, st);
   b.pool_cur = 0;
   hipError_t e = hipMemsetAsync(b.state, 0, (size_t)b.P * kMpStateFloats * sizeof(float), st);
   if (e == hipSuccess) e = hipMemsetAsync(b.done, 0, (size_t)b.P * sizeof(int), st);
@@ -2669,10 +2673,18 @@ hipError_t mp_reset(MpBuffers& b, hipStream_t st) {
   return hipGetLastError();
 }
 
+void mp_wait_update(MpBuffers& b, hipStream_t st) {
+  if (!b.upd_pending) return;
+  b.note(hipStreamWaitEvent(st, b.upd_done, 0));
+  b.upd_pending = false;
+}
+
 void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool map_empty,
-              const std::function<void()>& before_register, int stack_max, const SideStream* side) {
+              const std::function<void()>& before_register, int stack_max, const SideStream* side,
+              hipStream_t defer) {
   const int P = b.P;
   auto mark = [&](const char* n) { if (prof) prof->mark(n); };
+  mp_wait_update(b, st);  // (the previous frame's map update, when it was deferred)
   hipLaunchKernelGGL(k_mp_prepare, dim3(P), dim3(kMpThreads), 0, st, b, in);
   mark("k_mp_prepare");
   hipLaunchKernelGGL(k_mp_stack, dim3(16, P), dim3(256), 0, st, b, in);
@@ -2776,7 +2788,16 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   hipLaunchKernelGGL(k_mp_lm_end, dim3((P + 255) / 256), dim3(256), 0, st, b);
   // the registration reads only the final pose and the full cloud: beside the insertion with a
   // side stream (the batch: no before_register hook)
-  const bool reg_side = fork && !before_register;
+  const bool reg_side = fork && !before_register && !defer;
+  // defer: the map update on the other stream, forked here; the registration stays on st
+  hipStream_t us = st;
+  if (defer) {
+    if (!b.upd_fork) b.note(hipEventCreateWithFlags(&b.upd_fork, hipEventDisableTiming));
+    if (!b.upd_done) b.note(hipEventCreateWithFlags(&b.upd_done, hipEventDisableTiming));
+    b.note(hipEventRecord(b.upd_fork, st));
+    b.note(hipStreamWaitEvent(defer, b.upd_fork, 0));
+    us = defer;
+  }
   if (reg_side) {
     b.note(hipEventRecord(side->fork[1], st));
     b.note(hipStreamWaitEvent(side->st, side->fork[1], 0));
@@ -2786,10 +2807,10 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   // insertion + per-valid-cube downsampling into the other pool
   // a few instances: 1024 threads per instance (the per-instance serial parts are the cost)
   // 1024 threads per instance also for batches (k_mp_insert 0.40 -> 0.25 ms/step at batch 1024 against 256)
-  hipLaunchKernelGGL(k_mp_insert<1024>, dim3(P), dim3(1024), 0, st, b, (int*)b.vg_k, (int*)b.vg_v);
+  hipLaunchKernelGGL(k_mp_insert<1024>, dim3(P), dim3(1024), 0, us, b, (int*)b.vg_k, (int*)b.vg_v);
   mark("k_mp_insert");
-  hipLaunchKernelGGL(k_mp_vseg, dim3(P), dim3(kMpThreads), 0, st, b);
-  hipLaunchKernelGGL(k_mp_vcopy, dim3(32, P), dim3(256), 0, st, b);
+  hipLaunchKernelGGL(k_mp_vseg, dim3(P), dim3(kMpThreads), 0, us, b);
+  hipLaunchKernelGGL(k_mp_vcopy, dim3(32, P), dim3(256), 0, us, b);
   mark("k_mp_vseg_vcopy");
   VgJob jv = vg_job(b);
   jv.in = b.vin; jv.out = b.vout; jv.begin = b.vseg_b; jv.end = b.vseg_e; jv.leaf = b.vseg_leaf;
@@ -2799,15 +2820,19 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   if (b.tune.vg_merge) {  // long cube segments with a short tail first (k_vg_merge), the rest by the cascade
     jv.nold = b.vseg_nold; jv.mlist = b.vg_mlist; jv.mlist_n = b.vg_cnt + 3; jv.skip = b.vseg_skip;
     // (its segments are rare: a small grid whose workgroups leave at once when the list is short)
-    hipLaunchKernelGGL((k_vg_merge<1024, kVgMergeNew>), dim3(std::min(2 * kMaxValid * P, 32)), dim3(1024), 0, st, jv);
+    hipLaunchKernelGGL((k_vg_merge<1024, kVgMergeNew>), dim3(std::min(2 * kMaxValid * P, 32)), dim3(1024), 0, us, jv);
   }
   // 2 x 125 cube segments per instance, most of them small: batches start with the 2048-point
   // kernel (many workgroups per CU); a few instances with the 12288-point one (one launch)
-  b.note(vg_run(jv, st, P <= 4 ? 12288 : 2048));
+  b.note(vg_run(jv, us, P <= 4 ? 12288 : 2048));
   mark("vg_cubes");
-  hipLaunchKernelGGL(k_mp_compact_table<1024>, dim3(P), dim3(1024), 0, st, b);
-  hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, st, b);
+  hipLaunchKernelGGL(k_mp_compact_table<1024>, dim3(P), dim3(1024), 0, us, b);
+  hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, us, b);
   mark("k_mp_compact");
+  if (defer) {
+    b.note(hipEventRecord(b.upd_done, us));
+    b.upd_pending = true;
+  }
   if (before_register) before_register();
   if (reg_side) {
     b.note(hipStreamWaitEvent(st, side->join[1], 0));
@@ -2821,12 +2846,12 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
 template <typename Hook>
 int mp_stream_run(MpBuffers& b, hipStream_t st, const MpInput& in, const int* n, loam_pose6* aft, loam_pose6* bef,
                   loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, const StreamIo& io,
-                  bool* updated, Hook hook);
+                  bool* updated, Hook hook, hipStream_t defer);
 
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
                     const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
                     loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, const StreamIo& io,
-                    const float* imu_rp, bool* updated, hipStream_t st2, hipEvent_t ev2) {
+                    const float* imu_rp, bool* updated, hipStream_t st2, hipEvent_t ev2, hipStream_t defer) {
   if (corner.count > (uint32_t)b.capC || surf.count > (uint32_t)b.capS || full.count > (uint32_t)b.capS) {
     err = "mapping input cloud exceeds capacity";
     return LOAM_E_CAPACITY;
@@ -2877,14 +2902,15 @@ int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, co
     if (le == hipSuccess) le = hipEventRecord(ev2, st2);
     if (le == hipSuccess) le = hipStreamWaitEvent(st, ev2, 0);
     return le;
-  });
+  }, defer);
 }
 
 // the device-resident chain (loam_chain_sweep): the clouds are already on the device (odometry's
 // published Last / full-end buffers, src, with device counts); n3: their counts on the host
 int mp_stream_frame_dev(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const MpInput& src, const int* n3,
                         loam_pose6* aft, loam_pose6* bef, loam_cloud_out* registered, loam_stats* stats,
-                        std::string& err, Staging& pin, const StreamIo& io, const float* imu_rp, bool* updated) {
+                        std::string& err, Staging& pin, const StreamIo& io, const float* imu_rp, bool* updated,
+                        hipStream_t defer) {
   if (n3[0] > b.capC || n3[1] > b.capS || n3[2] > b.capS) {
     err = "mapping input cloud exceeds capacity";
     return LOAM_E_CAPACITY;
@@ -2905,22 +2931,33 @@ int mp_stream_frame_dev(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum
   in.pose = b.in_pose;
   in.pose_stride = 6;
   return mp_stream_run(b, st, in, n3, aft, bef, registered, stats, err, pin, io, updated,
-                       []() { return hipSuccess; });
+                       []() { return hipSuccess; }, defer);
 }
 
 // the frame's kernels on `in` and the downloads (both stream entry points); hook: called just
-// before k_mp_register (the late full-cloud staging)
+// before k_mp_register (the late full-cloud staging); defer: the map update's stream (mp_frame),
+// nullptr = in order on st
 template <typename Hook>
 int mp_stream_run(MpBuffers& b, hipStream_t st, const MpInput& in, const int* n, loam_pose6* aft, loam_pose6* bef,
                   loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, const StreamIo& io,
-                  bool* updated, Hook hook) {
+                  bool* updated, Hook hook, hipStream_t defer) {
   const hipEvent_t e0 = io.e0, e1 = io.e1;
   hipError_t le = hipEventRecord(e0, st);
   mp_frame(b, in, st, nullptr, false, [&]() {
     if (le != hipSuccess) return;
     le = hook();
-  }, std::max(n[0], n[1]));
+  }, std::max(n[0], n[1]), nullptr, defer);
   if (le == hipSuccess) le = hipEventRecord(e1, st);
+  // a deferred update's valid-point count (stats) into the mapped host block after it, one slot
+  // per frame parity: this call reads the previous frame's (complete: this frame's kernels on st
+  // waited for that update), while this frame's may still be writing the other slot
+  const bool deferred = defer && b.upd_pending;
+  if (deferred && le == hipSuccess) {
+    Xfer xg;
+    xg.get(io.xb.d + kXferMpUpd + 4 * (1 - b.pool_cur), b.istate + kMiValidPts, sizeof(int));
+    le = xfer_launch(xg, defer);
+    if (le == hipSuccess) le = hipEventRecord(b.upd_done, defer);
+  }
   // state (kMpStateFloats), istate (kMpStateInts), nreg into the mapped host block, one launch
   static_assert(kXferMp + 4 * (kMpStateFloats + kMpStateInts + 1) <= kXferBytes, "mapping transfer region");
   const float* sf = (const float*)(io.xb.h + kXferMp);
@@ -2978,7 +3015,9 @@ int mp_stream_run(MpBuffers& b, hipStream_t st, const MpInput& in, const int* n,
     stats->mp_stack_iters = (uint64_t)si[kMiIters] * (si[kMiStackC] + si[kMiStackS]);
     stats->mp_fits = (uint64_t)si[kMiFits];
     stats->mp_map_points = (uint64_t)(si[kMiFromC] + si[kMiFromS]);
-    stats->mp_map_valid_points = (uint64_t)si[kMiValidPts];
+    // (a deferred update: the previous frame's map, this frame's is not counted yet)
+    stats->mp_map_valid_points =
+        (uint64_t)(deferred ? *(const int*)(io.xb.h + kXferMpUpd + 4 * b.pool_cur) : si[kMiValidPts]);
     stats->mp_degenerate_steps = (uint64_t)si[kMiDegSteps];
     stats->mp_grid_shifts = (uint64_t)si[kMiShifts];
     stats->mp_nn_candidates = (uint64_t)(uint32_t)si[kMiNnCand];
@@ -3029,6 +3068,7 @@ __global__ __launch_bounds__(256) void k_mp_surround(MpBuffers b) {
 }
 
 int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::string& err) {
+  mp_wait_update(b, st);  // (the last frame's map update, when deferred)
   hipLaunchKernelGGL(k_mp_surround, dim3(1), dim3(256), 0, st, b);
   VgJob j = vg_job(b);
   j.in = b.vin; j.out = b.vout; j.begin = b.vseg_b; j.end = b.vseg_e; j.leaf = b.vseg_leaf;

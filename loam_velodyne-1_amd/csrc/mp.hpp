@@ -131,6 +131,11 @@ struct MpBuffers {
   int* done = nullptr;        // [P] its workgroups finished (the last one runs the step)
   double* rot = nullptr;      // [P][6] cos / sin of the TobeMapped rotation (rot_store in mp.hip)
   int* nreg = nullptr;
+  // the streaming frame's map update (insertion, per-cube VoxelGrid, compaction) deferred to a side
+  // stream (mp_frame's `defer`): upd_done is recorded there; the next frame, the surround cloud
+  // and a reset wait for it first (upd_pending)
+  hipEvent_t upd_fork = nullptr, upd_done = nullptr;
+  bool upd_pending = false;
   Tuning tune;                // host-side launch choices (mp_frame)
   hipError_t sticky = hipSuccess;  // first failed HIP call of the launch sequences
   void note(hipError_t e) {
@@ -160,21 +165,26 @@ struct SideStream {
   hipEvent_t fork[2] = {nullptr, nullptr}, join[2] = {nullptr, nullptr};
   hipEvent_t inputs_read = nullptr;  // optional: recorded once the frame has read its input clouds
 };
+// defer: a second stream for the map update (streaming frames): the update runs there after the
+// L-M, beside the registration and the caller's downloads; the frame's pose and registered cloud do
+// not wait for it (b.upd_pending until the next frame's first kernel has waited for it)
 void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof = nullptr, bool map_empty = false,
               const std::function<void()>& before_register = nullptr, int stack_max = -1,
-              const SideStream* side = nullptr);
+              const SideStream* side = nullptr, hipStream_t defer = nullptr);
+// the pending deferred map update (if any) before later work on st
+void mp_wait_update(MpBuffers& b, hipStream_t st);
 // imu_rp: the IMU (roll, pitch) transformUpdate blends in (nullptr = no IMU); *updated = whether
 // transformUpdate ran (the caller then commits its IMU queue pointer)
 int mp_stream_frame(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const loam_cloud_out& corner,
                     const loam_cloud_out& surf, const loam_cloud_out& full, loam_pose6* aft, loam_pose6* bef,
                     loam_cloud_out* registered, loam_stats* stats, std::string& err, Staging& pin, const StreamIo& io,
                     const float* imu_rp = nullptr, bool* updated = nullptr, hipStream_t st2 = nullptr,
-                    hipEvent_t ev2 = nullptr);
+                    hipEvent_t ev2 = nullptr, hipStream_t defer = nullptr);
 // the same frame on clouds already on the device (src: pointers + device counts, n3: host counts)
 int mp_stream_frame_dev(MpBuffers& b, hipStream_t st, const loam_pose6& odom_sum, const MpInput& src, const int* n3,
                         loam_pose6* aft, loam_pose6* bef, loam_cloud_out* registered, loam_stats* stats,
                         std::string& err, Staging& pin, const StreamIo& io, const float* imu_rp = nullptr,
-                        bool* updated = nullptr);
+                        bool* updated = nullptr, hipStream_t defer = nullptr);
 // /laser_cloud_surround of the last streaming frame (instance 0): its 5x5x5 cube neighbourhood
 // concatenated and VoxelGrid 0.2 (src/laserMapping.cpp:1038-1058)
 int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::string& err);

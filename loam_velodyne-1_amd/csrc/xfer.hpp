@@ -69,7 +69,7 @@ struct StreamIo {
   XferBuf xb;
   hipEvent_t e0 = nullptr, e1 = nullptr;
 };
-constexpr int kXferSr = 0, kXferOd = 64, kXferMp = 512, kXferBytes = 4096;
+constexpr int kXferSr = 0, kXferOd = 64, kXferMp = 512, kXferMpUpd = 1024, kXferBytes = 4096;
 
 }  // namespace loam
 
