@@ -140,7 +140,7 @@ struct loam_ctx {
   // step that consumes it waits on sr_done.  The raw sweeps are uploaded into both sets.
   SrBuffers srb2;
   hipStream_t st3 = nullptr;
-  hipEvent_t sr_done = nullptr, step_done[2] = {nullptr, nullptr};
+  hipEvent_t sr_done = nullptr, step_done[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ahead_at = nullptr;  // the point of this step after which it may start (tune.sr_ahead_at)
   // ... followed by the next step's odometry seed (Last[0] and its hashes, into the other istate
   // set), once this step's second mapping frame begins (the odometry no longer reads Last[0])
@@ -151,19 +151,25 @@ struct loam_ctx {
   hipStream_t st4 = nullptr;
   hipEvent_t od_done = nullptr, mp1_done = nullptr, a_start = nullptr, b_last = nullptr;
   hipEvent_t mp1_read = nullptr;  // frame 1 has read Last[s] (after its k_mp_stack)
-  hipEvent_t inputs_read[2] = {nullptr, nullptr};  // frame 2 of the steps reading SR set i has read Last[e]
-  hipEvent_t mp_done[2] = {nullptr, nullptr};
-  bool mp_done_rec[2] = {false, false}, inputs_read_rec[2] = {false, false}, b_used = false;
+  // per SR set (slot) of the step pipeline: frame 2 of the step reading set i has read Last[e]; that
+  // step's mapping is done (the set's last reader)
+  hipEvent_t inputs_read[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t mp_done[3] = {nullptr, nullptr, nullptr};
+  bool mp_done_rec[3] = {false, false, false}, inputs_read_rec[3] = {false, false, false}, b_used = false;
   // the Last buffers (OdBuffers, kOdBufs of them) of the next step: its seed's (od_s, the odometry's
   // Last) and its TransformToEnd's (od_e, frame 2's input).  The step pipeline rotates (s, e) ->
   // (3 - s - e, s), so the next seed writes the buffer no running step reads and never waits for the
   // odometry; batch_enqueue keeps them.  od_s_last: the seed buffer of the last enqueued step.
   int od_s = 0, od_e = 1, od_s_last = 0;
-  bool step_done_rec[2] = {false, false};
+  bool step_done_rec[3] = {false, false, false};
   int sr_idx = 0;         // the set the next step reads
   bool sr_ready = false;  // its scan registration is already enqueued (st3, sr_done)
   int srb_last = 0;       // the set of the last enqueued step (loam_batch_download)
-  SrBuffers& srbuf(int i) { return i ? srb2 : srb; }
+  // tune.pipe_sr_sets = 3: the step pipeline rotates three SR sets (and odometry state sets), so a
+  // step's scan registration waits for the mapping of the step three back, not two
+  SrBuffers srb3;
+  SrBuffers& srbuf(int i) { return i == 2 ? srb3 : (i ? srb2 : srb); }
+  int pipe_k = 0;         // pipelined steps since the last drain (their mapping sets alternate by parity)
   MpBuffers mpb2;         // the second mapping set: the step pipeline's steps alternate (mpbuf)
   MpBuffers& mpbuf(int i) { return i ? mpb2 : mpb; }
   int mp_last = 0;        // the mapping set of the last enqueued step (loam_batch_download)
@@ -171,12 +177,12 @@ struct loam_ctx {
   // reads (copied on st3 behind that set's previous reader, then its scan registration + seed
   // there); a fed context enqueues nothing ahead at the end of a run (the feed does)
   bool fed = false;
-  float4* feed_pin[2] = {nullptr, nullptr};  // pinned staging per SR set, [2P][cap]
-  int* feed_n[2] = {nullptr, nullptr};       // pinned sweep sizes per SR set, [2P]
-  hipEvent_t feed_copied[2] = {nullptr, nullptr};
-  bool feed_rec[2] = {false, false};
+  float4* feed_pin[3] = {nullptr, nullptr, nullptr};  // pinned staging per SR set, [2P][cap]
+  int* feed_n[3] = {nullptr, nullptr, nullptr};       // pinned sweep sizes per SR set, [2P]
+  hipEvent_t feed_copied[3] = {nullptr, nullptr, nullptr};
+  bool feed_rec[3] = {false, false, false};
   void free_feed() {
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 3; ++i) {
       if (feed_rec[i]) (void)hipEventSynchronize(feed_copied[i]);
       if (feed_pin[i]) (void)hipHostFree(feed_pin[i]);
       if (feed_n[i]) (void)hipHostFree(feed_n[i]);
@@ -188,10 +194,10 @@ struct loam_ctx {
   void reset_ahead() {    // (after draining st3 / st4)
     sr_ready = false;
     seed_ready = false;
-    mp_done_rec[0] = mp_done_rec[1] = false;
-    inputs_read_rec[0] = inputs_read_rec[1] = b_used = false;
-    sr_idx = srb_last = 0;
-    step_done_rec[0] = step_done_rec[1] = false;
+    for (int i = 0; i < 3; ++i) mp_done_rec[i] = inputs_read_rec[i] = false;
+    b_used = false;
+    sr_idx = srb_last = pipe_k = 0;
+    step_done_rec[0] = step_done_rec[1] = step_done_rec[2] = false;
   }
   OdBuffers odb;
   MpBuffers mpb;
@@ -363,8 +369,8 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->sr_done, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->ahead_at, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_at, hipEventDisableTiming);
-  for (hipEvent_t* e : {&x->od_done, &x->mp1_done, &x->inputs_read[0], &x->inputs_read[1], &x->a_start, &x->b_last,
-                        &x->mp_done[0], &x->mp_done[1], &x->mp1_read})
+  for (hipEvent_t* e : {&x->od_done, &x->mp1_done, &x->inputs_read[0], &x->inputs_read[1], &x->inputs_read[2],
+                        &x->a_start, &x->b_last, &x->mp_done[0], &x->mp_done[1], &x->mp_done[2], &x->mp1_read})
     if (he == hipSuccess) he = hipEventCreateWithFlags(e, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&x->seed_done, hipEventDisableTiming);
   for (auto& e : x->step_done)
@@ -420,6 +426,7 @@ void loam_destroy(loam_ctx* x) {
   mp_free(x->mp1);
   sr_free(x->srb);
   sr_free(x->srb2);
+  sr_free(x->srb3);
   od_free(x->odb);
   mp_free(x->mpb);
   mp_free(x->mpb2);
@@ -442,8 +449,8 @@ void loam_destroy(loam_ctx* x) {
   if (x->sr_done) (void)hipEventDestroy(x->sr_done);
   if (x->ahead_at) (void)hipEventDestroy(x->ahead_at);
   if (x->seed_at) (void)hipEventDestroy(x->seed_at);
-  for (hipEvent_t e : {x->od_done, x->mp1_done, x->inputs_read[0], x->inputs_read[1], x->a_start, x->b_last,
-                       x->mp_done[0], x->mp_done[1], x->mp1_read})
+  for (hipEvent_t e : {x->od_done, x->mp1_done, x->inputs_read[0], x->inputs_read[1], x->inputs_read[2], x->a_start,
+                       x->b_last, x->mp_done[0], x->mp_done[1], x->mp_done[2], x->mp1_read})
     if (e) (void)hipEventDestroy(e);
   if (x->st4) (void)hipStreamDestroy(x->st4);
   if (x->seed_done) (void)hipEventDestroy(x->seed_done);
@@ -455,20 +462,15 @@ void loam_destroy(loam_ctx* x) {
   delete x;
 }
 
-int loam_set_stream_priority(loam_ctx* x, int priority) {
-  if (!x) return fail(LOAM_E_INVAL, "null argument");
-  HIP_TRY(hipSetDevice(x->device));
-  int least = 0, greatest = 0;  // HIP: a numerically lower value is a higher priority
-  HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-  const int prio = priority > 0 ? greatest : priority < 0 ? least : 0;
-  // drain the old streams first: a failure here leaves the context on its old streams, unchanged
+namespace {
+// the context's streams recreated at priority prio, in loam_create's order (st, st2, st3, st4: streams take the process's
+// hardware queues in creation order); the batch pipeline's two only when the context keeps them
+// (tuning batch_streams).  Drains the old streams first: a failure leaves the context on them.
+int remake_streams(loam_ctx* x, int prio) {
   HIP_TRY(hipStreamSynchronize(x->st));
   if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
   if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));
   if (x->st4) HIP_TRY(hipStreamSynchronize(x->st4));
-  // all of the context's streams at the new priority, created in loam_create's order (st, st2, st3,
-  // st4: streams take the process's hardware queues in creation order); the batch pipeline's two
-  // only when the context keeps them (tuning batch_streams)
   const bool batch = x->st3 != nullptr || x->st4 != nullptr;
   hipStream_t ns[4] = {nullptr, nullptr, nullptr, nullptr};
   hipError_t he = hipSuccess;
@@ -491,6 +493,15 @@ int loam_set_stream_priority(loam_ctx* x, int priority) {
   x->pin.streams[0] = x->st;
   x->pin.streams[1] = x->st2;
   return LOAM_OK;
+}
+}  // namespace
+
+int loam_set_stream_priority(loam_ctx* x, int priority) {
+  if (!x) return fail(LOAM_E_INVAL, "null argument");
+  HIP_TRY(hipSetDevice(x->device));
+  int least = 0, greatest = 0;  // HIP: a numerically lower value is a higher priority
+  HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  return remake_streams(x, priority > 0 ? greatest : priority < 0 ? least : 0);
 }
 
 int loam_set_tuning(loam_ctx* x, const char* key, long long value) {
@@ -996,6 +1007,8 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
     x->free_feed();   // (sized for the old batch)
     sr_free(x->srb);
     sr_free(x->srb2);
+    sr_free(x->srb3);
+  sr_free(x->srb3);
     od_free(x->odb);
     mp_free(x->mpb);
     mp_free(x->mpb2);
@@ -1008,6 +1021,9 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
     if (he != hipSuccess) {
       sr_free(x->srb);
       sr_free(x->srb2);
+      sr_free(x->srb3);
+    sr_free(x->srb3);
+  sr_free(x->srb3);
       od_free(x->odb);
       mp_free(x->mpb);
       mp_free(x->mpb2);
@@ -1028,10 +1044,11 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
                         hipMemcpyHostToDevice));
     }
   HIP_TRY(hipMemcpy(x->srb.raw_n, counts.data(), counts.size() * sizeof(int), hipMemcpyHostToDevice));
-  if (x->srb2.S) {  // the second set's raw sweeps (tune.sr_ahead / step_pipe)
-    HIP_TRY(hipMemcpy(x->srb2.raw, x->srb.raw, (size_t)2 * n * x->cap * sizeof(float4), hipMemcpyDeviceToDevice));
-    HIP_TRY(hipMemcpy(x->srb2.raw_n, x->srb.raw_n, counts.size() * sizeof(int), hipMemcpyDeviceToDevice));
-  }
+  for (SrBuffers* o : {&x->srb2, &x->srb3})
+    if (o->S) {  // the other sets' raw sweeps (tune.sr_ahead / step_pipe)
+      HIP_TRY(hipMemcpy(o->raw, x->srb.raw, (size_t)2 * n * x->cap * sizeof(float4), hipMemcpyDeviceToDevice));
+      HIP_TRY(hipMemcpy(o->raw_n, x->srb.raw_n, counts.size() * sizeof(int), hipMemcpyDeviceToDevice));
+    }
   return LOAM_OK;
 }
 
@@ -1059,14 +1076,28 @@ void pack_batch(const loam_cloud_in* prev, const loam_cloud_in* cur, uint32_t np
 // the sets between steps use (tune.sr_ahead, tune.step_pipe): allocated on the first step that
 // needs them, the uploaded raw sweeps copied from the first set.  The sets of the batch are then
 // kept until an upload of another size.
-int ensure_second_sets(loam_ctx* x) {
-  if (x->srb2.S) return LOAM_OK;
+// the SR sets the step pipeline rotates (tune.pipe_sr_sets when pipelined, else 2)
+int pipe_slots(const loam_ctx* x, bool pipe) { return pipe ? x->tune.pipe_sr_sets : 2; }
+
+int ensure_second_sets(loam_ctx* x, int slots) {
   const int P = x->P;
+  if (slots > 2 && !x->srb3.S) {  // the third SR set (tune.pipe_sr_sets = 3)
+    const hipError_t he = sr_alloc(x->srb3, 2 * P, x->cap, x->R);
+    if (he != hipSuccess) {
+      sr_free(x->srb3);
+      return fail(LOAM_E_NOMEM, std::string("third batch set allocation failed: ") + hipGetErrorString(he));
+    }
+    HIP_TRY(hipMemcpy(x->srb3.raw, x->srb.raw, (size_t)2 * P * x->cap * sizeof(float4), hipMemcpyDeviceToDevice));
+    HIP_TRY(hipMemcpy(x->srb3.raw_n, x->srb.raw_n, (size_t)2 * P * sizeof(int), hipMemcpyDeviceToDevice));
+  }
+  if (x->srb2.S) return LOAM_OK;
   hipError_t he = sr_alloc(x->srb2, 2 * P, x->cap, x->R);
   if (he == hipSuccess)
     he = mp_alloc(x->mpb2, P, x->R, x->cap, mp_batch_map_capacity(x->cap), (int)x->cfg.mp_max_iter);
   if (he != hipSuccess) {
     sr_free(x->srb2);
+    sr_free(x->srb3);
+  sr_free(x->srb3);
     mp_free(x->mpb2);
     return fail(LOAM_E_NOMEM, std::string("second batch set allocation failed: ") + hipGetErrorString(he));
   }
@@ -1094,7 +1125,7 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   if (events) T(hipEventRecord(x->ev[0], x->st));
   x->prof.begin(x->st);
   if (x->b_used) {  // pipelined steps' mappings may still run on st4 / st2 (batch_enqueue_pipe)
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 3; ++i)
       if (x->mp_done_rec[i]) T(hipStreamWaitEvent(x->st, x->mp_done[i], 0));
     x->b_used = false;
   }
@@ -1172,7 +1203,7 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
   if (ahead) {
     T(hipEventRecord(x->step_done[idx], x->st));
     x->step_done_rec[idx] = true;
-    const int nx = 1 - idx;
+    const int nx = idx == 0 ? 1 : 0;  // (two sets here; a slot 2 left by pipelined runs goes back to 0)
     if (x->step_done_rec[nx]) T(hipStreamWaitEvent(x->st3, x->step_done[nx], 0));
     T(hipStreamWaitEvent(x->st3, x->ahead_at, 0));
     sr_launch(x->srbuf(nx), sr_params(x), x->st3, nullptr);
@@ -1199,6 +1230,12 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
 // (mp_done[i]: its mapping, the last reader, after that step's odometry), and, when `free_last` is
 // recorded, Last[ls]'s last reader: frame 2 of the step before the current one (the rotation of
 // batch_enqueue_pipe leaves Last[ls] to no running step's odometry or frame 1).
+// the event after which the seed of the step reading SR slot j may rewrite its Last buffer: frame 2
+// of the step two before it (slot j - 2 of n) read that buffer last (its inputs_read), if recorded
+hipEvent_t seed_free_last(const loam_ctx* x, int j, int n) {
+  const int k = (j + n - 2) % n;
+  return x->inputs_read_rec[k] ? x->inputs_read[k] : nullptr;
+}
 hipError_t enqueue_ahead(loam_ctx* x, int i, int ls, hipEvent_t free_last) {
   const int P = x->P;
   OdBuffers on = x->odb;
@@ -1237,7 +1274,7 @@ hipError_t batch_enqueue_pipe(loam_ctx* x) {
   OdBuffers& o = x->odb;
   hipError_t e = hipSuccess;
   auto T = [&](hipError_t r) { if (e == hipSuccess) e = r; };
-  const int idx = x->sr_idx, nx = 1 - idx;
+  const int n = pipe_slots(x, true), idx = x->sr_idx, nx = (idx + 1) % n;
   const int ls = x->od_s, le = x->od_e, lf = kOdBufs - ls - le;
   static_assert(kOdBufs == 3, "the rotation takes three Last buffers");
   SrBuffers& sb = x->srbuf(idx);
@@ -1245,8 +1282,7 @@ hipError_t batch_enqueue_pipe(loam_ctx* x) {
   T(hipEventRecord(x->ev[0], x->st));
   // (not enqueued ahead: the first pipelined step, or a fed context's step without a feed, which
   // re-runs the set's resident sweeps; Last[ls]'s last reader as for the trailing call below)
-  if (!x->sr_ready || !x->seed_ready)
-    T(enqueue_ahead(x, idx, ls, x->inputs_read_rec[idx] ? x->inputs_read[idx] : nullptr));
+  if (!x->sr_ready || !x->seed_ready) T(enqueue_ahead(x, idx, ls, seed_free_last(x, idx, n)));
   x->sr_ready = x->seed_ready = false;
   x->od_s_last = ls;
   const FeatView fprev = feat_view(sb, 0, 2), fcur = feat_view(sb, 1, 2);
@@ -1271,8 +1307,9 @@ hipError_t batch_enqueue_pipe(loam_ctx* x) {
   // so the next step's frame 1 runs beside this step's frame 2 (no side branches then); 1: one set
   // on st4, frame 2's independent branches on st2
   const bool two = x->tune.pipe_mp_sets == 2;
-  hipStream_t ms = two && idx ? x->st2 : x->st4;
-  MpBuffers& mb = two ? x->mpbuf(idx) : x->mpb;
+  const int m = x->pipe_k++ & 1;  // (the mapping sets alternate by step, whatever the SR slots)
+  hipStream_t ms = two && m ? x->st2 : x->st4;
+  MpBuffers& mb = two ? x->mpbuf(m) : x->mpb;
   T(hipStreamWaitEvent(ms, x->a_start, 0));
   T(hipStreamWaitEvent(ms, x->seed_done, 0));
   SideStream side1;  // (no branches: only the event once Last[ls] is read)
@@ -1295,13 +1332,13 @@ hipError_t batch_enqueue_pipe(loam_ctx* x) {
   T(hipEventRecord(x->mp_done[idx], ms));
   x->mp_done_rec[idx] = true;
   x->b_used = true;
-  x->mp_last = two ? idx : 0;
+  x->mp_last = two ? m : 0;
   T(hipEventRecord(x->ev[3], ms));
   x->srb_last = idx;
   // the next step's scan registration + seed (st3) into Last[lf], which frame 2 of the previous
   // step (SR set nx) read last; a fed context's next loam_batch_feed enqueues them instead, after
   // copying its sweeps into set nx
-  if (!x->fed) T(enqueue_ahead(x, nx, lf, x->inputs_read_rec[nx] ? x->inputs_read[nx] : nullptr));
+  if (!x->fed) T(enqueue_ahead(x, nx, lf, seed_free_last(x, nx, n)));
   x->inputs_read_rec[idx] = true;
   x->od_s = lf;
   x->od_e = ls;
@@ -1318,7 +1355,7 @@ int loam_batch_run(loam_ctx* x) {
   const bool pipe = !pf && !x->tune.graph && x->st2 && x->st3 && x->st4 && x->tune.step_pipe > 0 && x->P >= x->tune.step_pipe;
   const bool ahead = !pf && !x->tune.graph && x->st3 && x->tune.sr_ahead > 0 && x->P >= x->tune.sr_ahead;
   if (pipe || ahead) {
-    const int rc = ensure_second_sets(x);
+    const int rc = ensure_second_sets(x, pipe_slots(x, pipe));
     if (rc) return rc;
   }
   if (pipe) {
@@ -1369,7 +1406,7 @@ int loam_batch_feed(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const lo
   if (!pipe) {  // sequential steps: the next step's sweeps replace the resident ones (as an upload)
     return loam_batch_upload(x, n, prev, cur);
   }
-  int rc = ensure_second_sets(x);
+  int rc = ensure_second_sets(x, pipe_slots(x, true));
   if (rc) return rc;
   const int i = x->sr_idx;  // the set the next step reads
   if (x->sr_ready || x->seed_ready) {
@@ -1401,7 +1438,7 @@ int loam_batch_feed(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const lo
   HIP_TRY(hipMemcpyAsync(sb.raw_n, x->feed_n[i], (size_t)2 * P * sizeof(int), hipMemcpyHostToDevice, x->st3));
   HIP_TRY(hipEventRecord(x->feed_copied[i], x->st3));
   x->feed_rec[i] = true;
-  HIP_TRY(enqueue_ahead(x, i, x->od_s, x->inputs_read_rec[i] ? x->inputs_read[i] : nullptr));
+  HIP_TRY(enqueue_ahead(x, i, x->od_s, seed_free_last(x, i, pipe_slots(x, true))));
   x->fed = true;
   return LOAM_OK;
 }

@@ -2267,9 +2267,11 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   b.tS = next_pow2(b.capS) > 65536 ? 65536 : next_pow2(b.capS);
   A(&b.state_set[0], (size_t)P * kOdStateFloats * sizeof(float));
   A(&b.state_set[1], (size_t)P * kOdStateFloats * sizeof(float));
+  A(&b.state_set[2], (size_t)P * kOdStateFloats * sizeof(float));
   b.state = b.state_set[0];
   A(&b.istate_set[0], (size_t)P * kOdStateInts * sizeof(int));
   A(&b.istate_set[1], (size_t)P * kOdStateInts * sizeof(int));
+  A(&b.istate_set[2], (size_t)P * kOdStateInts * sizeof(int));
   b.istate = b.istate_set[0];
   A(&b.lastC, (size_t)kOdBufs * P * b.capC * sizeof(float4));
   A(&b.lastS, (size_t)kOdBufs * P * b.capS * sizeof(float4));
@@ -2305,9 +2307,9 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
     return A.err;
   }
   if (A.err == hipSuccess) A.err = hipMemset(b.done, 0, (size_t)P * sizeof(int));
-  for (int k = 0; k < 2; ++k)
+  for (int k = 0; k < 3; ++k)
     if (A.err == hipSuccess) A.err = hipMemset(b.state_set[k], 0, (size_t)P * kOdStateFloats * sizeof(float));
-  for (int k = 0; k < 2; ++k)
+  for (int k = 0; k < 3; ++k)
     if (A.err == hipSuccess) A.err = hipMemset(b.istate_set[k], 0, (size_t)P * kOdStateInts * sizeof(int));
   if (A.err == hipSuccess) A.err = hipMemset(b.nlast, 0, (size_t)P * kOdBufs * 2 * sizeof(int));
   if (A.err == hipSuccess) A.err = hipMemset(b.nfullEnd, 0, (size_t)P * kOdBufs * sizeof(int));
@@ -2318,7 +2320,7 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
 }
 
 void od_free(OdBuffers& b) {
-  void* ptrs[] = {b.state_set[0], b.state_set[1], b.istate_set[0], b.istate_set[1], b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
+  void* ptrs[] = {b.state_set[0], b.state_set[1], b.state_set[2], b.istate_set[0], b.istate_set[1], b.istate_set[2], b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
                   b.ind, b.sel, b.q_cf, b.q_ok, b.mom, b.cert, b.qa, b.part, b.done, b.mono, b.rstart, b.fC, b.fS};
   for (void* q : ptrs)

@@ -82,9 +82,9 @@ constexpr int kOdBufs = 3;
 struct OdBuffers {
   int P = 0, capC = 0, capS = 0, cap_q = 0, gq = 0, tC = 0, tS = 0, max_iter = 25;
   float* state = nullptr;   // [P][kOdStateFloats] (one of state_set: batches alternate per step)
-  float* state_set[2] = {nullptr, nullptr};
+  float* state_set[3] = {nullptr, nullptr, nullptr};  // (the step pipeline's buffer slots)
   int* istate = nullptr;    // [P][kOdStateInts] (one of istate_set: batches alternate per step)
-  int* istate_set[2] = {nullptr, nullptr};
+  int* istate_set[3] = {nullptr, nullptr, nullptr};
   float4* lastC = nullptr;  // [kOdBufs][P][capC]
   float4* lastS = nullptr;  // [kOdBufs][P][capS]
   float4* fullEnd = nullptr;  // [kOdBufs][P][capS]
