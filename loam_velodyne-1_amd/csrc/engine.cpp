@@ -756,6 +756,7 @@ int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_i
     xp.put(o.state + kOdImu, mi + 8, 12 * sizeof(float));
     HIP_TRY(xfer_launch(xp, x->st));
   }
+  HIP_TRY(od_wait_hashes(o, x->st));  // (the previous frame's hash build, when deferred)
   if (!x->od_inited) {  // src/laserOdometry.cpp:427-456: Last = raw lessSharp / lessFlat, no L-M
     // :451-452 transformSum[0] += imuPitchStart; transformSum[2] += imuRollStart (from zero)
     const float sum0[3] = {0.0f + imu_in[0], 0.0f, 0.0f + imu_in[2]};
@@ -791,7 +792,11 @@ int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_i
   x->od_frame_count++;
   const bool pub = x->od_frame_count >= (int)x->cfg.skip_frame_num + 1;
   hipLaunchKernelGGL(k_od_end, dim3(64, 1), dim3(256), 0, x->st, o, fv, nxt, 2, pub ? 1 : 0);  // one sweep: a wider grid
-  od_build_hashes(o, nxt, x->st);
+  // the new Last clouds' hash tables are read by the next frame's association only: with
+  // stream_defer they are built on the second stream while this frame's results go out (and the
+  // mapping runs)
+  if (x->tune.stream_defer && x->st2) HIP_TRY(od_build_hashes_deferred(o, nxt, x->st, x->st2));
+  else od_build_hashes(o, nxt, x->st);
   HIP_TRY(hipEventRecord(x->ev[1], x->st));
   HIP_TRY(hipGetLastError());
   x->od_last = nxt;
@@ -886,7 +891,7 @@ int loam_mapping(loam_ctx* x, double stamp, const loam_pose6* odom_sum, const lo
   bool updated = false;
   const int rc = mp_stream_frame(x->mp1, x->st, *odom_sum, *corner_last, *surf_last, *full_end, aft, bef,
                                  registered, &x->stats, g_err, x->pin, x->io(), have_imu ? rp : nullptr, &updated,
-                                 x->st2, x->join, x->tune.mp_defer ? x->st2 : nullptr);
+                                 x->st2, x->join, x->tune.stream_defer ? x->st2 : nullptr);
   if (have_imu && updated) x->mp_imu.front = front;  // the pointer walk happens inside transformUpdate
   x->surround_due = false;
   if (rc == LOAM_OK && ++x->map_frame_count >= 5) {  // :1038-1040
@@ -933,7 +938,7 @@ int loam_chain_sweep(loam_ctx* x, double stamp, loam_cloud_in raw, loam_chain_ou
   loam_cloud_out* reg = out->registered.capacity ? &out->registered : nullptr;
   if (!reg) out->registered.count = 0;
   rc = mp_stream_frame_dev(x->mp1, x->st, out->od_sum, in, nl3, &out->aft, &out->bef, reg, &x->stats, g_err,
-                           x->pin, x->io(), have_imu ? rp : nullptr, &updated, x->tune.mp_defer ? x->st2 : nullptr);
+                           x->pin, x->io(), have_imu ? rp : nullptr, &updated, x->tune.stream_defer ? x->st2 : nullptr);
   if (have_imu && updated) x->mp_imu.front = front;
   x->surround_due = false;
   if (rc == LOAM_OK && ++x->map_frame_count >= 5) {  // :1038-1040

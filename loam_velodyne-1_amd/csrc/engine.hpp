@@ -94,9 +94,12 @@ struct Tuning {
                            // certificate when it still separates every choice from its rivals (exact)
   int od_lm_mom_min = 1;   // with the moments: k_od_lm_mom (an association round's 5 iterations in one
   int od_lm_mom_max = 0;   //   workgroup per problem) for od_lm_mom_min <= P <= od_lm_mom_max
-  int mp_defer = 1;        // streaming mapping frames run the map update (insertion, per-cube VoxelGrid,
-                           // compaction) on the second stream after the L-M: the pose and registered cloud
-                           // are downloaded without waiting for it; the next frame waits for it first
+  int stream_defer = 1;    // streaming frames leave the bookkeeping only the next frame reads to the second
+                           // stream: mapping's map update (insertion, per-cube VoxelGrid, compaction) after
+                           // the L-M, odometry's hash tables of the new Last clouds after TransformToEnd.
+                           // The frame's outputs are downloaded without waiting for it; the next frame waits
+                           // for it first (round 5, config 3 chain: 0.70-0.74 -> 0.62-0.65 ms/sweep with the
+                           // map update)
   int od_moments_min = 64; // for P >= this (and P > od_small_max), k_od_rows keeps each query's
                            // stored rows (Q12) as fp64 moments instead of re-evaluating them every
                            // iteration: O(queries) per iteration, not bit-identical, within 1e-4 of the
@@ -109,7 +112,7 @@ struct Tuning {
   }
   bool set(const char* key, long long v, long long* read = nullptr) {
     struct K { const char* n; int* f; long long lo, hi; };
-    const K ks[] = {{"od_small_max", &od_small_max, 0, 1 << 20}, {"mp_defer", &mp_defer, 0, 1}, {"pipe_sr_sets", &pipe_sr_sets, 2, 3}, {"od_lm_min", &od_lm_min, 1, 1 << 20},
+    const K ks[] = {{"od_small_max", &od_small_max, 0, 1 << 20}, {"stream_defer", &stream_defer, 0, 1}, {"pipe_sr_sets", &pipe_sr_sets, 2, 3}, {"od_lm_min", &od_lm_min, 1, 1 << 20},
                     {"od_lm_max", &od_lm_max, 0, 1 << 20}, {"od_fused_max", &od_fused_max, 0, 1 << 20},
                     {"mp_small_max", &mp_small_max, 0, 1 << 20}, {"mp_fused_max", &mp_fused_max, 0, 1 << 20},
                     {"nn_lanes", &nn_lanes, 1, 4}, {"nn_lanes_maxp", &nn_lanes_maxp, 0, 1 << 20},

@@ -2320,6 +2320,9 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
 }
 
 void od_free(OdBuffers& b) {
+  if (b.hash_pending && b.hash_done) (void)hipEventSynchronize(b.hash_done);
+  if (b.hash_fork) (void)hipEventDestroy(b.hash_fork);
+  if (b.hash_done) (void)hipEventDestroy(b.hash_done);
   void* ptrs[] = {b.state_set[0], b.state_set[1], b.state_set[2], b.istate_set[0], b.istate_set[1], b.istate_set[2], b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
                   b.ind, b.sel, b.q_cf, b.q_ok, b.mom, b.cert, b.qa, b.part, b.done, b.mono, b.rstart, b.fC, b.fS};
@@ -2329,6 +2332,25 @@ void od_free(OdBuffers& b) {
 }
 
 // voxel hashes of Last[buf] (corner and surf), 1 m cells
+hipError_t od_build_hashes_deferred(OdBuffers& b, int buf, hipStream_t st, hipStream_t side) {
+  hipError_t e = hipSuccess;
+  if (!b.hash_fork) e = hipEventCreateWithFlags(&b.hash_fork, hipEventDisableTiming);
+  if (e == hipSuccess && !b.hash_done) e = hipEventCreateWithFlags(&b.hash_done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(b.hash_fork, st);
+  if (e == hipSuccess) e = hipStreamWaitEvent(side, b.hash_fork, 0);
+  if (e != hipSuccess) return e;
+  od_build_hashes(b, buf, side);
+  e = hipEventRecord(b.hash_done, side);
+  if (e == hipSuccess) b.hash_pending = true;
+  return e;
+}
+
+hipError_t od_wait_hashes(OdBuffers& b, hipStream_t st) {
+  if (!b.hash_pending) return hipSuccess;
+  b.hash_pending = false;
+  return hipStreamWaitEvent(st, b.hash_done, 0);
+}
+
 void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st) {
   HashJob jc;
   jc.pts = b.lastC + (size_t)buf * b.P * b.capC;

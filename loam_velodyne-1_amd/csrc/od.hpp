@@ -85,6 +85,10 @@ struct OdBuffers {
   float* state_set[3] = {nullptr, nullptr, nullptr};  // (the step pipeline's buffer slots)
   int* istate = nullptr;    // [P][kOdStateInts] (one of istate_set: batches alternate per step)
   int* istate_set[3] = {nullptr, nullptr, nullptr};
+  // the streaming frame's hash build of the new Last clouds deferred to a side stream (engine
+  // od_frame, tuning stream_defer): recorded there, waited for by the next frame (hash_pending)
+  hipEvent_t hash_fork = nullptr, hash_done = nullptr;
+  bool hash_pending = false;
   float4* lastC = nullptr;  // [kOdBufs][P][capC]
   float4* lastS = nullptr;  // [kOdBufs][P][capS]
   float4* fullEnd = nullptr;  // [kOdBufs][P][capS]
@@ -127,6 +131,9 @@ __global__ void k_od_end(OdBuffers b, FeatView f, int dst, int mode, int do_full
 hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter);  // on failure: freed, b empty
 void od_free(OdBuffers& b);
 void od_build_hashes(const OdBuffers& b, int buf, hipStream_t st);
+// od_build_hashes on `side` after the work enqueued on st so far (b.hash_pending until od_wait_hashes)
+hipError_t od_build_hashes_deferred(OdBuffers& b, int buf, hipStream_t st, hipStream_t side);
+hipError_t od_wait_hashes(OdBuffers& b, hipStream_t st);
 // the laserOdometry L-M loop + pose accumulation for every problem against Last[last_buf]
 // device_fini: the pose accumulation (k_od_fini) on the device; the streaming path does it on the host
 void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t st, Prof* prof = nullptr,
