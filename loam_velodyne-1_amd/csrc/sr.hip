@@ -296,6 +296,14 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_count(SrBuffers b, SrPar
   __shared__ int sh_first, sh_last, sh_F;
   __shared__ float sh_start, sh_end_raw;
   __shared__ int sh_cnt[64];
+  // the tile's points first: their loads are in flight during the sweep-end scans and the start
+  // orientation below
+  float4 q[kRingE];
+#pragma unroll
+  for (int e = 0; e < kRingE; ++e) {
+    const int i = t * kRingTile + e * kSrThreads + tid;
+    q[e] = i < n ? raw[i] : make_float4(0, 0, 0, 0);
+  }
   if (w == 0) {
     int f = -1;
     for (int base = 0; base < n; base += 64) {
@@ -332,12 +340,6 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_count(SrBuffers b, SrPar
     }
     b.sweep_ori[2 * s] = startOri;
     b.sweep_ori[2 * s + 1] = endOri;
-  }
-  float4 q[kRingE];
-#pragma unroll
-  for (int e = 0; e < kRingE; ++e) {
-    const int i = t * kRingTile + e * kSrThreads + tid;
-    q[e] = i < n ? raw[i] : make_float4(0, 0, 0, 0);
   }
   int Floc = 0x7fffffff;
 #pragma unroll
@@ -376,6 +378,23 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_scatter(SrBuffers b, SrP
   if (t >= (nt > 0 ? nt : 1)) return;
   __shared__ int sh_tot[64], sh_pre[64], sh_base[64], sh_F;
   __shared__ int sh_wcnt[64][kSlots];  // per ring: points of each slot, then their exclusive prefix
+  // the tile's ring IDs, points and orientations first: their loads are in flight during the tile
+  // prefix below (a point whose ring ID turns out invalid is loaded for nothing: rare)
+  int sid[kRingE], rank[kRingE];
+  float4 q[kRingE];
+  float ori[kRingE];
+#pragma unroll
+  for (int e = 0; e < kRingE; ++e) {
+    const int i = t * kRingTile + e * kSrThreads + tid;
+    sid[e] = 255;
+    q[e] = make_float4(0, 0, 0, 0);
+    ori[e] = 0.0f;
+    if (i < n) {
+      sid[e] = (int)b.tmp_sid[(size_t)s * b.cap + i];
+      q[e] = b.raw[(size_t)s * b.cap + i];
+      ori[e] = b.tmp_ori[(size_t)s * b.cap + i];
+    }
+  }
   if (tid < R) { sh_tot[tid] = 0; sh_pre[tid] = 0; }
   if (tid == 0) sh_F = 0x7fffffff;
   for (int k = tid; k < 64 * kSlots; k += kSrThreads) (&sh_wcnt[0][0])[k] = 0;
@@ -393,12 +412,6 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_scatter(SrBuffers b, SrP
   F = wave_min_i(F);
   if (lane == 0 && F != 0x7fffffff) atomicMin(&sh_F, F);
   // stable ranks within each (sub-tile, wave) slot by wave ballots
-  int sid[kRingE], rank[kRingE];
-#pragma unroll
-  for (int e = 0; e < kRingE; ++e) {
-    const int i = t * kRingTile + e * kSrThreads + tid;
-    sid[e] = i < n ? (int)b.tmp_sid[(size_t)s * b.cap + i] : 255;
-  }
 #pragma unroll
   for (int e = 0; e < kRingE; ++e) {
     const bool valid = sid[e] != 255;
@@ -438,16 +451,6 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_scatter(SrBuffers b, SrP
   if (nt == 0) return;
   F = sh_F;
   const float startOri = b.sweep_ori[2 * s], endOri = b.sweep_ori[2 * s + 1];
-  float4 q[kRingE];
-  float ori[kRingE];
-#pragma unroll
-  for (int e = 0; e < kRingE; ++e) {
-    const int i = t * kRingTile + e * kSrThreads + tid;
-    if (sid[e] != 255) {
-      q[e] = b.raw[(size_t)s * b.cap + i];
-      ori[e] = b.tmp_ori[(size_t)s * b.cap + i];
-    }
-  }
 #pragma unroll
   for (int e = 0; e < kRingE; ++e) {
     const int i = t * kRingTile + e * kSrThreads + tid;
