@@ -168,10 +168,10 @@ int loam_mapping_surround(loam_ctx *ctx, loam_cloud_out *out, int *published);
  * odometry's published CornerLast / SurfLast / full-end buffers in place.  Same kernels, same values
  * as the three message calls; loam_mapping_surround works after it as after loam_mapping.
  * Returns LOAM_E_NOT_READY inside system_delay.  registered: capacity 0 = not downloaded.
- * (Tuning stream_defer, default on, for this call and the node calls: the bookkeeping only the next
- * frame reads — mapping's map update, odometry's hash tables of the new Last clouds — runs on the
- * context's second stream after the call has its results; the next call waits for it on the device.
- * A map-update capacity error is then reported by the next mapping call.) */
+ * (Tuning stream_defer, default on, for this call: the bookkeeping only the next sweep reads —
+ * mapping's map update, odometry's hash tables of the new Last clouds — runs on the context's second
+ * stream after the call has its results; the next call waits for it on the device.  A map-update
+ * capacity error is then reported by the next call.) */
 typedef struct {
   int32_t published;          /* loam_odometry's LOAM_PUB_* flags for this sweep */
   int32_t mapped;             /* 1 when laserMapping ran on this sweep */

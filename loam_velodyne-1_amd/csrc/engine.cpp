@@ -687,7 +687,7 @@ int sr_frame(loam_ctx* x, double stamp, const loam_cloud_in& raw, loam_features*
 // the published CornerLast / SurfLast / full-cloud counts, for a mapping on the device copies.
 int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu, const loam_cloud_out* late_full,
              loam_pose6* sum_out, loam_cloud_out* corner_last, loam_cloud_out* surf_last, loam_cloud_out* full_end,
-             int* published, int* nl3);
+             int* published, int* nl3, bool defer = false);
 }  // namespace
 
 extern "C" {
@@ -742,7 +742,7 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
 namespace {
 int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_in, const loam_cloud_out* late_full,
              loam_pose6* sum_out, loam_cloud_out* corner_last, loam_cloud_out* surf_last, loam_cloud_out* full_end,
-             int* published, int* nl3) {
+             int* published, int* nl3, bool defer) {
   *published = 0;
   OdBuffers& o = x->od1;
   SrBuffers& fi = x->odin;
@@ -795,7 +795,7 @@ int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_i
   // the new Last clouds' hash tables are read by the next frame's association only: with
   // stream_defer they are built on the second stream while this frame's results go out (and the
   // mapping runs)
-  if (x->tune.stream_defer && x->st2) HIP_TRY(od_build_hashes_deferred(o, nxt, x->st, x->st2));
+  if (defer && x->tune.stream_defer && x->st2) HIP_TRY(od_build_hashes_deferred(o, nxt, x->st, x->st2));
   else od_build_hashes(o, nxt, x->st);
   HIP_TRY(hipEventRecord(x->ev[1], x->st));
   HIP_TRY(hipGetLastError());
@@ -891,7 +891,7 @@ int loam_mapping(loam_ctx* x, double stamp, const loam_pose6* odom_sum, const lo
   bool updated = false;
   const int rc = mp_stream_frame(x->mp1, x->st, *odom_sum, *corner_last, *surf_last, *full_end, aft, bef,
                                  registered, &x->stats, g_err, x->pin, x->io(), have_imu ? rp : nullptr, &updated,
-                                 x->st2, x->join, x->tune.stream_defer ? x->st2 : nullptr);
+                                 x->st2, x->join);
   if (have_imu && updated) x->mp_imu.front = front;  // the pointer walk happens inside transformUpdate
   x->surround_due = false;
   if (rc == LOAM_OK && ++x->map_frame_count >= 5) {  // :1038-1040
@@ -918,7 +918,7 @@ int loam_chain_sweep(loam_ctx* x, double stamp, loam_cloud_in raw, loam_chain_ou
   if (rc) return rc;
   int nl3[3] = {0, 0, 0};
   rc = od_frame(x, feat_view(x->sr1, 0, 1), cnt5, imu12, nullptr, &out->od_sum, nullptr, nullptr, nullptr,
-                &out->published, nl3);
+                &out->published, nl3, /*defer=*/true);
   if (rc) return rc;
   if (out->published != (LOAM_PUB_POSE | LOAM_PUB_CLOUDS | LOAM_PUB_FULL)) return LOAM_OK;
   const OdBuffers& o = x->od1;

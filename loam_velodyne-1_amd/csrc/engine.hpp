@@ -94,12 +94,14 @@ struct Tuning {
                            // certificate when it still separates every choice from its rivals (exact)
   int od_lm_mom_min = 1;   // with the moments: k_od_lm_mom (an association round's 5 iterations in one
   int od_lm_mom_max = 0;   //   workgroup per problem) for od_lm_mom_min <= P <= od_lm_mom_max
-  int stream_defer = 1;    // streaming frames leave the bookkeeping only the next frame reads to the second
+  int stream_defer = 1;    // loam_chain_sweep leaves the bookkeeping only the next sweep reads to the second
                            // stream: mapping's map update (insertion, per-cube VoxelGrid, compaction) after
                            // the L-M, odometry's hash tables of the new Last clouds after TransformToEnd.
-                           // The frame's outputs are downloaded without waiting for it; the next frame waits
+                           // The sweep's outputs are downloaded without waiting for it; the next sweep waits
                            // for it first (round 5, config 3 chain: 0.70-0.74 -> 0.62-0.65 ms/sweep with the
-                           // map update)
+                           // map update).  Not the message calls: their host staging waits on the second
+                           // stream, and a node graph's contexts share the process's hardware queues (the
+                           // three-context pipeline measured 0.45-0.51 -> 0.77-1.13 ms/sweep with it)
   int od_moments_min = 64; // for P >= this (and P > od_small_max), k_od_rows keeps each query's
                            // stored rows (Q12) as fp64 moments instead of re-evaluating them every
                            // iteration: O(queries) per iteration, not bit-identical, within 1e-4 of the
