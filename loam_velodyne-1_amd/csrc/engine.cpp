@@ -229,7 +229,17 @@ struct loam_ctx {
     graph_exec = nullptr;
     graph = nullptr;
     graph_P = 0;
+    for (int i = 0; i < 2; ++i) {
+      if (od_graph_exec[i]) (void)hipGraphExecDestroy(od_graph_exec[i]);
+      if (od_graph[i]) (void)hipGraphDestroy(od_graph[i]);
+      od_graph_exec[i] = nullptr;
+      od_graph[i] = nullptr;
+    }
   }
+  // tune.od_graph: the streaming odometry's L-M launches (od_solve) captured once per Last-buffer
+  // parity and replayed (one host call instead of ~35 launches per frame)
+  hipGraph_t od_graph[2] = {nullptr, nullptr};
+  hipGraphExec_t od_graph_exec[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -570,7 +580,13 @@ namespace {
 // The laserCloudHandler body on ctx->sr1.  out == nullptr (the device-resident chain): the topics
 // stay in sr1 for the odometry that follows; cnt5 (sharp, lessSharp, flat, lessFlat, full counts)
 // and imu12 (/imu_trans) are returned either way.
-int sr_frame(loam_ctx* x, double stamp, const loam_cloud_in& raw, loam_features* out, int* cnt5, float* imu12) {
+// pending (the chain, optional): when the sweep needs no host work between the scan registration
+// and the odometry (no IMU queue, no host outputs), the call returns once the kernels and the
+// counts' download are enqueued, *pending = true: cnt5 are then read after the odometry's sync
+// (sr_collect), and an error the scan registration reports is returned there (the odometry
+// kernels it fed are undone: od_frame)
+int sr_frame(loam_ctx* x, double stamp, const loam_cloud_in& raw, loam_features* out, int* cnt5, float* imu12,
+             bool* pending = nullptr) {
   if (!x->sr_inited) {  // src/scanRegistration.cpp:213-219 (Q1)
     x->sr_init_count++;
     if (x->sr_init_count >= (int)x->cfg.system_delay) x->sr_inited = true;
@@ -633,6 +649,14 @@ int sr_frame(loam_ctx* x, double stamp, const loam_cloud_in& raw, loam_features*
     HIP_TRY(xfer_launch(xg, x->st));
   }
   HIP_TRY(hipGetLastError());
+  if (pending && !out && q->last < 0) {  // (the chain: no sync here, sr_collect after the odometry)
+    const float it[12] = {q->pitchStart, q->yawStart, q->rollStart, q->pitchCur, q->yawCur, q->rollCur,
+                          q->shiftFSX,   q->shiftFSY, q->shiftFSZ,  q->veloFSX,  q->veloFSY, q->veloFSZ};
+    std::memcpy(imu12, it, sizeof(it));
+    for (int k = 0; k < 5; ++k) cnt5[k] = 0;
+    *pending = true;
+    return LOAM_OK;
+  }
   HIP_TRY(hipStreamSynchronize(x->st));
   int cnt[4] = {mi[1], mi[2], mi[3], mi[4]};
   const int nfull = mi[5];
@@ -680,6 +704,15 @@ int sr_frame(loam_ctx* x, double stamp, const loam_cloud_in& raw, loam_features*
   return e ? LOAM_E_CAPACITY : LOAM_OK;
 }
 
+// a pending scan registration's results (sr_frame's pending mode), once the stream has been
+// synchronised past them: its error code; cnt5 filled
+int sr_collect(loam_ctx* x, int* cnt5) {
+  const int* mi = (const int*)(x->xb.h + kXferSr) - 1;
+  for (int k = 0; k < 4; ++k) cnt5[k] = mi[1 + k];
+  cnt5[4] = mi[5];
+  return sr_errors(mi[6]);
+}
+
 // ------------------------------------------------------------------ laserOdometry
 // The laserOdometry loop body on the features fv (cnt: sharp, lessSharp, flat, lessFlat, full
 // counts; imu: /imu_trans).  late_full: the full cloud is still on the host (message mode) and is
@@ -687,7 +720,7 @@ int sr_frame(loam_ctx* x, double stamp, const loam_cloud_in& raw, loam_features*
 // the published CornerLast / SurfLast / full-cloud counts, for a mapping on the device copies.
 int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu, const loam_cloud_out* late_full,
              loam_pose6* sum_out, loam_cloud_out* corner_last, loam_cloud_out* surf_last, loam_cloud_out* full_end,
-             int* published, int* nl3, bool defer = false);
+             int* published, int* nl3, bool defer = false, bool sr_pending = false);
 }  // namespace
 
 extern "C" {
@@ -742,7 +775,7 @@ int loam_odometry(loam_ctx* x, double stamp, const loam_features* in, loam_pose6
 namespace {
 int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_in, const loam_cloud_out* late_full,
              loam_pose6* sum_out, loam_cloud_out* corner_last, loam_cloud_out* surf_last, loam_cloud_out* full_end,
-             int* published, int* nl3, bool defer) {
+             int* published, int* nl3, bool defer, bool sr_pending) {
   *published = 0;
   OdBuffers& o = x->od1;
   SrBuffers& fi = x->odin;
@@ -783,12 +816,37 @@ int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_i
   HIP_TRY(hipEventRecord(x->ev[0], x->st));
   // the pose accumulation (:830-856) runs on the host after the download: one scalar chain of
   // double trig, which a one-thread kernel took ~16 us for (the batch path keeps it on the device)
-  od_solve(o, fv, cur, x->st, nullptr, /*device_fini=*/false);
+  // sr_pending: k_od_begin keeps a copy of the state to undo this frame with (the third state slot,
+  // unused by the one-problem context)
+  OdBuffers ob = o;
+  const bool graph = x->tune.od_graph && defer;  // (the chain: fv is the context's own sr1)
+  if (sr_pending || graph) {  // (a graph bakes the copy in: every replayed frame keeps it)
+    ob.bk_state = o.state_set[2];
+    ob.bk_istate = o.istate_set[2];
+  }
+  if (graph) {
+    if (!x->od_graph_exec[cur]) {
+      HIP_TRY(hipStreamBeginCapture(x->st, hipStreamCaptureModeThreadLocal));
+      od_solve(ob, fv, cur, x->st, nullptr, /*device_fini=*/false);
+      hipGraph_t g = nullptr;
+      const hipError_t ce = hipGetLastError(), ee = hipStreamEndCapture(x->st, &g);
+      if (ce != hipSuccess || ee != hipSuccess) {
+        if (g) (void)hipGraphDestroy(g);
+        return fail(LOAM_E_HIP, std::string("odometry graph capture: ") + hipGetErrorString(ce != hipSuccess ? ce : ee));
+      }
+      x->od_graph[cur] = g;
+      HIP_TRY(hipGraphInstantiate(&x->od_graph_exec[cur], g, nullptr, nullptr, 0));
+    }
+    HIP_TRY(hipGraphLaunch(x->od_graph_exec[cur], x->st));
+  } else {
+    od_solve(ob, fv, cur, x->st, nullptr, /*device_fini=*/false);
+  }
   if (late) {  // late_full: host copy + DMA on the second stream, overlapping the L-M above
     HIP_TRY(x->pin.up(x->st2, fi.full, late_full->pts, (size_t)late_full->count));
     HIP_TRY(hipEventRecord(x->join, x->st2));
     HIP_TRY(hipStreamWaitEvent(x->st, x->join, 0));
   }
+  const int frame_count0 = x->od_frame_count;
   x->od_frame_count++;
   const bool pub = x->od_frame_count >= (int)x->cfg.skip_frame_num + 1;
   hipLaunchKernelGGL(k_od_end, dim3(64, 1), dim3(256), 0, x->st, o, fv, nxt, 2, pub ? 1 : 0);  // one sweep: a wider grid
@@ -815,6 +873,19 @@ int od_frame(loam_ctx* x, const FeatView& fv, const int* cnt, const float* imu_i
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(x->st));
+  int cnt_l[5];
+  if (sr_pending) {  // the scan registration's result is known now
+    const int src = sr_collect(x, cnt_l);
+    cnt = cnt_l;
+    if (src) {  // undo this frame: the state from k_od_begin's copy, the host counters (Last[nxt] unused)
+      HIP_TRY(hipMemcpyAsync(o.state, o.state_set[2], kOdStateFloats * sizeof(float), hipMemcpyDeviceToDevice, x->st));
+      HIP_TRY(hipMemcpyAsync(o.istate, o.istate_set[2], kOdStateInts * sizeof(int), hipMemcpyDeviceToDevice, x->st));
+      HIP_TRY(hipStreamSynchronize(x->st));
+      x->od_last = cur;
+      x->od_frame_count = frame_count0;
+      return src;
+    }
+  }
   float* st = (float*)(mi + 32);                  // kOdStateFloats
   int* ist = mi + 32 + kOdStateFloats;             // kOdStateInts
   int* nl = ist + kOdStateInts;                    // 4
@@ -914,11 +985,14 @@ int loam_chain_sweep(loam_ctx* x, double stamp, loam_cloud_in raw, loam_chain_ou
   out->mapped = 0;
   int cnt5[5];
   float imu12[12];
-  int rc = sr_frame(x, stamp, raw, nullptr, cnt5, imu12);
+  // (stream_defer, after the odometry's first frame: the odometry is enqueued behind the scan
+  // registration without a host round trip; sr_frame's pending mode)
+  bool sr_pending = false;
+  int rc = sr_frame(x, stamp, raw, nullptr, cnt5, imu12, x->od_inited && x->tune.stream_defer ? &sr_pending : nullptr);
   if (rc) return rc;
   int nl3[3] = {0, 0, 0};
   rc = od_frame(x, feat_view(x->sr1, 0, 1), cnt5, imu12, nullptr, &out->od_sum, nullptr, nullptr, nullptr,
-                &out->published, nl3, /*defer=*/true);
+                &out->published, nl3, /*defer=*/true, sr_pending);
   if (rc) return rc;
   if (out->published != (LOAM_PUB_POSE | LOAM_PUB_CLOUDS | LOAM_PUB_FULL)) return LOAM_OK;
   const OdBuffers& o = x->od1;

@@ -72,6 +72,7 @@ struct Tuning {
   int pipe_mp_sets = 2;    // the step pipeline's mapping: 1 one set (st4, side branches on st2), 2 two sets
                            // alternating on st4 / st2 (the next frame 1 beside this frame 2; round 4:
                            // 128 problems 2.37 -> 2.20 ms/step, 1024: 14.23 -> 14.03)
+  int od_graph = 1;        // loam_chain_sweep replays the odometry's L-M launches as a captured HIP graph
   int pipe_sr_sets = 3;    // the step pipeline's SR sets (and odometry state sets): with 2, a step's scan
                            // registration waits for the mapping of the step two back, so SR, seed,
                            // odometry and mapping frame 2 of one step form a cycle over two steps; with 3
@@ -114,7 +115,7 @@ struct Tuning {
   }
   bool set(const char* key, long long v, long long* read = nullptr) {
     struct K { const char* n; int* f; long long lo, hi; };
-    const K ks[] = {{"od_small_max", &od_small_max, 0, 1 << 20}, {"stream_defer", &stream_defer, 0, 1}, {"pipe_sr_sets", &pipe_sr_sets, 2, 3}, {"od_lm_min", &od_lm_min, 1, 1 << 20},
+    const K ks[] = {{"od_small_max", &od_small_max, 0, 1 << 20}, {"stream_defer", &stream_defer, 0, 1}, {"pipe_sr_sets", &pipe_sr_sets, 2, 3}, {"od_graph", &od_graph, 0, 1}, {"od_lm_min", &od_lm_min, 1, 1 << 20},
                     {"od_lm_max", &od_lm_max, 0, 1 << 20}, {"od_fused_max", &od_fused_max, 0, 1 << 20},
                     {"mp_small_max", &mp_small_max, 0, 1 << 20}, {"mp_fused_max", &mp_fused_max, 0, 1 << 20},
                     {"nn_lanes", &nn_lanes, 1, 4}, {"nn_lanes_maxp", &nn_lanes_maxp, 0, 1 << 20},

@@ -1020,6 +1020,11 @@ LOAM_D void wave_assoc_surf(const float4* SL, const float4* ch, int fwd_end, uin
 
 __global__ void k_od_begin(OdBuffers b, FeatView f) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b.bk_state && blockIdx.x == 0) {  // (one problem: the whole state before this frame touches it)
+    for (int k = threadIdx.x; k < kOdStateFloats; k += blockDim.x) b.bk_state[k] = b.state[k];
+    for (int k = threadIdx.x; k < kOdStateInts; k += blockDim.x) b.bk_istate[k] = b.istate[k];
+    __syncthreads();
+  }
   if (p >= b.P) return;
   float* st = b.state + (size_t)p * kOdStateFloats;
   int* ist = b.istate + (size_t)p * kOdStateInts;

@@ -89,6 +89,11 @@ struct OdBuffers {
   // od_frame, tuning stream_defer): recorded there, waited for by the next frame (hash_pending)
   hipEvent_t hash_fork = nullptr, hash_done = nullptr;
   bool hash_pending = false;
+  // (one problem, optional) k_od_begin first copies the state / istate here: the chain's odometry
+  // may run before its scan registration's result is known, and is undone from the copy when that
+  // reports an error (engine od_frame)
+  float* bk_state = nullptr;
+  int* bk_istate = nullptr;
   float4* lastC = nullptr;  // [kOdBufs][P][capC]
   float4* lastS = nullptr;  // [kOdBufs][P][capS]
   float4* fullEnd = nullptr;  // [kOdBufs][P][capS]

@@ -222,3 +222,33 @@ def test_node_chain_through_messages(loam, oc, sg):
     assert nmap >= 10
     # the chain is not the identity: the fused pose moves with the trajectory
     assert np.abs(rg[-1]["integrated"][3:]).max() > 0.5
+
+
+def test_device_chain_rejected_sweep_is_undone(loam, sg):
+    """loam_chain_sweep enqueues the odometry behind the scan registration without waiting for its
+    result (tuning stream_defer): a sweep the scan registration rejects (every point NaN: "no finite
+    point") in the middle of the stream is reported exactly as the synchronous path reports it, and
+    leaves no trace — every later pose equals the run that never saw it, bit for bit"""
+    sweeps = sg.stream_sweeps(40, 1)
+    bad = np.full_like(sweeps[0], np.nan)
+
+    def run(defer, insert):
+        e = loam.Engine(loam.default_config(system_delay=1))
+        e.set_tuning(stream_defer=defer)
+        seq = list(sweeps[:25]) + ([bad] if insert else []) + list(sweeps[25:])
+        out = []
+        for k, sw in enumerate(seq):
+            try:
+                rc, pub, od, aft, bef, _ = e.chain_sweep(sw, stamp=0.1 * k)
+            except loam.LoamError as ex:
+                out.append(("error", ex.args[0]))
+                continue
+            out.append((rc, pub, None if od is None else od.tobytes(), None if aft is None else aft.tobytes()))
+        e.close()
+        return out
+
+    a = run(1, True)
+    assert a == run(0, True)
+    errors = [r for r in a if r[0] == "error"]
+    assert len(errors) == 1 and a[25][0] == "error"
+    assert a[:25] + a[26:] == run(1, False)
