@@ -47,7 +47,8 @@ struct Tuning {
                            // with the register reduce-scatter, 15.31 -> 15.23 with the LDS row sums)
   int nn_lanes = 1;        // lanes per query of the batch 5-NN (1, 2, 4) ...
   int nn_lanes_maxp = 256; //   for P <= this
-  int od_assoc_wg = 64;    // k_od_assoc query waves (workgroups) per problem (batches, P >= 64)
+  int od_assoc_wg = 0;     // k_od_assoc query waves (workgroups) per problem (batches, P >= 64; 0: the query
+                           // capacity / 9, i.e. 64 for VLP-16, 256 for HDL-64E)
   int nn_lds = 0;          // batch 5-NN with the workgroup's map cells staged in LDS (k_mp_nn_lds)
   int od_rows_deep_max = 0;  // k_od_rows with 8 (not 2) stored rows' loads in flight for P <= this
   int nn_wg = 0;           // k_mp_nn workgroups per problem (0: one pass over a VLP-16 stack)
@@ -119,7 +120,7 @@ struct Tuning {
                     {"od_lm_max", &od_lm_max, 0, 1 << 20}, {"od_fused_max", &od_fused_max, 0, 1 << 20},
                     {"mp_small_max", &mp_small_max, 0, 1 << 20}, {"mp_fused_max", &mp_fused_max, 0, 1 << 20},
                     {"nn_lanes", &nn_lanes, 1, 4}, {"nn_lanes_maxp", &nn_lanes_maxp, 0, 1 << 20},
-                    {"od_assoc_wg", &od_assoc_wg, 1, 1024}, {"nn_lds", &nn_lds, 0, 1},
+                    {"od_assoc_wg", &od_assoc_wg, 0, 1024}, {"nn_lds", &nn_lds, 0, 1},
                     {"od_rows_deep_max", &od_rows_deep_max, 0, 1 << 20}, {"nn_wg", &nn_wg, 0, 4096},
                     {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20},
                     {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20},

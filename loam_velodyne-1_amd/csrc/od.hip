@@ -2424,7 +2424,11 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
     if (it % 5 == 0) {  // Q10
       // one wave per query when the batch is small (streaming: TransformToStart in the wave), 64
       // waves per problem otherwise (the queries transformed by k_od_sel first)
-      const int ga = P >= 64 ? tn.od_assoc_wg : (b.cap_q + kAsWaves - 1) / kAsWaves;  // (8 / 32 / 64 measured slower)
+      // (batches: about nine query capacity per wave — 64 waves per VLP-16 problem, 256 per HDL-64E
+      // one; round 5, config 5: 64 -> 256 waves took k_od_assoc 4.09 -> 2.48 ms/step, while at
+      // VLP-16 batches 32 / 128 / 256 measured equal / slower)
+      const int ga = P >= 64 ? (tn.od_assoc_wg > 0 ? tn.od_assoc_wg : std::max(16, std::min(1024, b.cap_q / 9)))
+                             : (b.cap_q + kAsWaves - 1) / kAsWaves;
       const bool half = P >= tn.od_assoc_half_min;
       if (P >= tn.od_sel_min) {
         hipLaunchKernelGGL(k_od_sel, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f);
