@@ -1179,10 +1179,9 @@ constexpr int kPickWaves = 1;
 constexpr int kPickWpe = 4;  // <= 128 VGPRs: four waves per SIMD (the LDS allows four workgroups per CU)
 constexpr int kPickSegRegs = (kPickCap / 6 + 2 + 63) / 64;  // a segment of a <= kPickCap ring, per lane
 
-struct PickWave {
+struct PickWave {  // (no candidate list: the register path's picks are wave arg-maxes)
   uint8_t pk[kPickCap + 16];
   int8_t lab[kPickCap + 16];
-  uint64_t list[512];
   int picks[kSharpPerRing + kLessSharpPerRing + kFlatPerRing];
   int nsharp, nlsharp, nflat;
 };
@@ -1281,7 +1280,7 @@ __global__ __launch_bounds__(64 * kPickWaves) __attribute__((amdgpu_waves_per_eu
     };
     if (s1 - 1 < s0) pre();
     if (s1 - 1 >= s0) {
-    select_segment_fast<kPickSegRegs>(n, lo, s0 - lo, s1 - 1 - lo, cv, P.list, P.pk, P.lab, wlo, P.picks, P.nsharp,
+    select_segment_fast<kPickSegRegs>(n, lo, s0 - lo, s1 - 1 - lo, cv, nullptr, P.pk, P.lab, wlo, P.picks, P.nsharp,
                                       P.nlsharp, P.nflat, cra, pre);
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
