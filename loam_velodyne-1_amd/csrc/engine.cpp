@@ -177,8 +177,10 @@ struct loam_ctx {
   // reads (copied on st3 behind that set's previous reader, then its scan registration + seed
   // there); a fed context enqueues nothing ahead at the end of a run (the feed does)
   bool fed = false;
-  float4* feed_pin[3] = {nullptr, nullptr, nullptr};  // pinned staging per SR set, [2P][cap]
-  int* feed_n[3] = {nullptr, nullptr, nullptr};       // pinned sweep sizes per SR set, [2P]
+  float4* feed_pin[3] = {nullptr, nullptr, nullptr};  // pinned staging per SR set: the sweeps back to back
+  int* feed_n[3] = {nullptr, nullptr, nullptr};       // pinned sweep sizes per SR set, [2P], then offsets [2P]
+  float4* feed_dev = nullptr;                         // device staging of the packed sweeps, [2P][cap] points
+  int* feed_doff = nullptr;                           // device sizes + offsets, [4P]
   hipEvent_t feed_copied[3] = {nullptr, nullptr, nullptr};
   bool feed_rec[3] = {false, false, false};
   void free_feed() {
@@ -190,6 +192,10 @@ struct loam_ctx {
       feed_n[i] = nullptr;
       feed_rec[i] = false;
     }
+    if (feed_dev) (void)hipFree(feed_dev);
+    if (feed_doff) (void)hipFree(feed_doff);
+    feed_dev = nullptr;
+    feed_doff = nullptr;
   }
   void reset_ahead() {    // (after draining st3 / st4)
     sr_ready = false;
@@ -1134,6 +1140,23 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
 namespace {
 // sweeps [s0, s1) of a batch (sweep 2i = prev[i], 2i + 1 = cur[i]) packed into dst at stride cap,
 // their sizes into n; several host threads for a large batch (the pack is a memory copy per sweep)
+// sweeps [s0, s1) packed back to back (sweep s at off[s]) into dst, on up to eight threads
+void pack_tight(const loam_cloud_in* prev, const loam_cloud_in* cur, size_t s0, size_t s1, const int* off, float4* dst) {
+  auto run = [&](size_t a, size_t b) {
+    for (size_t s = a; s < b; ++s) {
+      const loam_cloud_in& c = (s & 1) ? cur[s / 2] : prev[s / 2];
+      pack(c, dst + off[s], 0, c.count);
+    }
+  };
+  const size_t S = s1 - s0;
+  const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  const size_t nt = S >= 64 ? hw : 1;
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; ++t) th.emplace_back(run, s0 + S * t / nt, s0 + S * (t + 1) / nt);
+  run(s0, s0 + S / nt);
+  for (auto& t : th) t.join();
+}
+
 void pack_batch(const loam_cloud_in* prev, const loam_cloud_in* cur, uint32_t nprob, int cap, float4* dst, int* n) {
   const size_t S = 2 * (size_t)nprob;
   auto run = [&](size_t s0, size_t s1) {
@@ -1497,24 +1520,42 @@ int loam_batch_feed(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const lo
   const size_t per = (size_t)2 * P * x->cap;
   if (!x->feed_pin[i]) {
     HIP_TRY(hipHostMalloc((void**)&x->feed_pin[i], per * sizeof(float4), hipHostMallocDefault));
-    HIP_TRY(hipHostMalloc((void**)&x->feed_n[i], (size_t)2 * P * sizeof(int), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&x->feed_n[i], (size_t)4 * P * sizeof(int), hipHostMallocDefault));
+  }
+  if (!x->feed_dev) {
+    HIP_TRY(hipMalloc((void**)&x->feed_dev, per * sizeof(float4)));
+    HIP_TRY(hipMalloc((void**)&x->feed_doff, (size_t)4 * P * sizeof(int)));
   }
   if (x->feed_rec[i]) HIP_TRY(hipEventSynchronize(x->feed_copied[i]));  // (the staging's last copy is out)
   SrBuffers& sb = x->srbuf(i);
   // behind the set's last reader (the step that used it: its mapping, after its scan registration)
   if (x->mp_done_rec[i]) HIP_TRY(hipStreamWaitEvent(x->st3, x->mp_done[i], 0));
-  // packed in chunks of problems, each chunk's copies enqueued before the next is packed, so the
-  // host packing overlaps the DMA of the chunk before
-  constexpr uint32_t kFeedChunk = 64;
-  for (uint32_t c0 = 0; c0 < n; c0 += kFeedChunk) {
-    const uint32_t nc = std::min(kFeedChunk, n - c0);
-    pack_batch(prev + c0, cur + c0, nc, x->cap, x->feed_pin[i] + (size_t)2 * c0 * x->cap, x->feed_n[i] + 2 * c0);
-    for (uint32_t s = 2 * c0; s < 2 * (c0 + nc); ++s)
-      if (x->feed_n[i][s] > 0)
-        HIP_TRY(hipMemcpyAsync(sb.raw + (size_t)s * x->cap, x->feed_pin[i] + (size_t)s * x->cap,
-                               (size_t)x->feed_n[i][s] * sizeof(float4), hipMemcpyHostToDevice, x->st3));
+  // the sweeps packed back to back in chunks, each chunk one copy into the device staging enqueued
+  // before the next is packed (the host packing overlaps the DMA of the chunk before); then one
+  // kernel puts every sweep at its stride in the set's raw array
+  const size_t S = (size_t)2 * P;
+  int* nn = x->feed_n[i];
+  int* off = nn + S;
+  {
+    size_t run = 0;
+    for (size_t s = 0; s < S; ++s) {
+      const loam_cloud_in& c = (s & 1) ? cur[s / 2] : prev[s / 2];
+      nn[s] = (int)c.count;
+      off[s] = (int)run;
+      run += c.count;
+    }
   }
-  HIP_TRY(hipMemcpyAsync(sb.raw_n, x->feed_n[i], (size_t)2 * P * sizeof(int), hipMemcpyHostToDevice, x->st3));
+  constexpr size_t kFeedChunk = 128;  // sweeps
+  for (size_t s0 = 0; s0 < S; s0 += kFeedChunk) {
+    const size_t s1 = std::min(S, s0 + kFeedChunk);
+    pack_tight(prev, cur, s0, s1, off, x->feed_pin[i]);
+    const size_t a = (size_t)off[s0], b = (size_t)off[s1 - 1] + (size_t)nn[s1 - 1];
+    if (b > a)
+      HIP_TRY(hipMemcpyAsync(x->feed_dev + a, x->feed_pin[i] + a, (b - a) * sizeof(float4), hipMemcpyHostToDevice, x->st3));
+  }
+  HIP_TRY(hipMemcpyAsync(x->feed_doff, nn, 2 * S * sizeof(int), hipMemcpyHostToDevice, x->st3));
+  HIP_TRY(sr_scatter_packed(x->feed_dev, x->feed_doff + S, x->feed_doff, sb.raw, x->cap, (int)S, x->st3));
+  HIP_TRY(hipMemcpyAsync(sb.raw_n, x->feed_doff, S * sizeof(int), hipMemcpyDeviceToDevice, x->st3));
   HIP_TRY(hipEventRecord(x->feed_copied[i], x->st3));
   x->feed_rec[i] = true;
   HIP_TRY(enqueue_ahead(x, i, x->od_s, seed_free_last(x, i, pipe_slots(x, true))));

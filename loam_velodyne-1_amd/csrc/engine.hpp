@@ -290,6 +290,10 @@ struct Staging {
 void set_last_error(const std::string& msg);
 
 hipError_t sr_alloc(SrBuffers& b, int S, int cap, int R);  // on failure: freed, b empty
+// S sweeps packed back to back in src (sweep s at off[s], n[s] points) into raw at stride cap
+// (loam_batch_feed: one host-to-device copy per chunk of sweeps instead of one per sweep)
+hipError_t sr_scatter_packed(const float4* src, const int* off, const int* n, float4* raw, int cap, int S,
+                             hipStream_t st);
 void sr_free(SrBuffers& b);
 // runs the whole scan registration for sweeps [0, S) already in b.raw / b.raw_n
 // sorted (optional): recorded once the ring sort has written the full cloud (the later kernels

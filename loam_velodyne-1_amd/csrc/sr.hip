@@ -1429,6 +1429,20 @@ __global__ __launch_bounds__(256) void k_sr_compact(SrBuffers b, SrParams p) {
 
 #define HIPCHK(x) (void)(x)
 
+__global__ __launch_bounds__(256) void k_sr_scatter_packed(const float4* src, const int* off, const int* n, float4* raw,
+                                                         int cap) {
+  const int s = blockIdx.y, m = n[s], o = off[s];
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < m; t += gridDim.x * 256) raw[(size_t)s * cap + t] = src[(size_t)o + t];
+}
+
+hipError_t sr_scatter_packed(const float4* src, const int* off, const int* n, float4* raw, int cap, int S,
+                             hipStream_t st) {
+  if (S <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sr_scatter_packed, dim3(std::max(1, std::min(64, (cap + 255) / 256)), S), dim3(256), 0, st, src,
+                     off, n, raw, cap);
+  return hipGetLastError();
+}
+
 hipError_t sr_alloc(SrBuffers& b, int S, int cap, int R) {
   DevAlloc A;
   b.S = S; b.cap = cap; b.R = R;
