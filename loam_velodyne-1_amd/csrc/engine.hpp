@@ -156,6 +156,7 @@ struct SrBuffers {
   uint8_t* tmp_sid = nullptr;
   int* tilecnt = nullptr;    // [S][ntiles][R]
   int* tileF = nullptr;      // [S][ntiles] first halfPassed flip index of each tile (tile-parallel ring sort)
+  int* ring_sync = nullptr;  // the fused ring sort's tile ticket
   float* sweep_ori = nullptr;  // [S][2] startOri, endOri
   float4* full = nullptr;    // ring-sorted cloud (camera frame, intensity = ring + 0.1 relTime)
   int* n_full = nullptr;

@@ -463,6 +463,176 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_scatter(SrBuffers b, SrP
   }
 }
 
+// The ring count and scatter in one launch, each raw point read once and held in registers from
+// its ring ID to its store (no tmp_ori / tmp_sid round trip, no second raw read).  A tile counts
+// its rings and its first flip, publishes them (tilecnt / tileF, [S][rtiles] rows here), ranks its
+// points by wave ballots while the sweep's other tiles count, waits for all of them, and
+// scatters.  Tiles take tickets in launch order (ring_sync[0]) and a sweep's tiles hold
+// consecutive tickets, so every tile a waiting tile needs has started: only the last sweep under
+// way can still be short of tiles, and the other resident tiles finish and free their slots.
+#ifndef LOAM_SR_RING_FUSED
+#define LOAM_SR_RING_FUSED 1
+#endif
+constexpr bool kSrRingFused = LOAM_SR_RING_FUSED;
+__global__ __launch_bounds__(kSrThreads) void k_sr_ring_fused(SrBuffers b, SrParams p, int rtiles) {
+  constexpr int kW = kSrThreads / 64, kSlots = kRingE * kW;
+  static_assert(kSlots <= 64 && (kSlots & (kSlots - 1)) == 0, "slot scan width");
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  __shared__ int sh_ticket, sh_first, sh_last, sh_F;
+  __shared__ float sh_start, sh_end_raw;
+  __shared__ int sh_cnt[64], sh_tot[64], sh_pre[64], sh_base[64];
+  __shared__ int sh_wcnt[64][kSlots];
+  if (tid == 0) sh_ticket = atomicAdd(&b.ring_sync[0], 1);
+  __syncthreads();
+  const int s = sh_ticket / rtiles, t = sh_ticket % rtiles;
+  const int n = b.raw_n[s], R = p.R, nt = (n + kRingTile - 1) / kRingTile;
+  if (n <= 0) {
+    if (t == 0 && tid == 0) {
+      b.n_full[s] = 0;
+      b.err[s] |= ERR_EMPTY;
+    }
+    return;
+  }
+  if (t >= nt) return;
+  const float4* raw = b.raw + (size_t)s * b.cap;
+  float4 q[kRingE];
+#pragma unroll
+  for (int e = 0; e < kRingE; ++e) {
+    const int i = t * kRingTile + e * kSrThreads + tid;
+    q[e] = i < n ? raw[i] : make_float4(0, 0, 0, 0);
+  }
+  if (w == 0) {  // :230-238's first and last finite points, scanned from either end
+    int f = -1;
+    for (int base = 0; base < n; base += 64) {
+      const int i = base + lane;
+      const uint64_t m = __ballot(i < n && finite3(raw[i]));
+      if (m) { f = base + __ffsll((unsigned long long)m) - 1; break; }
+    }
+    if (lane == 0) sh_first = f;
+  } else if (w == 1) {
+    int l = -1;
+    for (int base = n - 1; base >= 0; base -= 64) {
+      const int i = base - lane;
+      const uint64_t m = __ballot(i >= 0 && finite3(raw[i]));
+      if (m) { l = base - (__ffsll((unsigned long long)m) - 1); break; }
+    }
+    if (lane == 0) sh_last = l;
+  }
+  if (tid < R) sh_cnt[tid] = 0;
+  if (tid == 0) sh_F = 0x7fffffff;
+  for (int k = tid; k < 64 * kSlots; k += kSrThreads) (&sh_wcnt[0][0])[k] = 0;
+  __syncthreads();
+  if (tid == 0) sh_start = sh_last >= 0 ? -atan2f_fdlibm(raw[sh_first].y, raw[sh_first].x) : 0.0f;
+  if (tid == 64 && sh_last >= 0) sh_end_raw = -atan2f_fdlibm(raw[sh_last].y, raw[sh_last].x);
+  __syncthreads();
+  const float startOri = sh_start;
+  float endOri = 0.0f;
+  if (sh_last >= 0) {
+    endOri = (float)(D(sh_end_raw) + 2 * M_PI);
+    if (D(endOri - startOri) > 3 * M_PI) endOri = (float)(D(endOri) - 2 * M_PI);
+    else if (D(endOri - startOri) < M_PI) endOri = (float)(D(endOri) + 2 * M_PI);
+  }
+  if (tid == 0 && t == 0) {
+    if (sh_last < 0) b.err[s] |= ERR_EMPTY;
+    b.sweep_ori[2 * s] = startOri;
+    b.sweep_ori[2 * s + 1] = endOri;
+  }
+  int sid[kRingE], rank[kRingE];
+  float ori[kRingE];
+  int Floc = 0x7fffffff;
+#pragma unroll
+  for (int e = 0; e < kRingE; ++e) {
+    const int i = t * kRingTile + e * kSrThreads + tid;
+    sid[e] = 255;
+    ori[e] = 0.0f;
+    if (i < n && finite3(q[e])) {
+      const float px = q[e].y, py = q[e].z, pz = q[e].x;
+      const int scanID = ring_of(p, px, py, pz);
+      if (scanID >= 0 && scanID <= R - 1) {
+        sid[e] = scanID;
+        ori[e] = -atan2f_fdlibm(px, pz);
+        if (D(ori_first(ori[e], startOri) - startOri) > M_PI) Floc = min(Floc, i);
+        atomicAdd(&sh_cnt[scanID], 1);
+      }
+    }
+  }
+  Floc = wave_min_i(Floc);
+  if (lane == 0 && Floc != 0x7fffffff) atomicMin(&sh_F, Floc);
+  __syncthreads();
+  // published with coherent single-word stores: a reader waits on each word itself (the launch
+  // presets them to -1), so no fence orders them (an agent-scope fence writes back / invalidates
+  // the XCD's whole L2)
+  if (tid < R) __hip_atomic_store(&b.tilecnt[((size_t)s * rtiles + t) * R + tid], sh_cnt[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) __hip_atomic_store(&b.tileF[(size_t)s * rtiles + t], sh_F, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // stable ranks within each (sub-tile, wave) slot by wave ballots, while the other tiles count
+#pragma unroll
+  for (int e = 0; e < kRingE; ++e) {
+    const bool valid = sid[e] != 255;
+    rank[e] = 0;
+    uint64_t mval = __ballot(valid);
+    while (mval) {
+      const int leader = __ffsll((unsigned long long)mval) - 1;
+      const int rl = __builtin_amdgcn_readlane(sid[e], leader);
+      const uint64_t mm = __ballot(valid && sid[e] == rl);
+      if (valid && sid[e] == rl) rank[e] = __popcll(mm & lanemask_lt());
+      if (lane == leader) sh_wcnt[rl][e * kW + w] = __popcll(mm);
+      mval &= ~mm;
+    }
+  }
+  if (tid < R) { sh_tot[tid] = 0; sh_pre[tid] = 0; }
+  __syncthreads();
+  // per ring, exclusive prefix over the slots: kSlots lanes per ring, groups aligned to kSlots
+  for (int k = tid; k < R * kSlots; k += kSrThreads) {
+    const int r = k / kSlots, j = k % kSlots;
+    const int v = sh_wcnt[r][j];
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < kSlots; o <<= 1) {
+      const int u = __shfl_up(incl, o, kSlots);
+      if (j >= o) incl += u;
+    }
+    sh_wcnt[r][j] = incl - v;
+  }
+  const int* tc = b.tilecnt + (size_t)s * rtiles * R;
+  for (int k = tid; k < nt * R; k += kSrThreads) {
+    int v;
+    while ((v = __hip_atomic_load(&tc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 0) __builtin_amdgcn_s_sleep(1);
+    if (v) {
+      atomicAdd(&sh_tot[k % R], v);
+      if (k / R < t) atomicAdd(&sh_pre[k % R], v);
+    }
+  }
+  int F = 0x7fffffff;
+  for (int k = tid; k < nt; k += kSrThreads) {
+    int v;
+    while ((v = __hip_atomic_load(&b.tileF[(size_t)s * rtiles + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 0)
+      __builtin_amdgcn_s_sleep(1);
+    F = min(F, v);
+  }
+  F = wave_min_i(F);
+  if (tid == 0) sh_F = 0x7fffffff;
+  __syncthreads();
+  if (lane == 0 && F != 0x7fffffff) atomicMin(&sh_F, F);
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int r = 0; r < R; ++r) { sh_base[r] = run; run += sh_tot[r]; }
+    if (t == 0) b.n_full[s] = run;
+  }
+  __syncthreads();
+  F = sh_F;
+#pragma unroll
+  for (int e = 0; e < kRingE; ++e) {
+    const int i = t * kRingTile + e * kSrThreads + tid;
+    if (sid[e] != 255) {
+      const int pos = sh_base[sid[e]] + sh_pre[sid[e]] + sh_wcnt[sid[e]][e * kW + w] + rank[e];
+      const float o = (i <= F) ? ori_first(ori[e], startOri) : ori_second(ori[e], endOri);
+      const float relTime = (o - startOri) / (endOri - startOri);
+      b.full[(size_t)s * b.cap + pos] = make_float4(q[e].y, q[e].z, q[e].x, (float)(sid[e] + 0.1 * D(relTime)));
+    }
+  }
+}
+
 // ---------------------------------------------------------------- curvature + marks
 constexpr int kFeatTile = 256;  // threads
 constexpr int kFeatE = 4;  // points per thread
@@ -1453,6 +1623,7 @@ hipError_t sr_alloc(SrBuffers& b, int S, int cap, int R) {
   A(&b.tmp_sid, n);
   A(&b.tilecnt, (size_t)S * b.ntiles() * R * sizeof(int));
   A(&b.tileF, (size_t)S * b.ntiles() * sizeof(int));
+  A(&b.ring_sync, sizeof(int));
   A(&b.sweep_ori, (size_t)S * 2 * sizeof(float));
   A(&b.full, n * sizeof(float4));
   A(&b.n_full, S * sizeof(int));
@@ -1485,7 +1656,7 @@ hipError_t sr_alloc(SrBuffers& b, int S, int cap, int R) {
 }
 
 void sr_free(SrBuffers& b) {
-  void* ptrs[] = {b.raw, b.raw_n, b.tmp_ori, b.tmp_sid, b.tilecnt, b.tileF, b.sweep_ori, b.full, b.n_full, b.curv,
+  void* ptrs[] = {b.raw, b.raw_n, b.tmp_ori, b.tmp_sid, b.tilecnt, b.tileF, b.ring_sync, b.sweep_ori, b.full, b.n_full, b.curv,
                   b.picked, b.sortind, b.label, b.ring_se, b.st_sharp, b.st_lsharp, b.st_flat,
                   b.st_lflat, b.st_cnt, b.st_cand, b.st_ncand, b.sharp, b.lsharp, b.flat, b.lflat, b.cnt, b.err, b.sel_big, b.st_loff, b.big_keys, b.big_sidx, b.big_cand};
   for (void* q : ptrs)
@@ -1502,8 +1673,15 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
     hipLaunchKernelGGL(k_sr_ring_sort<true>, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
   } else {
     const int rtiles = (b.cap + kRingTile - 1) / kRingTile;  // <= b.ntiles(): tilecnt rows fit
-    hipLaunchKernelGGL(k_sr_ring_count, dim3(rtiles, b.S), dim3(kSrThreads), 0, st, b, p);
-    hipLaunchKernelGGL(k_sr_ring_scatter, dim3(rtiles, b.S), dim3(kSrThreads), 0, st, b, p);
+    if (kSrRingFused) {
+      HIPCHK(hipMemsetAsync(b.ring_sync, 0, sizeof(int), st));
+      HIPCHK(hipMemsetAsync(b.tilecnt, 0xff, (size_t)b.S * rtiles * b.R * sizeof(int), st));
+      HIPCHK(hipMemsetAsync(b.tileF, 0xff, (size_t)b.S * rtiles * sizeof(int), st));
+      hipLaunchKernelGGL(k_sr_ring_fused, dim3(rtiles * b.S), dim3(kSrThreads), 0, st, b, p, rtiles);
+    } else {
+      hipLaunchKernelGGL(k_sr_ring_count, dim3(rtiles, b.S), dim3(kSrThreads), 0, st, b, p);
+      hipLaunchKernelGGL(k_sr_ring_scatter, dim3(rtiles, b.S), dim3(kSrThreads), 0, st, b, p);
+    }
   }
   mark("k_sr_ring_sort");
   if (sorted) HIPCHK(hipEventRecord(sorted, st));  // the ring-sorted full cloud is final here
