@@ -285,7 +285,10 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_sort(SrBuffers b, SrPara
 // and scatters with the same wave-ballot ranks.  src/scanRegistration.cpp:225-357
 // A tile is kRingE sub-tiles of kSrThreads points (each thread's kRingE loads in flight at once),
 // which also cuts the per-tile fixed work (sweep ends, start orientation, tile prefix) kRingE-fold.
-constexpr int kRingE = 4;
+#ifndef LOAM_RING_E
+#define LOAM_RING_E 4
+#endif
+constexpr int kRingE = LOAM_RING_E;
 constexpr int kRingTile = kSrThreads * kRingE;
 
 __global__ __launch_bounds__(kSrThreads) void k_sr_ring_count(SrBuffers b, SrParams p) {
@@ -478,7 +481,7 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_fused(SrBuffers b, SrPar
   constexpr int kW = kSrThreads / 64, kSlots = kRingE * kW;
   static_assert(kSlots <= 64 && (kSlots & (kSlots - 1)) == 0, "slot scan width");
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  __shared__ int sh_ticket, sh_first, sh_last, sh_F;
+  __shared__ int sh_ticket, sh_last, sh_F;
   __shared__ float sh_start, sh_end_raw;
   __shared__ int sh_cnt[64], sh_tot[64], sh_pre[64], sh_base[64];
   __shared__ int sh_wcnt[64][kSlots];
@@ -501,29 +504,36 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_fused(SrBuffers b, SrPar
     const int i = t * kRingTile + e * kSrThreads + tid;
     q[e] = i < n ? raw[i] : make_float4(0, 0, 0, 0);
   }
-  if (w == 0) {  // :230-238's first and last finite points, scanned from either end
+  // :230-238's first and last finite points, scanned from either end by waves 0 / 1; the lane
+  // that holds the point hands its coordinates over (no second load), -atan2 on lane 0
+  if (w < 2) {
     int f = -1;
-    for (int base = 0; base < n; base += 64) {
-      const int i = base + lane;
-      const uint64_t m = __ballot(i < n && finite3(raw[i]));
-      if (m) { f = base + __ffsll((unsigned long long)m) - 1; break; }
+    float4 v = make_float4(0, 0, 0, 0);
+    for (int k = 0; k < n; k += 64) {
+      const int i = w == 0 ? k + lane : n - 1 - k - lane;
+      const bool in = w == 0 ? i < n : i >= 0;
+      v = in ? raw[i] : make_float4(0, 0, 0, 0);
+      const uint64_t m = __ballot(in && finite3(v));
+      if (m) {
+        const int src = __ffsll((unsigned long long)m) - 1;
+        f = w == 0 ? k + src : n - 1 - k - src;
+        v.x = __shfl(v.x, src, 64);
+        v.y = __shfl(v.y, src, 64);
+        break;
+      }
     }
-    if (lane == 0) sh_first = f;
-  } else if (w == 1) {
-    int l = -1;
-    for (int base = n - 1; base >= 0; base -= 64) {
-      const int i = base - lane;
-      const uint64_t m = __ballot(i >= 0 && finite3(raw[i]));
-      if (m) { l = base - (__ffsll((unsigned long long)m) - 1); break; }
+    if (lane == 0) {
+      if (w == 0) {
+        sh_start = f >= 0 ? -atan2f_fdlibm(v.y, v.x) : 0.0f;
+      } else {
+        sh_last = f;
+        if (f >= 0) sh_end_raw = -atan2f_fdlibm(v.y, v.x);
+      }
     }
-    if (lane == 0) sh_last = l;
   }
   if (tid < R) sh_cnt[tid] = 0;
   if (tid == 0) sh_F = 0x7fffffff;
   for (int k = tid; k < 64 * kSlots; k += kSrThreads) (&sh_wcnt[0][0])[k] = 0;
-  __syncthreads();
-  if (tid == 0) sh_start = sh_last >= 0 ? -atan2f_fdlibm(raw[sh_first].y, raw[sh_first].x) : 0.0f;
-  if (tid == 64 && sh_last >= 0) sh_end_raw = -atan2f_fdlibm(raw[sh_last].y, raw[sh_last].x);
   __syncthreads();
   const float startOri = sh_start;
   float endOri = 0.0f;
