@@ -2528,6 +2528,11 @@ __global__ __launch_bounds__(256) void k_mp_compact_copy(MpBuffers b) {
   }
 }
 
+// k_mp_register workgroups per problem
+#ifndef LOAM_REG_WG
+#define LOAM_REG_WG 8  // (1024 problems, k_mp_register ms/step: 64 -> 1.02, 32 -> 0.77, 16 -> 0.52, 8 -> 0.50, 4 -> 0.51)
+#endif
+constexpr int kMpRegWg = LOAM_REG_WG;
 __global__ __launch_bounds__(256) void k_mp_register(MpBuffers b, MpInput in) {
   const int p = blockIdx.y;
   const loampose::MapRot r = rot_load(b, p);
@@ -2544,7 +2549,7 @@ __global__ __launch_bounds__(256) void k_mp_register(MpBuffers b, MpInput in) {
       imu.shiftX = q[6]; imu.shiftY = q[7]; imu.shiftZ = q[8];
       imu.veloX = q[9]; imu.veloY = q[10]; imu.veloZ = q[11];
     }
-    const loampose::EndRot er = loampose::end_rot(t, imu);
+    const loampose::EndRot er = loampose::end_rot_wave(t, imu);
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
       const float4 a = loampose::transform_to_end(t, imu, er, in.full[(size_t)p * in.full_stride + i], in.end_mode == 1);
       b.reg[(size_t)p * b.capS + i] = loampose::point_to_map(r, a);
@@ -2801,7 +2806,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   if (reg_side) {
     b.note(hipEventRecord(side->fork[1], st));
     b.note(hipStreamWaitEvent(side->st, side->fork[1], 0));
-    hipLaunchKernelGGL(k_mp_register, dim3(16, P), dim3(256), 0, side->st, b, in);
+    hipLaunchKernelGGL(k_mp_register, dim3(kMpRegWg, P), dim3(256), 0, side->st, b, in);
     b.note(hipEventRecord(side->join[1], side->st));
   }
   // insertion + per-valid-cube downsampling into the other pool
@@ -2837,7 +2842,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   if (reg_side) {
     b.note(hipStreamWaitEvent(st, side->join[1], 0));
   } else {
-    hipLaunchKernelGGL(k_mp_register, dim3(16, P), dim3(256), 0, st, b, in);
+    hipLaunchKernelGGL(k_mp_register, dim3(kMpRegWg, P), dim3(256), 0, st, b, in);
     mark("k_mp_register");
   }
   b.pool_cur = 1 - b.pool_cur;

@@ -2238,7 +2238,7 @@ __global__ __launch_bounds__(256) void k_od_end(OdBuffers b, FeatView f, int dst
   float4* oc = b.lastC + ((size_t)dst * b.P + p) * b.capC;
   float4* os = b.lastS + ((size_t)dst * b.P + p) * b.capS;
   float4* ofl = b.fullEnd + ((size_t)dst * b.P + p) * b.capS;
-  const loampose::EndRot er = loampose::end_rot(t, imu);
+  const loampose::EndRot er = loampose::end_rot_wave(t, imu);
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     float4 a;
     float4* o;

@@ -69,6 +69,34 @@ LOAM_HD EndRot end_rot(const float* t, const Imu& m) {
   return e;
 }
 
+// end_rot by a converged wave: lane k < 9 evaluates the k-th of its nine sines / cosines (the same
+// calls, so the same values) and every lane takes them by readlane — one library sincos per wave
+// instead of nine per lane (k_mp_register / k_od_end run it once per workgroup)
+LOAM_D EndRot end_rot_wave(const float* t, const Imu& m) {
+  const int lane = __lane_id();
+  const float a = lane == 0 ? t[0] : lane == 1 ? t[1] : lane == 2 ? t[2] : lane == 3 ? m.rollStart :
+                  lane == 4 ? m.pitchStart : lane == 5 ? m.yawStart : lane == 6 ? m.yawLast :
+                  lane == 7 ? m.pitchLast : m.rollLast;
+  double sv, cv;
+  dsincos(a, sv, cv);
+  auto rl = [&](double v, int k) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, k), hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), k);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+  };
+  EndRot e;
+  e.srx = rl(sv, 0); e.crx = rl(cv, 0);
+  e.sry = rl(sv, 1); e.cry = rl(cv, 1);
+  e.srz = rl(sv, 2); e.crz = rl(cv, 2);
+  e.srs = rl(sv, 3); e.crs = rl(cv, 3);
+  e.sps = rl(sv, 4); e.cps = rl(cv, 4);
+  e.sys = rl(sv, 5); e.cys = rl(cv, 5);
+  e.syl = rl(sv, 6); e.cyl = rl(cv, 6);
+  e.spl = rl(sv, 7); e.cpl = rl(cv, 7);
+  e.srl = rl(sv, 8); e.crl = rl(cv, 8);
+  return e;
+}
+
 // TransformToEnd (:126-194).  `zero`: the transform is known to be all +0, so for s >= 0 the
 // scaled angles are +0 and their sines / cosines exactly 0 / 1 (no library calls).
 LOAM_HD float4 transform_to_end(const float* t, const Imu& m, const EndRot& e, float4 pi, bool zero) {
