@@ -2530,7 +2530,7 @@ __global__ __launch_bounds__(256) void k_mp_compact_copy(MpBuffers b) {
 
 // k_mp_register workgroups per problem
 #ifndef LOAM_REG_WG
-#define LOAM_REG_WG 8  // (1024 problems, k_mp_register ms/step: 64 -> 1.02, 32 -> 0.77, 16 -> 0.52, 8 -> 0.50, 4 -> 0.51)
+#define LOAM_REG_WG 8  // (1024 problems, k_mp_register ms/step with a per-lane end_rot: 64 -> 1.02, 32 -> 0.77, 16 -> 0.61; with end_rot_wave: 16 -> 0.52, 8 -> 0.50, 4 -> 0.51)
 #endif
 constexpr int kMpRegWg = LOAM_REG_WG;
 __global__ __launch_bounds__(256) void k_mp_register(MpBuffers b, MpInput in) {
