@@ -294,6 +294,10 @@ constexpr int kRingTile = kSrThreads * kRingE;
 __global__ __launch_bounds__(kSrThreads) void k_sr_ring_count(SrBuffers b, SrParams p) {
   const int s = blockIdx.y, t = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const int n = b.raw_n[s], R = p.R;
+  if (t == 0) {  // the sweep's error bits and ring bounds start here (tile 0 alone writes err in this launch)
+    if (tid < 2 * R) b.ring_se[s * 2 * R + tid] = 0;
+    if (tid == 0) b.err[s] = 0;
+  }
   if (t * kRingTile >= n) return;
   const float4* raw = b.raw + (size_t)s * b.cap;
   __shared__ int sh_first, sh_last, sh_F;
@@ -477,6 +481,9 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_scatter(SrBuffers b, SrP
 #define LOAM_SR_RING_FUSED 1
 #endif
 constexpr bool kSrRingFused = LOAM_SR_RING_FUSED;
+// ... for launches of at least this many sweeps (its three presets are launches of their own: a
+// one-sweep chain keeps the two-kernel form)
+constexpr int kSrRingFusedMin = 64;
 __global__ __launch_bounds__(kSrThreads) void k_sr_ring_fused(SrBuffers b, SrParams p, int rtiles) {
   constexpr int kW = kSrThreads / 64, kSlots = kRingE * kW;
   static_assert(kSlots <= 64 && (kSlots & (kSlots - 1)) == 0, "slot scan width");
@@ -489,6 +496,10 @@ __global__ __launch_bounds__(kSrThreads) void k_sr_ring_fused(SrBuffers b, SrPar
   __syncthreads();
   const int s = sh_ticket / rtiles, t = sh_ticket % rtiles;
   const int n = b.raw_n[s], R = p.R, nt = (n + kRingTile - 1) / kRingTile;
+  if (t == 0) {  // the sweep's error bits and ring bounds start here (tile 0 alone writes err in this launch)
+    if (tid < 2 * R) b.ring_se[s * 2 * R + tid] = 0;
+    if (tid == 0) b.err[s] = 0;
+  }
   if (n <= 0) {
     if (t == 0 && tid == 0) {
       b.n_full[s] = 0;
@@ -1676,14 +1687,16 @@ void sr_free(SrBuffers& b) {
 
 void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof, hipEvent_t sorted) {
   auto mark = [&](const char* n) { if (prof) prof->mark(n); };
-  HIPCHK(hipMemsetAsync(b.ring_se, 0, (size_t)b.S * 2 * b.R * sizeof(int), st));
-  HIPCHK(hipMemsetAsync(b.err, 0, (size_t)b.S * sizeof(int), st));
+  if (p.imu) {  // (the tile-parallel ring sorts clear them in their tile 0)
+    HIPCHK(hipMemsetAsync(b.ring_se, 0, (size_t)b.S * 2 * b.R * sizeof(int), st));
+    HIPCHK(hipMemsetAsync(b.err, 0, (size_t)b.S * sizeof(int), st));
+  }
   mark("sr_memset");
   if (p.imu) {
     hipLaunchKernelGGL(k_sr_ring_sort<true>, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
   } else {
     const int rtiles = (b.cap + kRingTile - 1) / kRingTile;  // <= b.ntiles(): tilecnt rows fit
-    if (kSrRingFused) {
+    if (kSrRingFused && b.S >= kSrRingFusedMin) {
       HIPCHK(hipMemsetAsync(b.ring_sync, 0, sizeof(int), st));
       HIPCHK(hipMemsetAsync(b.tilecnt, 0xff, (size_t)b.S * rtiles * b.R * sizeof(int), st));
       HIPCHK(hipMemsetAsync(b.tileF, 0xff, (size_t)b.S * rtiles * sizeof(int), st));
