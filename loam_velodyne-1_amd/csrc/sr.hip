@@ -768,6 +768,11 @@ struct SelShared {
 #ifndef LOAM_RINGVG_PAD
 #define LOAM_RINGVG_PAD 0
 #endif
+// member gathers in flight per step of a voxel's mean in ring_vg
+#ifndef LOAM_VG_GATHER
+#define LOAM_VG_GATHER 8
+#endif
+constexpr int kVgGather = LOAM_VG_GATHER;
 #ifndef LOAM_RINGVG_HOLD
 #define LOAM_RINGVG_HOLD 1
 #endif
@@ -836,8 +841,52 @@ LOAM_D int ring_vg(const float4* pts, int lo, const CandT* cand, int nc, uint64_
         // VLP-16): sort the runs, (voxel, first candidate, length), instead of the candidates.
         // Runs of one voxel sorted by their first candidate list its members in the same order as
         // the stable (voxel, candidate) sort, so the means are summed in the same order.
-        uint32_t* edge = reinterpret_cast<uint32_t*>(&red[0][0]);  // last voxel of each wave's chunk
+        constexpr int NW = kSelThreads / 64;
         int nruns = 0;
+        if constexpr (HOLD) {
+          // all chunks at once: the thread's held candidates e * NT + tid, their run heads ranked by
+          // wave ballots and the (chunk, wave) slots' counts prefixed in candidate order (two
+          // barriers instead of four per chunk)
+          static_assert(RH * NW <= 64, "slot prefix over one wave");
+          __shared__ uint32_t rs_edge[RH * NW];
+          __shared__ int rs_cnt[RH * NW];
+          uint32_t idx[RH];
+          int ex[RH];
+#pragma unroll
+          for (int e = 0; e < RH; ++e) {
+            const int t = e * kSelThreads + tid;
+            idx[e] = 0xffffffffu;
+            if (t < nc) {
+              const float4 a = held[e];
+              const int i0 = (int)(floorf(a.x * inv) - (float)minb[0]);
+              const int i1 = (int)(floorf(a.y * inv) - (float)minb[1]);
+              const int i2 = (int)(floorf(a.z * inv) - (float)minb[2]);
+              idx[e] = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
+            }
+            if (lane == 63) rs_edge[e * NW + w] = idx[e];
+          }
+          __syncthreads();
+#pragma unroll
+          for (int e = 0; e < RH; ++e) {
+            const int t = e * kSelThreads + tid, slot = e * NW + w;
+            uint32_t up = (uint32_t)__shfl_up((int)idx[e], 1, 64);
+            if (lane == 0 && slot > 0) up = rs_edge[slot - 1];  // the previous 64 candidates' last
+            const bool head = t < nc && (t == 0 || idx[e] != up);
+            const uint64_t m = __ballot(head);
+            ex[e] = head ? __popcll(m & lanemask_lt()) : -1;
+            if (lane == 0) rs_cnt[slot] = __popcll(m);
+          }
+          __syncthreads();
+          const int c = lane < RH * NW ? rs_cnt[lane] : 0;
+          const int incl = wave_incl_scan(c);
+          nruns = __shfl(incl, RH * NW - 1, 64);
+#pragma unroll
+          for (int e = 0; e < RH; ++e) {
+            const int base = __shfl(incl - c, e * NW + w, 64);
+            if (ex[e] >= 0) keys[base + ex[e]] = ((uint64_t)idx[e] << 32) | ((uint32_t)(e * kSelThreads + tid) << 16);
+          }
+        } else {
+        uint32_t* edge = reinterpret_cast<uint32_t*>(&red[0][0]);  // last voxel of each wave's chunk
         for (int base = 0; base < nc; base += kSelThreads) {
           const int t = base + tid;
           uint32_t idx = 0xffffffffu;
@@ -867,6 +916,7 @@ LOAM_D int ring_vg(const float4* pts, int lo, const CandT* cand, int nc, uint64_
           if (tid == kSelThreads - 1) edge[0] = idx;
           nruns += tot;
         }
+        }
         __syncthreads();
         constexpr int RE = CAP / kSelThreads;
         uint32_t nxt[RE];
@@ -883,35 +933,68 @@ LOAM_D int ring_vg(const float4* pts, int lo, const CandT* cand, int nc, uint64_
         }
         __syncthreads();
         reg_bitonic_sort<kSelThreads, CAP / kSelThreads>(keys, nruns);
-        int run = 0;
-        for (int base = 0; base < nruns; base += kSelThreads) {
-          const int r = base + tid;
-          const int head = (r < nruns && (r == 0 || (keys[r] >> 32) != (keys[r - 1] >> 32))) ? 1 : 0;
-          int tot;
-          const int ex = block_excl_scan<kSelThreads>(head, scratch, tot);
-          if (head) {
+        // voxel heads among the sorted runs r = e * NT + tid, ranked like the runs above (one barrier)
+        static_assert(RE * NW <= 64, "slot prefix over one wave");
+        __shared__ int vs_cnt[RE * NW];
+        int vex[RE];
+#pragma unroll
+        for (int e = 0; e < RE; ++e) {
+          const int r = e * kSelThreads + tid;
+          const bool head = r < nruns && (r == 0 || (keys[r] >> 32) != (keys[r - 1] >> 32));
+          const uint64_t m = __ballot(head);
+          vex[e] = head ? __popcll(m & lanemask_lt()) : -1;
+          if (lane == 0) vs_cnt[e * NW + w] = __popcll(m);
+        }
+        __syncthreads();
+        const int vc = lane < RE * NW ? vs_cnt[lane] : 0;
+        const int vincl = wave_incl_scan(vc);
+#pragma unroll
+        for (int e = 0; e < RE; ++e) {
+          const int r = e * kSelThreads + tid;
+          const int vbase = __shfl(vincl - vc, e * NW + w, 64);
+          if (vex[e] >= 0) {
+            const int slot_out = vbase + vex[e];
             const uint32_t vk = (uint32_t)(keys[r] >> 32);
             float sx = 0, sy = 0, sz = 0, si = 0;
             int cnt = 0;
-            for (int e = r; e < nruns && (uint32_t)(keys[e] >> 32) == vk; ++e) {
-              const uint32_t k = (uint32_t)keys[e];
-              const int m0 = (int)(k >> 16), m1 = m0 + (int)(k & 0xffffu);
-              cnt += m1 - m0;
-              for (int m = m0; m < m1; m += 4) {  // four independent gathers in flight per step
-                float4 a[4];
+            // the voxel's members over all its runs (in run order, members ascending: the sorted
+            // order), kVgGather gathers in flight per step whatever the run lengths
+            int rr = r;
+            uint32_t kk = (uint32_t)keys[r];
+            int m = (int)(kk >> 16), m1 = m + (int)(kk & 0xffffu);
+            const int mfirst = m;
+            bool more = true;
+            while (more) {
+              int mi[kVgGather];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) a[u] = pts[lo + cand[min(m + u, m1 - 1)]];
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                  if (m + u < m1) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; }
+              for (int u = 0; u < kVgGather; ++u) {
+                if (more && m >= m1) {  // the voxel's next run
+                  ++rr;
+                  if (rr < nruns && (uint32_t)(keys[rr] >> 32) == vk) {
+                    kk = (uint32_t)keys[rr];
+                    m = (int)(kk >> 16);
+                    m1 = m + (int)(kk & 0xffffu);
+                  } else {
+                    more = false;
+                  }
+                }
+                mi[u] = more ? m++ : -1;
               }
+              float4 a[kVgGather];
+#pragma unroll
+              for (int u = 0; u < kVgGather; ++u) a[u] = pts[lo + cand[mi[u] >= 0 ? mi[u] : mfirst]];
+#pragma unroll
+              for (int u = 0; u < kVgGather; ++u)
+                if (mi[u] >= 0) { sx += a[u].x; sy += a[u].y; sz += a[u].z; si += a[u].w; ++cnt; }
+              if (more && m >= m1)  // run consumed: go on only when the voxel has another
+                more = rr + 1 < nruns && (uint32_t)(keys[rr + 1] >> 32) == vk;
             }
             const float fc = (float)cnt;
-            if (run + ex < outcap) outp[run + ex] = make_float4(sx / fc, sy / fc, sz / fc, si / fc);
+            if (slot_out < outcap) outp[slot_out] = make_float4(sx / fc, sy / fc, sz / fc, si / fc);
           }
-          run += tot;
         }
-        nout = run;
+        __syncthreads();  // the keys are read until here (a caller may reuse them)
+        nout = __shfl(vincl, RE * NW - 1, 64);
       } else
       {
         const int P2c = next_pow2(nc);
@@ -1499,10 +1582,11 @@ __global__ __launch_bounds__(64 * kPickWaves) __attribute__((amdgpu_waves_per_eu
 
 __global__ __launch_bounds__(kSelThreads) void k_sr_ringvg(SrBuffers b, SrParams p) {
   const int q = blockIdx.x, s = blockIdx.y, tid = threadIdx.x, R = p.R;
-  if (b.sel_big[s] != 0) return;
-  const int n = b.n_full[s];
-  if (n <= 0) return;
+  // the ring's words loaded together (one round trip), then the early exits
+  const int big = b.sel_big[s], n = b.n_full[s];
   int lo = b.ring_se[s * 2 * R + q], en = b.ring_se[s * 2 * R + R + q];
+  const int nc = min(b.st_ncand[s * R + q], kPickCap);
+  if (big != 0 || n <= 0) return;
   if (q == 0) lo = 5;
   if (q == R - 1) en = n - 5;
   if (lo > en - 1) return;
@@ -1510,7 +1594,6 @@ __global__ __launch_bounds__(kSelThreads) void k_sr_ringvg(SrBuffers b, SrParams
   __shared__ uint16_t cand[kPickCap];
   __shared__ float red[6][kSelThreads / 64];
   __shared__ int scratch[16];
-  const int nc = min(b.st_ncand[s * R + q], kPickCap);
   const uint16_t* cg = b.st_cand + (size_t)(s * R + q) * kRingCap;
   for (int t = tid; t < nc; t += kSelThreads) cand[t] = cg[t];
   __syncthreads();
