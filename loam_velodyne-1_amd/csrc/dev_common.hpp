@@ -293,6 +293,45 @@ LOAM_D float wave_min_f_x(float v) {
   }
   return v;
 }
+// float maximum, likewise
+LOAM_D float wave_max_f_x(float v) {
+  constexpr uint32_t kNInf = 0xff800000u;
+  v = fmaxf(v, __uint_as_float(dpp_u32<kDppXor1>(kNInf, __float_as_uint(v))));
+  v = fmaxf(v, __uint_as_float(dpp_u32<kDppXor2>(kNInf, __float_as_uint(v))));
+  v = fmaxf(v, __uint_as_float(dpp_u32<kDppHalfMirror>(kNInf, __float_as_uint(v))));
+  v = fmaxf(v, __uint_as_float(dpp_u32<kDppRor8>(kNInf, __float_as_uint(v))));
+  {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  }
+  {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  }
+  return v;
+}
+// the workgroup's bounding box: the six minima / maxima reduced together (two barriers instead of
+// two per value); every thread of the workgroup must call it, and gets the box
+template <int NT>
+LOAM_D void block_bbox(float (&mn)[3], float (&mx)[3]) {
+  constexpr int NW = NT / 64;
+  __shared__ float bb[6][NW];
+  const int w = threadIdx.x >> 6, l = lane_id();
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const float a = wave_min_f_x(mn[d]), b = wave_max_f_x(mx[d]);
+    if (l == 0) { bb[d][w] = a; bb[3 + d][w] = b; }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    float a = bb[d][0], b = bb[3 + d][0];
+    for (int v = 1; v < NW; ++v) { a = fminf(a, bb[d][v]); b = fmaxf(b, bb[3 + d][v]); }
+    mn[d] = a;
+    mx[d] = b;
+  }
+  __syncthreads();
+}
 // inclusive prefix sum over the wave (HALF: over each 32-lane half), the row-shift / row-broadcast
 // ladder: lanes beyond a row's start read 0
 template <bool HALF = false>

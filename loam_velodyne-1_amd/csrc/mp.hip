@@ -253,7 +253,6 @@ __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
   __shared__ uint32_t ka[N], kb[N];
   __shared__ uint16_t va[N], vb[N];
   __shared__ uint32_t sc[(NT / 64 + 1) * 8];
-  __shared__ float fsc[16];
   __shared__ int isc[24];
   const int tid = threadIdx.x;
   const int nl = j.list ? *j.list_n : j.nseg;
@@ -276,10 +275,7 @@ __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
       mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
       mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
     }
-    for (int d = 0; d < 3; ++d) {
-      mn[d] = block_reduce<NT>(mn[d], fsc, [](float a, float c) { return fminf(a, c); });
-      mx[d] = block_reduce<NT>(mx[d], fsc, [](float a, float c) { return fmaxf(a, c); });
-    }
+    block_bbox<NT>(mn, mx);
     const float inv = 1.0f / j.leaf[s];
     if (vg_leaf_too_small(mn, mx, inv)) {  // "leaf size too small": output = input
       for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
@@ -379,10 +375,7 @@ __device__ __forceinline__ void vg_idx_segment(const VgJob& j, int s, int b0, in
       mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
       mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
     }
-    for (int d = 0; d < 3; ++d) {
-      mn[d] = block_reduce<NT>(mn[d], fsc, [](float a, float c) { return fminf(a, c); });
-      mx[d] = block_reduce<NT>(mx[d], fsc, [](float a, float c) { return fmaxf(a, c); });
-    }
+    block_bbox<NT>(mn, mx);
     const float inv = 1.0f / j.leaf[s];
     if (vg_leaf_too_small(mn, mx, inv)) {  // "leaf size too small": output = input
       for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
@@ -535,7 +528,6 @@ __global__ __launch_bounds__(NT) void k_vg_big(VgJob j) {
   __shared__ uint32_t hist[8][16];
   __shared__ uint32_t dbase[16], ttot[16];
   __shared__ uint32_t sc[(NT / 64 + 1) * 8];
-  __shared__ float fsc[16];
   __shared__ int isc[24];
   const int tid = threadIdx.x;
   const int nl = *j.list_n;
@@ -549,10 +541,7 @@ __global__ __launch_bounds__(NT) void k_vg_big(VgJob j) {
       mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
       mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
     }
-    for (int d = 0; d < 3; ++d) {
-      mn[d] = block_reduce<NT>(mn[d], fsc, [](float a, float c) { return fminf(a, c); });
-      mx[d] = block_reduce<NT>(mx[d], fsc, [](float a, float c) { return fmaxf(a, c); });
-    }
+    block_bbox<NT>(mn, mx);
     const float inv = 1.0f / j.leaf[s];
     if (vg_leaf_too_small(mn, mx, inv)) {  // "leaf size too small": output = input
       for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
@@ -678,7 +667,6 @@ __global__ __launch_bounds__(NT) void k_vg_merge(VgJob j) {
   static_assert((NEW & (NEW - 1)) == 0 && NEW % NT == 0 && NEW <= 65536, "bitonic sort / scan layout");
   __shared__ uint64_t nk[NEW];      // tail (key << 32 | tail position), sorted
   __shared__ uint16_t nhp[NEW];     // first entry in nk of each tail voxel that holds no old point
-  __shared__ float fsc[16];
   __shared__ int isc[24];
   const int tid = threadIdx.x;
   const int nl = *j.mlist_n;
@@ -692,10 +680,7 @@ __global__ __launch_bounds__(NT) void k_vg_merge(VgJob j) {
       mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
       mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
     }
-    for (int d = 0; d < 3; ++d) {
-      mn[d] = block_reduce<NT>(mn[d], fsc, [](float a, float c) { return fminf(a, c); });
-      mx[d] = block_reduce<NT>(mx[d], fsc, [](float a, float c) { return fmaxf(a, c); });
-    }
+    block_bbox<NT>(mn, mx);
     const float inv = 1.0f / j.leaf[s];
     if (vg_leaf_too_small(mn, mx, inv)) {  // (the cascade copies it)
       if (tid == 0) j.skip[s] = 0;
