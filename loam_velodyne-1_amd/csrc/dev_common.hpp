@@ -378,12 +378,12 @@ LOAM_D int block_incl_max(int v, int* scratch, int& total) {
 template <int NT>
 LOAM_D int block_excl_scan(int v, int* scratch, int& total) {
   const int nw = NT / 64, w = threadIdx.x >> 6, l = lane_id();
-  int incl = wave_incl_scan(v);
+  int incl = wave_incl_scan_x(v);
   if (l == 63) scratch[w] = incl;
   __syncthreads();
   if (w == 0) {
     int s = l < nw ? scratch[l] : 0;
-    int si = wave_incl_scan(s);
+    int si = wave_incl_scan_x(s);
     if (l < nw) scratch[l] = si - s;
     if (l == nw - 1) scratch[nw] = si;
   }
@@ -604,12 +604,7 @@ LOAM_D int block_radix_sort_kv(uint32_t* ka, uint16_t* va, uint32_t* kb, uint16_
       inc[i] = p[i];
     }
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t t = (uint32_t)__shfl_up((int)inc[i], o, 64);
-        if (lane >= o) inc[i] += t;
-      }
+    for (int i = 0; i < 8; ++i) inc[i] = (uint32_t)wave_incl_scan_x((int)inc[i]);  // (DPP: integer sums, any order)
     if (lane == 63)
 #pragma unroll
       for (int i = 0; i < 8; ++i) sc[w * 8 + i] = inc[i];
@@ -682,12 +677,7 @@ LOAM_D void tile_rank4(const uint32_t* k, int shift, int n_tile, uint32_t* sc, u
     inc[i] = p[i];
   }
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t t = (uint32_t)__shfl_up((int)inc[i], o, 64);
-      if (lane >= o) inc[i] += t;
-    }
+  for (int i = 0; i < 8; ++i) inc[i] = (uint32_t)wave_incl_scan_x((int)inc[i]);  // (DPP: integer sums, any order)
   if (lane == 63)
 #pragma unroll
     for (int i = 0; i < 8; ++i) sc[w * 8 + i] = inc[i];
