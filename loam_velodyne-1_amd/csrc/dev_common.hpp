@@ -310,6 +310,20 @@ LOAM_D float wave_max_f_x(float v) {
   }
   return v;
 }
+// the workgroup's maximum of an unsigned value (DPP wave maxima, one LDS exchange); every thread
+// of the workgroup must call it
+template <int NT>
+LOAM_D uint32_t block_max_u32(uint32_t v) {
+  constexpr int NW = NT / 64;
+  __shared__ uint32_t bm[NW];
+  const uint32_t m = ~wave_min_u32_x(~v);
+  if (lane_id() == 0) bm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  uint32_t r = bm[0];
+  for (int i = 1; i < NW; ++i) r = bm[i] > r ? bm[i] : r;
+  __syncthreads();
+  return r;
+}
 // the workgroup's bounding box: the six minima / maxima reduced together (two barriers instead of
 // two per value); every thread of the workgroup must call it, and gets the box
 template <int NT>

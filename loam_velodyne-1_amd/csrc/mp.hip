@@ -296,7 +296,7 @@ __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
       va[i] = (uint16_t)i;
       kmax = key > kmax ? key : kmax;
     }
-    kmax = (uint32_t)block_reduce<NT>((int)(kmax >> 1), (int*)isc, [](int a, int c) { return a > c ? a : c; });
+    kmax = block_max_u32<NT>(kmax >> 1);
     const int nbits = kmax ? 33 - __clz((int)kmax) : (n > 1 ? 1 : 0);  // bits of the max key
     const int cur = block_radix_sort_kv<NT, E>(ka, va, kb, vb, n, nbits, sc);
     const uint32_t* ks = cur ? kb : ka;
@@ -396,7 +396,7 @@ __device__ __forceinline__ void vg_idx_segment(const VgJob& j, int s, int b0, in
       va[i] = (uint16_t)i;
       kmax = key > kmax ? key : kmax;
     }
-    kmax = (uint32_t)block_reduce<NT>((int)(kmax >> 1), (int*)isc, [](int a, int c) { return a > c ? a : c; });
+    kmax = block_max_u32<NT>(kmax >> 1);
     const int nbits = kmax ? 33 - __clz((int)kmax) : (n > 1 ? 1 : 0);
     int cur = 0;
     for (int shift = 0; shift < nbits; shift += 4) {
@@ -571,7 +571,7 @@ __global__ __launch_bounds__(NT) void k_vg_big(VgJob j) {
 #pragma unroll
       for (int p = 0; p < 8; ++p) atomicAdd(&hist[p][(key >> (4 * p)) & 15u], 1u);
     }
-    kmax = (uint32_t)block_reduce<NT>((int)(kmax >> 1), (int*)isc, [](int a, int c) { return a > c ? a : c; });
+    kmax = block_max_u32<NT>(kmax >> 1);
     const int nbits = kmax ? 33 - __clz((int)kmax) : (n > 1 ? 1 : 0);
     int cur = 0;  // 0: the data is in (K, V)
     for (int pass = 0; pass * 4 < nbits; ++pass) {

@@ -810,8 +810,8 @@ LOAM_D int ring_vg(const float4* pts, int lo, const CandT* cand, int nc, uint64_
     }
   }
   for (int d = 0; d < 3; ++d) {
-    mn[d] = wave_min_f(mn[d]);
-    mx[d] = wave_max_f(mx[d]);
+    mn[d] = wave_min_f_x(mn[d]);
+    mx[d] = wave_max_f_x(mx[d]);
     if (lane == 0) { red[d][w] = mn[d]; red[3 + d][w] = mx[d]; }
   }
   __syncthreads();
@@ -878,7 +878,7 @@ LOAM_D int ring_vg(const float4* pts, int lo, const CandT* cand, int nc, uint64_
           }
           __syncthreads();
           const int c = lane < RH * NW ? rs_cnt[lane] : 0;
-          const int incl = wave_incl_scan(c);
+          const int incl = wave_incl_scan_x(c);
           nruns = __shfl(incl, RH * NW - 1, 64);
 #pragma unroll
           for (int e = 0; e < RH; ++e) {
@@ -947,7 +947,7 @@ LOAM_D int ring_vg(const float4* pts, int lo, const CandT* cand, int nc, uint64_
         }
         __syncthreads();
         const int vc = lane < RE * NW ? vs_cnt[lane] : 0;
-        const int vincl = wave_incl_scan(vc);
+        const int vincl = wave_incl_scan_x(vc);
 #pragma unroll
         for (int e = 0; e < RE; ++e) {
           const int r = e * kSelThreads + tid;
