@@ -2461,10 +2461,17 @@ __global__ __launch_bounds__(NT) void k_mp_compact_table(MpBuffers b) {
   __syncthreads();
   // the table and the non-empty (kind, cube) list written (kind, cube)-consecutive across the lanes
   // (each lane's own run of entries would scatter every store): kind | cube << 1 | (valid + 1) << 14
+  // (all passes at once: the non-empty entries ranked by wave ballots, the (pass, wave) counts
+  // prefixed by each wave in x order — two barriers instead of three per pass)
   int* items = b.citems + (size_t)p * 2 * kCubeNum;
-  int nitems = 0;
-  for (int xb = 0; xb < N; xb += NT) {
-    const int x = xb + tid;
+  constexpr int NW = NT / 64;
+  static_assert(NW <= 64, "one count per lane");
+  __shared__ int icnt[E][NW];
+  const int lane = lane_id(), w = tid >> 6;
+  int iex[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int x = e * NT + tid;
     int n = 0;
     if (x < N) {
       const int kind = x / kCubeNum, s = x % kCubeNum, o = nn[x];
@@ -2472,10 +2479,22 @@ __global__ __launch_bounds__(NT) void k_mp_compact_table(MpBuffers b) {
       nw[s * 4 + 2 * kind] = o;
       nw[s * 4 + 1 + 2 * kind] = n;
     }
-    int tot;
-    const int ex = block_excl_scan<NT>(n > 0 ? 1 : 0, scratch, tot);
-    if (n > 0) items[nitems + ex] = (x / kCubeNum) | ((x % kCubeNum) << 1) | (((int)vidx[x % kCubeNum] + 1) << 14);
-    nitems += tot;
+    const uint64_t m = __ballot(n > 0);
+    iex[e] = n > 0 ? __popcll(m & lanemask_lt()) : -1;
+    if (lane == 0) icnt[e][w] = __popcll(m);
+  }
+  __syncthreads();
+  int nitems = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int c = lane < NW ? icnt[e][lane] : 0;
+    const int incl = wave_incl_scan_x(c);
+    const int base = nitems + __shfl(incl - c, w, 64);
+    if (iex[e] >= 0) {
+      const int x = e * NT + tid;
+      items[base + iex[e]] = (x / kCubeNum) | ((x % kCubeNum) << 1) | (((int)vidx[x % kCubeNum] + 1) << 14);
+    }
+    nitems += __shfl(incl, NW - 1, 64);
   }
   vpts = block_reduce<NT>(vpts, scratch, [](int a, int c) { return a + c; });
   if (tid == 0) {
