@@ -1,4 +1,7 @@
 #!/bin/bash
+# A/B of the config-3 device chain across libraries (loam_velodyne-1_amd/exp/NAME.so, see
+# tools/build_ref_variant.sh) against the working tree, alternating 5 times; medians:
+#   tools/ab_chain_lib.sh base [other ...]
 R=$GRAFT_REPO_ROOT; cd $R
 : > gpurun_out/_chain_lib.txt
 for rep in 1 2 3 4 5; do

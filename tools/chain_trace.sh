@@ -1,3 +1,4 @@
+# Kernel trace of the config-3 device chain (tools/chain_bench.py) and its per-sweep timeline
 R=$GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 cd /tmp
