@@ -1255,7 +1255,7 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
     x->seed_ready = false;
   } else {
     T(hipMemsetAsync(o.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st));
-    hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fprev, ls, 1, 0);
+    hipLaunchKernelGGL(k_od_end, dim3(kOdEndWg, P), dim3(256), 0, x->st, o, fprev, ls, 1, 0);
     x->prof.mark("k_od_end_seed");
     od_build_hashes(o, ls, x->st);
     x->prof.mark("k_hash_build_last");
@@ -1280,7 +1280,7 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
     od_fini(o, fcur, x->st2);
     T(hipEventRecord(x->join2, x->st2));
   }
-  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, le, 2, 0);
+  hipLaunchKernelGGL(k_od_end, dim3(kOdEndWg, P), dim3(256), 0, x->st, o, fcur, le, 2, 0);
   x->prof.mark("k_od_end");
   if (overlap) T(hipStreamWaitEvent(x->st, x->join2, 0));
   if (events) T(hipEventRecord(x->ev[2], x->st));
@@ -1319,7 +1319,7 @@ hipError_t batch_enqueue(loam_ctx* x, Prof* pf, bool events) {
     OdBuffers on = o;
     on.istate = o.istate_set[nx];
     T(hipMemsetAsync(on.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st3));
-    hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st3, on, feat_view(x->srbuf(nx), 0, 2), ls, 1, 0);
+    hipLaunchKernelGGL(k_od_end, dim3(kOdEndWg, P), dim3(256), 0, x->st3, on, feat_view(x->srbuf(nx), 0, 2), ls, 1, 0);
     od_build_hashes(on, ls, x->st3);
     T(hipEventRecord(x->seed_done, x->st3));
     x->seed_ready = true;
@@ -1352,7 +1352,7 @@ hipError_t enqueue_ahead(loam_ctx* x, int i, int ls, hipEvent_t free_last) {
   if (free_last) T(hipStreamWaitEvent(x->st3, free_last, 0));
   on.istate = on.istate_set[i];
   T(hipMemsetAsync(on.istate, 0, (size_t)P * kOdStateInts * sizeof(int), x->st3));
-  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st3, on, feat_view(x->srbuf(i), 0, 2), ls, 1, 0);
+  hipLaunchKernelGGL(k_od_end, dim3(kOdEndWg, P), dim3(256), 0, x->st3, on, feat_view(x->srbuf(i), 0, 2), ls, 1, 0);
   od_build_hashes(on, ls, x->st3);
   T(hipEventRecord(x->seed_done, x->st3));
   x->sr_ready = x->seed_ready = true;
@@ -1400,7 +1400,7 @@ hipError_t batch_enqueue_pipe(loam_ctx* x) {
   // Last[le] was the previous step's Last[s]: its frame 1 has read it (its odometry is ahead on st);
   // before that, frame 2 of the step before read it, which the previous seed waited for
   if (x->b_used) T(hipStreamWaitEvent(x->st, x->mp1_read, 0));
-  hipLaunchKernelGGL(k_od_end, dim3(16, P), dim3(256), 0, x->st, o, fcur, le, 2, 0);
+  hipLaunchKernelGGL(k_od_end, dim3(kOdEndWg, P), dim3(256), 0, x->st, o, fcur, le, 2, 0);
   PT_END("od", x->st);
   T(hipEventRecord(x->od_done, x->st));
   T(hipEventRecord(x->ev[2], x->st));

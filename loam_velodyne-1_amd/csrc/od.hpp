@@ -13,6 +13,11 @@ namespace loam {
 #ifndef LOAM_OD_CHUNK
 #define LOAM_OD_CHUNK 64
 #endif
+// k_od_end workgroups per problem in batches (TransformToEnd of the Last clouds)
+#ifndef LOAM_OD_END_WG
+#define LOAM_OD_END_WG 16  // (1024 problems: 16 / 8 / 4 measured equal once end_rot_wave took the setup)
+#endif
+constexpr int kOdEndWg = LOAM_OD_END_WG;
 constexpr int kChunk = LOAM_OD_CHUNK;  // points per chunk box (<= 64)
 __host__ __device__ inline int chunks_of(int cap) { return (cap + kChunk - 1) / kChunk; }
 // the association's best-first ring windows (ring-monotone clouds) visit kSub-point sub-chunks
