@@ -86,12 +86,13 @@ def kernel_bytes(st):
         # per query-iteration: accept flag, stack point and coefficient read back for JtJ
         "k_mp_iter": 33 * st["mp_stack_iters"],
         # the search and the fit in one launch, one 64-B record per query (last 5-NN + its fit): per
-        # query-iteration the stack point (16 B), the record's 5-NN read and written (32 + 32 B), its
-        # fit read (32 B, an upper bound: only reused fits are read) and the row written (17 B); per
-        # refit the 5 neighbours (80 B) and the fit written (32 B) less the fit read; the search's
-        # 8 B per bucket range and 16 B per map point evaluated (seeds included)
-        "k_mp_nnfit": 129 * st["mp_stack_iters"] + 8 * st["mp_nn_cells"] + 16 * st["mp_nn_candidates"]
-                      + 80 * st["mp_fits"],
+        # query-iteration the stack point (16 B), the record's 5-NN read (32 B) and its fit read (32 B,
+        # an upper bound: only reused fits are read); per refit the 5 neighbours (80 B) and the record
+        # written (64 B; a record is written only when its list changes, round 6); the rows stay in
+        # the kernel (fused step); the search's 8 B per bucket range and 16 B per map point evaluated
+        # (seeds included)
+        "k_mp_nnfit": 80 * st["mp_stack_iters"] + 8 * st["mp_nn_cells"] + 16 * st["mp_nn_candidates"]
+                      + 144 * st["mp_fits"],
     }
 
 
@@ -113,7 +114,24 @@ def algorithmic_bytes(st):
     alg["k_mp_nnfit"] = 96 * st["mp_stack_iters"] + 64 * st["mp_rows_sum"]
     alg.pop("k_mp_iter")
     alg["k_od_assoc"] = 16 * st["od_assoc_points"]
+    # the VoxelGrid jobs (B_MP's 32 s and 32 M_valid, MP-4 / MP-8): the stacks read every mapped
+    # sweep's lessSharp + lessFlat point once (16 B) and write the downsampled stack (16 B per
+    # point; the solved frame's stack, mp_stack: the first frame's output is not counted, a lower
+    # bound); the cubes read and write the valid cubes' points (32 B per point of the solved
+    # frame's valid cubes: the first frame's smaller map is not counted)
+    alg["vg_stack"] = 16 * (st["n_less_sharp"] + st["n_less_flat"]) + 16 * st["mp_stack"]
+    alg["vg_cubes"] = 32 * st["mp_map_valid_points"]
     return alg
+
+
+def moved_od_bytes(st):
+    """B_OD as the engine moves it: with the per-query moments (tuning od_moments_min) the stored
+    rows are never re-read, so SURVEY.md §8(d)'s Σ 32 R_k term (Q12's row re-reads) is replaced
+    by the moments' 176 B per query-iteration (query point 16 B + ten fp64 moments read and
+    written, 160 B)"""
+    if not st.get("od_moments"):
+        return st["bytes_od"]
+    return st["bytes_od"] - 32 * st["od_rows_sum"] + 176 * st["od_query_iters"]
 
 
 # what bounds each kernel in practice (DESIGN.md §4): the roofline is priced against HBM, but the
@@ -121,6 +139,16 @@ def algorithmic_bytes(st):
 LIMITED_BY = {"k_mp_nn": "latency (dependent gathers)", "k_od_assoc": "latency (dependent gathers)",
               "k_mp_nnfit": "latency (dependent gathers, then the fit's VALU)",
               "k_sr_select": "latency (serial greedy picks)", "k_mp_fit": "latency (gathers + VALU)"}
+
+
+def load_traffic(traffic_file):
+    """{kernel: PMC HBM bytes per launch} (profiles/traffic*.json, tools/pmc_traffic.py), or {}"""
+    tpath = os.path.join(ROOT, "profiles", traffic_file)
+    try:
+        d = json.load(open(tpath))
+    except Exception:
+        return {}
+    return {k: v for k, v in d.items() if isinstance(v, (int, float))}
 
 
 def rooflines(st, st_prof, ktimes, psteps, ms_per_step, traffic_file="traffic.json"):
@@ -134,17 +162,12 @@ def rooflines(st, st_prof, ktimes, psteps, ms_per_step, traffic_file="traffic.js
     priced = {k: v for k, v in ktimes.items() if k in alg_kb}
     dom = max(priced.items(), key=lambda kv: kv[1][0])[0] if priced else None
     roof = None
+    tmap = load_traffic(traffic_file)
     if dom:
         tot_ms, launches = ktimes[dom]
         avg_ms = tot_ms / max(launches, 1)
         launches_per_step = launches / psteps
-        traffic = None
-        tpath = os.path.join(ROOT, "profiles", traffic_file)
-        if os.path.exists(tpath):
-            try:
-                traffic = json.load(open(tpath)).get(dom)
-            except Exception:
-                traffic = None
+        traffic = tmap.get(dom)
         alg_launch = alg_kb[dom] / launches_per_step
         achieved = alg_launch / (avg_ms * 1e-3) / 1e9
         roof = {"kernel": dom, "bound": "hbm", "limited_by": LIMITED_BY.get(dom, "hbm"),
@@ -172,14 +195,27 @@ def rooflines(st, st_prof, ktimes, psteps, ms_per_step, traffic_file="traffic.js
             roof_all[k] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                            "ms_per_step": round(ktimes[k][0] / psteps, 4),
                            "bytes_per_step": int(nbytes), "limited_by": LIMITED_BY.get(k, "hbm")}
+            if k in tmap and nbytes > 0:  # PMC HBM bytes (per launch x launches per step) / algorithmic
+                t_step = tmap[k] * ktimes[k][1] / psteps
+                roof_all[k]["traffic_per_step"] = int(t_step)
+                roof_all[k]["traffic_over_algorithmic"] = round(t_step / nbytes, 3)
             if k in SEARCH_KERNELS:
                 ggbs = kb[k] / sec / 1e9
                 roof_all[k]["gathered"] = {"bytes_per_step": int(kb[k]), "achieved_gbs": round(ggbs, 1),
                                            "l2_frac": round(ggbs / L2_GATHER_PEAK_GBS, 4)}
-    # the whole pipeline against HBM: SURVEY.md §8(d)'s algorithmic bytes per step / step time
-    alg = int(st["bytes_sr"] + st["bytes_od"] + st["bytes_mp"])
-    pipeline = {"algorithmic_bytes_per_step": alg, "achieved_gbs": alg / (ms_per_step * 1e-3) / 1e9,
-                "frac": alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+    # the whole pipeline against HBM: the algorithmic bytes the engine's path moves per step / step
+    # time (B_SR + B_OD + B_MP; B_OD in its moments form when the odometry keeps them, which moves no
+    # stored rows), with SURVEY.md §8(d)'s literal figure (the Q12 row re-reads) beside it
+    alg = int(st["bytes_sr"] + moved_od_bytes(st) + st["bytes_mp"])
+    survey = int(st["bytes_sr"] + st["bytes_od"] + st["bytes_mp"])
+    sec = ms_per_step * 1e-3
+    pipeline = {"algorithmic_bytes_per_step": alg, "achieved_gbs": alg / sec / 1e9,
+                "frac": alg / sec / 1e9 / HBM_PEAK_GBS,
+                "bytes_model": ("B_SR + B_OD + B_MP per step (SURVEY.md §8(d)); B_OD's stored-row term "
+                                "as moved: " + ("176 B per query-iteration (per-query moments)"
+                                                if st.get("od_moments") else "32 R_k (rows re-read)")),
+                "survey_literal": {"bytes_per_step": survey, "frac": survey / sec / 1e9 / HBM_PEAK_GBS,
+                                   "note": "B_OD with Sigma 32 R_k, the row re-reads the reference's Q12 implies"},
                 "kernel_busy_ms_per_step": round(sum(v[0] for v in ktimes.values()) / psteps, 4) if ktimes else None}
     return roof, roof_all, pipeline, stage_ms
 

@@ -414,6 +414,7 @@ int loam_create(loam_ctx** out, const loam_config* cfg, int device) {
   if (he != hipSuccess) x->meta = nullptr;
   if (he == hipSuccess) he = hipHostMalloc((void**)&x->xb.h, kXferBytes, hipHostMallocCoherent | hipHostMallocMapped);
   if (he != hipSuccess) x->xb.h = nullptr;
+  else std::memset(x->xb.h, 0, kXferBytes);  // (the deferred valid-point slots are read before written)
   if (he == hipSuccess) he = hipHostGetDevicePointer((void**)&x->xb.d, x->xb.h, 0);
   x->sr_imu = new loamimu::SrQueue();
   std::memset(x->sr_imu, 0, sizeof(loamimu::SrQueue));
@@ -530,17 +531,27 @@ int loam_set_tuning(loam_ctx* x, const char* key, long long value) {
   if (x->st2) HIP_TRY(hipStreamSynchronize(x->st2));
   if (x->st3) HIP_TRY(hipStreamSynchronize(x->st3));
   if (x->st4) HIP_TRY(hipStreamSynchronize(x->st4));
-  x->tune = t;
-  x->reset_ahead();
-  if (!t.batch_streams) {  // (the batch then runs on st / st2 alone)
+  if (t.batch_streams) {
+    // created before anything changes (at the context's stream priority, as
+    // loam_set_stream_priority creates them): a failure leaves the context as it was
+    hipStream_t n3 = x->st3, n4 = x->st4;
+    if (!n3) HIP_TRY(hipStreamCreateWithPriority(&n3, hipStreamNonBlocking, x->prio));
+    if (!n4) {
+      const hipError_t e = hipStreamCreateWithPriority(&n4, hipStreamNonBlocking, x->prio);
+      if (e != hipSuccess) {
+        if (n3 != x->st3) (void)hipStreamDestroy(n3);
+        return fail(LOAM_E_HIP, std::string("hipStreamCreateWithPriority: ") + hipGetErrorString(e));
+      }
+    }
+    x->st3 = n3;
+    x->st4 = n4;
+  } else {  // (the batch then runs on st / st2 alone)
     if (x->st3) (void)hipStreamDestroy(x->st3);
     if (x->st4) (void)hipStreamDestroy(x->st4);
     x->st3 = x->st4 = nullptr;
-  } else {
-    // (at the context's stream priority, as loam_set_stream_priority creates them)
-    if (!x->st3) HIP_TRY(hipStreamCreateWithPriority(&x->st3, hipStreamNonBlocking, x->prio));
-    if (!x->st4) HIP_TRY(hipStreamCreateWithPriority(&x->st4, hipStreamNonBlocking, x->prio));
   }
+  x->tune = t;
+  x->reset_ahead();
   x->drop_graph();  // (captured with the old choices)
   x->od1.tune = x->odb.tune = t;
   x->mp1.tune = x->mpb.tune = x->mpb2.tune = t;
@@ -1093,7 +1104,6 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
     sr_free(x->srb);
     sr_free(x->srb2);
     sr_free(x->srb3);
-  sr_free(x->srb3);
     od_free(x->odb);
     mp_free(x->mpb);
     mp_free(x->mpb2);
@@ -1107,8 +1117,6 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
       sr_free(x->srb);
       sr_free(x->srb2);
       sr_free(x->srb3);
-    sr_free(x->srb3);
-  sr_free(x->srb3);
       od_free(x->odb);
       mp_free(x->mpb);
       mp_free(x->mpb2);
@@ -1138,9 +1146,7 @@ int loam_batch_upload(loam_ctx* x, uint32_t n, const loam_cloud_in* prev, const 
 }
 
 namespace {
-// sweeps [s0, s1) of a batch (sweep 2i = prev[i], 2i + 1 = cur[i]) packed into dst at stride cap,
-// their sizes into n; several host threads for a large batch (the pack is a memory copy per sweep)
-// sweeps [s0, s1) packed back to back (sweep s at off[s]) into dst, on up to eight threads
+// sweeps [s0, s1) of a batch (sweep 2i = prev[i], 2i + 1 = cur[i]) packed back to back (sweep s at off[s]) into dst, on up to eight threads
 void pack_tight(const loam_cloud_in* prev, const loam_cloud_in* cur, size_t s0, size_t s1, const int* off, float4* dst) {
   auto run = [&](size_t a, size_t b) {
     for (size_t s = a; s < b; ++s) {
@@ -1154,23 +1160,6 @@ void pack_tight(const loam_cloud_in* prev, const loam_cloud_in* cur, size_t s0, 
   std::vector<std::thread> th;
   for (size_t t = 1; t < nt; ++t) th.emplace_back(run, s0 + S * t / nt, s0 + S * (t + 1) / nt);
   run(s0, s0 + S / nt);
-  for (auto& t : th) t.join();
-}
-
-void pack_batch(const loam_cloud_in* prev, const loam_cloud_in* cur, uint32_t nprob, int cap, float4* dst, int* n) {
-  const size_t S = 2 * (size_t)nprob;
-  auto run = [&](size_t s0, size_t s1) {
-    for (size_t s = s0; s < s1; ++s) {
-      const loam_cloud_in& c = (s & 1) ? cur[s / 2] : prev[s / 2];
-      pack(c, dst + s * (size_t)cap, 0, c.count);
-      n[s] = (int)c.count;
-    }
-  };
-  const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-  const size_t nt = S >= 64 ? hw : 1;
-  std::vector<std::thread> th;
-  for (size_t t = 1; t < nt; ++t) th.emplace_back(run, S * t / nt, S * (t + 1) / nt);
-  run(0, S / nt);
   for (auto& t : th) t.join();
 }
 
@@ -1199,7 +1188,6 @@ int ensure_second_sets(loam_ctx* x, int slots) {
   if (he != hipSuccess) {
     sr_free(x->srb2);
     sr_free(x->srb3);
-  sr_free(x->srb3);
     mp_free(x->mpb2);
     return fail(LOAM_E_NOMEM, std::string("second batch set allocation failed: ") + hipGetErrorString(he));
   }

@@ -247,7 +247,7 @@ __global__ __launch_bounds__(256) void k_mp_stack(MpBuffers b, MpInput in) {
 // points does the bbox, the voxel keys, a stable radix sort of (voxel, position) pairs over the
 // bits the keys can differ in, and the ordered per-voxel means.  Segments beyond NT*E are appended
 // to the job's big list.
-template <int NT, int E>
+template <int NT, int E, int TAG = 0>  // TAG: which VoxelGrid job (vg_run), a distinct symbol for rocprof
 __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
   constexpr int N = NT * E;
   __shared__ uint32_t ka[N], kb[N];
@@ -488,7 +488,7 @@ __device__ __forceinline__ void vg_idx_segment(const VgJob& j, int s, int b0, in
     }
 }
 
-template <int NT, int E>
+template <int NT, int E, int TAG = 0>  // TAG: which VoxelGrid job (vg_run), a distinct symbol for rocprof
 __global__ __launch_bounds__(NT) void k_vg_idx(VgJob j) {
   constexpr int N = NT * E;
   static_assert(N <= 65536, "16-bit positions");
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(NT) void k_vg_idx(VgJob j) {
 // of NT*E items ranked in registers (tile_rank4), digit bases carried from tile to tile — and the
 // ordered per-voxel means over the sorted arrays.  Rare in VLP-16 batches (long surf stacks); the
 // HDL-64E stack and a large surround map take it.
-template <int NT, int E>
+template <int NT, int E, int TAG = 0>  // TAG: which VoxelGrid job (vg_run), a distinct symbol for rocprof
 __global__ __launch_bounds__(NT) void k_vg_big(VgJob j) {
   constexpr int TILE = NT * E;
   __shared__ uint32_t hist[8][16];
@@ -814,7 +814,10 @@ __global__ __launch_bounds__(NT) void k_vg_merge(VgJob j) {
 // tier2_idx: the second tier is k_vg_idx (16384 points; the long surf stacks) rather than
 // k_vg_radix<1024, 12> (12288; measured faster on the 2k-12k cube segments: at batch 1024 the cubes
 // took 0.68 ms/step with it against 0.85 with k_vg_idx, the stacks 0.86 with k_vg_idx against 1.20)
+// TAG: kVgStack / kVgCubes / kVgSurround, so a kernel trace or PMC pass tells the jobs apart
 constexpr int kVgListGrid = 1024, kVgBigGrid = 256;
+constexpr int kVgStack = 0, kVgCubes = 1, kVgSurround = 2;
+template <int TAG>
 hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true, bool tier2_idx = false) {
   if (j0.nseg == 0) return hipSuccess;
   if (!j0.zeroed) {
@@ -828,25 +831,25 @@ hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true,
   a.big_n = j0.counts;
   int last = 0;  // the list k_vg_big takes
   if (cap1 <= 2048) {
-    hipLaunchKernelGGL((k_vg_radix<256, 8>), dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_vg_radix<256, 8, TAG>), dim3(grid), dim3(256), 0, st, a);
     if (finish) {
       VgJob b = j0;
       b.list = j0.lists[0];
       b.list_n = j0.counts;
       b.big = j0.lists[1];
       b.big_n = j0.counts + 1;
-      if (tier2_idx) hipLaunchKernelGGL((k_vg_idx<1024, 16>), dim3(std::min(j0.nseg, kVgListGrid)), dim3(1024), 0, st, b);
-      else hipLaunchKernelGGL((k_vg_radix<1024, 12>), dim3(std::min(j0.nseg, kVgListGrid)), dim3(1024), 0, st, b);
+      if (tier2_idx) hipLaunchKernelGGL((k_vg_idx<1024, 16, TAG>), dim3(std::min(j0.nseg, kVgListGrid)), dim3(1024), 0, st, b);
+      else hipLaunchKernelGGL((k_vg_radix<1024, 12, TAG>), dim3(std::min(j0.nseg, kVgListGrid)), dim3(1024), 0, st, b);
       last = 1;
     }
   } else {
-    hipLaunchKernelGGL((k_vg_radix<1024, 12>), dim3(grid), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL((k_vg_radix<1024, 12, TAG>), dim3(grid), dim3(1024), 0, st, a);
   }
   if (finish) {
     VgJob c = j0;
     c.list = j0.lists[last];
     c.list_n = j0.counts + last;
-    hipLaunchKernelGGL((k_vg_big<1024, 12>), dim3(std::min(j0.nseg, kVgBigGrid)), dim3(1024), 0, st, c);
+    hipLaunchKernelGGL((k_vg_big<1024, 12, TAG>), dim3(std::min(j0.nseg, kVgBigGrid)), dim3(1024), 0, st, c);
   }
   return hipGetLastError();
 }
@@ -1847,7 +1850,7 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(L
       term_y = 7;
     }
   }
-  // one record per query (MpFit in q_fit): the 5-NN of the last iteration (i0..i3 | i4, d4 bits,
+  // one record per query (MpFit in q_fit): the 5-NN of the last iteration (i0..i3 | i4, 0,
   // distinct, fit valid) and the fit made for them — the seeds and the reuse test in one read
   MpFit* qrec = (MpFit*)b.q_fit + (size_t)p * b.cap_stack;
   for (int q0 = blk.x * NT; q0 < nq; q0 += gridDim.x * NT) {  // (wave-uniform trip count)
@@ -1864,6 +1867,17 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(L
       mp_nn_seed_from(c, q, corner, first, r0, r1, sel, t, work);
       if (corner) knn5_flat<NT, 1, kNnListCap>(c.hcs, c.hcr, c.hcp, c.TC, sel, t, lds + tid, work, 0);
       else knn5_flat<NT, 1, kNnListCap>(c.hss, c.hsr, c.hsp, c.TS, sel, t, lds + tid, work, 0);
+#ifdef LOAM_DIAG_SEARCH2  // (diagnostic build: the search twice, its cost measured by the difference)
+      {
+        Top5 t2;
+        int w2 = 0;
+        asm volatile("" ::: "memory");
+        mp_nn_seed_from(c, q, corner, first, r0, r1, sel, t2, w2);
+        if (corner) knn5_flat<NT, 1, kNnListCap>(c.hcs, c.hcr, c.hcp, c.TC, sel, t2, lds + tid, w2, 0);
+        else knn5_flat<NT, 1, kNnListCap>(c.hss, c.hsr, c.hsp, c.TS, sel, t2, lds + tid, w2, 0);
+        if (t2.i[0] != t.i[0]) nfits += 1 << 20;
+      }
+#endif
       LOAM_CHECK(q < b.cap_stack && (t.i[4] == 0x7fffffff || t.i[4] < (corner ? c.nfc : c.nfs)), q, t.i[4]);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1891,16 +1905,32 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(L
             nb[k] = from[t.i[k]];
           }
           mp_fit_compute(corner, nb, jw, g0, g1);
+#ifdef LOAM_DIAG_FIT2  // (diagnostic build: every fit twice)
+          {
+            float4 h0, h1;
+            asm volatile("" ::: "memory");
+            mp_fit_compute(corner, nb, jw, h0, h1);
+            if (h0.x != g0.x) nfits += 1 << 20;
+          }
+#endif
           qrec[q].g0 = g0;
           qrec[q].g1 = g1;
           valid = true;
         }
         mp_fit_residual(corner, g0, g1, sel, cf, ok);
       }
-      qrec[q].n0 = n0;
-      qrec[q].n1 = make_int4(t.i[4], __float_as_int(t.d[4]), top5_distinct(t), valid ? 1 : 0);
-      qok[q] = (int8_t)ok;
-      qcf[q] = cf;
+      // the record is written only when it changes: a reused fit's list is the stored one (the
+      // next iteration's seeds and reuse test read indices and flags only)
+      const int4 n1 = make_int4(t.i[4], 0, top5_distinct(t), valid ? 1 : 0);
+      if (first || r0.x != n0.x || r0.y != n0.y || r0.z != n0.z || r0.w != n0.w || r1.x != n1.x || r1.z != n1.z ||
+          r1.w != n1.w) {
+        qrec[q].n0 = n0;
+        qrec[q].n1 = n1;
+      }
+      if constexpr (!FUSED) {  // (k_mp_iter reads the rows back; the fused step sums them below)
+        qok[q] = (int8_t)ok;
+        qcf[q] = cf;
+      }
       row_ok = ok != 0;
     }
     if constexpr (FUSED) {  // (outside the branch: every lane takes part)
@@ -2716,7 +2746,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     b.note(hipEventRecord(side->fork[0], st));
     b.note(hipStreamWaitEvent(side->st, side->fork[0], 0));
   }
-  b.note(vg_run(js, fork ? side->st : st, P <= 4 ? 12288 : 2048, !fits, /*tier2_idx=*/true));
+  b.note(vg_run<kVgStack>(js, fork ? side->st : st, P <= 4 ? 12288 : 2048, !fits, /*tier2_idx=*/true));
   if (fork) b.note(hipEventRecord(side->join[0], side->st));
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);
@@ -2833,7 +2863,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   }
   // 2 x 125 cube segments per instance, most of them small: batches start with the 2048-point
   // kernel (many workgroups per CU); a few instances with the 12288-point one (one launch)
-  b.note(vg_run(jv, us, P <= 4 ? 12288 : 2048));
+  b.note(vg_run<kVgCubes>(jv, us, P <= 4 ? 12288 : 2048));
   mark("vg_cubes");
   hipLaunchKernelGGL(k_mp_compact_table<1024>, dim3(P), dim3(1024), 0, us, b);
   hipLaunchKernelGGL(k_mp_compact_copy, dim3(64, P), dim3(256), 0, us, b);
@@ -2968,7 +2998,8 @@ int mp_stream_run(MpBuffers& b, hipStream_t st, const MpInput& in, const int* n,
     if (le == hipSuccess) le = hipEventRecord(b.upd_done, defer);
   }
   // state (kMpStateFloats), istate (kMpStateInts), nreg into the mapped host block, one launch
-  static_assert(kXferMp + 4 * (kMpStateFloats + kMpStateInts + 1) <= kXferBytes, "mapping transfer region");
+  static_assert(kXferMp + 4 * (kMpStateFloats + kMpStateInts + 1) <= kXferMpUpd, "mapping transfer region");
+  static_assert(kXferMpUpd + 8 <= kXferBytes, "deferred valid-point slots");
   const float* sf = (const float*)(io.xb.h + kXferMp);
   const int* si = (const int*)(io.xb.h + kXferMp) + kMpStateFloats;
   const int* pnreg = si + kMpStateInts;
@@ -3083,7 +3114,7 @@ int mp_stream_surround(MpBuffers& b, hipStream_t st, loam_cloud_out* out, std::s
   j.in = b.vin; j.out = b.vout; j.begin = b.vseg_b; j.end = b.vseg_e; j.leaf = b.vseg_leaf;
   j.out_count = b.vseg_cnt; j.nseg = 1; j.total = b.P * b.map_cap;
   j.zeroed = true;  // (by k_mp_surround)
-  b.note(vg_run(j, st, 12288));
+  b.note(vg_run<kVgSurround>(j, st, 12288));
   int cnt = 0;
   hipError_t he = hipMemcpyAsync(&cnt, b.vseg_cnt, sizeof(int), hipMemcpyDeviceToHost, st);
   if (he == hipSuccess) he = hipStreamSynchronize(st);

@@ -1768,6 +1768,24 @@ void sr_free(SrBuffers& b) {
   b = SrBuffers();
 }
 
+// k_sr_ring_fused's tiles wait for the other tiles of their sweep, so a launch is safe only when a
+// whole sweep's tiles can be resident at once: its workgroups per CU (the occupancy its registers
+// and LDS allow, queried once per device) times the CUs.  Other streams' kernels may hold slots
+// for a while, but they never wait on this launch, so the bound is the idle device's.
+int sr_ring_fused_capacity() {
+  static int cap[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cap[dev] == 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sr_ring_fused, kSrThreads, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      per_cu = cus = 0;
+    cap[dev] = std::max(1, per_cu * cus);  // (1: a failed query keeps the two-kernel form below)
+  }
+  return cap[dev];
+}
+
 void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof, hipEvent_t sorted) {
   auto mark = [&](const char* n) { if (prof) prof->mark(n); };
   if (p.imu) {  // (the tile-parallel ring sorts clear them in their tile 0)
@@ -1779,7 +1797,9 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
     hipLaunchKernelGGL(k_sr_ring_sort<true>, dim3(b.S), dim3(kSrThreads), 0, st, b, p);
   } else {
     const int rtiles = (b.cap + kRingTile - 1) / kRingTile;  // <= b.ntiles(): tilecnt rows fit
-    if (kSrRingFused && b.S >= kSrRingFusedMin) {
+    // (a margin of 2: a sweep's tiles fit in half the co-resident slots; HDL-64E's 160k-point
+    // sweeps are 79 tiles against several per CU x 256 CUs on MI355X)
+    if (kSrRingFused && b.S >= kSrRingFusedMin && 2 * rtiles <= sr_ring_fused_capacity()) {
       HIPCHK(hipMemsetAsync(b.ring_sync, 0, sizeof(int), st));
       HIPCHK(hipMemsetAsync(b.tilecnt, 0xff, (size_t)b.S * rtiles * b.R * sizeof(int), st));
       HIPCHK(hipMemsetAsync(b.tileF, 0xff, (size_t)b.S * rtiles * sizeof(int), st));

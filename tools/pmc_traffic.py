@@ -12,11 +12,23 @@ import json
 import sys
 
 
+# the VoxelGrid cascade's kernels carry their job as the last template argument (mp.hip vg_run's
+# TAG): they are reported per job, under bench.py's names for the two jobs of a step
+VG_JOBS = {"0": "vg_stack", "1": "vg_cubes", "2": "vg_surround"}
+
+
 def short(name):
     base = name.replace("(anonymous namespace)", "").split("(")[0]
     if "rocprim" in base:
         return "rocprim_segmented_radix_sort" if "segmented_radix_sort" in name else "rocprim_other"
-    return base.split("::")[-1]
+    base = base.split("::")[-1]
+    if base.startswith(("k_vg_radix<", "k_vg_idx<", "k_vg_big<")):
+        # vg_stack<k_vg_idx>: one instantiation of the job's cascade (summed per launch below)
+        tag = base.rstrip(">").split(",")[-1].strip()
+        return VG_JOBS.get(tag, "vg_other") + "<" + base.split("<")[0] + ">"
+    if base.startswith("k_vg_merge<"):
+        return "vg_cubes<k_vg_merge>"
+    return base
 
 
 def load(path):
