@@ -830,9 +830,6 @@ def main(argv=None):
                            "mp_fit_fraction": st["mp_fits"] / max(st["mp_stack_iters"], 1),
                            "mp_nn_candidates_per_query": st_prof["mp_nn_candidates"] / max(st["mp_stack_iters"], 1),
                            "mp_nn_cells_per_query": st_prof["mp_nn_cells"] / max(st["mp_stack_iters"], 1),
-                           **({"mp_nn_lds_fit_fraction": st_prof["mp_nn_lds_fit"] / st_prof["mp_nn_lds_blocks"],
-                               "mp_nn_lds_staged_per_query": st_prof["mp_nn_lds_staged"] / max(st["mp_stack_iters"], 1)}
-                              if st_prof.get("mp_nn_lds_blocks") else {}),
                            "od_assoc_points_per_query": st_prof["od_assoc_gathered"] / max(st["od_queries"], 1),
                            "od_assoc_boxes_per_query": st_prof["od_assoc_boxes"] / max(st["od_queries"], 1)},
     }

@@ -111,10 +111,6 @@ typedef struct {
   uint64_t mp_nn_cells;         /* hash bucket ranges the 5-NN read */
   uint64_t od_assoc_gathered;   /* Last-cloud points the association loaded (cells, fallback, windows) */
   uint64_t od_assoc_boxes;      /* 64-point chunk boxes the association loaded */
-  uint64_t mp_nn_lds_blocks;    /* query blocks of the LDS-staged 5-NN (tuning nn_lds; profiling pass) */
-  uint64_t mp_nn_lds_fit;       /*   of them whose buckets fit the LDS set and point buffer */
-  uint64_t mp_nn_lds_staged;    /*   queries searched from LDS */
-  uint64_t od_assoc_settled;    /* association queries settled by their certificate (tuning od_assoc_cert) */
 } loam_stats;
 
 typedef struct loam_ctx loam_ctx;
@@ -209,6 +205,9 @@ int loam_batch_run(loam_ctx *ctx);
 int loam_batch_feed(loam_ctx *ctx, uint32_t n, const loam_cloud_in *prev, const loam_cloud_in *cur);
 int loam_batch_sync(loam_ctx *ctx);   /* waits for the work enqueued by loam_batch_run */
 int loam_batch_download(loam_ctx *ctx, loam_pose6 *od_sum, loam_pose6 *aft, loam_stats *stats);
+/* per-problem L-M iteration counts of the last run (odometry, mapping; either pointer may be NULL):
+ * the convergence decisions behind loam_batch_download's poses, for parity checks */
+int loam_batch_iterations(loam_ctx *ctx, int32_t *od_iters, int32_t *mp_iters);
 
 /* scheduling (no reference equivalent; the reference's nodes are OS processes): priority of the
  * context's HIP streams.  priority > 0 = the device's highest stream priority, 0 = normal,
@@ -218,8 +217,9 @@ int loam_set_stream_priority(loam_ctx *ctx, int priority);
 
 /* launch-shape choices of the batch / streaming L-M loops by batch size (no reference equivalent):
  * key = one of od_small_max, od_lm_min, od_lm_max, od_fused_max, mp_small_max, mp_fused_max,
- * nn_lanes, nn_lanes_maxp, od_assoc_wg, nn_lds, od_rows_deep_max, nn_wg, fit_wg, nnfit_max, graph, mp_iter_wide_max, vg_merge, vg_merge_min, sr_ahead, sr_ahead_at, step_pipe, batch_streams, pipe_mp_sets, od_sel_min, od_win_mono, od_win_mono_min, od_moments_min, od_lm_mom_min, od_lm_mom_max,
- * od_assoc_half_min, od_assoc_cert, stream_defer, od_graph, pipe_sr_sets (loam_velodyne-1_amd/csrc/engine.hpp,
+ * nn_lanes, nn_lanes_maxp, od_assoc_wg, od_rows_deep_max, nn_wg, fit_wg, nnfit_max, graph, mp_iter_wide_max,
+ * vg_merge, vg_merge_min, sr_ahead, sr_ahead_at, step_pipe, batch_streams, pipe_mp_sets, od_sel_min, od_win_mono,
+ * od_win_mono_min, od_moments_min, stream_defer, od_graph, pipe_sr_sets (loam_velodyne-1_amd/csrc/engine.hpp,
  * struct Tuning).  Every choice computes the same results bit for bit except od_moments_min (the odometry's
  * stored rows as per-query fp64 moments: within the north star's 1e-4 of the reference);
  * the defaults are the measured fastest.  LOAM_E_INVAL for an unknown key or a value out of range.

@@ -89,8 +89,7 @@ STAT_U64 = ("n_raw", "n_ring", "n_sharp", "n_less_sharp", "n_flat", "n_less_flat
 
 
 STAT_BRANCH = ("od_degenerate_steps", "od_nan_skips", "mp_degenerate_steps", "mp_grid_shifts")
-STAT_WORK = ("mp_nn_candidates", "mp_nn_cells", "od_assoc_gathered", "od_assoc_boxes",
-             "mp_nn_lds_blocks", "mp_nn_lds_fit", "mp_nn_lds_staged", "od_assoc_settled")
+STAT_WORK = ("mp_nn_candidates", "mp_nn_cells", "od_assoc_gathered", "od_assoc_boxes")
 
 
 class ChainOut(ctypes.Structure):
@@ -110,7 +109,7 @@ class Stats(ctypes.Structure):
 EXPORTS = ("loam_config_default", "loam_create", "loam_destroy", "loam_last_error", "loam_imu",
            "loam_scan_registration", "loam_odometry", "loam_mapping", "loam_mapping_surround",
            "loam_maintenance", "loam_chain_sweep",
-           "loam_batch_upload", "loam_batch_feed", "loam_batch_run", "loam_batch_sync", "loam_batch_download", "loam_get_stats",
+           "loam_batch_upload", "loam_batch_feed", "loam_batch_run", "loam_batch_sync", "loam_batch_download", "loam_batch_iterations", "loam_get_stats",
            "loam_set_profiling", "loam_get_kernel_times", "loam_set_stream_priority", "loam_set_tuning",
            "loam_get_tuning",
            # include/loam/loam_bag.h: recorded-sweep ingest (rosbag v2, PointCloud2, Imu)
@@ -150,6 +149,7 @@ def lib():
         L.loam_get_tuning.argtypes = [PP, ctypes.c_char_p, P(ctypes.c_longlong)]
         L.loam_get_kernel_times.argtypes = [PP, ctypes.c_char_p, ctypes.c_uint32]
         L.loam_batch_download.argtypes = [PP, P(Pose6), P(Pose6), P(Stats)]
+        L.loam_batch_iterations.argtypes = [PP, P(ctypes.c_int32), P(ctypes.c_int32)]
         L.loam_get_stats.argtypes = [PP, P(Stats)]
         L.loam_msg_from_pose.argtypes = [ctypes.c_int, ctypes.c_double, P(Pose6), P(Pose6), P(OdometryMsg), P(TfMsg)]
         L.loam_pose_from_msg.argtypes = [P(OdometryMsg), P(Pose6), P(Pose6)]
@@ -364,6 +364,14 @@ class Engine:
         st = Stats()
         _check(lib().loam_batch_download(self.h, od, aft, ctypes.byref(st)))
         return (np.array([p.arr() for p in od]), np.array([p.arr() for p in aft]), st.as_dict())
+
+    def batch_iterations(self):
+        """per-problem (odometry, mapping) L-M iteration counts of the last run"""
+        od = np.zeros(self.n, np.int32)
+        mp = np.zeros(self.n, np.int32)
+        P = ctypes.POINTER(ctypes.c_int32)
+        _check(lib().loam_batch_iterations(self.h, od.ctypes.data_as(P), mp.ctypes.data_as(P)))
+        return od, mp
 
 
 def maintenance(odom_sum, bef, aft):

@@ -1568,6 +1568,21 @@ int loam_batch_sync(loam_ctx* x) {
   return LOAM_OK;
 }
 
+int loam_batch_iterations(loam_ctx* x, int32_t* od_iters, int32_t* mp_iters) {
+  if (!x || x->P == 0) return fail(LOAM_E_INVAL, "no batch");
+  HIP_TRY(hipSetDevice(x->device));
+  const int P = x->P;
+  for (hipStream_t s : {x->st, x->st2, x->st3, x->st4})
+    if (s) HIP_TRY(hipStreamSynchronize(s));
+  if (od_iters) {
+    std::vector<int> ist((size_t)P * kOdStateInts);
+    HIP_TRY(hipMemcpy(ist.data(), x->odb.istate, ist.size() * sizeof(int), hipMemcpyDeviceToHost));
+    for (int i = 0; i < P; ++i) od_iters[i] = ist[(size_t)i * kOdStateInts + kIsIters];
+  }
+  if (mp_iters) HIP_TRY(mp_batch_iters(x->mpbuf(x->mp_last), x->st, mp_iters));
+  return LOAM_OK;
+}
+
 int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_stats* stats) {
   if (!x || x->P == 0) return fail(LOAM_E_INVAL, "no batch");
   HIP_TRY(hipSetDevice(x->device));
@@ -1619,7 +1634,6 @@ int loam_batch_download(loam_ctx* x, loam_pose6* od_sum, loam_pose6* aft, loam_s
     s.od_nan_skips += (uint64_t)q[kIsNanSkips];
     s.od_assoc_gathered += (uint64_t)(uint32_t)q[kIsGathered];
     s.od_assoc_boxes += (uint64_t)(uint32_t)q[kIsBoxes];
-    s.od_assoc_settled += (uint64_t)(uint32_t)q[kIsCert];
     const uint64_t nq = q[kIsAssoc] ? (uint64_t)(q[kIsQueries] / q[kIsAssoc]) : 0, it = (uint64_t)q[kIsIters];
     s.od_query_iters += nq * it;
     s.od_row_evals += nq * it * (it + 1) / 2;

@@ -49,7 +49,6 @@ struct Tuning {
   int nn_lanes_maxp = 256; //   for P <= this
   int od_assoc_wg = 0;     // k_od_assoc query waves (workgroups) per problem (batches, P >= 64; 0: the query
                            // capacity / 9, i.e. 64 for VLP-16, 256 for HDL-64E)
-  int nn_lds = 0;          // batch 5-NN with the workgroup's map cells staged in LDS (k_mp_nn_lds)
   int od_rows_deep_max = 0;  // k_od_rows with 8 (not 2) stored rows' loads in flight for P <= this
   int nn_wg = 0;           // k_mp_nn workgroups per problem (0: one pass over a VLP-16 stack)
   int fit_wg = 0;          // k_mp_fit workgroups per problem (0: likewise)
@@ -90,12 +89,6 @@ struct Tuning {
                            // first (unseeded) round, bit 1 the seeded ones (round 4, 1024 problems:
                            // k_od_assoc 2.76 -> 2.42 ms/step with both)
   int od_win_mono_min = 2; // ... for P >= this (config 3's chain, P = 1: 0.733 -> 0.743 ms/sweep with them)
-  int od_assoc_half_min = 1 << 30;  // k_od_assoc with two queries per wave (half_hash_nn /
-                           // half_window_mono) for P >= this (with k_od_sel: P >= od_sel_min)
-  int od_assoc_cert = 0;   // association queries of the seeded rounds settled by their last full search's
-                           // certificate when it still separates every choice from its rivals (exact)
-  int od_lm_mom_min = 1;   // with the moments: k_od_lm_mom (an association round's 5 iterations in one
-  int od_lm_mom_max = 0;   //   workgroup per problem) for od_lm_mom_min <= P <= od_lm_mom_max
   int stream_defer = 1;    // loam_chain_sweep leaves the bookkeeping only the next sweep reads to the second
                            // stream: mapping's map update (insertion, per-cube VoxelGrid, compaction) after
                            // the L-M, odometry's hash tables of the new Last clouds after TransformToEnd.
@@ -120,7 +113,7 @@ struct Tuning {
                     {"od_lm_max", &od_lm_max, 0, 1 << 20}, {"od_fused_max", &od_fused_max, 0, 1 << 20},
                     {"mp_small_max", &mp_small_max, 0, 1 << 20}, {"mp_fused_max", &mp_fused_max, 0, 1 << 20},
                     {"nn_lanes", &nn_lanes, 1, 4}, {"nn_lanes_maxp", &nn_lanes_maxp, 0, 1 << 20},
-                    {"od_assoc_wg", &od_assoc_wg, 0, 1024}, {"nn_lds", &nn_lds, 0, 1},
+                    {"od_assoc_wg", &od_assoc_wg, 0, 1024},
                     {"od_rows_deep_max", &od_rows_deep_max, 0, 1 << 20}, {"nn_wg", &nn_wg, 0, 4096},
                     {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20},
                     {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20},
@@ -129,9 +122,7 @@ struct Tuning {
                     {"step_pipe", &step_pipe, 0, 1 << 20}, {"batch_streams", &batch_streams, 0, 1},
                     {"pipe_mp_sets", &pipe_mp_sets, 1, 2}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
                     {"od_win_mono", &od_win_mono, 0, 3}, {"od_win_mono_min", &od_win_mono_min, 1, 1 << 20},
-                    {"od_moments_min", &od_moments_min, 1, 1 << 30}, {"od_lm_mom_min", &od_lm_mom_min, 1, 1 << 20},
-                    {"od_lm_mom_max", &od_lm_mom_max, 0, 1 << 20},
-                    {"od_assoc_half_min", &od_assoc_half_min, 1, 1 << 30}, {"od_assoc_cert", &od_assoc_cert, 0, 1}};
+                    {"od_moments_min", &od_moments_min, 1, 1 << 30}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {
         if (read) {

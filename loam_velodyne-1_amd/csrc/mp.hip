@@ -1148,9 +1148,6 @@ __global__ void k_mp_lm_begin(MpBuffers b) {
   ist[kMiDegSteps] = 0;
   ist[kMiNnCand] = 0;
   ist[kMiNnCells] = 0;
-  ist[kMiLdsBlocks] = 0;
-  ist[kMiLdsFit] = 0;
-  ist[kMiLdsStaged] = 0;
 }
 
 // One L-M iteration's correspondences (:714-877), lane per stack point (corner, then surf), in
@@ -1505,195 +1502,6 @@ __global__ __launch_bounds__(kMpNnThreads) __attribute__((amdgpu_waves_per_eu(L 
   }
   if (!COUNT) return;
   if (sub != 0) work = 0;  // (every lane of a group counted the group's whole list)
-  const int ncand = wave_sum(work & ((1 << kWorkCellShift) - 1)), ncell = wave_sum(work >> kWorkCellShift);
-  if (lane_id() == 0 && ncand) {
-    atomicAdd((int*)&ist[kMiNnCand], ncand);
-    atomicAdd((int*)&ist[kMiNnCells], ncell);
-  }
-}
-
-// The same 5-NN with the map's cells staged in LDS per workgroup (north_star: "LDS-staged voxel
-// cells"; src/laserMapping.cpp:714-719, 821-826).  A workgroup takes NT consecutive stack points
-// (VoxelGrid order: spatial neighbours), so their 3x3x3 cell neighbourhoods overlap heavily (the
-// candidate walks of 256 queries read ~15x fewer distinct map points than candidates).  Per block:
-//   1. each lane maps its point, bounds the search with its seeds (as mp_nn_query) and lists its
-//      non-empty buckets within the bound in an LDS hash set of the block's buckets (key = the
-//      bucket's one-word record: start | count << 19, unique per non-empty bucket);
-//   2. two block scans give each listed bucket its LDS offset; the buckets' points are copied into
-//      LDS as one flat, mostly contiguous copy (runs of consecutive hash-ordered points);
-//   3. each lane walks its buckets' points from LDS into the same seeded top-5 (the 5-NN of a point
-//      set does not depend on the visiting order: ordered (distance, index) keys).
-// Lanes whose cell records do not fit (kRecNone) or whose kind differs from the block's first
-// lane's (the one block that straddles corner -> surf) search from global memory (knn5), and so do
-// all lanes of a block whose buckets overflow the set or the point buffer.  Results are identical
-// to k_mp_nn's.
-#ifndef LOAM_NN_LDS_PTS
-#define LOAM_NN_LDS_PTS 1024
-#endif
-constexpr int kNnLdsThreads = 256;
-constexpr int kNnLdsPts = LOAM_NN_LDS_PTS;  // staged points per block (16 B each)
-constexpr int kNnLdsSlots = 1024;           // hash-set slots of the block's buckets (power of 2)
-constexpr int kNnLdsCap = 512;              // distinct buckets a block may stage
-template <bool COUNT>
-__global__ __launch_bounds__(kNnLdsThreads) void k_mp_nn_lds(MpBuffers b) {
-  constexpr int NT = kNnLdsThreads;
-  const XcdBlock blk = xcd_block();
-  const int p = blk.y, tid = threadIdx.x;
-  const int* ist = b.istate + (size_t)p * kMpStateInts;
-  if (!ist[kMiLmRan] || ist[kMiStop]) return;  // (uniform over the workgroup)
-  const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
-  const int nq = nsc + nss;
-  __shared__ uint16_t lst[27 * NT];           // the lane's listed buckets as set slots, stride NT
-  __shared__ uint32_t key[kNnLdsSlots];       // bucket record, 0 = free
-  __shared__ uint16_t soff[kNnLdsSlots];      // the bucket's first point in pts
-  __shared__ uint32_t cstart[kNnLdsCap];      // staged buckets in slot order: start in the hash points
-  __shared__ uint16_t coff[kNnLdsCap + 1];    //   and offset in pts
-  __shared__ float4 pts[kNnLdsPts];
-  __shared__ int scan_ws[NT / 64 + 1];
-  __shared__ int sh_over;
-  const bool first = ist[kMiIters] == 0;
-  const loampose::MapRot r = rot_load(b, p);
-  const MpNnCtx c = mp_nn_ctx(b, p);
-  int work = 0;
-  for (int q0 = blk.x * NT; q0 < nq; q0 += gridDim.x * NT) {
-    const int q = q0 + tid;
-    // (the previous block's walks are done: the set and the staged points are free)
-    for (int s = tid; s < kNnLdsSlots; s += NT) key[s] = 0u;
-    if (tid == 0) sh_over = 0;
-    __syncthreads();
-    const bool kind_c = q0 < nsc;  // the block's kind (its first lane's)
-    const bool act = q < nq, corner = q < nsc;
-    float4 sel = make_float4(0, 0, 0, 0);
-    Top5 t;
-    int n = 0, total = 0;
-    bool staged = act && corner == kind_c;  // else: the global search below
-    if (act) {
-      sel = loampose::point_to_map(r, c.stack[corner ? q : b.capC + (q - nsc)]);
-      mp_nn_seed(c, q, corner, first, sel, t, work);
-    }
-    if (staged) {
-      const uint32_t* rec = corner ? c.hcr : c.hsr;
-      const int T = corner ? c.TC : c.TS;
-      if (T <= 0) {
-        staged = false;  // an empty map: nothing to search (the global path returns at once)
-      } else {
-        const int cx = cell_of(sel.x, 1.0f), cy = cell_of(sel.y, 1.0f), cz = cell_of(sel.z, 1.0f);
-        const float gxl = sel.x - (float)cx, gyl = sel.y - (float)cy, gzl = sel.z - (float)cz;
-        const float gxh = (float)(cx + 1) - sel.x, gyh = (float)(cy + 1) - sel.y, gzh = (float)(cz + 1) - sel.z;
-        const float bound = t.d[4];
-        uint32_t rg[27];
-#pragma unroll
-        for (int o = 0; o < 27; ++o) {
-          const int cc = kCellOrder[o];
-          const int dx = cc % 3 - 1, dy = (cc / 3) % 3 - 1, dz = cc / 9 - 1;
-          const float gx = dx < 0 ? gxl : (dx > 0 ? gxh : 0.0f);
-          const float gy = dy < 0 ? gyl : (dy > 0 ? gyh : 0.0f);
-          const float gz = dz < 0 ? gzl : (dz > 0 ? gzh : 0.0f);
-          const float bd = sqdist(gx, gy, gz, 0.0f, 0.0f, 0.0f);
-          rg[o] = 0;
-          if (bd < 1.0f && bd <= bound) rg[o] = rec[cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1)];
-        }
-#pragma unroll
-        for (int o = 0; o < 27; ++o)
-          if (rg[o] == kRecNone) staged = false;
-        if (staged) {
-#pragma unroll
-          for (int o = 0; o < 27; ++o) {
-            const uint32_t e = rg[o];
-            if ((e >> 19) == 0) continue;
-            uint32_t h = (e * 2654435761u) >> 22;  // 10 bits: kNnLdsSlots
-            int probe = 0;
-            for (;;) {
-              const uint32_t old = atomicCAS(&key[h], 0u, e);
-              if (old == 0u || old == e) break;
-              h = (h + 1) & (kNnLdsSlots - 1);
-              if (++probe == kNnLdsSlots) { h = 0xffffu; break; }
-            }
-            if (h == 0xffffu) { sh_over = 1; continue; }
-            lst[n * NT + tid] = (uint16_t)h;
-            ++n;
-            total += (int)(e >> 19);
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // offsets of the listed buckets (slot order): thread tid owns slots tid * 4 .. tid * 4 + 3
-    constexpr int SPT = kNnLdsSlots / NT;
-    int cnt4[SPT], occ = 0, npts = 0;
-#pragma unroll
-    for (int u = 0; u < SPT; ++u) {
-      const uint32_t e = key[tid * SPT + u];
-      cnt4[u] = (int)(e >> 19);
-      occ += e ? 1 : 0;
-      npts += cnt4[u];
-    }
-    int nocc = 0, tpts = 0;
-    int r0 = block_excl_scan<NT>(occ, scan_ws, nocc);
-    int o0 = block_excl_scan<NT>(npts, scan_ws, tpts);
-    const bool fit = !sh_over && nocc <= kNnLdsCap && tpts <= kNnLdsPts;  // (uniform)
-    if (fit) {
-#pragma unroll
-      for (int u = 0; u < SPT; ++u) {
-        const uint32_t e = key[tid * SPT + u];
-        if (e) {
-          soff[tid * SPT + u] = (uint16_t)o0;
-          cstart[r0] = e & ((1u << 19) - 1);
-          coff[r0] = (uint16_t)o0;
-          ++r0;
-          o0 += cnt4[u];
-        }
-      }
-      if (tid == 0) coff[nocc] = (uint16_t)tpts;
-    }
-    __syncthreads();
-    if (fit && nocc > 0) {
-      // the flat copy: point i of the staged run belongs to the last bucket whose offset is <= i
-      const float4* hp = kind_c ? c.hcp : c.hsp;
-      for (int i = tid; i < tpts; i += NT) {
-        int lo = 0, hi = nocc - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if ((int)coff[mid] <= i) lo = mid; else hi = mid - 1;
-        }
-        pts[i] = hp[cstart[lo] + (uint32_t)(i - (int)coff[lo])];
-      }
-    }
-    __syncthreads();
-    if (act) {
-      if (staged && fit) {
-        work += total + (n << kWorkCellShift);
-        for (int k = 0; k < n; ++k) {
-          const int s = lst[k * NT + tid];
-          const int cnt = (int)(key[s] >> 19);
-          const float4* src = pts + soff[s];
-          for (int j = 0; j < cnt; j += 4) {
-            float4 a[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) a[u] = src[min(j + u, cnt - 1)];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              if (j + u < cnt) top5_offer_new(t, sqdist(a[u].x, a[u].y, a[u].z, sel.x, sel.y, sel.z), __builtin_bit_cast(int, a[u].w));
-          }
-        }
-      } else if (corner) {  // (a lane the block could not stage: the whole search from global memory)
-        knn5(c.hcs, c.hcp, c.TC, sel, t, work);
-      } else {
-        knn5(c.hss, c.hsp, c.TS, sel, t, work);
-      }
-      mp_nn_store(c, q, t);
-    }
-    if (COUNT) {
-      const int ns = wave_sum((act && staged && fit) ? 1 : 0);
-      if (lane_id() == 0 && ns) atomicAdd((int*)&ist[kMiLdsStaged], ns);
-      if (tid == 0) {
-        atomicAdd((int*)&ist[kMiLdsBlocks], 1);
-        if (fit) atomicAdd((int*)&ist[kMiLdsFit], 1);
-      }
-    }
-    __syncthreads();
-  }
-  if (!COUNT) return;
   const int ncand = wave_sum(work & ((1 << kWorkCellShift) - 1)), ncell = wave_sum(work >> kWorkCellShift);
   if (lane_id() == 0 && ncand) {
     atomicAdd((int*)&ist[kMiNnCand], ncand);
@@ -2798,10 +2606,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     const int gnn = b.tune.nn_wg > 0 ? b.tune.nn_wg : gq * (kMpQueryThreads / kMpNnThreads);
     // L lanes per query for shares of a few hundred problems (the slowest wave is the launch)
     const int L = P <= b.tune.nn_lanes_maxp ? b.tune.nn_lanes : 1;
-    if (b.tune.nn_lds) {  // the block's cells staged in LDS (k_mp_nn_lds: 256 queries per workgroup)
-      if (prof) hipLaunchKernelGGL(k_mp_nn_lds<true>, dim3(gq, P), dim3(kNnLdsThreads), 0, st, b);
-      else hipLaunchKernelGGL(k_mp_nn_lds<false>, dim3(gq, P), dim3(kNnLdsThreads), 0, st, b);
-    } else if (L == 4) {
+    if (L == 4) {
       if (prof) hipLaunchKernelGGL((k_mp_nn<true, 4>), dim3(gnn * 4, P), dim3(kMpNnThreads), 0, st, b);
       else hipLaunchKernelGGL((k_mp_nn<false, 4>), dim3(gnn * 4, P), dim3(kMpNnThreads), 0, st, b);
     } else if (L == 2) {
@@ -3173,6 +2978,16 @@ void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, int buf, const FeatView&
   mp_frame(b, in, st, prof, false, nullptr, -1, side);
 }
 
+// per-instance mapping L-M iteration counts of the last frame (loam_batch_iterations)
+hipError_t mp_batch_iters(MpBuffers& b, hipStream_t st, int32_t* iters) {
+  std::vector<int> si((size_t)b.P * kMpStateInts);
+  hipError_t he = hipStreamSynchronize(st);
+  if (he == hipSuccess) he = hipMemcpy(si.data(), b.istate, si.size() * sizeof(int), hipMemcpyDeviceToHost);
+  if (he == hipSuccess)
+    for (int p = 0; p < b.P; ++p) iters[p] = si[(size_t)p * kMpStateInts + kMiIters];
+  return he;
+}
+
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err) {
   std::vector<float> sf((size_t)b.P * kMpStateFloats);
   std::vector<int> si((size_t)b.P * kMpStateInts);
@@ -3203,9 +3018,6 @@ int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats*
       stats->mp_grid_shifts += (uint64_t)q[kMiShifts];
       stats->mp_nn_candidates += (uint64_t)(uint32_t)q[kMiNnCand];
       stats->mp_nn_cells += (uint64_t)(uint32_t)q[kMiNnCells];
-      stats->mp_nn_lds_blocks += (uint64_t)(uint32_t)q[kMiLdsBlocks];
-      stats->mp_nn_lds_fit += (uint64_t)(uint32_t)q[kMiLdsFit];
-      stats->mp_nn_lds_staged += (uint64_t)(uint32_t)q[kMiLdsStaged];
     }
   }
   return LOAM_OK;

@@ -28,9 +28,8 @@ enum { kMiCenW = 0, kMiCenH, kMiCenD, kMiDegen, kMiNValid, kMiIters, kMiRows, kM
        kMiShifts,    // cube-grid slab shifts of this frame's recentring (the reference's passes)
        kMiNnCand,    // map points the 5-NN evaluated this frame (seeds included)
        kMiNnCells,   // hash bucket ranges the 5-NN read this frame
-       kMiLdsBlocks, kMiLdsFit, kMiLdsStaged,  // k_mp_nn_lds<COUNT>: blocks, blocks staged, queries staged
        kMpStateInts = 28 };
-static_assert(kMiLdsStaged < kMpStateInts, "istate layout");
+static_assert(kMiNnCells < kMpStateInts, "istate layout");
 
 // one mapping frame's inputs for every instance (device pointers)
 struct MpInput {
@@ -196,6 +195,7 @@ void mp_batch_frame1(MpBuffers& b, const OdBuffers& od, int buf, const FeatView&
 void mp_batch_frame2(MpBuffers& b, const OdBuffers& od, int buf, const FeatView& fcur, hipStream_t st,
                      Prof* prof = nullptr, const SideStream* side = nullptr);
 int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats* stats, std::string& err);
+hipError_t mp_batch_iters(MpBuffers& b, hipStream_t st, int32_t* iters);
 
 }  // namespace loam
 #endif

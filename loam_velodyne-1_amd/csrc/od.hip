@@ -406,17 +406,12 @@ struct WinBound {
 // kind 0 / 1 (corner / surf, 1 m cells only; -1: none) with mono: when the nearest point lies in the
 // 27 cells, the cells' points that belong to its window sets (window_member, fwd_end) bound the
 // window minima (wb): a chunk beyond such a member cannot hold the minimum.
-// cert_l (h = 1 only): when the minimum lies within one cell, a lower bound of the squared distance
-// from q of every point of the cloud but the minimum (the second smallest candidate, the skipped
-// cells' boxes, 1 beyond the 27 cells); 0 when the chunk fallback ran (no bound kept)
 LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const float4* cloud, const float4* ch,
                              int n, float h, float inv_h, float4 q, float bound, int* cells, int& wpts, int& wbox,
-                             int kind = -1, int fwd_end = 0, bool mono = false, WinBound* wb = nullptr,
-                             float* cert_l = nullptr) {
+                             int kind = -1, int fwd_end = 0, bool mono = false, WinBound* wb = nullptr) {
   const int lane = lane_id();
   const int cx = cell_of(q.x, inv_h), cy = cell_of(q.y, inv_h), cz = cell_of(q.z, inv_h);
   int bucket = -1, b0 = 0, cnt = 0;
-  float skip_bd = 3.4e38f;  // a skipped cell's box distance (cert_l)
   if (lane < 27 && T > 0) {
     const int dx = lane % 3 - 1, dy = (lane / 3) % 3 - 1, dz = lane / 9 - 1;
     const float4 lo = make_float4((float)(cx + dx) * h, (float)(cy + dy) * h, (float)(cz + dz) * h, 0.0f);
@@ -428,8 +423,6 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
       b0 = rg.x;
       cnt = rg.y - b0;
       LOAM_CHECK(b0 >= 0 && cnt >= 0 && b0 + cnt <= n, b0, cnt);
-    } else {
-      skip_bd = bd;
     }
   }
   // (two of the 27 cells may share a bucket: its points are then offered twice, which does not
@@ -448,7 +441,6 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
     LOAM_CHECK(cells[32 + k] + (t - cells[k]) < n && cells[32 + k] >= 0, cells[32 + k] + (t - cells[k]), n);
     return hp[cells[32 + k] + (t - cells[k])];
   };
-  uint64_t second = ~0ull;  // (cert_l: the lane's second smallest distinct key)
   float4 a0 = make_float4(0, 0, 0, 0);  // the lane's first candidate, kept for the window bounds
   for (int t = lane; t < total; t += 64) {
     const float4 a = cand(t);
@@ -456,22 +448,10 @@ LOAM_D uint64_t wave_hash_nn(const int* start, const float4* hp, int T, const fl
     const float d = sqdist(a.x, a.y, a.z, q.x, q.y, q.z);
     const uint32_t tag = (uint32_t)__float_as_int(a.w);  // index | ring << 24
     const uint64_t key = ((uint64_t)fkey(d) << 32) | ((tag & 0xffffffu) << 8) | (tag >> 24);
-    if (cert_l) {
-      second = key < best ? best : (key != best && key < second ? key : second);
-    }
     best = key < best ? key : best;
   }
-  const uint64_t lbest = best;
   best = wave_min_u64_x(best);
   __builtin_amdgcn_wave_barrier();
-  if (cert_l) {
-    *cert_l = 0.0f;
-    if (best != ~0ull && __uint_as_float((uint32_t)(best >> 32)) < 1.0f) {
-      const uint64_t sec = wave_min_u64_x(lbest == best ? second : lbest);
-      const float ds = sec == ~0ull ? 3.4e38f : __uint_as_float((uint32_t)(sec >> 32));
-      *cert_l = fminf(fminf(ds, wave_min_f_x(skip_bd)), 1.0f);
-    }
-  }
   if (best != ~0ull && __uint_as_float((uint32_t)(best >> 32)) < h * h) {
     if (kind >= 0 && mono && D(__uint_as_float((uint32_t)(best >> 32))) < 25) {
       const int c = (int)((uint32_t)best >> 8), scan = (int)((uint32_t)best & 255u);
@@ -658,12 +638,9 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
 #define LOAM_WIN_TIGHTEN 0  // bounds tightened after every wave step: 0 never (the seeds' / cells' only),
 #endif                      // 1 always, 2 in the first (unseeded) round
 
-// cert (optional, no tightening): per category a lower bound of the squared distance from sel of every
-// member but the minimum (the second smallest distinct key, the boxes of the sub-chunks not visited
-// that may hold the category): cert[0] the same ring (surf min2), cert[1] the others
 LOAM_D void wave_window_mono(const float4* L, const float4* fb, const int* rs, int c, int scan, int fwd_end,
                              float4 sel, bool want_same, const WinBound& wb, bool tighten, uint64_t& best2,
-                             uint64_t& best3, int& wpts, int& wbox, float* cert = nullptr) {
+                             uint64_t& best3, int& wpts, int& wbox) {
   constexpr int PER = 64 / kSub;            // sub-chunks visited per wave step
   constexpr int BPL = kSub == 16 ? 2 : 1;   // boxes per lane per box step
   const int lane = lane_id();
@@ -677,8 +654,6 @@ LOAM_D void wave_window_mono(const float4* L, const float4* fb, const int* rs, i
   d2 = fminf(d2, 25.0f);
   d3 = fminf(d3, 25.0f);
   const int k0 = w0 / kSub, k1 = (w1 - 1) / kSub;  // sub-chunks overlapping [w0, w1)
-  uint64_t s2 = ~0ull, s3 = ~0ull;      // (cert: the lane's second smallest distinct keys)
-  float f2 = 3.4e38f, f3 = 3.4e38f;     // (cert: boxes of the sub-chunks not visited)
   for (int g = k0; g <= k1; g += 64 * BPL) {
     wbox += min(64 * BPL, k1 - g + 1);
     float bd[BPL];
@@ -696,10 +671,6 @@ LOAM_D void wave_window_mono(const float4* L, const float4* fb, const int* rs, i
         ho[u] = lo < rs0 || hi > rs1;
       }
       live[u] = ~0ull;
-      if (cert && !((hs[u] && bd[u] <= d2) || (ho[u] && bd[u] <= d3))) {
-        if (hs[u]) f2 = fminf(f2, bd[u]);
-        if (ho[u]) f3 = fminf(f3, bd[u]);
-      }
     }
     while (true) {
       // the boxes that may still hold a point at or below a wanted category's bound
@@ -734,12 +705,10 @@ LOAM_D void wave_window_mono(const float4* L, const float4* fb, const int* rs, i
         const uint64_t key = ((uint64_t)fkey(d) << 32) | pos;
         if (j >= rs0 && j < rs1) {
           if (want_same) {
-            if (cert) s2 = key < k2 ? k2 : (key != k2 && key < s2 ? key : s2);
             k2 = key < k2 ? key : k2;
             ds = d;
           }
         } else {
-          if (cert) s3 = key < k3 ? k3 : (key != k3 && key < s3 ? key : s3);
           k3 = key < k3 ? key : k3;
           dot = d;
         }
@@ -751,18 +720,6 @@ LOAM_D void wave_window_mono(const float4* L, const float4* fb, const int* rs, i
     }
   }
   const uint64_t kNone = (uint64_t)fkey(25.0f) << 32;  // keys below this have d < 25 (:491, :602)
-  if (cert) {
-    // the minimum's runner-up over the wave (lanes holding the minimum offer their second key), or
-    // the minimum itself when it does not count (>= 25 m²: then every member is a rival of "none")
-    auto lower = [&](uint64_t k, uint64_t sk, float fl) {
-      const uint64_t m = wave_min_u64_x(k);
-      const uint64_t r = m >= kNone ? m : wave_min_u64_x(k == m ? sk : k);
-      const float dr = r == ~0ull ? 3.4e38f : __uint_as_float((uint32_t)(r >> 32));
-      return fminf(dr, wave_min_f_x(fl));
-    };
-    cert[0] = want_same ? lower(k2, s2, f2) : 0.0f;
-    cert[1] = lower(k3, s3, f3);
-  }
   best2 = want_same ? wave_min_u64_x(k2) : ~0ull;
   best3 = wave_min_u64_x(k3);
   if (best2 >= kNone) best2 = ~0ull;
@@ -782,152 +739,6 @@ LOAM_D uint64_t mono_seed_key(const int* rs, int c, int scan, int fwd_end, int j
 LOAM_D int mono_decode(int c, uint64_t k) {
   const uint32_t o = (uint32_t)k;
   return o >= (1u << 30) ? c - 1 - (int)(o - (1u << 30)) : c + 1 + (int)o;
-}
-
-// ---- two queries per wave (tuning od_assoc_half): lanes 32h .. 32h + 31 serve query h ----
-// The association is bound by its per-query chain of dependent gathers and by the wave-wide
-// reductions / ballots of each step (about half its cycles issue VALU, the rest wait): with half a
-// wave per query, two chains progress per wave and each shuffle / ballot serves both queries.  The
-// searches below are wave_hash_nn (kind -1) and wave_window_mono restated over 32 lanes; they visit
-// the same candidates and keep the same (distance, index / walk position) minima, so the results are
-// identical.
-static_assert(kSub <= 32, "half-wave windows take kSub <= 32 point sub-chunks");
-LOAM_D int half_lane() { return lane_id() & 31; }
-LOAM_D uint32_t half_bits(uint64_t m) { return (uint32_t)(m >> (lane_id() & 32)); }
-
-// wave_hash_nn (1 m cells, no window bounds) over the half's 32 lanes; cells: the half's 64 ints of LDS
-LOAM_D uint64_t half_hash_nn(const int* start, const float4* hp, int T, const float4* cloud, const float4* ch,
-                             int n, float4 q, float bound, int* cells, int& wpts, int& wbox) {
-  const int hl = half_lane();
-  const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
-  int b0 = 0, cnt = 0;
-  if (hl < 27 && T > 0) {
-    const int dx = hl % 3 - 1, dy = (hl / 3) % 3 - 1, dz = hl / 9 - 1;
-    const float4 lo = make_float4((float)(cx + dx), (float)(cy + dy), (float)(cz + dz), 0.0f);
-    const float4 hi = make_float4((float)(cx + dx + 1), (float)(cy + dy + 1), (float)(cz + dz + 1), 0.0f);
-    const float bd = box_d2(lo, hi, q);
-    if (bd < 1.0f && bd <= bound) {
-      const int bucket = (int)(cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1));
-      const int2 rg = load_pair(start + bucket);
-      b0 = rg.x;
-      cnt = rg.y - b0;
-      LOAM_CHECK(b0 >= 0 && cnt >= 0 && b0 + cnt <= n, b0, cnt);
-    }
-  }
-  const int incl = wave_incl_scan_x<true>(cnt);
-  const int total = __shfl(incl, (lane_id() & 32) + 31, 64);
-  if (LOAM_ASSOC_PHASE == 0 || LOAM_ASSOC_PHASE == 1) wpts += total;
-  cells[hl] = hl < 27 ? incl - cnt : 0x7fffffff;
-  cells[32 + hl] = b0;
-  __builtin_amdgcn_wave_barrier();
-  uint64_t best = ~0ull;
-  for (int t = hl; t < total; t += 32) {
-    int k = 0;  // last cell whose prefix is <= t
-#pragma unroll
-    for (int step = 16; step > 0; step >>= 1)
-      if (cells[k + step] <= t) k += step;
-    LOAM_CHECK(cells[32 + k] + (t - cells[k]) < n && cells[32 + k] >= 0, cells[32 + k] + (t - cells[k]), n);
-    const float4 a = hp[cells[32 + k] + (t - cells[k])];
-    const float d = sqdist(a.x, a.y, a.z, q.x, q.y, q.z);
-    const uint32_t tag = (uint32_t)__float_as_int(a.w);  // index | ring << 24
-    const uint64_t key = ((uint64_t)fkey(d) << 32) | ((tag & 0xffffffu) << 8) | (tag >> 24);
-    best = key < best ? key : best;
-  }
-  best = wave_min_u64_x<true>(best);
-  __builtin_amdgcn_wave_barrier();
-  if ((best != ~0ull && __uint_as_float((uint32_t)(best >> 32)) < 1.0f) || (LOAM_ASSOC_SKIP & 2)) return best;
-  // farther than one cell: the chunks of the whole cloud that may hold a point closer than 5 m
-  best = ~0ull;
-  const int nch = (n + kChunk - 1) / kChunk;
-  for (int k0 = 0; k0 < nch; k0 += 32) {
-    const int k = k0 + hl;
-    float bd = 0.0f;
-    if (k < nch) bd = box_d2(ch[2 * k], ch[2 * k + 1], q);
-    uint32_t nb = half_bits(__ballot(k < nch && bd < 25.0f && bd <= bound));
-    wbox += min(32, nch - k0);
-    while (nb) {
-      const int c = k0 + __ffs(nb) - 1;
-      nb &= nb - 1;
-      if (LOAM_ASSOC_PHASE == 0 || LOAM_ASSOC_PHASE == 2) wpts += min(kChunk, n - c * kChunk);
-#pragma unroll
-      for (int u = 0; u < kChunk; u += 32) {
-        const int t = c * kChunk + u + hl;
-        if (u + hl < kChunk && t < n) {
-          const float4 a = cloud[t];
-          const float d = sqdist(a.x, a.y, a.z, q.x, q.y, q.z);
-          const uint64_t key = ((uint64_t)fkey(d) << 32) | ((uint32_t)t << 8) | (uint32_t)(int)a.w;
-          best = key < best ? key : best;
-        }
-      }
-    }
-  }
-  return wave_min_u64_x<true>(best);
-}
-
-// wave_window_mono (no tightening) over the half's 32 lanes: 32 / kSub sub-chunks per step, the
-// boxes of 64 sub-chunks per box step (two per lane)
-LOAM_D void half_window_mono(const float4* L, const float4* fb, const int* rs, int c, int scan, int fwd_end,
-                             float4 sel, bool want_same, uint64_t& best2, uint64_t& best3, int& wpts, int& wbox) {
-  constexpr int PER = 32 / kSub;  // sub-chunks visited per step
-  constexpr int BPL = 2;          // boxes per lane per box step
-  const int hl = half_lane();
-  const int w0 = rs[max(scan - 2, 0)], rs0 = rs[scan], rs1 = rs[scan + 1];
-  const int w1 = max(min(fwd_end, rs[min(scan + 3, kRingTab - 1)]), c + 1);
-  uint64_t k2 = best2, k3 = best3;
-  const float d2 = fminf(__uint_as_float((uint32_t)(best2 >> 32)), 25.0f);
-  const float d3 = fminf(__uint_as_float((uint32_t)(best3 >> 32)), 25.0f);
-  const int k0 = w0 / kSub, k1 = (w1 - 1) / kSub;
-  for (int g = k0; g <= k1; g += 32 * BPL) {
-    wbox += min(32 * BPL, k1 - g + 1);
-    uint32_t live[BPL];
-#pragma unroll
-    for (int u = 0; u < BPL; ++u) {
-      const int k = g + u * 32 + hl;
-      bool need = false;
-      if (k <= k1) {
-        const float bd = box_d2(fb[2 * k], fb[2 * k + 1], sel);
-        const int lo = max(k * kSub, w0), hi = min(k * kSub + kSub, w1);
-        const bool hs = want_same && max(lo, rs0) < min(hi, rs1);
-        const bool ho = lo < rs0 || hi > rs1;
-        need = (hs && bd <= d2) || (ho && bd <= d3);
-      }
-      live[u] = half_bits(__ballot(need));  // (bounds fixed: one ballot per box step)
-    }
-    while (live[0] | live[1]) {
-      // the first PER live sub-chunks in index order; lane l visits point l % kSub of pick l / kSub
-      int mine = -1, npick = 0;
-#pragma unroll
-      for (int s2 = 0; s2 < PER; ++s2) {
-        int pk = -1;
-#pragma unroll
-        for (int u = 0; u < BPL; ++u)
-          if (pk < 0 && live[u]) {
-            pk = u * 32 + __ffs(live[u]) - 1;
-            live[u] &= live[u] - 1;
-          }
-        if (pk >= 0) ++npick;
-        if (hl / kSub == s2) mine = pk;
-      }
-      if (LOAM_ASSOC_PHASE == 0 || LOAM_ASSOC_PHASE == 3) wpts += npick * kSub;
-      const int j = (g + mine) * kSub + hl % kSub;
-      if (mine >= 0 && j >= w0 && j < w1 && j != c) {
-        const float4 a = L[j];
-        const float d = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
-        const uint32_t pos = j > c ? (uint32_t)(j - c - 1) : (1u << 30) + (uint32_t)(c - 1 - j);
-        const uint64_t key = ((uint64_t)fkey(d) << 32) | pos;
-        if (j >= rs0 && j < rs1) {
-          if (want_same) k2 = key < k2 ? key : k2;
-        } else {
-          k3 = key < k3 ? key : k3;
-        }
-      }
-    }
-  }
-  const uint64_t kNone = (uint64_t)fkey(25.0f) << 32;
-  best2 = want_same ? wave_min_u64_x<true>(k2) : ~0ull;
-  best3 = wave_min_u64_x<true>(k3);
-  if (best2 >= kNone) best2 = ~0ull;
-  if (best3 >= kNone) best3 = ~0ull;
 }
 
 // corner association (:478-527): closest (kd NN, sqDis < 25) and the best point of an adjacent
@@ -1045,7 +856,6 @@ __global__ void k_od_begin(OdBuffers b, FeatView f) {
   ist[kIsNanSkips] = 0;
   ist[kIsGathered] = 0;
   ist[kIsBoxes] = 0;
-  ist[kIsCert] = 0;
   b.done[p] = 0;
 }
 
@@ -1074,22 +884,16 @@ __global__ __launch_bounds__(kOdThreads) void k_od_sel(OdBuffers b, FeatView f) 
 // COUNT: the profiling variant that also sums the points / chunk boxes it loads into istate
 // SEL: the wave computes its query's TransformToStart itself (small batches: one launch fewer per
 // association round); otherwise it reads k_od_sel's result
-#ifndef LOAM_ASSOC_HALF_WPE
-#define LOAM_ASSOC_HALF_WPE 7
-#endif
-// HALF: pairs of consecutive queries of the wave's list on its two halves (half_hash_nn /
-// half_window_mono) when both take the index-range windows, one after the other otherwise
-// CERT: keeps / uses the association certificates (tuning od_assoc_cert)
-#ifndef LOAM_ASSOC_CERT_WPE
-#define LOAM_ASSOC_CERT_WPE 7
-#endif
-template <bool COUNT, bool SEL, bool HALF = false, bool CERT = false>
-__global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL ? 1 : HALF ? LOAM_ASSOC_HALF_WPE : CERT ? LOAM_ASSOC_CERT_WPE : 8))) void k_od_assoc(OdBuffers b, FeatView f, int last_buf) {
+// (measured and removed in round 6: two queries per wave on the wave's halves, round 5: equal or
+// slower; per-query certificates that settle a seeded query without a search, round 5: exact, 31 %
+// of the queries settled at config 4, but slower: DESIGN.md §15)
+template <bool COUNT, bool SEL>
+__global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL ? 1 : 8))) void k_od_assoc(OdBuffers b, FeatView f, int last_buf) {
   const XcdBlock blk = xcd_block();
   const int p = blk.y, lane = lane_id(), w = threadIdx.x >> 6;
   const int* ist = b.istate + (size_t)p * kOdStateInts;
   if (!ist[kIsActive] || ist[kIsStop]) return;
-  __shared__ int cells[kAsWaves][128];  // (the half-wave searches: 64 per half)
+  __shared__ int cells[kAsWaves][64];
   __shared__ float4 bq_s4[kAsWaves][64], bq_d[kAsWaves][64];
   __shared__ int4 bq_j[kAsWaves][64];
   const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
@@ -1100,16 +904,9 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
   const float4* SL = b.lastS + lp * b.capS;
   int* ind = b.ind + (size_t)p * 3 * b.cap_q;
   int wpts = 0, wbox = 0;  // wave-uniform work counters (loam_stats od_assoc_gathered / _boxes)
-  int hpts = 0, hbox = 0;  // the half-wave searches' (uniform per half)
   const bool seeded = ist[kIsIters] > 0;  // ind holds this frame's previous round
   const bool use_mono = b.P >= b.tune.od_win_mono_min && (b.tune.od_win_mono & (seeded ? 2 : 1)) != 0;
   const bool tight = LOAM_WIN_TIGHTEN == 1 || (LOAM_WIN_TIGHTEN == 2 && !seeded);
-  // association certificates (tuning od_assoc_cert): kept by every full search on the index-range
-  // path (its bounds need the untightened windows), used in the seeded rounds
-  const bool keep_cert = CERT && use_mono && !tight;
-  const bool use_cert = keep_cert && seeded;
-  float4* certq = b.cert + (size_t)p * b.cap_q * 2;
-  int nsettled = 0;
   const int hCT = b.hC_T[last_buf * b.P + p], hST = b.hS_T[last_buf * b.P + p];
   const bool monoC = b.mono[lp * 2 + 0] != 0, monoS = b.mono[lp * 2 + 1] != 0;
   __shared__ int rsC[kRingTab], rsS[kRingTab];  // the ring start tables (ring-monotone clouds)
@@ -1151,98 +948,19 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
         const float nnb = j[0] >= 0 ? sqdist(sp[0].x, sp[0].y, sp[0].z, s4.x, s4.y, s4.z) : 3.4e38f;
         const float d1 = sqdist(sp[1].x, sp[1].y, sp[1].z, s4.x, s4.y, s4.z);
         const float d2 = sqdist(sp[2].x, sp[2].y, sp[2].z, s4.x, s4.y, s4.z);
-        // The certificate of the query's last full search (index-range windows, this frame): every
-        // rival of its choices (nearest point; window minima or "none") lay at >= sqrt(bound) from
-        // the query point then.  The query has moved by delta since, so when each choice's distance
-        // now (the seeds' d) stays below every rival's lower bound sqrt(bound) - delta, with margins
-        // far above the float rounding of the distances, the search would return the same indices:
-        // they stay in ind and the query is settled without a search.
-        bool settled = false;
-        if (CERT && use_cert && (ql < nc ? monoC : monoS) && j[0] >= 0 && D(nnb) < 25) {
-          const float4 c0 = certq[2 * ql], c1 = certq[2 * ql + 1];
-          if (c0.w > 0.0f) {
-            // (float: relative margins of 1e-4 and 1e-5 m cover the rounding of every distance here)
-            const float ex = s4.x - c0.x, ey = s4.y - c0.y, ez = s4.z - c0.z;
-            const float delta = sqrtf(ex * ex + ey * ey + ez * ez) * 1.0001f + 1e-5f;
-            auto rival = [&](float l) { return sqrtf(l) * 0.9999f - delta; };
-            auto near = [&](float dn) { return sqrtf(dn) * 1.0001f + 1e-5f; };
-            auto sep = [&](int jj2, float dn, float l) {  // the choice (or "none") is still the window minimum
-              return jj2 >= 0 ? D(dn) < 25 && near(dn) < rival(l) : rival(l) > 5.001f;
-            };
-            settled = near(nnb) < rival(c0.w) && (ql < nc ? sep(j[1], d1, c1.y) : sep(j[1], d1, c1.x) && sep(j[2], d2, c1.y));
-          }
-        }
         bq_s4[w][lane] = s4;
-        bq_j[w][lane] = make_int4(j[0], j[1], j[2], (int)sp[1].w | ((int)sp[2].w << 16) | (settled ? 1 << 14 : 0));
+        bq_j[w][lane] = make_int4(j[0], j[1], j[2], (int)sp[1].w | ((int)sp[2].w << 16));
         bq_d[w][lane] = make_float4(nnb, d1, d2, 0.0f);
       }
     }
     __builtin_amdgcn_wave_barrier();
     const int nb = min(64, (nq - q0 + G - 1) / G - i0);
     for (int i = 0; i < nb; ++i) {
-      if constexpr (CERT) {
-        if (bq_j[w][i].w & (1 << 14)) {  // settled by its certificate (ind keeps its choices)
-          ++nsettled;
-          continue;
-        }
-      }
-      if constexpr (HALF) {
-        // entries i, i + 1 on the two halves when both (or the only one) take the index-range
-        // windows (wave-uniform test); else entry i alone below
-        auto mono_q = [&](int e) {
-          const int qe = q0 + (i0 + e) * G;
-          return use_mono && (qe < nc ? monoC : monoS);
-        };
-        if (mono_q(i) && (i + 1 >= nb || mono_q(i + 1))) {
-          const int e = i + (lane >> 5);
-          const bool act = e < nb;
-          const int q = q0 + (i0 + e) * G;
-          int i1 = -1, i2 = -1, i3 = -1;
-          if (act) {
-            const float4 s4 = bq_s4[w][e];
-            const int4 jj = bq_j[w][e];
-            const float4 dd = bq_d[w][e];
-            const bool corner = q < nc;
-            const float4* L = corner ? CL : SL;
-            const int n = corner ? C : S, fe = corner ? min(nc, C) : min(ns, S);
-            const uint64_t nn =
-                half_hash_nn(corner ? b.hC_start + lp * (b.tC + 1) : b.hS_start + lp * (b.tS + 1),
-                             corner ? b.hC_pts + lp * b.capC : b.hS_pts + lp * b.capS, corner ? hCT : hST, L,
-                             corner ? b.cC + lp * 2 * chunks_of(b.capC) : b.cS + lp * 2 * chunks_of(b.capS), n, s4, dd.x,
-                             &cells[w][(lane & 32) * 2], hpts, hbox);
-            if (nn != ~0ull && D(__uint_as_float((uint32_t)(nn >> 32))) < 25) {
-              const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u);
-              const int* rs = corner ? rsC : rsS;
-              i1 = c;
-              uint64_t k2 = corner ? ~0ull : mono_seed_key(rs, c, scan, fe, jj.y, dd.y, true);
-              uint64_t k3 = corner ? mono_seed_key(rs, c, scan, fe, jj.y, dd.y, false)
-                                   : mono_seed_key(rs, c, scan, fe, jj.z, dd.z, false);
-              half_window_mono(L, corner ? b.fC + lp * 2 * subs_of(b.capC) : b.fS + lp * 2 * subs_of(b.capS), rs,
-                               c, scan, fe, s4, !corner, k2, k3, hpts, hbox);
-              if (corner) {
-                if (k3 != ~0ull) i2 = mono_decode(c, k3);
-              } else {
-                if (k2 != ~0ull) i2 = mono_decode(c, k2);
-                if (k3 != ~0ull) i3 = mono_decode(c, k3);
-              }
-            }
-            if ((lane & 31) == 0) {
-              LOAM_CHECK(q < b.cap_q && p < b.P, q, p);
-              ind[q] = i1;
-              ind[b.cap_q + q] = i2;
-              ind[2 * b.cap_q + q] = i3;
-            }
-          }
-          ++i;  // (the pair's second entry is done)
-          __builtin_amdgcn_wave_barrier();
-          continue;
-        }
-      }
       const int q = q0 + (i0 + i) * G;
       const float4 s4 = bq_s4[w][i];
       const int4 jj = bq_j[w][i];
       const float4 dd = bq_d[w][i];
-      const int j1 = jj.y, j2 = jj.z, r1 = jj.w & (CERT ? 0x3fff : 0xffff), r2 = jj.w >> 16;
+      const int j1 = jj.y, j2 = jj.z, r1 = jj.w & 0xffff, r2 = jj.w >> 16;
       const float nnb = dd.x, d1 = dd.y, d2 = dd.z;
       int i1, i2, i3 = -1;
       // the cells' window bounds in the first round only (later rounds have their seeds: the extra
@@ -1250,60 +968,40 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
       WinBound wb;
       if (q < nc && monoC && use_mono) {
         const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
-        float lnn = 0.0f, cw[2] = {0.0f, 0.0f};
         const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC, hCT, CL, ch, C, 1.0f,
-                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded || !LOAM_WIN_WB ? -1 : 0, min(nc, C), true, &wb,
-                                         CERT && keep_cert ? &lnn : nullptr);
+                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded || !LOAM_WIN_WB ? -1 : 0, min(nc, C), true, &wb);
         i1 = i2 = -1;
         if (nn != ~0ull && D(__uint_as_float((uint32_t)(nn >> 32))) < 25) {
           const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u), fe = min(nc, C);
           i1 = c;
           uint64_t k2 = ~0ull, k3 = mono_seed_key(rsC, c, scan, fe, j1, d1, false);
-          wave_window_mono(CL, b.fC + lp * 2 * subs_of(b.capC), rsC, c, scan, fe, s4, false, wb, tight, k2, k3, wpts, wbox,
-                           CERT && keep_cert ? cw : nullptr);
+          wave_window_mono(CL, b.fC + lp * 2 * subs_of(b.capC), rsC, c, scan, fe, s4, false, wb, tight, k2, k3, wpts, wbox);
           if (k3 != ~0ull) i2 = mono_decode(c, k3);
-        } else {
-          lnn = 0.0f;
-        }
-        if (CERT && keep_cert && lane == 0) {
-          certq[2 * q] = make_float4(s4.x, s4.y, s4.z, lnn);
-          certq[2 * q + 1] = make_float4(cw[0], cw[1], 0.0f, 0.0f);
         }
       } else if (q >= nc && monoS && use_mono) {
         const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
-        float lnn = 0.0f, cw[2] = {0.0f, 0.0f};
         const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS, hST, SL, ch, S, 1.0f,
-                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded || !LOAM_WIN_WB ? -1 : 1, min(ns, S), true, &wb,
-                                         CERT && keep_cert ? &lnn : nullptr);
+                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded || !LOAM_WIN_WB ? -1 : 1, min(ns, S), true, &wb);
         i1 = i2 = -1;
         if (nn != ~0ull && D(__uint_as_float((uint32_t)(nn >> 32))) < 25) {
           const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u), fe = min(ns, S);
           i1 = c;
           uint64_t k2 = mono_seed_key(rsS, c, scan, fe, j1, d1, true);
           uint64_t k3 = mono_seed_key(rsS, c, scan, fe, j2, d2, false);
-          wave_window_mono(SL, b.fS + lp * 2 * subs_of(b.capS), rsS, c, scan, fe, s4, true, wb, tight, k2, k3, wpts, wbox,
-                           CERT && keep_cert ? cw : nullptr);
+          wave_window_mono(SL, b.fS + lp * 2 * subs_of(b.capS), rsS, c, scan, fe, s4, true, wb, tight, k2, k3, wpts, wbox);
           if (k2 != ~0ull) i2 = mono_decode(c, k2);
           if (k3 != ~0ull) i3 = mono_decode(c, k3);
-        } else {
-          lnn = 0.0f;
-        }
-        if (CERT && keep_cert && lane == 0) {
-          certq[2 * q] = make_float4(s4.x, s4.y, s4.z, lnn);
-          certq[2 * q + 1] = make_float4(cw[0], cw[1], 0.0f, 0.0f);
         }
       } else if (q < nc) {
         const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
         const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC, hCT, CL, ch, C, 1.0f,
                                          1.0f, s4, nnb, cells[w], wpts, wbox, seeded ? -1 : 0, min(nc, C), monoC, &wb);
         wave_assoc_corner(CL, ch, min(nc, C), nn, s4, j1, r1, d1, wb, monoC, i1, i2, wpts, wbox);
-        if (CERT && lane == 0) certq[2 * q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // (no certificate kept)
       } else {
         const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
         const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS, hST, SL, ch, S, 1.0f,
                                          1.0f, s4, nnb, cells[w], wpts, wbox, seeded ? -1 : 1, min(ns, S), monoS, &wb);
         wave_assoc_surf(SL, ch, min(ns, S), nn, s4, j1, r1, d1, j2, r2, d2, wb, monoS, i1, i2, i3, wpts, wbox);
-        if (CERT && lane == 0) certq[2 * q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // (no certificate kept)
       }
       if (lane == 0) {
         LOAM_CHECK(q < b.cap_q && p < b.P, q, p);
@@ -1315,11 +1013,9 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
     }
     __builtin_amdgcn_wave_barrier();
   }
-  if (COUNT && (lane & 31) == 0) {  // (lane 0: the full-wave counts and half 0's, lane 32: half 1's)
-    const int pts = hpts + (lane == 0 ? wpts : 0), box = hbox + (lane == 0 ? wbox : 0);
-    if (pts) atomicAdd((int*)&ist[kIsGathered], pts);
-    if (box) atomicAdd((int*)&ist[kIsBoxes], box);
-    if (CERT && lane == 0 && nsettled) atomicAdd((int*)&ist[kIsCert], nsettled);
+  if (COUNT && lane == 0) {
+    if (wpts) atomicAdd((int*)&ist[kIsGathered], wpts);
+    if (wbox) atomicAdd((int*)&ist[kIsBoxes], wbox);
   }
 }
 
@@ -2110,106 +1806,6 @@ __global__ __launch_bounds__(kOdLmThreads) void k_od_lm(OdBuffers b, FeatView f,
   }
 }
 
-// One association round's iterations (it0 .. it0 + 4) of a problem in one workgroup with the stored
-// rows as per-query moments (od_mom_add / od_mom_accum; tuning od_moments_min): k_od_lm's shape (the
-// step on the first wave between iterations, no launch or grid-wide partial hand-off per iteration)
-// without its O(rows) re-evaluation, so an iteration costs O(queries).  Lanes loop over the queries
-// (any cap_q: HDL-64E's 2304 included); a query's raw and associated Last points stay in LDS for the
-// round, its moments in global memory (b.mom, as k_od_rows<., ., true> keeps them: L2-resident).
-// The fp64 sums are reduced in a fixed order (each lane's queries in order, wave butterflies, the
-// waves in order).
-constexpr int kOdLmMomThreads = 512;
-#ifndef LOAM_LM_MOM_WPE
-#define LOAM_LM_MOM_WPE 3  // 168 VGPRs: the query loop unspilled (137), the step's solver spills (one wave)
-#endif
-inline size_t od_lm_mom_lds(int cap_q) { return (size_t)cap_q * 4 * sizeof(float4); }
-__global__ __launch_bounds__(kOdLmMomThreads) __attribute__((amdgpu_waves_per_eu(LOAM_LM_MOM_WPE))) void k_od_lm_mom(OdBuffers b, FeatView f, int last_buf, int it0) {
-  const int p = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  int* ist = b.istate + (size_t)p * kOdStateInts;
-  if (!ist[kIsActive] || ist[kIsStop]) return;
-  constexpr int NT = kOdLmMomThreads, NW = NT / 64;
-  __shared__ double red[NW][28];
-  __shared__ double tot[28];
-  __shared__ float Tsh[6], trig[6];
-  __shared__ int stop_sh;
-  __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs], jE[6], jV[36];
-  __shared__ int lm_iws[12];
-  extern __shared__ float4 od_lm_dyn[];
-  const int CQ = b.cap_q;
-  float4* qpts = od_lm_dyn;  // [4][CQ]: raw point, associated Last points (t1.w: the association holds)
-  float* st = b.state + (size_t)p * kOdStateFloats;
-  if (tid < 6) {  // the transform, and the double sin / cos of its angles one per lane
-    Tsh[tid] = st[tid];
-    const float a = st[tid >> 1];
-    trig[tid] = (float)((tid & 1) ? dcos(a) : dsin(a));
-  }
-  const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
-  const size_t lp = (size_t)last_buf * b.P + p;
-  for (int q = tid; q < nq; q += NT) {
-    float4 t1, t2, t3;
-    const bool has = od_assoc_pts(b, p, q, nc, lp, t1, t2, t3);
-    t1.w = has ? 1.0f : 0.0f;
-    qpts[q] = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
-    qpts[CQ + q] = t1;
-    qpts[2 * CQ + q] = t2;
-    qpts[3 * CQ + q] = t3;
-  }
-  double* mom = b.mom + (size_t)p * kOdMom * CQ;  // [kOdMom][CQ]
-  __syncthreads();
-  const int it_end = min(it0 + 5, b.max_iter);
-  for (int iter = it0; iter < it_end; ++iter) {
-    float T[6], tg[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      T[k] = Tsh[k];
-      tg[k] = trig[k];
-    }
-    double acc[28];
-#pragma unroll
-    for (int k = 0; k < 28; ++k) acc[k] = 0.0;
-    for (int q = tid; q < nq; q += NT) {
-      const float4 po = qpts[q], t1 = qpts[CQ + q];
-      float4 cf;
-      int ok;
-      od_coeff_from(iter, T, po, q < nc, t1.w != 0.0f, t1, qpts[2 * CQ + q], qpts[3 * CQ + q], cf, ok);
-      double m[kOdMom];
-#pragma unroll
-      for (int k = 0; k < kOdMom; ++k) m[k] = iter == 0 ? 0.0 : mom[(size_t)k * CQ + q];
-      od_mom_add(m, cf);
-#pragma unroll
-      for (int k = 0; k < kOdMom; ++k) mom[(size_t)k * CQ + q] = m[k];
-      od_mom_accum(od_jfactors(tg, T, po), m, acc);
-    }
-    wave_reduce_scatter_28(acc);
-    if ((lane & 1) == 0 && (lane >> 1) < 28) red[w][lane >> 1] = acc[0];
-    __syncthreads();
-    if (tid < 28) {
-      double v = red[0][tid];
-#pragma unroll
-      for (int ww = 1; ww < NW; ++ww) v += red[ww][tid];
-      tot[tid] = v;
-    }
-    __syncthreads();
-    if (tid < 64) {  // the first wave: the step (od_step writes the state; lane 0 reads its own writes)
-      od_step_call(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
-      if (tid == 0) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) Tsh[k] = st[k];
-        stop_sh = ist[kIsStop];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (tid < 6) {
-        const float a = Tsh[tid >> 1];
-        trig[tid] = (float)((tid & 1) ? dcos(a) : dsin(a));
-      }
-    }
-    __syncthreads();
-    if (stop_sh) break;
-  }
-}
-
 // pose accumulation (:830-856) for every problem
 __global__ __launch_bounds__(64) void k_od_fini(OdBuffers b, FeatView f) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2300,7 +1896,6 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   A(&b.q_cf, (size_t)P * max_iter * b.cap_q * sizeof(float4));
   A(&b.q_ok, (size_t)P * max_iter * b.cap_q * sizeof(int8_t));
   A(&b.mom, (size_t)P * kOdMom * b.cap_q * sizeof(double));
-  A(&b.cert, (size_t)P * b.cap_q * 2 * sizeof(float4));
   A(&b.qa, (size_t)P * b.cap_q * 3 * sizeof(float4));
   // per-workgroup partials: [P][gq][28], or [P][gq * max_iter][28] for the small-batch rows kernel
   A(&b.part, (size_t)P * b.gq * max_iter * 28 * sizeof(double));  // (k_od_rows_small: per stored iteration)
@@ -2330,7 +1925,7 @@ void od_free(OdBuffers& b) {
   if (b.hash_done) (void)hipEventDestroy(b.hash_done);
   void* ptrs[] = {b.state_set[0], b.state_set[1], b.state_set[2], b.istate_set[0], b.istate_set[1], b.istate_set[2], b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
-                  b.ind, b.sel, b.q_cf, b.q_ok, b.mom, b.cert, b.qa, b.part, b.done, b.mono, b.rstart, b.fC, b.fS};
+                  b.ind, b.sel, b.q_cf, b.q_ok, b.mom, b.qa, b.part, b.done, b.mono, b.rstart, b.fC, b.fS};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = OdBuffers();
@@ -2404,22 +1999,6 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
   // workgroup per problem (the queries must fit its lanes)
   const Tuning& tn = b.tune;
   const bool lm_round = P >= tn.od_lm_min && P <= tn.od_lm_max && b.cap_q <= kOdLmThreads;
-  // ... with the stored rows as moments (any cap_q whose round data fits the LDS)
-  // (dynamic LDS beyond 64 KB needs the kernel attribute: HDL-64E's 2304 queries take 144 KB, plus
-  // the kernel's 3.5 KB of static LDS within the CU's 160 KB)
-  const size_t lm_lds = od_lm_mom_lds(b.cap_q);
-  bool lm_mom = P > tn.od_small_max && P >= tn.od_moments_min && P >= tn.od_lm_mom_min &&
-                P <= tn.od_lm_mom_max && lm_lds <= 156 * 1024;
-  if (lm_mom && lm_lds > 64 * 1024) {
-    static size_t attr = 0;
-    if (attr < lm_lds) {
-      if (hipFuncSetAttribute((const void*)k_od_lm_mom, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lm_lds) == hipSuccess)
-        attr = lm_lds;
-      else
-        (void)hipGetLastError();  // (not left for the launch checks to find: the per-iteration kernels run instead)
-    }
-    lm_mom = attr >= lm_lds;
-  }
   for (int it = 0; it < b.max_iter; ++it) {
     if (it % 5 == 0) {  // Q10
       // one wave per query when the batch is small (streaming: TransformToStart in the wave), 64
@@ -2429,16 +2008,9 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
       // VLP-16 batches 32 / 128 / 256 measured equal / slower)
       const int ga = P >= 64 ? (tn.od_assoc_wg > 0 ? tn.od_assoc_wg : std::max(16, std::min(1024, b.cap_q / 9)))
                              : (b.cap_q + kAsWaves - 1) / kAsWaves;
-      const bool half = P >= tn.od_assoc_half_min;
       if (P >= tn.od_sel_min) {
         hipLaunchKernelGGL(k_od_sel, dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f);
-        if (tn.od_assoc_cert) {
-          if (prof) hipLaunchKernelGGL((k_od_assoc<true, false, false, true>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
-          else hipLaunchKernelGGL((k_od_assoc<false, false, false, true>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
-        } else if (half) {
-          if (prof) hipLaunchKernelGGL((k_od_assoc<true, false, true>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
-          else hipLaunchKernelGGL((k_od_assoc<false, false, true>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
-        } else if (prof) {
+        if (prof) {
           hipLaunchKernelGGL((k_od_assoc<true, false>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
         } else {
           hipLaunchKernelGGL((k_od_assoc<false, false>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
@@ -2448,12 +2020,6 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
         else hipLaunchKernelGGL((k_od_assoc<false, true>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
       }
       mark("k_od_assoc");
-      if (lm_mom) {  // the round's iterations in one workgroup per problem, rows as moments
-        hipLaunchKernelGGL(k_od_lm_mom, dim3(P), dim3(kOdLmMomThreads), lm_lds, st, b, f, last_buf, it);
-        mark("k_od_lm");
-        it += 4;
-        continue;
-      }
       if (lm_round) {  // the round's iterations in one workgroup per problem
         hipLaunchKernelGGL(k_od_lm, dim3(P), dim3(kOdLmThreads), od_lm_lds(b.cap_q), st, b, f, last_buf, it);
         mark("k_od_lm");

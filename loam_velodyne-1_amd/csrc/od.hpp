@@ -35,7 +35,6 @@ enum { kIsDegenerate = 0, kIsCornerLastNum, kIsSurfLastNum, kIsIters, kIsAssoc, 
        kIsNanSkips,  // L-M updates of this frame skipped by the NaN guard (Q16)
        kIsGathered,  // Last-cloud points the association loaded this frame (work counter)
        kIsBoxes,     // chunk boxes the association loaded this frame (work counter)
-       kIsCert,      // association queries settled by their certificate this frame (work counter)
        kOdStateInts = 16 };
 
 // read-only view of one feature set per problem (stride = elements between problems)
@@ -120,8 +119,6 @@ struct OdBuffers {
   int* ind = nullptr;         // [P][3][cap_q] association of every query (refreshed every 5th iteration)
   float4* q_cf = nullptr;     // [P][max_iter][cap_q] coefficients (zero when rejected)
   int8_t* q_ok = nullptr;     // [P][max_iter][cap_q] accepted flags
-  float4* cert = nullptr;     // [P][cap_q][2] association certificates: the query point of the last full
-                              // search and its rivals' distance bounds (k_od_assoc, tuning od_assoc_cert)
   float4* qa = nullptr;       // [P][cap_q][3] a query's associated Last points for its round (k_od_rows_mom)
   double* mom = nullptr;      // [P][10][cap_q] per-query fp64 moments of the stored rows (tuning od_moments)
   double* part = nullptr;     // [P][gq][28] per-workgroup JᵀJ | Jᵀb | rows

@@ -58,8 +58,7 @@ class Stats(ctypes.Structure):
                                         # engine-only search counters (zero here: the oracle's kd-tree
                                         # does different work)
                                         "mp_nn_candidates", "mp_nn_cells", "od_assoc_gathered",
-                                        "od_assoc_boxes", "mp_nn_lds_blocks", "mp_nn_lds_fit",
-                                        "mp_nn_lds_staged", "od_assoc_settled")]
+                                        "od_assoc_boxes")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -237,7 +237,6 @@ def _share_run(loam, sg, **tune):
     {"nnfit_max": 0, "nn_lanes": 2},         # k_mp_nn<., L>: L lanes per query, merged 5-lists
     {"nnfit_max": 0, "nn_lanes": 4},
     {"od_assoc_wg": 16},                     # fewer association waves per problem (queries looped)
-    {"nnfit_max": 0, "nn_lds": 1},           # k_mp_nn_lds: the workgroup's map cells staged in LDS
     {"od_rows_deep_max": 128},               # k_od_rows<., 8>: eight stored rows' loads in flight
     {"od_rows_deep_max": 128, "od_fused_max": 128},
     {"mp_fused_max": 0},                     # k_mp_nnfit<false> + k_mp_iter
@@ -249,10 +248,6 @@ def _share_run(loam, sg, **tune):
     {"od_win_mono": 1},
     {"od_win_mono": 2},
     {"od_win_mono": 0},
-    {"od_assoc_cert": 1},                    # seeded association queries settled by certificates
-    {"od_assoc_cert": 1, "od_win_mono": 1},
-    {"od_assoc_half_min": 1},                # two association queries per wave (half-wave searches)
-    {"od_assoc_half_min": 1, "od_win_mono": 2},
     {"sr_ahead": 1},                         # scan registration one step ahead (three steps)
     {"sr_ahead": 1, "sr_ahead_at": 0},
     {"step_pipe": 1},                        # steps as a software pipeline (three steps)
@@ -313,38 +308,3 @@ def test_pipeline_rotation_then_sequential(loam, oc, sg):
         for k in ("od_iters", "mp_iters", "od_corner_last", "od_surf_last", "od_assoc_points"):
             assert st[k] == st0[k], ("sequential", n, k)
     e.close()
-
-
-@pytest.mark.parametrize("dense", [False, True], ids=["config4_1024", "config5_64"])
-def test_assoc_certificates_bitexact(loam, sg, dense):
-    """association queries settled by the certificate of their last full search (tuning
-    od_assoc_cert) return exactly what the search returns: every pose of the bench's 1024 config-4
-    problems and of the 64 config-5 problems equal to the searching run's, and the certificates do
-    settle queries (od_assoc_settled, counted in the profiling pass)"""
-    kw = dict(n_rings=64, max_points=160000, od_max_iter=100, mp_max_iter=20)
-    if dense:
-        prevs, curs = sg.batch_problems(64, base_seed=5000, lidar=sg.HDL64)
-        cfg = loam.default_config(ring_model=loam.RING_LINEAR, **kw)
-    else:
-        prevs, curs = sg.batch_problems(1024, base_seed=1000)
-        cfg = None
-
-    def run(cert):
-        e = loam.Engine(cfg) if cfg is not None else loam.Engine()
-        e.set_tuning(od_assoc_cert=cert)
-        e.batch_upload(prevs, curs)
-        e.batch_run()
-        r = e.batch_download()
-        e.set_profiling(True)
-        e.batch_run()
-        st = e.batch_download()[2]
-        e.close()
-        return r, st
-
-    (od0, aft0, st0), _ = run(0)
-    (od1, aft1, st1), sp = run(1)
-    np.testing.assert_array_equal(od1, od0)
-    np.testing.assert_array_equal(aft1, aft0)
-    assert st1["od_iters"] == st0["od_iters"] and st1["mp_iters"] == st0["mp_iters"]
-    print(f"settled {sp['od_assoc_settled']} of {sp['od_queries']} association queries")
-    assert sp["od_assoc_settled"] > 0

@@ -4,10 +4,18 @@ against the oracle on EVERY problem of the benched batches.
 The reference re-evaluates every stored row's Jacobian each L-M iteration with float J entries
 (src/laserOdometry.cpp:697-764, Q12).  The moments form sums the same rows as E_q M_q E_qᵀ in fp64,
 so it is not bit-identical: the bar is the north star's 1e-4 m / 1e-4 rad on the odometry and the
-mapping pose of every problem.  The bit-exact form (the default at these sizes unless the default
-changes) is checked against the same oracle runs bit for bit, so both forms are pinned on all
-1024 config-4 problems and all 64 config-5 problems.  The oracle runs on a thread pool (ctypes
-releases the GIL; the oracle keeps no global state)."""
+mapping pose of every problem.  The bit-exact form (od_moments_min above the batch size) is checked
+against the same oracle runs bit for bit, poses and per-problem L-M iteration counts, so both forms
+are pinned on all 1024 config-4 problems and all 64 config-5 problems.
+
+Every moments error is attributed: the fp64 moments round the normal equations differently from
+the reference's float J entries, a ~1e-7 relative perturbation of each L-M step.  It reaches the
+poses at that size (<= ATTRIB) unless a convergence test (ΔR < 0.1° and ΔT < 0.1 cm odometry,
+0.05 / 0.05 mapping, src/laserOdometry.cpp:824, src/laserMapping.cpp:972) flips, which changes the
+problem's iteration count: every problem with a larger error must show such a flip (odometry or
+mapping iteration count different from the oracle's).  The test prints the error histogram and the
+flipped problems.  The oracle runs on a thread pool (ctypes releases the GIL; the oracle keeps no
+global state)."""
 import os
 from concurrent.futures import ThreadPoolExecutor
 
@@ -17,6 +25,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-4  # north star: output transforms within 1e-4 m / 1e-4 rad
+ATTRIB = 1e-6  # the largest error the moments' rounding alone is allowed without a convergence flip
 DENSE = dict(n_rings=64, max_points=160000, od_max_iter=100, mp_max_iter=20)
 
 
@@ -26,8 +35,9 @@ def _oracle_all(oc, prevs, curs, ocfg=None):
         outs = list(ex.map(lambda pc: oc.problem(pc[0], pc[1], ocfg), zip(prevs, curs)))
     od = np.array([o[0] for o in outs])
     aft = np.array([o[1] for o in outs])
-    iters = sum(o[2]["od_iters"] for o in outs)
-    return od, aft, iters
+    od_it = np.array([o[2]["od_iters"] for o in outs])
+    mp_it = np.array([o[2]["mp_iters"] for o in outs])
+    return od, aft, od_it, mp_it
 
 
 def _run(loam, prevs, curs, cfg, **tune):
@@ -36,26 +46,39 @@ def _run(loam, prevs, curs, cfg, **tune):
     e.batch_upload(prevs, curs)
     e.batch_run()
     od, aft, st = e.batch_download()
+    od_it, mp_it = e.batch_iterations()
     e.close()
-    return od, aft, st
+    return od, aft, st, od_it, mp_it
 
 
 def _check(loam, prevs, curs, cfg, oracle):
-    od_o, aft_o, iters_o = oracle
+    od_o, aft_o, od_it_o, mp_it_o = oracle
     exact = _run(loam, prevs, curs, cfg, od_moments_min=1 << 30)
     mom = _run(loam, prevs, curs, cfg, od_moments_min=1)
-    # the reference's row re-evaluation: bit-exact on every problem
+    # the reference's row re-evaluation: bit-exact on every problem, every convergence decision equal
     np.testing.assert_array_equal(exact[0], od_o)
     np.testing.assert_array_equal(exact[1], aft_o)
-    assert exact[2]["od_iters"] == iters_o
-    # the moments: every problem within the north star
+    np.testing.assert_array_equal(exact[3], od_it_o)
+    np.testing.assert_array_equal(exact[4], mp_it_o)
+    # the moments: every problem within the north star, every error above ATTRIB explained by a flip
     e_od = np.abs(mom[0] - od_o).max(axis=1)
     e_mp = np.abs(mom[1] - aft_o).max(axis=1)
-    worst = int(np.argmax(np.maximum(e_od, e_mp)))
-    print(f"moments: {len(prevs)} problems, max |d odometry| {e_od.max():.3g}, max |d mapping| "
-          f"{e_mp.max():.3g} (problem {worst}), bit-identical {int(np.sum((e_od == 0) & (e_mp == 0)))}, "
-          f"odometry iterations {mom[2]['od_iters']} vs oracle {iters_o}")
-    assert e_od.max() <= TOL and e_mp.max() <= TOL, worst
+    err = np.maximum(e_od, e_mp)
+    flip_od = mom[3] != od_it_o
+    flip_mp = mom[4] != mp_it_o
+    edges = [0.0, 1e-9, 1e-8, 1e-7, 1e-6, 1e-5, TOL, np.inf]
+    hist = {f"<= {edges[i + 1]:.0e}" if i else "== 0": int(np.sum((err > edges[i]) & (err <= edges[i + 1])) if i
+                                                        else np.sum(err == 0))
+            for i in range(len(edges) - 1)}
+    print(f"moments: {len(prevs)} problems, max |d odometry| {e_od.max():.3g}, max |d mapping| {e_mp.max():.3g}; "
+          f"error histogram {hist}; odometry iterations {int(mom[3].sum())} vs oracle {int(od_it_o.sum())}, "
+          f"mapping {int(mom[4].sum())} vs {int(mp_it_o.sum())}")
+    for i in np.flatnonzero(flip_od | flip_mp | (err > ATTRIB)):
+        print(f"  problem {i}: |d odometry| {e_od[i]:.3g} |d mapping| {e_mp[i]:.3g}; odometry iterations "
+              f"{mom[3][i]} (oracle {od_it_o[i]}), mapping {mom[4][i]} (oracle {mp_it_o[i]})")
+    assert err.max() <= TOL, int(np.argmax(err))
+    unexplained = np.flatnonzero((err > ATTRIB) & ~flip_od & ~flip_mp)
+    assert unexplained.size == 0, f"errors above {ATTRIB} without a convergence flip: {unexplained.tolist()}"
     return mom
 
 
@@ -72,29 +95,12 @@ def test_moments_config5_all_64(loam, oc, sg):
     _check(loam, prevs, curs, cfg, _oracle_all(oc, prevs, curs, oc.default_config(ring_model=1, **DENSE)))
 
 
-@pytest.mark.parametrize("P,seed,dense", [(128, 1896, False), (64, 5000, True)], ids=["share128", "config5"])
-def test_moments_round_kernel(loam, oc, sg, P, seed, dense):
-    """k_od_lm_mom (an association round's five iterations in one workgroup per problem, the rows as
-    moments; tuning od_lm_mom_max) at the 8-GPU share and on config 5's 2304-query HDL-64E problems
-    (144 KB of LDS per workgroup): every problem within the north star of the oracle"""
-    kw = dict(lidar=sg.HDL64) if dense else {}
-    prevs, curs = sg.batch_problems(P, base_seed=seed, **kw)
-    cfg = loam.default_config(ring_model=loam.RING_LINEAR, **DENSE) if dense else None
-    ocfg = oc.default_config(ring_model=1, **DENSE) if dense else None
-    od_o, aft_o, iters_o = _oracle_all(oc, prevs, curs, ocfg)
-    od, aft, st = _run(loam, prevs, curs, cfg, od_lm_mom_max=1 << 20)
-    e_od, e_mp = np.abs(od - od_o).max(), np.abs(aft - aft_o).max()
-    print(f"k_od_lm_mom P={P}: max |d odometry| {e_od:.3g}, |d mapping| {e_mp:.3g}, "
-          f"iterations {st['od_iters']} vs {iters_o}")
-    assert e_od <= TOL and e_mp <= TOL
-
-
 def test_moments_8gpu_share_fused(loam, oc, sg):
     """the share (P = 128): the moments in the fused rows kernel (step in the last workgroup) and
     through the step pipeline (three steps), against the oracle"""
     P, r = 128, 7
     prevs, curs = sg.batch_problems(P, base_seed=1000 + r * P)
-    od_o, aft_o, _ = _oracle_all(oc, prevs, curs)
+    od_o, aft_o, _, _ = _oracle_all(oc, prevs, curs)
     e = loam.Engine()
     e.set_tuning(od_moments_min=1, step_pipe=1)
     e.batch_upload(prevs, curs)

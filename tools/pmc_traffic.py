@@ -43,7 +43,7 @@ def load(path):
     # launches in place of the plain one in the bench's profiling pass, so both are dispatches of
     # the same launch: every dispatch of either counts, averaged together
     counted = {k.split("<")[0] for k in inst if "<true" in k}
-    counted |= {k.split("<")[0] for k in inst if k.startswith(("k_mp_nnfit<", "k_mp_nn_lds<"))}  # (COUNT last)
+    counted |= {k.split("<")[0] for k in inst if k.startswith("k_mp_nnfit<")}  # (COUNT last)
     merged = collections.defaultdict(lambda: [0.0, 0])
     for k, (v, n) in inst.items():
         if k.split("<")[0] in counted:
