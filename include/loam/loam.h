@@ -205,9 +205,11 @@ int loam_batch_run(loam_ctx *ctx);
 int loam_batch_feed(loam_ctx *ctx, uint32_t n, const loam_cloud_in *prev, const loam_cloud_in *cur);
 int loam_batch_sync(loam_ctx *ctx);   /* waits for the work enqueued by loam_batch_run */
 int loam_batch_download(loam_ctx *ctx, loam_pose6 *od_sum, loam_pose6 *aft, loam_stats *stats);
-/* per-problem L-M iteration counts of the last run (odometry, mapping; either pointer may be NULL):
- * the convergence decisions behind loam_batch_download's poses, for parity checks */
-int loam_batch_iterations(loam_ctx *ctx, int32_t *od_iters, int32_t *mp_iters);
+/* per-problem L-M results of the last run behind loam_batch_download's poses, for parity checks
+ * (any pointer may be NULL): the odometry and mapping iteration counts (the convergence decisions)
+ * and the odometry's solved increment transform[6] (src/laserOdometry.cpp:93, :811; the pose the
+ * accumulation and TransformToEnd use) */
+int loam_batch_lm_info(loam_ctx *ctx, int32_t *od_iters, int32_t *mp_iters, loam_pose6 *od_transform);
 
 /* scheduling (no reference equivalent; the reference's nodes are OS processes): priority of the
  * context's HIP streams.  priority > 0 = the device's highest stream priority, 0 = normal,

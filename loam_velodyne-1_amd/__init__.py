@@ -109,7 +109,7 @@ class Stats(ctypes.Structure):
 EXPORTS = ("loam_config_default", "loam_create", "loam_destroy", "loam_last_error", "loam_imu",
            "loam_scan_registration", "loam_odometry", "loam_mapping", "loam_mapping_surround",
            "loam_maintenance", "loam_chain_sweep",
-           "loam_batch_upload", "loam_batch_feed", "loam_batch_run", "loam_batch_sync", "loam_batch_download", "loam_batch_iterations", "loam_get_stats",
+           "loam_batch_upload", "loam_batch_feed", "loam_batch_run", "loam_batch_sync", "loam_batch_download", "loam_batch_lm_info", "loam_get_stats",
            "loam_set_profiling", "loam_get_kernel_times", "loam_set_stream_priority", "loam_set_tuning",
            "loam_get_tuning",
            # include/loam/loam_bag.h: recorded-sweep ingest (rosbag v2, PointCloud2, Imu)
@@ -149,7 +149,7 @@ def lib():
         L.loam_get_tuning.argtypes = [PP, ctypes.c_char_p, P(ctypes.c_longlong)]
         L.loam_get_kernel_times.argtypes = [PP, ctypes.c_char_p, ctypes.c_uint32]
         L.loam_batch_download.argtypes = [PP, P(Pose6), P(Pose6), P(Stats)]
-        L.loam_batch_iterations.argtypes = [PP, P(ctypes.c_int32), P(ctypes.c_int32)]
+        L.loam_batch_lm_info.argtypes = [PP, P(ctypes.c_int32), P(ctypes.c_int32), P(Pose6)]
         L.loam_get_stats.argtypes = [PP, P(Stats)]
         L.loam_msg_from_pose.argtypes = [ctypes.c_int, ctypes.c_double, P(Pose6), P(Pose6), P(OdometryMsg), P(TfMsg)]
         L.loam_pose_from_msg.argtypes = [P(OdometryMsg), P(Pose6), P(Pose6)]
@@ -365,13 +365,15 @@ class Engine:
         _check(lib().loam_batch_download(self.h, od, aft, ctypes.byref(st)))
         return (np.array([p.arr() for p in od]), np.array([p.arr() for p in aft]), st.as_dict())
 
-    def batch_iterations(self):
-        """per-problem (odometry, mapping) L-M iteration counts of the last run"""
+    def batch_lm_info(self):
+        """per-problem L-M results of the last run: (odometry iterations, mapping iterations, the
+        odometry's solved transform [n, 6])"""
         od = np.zeros(self.n, np.int32)
         mp = np.zeros(self.n, np.int32)
+        tr = (Pose6 * self.n)()
         P = ctypes.POINTER(ctypes.c_int32)
-        _check(lib().loam_batch_iterations(self.h, od.ctypes.data_as(P), mp.ctypes.data_as(P)))
-        return od, mp
+        _check(lib().loam_batch_lm_info(self.h, od.ctypes.data_as(P), mp.ctypes.data_as(P), tr))
+        return od, mp, np.array([p.arr() for p in tr])
 
 
 def maintenance(odom_sum, bef, aft):

@@ -1568,7 +1568,7 @@ int loam_batch_sync(loam_ctx* x) {
   return LOAM_OK;
 }
 
-int loam_batch_iterations(loam_ctx* x, int32_t* od_iters, int32_t* mp_iters) {
+int loam_batch_lm_info(loam_ctx* x, int32_t* od_iters, int32_t* mp_iters, loam_pose6* od_transform) {
   if (!x || x->P == 0) return fail(LOAM_E_INVAL, "no batch");
   HIP_TRY(hipSetDevice(x->device));
   const int P = x->P;
@@ -1578,6 +1578,11 @@ int loam_batch_iterations(loam_ctx* x, int32_t* od_iters, int32_t* mp_iters) {
     std::vector<int> ist((size_t)P * kOdStateInts);
     HIP_TRY(hipMemcpy(ist.data(), x->odb.istate, ist.size() * sizeof(int), hipMemcpyDeviceToHost));
     for (int i = 0; i < P; ++i) od_iters[i] = ist[(size_t)i * kOdStateInts + kIsIters];
+  }
+  if (od_transform) {  // (state floats 0..5: the L-M transform, kOdSum the accumulated pose)
+    std::vector<float> st((size_t)P * kOdStateFloats);
+    HIP_TRY(hipMemcpy(st.data(), x->odb.state, st.size() * sizeof(float), hipMemcpyDeviceToHost));
+    for (int i = 0; i < P; ++i) std::memcpy(&od_transform[i], &st[(size_t)i * kOdStateFloats], sizeof(loam_pose6));
   }
   if (mp_iters) HIP_TRY(mp_batch_iters(x->mpbuf(x->mp_last), x->st, mp_iters));
   return LOAM_OK;

@@ -868,6 +868,10 @@ void od_lm(const Cfg& cfg, OdState& s, const std::vector<P>& sharp, const std::v
 }
 
 // laserOdometry loop body :420-931
+// hook of the oracle's own tests (oracle_problem_with_od): the odometry L-M solution replaced by a
+// given transform before the pose accumulation and TransformToEnd
+thread_local const float* g_od_override = nullptr;
+
 void od_body(const Cfg& cfg, OdState& s, const OdIn& in, OdOut& out) {
   out.published = 0;
   if (!s.inited) {  // :427-456
@@ -888,6 +892,8 @@ void od_body(const Cfg& cfg, OdState& s, const OdIn& in, OdOut& out) {
   s.transform[4] -= s.imuVeloFromStartY * scanPeriod;
   s.transform[5] -= s.imuVeloFromStartZ * scanPeriod;
   if (s.cornerLastNum > 10 && s.surfLastNum > 100) od_lm(cfg, s, *in.sharp, *in.flat);
+  if (g_od_override)
+    for (int k = 0; k < 6; ++k) s.transform[k] = g_od_override[k];
 
   // :830-856
   float rx, ry, rz;
@@ -1634,6 +1640,17 @@ int oracle_problem(const loam_config* cfg, loam_cloud_in prev, loam_cloud_in cur
     st->mp_degenerate_steps = mp.deg_steps; st->mp_grid_shifts = mp.shifts;
   }
   return LOAM_OK;
+}
+
+// oracle_problem with the odometry's L-M solution (transform[6]) replaced by od_transform before it
+// is accumulated and used for TransformToEnd: the reference's mapping for another odometry result
+// (tests/test_gpu_moments.py replays the engine's per-query-moments odometry through it)
+int oracle_problem_with_od(const loam_config* cfg, loam_cloud_in prev, loam_cloud_in cur,
+                           const loam_pose6* od_transform, loam_pose6* od_sum, loam_pose6* aft, loam_stats* st) {
+  g_od_override = &od_transform->rx;
+  const int rc = oracle_problem(cfg, prev, cur, od_sum, aft, st);
+  g_od_override = nullptr;
+  return rc;
 }
 
 // ---- component hooks for the oracle's own known-answer tests

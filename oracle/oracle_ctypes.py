@@ -94,6 +94,8 @@ def lib():
         L.oracle_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(Stats)]
         L.oracle_problem.argtypes = [ctypes.POINTER(Config), CloudIn, CloudIn, ctypes.POINTER(Pose6),
                                      ctypes.POINTER(Pose6), ctypes.POINTER(Stats)]
+        L.oracle_problem_with_od.argtypes = [ctypes.POINTER(Config), CloudIn, CloudIn, ctypes.POINTER(Pose6),
+                                             ctypes.POINTER(Pose6), ctypes.POINTER(Pose6), ctypes.POINTER(Stats)]
         L.oracle_voxel_grid.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_float,
                                         ctypes.c_void_p, ctypes.c_int]
         L.oracle_knn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
@@ -238,5 +240,18 @@ def problem(prev, cur, cfg=None):
     od, aft, st = Pose6(), Pose6(), Stats()
     rc = lib().oracle_problem(ctypes.byref(cfg), a, b, ctypes.byref(od), ctypes.byref(aft),
                               ctypes.byref(st))
+    assert rc == 0, rc
+    return od.arr(), aft.arr(), st.as_dict()
+
+
+def problem_with_od(prev, cur, od_transform, cfg=None):
+    """problem() with the odometry's L-M solution replaced by od_transform (6 floats) before its
+    accumulation and TransformToEnd: the reference's mapping for that odometry result"""
+    cfg = cfg or default_config()
+    a, ka = cloud_in(prev)
+    b, kb = cloud_in(cur)
+    od, aft, st = Pose6(), Pose6(), Stats()
+    rc = lib().oracle_problem_with_od(ctypes.byref(cfg), a, b, ctypes.byref(Pose6.of(od_transform)),
+                                      ctypes.byref(od), ctypes.byref(aft), ctypes.byref(st))
     assert rc == 0, rc
     return od.arr(), aft.arr(), st.as_dict()

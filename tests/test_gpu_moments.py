@@ -8,13 +8,17 @@ mapping pose of every problem.  The bit-exact form (od_moments_min above the bat
 against the same oracle runs bit for bit, poses and per-problem L-M iteration counts, so both forms
 are pinned on all 1024 config-4 problems and all 64 config-5 problems.
 
-Every moments error is attributed: the fp64 moments round the normal equations differently from
-the reference's float J entries, a ~1e-7 relative perturbation of each L-M step.  It reaches the
-poses at that size (<= ATTRIB) unless a convergence test (ΔR < 0.1° and ΔT < 0.1 cm odometry,
-0.05 / 0.05 mapping, src/laserOdometry.cpp:824, src/laserMapping.cpp:972) flips, which changes the
-problem's iteration count: every problem with a larger error must show such a flip (odometry or
-mapping iteration count different from the oracle's).  The test prints the error histogram and the
-flipped problems.  The oracle runs on a thread pool (ctypes releases the GIL; the oracle keeps no
+Every moments error is attributed.  The fp64 moments round the odometry's normal equations
+differently from the reference's float J entries: a ~1e-7 relative perturbation of each L-M step,
+which leaves the odometry within a few float ulps of the reference (<= ATTRIB).  A larger error
+has one of two causes, and the test names it for every such problem:
+  * a convergence test flipped (ΔR < 0.1° and ΔT < 0.1 cm odometry, 0.05 / 0.05 mapping,
+    src/laserOdometry.cpp:824, src/laserMapping.cpp:972): the problem's iteration count differs;
+  * the reference's mapping itself moves that far for an odometry input a few ulps away (a 5-NN /
+    acceptance decision at a threshold in :714-877, on a problem whose mapping L-M does not
+    converge): replaying the oracle with the engine's solved odometry transform
+    (oracle_problem_with_od) gives the engine's mapping pose to within ATTRIB.
+The test prints the error histogram and every problem above ATTRIB with its cause.  The oracle runs on a thread pool (ctypes releases the GIL; the oracle keeps no
 global state)."""
 import os
 from concurrent.futures import ThreadPoolExecutor
@@ -46,12 +50,12 @@ def _run(loam, prevs, curs, cfg, **tune):
     e.batch_upload(prevs, curs)
     e.batch_run()
     od, aft, st = e.batch_download()
-    od_it, mp_it = e.batch_iterations()
+    od_it, mp_it, tr = e.batch_lm_info()
     e.close()
-    return od, aft, st, od_it, mp_it
+    return od, aft, st, od_it, mp_it, tr
 
 
-def _check(loam, prevs, curs, cfg, oracle):
+def _check(loam, oc, prevs, curs, cfg, ocfg, oracle):
     od_o, aft_o, od_it_o, mp_it_o = oracle
     exact = _run(loam, prevs, curs, cfg, od_moments_min=1 << 30)
     mom = _run(loam, prevs, curs, cfg, od_moments_min=1)
@@ -73,26 +77,35 @@ def _check(loam, prevs, curs, cfg, oracle):
     print(f"moments: {len(prevs)} problems, max |d odometry| {e_od.max():.3g}, max |d mapping| {e_mp.max():.3g}; "
           f"error histogram {hist}; odometry iterations {int(mom[3].sum())} vs oracle {int(od_it_o.sum())}, "
           f"mapping {int(mom[4].sum())} vs {int(mp_it_o.sum())}")
+    assert e_od.max() <= ATTRIB or np.all(flip_od[e_od > ATTRIB]), "odometry error without a flip"
+    unexplained = []
     for i in np.flatnonzero(flip_od | flip_mp | (err > ATTRIB)):
+        cause = "odometry convergence flip" if flip_od[i] else "mapping convergence flip" if flip_mp[i] else None
+        if cause is None:  # the reference's mapping for the engine's odometry result
+            _, aft_r, _ = oc.problem_with_od(prevs[i], curs[i], mom[5][i], ocfg)
+            d = float(np.abs(mom[1][i] - aft_r).max())
+            cause = f"reference mapping for this odometry result within {d:.2g} of the engine's"
+            if d > ATTRIB:
+                unexplained.append(int(i))
         print(f"  problem {i}: |d odometry| {e_od[i]:.3g} |d mapping| {e_mp[i]:.3g}; odometry iterations "
-              f"{mom[3][i]} (oracle {od_it_o[i]}), mapping {mom[4][i]} (oracle {mp_it_o[i]})")
+              f"{mom[3][i]} (oracle {od_it_o[i]}), mapping {mom[4][i]} (oracle {mp_it_o[i]}): {cause}")
     assert err.max() <= TOL, int(np.argmax(err))
-    unexplained = np.flatnonzero((err > ATTRIB) & ~flip_od & ~flip_mp)
-    assert unexplained.size == 0, f"errors above {ATTRIB} without a convergence flip: {unexplained.tolist()}"
+    assert not unexplained, f"errors above {ATTRIB} with no identified cause: {unexplained}"
     return mom
 
 
 def test_moments_config4_all_1024(loam, oc, sg):
     P = 1024
     prevs, curs = sg.batch_problems(P, base_seed=1000)
-    _check(loam, prevs, curs, None, _oracle_all(oc, prevs, curs))
+    _check(loam, oc, prevs, curs, None, None, _oracle_all(oc, prevs, curs))
 
 
 def test_moments_config5_all_64(loam, oc, sg):
     P = 64
     prevs, curs = sg.batch_problems(P, base_seed=5000, lidar=sg.HDL64)
     cfg = loam.default_config(ring_model=loam.RING_LINEAR, **DENSE)
-    _check(loam, prevs, curs, cfg, _oracle_all(oc, prevs, curs, oc.default_config(ring_model=1, **DENSE)))
+    ocfg = oc.default_config(ring_model=1, **DENSE)
+    _check(loam, oc, prevs, curs, cfg, ocfg, _oracle_all(oc, prevs, curs, ocfg))
 
 
 def test_moments_8gpu_share_fused(loam, oc, sg):

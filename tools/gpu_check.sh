@@ -30,3 +30,10 @@ print("dense", d["dense_batch"]["ms_per_step"], d["dense_batch"]["value"])
 print(" ".join(f"{k}={v:.3f}" for k, v in sorted(d["kernel_ms_per_step"].items(), key=lambda kv: -kv[1])[:14]))
 EOF
 fi
+if [ "${CHAIN:-0}" = 1 ]; then
+  timeout -k 10 300 python tools/chain_split.py > $O/chain_split.txt 2>&1 || { tail -20 $O/chain_split.txt; exit 1; }
+  cat $O/chain_split.txt
+  TAGDIR=$O timeout -k 10 400 bash tools/chain_trace.sh > $O/chain_trace.txt 2>&1 || { tail -20 $O/chain_trace.txt; exit 1; }
+  cp $R/gpurun_out/chain_timeline.txt $O/ 2>/dev/null
+  head -60 $O/chain_trace.txt
+fi
