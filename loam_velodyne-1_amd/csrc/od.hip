@@ -857,6 +857,7 @@ __global__ void k_od_begin(OdBuffers b, FeatView f) {
   ist[kIsGathered] = 0;
   ist[kIsBoxes] = 0;
   b.done[p] = 0;
+  if (p == 0 && b.P == 1) ++b.ls_epoch[0];  // (k_od_lm_stream's publication words)
 }
 
 // TransformToStart of every query at the current transform (:472, :587), lane per query, for
@@ -875,6 +876,120 @@ __global__ __launch_bounds__(kOdThreads) void k_od_sel(OdBuffers b, FeatView f) 
   if (q >= nq) return;
   const float4 po = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
   b.sel[(size_t)p * b.cap_q + q] = loampose::transform_to_start(T, po);
+}
+
+// One wave's association queries q0, q0 + G, ... of problem p (:472-527, :587-650): k_od_assoc's
+// body, also the association phase of the persistent streaming L-M (k_od_lm_stream).  T: the
+// transform for TransformToStart (SEL; otherwise the queries' k_od_sel points are read); seeded:
+// ind holds this frame's previous round; cells / bq_*: the wave's LDS scratch (64 entries each);
+// rsC / rsS: the Last clouds' ring start tables (LDS); wpts / wbox: the wave's work counters
+template <bool SEL>
+LOAM_D void od_assoc_wave(const OdBuffers& b, const FeatView& f, int p, int last_buf, int q0, int G, const float* T,
+                          bool seeded, int* cells, float4* bq_s4, float4* bq_d, int4* bq_j, const int* rsC,
+                          const int* rsS, int& wpts, int& wbox) {
+  const int lane = lane_id();
+  const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
+  const size_t lp = (size_t)last_buf * b.P + p;
+  const int C = b.nlast[(p * kOdBufs + last_buf) * 2 + 0], S = b.nlast[(p * kOdBufs + last_buf) * 2 + 1];
+  const float4* CL = b.lastC + lp * b.capC;
+  const float4* SL = b.lastS + lp * b.capS;
+  int* ind = b.ind + (size_t)p * 3 * b.cap_q;
+  const bool use_mono = b.P >= b.tune.od_win_mono_min && (b.tune.od_win_mono & (seeded ? 2 : 1)) != 0;
+  const bool tight = LOAM_WIN_TIGHTEN == 1 || (LOAM_WIN_TIGHTEN == 2 && !seeded);
+  const int hCT = b.hC_T[last_buf * b.P + p], hST = b.hS_T[last_buf * b.P + p];
+  const bool monoC = b.mono[lp * 2 + 0] != 0, monoS = b.mono[lp * 2 + 1] != 0;
+  // The wave's queries q0, q0 + G, ... in batches of 64: lane l first fetches query l's
+  // TransformToStart point and its seeds — the previous round's choices (ind, rounds after the
+  // first), their rings and squared distances at this round's transform — for all 64 at once
+  // (two dependent loads per batch instead of per query), staged in LDS for the per-query walks.
+  for (int i0 = 0; q0 + i0 * G < nq; i0 += 64) {
+    {
+      const int ql = q0 + (i0 + lane) * G;
+      if (ql < nq) {
+        float4 s4;
+        if constexpr (SEL) {
+          const float4 po = ql < nc ? f.sharp[(size_t)p * f.sharp_stride + ql] : f.flat[(size_t)p * f.flat_stride + (ql - nc)];
+          s4 = loampose::transform_to_start(T, po);
+        } else {
+          s4 = b.sel[(size_t)p * b.cap_q + ql];
+        }
+        const float4* Lc = ql < nc ? CL : SL;
+        int j[3] = {-1, -1, -1};
+        if (seeded) {
+#pragma unroll
+          for (int k = 0; k < 3; ++k) j[k] = ind[k * b.cap_q + ql];
+        }
+        float4 sp[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sp[k] = j[k] >= 0 ? Lc[j[k]] : make_float4(0, 0, 0, 0);
+        const float nnb = j[0] >= 0 ? sqdist(sp[0].x, sp[0].y, sp[0].z, s4.x, s4.y, s4.z) : 3.4e38f;
+        const float d1 = sqdist(sp[1].x, sp[1].y, sp[1].z, s4.x, s4.y, s4.z);
+        const float d2 = sqdist(sp[2].x, sp[2].y, sp[2].z, s4.x, s4.y, s4.z);
+        bq_s4[lane] = s4;
+        bq_j[lane] = make_int4(j[0], j[1], j[2], (int)sp[1].w | ((int)sp[2].w << 16));
+        bq_d[lane] = make_float4(nnb, d1, d2, 0.0f);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int nb = min(64, (nq - q0 + G - 1) / G - i0);
+    for (int i = 0; i < nb; ++i) {
+      const int q = q0 + (i0 + i) * G;
+      const float4 s4 = bq_s4[i];
+      const int4 jj = bq_j[i];
+      const float4 dd = bq_d[i];
+      const int j1 = jj.y, j2 = jj.z, r1 = jj.w & 0xffff, r2 = jj.w >> 16;
+      const float nnb = dd.x, d1 = dd.y, d2 = dd.z;
+      int i1, i2, i3 = -1;
+      // the cells' window bounds in the first round only (later rounds have their seeds: the extra
+      // pass over the cells cost more than the chunks it saved there)
+      WinBound wb;
+      if (q < nc && monoC && use_mono) {
+        const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
+        const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC, hCT, CL, ch, C, 1.0f,
+                                         1.0f, s4, nnb, cells, wpts, wbox, seeded || !LOAM_WIN_WB ? -1 : 0, min(nc, C), true, &wb);
+        i1 = i2 = -1;
+        if (nn != ~0ull && D(__uint_as_float((uint32_t)(nn >> 32))) < 25) {
+          const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u), fe = min(nc, C);
+          i1 = c;
+          uint64_t k2 = ~0ull, k3 = mono_seed_key(rsC, c, scan, fe, j1, d1, false);
+          wave_window_mono(CL, b.fC + lp * 2 * subs_of(b.capC), rsC, c, scan, fe, s4, false, wb, tight, k2, k3, wpts, wbox);
+          if (k3 != ~0ull) i2 = mono_decode(c, k3);
+        }
+      } else if (q >= nc && monoS && use_mono) {
+        const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
+        const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS, hST, SL, ch, S, 1.0f,
+                                         1.0f, s4, nnb, cells, wpts, wbox, seeded || !LOAM_WIN_WB ? -1 : 1, min(ns, S), true, &wb);
+        i1 = i2 = -1;
+        if (nn != ~0ull && D(__uint_as_float((uint32_t)(nn >> 32))) < 25) {
+          const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u), fe = min(ns, S);
+          i1 = c;
+          uint64_t k2 = mono_seed_key(rsS, c, scan, fe, j1, d1, true);
+          uint64_t k3 = mono_seed_key(rsS, c, scan, fe, j2, d2, false);
+          wave_window_mono(SL, b.fS + lp * 2 * subs_of(b.capS), rsS, c, scan, fe, s4, true, wb, tight, k2, k3, wpts, wbox);
+          if (k2 != ~0ull) i2 = mono_decode(c, k2);
+          if (k3 != ~0ull) i3 = mono_decode(c, k3);
+        }
+      } else if (q < nc) {
+        const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
+        const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC, hCT, CL, ch, C, 1.0f,
+                                         1.0f, s4, nnb, cells, wpts, wbox, seeded ? -1 : 0, min(nc, C), monoC, &wb);
+        wave_assoc_corner(CL, ch, min(nc, C), nn, s4, j1, r1, d1, wb, monoC, i1, i2, wpts, wbox);
+      } else {
+        const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
+        const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS, hST, SL, ch, S, 1.0f,
+                                         1.0f, s4, nnb, cells, wpts, wbox, seeded ? -1 : 1, min(ns, S), monoS, &wb);
+        wave_assoc_surf(SL, ch, min(ns, S), nn, s4, j1, r1, d1, j2, r2, d2, wb, monoS, i1, i2, i3, wpts, wbox);
+      }
+      if (lane == 0) {
+        LOAM_CHECK(q < b.cap_q && p < b.P, q, p);
+        LOAM_CHECK(i1 < (q < nc ? C : S) && i2 < (q < nc ? C : S) && i3 < S, i1, i2);
+        ind[q] = i1;
+        ind[b.cap_q + q] = i2;
+        ind[2 * b.cap_q + q] = i3;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
 }
 
 // association (:472-527, :587-650), one wave per query: exact NN through the hash, then the
@@ -896,123 +1011,24 @@ __global__ __launch_bounds__(kAsThreads) __attribute__((amdgpu_waves_per_eu(SEL 
   __shared__ int cells[kAsWaves][64];
   __shared__ float4 bq_s4[kAsWaves][64], bq_d[kAsWaves][64];
   __shared__ int4 bq_j[kAsWaves][64];
-  const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
-  const float4* sel = b.sel + (size_t)p * b.cap_q;
-  const size_t lp = (size_t)last_buf * b.P + p;
-  const int C = b.nlast[(p * kOdBufs + last_buf) * 2 + 0], S = b.nlast[(p * kOdBufs + last_buf) * 2 + 1];
-  const float4* CL = b.lastC + lp * b.capC;
-  const float4* SL = b.lastS + lp * b.capS;
-  int* ind = b.ind + (size_t)p * 3 * b.cap_q;
-  int wpts = 0, wbox = 0;  // wave-uniform work counters (loam_stats od_assoc_gathered / _boxes)
-  const bool seeded = ist[kIsIters] > 0;  // ind holds this frame's previous round
-  const bool use_mono = b.P >= b.tune.od_win_mono_min && (b.tune.od_win_mono & (seeded ? 2 : 1)) != 0;
-  const bool tight = LOAM_WIN_TIGHTEN == 1 || (LOAM_WIN_TIGHTEN == 2 && !seeded);
-  const int hCT = b.hC_T[last_buf * b.P + p], hST = b.hS_T[last_buf * b.P + p];
-  const bool monoC = b.mono[lp * 2 + 0] != 0, monoS = b.mono[lp * 2 + 1] != 0;
   __shared__ int rsC[kRingTab], rsS[kRingTab];  // the ring start tables (ring-monotone clouds)
   static_assert(kAsWaves == 1, "the ring tables are loaded by the workgroup's one wave");
+  const size_t lp = (size_t)last_buf * b.P + p;
   for (int r = lane; r < kRingTab; r += 64) {
     rsC[r] = b.rstart[lp * 2 * kRingTab + r];
     rsS[r] = b.rstart[lp * 2 * kRingTab + kRingTab + r];
   }
   __builtin_amdgcn_wave_barrier();
-  const int G = gridDim.x * kAsWaves, q0 = blk.x * kAsWaves + w;
-  // The wave's queries q0, q0 + G, ... in batches of 64: lane l first fetches query l's
-  // TransformToStart point and its seeds — the previous round's choices (ind, rounds after the
-  // first), their rings and squared distances at this round's transform — for all 64 at once
-  // (two dependent loads per batch instead of per query), staged in LDS for the per-query walks.
-  for (int i0 = 0; q0 + i0 * G < nq; i0 += 64) {
-    {
-      const int ql = q0 + (i0 + lane) * G;
-      if (ql < nq) {
-        float4 s4;
-        if constexpr (SEL) {
-          const float* st = b.state + (size_t)p * kOdStateFloats;
-          float T[6];
+  float T[6];
+  if constexpr (SEL) {
+    const float* st = b.state + (size_t)p * kOdStateFloats;
 #pragma unroll
-          for (int k = 0; k < 6; ++k) T[k] = st[k];
-          const float4 po = ql < nc ? f.sharp[(size_t)p * f.sharp_stride + ql] : f.flat[(size_t)p * f.flat_stride + (ql - nc)];
-          s4 = loampose::transform_to_start(T, po);
-        } else {
-          s4 = sel[ql];
-        }
-        const float4* Lc = ql < nc ? CL : SL;
-        int j[3] = {-1, -1, -1};
-        if (seeded) {
-#pragma unroll
-          for (int k = 0; k < 3; ++k) j[k] = ind[k * b.cap_q + ql];
-        }
-        float4 sp[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) sp[k] = j[k] >= 0 ? Lc[j[k]] : make_float4(0, 0, 0, 0);
-        const float nnb = j[0] >= 0 ? sqdist(sp[0].x, sp[0].y, sp[0].z, s4.x, s4.y, s4.z) : 3.4e38f;
-        const float d1 = sqdist(sp[1].x, sp[1].y, sp[1].z, s4.x, s4.y, s4.z);
-        const float d2 = sqdist(sp[2].x, sp[2].y, sp[2].z, s4.x, s4.y, s4.z);
-        bq_s4[w][lane] = s4;
-        bq_j[w][lane] = make_int4(j[0], j[1], j[2], (int)sp[1].w | ((int)sp[2].w << 16));
-        bq_d[w][lane] = make_float4(nnb, d1, d2, 0.0f);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    const int nb = min(64, (nq - q0 + G - 1) / G - i0);
-    for (int i = 0; i < nb; ++i) {
-      const int q = q0 + (i0 + i) * G;
-      const float4 s4 = bq_s4[w][i];
-      const int4 jj = bq_j[w][i];
-      const float4 dd = bq_d[w][i];
-      const int j1 = jj.y, j2 = jj.z, r1 = jj.w & 0xffff, r2 = jj.w >> 16;
-      const float nnb = dd.x, d1 = dd.y, d2 = dd.z;
-      int i1, i2, i3 = -1;
-      // the cells' window bounds in the first round only (later rounds have their seeds: the extra
-      // pass over the cells cost more than the chunks it saved there)
-      WinBound wb;
-      if (q < nc && monoC && use_mono) {
-        const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
-        const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC, hCT, CL, ch, C, 1.0f,
-                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded || !LOAM_WIN_WB ? -1 : 0, min(nc, C), true, &wb);
-        i1 = i2 = -1;
-        if (nn != ~0ull && D(__uint_as_float((uint32_t)(nn >> 32))) < 25) {
-          const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u), fe = min(nc, C);
-          i1 = c;
-          uint64_t k2 = ~0ull, k3 = mono_seed_key(rsC, c, scan, fe, j1, d1, false);
-          wave_window_mono(CL, b.fC + lp * 2 * subs_of(b.capC), rsC, c, scan, fe, s4, false, wb, tight, k2, k3, wpts, wbox);
-          if (k3 != ~0ull) i2 = mono_decode(c, k3);
-        }
-      } else if (q >= nc && monoS && use_mono) {
-        const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
-        const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS, hST, SL, ch, S, 1.0f,
-                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded || !LOAM_WIN_WB ? -1 : 1, min(ns, S), true, &wb);
-        i1 = i2 = -1;
-        if (nn != ~0ull && D(__uint_as_float((uint32_t)(nn >> 32))) < 25) {
-          const int c = (int)((uint32_t)nn >> 8), scan = (int)((uint32_t)nn & 255u), fe = min(ns, S);
-          i1 = c;
-          uint64_t k2 = mono_seed_key(rsS, c, scan, fe, j1, d1, true);
-          uint64_t k3 = mono_seed_key(rsS, c, scan, fe, j2, d2, false);
-          wave_window_mono(SL, b.fS + lp * 2 * subs_of(b.capS), rsS, c, scan, fe, s4, true, wb, tight, k2, k3, wpts, wbox);
-          if (k2 != ~0ull) i2 = mono_decode(c, k2);
-          if (k3 != ~0ull) i3 = mono_decode(c, k3);
-        }
-      } else if (q < nc) {
-        const float4* ch = b.cC + lp * 2 * chunks_of(b.capC);
-        const uint64_t nn = wave_hash_nn(b.hC_start + lp * (b.tC + 1), b.hC_pts + lp * b.capC, hCT, CL, ch, C, 1.0f,
-                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded ? -1 : 0, min(nc, C), monoC, &wb);
-        wave_assoc_corner(CL, ch, min(nc, C), nn, s4, j1, r1, d1, wb, monoC, i1, i2, wpts, wbox);
-      } else {
-        const float4* ch = b.cS + lp * 2 * chunks_of(b.capS);
-        const uint64_t nn = wave_hash_nn(b.hS_start + lp * (b.tS + 1), b.hS_pts + lp * b.capS, hST, SL, ch, S, 1.0f,
-                                         1.0f, s4, nnb, cells[w], wpts, wbox, seeded ? -1 : 1, min(ns, S), monoS, &wb);
-        wave_assoc_surf(SL, ch, min(ns, S), nn, s4, j1, r1, d1, j2, r2, d2, wb, monoS, i1, i2, i3, wpts, wbox);
-      }
-      if (lane == 0) {
-        LOAM_CHECK(q < b.cap_q && p < b.P, q, p);
-        LOAM_CHECK(i1 < (q < nc ? C : S) && i2 < (q < nc ? C : S) && i3 < S, i1, i2);
-        ind[q] = i1;
-        ind[b.cap_q + q] = i2;
-        ind[2 * b.cap_q + q] = i3;
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
+    for (int k = 0; k < 6; ++k) T[k] = st[k];
   }
+  int wpts = 0, wbox = 0;  // wave-uniform work counters (loam_stats od_assoc_gathered / _boxes)
+  const bool seeded = ist[kIsIters] > 0;  // ind holds this frame's previous round
+  od_assoc_wave<SEL>(b, f, p, last_buf, blk.x * kAsWaves + w, gridDim.x * kAsWaves, T, seeded, cells[w], bq_s4[w],
+                     bq_d[w], bq_j[w], rsC, rsS, wpts, wbox);
   if (COUNT && lane == 0) {
     if (wpts) atomicAdd((int*)&ist[kIsGathered], wpts);
     if (wbox) atomicAdd((int*)&ist[kIsBoxes], wbox);
@@ -1619,6 +1635,240 @@ __global__ __launch_bounds__(kOdThreads) void k_od_rows_small(OdBuffers b, FeatV
   }
 }
 
+// ---- the one-problem L-M as one persistent launch (streaming: the config-3 chain, config 2) ----
+// The launch-per-iteration form pays a dispatch and a grid-wide hand-off per iteration (25 rows
+// launches + 5 association launches per sweep, ~8 us each plus the gaps between them).  Here G
+// workgroups of kOdLsThreads stay resident for the whole loop.  Each query belongs to one wave
+// for the association and to its workgroup for the rows (its stored coefficients of earlier
+// iterations, Q12, are read back only by the workgroup that wrote them), so the one exchange per
+// iteration is the 28 partial sums: every workgroup publishes its partial with write-through
+// stores and a publication word, reads all G partials, sums them in workgroup order and runs the
+// step itself — the same sums and the same code in every workgroup, so every workgroup holds the
+// same transform and takes the same convergence decision, with no second hand-off.  Partials are
+// double-buffered by iteration parity (a workgroup can be at most one iteration ahead of the
+// slowest).  Co-residency of the G workgroups is checked on the host (od_solve); a workgroup
+// waits only for partials of the current iteration, which every resident workgroup produces.
+constexpr int kOdLsThreads = 512, kOdLsWaves = kOdLsThreads / 64;
+
+// the workgroup-local L-M state (LDS): od_step's global state for the persistent kernel
+struct OdLsState {
+  float T[6], matP[36], trig[6];
+  int degen, iters, assoc, rows, deg_steps, nan_skips, stop;
+};
+
+// od_step on the workgroup-local state (wave 0): the same reads, arithmetic and decisions
+LOAM_D void od_step_ls(int iter, const double* tot, OdLsState& S, float* AtA, float* AtB, float* X, float* lm_ws,
+                       int* lm_iws, float* jE, float* jV) {
+  const int lane = lane_id();
+  const int nrows = (int)tot[27];
+  if (lane == 0) {
+    S.iters = iter + 1;
+    if (iter % 5 == 0) ++S.assoc;
+    S.rows += nrows;
+    if (nrows >= 10) {  // :697-700
+      int k = 0;
+      for (int i = 0; i < 6; ++i)
+        for (int jj = i; jj < 6; ++jj) {
+          AtA[i * 6 + jj] = (float)tot[k];
+          AtA[jj * 6 + i] = (float)tot[k];
+          ++k;
+        }
+      for (int i = 0; i < 6; ++i) AtB[i] = (float)tot[21 + i];
+    }
+  }
+  if (nrows < 10) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  bool eig = iter == 0, cert = false;
+  if (eig) {
+    cert = loamla::nondegenerate_certified(AtA, 10.0f);
+    eig = !cert;
+    if (eig) loamla::jacobi6_wave(AtA, jE, jV);
+  }
+  int degen = S.degen;
+  loamla::lm_step_wave(AtA, AtB, iter, 10.0f, &degen, S.matP, X, lm_ws, lm_iws, eig ? jE : nullptr, eig ? jV : nullptr,
+                       cert);
+  if (lane != 0) return;
+  S.degen = degen;
+  if (degen) ++S.deg_steps;
+  const bool nan = isnan(X[0]) || isnan(X[1]) || isnan(X[2]) || isnan(X[3]) || isnan(X[4]) || isnan(X[5]);
+  if (!nan)  // Q16
+    for (int q = 0; q < 6; ++q) S.T[q] = S.T[q] + X[q];
+  else
+    ++S.nan_skips;
+  const float dR = loamla::delta_r(X), dT = loamla::delta_t(X);
+  if (D(dR) < 0.1 && D(dT) < 0.1) S.stop = 1;
+}
+
+__global__ __launch_bounds__(kOdLsThreads) void k_od_lm_stream(OdBuffers b, FeatView f, int last_buf) {
+  constexpr int NW = kOdLsWaves;
+  const int g = blockIdx.x, G = gridDim.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6, p = 0;
+  int* ist = b.istate;
+  float* st = b.state;
+  if (!ist[kIsActive] || ist[kIsStop]) return;  // (the same value in every workgroup)
+  __shared__ int cells[NW][64];
+  __shared__ float4 bq_s4[NW][64], bq_d[NW][64];
+  __shared__ int4 bq_j[NW][64];
+  __shared__ int rsC[kRingTab], rsS[kRingTab];
+  __shared__ double red[NW][28], slice[8][28], tot[28];
+  __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs], jE[6], jV[36];
+  __shared__ int lm_iws[12];
+  __shared__ OdLsState S;
+  __shared__ unsigned long long sh_epoch;
+  const size_t lp = (size_t)last_buf * b.P + p;
+  for (int r = tid; r < kRingTab; r += kOdLsThreads) {
+    rsC[r] = b.rstart[lp * 2 * kRingTab + r];
+    rsS[r] = b.rstart[lp * 2 * kRingTab + kRingTab + r];
+  }
+  if (tid < 6) S.T[tid] = st[tid];
+  if (tid < 36) S.matP[tid] = st[kOdMatP + tid];
+  if (tid == 0) {
+    S.degen = ist[kIsDegenerate];
+    S.iters = 0;
+    S.assoc = 0;
+    S.rows = 0;
+    S.deg_steps = 0;
+    S.nan_skips = 0;
+    S.stop = 0;
+    sh_epoch = b.ls_epoch[0];
+  }
+  __syncthreads();
+  if (tid < 6) S.trig[tid] = (float)((tid & 1) ? dcos(S.T[tid >> 1]) : dsin(S.T[tid >> 1]));
+  const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
+  const int Wt = G * NW;                 // association waves: wave (g, w) takes queries g NW + w + k Wt
+  const int nloc = nq > g * NW ? ((nq - g * NW - 1) / Wt + 1) * NW : 0;  // (an upper bound; q < nq tested)
+  float4* qcf = b.q_cf;
+  const unsigned long long tag0 = sh_epoch << 8;
+  int wpts = 0, wbox = 0;
+  __syncthreads();
+  for (int it = 0; it < b.max_iter; ++it) {
+    if (it % 5 == 0) {  // Q10
+      float T[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) T[k] = S.T[k];
+      od_assoc_wave<true>(b, f, p, last_buf, g * NW + w, Wt, T, it > 0, cells[w], bq_s4[w], bq_d[w], bq_j[w], rsC, rsS,
+                          wpts, wbox);
+      __syncthreads();  // (the rows below read the association of this workgroup's queries)
+    }
+    // rows: every (query of this workgroup, stored iteration) pair re-evaluated at the current
+    // transform; the current iteration's coefficient computed and stored first by its own pair
+    double acc[28];
+#pragma unroll
+    for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+    {
+      float T[6], trig[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) { T[k] = S.T[k]; trig[k] = S.trig[k]; }
+      const int npair = nloc * (it + 1);
+      for (int e = tid; e < npair; e += kOdLsThreads) {
+        const int l = e % nloc, its = e / nloc;
+        const int q = g * NW + (l % NW) + (l / NW) * Wt;
+        if (q >= nq) continue;
+        const float4 po = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
+        float4 c4;
+        bool okit;
+        if (its == it) {
+          int ok;
+          od_row_coeff(b, f, p, q, nc, lp, it, T, po, c4, ok);
+          okit = ok != 0;
+          qcf[(size_t)it * b.cap_q + q] = c4;
+        } else {
+          c4 = qcf[(size_t)its * b.cap_q + q];
+          okit = row_ok(c4);
+        }
+        od_row_accum(od_jfactors(trig, T, po), c4, okit, acc);
+      }
+    }
+    wave_reduce_scatter_28(acc);
+    if ((lane & 1) == 0 && (lane >> 1) < 28) red[w][lane >> 1] = acc[0];
+    __syncthreads();
+    const int par = it & 1;
+    if (tid < 28) {  // this workgroup's partial, waves in order, stored write-through
+      double v = red[0][tid];
+      for (int ww = 1; ww < NW; ++ww) v += red[ww][tid];
+      store_partial(&b.ls_part[((size_t)par * kOdLsMaxG + g) * 28 + tid], v);
+    }
+    if (tid < 64) {
+      __builtin_amdgcn_wave_barrier();  // (every lane's store drained: store_partial waits for it)
+      if (tid == 0)
+        __hip_atomic_store(&b.ls_flag[g], tag0 + (unsigned long long)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // every workgroup's partial of this iteration
+    if (tid < G) {
+      const unsigned long long want = tag0 + (unsigned long long)(it + 1);
+      while (__hip_atomic_load(&b.ls_flag[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want)
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();
+    if (tid < 8 * 28) {  // fixed order: slice s sums partials s, s + 8, ...; the slices in order
+      const int v = tid % 28, sl = tid / 28;
+      const double* pp = b.ls_part + (size_t)par * kOdLsMaxG * 28 + v;
+      double a = 0.0;
+      for (int g0 = sl; g0 < G; g0 += 8 * 8) {
+        double t8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int gg = g0 + 8 * u;
+          t8[u] = gg < G ? __hip_atomic_load(&pp[(size_t)gg * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (g0 + 8 * u < G) a += t8[u];
+      }
+      slice[sl][v] = a;
+    }
+    __syncthreads();
+    if (tid < 28) {
+      double v = slice[0][tid];
+#pragma unroll
+      for (int sl = 1; sl < 8; ++sl) v += slice[sl][tid];
+      tot[tid] = v;
+    }
+    __syncthreads();
+    if (tid < 64) od_step_ls(it, tot, S, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
+    __syncthreads();
+    if (S.stop) break;
+    if (tid < 6) S.trig[tid] = (float)((tid & 1) ? dcos(S.T[tid >> 1]) : dsin(S.T[tid >> 1]));
+    __syncthreads();
+  }
+  if (g == 0) {  // the state for the kernels after the loop (the same in every workgroup)
+    if (tid < 6) st[tid] = S.T[tid];
+    if (tid < 36) st[kOdMatP + tid] = S.matP[tid];
+    if (tid == 0) {
+      ist[kIsDegenerate] = S.degen;
+      ist[kIsIters] = S.iters;
+      ist[kIsAssoc] = S.assoc;
+      ist[kIsRows] = S.rows;
+      ist[kIsDegSteps] = S.deg_steps;
+      ist[kIsNanSkips] = S.nan_skips;
+      ist[kIsStop] = S.stop;
+    }
+  }
+  if (lane == 0) {  // (work counters: every wave's association)
+    if (wpts) atomicAdd((int*)&ist[kIsGathered], wpts);
+    if (wbox) atomicAdd((int*)&ist[kIsBoxes], wbox);
+  }
+}
+
+// workgroups of k_od_lm_stream for a query capacity (one association wave per query up to
+// kOdLsMaxG workgroups), or 0 when they could not all be resident at once (the per-iteration
+// launches run instead)
+int od_lm_stream_grid(int cap_q) {
+  static int cap[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cap[dev] == 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_od_lm_stream, kOdLsThreads, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      per_cu = cus = 0;
+    cap[dev] = std::max(1, per_cu * cus);
+  }
+  const int G = std::min(kOdLsMaxG, (cap_q + kOdLsWaves - 1) / kOdLsWaves);
+  return 2 * G <= cap[dev] ? G : 0;  // (a margin of 2: other streams' kernels may hold slots a while)
+}
+
 // the step as its own launch (large batches): one wave per problem
 __global__ __launch_bounds__(64) void k_od_step(OdBuffers b, int iter, int gq) {
   const int p = blockIdx.x, lane = threadIdx.x;
@@ -1900,6 +2150,9 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   // per-workgroup partials: [P][gq][28], or [P][gq * max_iter][28] for the small-batch rows kernel
   A(&b.part, (size_t)P * b.gq * max_iter * 28 * sizeof(double));  // (k_od_rows_small: per stored iteration)
   A(&b.done, (size_t)P * sizeof(int));
+  A(&b.ls_part, (size_t)2 * kOdLsMaxG * 28 * sizeof(double));
+  A(&b.ls_flag, (size_t)kOdLsMaxG * sizeof(unsigned long long));
+  A(&b.ls_epoch, sizeof(unsigned long long));
   A(&b.mono, (size_t)kOdBufs * P * 2 * sizeof(int));
   A(&b.rstart, (size_t)kOdBufs * P * 2 * kRingTab * sizeof(int));
   if (A.err != hipSuccess) {
@@ -1907,6 +2160,8 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
     return A.err;
   }
   if (A.err == hipSuccess) A.err = hipMemset(b.done, 0, (size_t)P * sizeof(int));
+  if (A.err == hipSuccess) A.err = hipMemset(b.ls_flag, 0, (size_t)kOdLsMaxG * sizeof(unsigned long long));
+  if (A.err == hipSuccess) A.err = hipMemset(b.ls_epoch, 0, sizeof(unsigned long long));
   for (int k = 0; k < 3; ++k)
     if (A.err == hipSuccess) A.err = hipMemset(b.state_set[k], 0, (size_t)P * kOdStateFloats * sizeof(float));
   for (int k = 0; k < 3; ++k)
@@ -1925,7 +2180,8 @@ void od_free(OdBuffers& b) {
   if (b.hash_done) (void)hipEventDestroy(b.hash_done);
   void* ptrs[] = {b.state_set[0], b.state_set[1], b.state_set[2], b.istate_set[0], b.istate_set[1], b.istate_set[2], b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
-                  b.ind, b.sel, b.q_cf, b.q_ok, b.mom, b.qa, b.part, b.done, b.mono, b.rstart, b.fC, b.fS};
+                  b.ind, b.sel, b.q_cf, b.q_ok, b.mom, b.qa, b.part, b.done, b.mono, b.rstart, b.fC, b.fS,
+                  b.ls_part, b.ls_flag, b.ls_epoch};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = OdBuffers();
@@ -1999,7 +2255,13 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
   // workgroup per problem (the queries must fit its lanes)
   const Tuning& tn = b.tune;
   const bool lm_round = P >= tn.od_lm_min && P <= tn.od_lm_max && b.cap_q <= kOdLmThreads;
-  for (int it = 0; it < b.max_iter; ++it) {
+  // one problem (streaming): the whole L-M loop as one persistent launch (tuning od_persist)
+  const int gls = P == 1 && tn.od_persist ? od_lm_stream_grid(b.cap_q) : 0;
+  if (gls > 0) {
+    hipLaunchKernelGGL(k_od_lm_stream, dim3(gls), dim3(kOdLsThreads), 0, st, b, f, last_buf);
+    mark("k_od_lm_stream");
+  }
+  for (int it = 0; it < (gls > 0 ? 0 : b.max_iter); ++it) {
     if (it % 5 == 0) {  // Q10
       // one wave per query when the batch is small (streaming: TransformToStart in the wave), 64
       // waves per problem otherwise (the queries transformed by k_od_sel first)

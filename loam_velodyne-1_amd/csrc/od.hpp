@@ -9,6 +9,8 @@
 
 namespace loam {
 
+// k_od_lm_stream: workgroups at most (each serves 8 association waves / their queries' rows)
+constexpr int kOdLsMaxG = 128;
 // per-problem float state: transform[6] | transformSum[6] | matP[36] | imu_trans[12]
 #ifndef LOAM_OD_CHUNK
 #define LOAM_OD_CHUNK 64
@@ -123,6 +125,12 @@ struct OdBuffers {
   double* mom = nullptr;      // [P][10][cap_q] per-query fp64 moments of the stored rows (tuning od_moments)
   double* part = nullptr;     // [P][gq][28] per-workgroup JᵀJ | Jᵀb | rows
   int* done = nullptr;        // [P] workgroups of k_od_rows finished (the last one runs the step)
+  // the persistent one-problem L-M (k_od_lm_stream): per workgroup and iteration parity its partial
+  // sums, per workgroup its publication word (epoch << 8 | iteration + 1), and the launch epoch
+  // (advanced by k_od_begin, so a replayed graph gets a fresh one)
+  double* ls_part = nullptr;              // [2][kOdLsMaxG][28]
+  unsigned long long* ls_flag = nullptr;  // [kOdLsMaxG]
+  unsigned long long* ls_epoch = nullptr; // [1]
   int* mono = nullptr;        // [kOdBufs][P][2] Last corner / surf of each buffer ring-monotone (HashJob::mono)
   int* rstart = nullptr;      // [kOdBufs][P][2][kRingTab] their ring start tables (HashJob::rstart)
   Tuning tune;                // host-side launch choices (od_solve)

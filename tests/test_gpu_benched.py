@@ -49,7 +49,8 @@ def test_config3_full220_device_chain(loam, sg):
     check_config3_full(traj)
 
 
-@pytest.mark.parametrize("tune", [{"vg_merge": 0}, {"od_win_mono_min": 1}], ids=["no_vg_merge", "win_mono"])
+@pytest.mark.parametrize("tune", [{"vg_merge": 0}, {"od_win_mono_min": 1}, {"od_persist": 0}, {"od_graph": 0}],
+                         ids=["no_vg_merge", "win_mono", "per_iteration_launches", "no_graph"])
 def test_config3_full220_tuned(loam, sg, tune):
     """the 220 sweeps through loam_chain_sweep with a non-default launch choice: the cascade instead of
     the incremental cube VoxelGrid (k_vg_merge, the default, takes the growing map's big cubes); the
