@@ -99,6 +99,8 @@ struct Tuning {
                            // three-context pipeline measured 0.45-0.51 -> 0.77-1.13 ms/sweep with it)
   int od_persist = 1;      // one problem (streaming): the odometry L-M loop as one persistent launch
                            // (k_od_lm_stream) instead of a launch per iteration and association round
+  int mp_persist = 1;      // one instance (streaming): the mapping L-M loop as one persistent launch
+                           // (k_mp_lm_stream) instead of a k_mp_lm_small launch per iteration
   int od_moments_min = 64; // for P >= this (and P > od_small_max), k_od_rows keeps each query's
                            // stored rows (Q12) as fp64 moments instead of re-evaluating them every
                            // iteration: O(queries) per iteration, not bit-identical, within 1e-4 of the
@@ -124,7 +126,8 @@ struct Tuning {
                     {"step_pipe", &step_pipe, 0, 1 << 20}, {"batch_streams", &batch_streams, 0, 1},
                     {"pipe_mp_sets", &pipe_mp_sets, 1, 2}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
                     {"od_win_mono", &od_win_mono, 0, 3}, {"od_win_mono_min", &od_win_mono_min, 1, 1 << 20},
-                    {"od_moments_min", &od_moments_min, 1, 1 << 30}, {"od_persist", &od_persist, 0, 1}};
+                    {"od_moments_min", &od_moments_min, 1, 1 << 30}, {"od_persist", &od_persist, 0, 1},
+                    {"mp_persist", &mp_persist, 0, 1}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {
         if (read) {

@@ -1148,6 +1148,7 @@ __global__ void k_mp_lm_begin(MpBuffers b) {
   ist[kMiDegSteps] = 0;
   ist[kMiNnCand] = 0;
   ist[kMiNnCells] = 0;
+  if (p == 0 && b.P == 1) ++b.ls_epoch[0];  // (k_mp_lm_stream's publication words)
 }
 
 // One L-M iteration's correspondences (:714-877), lane per stack point (corner, then surf), in
@@ -1965,6 +1966,196 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_small(MpBuffers b) {
   }
 }
 
+// ---- the one-instance mapping L-M as one persistent launch (streaming: config 3, config 2) ----
+// k_mp_lm_small's iteration (5-NN, fit, row per query group of kMpNnLanes lanes) for every
+// iteration in one launch, as k_od_lm_stream does for the odometry: a query stays on the same
+// lanes for the whole loop (its 5-NN seeds and fit record are read back by the lanes that wrote
+// them), the partial sums are exchanged per iteration with write-through stores and a publication
+// word per workgroup, and every workgroup sums all G partials in workgroup order and runs the step
+// on its own copy of the state: the same transform and the same convergence decision everywhere.
+struct MpLsState {
+  float T[6], matP[36];
+  int degen, iters, rows, deg_steps, stop;
+};
+
+// mp_step on the workgroup-local state (the first wave): the same arithmetic and decisions
+LOAM_D void mp_step_ls(int max_iter, const double* tot, MpLsState& S, MpStepScratch& sh) {
+  const int lane = lane_id();
+  const int iter = S.iters;
+  const int nrows = (int)tot[27];
+  if (nrows >= 50 && lane == 0) {
+    int k = 0;
+    for (int i = 0; i < 6; ++i)
+      for (int jj = i; jj < 6; ++jj) {
+        sh.AtA[i * 6 + jj] = (float)tot[k];
+        sh.AtA[jj * 6 + i] = (float)tot[k];
+        ++k;
+      }
+    for (int i = 0; i < 6; ++i) sh.AtB[i] = (float)tot[21 + i];
+  }
+  const bool solve = nrows >= 50;  // (uniform)
+  bool eig = solve && iter == 0, cert = false;
+  int degen = S.degen;
+  if (solve) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (eig) {
+      cert = loamla::nondegenerate_certified(sh.AtA, 100.0f);
+      eig = !cert;
+      if (eig) loamla::jacobi6_wave(sh.AtA, sh.jE, sh.jV);
+    }
+    loamla::lm_step_wave(sh.AtA, sh.AtB, iter, 100.0f, &degen, S.matP, sh.X, sh.lm_ws, sh.lm_iws,
+                         eig ? sh.jE : nullptr, eig ? sh.jV : nullptr, cert);
+  }
+  if (lane != 0) return;
+  S.iters = iter + 1;
+  S.rows += nrows;
+  if (solve) {
+    S.degen = degen;
+    if (degen) ++S.deg_steps;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) S.T[q] = S.T[q] + sh.X[q];
+    const float dR = loamla::delta_r(sh.X), dT = loamla::delta_t(sh.X);
+    if (D(dR) < 0.05 && D(dT) < 0.05) S.stop = 1;
+  }
+  if (iter + 1 >= max_iter) S.stop = 1;
+}
+
+__global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_stream(MpBuffers b) {
+  const int g = blockIdx.x, G = gridDim.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6, p = 0;
+  int* ist = b.istate;
+  float* st = b.state;
+  if (!ist[kMiLmRan] || ist[kMiStop]) return;  // (the same value in every workgroup)
+  __shared__ uint32_t lists[27 * kMpQueryThreads];
+  __shared__ float jac[kMpQueryThreads][27];
+  __shared__ double red[kMpQueryThreads / 64][28], slice[8][28], tot[28];
+  __shared__ MpStepScratch sh;
+  __shared__ MpLsState S;
+  __shared__ unsigned long long sh_epoch;
+  if (tid < 6) S.T[tid] = st[kMpTobe + tid];
+  if (tid < 36) S.matP[tid] = st[kMpMatP + tid];
+  if (tid == 0) {
+    S.degen = ist[kMiDegen];
+    S.iters = ist[kMiIters];
+    S.rows = ist[kMiRows];
+    S.deg_steps = ist[kMiDegSteps];
+    S.stop = 0;
+    sh_epoch = b.ls_epoch[0];
+  }
+  __syncthreads();
+  const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
+  const int nq = nsc + nss;
+  const float4* stack = b.stack;
+  int8_t* qok = b.q_ok;
+  float4* qcf = b.q_cf;
+  const MpNnCtx c = mp_nn_ctx(b, p);
+  constexpr int L = kMpNnLanes, QPB = kMpQueryThreads / L;
+  const int sub = tid % L;
+  const unsigned long long tag0 = sh_epoch << 8;
+  int nfits = 0;
+  for (int it = 0; it < b.max_iter; ++it) {
+    const bool first = S.iters == 0;
+    const loampose::MapRot r = loampose::map_rot(S.T);  // (rot_store's values: the same dsin / dcos)
+    const MpTrig tg = mp_trig_of(r);
+    int work = 0;
+    double acc[28];
+#pragma unroll
+    for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+    for (int q = g * QPB + tid / L; q < nq; q += G * QPB) {
+      float4 sel;
+      Top5 t;
+      mp_nn_query<kMpQueryThreads, L>(b, c, q, nsc, first, r, lists + tid, sel, t, work, sub);
+      float4 cf = make_float4(0, 0, 0, 0);
+      int ok = 0;
+      if (sub == 0) {
+        mp_fit_query(b, p, q, nsc, first, make_int4(t.i[0], t.i[1], t.i[2], t.i[3]),
+                     make_int4(t.i[4], __float_as_int(t.d[4]), 0, 0), sel, jac[tid], nfits, cf, ok);
+        qok[q] = (int8_t)ok;
+        qcf[q] = cf;
+        if (ok) mp_row_accum(tg, stack[q < nsc ? q : b.capC + (q - nsc)], cf, acc);
+      }
+    }
+    wave_reduce_scatter_28(acc);
+    if ((lane & 1) == 0 && (lane >> 1) < 28) red[w][lane >> 1] = acc[0];
+    __syncthreads();
+    const int par = it & 1;
+    if (tid < 28) {  // this workgroup's partial, waves in order, stored write-through
+      double v = red[0][tid];
+      for (int ww = 1; ww < kMpQueryThreads / 64; ++ww) v += red[ww][tid];
+      store_partial(&b.ls_part[((size_t)par * kMpSmallGrid + g) * 28 + tid], v);
+    }
+    if (tid < 64) {
+      __builtin_amdgcn_wave_barrier();  // (every lane's store drained: store_partial waits for it)
+      if (tid == 0)
+        __hip_atomic_store(&b.ls_flag[g], tag0 + (unsigned long long)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid < G) {  // every workgroup's partial of this iteration
+      const unsigned long long want = tag0 + (unsigned long long)(it + 1);
+      while (__hip_atomic_load(&b.ls_flag[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want)
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();
+    if (tid < 8 * 28) {  // fixed order: slice s sums partials s, s + 8, ...; the slices in order
+      const int v = tid % 28, sl = tid / 28;
+      const double* pp = b.ls_part + (size_t)par * kMpSmallGrid * 28 + v;
+      double t8[kMpSmallGrid / 8];
+#pragma unroll
+      for (int u = 0; u < kMpSmallGrid / 8; ++u) {
+        const int gg = sl + 8 * u;
+        t8[u] = gg < G ? __hip_atomic_load(&pp[(size_t)gg * 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+      }
+      double a1 = 0.0;
+#pragma unroll
+      for (int u = 0; u < kMpSmallGrid / 8; ++u)
+        if (sl + 8 * u < G) a1 += t8[u];
+      slice[sl][v] = a1;
+    }
+    __syncthreads();
+    if (tid < 28) {
+      double v = slice[0][tid];
+#pragma unroll
+      for (int sl = 1; sl < 8; ++sl) v += slice[sl][tid];
+      tot[tid] = v;
+    }
+    __syncthreads();
+    if (tid < 64) mp_step_ls(b.max_iter, tot, S, sh);
+    __syncthreads();
+    if (S.stop) break;
+  }
+  nfits = wave_sum(nfits);
+  if (lane == 0 && nfits) atomicAdd(&ist[kMiFits], nfits);
+  if (g == 0) {  // the state for the kernels after the loop (the same in every workgroup)
+    if (tid < 6) st[kMpTobe + tid] = S.T[tid];
+    if (tid < 36) st[kMpMatP + tid] = S.matP[tid];
+    if (tid == 0) {
+      rot_store(b, p, S.T);
+      ist[kMiDegen] = S.degen;
+      ist[kMiIters] = S.iters;
+      ist[kMiRows] = S.rows;
+      ist[kMiDegSteps] = S.deg_steps;
+      ist[kMiStop] = S.stop;
+    }
+  }
+}
+
+// workgroups of k_mp_lm_stream (kMpSmallGrid, as k_mp_lm_small), or 0 when they could not all be
+// resident at once (the per-iteration launches run instead)
+int mp_lm_stream_grid() {
+  static int cap[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cap[dev] == 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_mp_lm_stream, kMpQueryThreads, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      per_cu = cus = 0;
+    cap[dev] = std::max(1, per_cu * cus);
+  }
+  // (a margin of 2: other streams' kernels may hold slots a while; half the grid loops twice)
+  return 2 * kMpSmallGrid <= cap[dev] ? kMpSmallGrid : (kMpSmallGrid <= cap[dev] ? kMpSmallGrid / 2 : 0);
+}
+
 // transformUpdate (:199-232) for the instances whose L-M ran; the IMU blend (:224-225) when the
 // host found IMU data for the odometry stamp
 __global__ void k_mp_lm_end(MpBuffers b) {
@@ -2479,8 +2670,13 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
   A(&b.part, (size_t)P * std::max(kMpSmallGrid, kMpFitGridMax) * 28 * sizeof(double));
   A(&b.rot, (size_t)P * 6 * sizeof(double));
   A(&b.done, (size_t)P * sizeof(int));
+  A(&b.ls_part, (size_t)2 * kMpSmallGrid * 28 * sizeof(double));
+  A(&b.ls_flag, (size_t)kMpSmallGrid * sizeof(unsigned long long));
+  A(&b.ls_epoch, sizeof(unsigned long long));
   A(&b.nreg, (size_t)P * sizeof(int));
   if (A.err == hipSuccess) A.err = mp_reset(b, nullptr);
+  if (A.err == hipSuccess) A.err = hipMemset(b.ls_flag, 0, (size_t)kMpSmallGrid * sizeof(unsigned long long));
+  if (A.err == hipSuccess) A.err = hipMemset(b.ls_epoch, 0, sizeof(unsigned long long));
   if (A.err == hipSuccess) A.err = hipDeviceSynchronize();
   if (A.err != hipSuccess) mp_free(b);
   return A.err;
@@ -2492,7 +2688,7 @@ void mp_free(MpBuffers& b) {
                   b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.citems, b.nitems, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
                   b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_l0, b.vg_l1, b.vg_lin, b.vg_cnt, b.reg, b.nreg, b.part, b.done, b.rot,
-                  b.vg_mlist, b.vseg_nold, b.vseg_skip};
+                  b.vg_mlist, b.vseg_nold, b.vseg_skip, b.ls_part, b.ls_flag, b.ls_epoch};
   if (b.upd_pending && b.upd_done) (void)hipEventSynchronize(b.upd_done);
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
@@ -2580,7 +2776,13 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
   // batches about one pass over a VLP-16 stack (bigger stacks loop), fewer idle workgroups
   const int gq = std::min(P >= 64 ? 24 : 64, (b.cap_stack + kMpQueryThreads - 1) / kMpQueryThreads);
   // an empty map store (the first frame after a reset) cannot run the L-M (:706): no launches
-  for (int it = 0; it < (map_empty ? 0 : b.max_iter); ++it) {
+  // one instance (streaming): the whole L-M loop as one persistent launch (tuning mp_persist)
+  const int gls = P == 1 && !map_empty && b.tune.mp_persist ? mp_lm_stream_grid() : 0;
+  if (gls > 0) {
+    hipLaunchKernelGGL(k_mp_lm_stream, dim3(gls), dim3(kMpQueryThreads), 0, st, b);
+    mark("k_mp_lm_stream");
+  }
+  for (int it = 0; it < (map_empty || gls > 0 ? 0 : b.max_iter); ++it) {
     if (P <= b.tune.mp_small_max) {  // small batches: one launch per iteration
       hipLaunchKernelGGL(k_mp_lm_small, dim3(kMpSmallGrid, P), dim3(kMpQueryThreads), 0, st, b);
       mark("k_mp_lm_small");

@@ -49,12 +49,15 @@ def test_config3_full220_device_chain(loam, sg):
     check_config3_full(traj)
 
 
-@pytest.mark.parametrize("tune", [{"vg_merge": 0}, {"od_win_mono_min": 1}, {"od_persist": 0}, {"od_graph": 0}],
-                         ids=["no_vg_merge", "win_mono", "per_iteration_launches", "no_graph"])
+@pytest.mark.parametrize("tune", [{"vg_merge": 0}, {"od_win_mono_min": 1}, {"od_persist": 0}, {"mp_persist": 0},
+                                  {"od_graph": 0}],
+                         ids=["no_vg_merge", "win_mono", "od_per_iteration", "mp_per_iteration", "no_graph"])
 def test_config3_full220_tuned(loam, sg, tune):
     """the 220 sweeps through loam_chain_sweep with a non-default launch choice: the cascade instead of
     the incremental cube VoxelGrid (k_vg_merge, the default, takes the growing map's big cubes); the
-    association's index-range ring windows (batch default) on the streaming path.  Every pose and
+    association's index-range ring windows (batch default) on the streaming path; the odometry's /
+    mapping's L-M as a launch per iteration instead of one persistent launch (k_od_lm_stream /
+    k_mp_lm_stream, the defaults); no graph replay of the odometry launches.  Every pose and
     registered cloud as the golden run"""
     e = loam.Engine(loam.default_config())
     e.set_tuning(**tune)
