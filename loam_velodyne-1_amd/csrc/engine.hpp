@@ -97,8 +97,9 @@ struct Tuning {
                            // map update).  Not the message calls: their host staging waits on the second
                            // stream, and a node graph's contexts share the process's hardware queues (the
                            // three-context pipeline measured 0.45-0.51 -> 0.77-1.13 ms/sweep with it)
-  int nn_cert = 4;         // batches: k_mp_nnfit_cert (the 5-NN certificate) with this many 64-query
-                           // chunks per wave (0: k_mp_nnfit, every query searched every iteration)
+  int nn_cert = 0;         // batches: the 5-NN certificate: 0 off (every query searched every iteration),
+                           // 1 in place (k_mp_nnfit<CERT>: a certified lane skips its search), K >= 2
+                           // with the uncertified queries of K 64-query chunks compacted (k_mp_nnfit_cert)
   int od_persist = 1;      // one problem (streaming): the odometry L-M loop as one persistent launch
                            // (k_od_lm_stream) instead of a launch per iteration and association round
   int mp_persist = 1;      // one instance (streaming): the mapping L-M loop as one persistent launch

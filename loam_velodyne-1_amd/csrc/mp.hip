@@ -1650,7 +1650,9 @@ __global__ __launch_bounds__(kMpFitThreads) void k_mp_fit(MpBuffers b) {
 #ifndef LOAM_NNFIT_WPE
 #define LOAM_NNFIT_WPE 4
 #endif
-template <bool FUSED, bool COUNT>
+// CERT: the 5-NN certificate in place (tuning nn_cert = 1; see k_mp_nnfit_cert): a certified lane
+// skips its search, the wave's other lanes search as before (no compaction)
+template <bool FUSED, bool COUNT, bool CERT = false>
 __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(LOAM_NNFIT_WPE))) void k_mp_nnfit(MpBuffers b) {
   constexpr int NT = kMpFitThreads;
   static_assert(NT == 64, "the list / scratch sharing needs one wave per workgroup");
@@ -1694,6 +1696,8 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(L
   // one record per query (MpFit in q_fit): the 5-NN of the last iteration (i0..i3 | i4, 0,
   // distinct, fit valid) and the fit made for them — the seeds and the reuse test in one read
   MpFit* qrec = (MpFit*)b.q_fit + (size_t)p * b.cap_stack;
+  float4* qcert = b.q_cert + (size_t)p * b.cap_stack;
+  int ncert = 0;
   for (int q0 = blk.x * NT; q0 < nq; q0 += gridDim.x * NT) {  // (wave-uniform trip count)
     const int q = q0 + tid;
     const bool corner = q < nsc;
@@ -1705,9 +1709,52 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(L
       o = c.stack[corner ? q : b.capC + (q - nsc)];
       if (!first) { r0 = qrec[q].n0; r1 = qrec[q].n1; }
       sel = loampose::point_to_map(r, o);
-      mp_nn_seed_from(c, q, corner, first, r0, r1, sel, t, work);
-      if (corner) knn5_flat<NT, 1, kNnListCap>(c.hcs, c.hcr, c.hcp, c.TC, sel, t, lds + tid, work, 0);
-      else knn5_flat<NT, 1, kNnListCap>(c.hss, c.hsr, c.hsp, c.TS, sel, t, lds + tid, work, 0);
+      if constexpr (CERT) {
+        bool cert = false;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { t.d[k] = 3.4e38f; t.i[k] = 0x7fffffff; }
+        if (!first && r1.z) {  // the seeds (mp_nn_seed_from) and the certificate test (k_mp_nnfit_cert)
+          const int prev[5] = {r0.x, r0.y, r0.z, r0.w, r1.x};
+          const float4* from = corner ? c.fromC : c.fromS;
+          const float4 cc = qcert[q];
+          float dk[5];
+          uint64_t B = 0;
+#pragma unroll
+          for (int k = 0; k < 5; ++k) {
+            const float4 a = from[prev[k]];
+            dk[k] = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
+            const uint64_t key = top5_key(dk[k], prev[k]);
+            B = key > B ? key : B;
+          }
+          work += 5;
+          if (cc.w > 0.0f) {
+            const float ex = sel.x - cc.x, ey = sel.y - cc.y, ez = sel.z - cc.z;
+            const float delta = sqrtf(ex * ex + ey * ey + ez * ez);
+            const float far = sqrtf(__uint_as_float((uint32_t)(B >> 32)));
+            cert = far * 1.00001f + 2e-5f < 1.0f && far * 1.00001f + delta * 1.00001f + 2e-5f < cc.w * 0.99999f;
+          }
+          if (cert) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) top5_offer_new(t, dk[k], prev[k]);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) { t.d[k] = __uint_as_float((uint32_t)(B >> 32)); t.i[k] = (int)(uint32_t)B; }
+          }
+        }
+        ncert += cert ? 1 : 0;
+        if (!cert) {
+          float lb = 0.0f;
+          if (corner) knn5_flat<NT, 1, kNnListCap, true>(c.hcs, c.hcr, c.hcp, c.TC, sel, t, lds + tid, work, 0, &lb);
+          else knn5_flat<NT, 1, kNnListCap, true>(c.hss, c.hsr, c.hsp, c.TS, sel, t, lds + tid, work, 0, &lb);
+          qcert[q] = top5_distinct(t) && lb > 0.0f
+                         ? make_float4(sel.x, sel.y, sel.z, (float)(sqrt((double)lb) * (1.0 - 1e-6)))
+                         : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+      } else {
+        mp_nn_seed_from(c, q, corner, first, r0, r1, sel, t, work);
+        if (corner) knn5_flat<NT, 1, kNnListCap>(c.hcs, c.hcr, c.hcp, c.TC, sel, t, lds + tid, work, 0);
+        else knn5_flat<NT, 1, kNnListCap>(c.hss, c.hsr, c.hsp, c.TS, sel, t, lds + tid, work, 0);
+      }
 #ifdef LOAM_DIAG_SEARCH2  // (diagnostic build: the search twice, its cost measured by the difference)
       {
         Top5 t2;
@@ -1809,6 +1856,10 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(L
     if (lane_id() == 0 && ncand) {
       atomicAdd(&ist[kMiNnCand], ncand);
       atomicAdd(&ist[kMiNnCells], ncell);
+    }
+    if constexpr (CERT) {
+      ncert = wave_sum(ncert);
+      if (lane_id() == 0 && ncert) atomicAdd(&ist[kMiNnCert], ncert);
     }
   }
   if constexpr (FUSED) mp_store_partial_and_step(b, p, blk.x, (int)gridDim.x, red);
@@ -3049,8 +3100,13 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     // through k_mp_nn<L> measured slower at P = 128: 3.15 -> 3.22 / 3.29 ms/step)
     if (P <= b.tune.nnfit_max && gfit <= kMpFitGridMax) {  // search + fit (+ step) in one launch
       const bool fused = P <= b.tune.mp_fused_max;
-      const int K = std::min(b.tune.nn_cert, kMpCertMaxK);  // (0: no certificate)
-      if (K > 0) {  // chunks of K x 64 queries per wave
+      const int K = b.tune.nn_cert;  // (0: no certificate, 1: in place, >= 2: compacted)
+      if (K == 1) {
+        if (fused && prof) hipLaunchKernelGGL((k_mp_nnfit<true, true, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+        else if (fused) hipLaunchKernelGGL((k_mp_nnfit<true, false, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+        else if (prof) hipLaunchKernelGGL((k_mp_nnfit<false, true, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+        else hipLaunchKernelGGL((k_mp_nnfit<false, false, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+      } else if (K > 1) {  // chunks of K x 64 queries per wave
         const int gc = (gfit + K - 1) / K;
         if (fused && prof) hipLaunchKernelGGL((k_mp_nnfit_cert<true, true>), dim3(gc, P), dim3(kMpFitThreads), 0, st, b, K);
         else if (fused) hipLaunchKernelGGL((k_mp_nnfit_cert<true, false>), dim3(gc, P), dim3(kMpFitThreads), 0, st, b, K);
