@@ -89,7 +89,7 @@ STAT_U64 = ("n_raw", "n_ring", "n_sharp", "n_less_sharp", "n_flat", "n_less_flat
 
 
 STAT_BRANCH = ("od_degenerate_steps", "od_nan_skips", "mp_degenerate_steps", "mp_grid_shifts")
-STAT_WORK = ("mp_nn_candidates", "mp_nn_cells", "od_assoc_gathered", "od_assoc_boxes", "mp_nn_certified")
+STAT_WORK = ("mp_nn_candidates", "mp_nn_cells", "od_assoc_gathered", "od_assoc_boxes")
 
 
 class ChainOut(ctypes.Structure):

@@ -97,9 +97,6 @@ struct Tuning {
                            // map update).  Not the message calls: their host staging waits on the second
                            // stream, and a node graph's contexts share the process's hardware queues (the
                            // three-context pipeline measured 0.45-0.51 -> 0.77-1.13 ms/sweep with it)
-  int nn_cert = 0;         // batches: the 5-NN certificate: 0 off (every query searched every iteration),
-                           // 1 in place (k_mp_nnfit<CERT>: a certified lane skips its search), K >= 2
-                           // with the uncertified queries of K 64-query chunks compacted (k_mp_nnfit_cert)
   int od_persist = 1;      // one problem (streaming): the odometry L-M loop as one persistent launch
                            // (k_od_lm_stream) instead of a launch per iteration and association round
   int mp_persist = 1;      // one instance (streaming): the mapping L-M loop as one persistent launch
@@ -129,7 +126,7 @@ struct Tuning {
                     {"step_pipe", &step_pipe, 0, 1 << 20}, {"batch_streams", &batch_streams, 0, 1},
                     {"pipe_mp_sets", &pipe_mp_sets, 1, 2}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
                     {"od_win_mono", &od_win_mono, 0, 3}, {"od_win_mono_min", &od_win_mono_min, 1, 1 << 20},
-                    {"od_moments_min", &od_moments_min, 1, 1 << 30}, {"od_persist", &od_persist, 0, 1}, {"nn_cert", &nn_cert, 0, 4},
+                    {"od_moments_min", &od_moments_min, 1, 1 << 30}, {"od_persist", &od_persist, 0, 1},
                     {"mp_persist", &mp_persist, 0, 1}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {

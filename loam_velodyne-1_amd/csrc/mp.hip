@@ -1006,15 +1006,9 @@ constexpr int kNnRangeGroup = LOAM_NN_RANGE_GROUP;
 // L > 1: one of L lanes searching the same query: every lane lists the same cells, lane `sub`
 // takes the candidates sub, sub + L, ... of the concatenated list (a crowded cell is shared too);
 // the caller merges the L partial top-5 lists (knn5_merge)
-// RU (one lane per query): *lb receives a lower bound of the squared distance from q of every map
-// point the final list does not hold — the smallest candidate key that was rejected or evicted
-// (the "runner-up"), the box distance of every cell skipped by the seeded bound, and 1 (the points
-// outside the 27 cells, and those of cells skipped at >= 1 m); 0 when the unlisted search ran (no
-// bound kept).  The 5-NN certificate of k_mp_nnfit_cert is made from it.
-template <int S = kMpQueryThreads, int L = 1, int CAPL = 27, bool RU = false>
+template <int S = kMpQueryThreads, int L = 1, int CAPL = 27>
 LOAM_D void knn5_flat(const int* start, const uint32_t* rec, const float4* hp, int T, float4 q, Top5& t,
-                      uint32_t* lst, int& work, int sub = 0, float* lb = nullptr) {
-  if (RU) *lb = 0.0f;
+                      uint32_t* lst, int& work, int sub = 0) {
   if (T <= 0) return;
   const int cx = cell_of(q.x, 1.0f), cy = cell_of(q.y, 1.0f), cz = cell_of(q.z, 1.0f);
   const float gxl = q.x - (float)cx, gyl = q.y - (float)cy, gzl = q.z - (float)cz;
@@ -1022,7 +1016,6 @@ LOAM_D void knn5_flat(const int* start, const uint32_t* rec, const float4* hp, i
   const float bound = t.d[4];
   int n = 0, total = 0;
   bool fits = true;
-  float skip_lb = 1.0f;  // (RU) the cells skipped by the bound, and 1
   // the range loads of a group of cells are all issued before any is used (a load whose count is
   // tested in the same block is waited for at once: one dependent round trip per cell)
 #pragma unroll
@@ -1042,8 +1035,6 @@ LOAM_D void knn5_flat(const int* start, const uint32_t* rec, const float4* hp, i
       if (bd < 1.0f && bd <= bound) {
         const uint32_t h = cell_hash(cx + dx, cy + dy, cz + dz) & (uint32_t)(T - 1);
         rg[u] = rec[h];  // the bucket's range packed in one word (hash_rec)
-      } else if (RU) {
-        skip_lb = fminf(skip_lb, bd);
       }
     }
 #pragma unroll
@@ -1067,7 +1058,6 @@ LOAM_D void knn5_flat(const int* start, const uint32_t* rec, const float4* hp, i
     return;
   }
   work += total + (n << kWorkCellShift);
-  uint64_t ru = ~0ull;  // (RU) the smallest rejected / evicted key
   // the list is walked one entry ahead: the LDS read of the next entry is issued when the current
   // one is taken, so its latency is not on the candidate chain
   int ci = 1, left = 0, pos = 0;
@@ -1113,29 +1103,8 @@ LOAM_D void knn5_flat(const int* start, const uint32_t* rec, const float4* hp, i
     for (int u = 0; u < kNnInFlight; ++u) a[u] = hp[idx[u]];
 #pragma unroll
     for (int u = 0; u < kNnInFlight; ++u)
-      if (k + u < mine) {
-        const float d = sqdist(a[u].x, a[u].y, a[u].z, q.x, q.y, q.z);
-        const int idx = __builtin_bit_cast(int, a[u].w);
-        if constexpr (RU) {
-          // a key below K_4 evicts K_4 (unless a copy of it stays held: the seeded list starts as
-          // five copies of the bound B, adjacent in the sorted list); a key above it is rejected; a
-          // key equal to it is the held point itself (B, met again by the walk)
-          const uint64_t key = top5_key(d, idx);
-          uint64_t K[5];
-#pragma unroll
-          for (int kk = 0; kk < 5; ++kk) K[kk] = top5_key(t.d[kk], t.i[kk]);
-          if (key < K[4]) {
-            if (K[4] != K[3]) ru = K[4] < ru ? K[4] : ru;
-            top5_insert(t, K, key);
-          } else if (key != K[4]) {
-            ru = key < ru ? key : ru;
-          }
-        } else {
-          top5_offer_new(t, d, idx);
-        }
-      }
+      if (k + u < mine) top5_offer_new(t, sqdist(a[u].x, a[u].y, a[u].z, q.x, q.y, q.z), __builtin_bit_cast(int, a[u].w));
   }
-  if constexpr (RU) *lb = ru == ~0ull ? skip_lb : fminf(__uint_as_float((uint32_t)(ru >> 32)), skip_lb);
 }
 
 // the L lanes of a query group (aligned, consecutive) exchange their top-5 lists in log2(L)
@@ -1179,7 +1148,6 @@ __global__ void k_mp_lm_begin(MpBuffers b) {
   ist[kMiDegSteps] = 0;
   ist[kMiNnCand] = 0;
   ist[kMiNnCells] = 0;
-  ist[kMiNnCert] = 0;
   if (p == 0 && b.P == 1) ++b.ls_epoch[0];  // (k_mp_lm_stream's publication words)
 }
 
@@ -1650,9 +1618,7 @@ __global__ __launch_bounds__(kMpFitThreads) void k_mp_fit(MpBuffers b) {
 #ifndef LOAM_NNFIT_WPE
 #define LOAM_NNFIT_WPE 4
 #endif
-// CERT: the 5-NN certificate in place (tuning nn_cert = 1; see k_mp_nnfit_cert): a certified lane
-// skips its search, the wave's other lanes search as before (no compaction)
-template <bool FUSED, bool COUNT, bool CERT = false>
+template <bool FUSED, bool COUNT>
 __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(LOAM_NNFIT_WPE))) void k_mp_nnfit(MpBuffers b) {
   constexpr int NT = kMpFitThreads;
   static_assert(NT == 64, "the list / scratch sharing needs one wave per workgroup");
@@ -1696,8 +1662,6 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(L
   // one record per query (MpFit in q_fit): the 5-NN of the last iteration (i0..i3 | i4, 0,
   // distinct, fit valid) and the fit made for them — the seeds and the reuse test in one read
   MpFit* qrec = (MpFit*)b.q_fit + (size_t)p * b.cap_stack;
-  float4* qcert = b.q_cert + (size_t)p * b.cap_stack;
-  int ncert = 0;
   for (int q0 = blk.x * NT; q0 < nq; q0 += gridDim.x * NT) {  // (wave-uniform trip count)
     const int q = q0 + tid;
     const bool corner = q < nsc;
@@ -1709,52 +1673,9 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(L
       o = c.stack[corner ? q : b.capC + (q - nsc)];
       if (!first) { r0 = qrec[q].n0; r1 = qrec[q].n1; }
       sel = loampose::point_to_map(r, o);
-      if constexpr (CERT) {
-        bool cert = false;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) { t.d[k] = 3.4e38f; t.i[k] = 0x7fffffff; }
-        if (!first && r1.z) {  // the seeds (mp_nn_seed_from) and the certificate test (k_mp_nnfit_cert)
-          const int prev[5] = {r0.x, r0.y, r0.z, r0.w, r1.x};
-          const float4* from = corner ? c.fromC : c.fromS;
-          const float4 cc = qcert[q];
-          float dk[5];
-          uint64_t B = 0;
-#pragma unroll
-          for (int k = 0; k < 5; ++k) {
-            const float4 a = from[prev[k]];
-            dk[k] = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
-            const uint64_t key = top5_key(dk[k], prev[k]);
-            B = key > B ? key : B;
-          }
-          work += 5;
-          if (cc.w > 0.0f) {
-            const float ex = sel.x - cc.x, ey = sel.y - cc.y, ez = sel.z - cc.z;
-            const float delta = sqrtf(ex * ex + ey * ey + ez * ez);
-            const float far = sqrtf(__uint_as_float((uint32_t)(B >> 32)));
-            cert = far * 1.00001f + 2e-5f < 1.0f && far * 1.00001f + delta * 1.00001f + 2e-5f < cc.w * 0.99999f;
-          }
-          if (cert) {
-#pragma unroll
-            for (int k = 0; k < 5; ++k) top5_offer_new(t, dk[k], prev[k]);
-          } else {
-#pragma unroll
-            for (int k = 0; k < 5; ++k) { t.d[k] = __uint_as_float((uint32_t)(B >> 32)); t.i[k] = (int)(uint32_t)B; }
-          }
-        }
-        ncert += cert ? 1 : 0;
-        if (!cert) {
-          float lb = 0.0f;
-          if (corner) knn5_flat<NT, 1, kNnListCap, true>(c.hcs, c.hcr, c.hcp, c.TC, sel, t, lds + tid, work, 0, &lb);
-          else knn5_flat<NT, 1, kNnListCap, true>(c.hss, c.hsr, c.hsp, c.TS, sel, t, lds + tid, work, 0, &lb);
-          qcert[q] = top5_distinct(t) && lb > 0.0f
-                         ? make_float4(sel.x, sel.y, sel.z, (float)(sqrt((double)lb) * (1.0 - 1e-6)))
-                         : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        }
-      } else {
-        mp_nn_seed_from(c, q, corner, first, r0, r1, sel, t, work);
-        if (corner) knn5_flat<NT, 1, kNnListCap>(c.hcs, c.hcr, c.hcp, c.TC, sel, t, lds + tid, work, 0);
-        else knn5_flat<NT, 1, kNnListCap>(c.hss, c.hsr, c.hsp, c.TS, sel, t, lds + tid, work, 0);
-      }
+      mp_nn_seed_from(c, q, corner, first, r0, r1, sel, t, work);
+      if (corner) knn5_flat<NT, 1, kNnListCap>(c.hcs, c.hcr, c.hcp, c.TC, sel, t, lds + tid, work, 0);
+      else knn5_flat<NT, 1, kNnListCap>(c.hss, c.hsr, c.hsp, c.TS, sel, t, lds + tid, work, 0);
 #ifdef LOAM_DIAG_SEARCH2  // (diagnostic build: the search twice, its cost measured by the difference)
       {
         Top5 t2;
@@ -1856,233 +1777,6 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(L
     if (lane_id() == 0 && ncand) {
       atomicAdd(&ist[kMiNnCand], ncand);
       atomicAdd(&ist[kMiNnCells], ncell);
-    }
-    if constexpr (CERT) {
-      ncert = wave_sum(ncert);
-      if (lane_id() == 0 && ncert) atomicAdd(&ist[kMiNnCert], ncert);
-    }
-  }
-  if constexpr (FUSED) mp_store_partial_and_step(b, p, blk.x, (int)gridDim.x, red);
-}
-
-// k_mp_nnfit with the 5-NN certificate (tuning nn_cert = K chunks of 64 queries per wave).  A full
-// search keeps, with its list, a lower bound L of the squared distance from the query point of every
-// map point not in the list (knn5_flat<RU>: the runner-up key, the cells the bound skipped, 1 m) and
-// the query point c it searched from (q_cert).  At a later iteration the query point has moved to
-// sel, |sel - c| = delta: every member is now at its exact distance (the five seeds are gathered
-// anyway), every other point at >= sqrt(L) - delta.  When the farthest member still lies below
-// that, and below 1 m (inside the cells the search would take), the search would return exactly
-// the members in (distance, index) order: the list is made from the seeds without a search, and the
-// certificate stays with c.  Margins of 1e-5 relative + 2e-5 m cover the float rounding of every
-// distance involved.  The uncertified queries of the wave's K chunks are compacted into dense passes
-// (an LDS list in query order with their seed bounds), so a wave searches ceil(U / 64) times, not K.
-// Results are the search's; only the fp64 row sums' grouping follows the passes.
-constexpr int kMpCertMaxK = 4;
-template <bool FUSED, bool COUNT>
-__global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(LOAM_NNFIT_WPE))) void k_mp_nnfit_cert(MpBuffers b, int K) {
-  constexpr int NT = kMpFitThreads;
-  static_assert(NT == 64, "the list / scratch sharing needs one wave per workgroup");
-  const XcdBlock blk = xcd_block();
-  const int p = blk.y, lane = lane_id();
-  int* ist = b.istate + (size_t)p * kMpStateInts;
-  if (!ist[kMiLmRan] || ist[kMiStop]) return;
-  const bool first = ist[kMiIters] == 0;
-  __shared__ uint32_t lds[kNnListCap * NT];  // candidate lists (column lane, stride NT) / Jacobi rows / rows
-  __shared__ uint16_t qq[kMpCertMaxK * NT];   // the uncertified queries (offset from the chunk group's first)
-  __shared__ uint64_t qB[kMpCertMaxK * NT];   // ... and their seed bounds (~0: unseeded)
-  const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
-  const int nq = nsc + nss;
-  int8_t* qok = b.q_ok + (size_t)p * b.cap_stack;
-  float4* qcf = b.q_cf + (size_t)p * b.cap_stack;
-  float4* qcert = b.q_cert + (size_t)p * b.cap_stack;
-  const loampose::MapRot r = rot_load(b, p);
-  const MpNnCtx c = mp_nn_ctx(b, p);
-  const MpTrig tg = mp_trig_of(r);
-  float* jw = (float*)lds + lane * 27;
-  int nfits = 0, work = 0, ncert = 0;
-  double red = 0.0;
-  int term_x = -1, term_y = -1;  // FUSED: lane 2t's term t of the 28 sums (as k_mp_nnfit)
-  if (FUSED && (lane & 1) == 0 && (lane >> 1) < 28) {
-    const int t = lane >> 1;
-    if (t < 21) {
-      int i = 0, r0 = t;
-      while (r0 >= 6 - i) { r0 -= 6 - i; ++i; }
-      term_x = i;
-      term_y = i + r0;
-    } else if (t < 27) {
-      term_x = t - 21;
-      term_y = 6;
-    } else {
-      term_x = 7;
-      term_y = 7;
-    }
-  }
-  MpFit* qrec = (MpFit*)b.q_fit + (size_t)p * b.cap_stack;
-  auto wave_sync = []() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  };
-  // the fit (reused while the ordered 5-NN is unchanged), the residual, the record, and (FUSED) the
-  // pass's rows summed into red: k_mp_nnfit's tail; every lane calls it (act: the lane has a query)
-  auto finish = [&](int q, bool act, bool corner, float4 o, float4 sel, const Top5& t, int4 r0, int4 r1) {
-    bool row_ok = false;
-    float4 cf = make_float4(0, 0, 0, 0);
-    if (act) {
-      const int4 n0 = make_int4(t.i[0], t.i[1], t.i[2], t.i[3]);
-      bool valid = !first && r1.w && r0.x == n0.x && r0.y == n0.y && r0.z == n0.z && r0.w == n0.w && r1.x == t.i[4];
-      int ok = 0;
-      if (t.i[4] != 0x7fffffff && D(t.d[4]) < 1.0) {  // :719, :826
-        float4 g0, g1;
-        if (valid) {
-          g0 = qrec[q].g0;
-          g1 = qrec[q].g1;
-        } else {
-          ++nfits;
-          const float4* from = corner ? c.fromC : c.fromS;
-          float4 nb[5];
-#pragma unroll
-          for (int k = 0; k < 5; ++k) {
-            LOAM_CHECK(t.i[k] >= 0 && t.i[k] < (corner ? c.nfc : c.nfs), t.i[k], q);
-            nb[k] = from[t.i[k]];
-          }
-          mp_fit_compute(corner, nb, jw, g0, g1);
-          qrec[q].g0 = g0;
-          qrec[q].g1 = g1;
-          valid = true;
-        }
-        mp_fit_residual(corner, g0, g1, sel, cf, ok);
-      }
-      const int4 n1 = make_int4(t.i[4], 0, top5_distinct(t), valid ? 1 : 0);
-      if (first || r0.x != n0.x || r0.y != n0.y || r0.z != n0.z || r0.w != n0.w || r1.x != n1.x || r1.z != n1.z ||
-          r1.w != n1.w) {
-        qrec[q].n0 = n0;
-        qrec[q].n1 = n1;
-      }
-      if constexpr (!FUSED) {
-        qok[q] = (int8_t)ok;
-        qcf[q] = cf;
-      }
-      row_ok = ok != 0;
-    }
-    if constexpr (FUSED) {
-      float a6[6] = {0, 0, 0, 0, 0, 0}, bb = 0.0f;
-      if (row_ok) mp_row_jac(tg, o, cf, a6, bb);
-      wave_sync();  // the fits' scratch reads are done
-      float* rw = (float*)lds + lane * 8;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) rw[k] = a6[k];
-      rw[6] = bb;
-      rw[7] = row_ok ? 1.0f : 0.0f;
-      wave_sync();
-      if (term_x >= 0) {
-        const float* rows = (const float*)lds;
-        double sum = 0.0;
-#pragma unroll 16
-        for (int l = 0; l < NT; ++l) sum = loamla::dmac(sum, rows[l * 8 + term_x], rows[l * 8 + term_y]);
-        red += sum;
-      }
-    }
-    wave_sync();  // the scratch is free before the next lists
-  };
-  for (int qb = blk.x * K * NT; qb < nq; qb += gridDim.x * K * NT) {  // (wave-uniform trip counts)
-    int nU = 0;
-    // phase A: each chunk's queries mapped, their seeds gathered, the certificate tested; the
-    // certified finish at once, the others are listed
-    for (int ck = 0; ck < K; ++ck) {
-      const int q = qb + ck * NT + lane;
-      const bool act = q < nq, corner = q < nsc;
-      float4 o = make_float4(0, 0, 0, 0), sel = o;
-      int4 r0 = make_int4(-1, -1, -1, -1), r1 = make_int4(0, 0, 0, 0);
-      Top5 t;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) { t.d[k] = 3.4e38f; t.i[k] = 0x7fffffff; }
-      uint64_t B = ~0ull;
-      bool cert = false;
-      if (act) {
-        o = c.stack[corner ? q : b.capC + (q - nsc)];
-        if (!first) { r0 = qrec[q].n0; r1 = qrec[q].n1; }
-        sel = loampose::point_to_map(r, o);
-        if (!first && r1.z) {  // five distinct neighbours last iteration: the seeds (mp_nn_seed_from)
-          const int prev[5] = {r0.x, r0.y, r0.z, r0.w, r1.x};
-          const float4* from = corner ? c.fromC : c.fromS;
-          const float4 cc = qcert[q];
-          float dk[5];
-#pragma unroll
-          for (int k = 0; k < 5; ++k) {
-            LOAM_CHECK(prev[k] >= 0 && prev[k] < (corner ? c.nfc : c.nfs), prev[k], q);
-            const float4 a = from[prev[k]];
-            dk[k] = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
-            const uint64_t key = top5_key(dk[k], prev[k]);
-            B = key > B || B == ~0ull ? key : B;
-          }
-          work += 5;
-          if (cc.w > 0.0f) {
-            const float ex = sel.x - cc.x, ey = sel.y - cc.y, ez = sel.z - cc.z;
-            const float delta = sqrtf(ex * ex + ey * ey + ez * ez);
-            const float far = sqrtf(__uint_as_float((uint32_t)(B >> 32)));
-            const float reach = far * 1.00001f + delta * 1.00001f + 2e-5f;
-            cert = far * 1.00001f + 2e-5f < 1.0f && reach < cc.w * 0.99999f;
-          }
-          if (cert) {
-#pragma unroll
-            for (int k = 0; k < 5; ++k) top5_offer_new(t, dk[k], prev[k]);
-          }
-        }
-      }
-      const bool listed = act && !cert;
-      const uint64_t m = __ballot(listed);
-      if (listed) {
-        const int pos = nU + __popcll(m & lanemask_lt());
-        qq[pos] = (uint16_t)(q - qb);
-        qB[pos] = B;
-      }
-      nU += __popcll(m);
-      ncert += cert ? 1 : 0;
-      finish(q, cert, corner, o, sel, t, r0, r1);
-    }
-    // phase B: the listed queries searched in dense passes (query order), each keeping its certificate
-    for (int pb = 0; pb < nU; pb += NT) {
-      const int i = pb + lane;
-      const bool act = i < nU;
-      const int q = act ? qb + (int)qq[i] : 0;
-      const bool corner = q < nsc;
-      float4 o = make_float4(0, 0, 0, 0), sel = o;
-      int4 r0 = make_int4(-1, -1, -1, -1), r1 = make_int4(0, 0, 0, 0);
-      Top5 t;
-      float lb = 0.0f;
-      if (act) {
-        const uint64_t B = qB[i];
-        const float bd = B == ~0ull ? 3.4e38f : __uint_as_float((uint32_t)(B >> 32));
-        const int bi = B == ~0ull ? 0x7fffffff : (int)(uint32_t)B;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) { t.d[k] = bd; t.i[k] = bi; }
-        o = c.stack[corner ? q : b.capC + (q - nsc)];
-        if (!first) { r0 = qrec[q].n0; r1 = qrec[q].n1; }
-        sel = loampose::point_to_map(r, o);
-        if (corner) knn5_flat<NT, 1, kNnListCap, true>(c.hcs, c.hcr, c.hcp, c.TC, sel, t, lds + lane, work, 0, &lb);
-        else knn5_flat<NT, 1, kNnListCap, true>(c.hss, c.hsr, c.hsp, c.TS, sel, t, lds + lane, work, 0, &lb);
-        LOAM_CHECK(q < b.cap_stack && (t.i[4] == 0x7fffffff || t.i[4] < (corner ? c.nfc : c.nfs)), q, t.i[4]);
-        // (a list of five distinct points keeps a certificate; sqrt rounded down)
-        qcert[q] = top5_distinct(t) && lb > 0.0f
-                       ? make_float4(sel.x, sel.y, sel.z, (float)(sqrt((double)lb) * (1.0 - 1e-6)))
-                       : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      }
-      wave_sync();  // every lane's list reads are done before the scratch reuse
-      finish(q, act, corner, o, sel, t, r0, r1);
-    }
-  }
-  nfits = wave_sum(nfits);
-  if (lane == 0 && nfits) atomicAdd(&ist[kMiFits], nfits);
-  if (COUNT) {
-    const int ncand = wave_sum(work & ((1 << kWorkCellShift) - 1)), ncell = wave_sum(work >> kWorkCellShift);
-    ncert = wave_sum(ncert);
-    if (lane == 0) {
-      if (ncand) {
-        atomicAdd(&ist[kMiNnCand], ncand);
-        atomicAdd(&ist[kMiNnCells], ncell);
-      }
-      if (ncert) atomicAdd(&ist[kMiNnCert], ncert);
     }
   }
   if constexpr (FUSED) mp_store_partial_and_step(b, p, blk.x, (int)gridDim.x, red);
@@ -2947,7 +2641,6 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
   A(&b.citems, (size_t)P * 2 * kCubeNum * sizeof(int));
   A(&b.nitems, (size_t)P * sizeof(int));
   A(&b.q_fit, Ps * 4 * sizeof(float4));
-  A(&b.q_cert, Ps * sizeof(float4));
   A(&b.app_cnt, (size_t)P * kCubeNum * 2 * sizeof(int));
   A(&b.app_off, (size_t)P * kCubeNum * 2 * sizeof(int));
   A(&b.app, Ps * sizeof(float4));
@@ -2992,7 +2685,7 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
 void mp_free(MpBuffers& b) {
   void* ptrs[] = {b.state, b.istate, b.slots, b.pool, b.valid, b.vpre, b.inC, b.inS, b.inF, b.in_n, b.in_pose,
                   b.stack2, b.stack, b.nstack, b.from, b.hC_start, b.hS_start, b.hC_rec, b.hS_rec, b.h_fill, b.hC_T, b.hS_T,
-                  b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.q_cert, b.citems, b.nitems, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
+                  b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.citems, b.nitems, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
                   b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_l0, b.vg_l1, b.vg_lin, b.vg_cnt, b.reg, b.nreg, b.part, b.done, b.rot,
                   b.vg_mlist, b.vseg_nold, b.vseg_skip, b.ls_part, b.ls_flag, b.ls_epoch};
@@ -3100,19 +2793,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     // through k_mp_nn<L> measured slower at P = 128: 3.15 -> 3.22 / 3.29 ms/step)
     if (P <= b.tune.nnfit_max && gfit <= kMpFitGridMax) {  // search + fit (+ step) in one launch
       const bool fused = P <= b.tune.mp_fused_max;
-      const int K = b.tune.nn_cert;  // (0: no certificate, 1: in place, >= 2: compacted)
-      if (K == 1) {
-        if (fused && prof) hipLaunchKernelGGL((k_mp_nnfit<true, true, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
-        else if (fused) hipLaunchKernelGGL((k_mp_nnfit<true, false, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
-        else if (prof) hipLaunchKernelGGL((k_mp_nnfit<false, true, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
-        else hipLaunchKernelGGL((k_mp_nnfit<false, false, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
-      } else if (K > 1) {  // chunks of K x 64 queries per wave
-        const int gc = (gfit + K - 1) / K;
-        if (fused && prof) hipLaunchKernelGGL((k_mp_nnfit_cert<true, true>), dim3(gc, P), dim3(kMpFitThreads), 0, st, b, K);
-        else if (fused) hipLaunchKernelGGL((k_mp_nnfit_cert<true, false>), dim3(gc, P), dim3(kMpFitThreads), 0, st, b, K);
-        else if (prof) hipLaunchKernelGGL((k_mp_nnfit_cert<false, true>), dim3(gc, P), dim3(kMpFitThreads), 0, st, b, K);
-        else hipLaunchKernelGGL((k_mp_nnfit_cert<false, false>), dim3(gc, P), dim3(kMpFitThreads), 0, st, b, K);
-      } else if (fused && prof) hipLaunchKernelGGL((k_mp_nnfit<true, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+      if (fused && prof) hipLaunchKernelGGL((k_mp_nnfit<true, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
       else if (fused) hipLaunchKernelGGL((k_mp_nnfit<true, false>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
       else if (prof) hipLaunchKernelGGL((k_mp_nnfit<false, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
       else hipLaunchKernelGGL((k_mp_nnfit<false, false>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
@@ -3539,7 +3220,6 @@ int mp_batch_download(MpBuffers& b, hipStream_t st, loam_pose6* aft, loam_stats*
       stats->mp_grid_shifts += (uint64_t)q[kMiShifts];
       stats->mp_nn_candidates += (uint64_t)(uint32_t)q[kMiNnCand];
       stats->mp_nn_cells += (uint64_t)(uint32_t)q[kMiNnCells];
-      stats->mp_nn_certified += (uint64_t)(uint32_t)q[kMiNnCert];
     }
   }
   return LOAM_OK;

@@ -28,9 +28,8 @@ enum { kMiCenW = 0, kMiCenH, kMiCenD, kMiDegen, kMiNValid, kMiIters, kMiRows, kM
        kMiShifts,    // cube-grid slab shifts of this frame's recentring (the reference's passes)
        kMiNnCand,    // map points the 5-NN evaluated this frame (seeds included)
        kMiNnCells,   // hash bucket ranges the 5-NN read this frame
-       kMiNnCert,    // 5-NN queries settled by their certificate this frame (k_mp_nnfit_cert)
        kMpStateInts = 28 };
-static_assert(kMiNnCert < kMpStateInts, "istate layout");
+static_assert(kMiNnCells < kMpStateInts, "istate layout");
 
 // one mapping frame's inputs for every instance (device pointers)
 struct MpInput {
@@ -107,8 +106,6 @@ struct MpBuffers {
   int4* q_nn = nullptr;       // [P][cap_stack][2] this iteration's ordered 5-NN (i0..i3 | i4, d4 bits)
   float4* q_fit = nullptr;    // [P][cap_stack][4] MpFit: the 5-NN a line / plane was fitted to + the fit
                               // (k_mp_nnfit: the last iteration's 5-NN, distinct, fit-valid + the fit)
-  float4* q_cert = nullptr;   // [P][cap_stack] the 5-NN certificate: the last full search's query point
-                              // and a lower bound of every other point's distance (w; 0: none)
   // insertion / per-cube downsampling
   int* app_cnt = nullptr;     // [P][kCubeNum][2] appended points per cube
   int* citems = nullptr;      // [P][2 * kCubeNum] non-empty (kind, cube, valid index) of the new store

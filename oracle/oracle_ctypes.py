@@ -58,7 +58,7 @@ class Stats(ctypes.Structure):
                                         # engine-only search counters (zero here: the oracle's kd-tree
                                         # does different work)
                                         "mp_nn_candidates", "mp_nn_cells", "od_assoc_gathered",
-                                        "od_assoc_boxes", "mp_nn_certified")]
+                                        "od_assoc_boxes")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -12,7 +12,7 @@ STAT_KEYS = ("n_raw", "n_ring", "n_sharp", "n_less_sharp", "n_flat", "n_less_fla
              "mp_map_valid_points", "mp_stack_iters", "mp_fits", "od_query_iters", "od_row_evals",
              "bytes_sr", "bytes_od", "bytes_mp", "od_degenerate_steps", "od_nan_skips",
              "mp_degenerate_steps", "mp_grid_shifts", "mp_nn_candidates", "mp_nn_cells",
-             "od_assoc_gathered", "od_assoc_boxes", "mp_nn_certified")
+             "od_assoc_gathered", "od_assoc_boxes")
 
 
 def poses_of(prev, cur):

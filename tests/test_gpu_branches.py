@@ -239,11 +239,7 @@ def _share_run(loam, sg, **tune):
     {"od_assoc_wg": 16},                     # fewer association waves per problem (queries looped)
     {"od_rows_deep_max": 128},               # k_od_rows<., 8>: eight stored rows' loads in flight
     {"od_rows_deep_max": 128, "od_fused_max": 128},
-    {"mp_fused_max": 0},                     # k_mp_nnfit_cert<false> + k_mp_iter
-    {"nn_cert": 0},                          # k_mp_nnfit: every query searched every iteration
-    {"nn_cert": 0, "mp_fused_max": 0},       # k_mp_nnfit<false> + k_mp_iter
-    {"nn_cert": 1},                          # the certificate with one 64-query chunk per wave
-    {"nn_cert": 2},
+    {"mp_fused_max": 0},                     # k_mp_nnfit<false> + k_mp_iter
     {"graph": 1},                            # the step captured as a HIP graph and replayed
     {"mp_fused_max": 0, "mp_iter_wide_max": 128},  # k_mp_iter<1024>
     {"vg_merge": 0},                         # the cube VoxelGrid cascade alone (no k_vg_merge)
@@ -312,41 +308,3 @@ def test_pipeline_rotation_then_sequential(loam, oc, sg):
         for k in ("od_iters", "mp_iters", "od_corner_last", "od_surf_last", "od_assoc_points"):
             assert st[k] == st0[k], ("sequential", n, k)
     e.close()
-
-
-@pytest.mark.parametrize("dense", [False, True], ids=["config4_1024", "config5_64"])
-def test_nn_certificate_bitexact(loam, sg, dense):
-    """5-NN queries settled by the certificate of their last full search (k_mp_nnfit_cert, tuning
-    nn_cert, the batch default) return exactly what the search returns: every pose of the bench's
-    1024 config-4 problems and of the 64 config-5 problems equal to the searching run's
-    (nn_cert = 0), the same iteration counts, and the certificate does settle queries
-    (mp_nn_certified, counted in the profiling pass)"""
-    kw = dict(n_rings=64, max_points=160000, od_max_iter=100, mp_max_iter=20)
-    if dense:
-        prevs, curs = sg.batch_problems(64, base_seed=5000, lidar=sg.HDL64)
-        cfg = loam.default_config(ring_model=loam.RING_LINEAR, **kw)
-    else:
-        prevs, curs = sg.batch_problems(1024, base_seed=1000)
-        cfg = None
-
-    def run(k):
-        e = loam.Engine(cfg) if cfg is not None else loam.Engine()
-        e.set_tuning(nn_cert=k)
-        e.batch_upload(prevs, curs)
-        e.batch_run()
-        r = e.batch_download()
-        it = e.batch_lm_info()[:2]
-        e.set_profiling(True)
-        e.batch_run()
-        st = e.batch_download()[2]
-        e.close()
-        return r, it, st
-
-    (od0, aft0, _), it0, _ = run(0)
-    (od1, aft1, _), it1, sp = run(4)
-    np.testing.assert_array_equal(od1, od0)
-    np.testing.assert_array_equal(aft1, aft0)
-    np.testing.assert_array_equal(it1[0], it0[0])
-    np.testing.assert_array_equal(it1[1], it0[1])
-    print(f"certified {sp['mp_nn_certified']} of {sp['mp_stack_iters']} 5-NN query-iterations")
-    assert sp["mp_nn_certified"] > 0
