@@ -634,11 +634,6 @@ LOAM_D void wave_window(const float4* L, const float4* ch, int c, int end, int d
                        // its second pass over the cells cost more than the sub-chunks it saved
                        // (k_od_assoc at 1024: 2.42 with, 2.35 without)
 #endif
-// sub-chunk picks per lane per wave step of wave_window_mono
-#ifndef LOAM_WIN_VISIT
-#define LOAM_WIN_VISIT 2
-#endif
-constexpr int kWinVisit = LOAM_WIN_VISIT;
 #ifndef LOAM_WIN_TIGHTEN
 #define LOAM_WIN_TIGHTEN 0  // bounds tightened after every wave step: 0 never (the seeds' / cells' only),
 #endif                      // 1 always, 2 in the first (unseeded) round
@@ -686,15 +681,10 @@ LOAM_D void wave_window_mono(const float4* L, const float4* fb, const int* rs, i
         any |= live[u] != 0;
       }
       if (!any) break;
-      // the first PER x V of them in index order; lane l visits point l % kSub of picks
-      // l / kSub, l / kSub + PER, ... (V points per lane, their loads in flight together).  Without
-      // tightening the bounds are fixed, so every live sub-chunk is visited whatever the grouping:
-      // V only sets how many dependent steps the window takes
-      int mine[kWinVisit], npick = 0;
+      // the first PER of them in index order; lane l visits point l % kSub of pick l / kSub
+      int mine = -1, npick = 0;
 #pragma unroll
-      for (int v = 0; v < kWinVisit; ++v) mine[v] = -1;
-#pragma unroll
-      for (int s = 0; s < PER * kWinVisit; ++s) {
+      for (int s = 0; s < PER; ++s) {
         int pk = -1;
 #pragma unroll
         for (int u = 0; u < BPL; ++u)
@@ -703,35 +693,24 @@ LOAM_D void wave_window_mono(const float4* L, const float4* fb, const int* rs, i
             live[u] &= live[u] - 1;
           }
         if (pk >= 0) ++npick;
-        if (lane / kSub == s % PER) mine[s / PER] = pk;
+        if (lane / kSub == s) mine = pk;
       }
       if (LOAM_ASSOC_PHASE == 0 || LOAM_ASSOC_PHASE == 3) wpts += npick * kSub;
       float ds = 3.4e38f, dot = 3.4e38f;
-      float4 av[kWinVisit];
-      int jv[kWinVisit];
-#pragma unroll
-      for (int v = 0; v < kWinVisit; ++v) {
-        jv[v] = mine[v] >= 0 ? (g + mine[v]) * kSub + lane % kSub : -1;
-        const bool in = mine[v] >= 0 && jv[v] >= w0 && jv[v] < w1 && jv[v] != c;
-        if (!in) jv[v] = -1;
-        av[v] = in ? L[jv[v]] : make_float4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int v = 0; v < kWinVisit; ++v) {
-        const int j = jv[v];
-        if (j < 0) continue;
-        const float4 a = av[v];
+      const int j = (g + mine) * kSub + lane % kSub;
+      if (mine >= 0 && j >= w0 && j < w1 && j != c) {
+        const float4 a = L[j];
         const float d = sqdist(a.x, a.y, a.z, sel.x, sel.y, sel.z);
         const uint32_t pos = j > c ? (uint32_t)(j - c - 1) : (1u << 30) + (uint32_t)(c - 1 - j);
         const uint64_t key = ((uint64_t)fkey(d) << 32) | pos;
         if (j >= rs0 && j < rs1) {
           if (want_same) {
             k2 = key < k2 ? key : k2;
-            ds = fminf(ds, d);
+            ds = d;
           }
         } else {
           k3 = key < k3 ? key : k3;
-          dot = fminf(dot, d);
+          dot = d;
         }
       }
       if (tighten) {
