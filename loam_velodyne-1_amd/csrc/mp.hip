@@ -243,6 +243,33 @@ __global__ __launch_bounds__(256) void k_mp_stack(MpBuffers b, MpInput in) {
 // input order — and one output point per voxel, the float mean of x, y, z, intensity summed in
 // sorted order.  vg_run cascades three hand-written kernels by segment size; no library sort.
 
+// The segment's voxel frame (PCL VoxelGrid: bbox over its points, min_b = floor(min / leaf), the
+// divb multipliers), or the one the job supplies (j.frame: a split parent's); false when the leaf is
+// "too small" for the bbox (PCL then outputs the input unchanged; a supplied frame never is)
+template <int NT>
+__device__ __forceinline__ bool vg_frame_of(const VgJob& j, int s, const float4* in, int n, float inv, VgFrame& fr) {
+  if (j.frame) {
+    fr = j.frame[s];
+    return true;
+  }
+  const int tid = threadIdx.x;
+  float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+  for (int i = tid; i < n; i += NT) {
+    const float4 a = in[i];
+    mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
+    mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
+  }
+  block_bbox<NT>(mn, mx);
+  if (vg_leaf_too_small(mn, mx, inv)) return false;
+  fr.m0 = (int)floorf(mn[0] * inv);
+  fr.m1 = (int)floorf(mn[1] * inv);
+  fr.m2 = (int)floorf(mn[2] * inv);
+  fr.divx = (int)floorf(mx[0] * inv) - fr.m0 + 1;
+  fr.divy = (int)floorf(mx[1] * inv) - fr.m1 + 1;
+  fr.pad = (int)floorf(mx[2] * inv) - fr.m2 + 1;  // (divz: the split's key range)
+  return true;
+}
+
 // Fused segmented VoxelGrid with an LDS radix sort: one workgroup per segment of at most NT*E
 // points does the bbox, the voxel keys, a stable radix sort of (voxel, position) pairs over the
 // bits the keys can differ in, and the ordered per-voxel means.  Segments beyond NT*E are appended
@@ -269,22 +296,15 @@ __global__ __launch_bounds__(NT) void k_vg_radix(VgJob j) {
       continue;
     }
     const float4* in = j.in + b0;
-    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
-    for (int i = tid; i < n; i += NT) {
-      const float4 a = in[i];
-      mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
-      mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
-    }
-    block_bbox<NT>(mn, mx);
     const float inv = 1.0f / j.leaf[s];
-    if (vg_leaf_too_small(mn, mx, inv)) {  // "leaf size too small": output = input
+    VgFrame fr;
+    if (!vg_frame_of<NT>(j, s, in, n, inv, fr)) {  // "leaf size too small": output = input
       for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
       if (tid == 0) j.out_count[s] = n;
       continue;
     }
-    const int m0 = (int)floorf(mn[0] * inv), m1 = (int)floorf(mn[1] * inv), m2 = (int)floorf(mn[2] * inv);
-    const int divx = (int)floorf(mx[0] * inv) - m0 + 1, divy = (int)floorf(mx[1] * inv) - m1 + 1;
-    const uint32_t mul1 = (uint32_t)divx, mul2 = (uint32_t)(divx * divy);
+    const int m0 = fr.m0, m1 = fr.m1, m2 = fr.m2;
+    const uint32_t mul1 = (uint32_t)fr.divx, mul2 = (uint32_t)(fr.divx * fr.divy);
     uint32_t kmax = 0;
     for (int i = tid; i < n; i += NT) {
       const float4 a = in[i];
@@ -369,22 +389,15 @@ __device__ __forceinline__ void vg_idx_segment(const VgJob& j, int s, int b0, in
                            uint32_t* sc, uint32_t* dtot, uint32_t* dbase, float* fsc, int* isc) {
   const int tid = threadIdx.x;
     const float4* in = j.in + b0;
-    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
-    for (int i = tid; i < n; i += NT) {
-      const float4 a = in[i];
-      mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
-      mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
-    }
-    block_bbox<NT>(mn, mx);
     const float inv = 1.0f / j.leaf[s];
-    if (vg_leaf_too_small(mn, mx, inv)) {  // "leaf size too small": output = input
+    VgFrame fr;
+    if (!vg_frame_of<NT>(j, s, in, n, inv, fr)) {  // "leaf size too small": output = input
       for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
       if (tid == 0) j.out_count[s] = n;
       return;
     }
-    const int m0 = (int)floorf(mn[0] * inv), m1 = (int)floorf(mn[1] * inv), m2 = (int)floorf(mn[2] * inv);
-    const int divx = (int)floorf(mx[0] * inv) - m0 + 1, divy = (int)floorf(mx[1] * inv) - m1 + 1;
-    const uint32_t mul1 = (uint32_t)divx, mul2 = (uint32_t)(divx * divy);
+    const int m0 = fr.m0, m1 = fr.m1, m2 = fr.m2;
+    const uint32_t mul1 = (uint32_t)fr.divx, mul2 = (uint32_t)(fr.divx * fr.divy);
     uint32_t kmax = 0;
     for (int i = tid; i < n; i += NT) {
       const float4 a = in[i];
@@ -535,23 +548,16 @@ __global__ __launch_bounds__(NT) void k_vg_big(VgJob j) {
     const int s = j.list[li];
     const int b0 = j.begin[s], n = j.end[s] - b0;
     const float4* in = j.in + b0;
-    float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
-    for (int i = tid; i < n; i += NT) {
-      const float4 a = in[i];
-      mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
-      mx[0] = fmaxf(mx[0], a.x); mx[1] = fmaxf(mx[1], a.y); mx[2] = fmaxf(mx[2], a.z);
-    }
-    block_bbox<NT>(mn, mx);
     const float inv = 1.0f / j.leaf[s];
-    if (vg_leaf_too_small(mn, mx, inv)) {  // "leaf size too small": output = input
+    VgFrame fr;
+    if (!vg_frame_of<NT>(j, s, in, n, inv, fr)) {  // "leaf size too small": output = input
       for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
       if (tid == 0) j.out_count[s] = n;
       __syncthreads();
       continue;
     }
-    const int m0 = (int)floorf(mn[0] * inv), m1 = (int)floorf(mn[1] * inv), m2 = (int)floorf(mn[2] * inv);
-    const int divx = (int)floorf(mx[0] * inv) - m0 + 1, divy = (int)floorf(mx[1] * inv) - m1 + 1;
-    const uint32_t mul1 = (uint32_t)divx, mul2 = (uint32_t)(divx * divy);
+    const int m0 = fr.m0, m1 = fr.m1, m2 = fr.m2;
+    const uint32_t mul1 = (uint32_t)fr.divx, mul2 = (uint32_t)(fr.divx * fr.divy);
     for (int i = tid; i < 8 * 16; i += NT) (&hist[0][0])[i] = 0;
     __syncthreads();
     uint32_t* K = j.keys + b0;
@@ -643,6 +649,129 @@ __global__ __launch_bounds__(NT) void k_vg_big(VgJob j) {
       outn += tot;
     }
     if (tid == 0) j.out_count[s] = outn;
+    __syncthreads();
+  }
+}
+
+// The big-segment split (VgSplit, the HDL-64E surf stacks): one workgroup per parent of the job's
+// big list computes the parent's frame (vg_frame_of), its voxel keys' top 4 bits (of the bit range
+// the frame allows) as a bucket, the bucket sizes, and re-orders the points stably into the buckets
+// (tiles ranked in registers by tile_rank4, as k_vg_big's passes): bucket d of parent li becomes
+// sub-segment li * 16 + d in the parent's frame.  Equal keys share a bucket and buckets are key
+// ranges in order, so the sub-segments' VoxelGrid outputs in bucket order are the parent's output,
+// each voxel summed over the same points in the same (input) order.  A parent whose leaf is "too
+// small" is copied to its output here (PCL) and gets empty sub-segments; list slots beyond the
+// job's big list too.
+template <int NT, int E>
+__global__ __launch_bounds__(NT) void k_vg_split(VgJob j, VgSplit x) {
+  constexpr int TILE = NT * E;
+  __shared__ uint32_t sc[(NT / 64 + 1) * 8];
+  __shared__ uint32_t hist[16], dbase[16], ttot[16];
+  const int tid = threadIdx.x;
+  const int nl = *j.list_n;
+  for (int li = blockIdx.x; li < x.npar; li += gridDim.x) {
+    int* sb = x.begin + (size_t)li * 16;
+    int* se = x.end + (size_t)li * 16;
+    if (li >= nl) {
+      if (tid < 16) { sb[tid] = 0; se[tid] = 0; }
+      continue;
+    }
+    const int s = j.list[li];
+    const int b0 = j.begin[s], n = j.end[s] - b0;
+    const float4* in = j.in + b0;
+    const float inv = 1.0f / j.leaf[s];
+    VgFrame fr;
+    if (!vg_frame_of<NT>(j, s, in, n, inv, fr)) {  // "leaf size too small": output = input
+      for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
+      if (tid == 0) j.out_count[s] = n;
+      if (tid < 16) { sb[tid] = 0; se[tid] = 0; }
+      __syncthreads();
+      continue;
+    }
+    const uint32_t mul1 = (uint32_t)fr.divx, mul2 = (uint32_t)(fr.divx * fr.divy);
+    // the key range the frame allows (keys are uint32: a wider range buckets the wrapped keys by
+    // their top bits, still a monotone bucket of the sorted key)
+    const uint64_t kmax = (uint64_t)(fr.divx - 1) + (uint64_t)(fr.divy - 1) * (uint64_t)fr.divx +
+                          (uint64_t)(fr.pad - 1) * (uint64_t)fr.divx * (uint64_t)fr.divy;
+    const uint32_t km = kmax > 0xffffffffull ? 0xffffffffu : (uint32_t)kmax;
+    const int bits = km ? 32 - __builtin_clz(km) : 0;
+    const int shift = bits > 4 ? bits - 4 : 0;
+    auto key_of = [&](const float4& a) {
+      const int i0 = (int)(floorf(a.x * inv) - (float)fr.m0);
+      const int i1 = (int)(floorf(a.y * inv) - (float)fr.m1);
+      const int i2 = (int)(floorf(a.z * inv) - (float)fr.m2);
+      return (uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2;
+    };
+    if (tid < 16) hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += NT) atomicAdd(&hist[(key_of(in[i]) >> shift) & 15u], 1u);
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t r = 0;
+      for (int d = 0; d < 16; ++d) { dbase[d] = r; r += hist[d]; }
+    }
+    __syncthreads();
+    if (tid < 16) {
+      const int k = li * 16 + tid;
+      sb[tid] = b0 + (int)dbase[tid];
+      se[tid] = b0 + (int)(dbase[tid] + hist[tid]);
+      x.leaf[k] = j.leaf[s];
+      x.frame[k] = fr;
+    }
+    float4* dst = x.pts + b0;
+    for (int t0 = 0; t0 < n; t0 += TILE) {
+      const int nt = min(TILE, n - t0);
+      uint32_t k[E];
+      float4 a[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = tid * E + e;
+        a[e] = i < nt ? in[t0 + i] : make_float4(0, 0, 0, 0);
+        k[e] = i < nt ? key_of(a[e]) : 0u;
+      }
+      int rank[E];
+      tile_rank4<NT, E>(k, shift, nt, sc, ttot, rank);
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (rank[e] >= 0) dst[dbase[(k[e] >> shift) & 15u] + rank[e]] = a[e];
+      __syncthreads();
+      if (tid < 16) dbase[tid] += ttot[tid];
+      __syncthreads();
+    }
+  }
+}
+
+// the split parents' outputs: the 16 sub-segments' VoxelGrid outputs concatenated in bucket order
+// into the parent's output (one workgroup per parent)
+template <int NT>
+__global__ __launch_bounds__(NT) void k_vg_join(VgJob j, VgSplit x) {
+  __shared__ int pre[17];
+  const int tid = threadIdx.x;
+  const int nl = min(*j.list_n, x.npar);
+  for (int li = blockIdx.x; li < nl; li += gridDim.x) {
+    const int s = j.list[li];
+    const int* sb = x.begin + (size_t)li * 16;
+    const int* se = x.end + (size_t)li * 16;
+    const int* sc = x.out_count + (size_t)li * 16;
+    if (tid == 0) {
+      int r = 0, any = 0;
+      for (int d = 0; d < 16; ++d) {
+        pre[d] = r;
+        const int m = se[d] - sb[d];
+        any |= m;
+        r += m > 0 ? sc[d] : 0;
+      }
+      pre[16] = any ? r : -1;  // (-1: the parent was copied by k_vg_split)
+    }
+    __syncthreads();
+    if (pre[16] >= 0) {
+      const int b0 = j.begin[s];
+      for (int d = 0; d < 16; ++d) {
+        const int m = se[d] - sb[d] > 0 ? sc[d] : 0;
+        for (int t = tid; t < m; t += NT) j.out[b0 + pre[d] + t] = x.out[sb[d] + t];
+      }
+      if (tid == 0) j.out_count[s] = pre[16];
+    }
     __syncthreads();
   }
 }
@@ -818,7 +947,8 @@ __global__ __launch_bounds__(NT) void k_vg_merge(VgJob j) {
 constexpr int kVgListGrid = 1024, kVgBigGrid = 256;
 constexpr int kVgStack = 0, kVgCubes = 1, kVgSurround = 2;
 template <int TAG>
-hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true, bool tier2_idx = false) {
+hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true, bool tier2_idx = false,
+                  const VgSplit* split = nullptr) {
   if (j0.nseg == 0) return hipSuccess;
   if (!j0.zeroed) {
     const hipError_t e = hipMemsetAsync(j0.counts, 0, 2 * sizeof(int), st);
@@ -849,7 +979,30 @@ hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true,
     VgJob c = j0;
     c.list = j0.lists[last];
     c.list_n = j0.counts + last;
-    hipLaunchKernelGGL((k_vg_big<1024, 12, TAG>), dim3(std::min(j0.nseg, kVgBigGrid)), dim3(1024), 0, st, c);
+    if (split && split->npar >= j0.nseg) {  // (every segment of the job fits the split's parents)
+      // the big segments split into 16 key-range buckets each, the buckets through the LDS tiers
+      hipLaunchKernelGGL((k_vg_split<1024, 12>), dim3(std::min(split->npar, 1024)), dim3(1024), 0, st, c, *split);
+      VgJob sj = j0;
+      sj.in = split->pts;
+      sj.out = split->out;
+      sj.begin = split->begin;
+      sj.end = split->end;
+      sj.leaf = split->leaf;
+      sj.out_count = split->out_count;
+      sj.frame = split->frame;
+      sj.nseg = split->npar * 16;
+      sj.lists[0] = split->lists[0];
+      sj.lists[1] = split->lists[1];
+      sj.counts = split->counts;
+      sj.zeroed = false;
+      sj.list = nullptr;
+      sj.list_n = nullptr;
+      const hipError_t e = vg_run<TAG>(sj, st, 2048, true, true);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL((k_vg_join<256>), dim3(std::min(split->npar, 1024)), dim3(256), 0, st, c, *split);
+    } else {
+      hipLaunchKernelGGL((k_vg_big<1024, 12, TAG>), dim3(std::min(j0.nseg, kVgBigGrid)), dim3(1024), 0, st, c);
+    }
   }
   return hipGetLastError();
 }
@@ -2666,6 +2819,18 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
   A(&b.vg_mlist, (size_t)P * 2 * kMaxValid * sizeof(int));
   A(&b.vseg_nold, (size_t)P * 2 * kMaxValid * sizeof(int));
   A(&b.vseg_skip, (size_t)P * 2 * kMaxValid * sizeof(int));
+  // the stack job's big-segment split: 2P parents x 16 sub-segments, points / outputs like the stacks
+  b.vgs.npar = 2 * P;
+  A(&b.vgs.pts, Ps * sizeof(float4));
+  A(&b.vgs.out, Ps * sizeof(float4));
+  A(&b.vgs.begin, (size_t)P * 32 * sizeof(int));
+  A(&b.vgs.end, (size_t)P * 32 * sizeof(int));
+  A(&b.vgs.out_count, (size_t)P * 32 * sizeof(int));
+  A(&b.vgs.leaf, (size_t)P * 32 * sizeof(float));
+  A(&b.vgs.frame, (size_t)P * 32 * sizeof(VgFrame));
+  A(&b.vgs.lists[0], (size_t)P * 32 * sizeof(int));
+  A(&b.vgs.lists[1], (size_t)P * 32 * sizeof(int));
+  A(&b.vgs.counts, 2 * sizeof(int));
   A(&b.reg, (size_t)P * b.capS * sizeof(float4));
   A(&b.part, (size_t)P * std::max(kMpSmallGrid, kMpFitGridMax) * 28 * sizeof(double));
   A(&b.rot, (size_t)P * 6 * sizeof(double));
@@ -2688,7 +2853,9 @@ void mp_free(MpBuffers& b) {
                   b.hC_pts, b.hS_pts, b.nfrom, b.q_ok, b.q_cf, b.q_nn, b.q_fit, b.citems, b.nitems, b.app_cnt, b.app_off, b.app, b.vin, b.vout,
                   b.vseg_b, b.vseg_e, b.vseg_cnt, b.vseg_leaf, b.sseg_b, b.sseg_e, b.sseg_cnt, b.sseg_leaf,
                   b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_l0, b.vg_l1, b.vg_lin, b.vg_cnt, b.reg, b.nreg, b.part, b.done, b.rot,
-                  b.vg_mlist, b.vseg_nold, b.vseg_skip, b.ls_part, b.ls_flag, b.ls_epoch};
+                  b.vg_mlist, b.vseg_nold, b.vseg_skip, b.ls_part, b.ls_flag, b.ls_epoch, b.vgs.pts, b.vgs.out,
+                  b.vgs.begin, b.vgs.end, b.vgs.out_count, b.vgs.leaf, b.vgs.frame, b.vgs.lists[0], b.vgs.lists[1],
+                  b.vgs.counts};
   if (b.upd_pending && b.upd_done) (void)hipEventSynchronize(b.upd_done);
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
@@ -2750,7 +2917,8 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     b.note(hipEventRecord(side->fork[0], st));
     b.note(hipStreamWaitEvent(side->st, side->fork[0], 0));
   }
-  b.note(vg_run<kVgStack>(js, fork ? side->st : st, P <= 4 ? 12288 : 2048, !fits, /*tier2_idx=*/true));
+  b.note(vg_run<kVgStack>(js, fork ? side->st : st, P <= 4 ? 12288 : 2048, !fits, /*tier2_idx=*/true,
+                          b.tune.vg_split ? &b.vgs : nullptr));
   if (fork) b.note(hipEventRecord(side->join[0], side->st));
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);

@@ -46,6 +46,12 @@ struct MpInput {
   int end_mode = 0;
 };
 
+// the voxel frame of a segment (PCL VoxelGrid's min_b and divb multipliers), for sub-segments that
+// take their parent's (vg_run's big-segment split)
+struct VgFrame {
+  int m0, m1, m2, divx, divy, pad;
+};
+
 // segmented PCL VoxelGrid job (segment s: input in[begin[s] .. end[s]), output out[begin[s] ..))
 struct VgJob {
   const float4* in;
@@ -75,6 +81,25 @@ struct VgJob {
   const int* mlist = nullptr;
   const int* mlist_n = nullptr;
   int* skip = nullptr;
+  // per segment: the voxel frame to use instead of the segment's own bounding box (sub-segments of a
+  // split parent); nullptr: every segment computes its own
+  const VgFrame* frame = nullptr;
+};
+
+// vg_run's split of the segments beyond the LDS tiers (the HDL-64E surf stacks): each parent's
+// points re-ordered stably into 16 buckets by the top bits of their voxel key (k_vg_split), the
+// buckets VoxelGridded as sub-segments in the parent's frame by the LDS cascade, their outputs
+// concatenated in bucket order (k_vg_join).  Sub-segment li * 16 + d; pts / out indexed like the
+// job's input
+struct VgSplit {
+  float4* pts = nullptr;
+  float4* out = nullptr;
+  int *begin = nullptr, *end = nullptr, *out_count = nullptr;
+  float* leaf = nullptr;
+  VgFrame* frame = nullptr;
+  int* lists[2] = {nullptr, nullptr};
+  int* counts = nullptr;  // [2]
+  int npar = 0;           // parents it holds (list entries beyond go to k_vg_big)
 };
 
 struct MpBuffers {
@@ -125,6 +150,7 @@ struct MpBuffers {
   int* vg_mlist = nullptr;                 // [P][2][kMaxValid] cube segments k_vg_merge may take
   int* vseg_nold = nullptr;                // [P][2][kMaxValid] leading points from the cube's last DS
   int* vseg_skip = nullptr;                // [P][2][kMaxValid] 1: k_vg_merge wrote the segment
+  VgSplit vgs;                             // the stack job's big-segment split (2P parents)
   float4* reg = nullptr;      // [P][capS] registered full cloud
   double* part = nullptr;     // [P][kMpSmallGrid][28] k_mp_lm_small's per-workgroup JᵀJ | Jᵀb | rows
   int* done = nullptr;        // [P] its workgroups finished (the last one runs the step)

@@ -28,6 +28,8 @@ def short(name):
         return VG_JOBS.get(tag, "vg_other") + "<" + base.split("<")[0] + ">"
     if base.startswith("k_vg_merge<"):
         return "vg_cubes<k_vg_merge>"
+    if base.startswith(("k_vg_split<", "k_vg_join<")):  # (the stack job's big-segment split)
+        return "vg_stack<" + base.split("<")[0] + ">"
     return base
 
 
