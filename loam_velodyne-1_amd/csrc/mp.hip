@@ -946,14 +946,46 @@ __global__ __launch_bounds__(NT) void k_vg_merge(VgJob j) {
 // TAG: kVgStack / kVgCubes / kVgSurround, so a kernel trace or PMC pass tells the jobs apart
 constexpr int kVgListGrid = 1024, kVgBigGrid = 256;
 constexpr int kVgStack = 0, kVgCubes = 1, kVgSurround = 2;
+// split (the stack job's VgSplit, when it holds every segment of the job as a parent): the segments
+// the cascade's LDS kernels cannot take are split into key-range buckets (k_vg_split / k_vg_join)
+// instead of k_vg_big; split_early: already the segments beyond the first kernel (instead of the
+// second tier too)
 template <int TAG>
 hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true, bool tier2_idx = false,
-                  const VgSplit* split = nullptr) {
+                  const VgSplit* split = nullptr, bool split_early = false) {
   if (j0.nseg == 0) return hipSuccess;
   if (!j0.zeroed) {
     const hipError_t e = hipMemsetAsync(j0.counts, 0, 2 * sizeof(int), st);
     if (e != hipSuccess) return e;
   }
+  if (split && split->npar < j0.nseg) split = nullptr;
+  // the segments of list `l` (count at j0.counts + l) through the split: 16 key-range buckets each,
+  // the buckets through the cascade in their parent's frame, the outputs joined
+  auto run_split = [&](int l) -> hipError_t {
+    VgJob c = j0;
+    c.list = j0.lists[l];
+    c.list_n = j0.counts + l;
+    hipLaunchKernelGGL((k_vg_split<1024, 12>), dim3(std::min(split->npar, 1024)), dim3(1024), 0, st, c, *split);
+    VgJob sj = j0;
+    sj.in = split->pts;
+    sj.out = split->out;
+    sj.begin = split->begin;
+    sj.end = split->end;
+    sj.leaf = split->leaf;
+    sj.out_count = split->out_count;
+    sj.frame = split->frame;
+    sj.nseg = split->npar * 16;
+    sj.lists[0] = split->lists[0];
+    sj.lists[1] = split->lists[1];
+    sj.counts = split->counts;
+    sj.zeroed = false;
+    sj.list = nullptr;
+    sj.list_n = nullptr;
+    const hipError_t e = vg_run<TAG>(sj, st, 2048, true, true);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_vg_join<256>), dim3(std::min(split->npar, 1024)), dim3(256), 0, st, c, *split);
+    return hipGetLastError();
+  };
   // the caller's input list (non-empty segments) is walked by a fixed grid
   const int grid = j0.list ? std::min(j0.nseg, 8192) : std::min(j0.nseg, 65536);
   VgJob a = j0;
@@ -962,6 +994,7 @@ hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true,
   int last = 0;  // the list k_vg_big takes
   if (cap1 <= 2048) {
     hipLaunchKernelGGL((k_vg_radix<256, 8, TAG>), dim3(grid), dim3(256), 0, st, a);
+    if (finish && split && split_early) return run_split(0);
     if (finish) {
       VgJob b = j0;
       b.list = j0.lists[0];
@@ -976,33 +1009,11 @@ hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true,
     hipLaunchKernelGGL((k_vg_radix<1024, 12, TAG>), dim3(grid), dim3(1024), 0, st, a);
   }
   if (finish) {
+    if (split) return run_split(last);
     VgJob c = j0;
     c.list = j0.lists[last];
     c.list_n = j0.counts + last;
-    if (split && split->npar >= j0.nseg) {  // (every segment of the job fits the split's parents)
-      // the big segments split into 16 key-range buckets each, the buckets through the LDS tiers
-      hipLaunchKernelGGL((k_vg_split<1024, 12>), dim3(std::min(split->npar, 1024)), dim3(1024), 0, st, c, *split);
-      VgJob sj = j0;
-      sj.in = split->pts;
-      sj.out = split->out;
-      sj.begin = split->begin;
-      sj.end = split->end;
-      sj.leaf = split->leaf;
-      sj.out_count = split->out_count;
-      sj.frame = split->frame;
-      sj.nseg = split->npar * 16;
-      sj.lists[0] = split->lists[0];
-      sj.lists[1] = split->lists[1];
-      sj.counts = split->counts;
-      sj.zeroed = false;
-      sj.list = nullptr;
-      sj.list_n = nullptr;
-      const hipError_t e = vg_run<TAG>(sj, st, 2048, true, true);
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL((k_vg_join<256>), dim3(std::min(split->npar, 1024)), dim3(256), 0, st, c, *split);
-    } else {
-      hipLaunchKernelGGL((k_vg_big<1024, 12, TAG>), dim3(std::min(j0.nseg, kVgBigGrid)), dim3(1024), 0, st, c);
-    }
+    hipLaunchKernelGGL((k_vg_big<1024, 12, TAG>), dim3(std::min(j0.nseg, kVgBigGrid)), dim3(1024), 0, st, c);
   }
   return hipGetLastError();
 }
@@ -2918,7 +2929,7 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     b.note(hipStreamWaitEvent(side->st, side->fork[0], 0));
   }
   b.note(vg_run<kVgStack>(js, fork ? side->st : st, P <= 4 ? 12288 : 2048, !fits, /*tier2_idx=*/true,
-                          b.tune.vg_split ? &b.vgs : nullptr));
+                          b.tune.vg_split ? &b.vgs : nullptr, b.tune.vg_split == 2));
   if (fork) b.note(hipEventRecord(side->join[0], side->st));
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);

@@ -149,15 +149,16 @@ def test_config5_batch_parity(loam, oc, sg):
     e.close()
     # the surf stacks beyond the LDS VoxelGrid kernels through k_vg_big instead of the key-range split
     # (tuning vg_split, k_vg_split / k_vg_join): the same poses and iterations bit for bit
-    e = loam.Engine(loam.default_config(ring_model=loam.RING_LINEAR, **kw))
-    e.set_tuning(vg_split=0)
-    e.batch_upload(prevs, curs)
-    e.batch_run()
-    od3, aft3, st3 = e.batch_download()
-    e.close()
-    np.testing.assert_array_equal(od3, od)
-    np.testing.assert_array_equal(aft3, aft)
-    assert (st3["od_iters"], st3["mp_iters"], st3["mp_stack"]) == (st["od_iters"], st["mp_iters"], st["mp_stack"])
+    for split in (0, 2):  # (2: already the segments beyond the first, 2048-point kernel split)
+        e = loam.Engine(loam.default_config(ring_model=loam.RING_LINEAR, **kw))
+        e.set_tuning(vg_split=split)
+        e.batch_upload(prevs, curs)
+        e.batch_run()
+        od3, aft3, st3 = e.batch_download()
+        e.close()
+        np.testing.assert_array_equal(od3, od)
+        np.testing.assert_array_equal(aft3, aft)
+        assert (st3["od_iters"], st3["mp_iters"], st3["mp_stack"]) == (st["od_iters"], st["mp_iters"], st["mp_stack"])
 
 
 def _msg_chain_engine(loam, sweeps):
