@@ -680,13 +680,34 @@ __global__ __launch_bounds__(NT) void k_vg_split(VgJob j, VgSplit x) {
     const int b0 = j.begin[s], n = j.end[s] - b0;
     const float4* in = j.in + b0;
     const float inv = 1.0f / j.leaf[s];
+    // the parent's frame (vg_frame_of's, with four loads in flight per thread)
     VgFrame fr;
-    if (!vg_frame_of<NT>(j, s, in, n, inv, fr)) {  // "leaf size too small": output = input
-      for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
-      if (tid == 0) j.out_count[s] = n;
-      if (tid < 16) { sb[tid] = 0; se[tid] = 0; }
-      __syncthreads();
-      continue;
+    {
+      float mn[3] = {3.4e38f, 3.4e38f, 3.4e38f}, mx[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+      for (int i0 = tid; i0 < n; i0 += 4 * NT) {
+        float4 a[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] = in[min(i0 + u * NT, n - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          mn[0] = fminf(mn[0], a[u].x); mn[1] = fminf(mn[1], a[u].y); mn[2] = fminf(mn[2], a[u].z);
+          mx[0] = fmaxf(mx[0], a[u].x); mx[1] = fmaxf(mx[1], a[u].y); mx[2] = fmaxf(mx[2], a[u].z);
+        }
+      }
+      block_bbox<NT>(mn, mx);
+      if (vg_leaf_too_small(mn, mx, inv)) {  // "leaf size too small": output = input
+        for (int i = tid; i < n; i += NT) j.out[b0 + i] = in[i];
+        if (tid == 0) j.out_count[s] = n;
+        if (tid < 16) { sb[tid] = 0; se[tid] = 0; }
+        __syncthreads();
+        continue;
+      }
+      fr.m0 = (int)floorf(mn[0] * inv);
+      fr.m1 = (int)floorf(mn[1] * inv);
+      fr.m2 = (int)floorf(mn[2] * inv);
+      fr.divx = (int)floorf(mx[0] * inv) - fr.m0 + 1;
+      fr.divy = (int)floorf(mx[1] * inv) - fr.m1 + 1;
+      fr.pad = (int)floorf(mx[2] * inv) - fr.m2 + 1;
     }
     const uint32_t mul1 = (uint32_t)fr.divx, mul2 = (uint32_t)(fr.divx * fr.divy);
     // the key range the frame allows (keys are uint32: a wider range buckets the wrapped keys by
@@ -704,7 +725,14 @@ __global__ __launch_bounds__(NT) void k_vg_split(VgJob j, VgSplit x) {
     };
     if (tid < 16) hist[tid] = 0;
     __syncthreads();
-    for (int i = tid; i < n; i += NT) atomicAdd(&hist[(key_of(in[i]) >> shift) & 15u], 1u);
+    for (int i0 = tid; i0 < n; i0 += 4 * NT) {  // (four loads in flight per thread)
+      float4 a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = in[min(i0 + u * NT, n - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + u * NT < n) atomicAdd(&hist[(key_of(a[u]) >> shift) & 15u], 1u);
+    }
     __syncthreads();
     if (tid == 0) {
       uint32_t r = 0;
@@ -764,13 +792,26 @@ __global__ __launch_bounds__(NT) void k_vg_join(VgJob j, VgSplit x) {
       pre[16] = any ? r : -1;  // (-1: the parent was copied by k_vg_split)
     }
     __syncthreads();
-    if (pre[16] >= 0) {
-      const int b0 = j.begin[s];
-      for (int d = 0; d < 16; ++d) {
-        const int m = se[d] - sb[d] > 0 ? sc[d] : 0;
-        for (int t = tid; t < m; t += NT) j.out[b0 + pre[d] + t] = x.out[sb[d] + t];
+    if (pre[16] >= 0) {  // output t of the parent: bucket d = the last with pre[d] <= t
+      const int b0 = j.begin[s], tot = pre[16];
+      for (int t0 = tid; t0 < tot; t0 += 4 * NT) {
+        float4 v[4];
+        int o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int t = t0 + u * NT;
+          int d = 0;
+#pragma unroll
+          for (int step = 8; step > 0; step >>= 1)
+            if (d + step < 16 && pre[d + step] <= t) d += step;
+          o[u] = t;
+          v[u] = t < tot ? x.out[sb[d] + (t - pre[d])] : make_float4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (o[u] < tot) j.out[b0 + o[u]] = v[u];
       }
-      if (tid == 0) j.out_count[s] = pre[16];
+      if (tid == 0) j.out_count[s] = tot;
     }
     __syncthreads();
   }
@@ -983,7 +1024,7 @@ hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true,
     sj.list_n = nullptr;
     const hipError_t e = vg_run<TAG>(sj, st, 2048, true, true);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_vg_join<256>), dim3(std::min(split->npar, 1024)), dim3(256), 0, st, c, *split);
+    hipLaunchKernelGGL((k_vg_join<1024>), dim3(std::min(split->npar, 1024)), dim3(1024), 0, st, c, *split);
     return hipGetLastError();
   };
   // the caller's input list (non-empty segments) is walked by a fixed grid
