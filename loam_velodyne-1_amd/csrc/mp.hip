@@ -668,14 +668,10 @@ __global__ __launch_bounds__(NT) void k_vg_split(VgJob j, VgSplit x) {
   __shared__ uint32_t sc[(NT / 64 + 1) * 8];
   __shared__ uint32_t hist[16], dbase[16], ttot[16];
   const int tid = threadIdx.x;
-  const int nl = *j.list_n;
-  for (int li = blockIdx.x; li < x.npar; li += gridDim.x) {
+  const int nl = min(*j.list_n, x.npar);
+  for (int li = blockIdx.x; li < nl; li += gridDim.x) {
     int* sb = x.begin + (size_t)li * 16;
     int* se = x.end + (size_t)li * 16;
-    if (li >= nl) {
-      if (tid < 16) { sb[tid] = 0; se[tid] = 0; }
-      continue;
-    }
     const int s = j.list[li];
     const int b0 = j.begin[s], n = j.end[s] - b0;
     const float4* in = j.in + b0;
@@ -739,12 +735,14 @@ __global__ __launch_bounds__(NT) void k_vg_split(VgJob j, VgSplit x) {
       for (int d = 0; d < 16; ++d) { dbase[d] = r; r += hist[d]; }
     }
     __syncthreads();
-    if (tid < 16) {
+    if (tid < 16) {  // the sub-segments; the non-empty ones listed for the cascade
       const int k = li * 16 + tid;
       sb[tid] = b0 + (int)dbase[tid];
       se[tid] = b0 + (int)(dbase[tid] + hist[tid]);
       x.leaf[k] = j.leaf[s];
       x.frame[k] = fr;
+      x.out_count[k] = 0;
+      if (hist[tid]) x.ilist[atomicAdd(&x.counts[2], 1)] = k;
     }
     float4* dst = x.pts + b0;
     for (int t0 = 0; t0 < n; t0 += TILE) {
@@ -1006,6 +1004,8 @@ hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true,
     VgJob c = j0;
     c.list = j0.lists[l];
     c.list_n = j0.counts + l;
+    const hipError_t ez = hipMemsetAsync(split->counts, 0, 3 * sizeof(int), st);
+    if (ez != hipSuccess) return ez;
     hipLaunchKernelGGL((k_vg_split<1024, 12>), dim3(std::min(split->npar, 1024)), dim3(1024), 0, st, c, *split);
     VgJob sj = j0;
     sj.in = split->pts;
@@ -1019,9 +1019,9 @@ hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true,
     sj.lists[0] = split->lists[0];
     sj.lists[1] = split->lists[1];
     sj.counts = split->counts;
-    sj.zeroed = false;
-    sj.list = nullptr;
-    sj.list_n = nullptr;
+    sj.zeroed = true;                  // (counts[0..1] zeroed above)
+    sj.list = split->ilist;            // the non-empty sub-segments k_vg_split listed
+    sj.list_n = split->counts + 2;
     const hipError_t e = vg_run<TAG>(sj, st, 2048, true, true);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_vg_join<1024>), dim3(std::min(split->npar, 1024)), dim3(1024), 0, st, c, *split);
@@ -2882,7 +2882,8 @@ hipError_t mp_alloc(MpBuffers& b, int P, int R, int cap_pts, int map_cap, int ma
   A(&b.vgs.frame, (size_t)P * 32 * sizeof(VgFrame));
   A(&b.vgs.lists[0], (size_t)P * 32 * sizeof(int));
   A(&b.vgs.lists[1], (size_t)P * 32 * sizeof(int));
-  A(&b.vgs.counts, 2 * sizeof(int));
+  A(&b.vgs.counts, 4 * sizeof(int));
+  A(&b.vgs.ilist, (size_t)P * 32 * sizeof(int));
   A(&b.reg, (size_t)P * b.capS * sizeof(float4));
   A(&b.part, (size_t)P * std::max(kMpSmallGrid, kMpFitGridMax) * 28 * sizeof(double));
   A(&b.rot, (size_t)P * 6 * sizeof(double));
@@ -2907,7 +2908,7 @@ void mp_free(MpBuffers& b) {
                   b.vg_k, b.vg_k2, b.vg_v, b.vg_v2, b.vg_l0, b.vg_l1, b.vg_lin, b.vg_cnt, b.reg, b.nreg, b.part, b.done, b.rot,
                   b.vg_mlist, b.vseg_nold, b.vseg_skip, b.ls_part, b.ls_flag, b.ls_epoch, b.vgs.pts, b.vgs.out,
                   b.vgs.begin, b.vgs.end, b.vgs.out_count, b.vgs.leaf, b.vgs.frame, b.vgs.lists[0], b.vgs.lists[1],
-                  b.vgs.counts};
+                  b.vgs.counts, b.vgs.ilist};
   if (b.upd_pending && b.upd_done) (void)hipEventSynchronize(b.upd_done);
   for (void* q : ptrs)
     if (q) (void)hipFree(q);

@@ -98,7 +98,8 @@ struct VgSplit {
   float* leaf = nullptr;
   VgFrame* frame = nullptr;
   int* lists[2] = {nullptr, nullptr};
-  int* counts = nullptr;  // [2]
+  int* ilist = nullptr;   // the non-empty sub-segments (the cascade's input list)
+  int* counts = nullptr;  // [3]: the cascade's two lists, ilist
   int npar = 0;           // parents it holds (list entries beyond go to k_vg_big)
 };
 
