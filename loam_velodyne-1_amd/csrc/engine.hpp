@@ -59,9 +59,10 @@ struct Tuning {
   int vg_merge = 1;        // the cubes' VoxelGrid merges an old sorted prefix with the appended tail
                            // (k_vg_merge; config 3's big cubes: 95 -> 50 us per mapping frame)
   int vg_merge_min = 12288;  // ... for segments of more than this many points
-  int vg_split = 1;        // the stack VoxelGrid's segments beyond the LDS kernels split into 16 key-range
-                           // buckets (k_vg_split / k_vg_join: the HDL-64E surf stacks) instead of k_vg_big;
-                           // 2: already those beyond the first (2048-point) kernel; 0: k_vg_big
+  int vg_split = 1;        // the stack VoxelGrid's big segments split into 16 key-range buckets (k_vg_split /
+                           // k_vg_join) instead of k_vg_big: 2 those beyond the LDS kernels, 3 already those
+                           // beyond the first (2048-point) kernel, 1 (auto) 3 for HDL-64E-sized sweeps, else 2;
+                           // 0: k_vg_big
   int sr_ahead = 64;       // for P >= this (0: never), loam_batch_run enqueues the next step's scan
                            // registration one step ahead (a second buffer set, a third stream), where
                            // it overlaps this step's latency-bound odometry / mapping launches.  A
@@ -124,7 +125,7 @@ struct Tuning {
                     {"od_rows_deep_max", &od_rows_deep_max, 0, 1 << 20}, {"nn_wg", &nn_wg, 0, 4096},
                     {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20},
                     {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20},
-                    {"vg_merge", &vg_merge, 0, 1}, {"vg_merge_min", &vg_merge_min, 0, 1 << 20}, {"vg_split", &vg_split, 0, 2},
+                    {"vg_merge", &vg_merge, 0, 1}, {"vg_merge_min", &vg_merge_min, 0, 1 << 20}, {"vg_split", &vg_split, 0, 3},
                     {"sr_ahead", &sr_ahead, 0, 1 << 20}, {"sr_ahead_at", &sr_ahead_at, -1, 2},
                     {"step_pipe", &step_pipe, 0, 1 << 20}, {"batch_streams", &batch_streams, 0, 1},
                     {"pipe_mp_sets", &pipe_mp_sets, 1, 2}, {"od_sel_min", &od_sel_min, 1, 1 << 20},

@@ -1006,7 +1006,7 @@ hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true,
     c.list_n = j0.counts + l;
     const hipError_t ez = hipMemsetAsync(split->counts, 0, 3 * sizeof(int), st);
     if (ez != hipSuccess) return ez;
-    hipLaunchKernelGGL((k_vg_split<1024, 12>), dim3(std::min(split->npar, 1024)), dim3(1024), 0, st, c, *split);
+    hipLaunchKernelGGL((k_vg_split<1024, 12>), dim3(std::min(split->npar, 256)), dim3(1024), 0, st, c, *split);
     VgJob sj = j0;
     sj.in = split->pts;
     sj.out = split->out;
@@ -1022,13 +1022,14 @@ hipError_t vg_run(const VgJob& j0, hipStream_t st, int cap1, bool finish = true,
     sj.zeroed = true;                  // (counts[0..1] zeroed above)
     sj.list = split->ilist;            // the non-empty sub-segments k_vg_split listed
     sj.list_n = split->counts + 2;
+    sj.grid_max = 2048;                // (the list is empty unless the job had big segments)
     const hipError_t e = vg_run<TAG>(sj, st, 2048, true, true);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_vg_join<1024>), dim3(std::min(split->npar, 1024)), dim3(1024), 0, st, c, *split);
+    hipLaunchKernelGGL((k_vg_join<1024>), dim3(std::min(split->npar, 256)), dim3(1024), 0, st, c, *split);
     return hipGetLastError();
   };
   // the caller's input list (non-empty segments) is walked by a fixed grid
-  const int grid = j0.list ? std::min(j0.nseg, 8192) : std::min(j0.nseg, 65536);
+  const int grid = std::min(j0.grid_max, j0.list ? std::min(j0.nseg, 8192) : std::min(j0.nseg, 65536));
   VgJob a = j0;
   a.big = j0.lists[0];
   a.big_n = j0.counts;
@@ -2970,8 +2971,12 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
     b.note(hipEventRecord(side->fork[0], st));
     b.note(hipStreamWaitEvent(side->st, side->fork[0], 0));
   }
+  // (vg_split 1: the split takes the segments beyond the first kernel when a sweep can fill several
+  // LDS-tier segments (HDL-64E: 64 problems 0.56 -> 0.49 ms/step), else only those beyond the LDS
+  // kernels (VLP-16 at 128 / 1024 problems: splitting beyond the first kernel 0.24 -> 0.32 ms/step))
+  const bool split_early = b.tune.vg_split == 3 || (b.tune.vg_split == 1 && b.capS > 4 * 16384);
   b.note(vg_run<kVgStack>(js, fork ? side->st : st, P <= 4 ? 12288 : 2048, !fits, /*tier2_idx=*/true,
-                          b.tune.vg_split ? &b.vgs : nullptr, b.tune.vg_split == 2));
+                          b.tune.vg_split ? &b.vgs : nullptr, split_early));
   if (fork) b.note(hipEventRecord(side->join[0], side->st));
   mark("vg_stack");
   hipLaunchKernelGGL(k_mp_gather, dim3(32, P), dim3(256), 0, st, b);

@@ -84,6 +84,7 @@ struct VgJob {
   // per segment: the voxel frame to use instead of the segment's own bounding box (sub-segments of a
   // split parent); nullptr: every segment computes its own
   const VgFrame* frame = nullptr;
+  int grid_max = 1 << 30;  // the first kernel's grid at most (the split's sub-job)
 };
 
 // vg_run's split of the segments beyond the LDS tiers (the HDL-64E surf stacks): each parent's

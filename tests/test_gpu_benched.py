@@ -149,7 +149,7 @@ def test_config5_batch_parity(loam, oc, sg):
     e.close()
     # the surf stacks beyond the LDS VoxelGrid kernels through k_vg_big instead of the key-range split
     # (tuning vg_split, k_vg_split / k_vg_join): the same poses and iterations bit for bit
-    for split in (0, 2):  # (2: already the segments beyond the first, 2048-point kernel split)
+    for split in (0, 2):  # (auto = 3 here: already the segments beyond the first kernel split; 2: those beyond the LDS kernels)
         e = loam.Engine(loam.default_config(ring_model=loam.RING_LINEAR, **kw))
         e.set_tuning(vg_split=split)
         e.batch_upload(prevs, curs)

@@ -243,7 +243,7 @@ def _share_run(loam, sg, **tune):
     {"graph": 1},                            # the step captured as a HIP graph and replayed
     {"mp_fused_max": 0, "mp_iter_wide_max": 128},  # k_mp_iter<1024>
     {"vg_merge": 0},                         # the cube VoxelGrid cascade alone (no k_vg_merge)
-    {"vg_split": 2},                         # stack segments beyond 2048 points split into key-range buckets
+    {"vg_split": 3},                         # stack segments beyond 2048 points split into key-range buckets
     {"vg_split": 0},                         # ... none split (k_vg_big beyond the LDS kernels)
     {"od_sel_min": 1024},                    # TransformToStart inside the association wave
     {"od_win_mono": 3},                      # index-range ring windows (ring-monotone clouds)

@@ -15,4 +15,8 @@ python3 $R/tools/pmc_traffic.py $S/dfetch/f_counter_collection.csv $S/dwrite/w_c
 python3 $R/tools/trace_timeline.py $S/kt/kt_kernel_trace.csv --step-kernel k_sr_ring_fused --skip 2 > $D/timeline_batch1024.txt
 python3 $R/tools/trace_timeline.py $S/kt128/kt_kernel_trace.csv --step-kernel k_sr_ring_fused --skip 3 > $D/timeline_share128.txt
 python3 $R/tools/trace_timeline.py $S/dkt/kt_kernel_trace.csv --step-kernel k_sr_ring_fused --skip 2 > $D/timeline_config5_batch64.txt
+if [ -d $S/ckt ]; then
+  cp $S/ckt/kt_kernel_stats.csv $D/kernel_stats_chain220.csv
+  python3 $R/tools/trace_timeline.py $S/ckt/kt_kernel_trace.csv --step-kernel k_sr_ring_count --skip 8 > $D/timeline_chain220.txt
+fi
 echo "$D"
