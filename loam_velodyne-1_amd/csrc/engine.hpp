@@ -110,11 +110,6 @@ struct Tuning {
                            // iteration: O(queries) per iteration, not bit-identical, within 1e-4 of the
                            // reference on every benched problem (round 5: config 5
                            // k_od_rows 4.50 -> 2.49 ms/step, 1024 problems 1.37 -> 1.03)
-  int od_round_max = 0;    // with the moments, for P <= this: each association round's iterations as one
-                           // launch (k_od_round_mom: the problem's workgroups stay resident, the same sums;
-                           // round 6, k_od_rows per step: config 5 2.11 -> 2.02 ms, 128 problems 0.46 -> 0.42,
-                           // 1024 0.91 -> 1.52, and no step faster: the resident workgroups hold slots the
-                           // pipelined mapping would use)
   // key = value (loam_set_tuning); false for an unknown key or a value out of range.  get: the
   // current value of a key (loam_get_tuning); false for an unknown key
   bool get(const char* key, long long* v) {
@@ -136,8 +131,7 @@ struct Tuning {
                     {"pipe_mp_sets", &pipe_mp_sets, 1, 2}, {"od_sel_min", &od_sel_min, 1, 1 << 20},
                     {"od_win_mono", &od_win_mono, 0, 3}, {"od_win_mono_min", &od_win_mono_min, 1, 1 << 20},
                     {"od_moments_min", &od_moments_min, 1, 1 << 30}, {"od_persist", &od_persist, 0, 1},
-                    {"mp_persist", &mp_persist, 0, 1},
-                    {"od_round_max", &od_round_max, 0, 1 << 20}};
+                    {"mp_persist", &mp_persist, 0, 1}};
     for (const K& k : ks)
       if (std::strcmp(key, k.n) == 0) {
         if (read) {

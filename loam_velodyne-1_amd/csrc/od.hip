@@ -1869,146 +1869,6 @@ int od_lm_stream_grid(int cap_q) {
   return 2 * G <= cap[dev] ? G : 0;  // (a margin of 2: other streams' kernels may hold slots a while)
 }
 
-// ---- batches with the per-query moments: one association round's iterations in one launch ----
-__global__ void k_od_round_mom(OdBuffers b, FeatView f, int last_buf, int it0);
-// k_od_round_mom's workgroups that can be resident at once (a problem's gq must fit, with a margin)
-static int od_round_capacity() {
-  static int cap[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (cap[dev] == 0) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_od_round_mom, kOdThreads, 0) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      per_cu = cus = 0;
-    cap[dev] = std::max(1, per_cu * cus);
-  }
-  return cap[dev];
-}
-// k_od_rows_mom<FUSED> is one launch per iteration (its workgroups' partials summed by the last to
-// arrive, which runs the step): ~20-25 µs per iteration at 64-128 problems, most of it the launch and
-// the hand-off, 100 iterations per sweep at config 5.  Here the gq workgroups of a problem stay
-// resident for the round's (up to) five iterations: each keeps its queries' moments and associated
-// points in registers, publishes its partial per iteration (write-through, then a publication word),
-// reads the problem's gq partials in workgroup order — k_od_rows_mom<true>'s order, so the same
-// sums — and runs the step on its own copy of the problem's state (od_step_ls: the same values in
-// every workgroup of the problem).  Workgroups take tickets in launch order (rm_ctr, zeroed with the
-// publication words before each launch), so a problem's workgroups hold consecutive tickets and
-// every workgroup a waiting one needs has started: only the last problem under way can be short of
-// workgroups, and the others finish and free their slots (k_sr_ring_fused's argument).
-__global__ __launch_bounds__(kOdThreads) __attribute__((amdgpu_waves_per_eu(kOdRowsWpe))) void k_od_round_mom(OdBuffers b, FeatView f, int last_buf, int it0) {
-  __shared__ int sh_ticket;
-  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6, gq = b.gq;
-  if (tid == 0) sh_ticket = atomicAdd(b.rm_ctr, 1);
-  __syncthreads();
-  const int p = sh_ticket / gq, g = sh_ticket % gq;
-  if (p >= b.P) return;
-  int* ist = b.istate + (size_t)p * kOdStateInts;
-  float* st = b.state + (size_t)p * kOdStateFloats;
-  if (!ist[kIsActive] || ist[kIsStop]) return;  // (the same for every workgroup of the problem)
-  __shared__ double red[kOdWaves][28], tot[28];
-  __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs], jE[6], jV[36];
-  __shared__ int lm_iws[12];
-  __shared__ OdLsState S;
-  if (tid < 6) S.T[tid] = st[tid];
-  if (tid < 36) S.matP[tid] = st[kOdMatP + tid];
-  if (tid == 0) {
-    S.degen = ist[kIsDegenerate];
-    S.iters = ist[kIsIters];
-    S.assoc = ist[kIsAssoc];
-    S.rows = ist[kIsRows];
-    S.deg_steps = ist[kIsDegSteps];
-    S.nan_skips = ist[kIsNanSkips];
-    S.stop = 0;
-  }
-  const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
-  const int q = g * kOdThreads + tid;
-  double* mq = b.mom + (size_t)p * kOdMom * b.cap_q + q;  // [P][kOdMom][cap_q]
-  double m[kOdMom];
-#pragma unroll
-  for (int k = 0; k < kOdMom; ++k) m[k] = it0 > 0 && q < nq ? mq[(size_t)k * b.cap_q] : 0.0;
-  // the query's raw point and its round's associated points (od_assoc_pts; t1.w: the association holds)
-  float4 po = make_float4(0, 0, 0, 0), t1 = po, t2 = po, t3 = po;
-  if (q < nq) {
-    po = q < nc ? f.sharp[(size_t)p * f.sharp_stride + q] : f.flat[(size_t)p * f.flat_stride + (q - nc)];
-    const bool has = od_assoc_pts(b, p, q, nc, (size_t)last_buf * b.P + p, t1, t2, t3);
-    t1.w = has ? 1.0f : 0.0f;
-  }
-  __syncthreads();
-  if (tid < 6) S.trig[tid] = (float)((tid & 1) ? dcos(S.T[tid >> 1]) : dsin(S.T[tid >> 1]));
-  __syncthreads();
-  const int it1 = min(it0 + 5, b.max_iter);
-  for (int it = it0; it < it1; ++it) {
-    float T[6], trig[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) { T[k] = S.T[k]; trig[k] = S.trig[k]; }
-    double acc[28];
-#pragma unroll
-    for (int k = 0; k < 28; ++k) acc[k] = 0.0;
-    if (q < nq) {
-      float4 cf;
-      int ok;
-      od_coeff_from(it, T, po, q < nc, t1.w != 0.0f, t1, t2, t3, cf, ok);
-      od_mom_add(m, cf);
-      od_mom_accum(od_jfactors(trig, T, po), m, acc);
-    }
-    wave_reduce_scatter_28(acc);
-    if ((lane & 1) == 0 && (lane >> 1) < 28) red[w][lane >> 1] = acc[0];
-    __syncthreads();
-    const int par = it & 1;
-    double* pp = b.rm_part + ((size_t)par * b.P + p) * gq * 28;
-    if (tid < 28) {  // this workgroup's partial, waves in order (k_od_rows_mom's), stored write-through
-      double v = red[0][tid];
-      for (int ww = 1; ww < kOdWaves; ++ww) v += red[ww][tid];
-      store_partial(&pp[(size_t)g * 28 + tid], v);
-    }
-    if (tid < 64) {
-      __builtin_amdgcn_wave_barrier();  // (every lane's store drained: store_partial waits for it)
-      if (tid == 0) __hip_atomic_store(&b.rm_flag[p * gq + g], it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (tid < gq)
-      while (__hip_atomic_load(&b.rm_flag[p * gq + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < it + 1)
-        __builtin_amdgcn_s_sleep(1);
-    __syncthreads();
-    if (tid < 28) {  // k_od_rows_mom<true>'s fixed order over the workgroups
-      double v = 0.0;
-      for (int g0 = 0; g0 < gq; g0 += 8) {
-        double t[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          t[u] = g0 + u < gq ? __hip_atomic_load(&pp[(size_t)(g0 + u) * 28 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                             : 0.0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (g0 + u < gq) v += t[u];
-      }
-      tot[tid] = v;
-    }
-    __syncthreads();
-    if (tid < 64) od_step_ls(it, tot, S, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
-    __syncthreads();
-    if (S.stop) break;
-    if (tid < 6) S.trig[tid] = (float)((tid & 1) ? dcos(S.T[tid >> 1]) : dsin(S.T[tid >> 1]));
-    __syncthreads();
-  }
-  if (q < nq)
-#pragma unroll
-    for (int k = 0; k < kOdMom; ++k) mq[(size_t)k * b.cap_q] = m[k];
-  if (g == 0) {  // the problem's state for the next round / the kernels after the loop
-    if (tid < 6) st[tid] = S.T[tid];
-    if (tid < 36) st[kOdMatP + tid] = S.matP[tid];
-    if (tid == 0) {
-      ist[kIsDegenerate] = S.degen;
-      ist[kIsIters] = S.iters;
-      ist[kIsAssoc] = S.assoc;
-      ist[kIsRows] = S.rows;
-      ist[kIsDegSteps] = S.deg_steps;
-      ist[kIsNanSkips] = S.nan_skips;
-      ist[kIsStop] = S.stop;
-    }
-  }
-}
-
 // the step as its own launch (large batches): one wave per problem
 __global__ __launch_bounds__(64) void k_od_step(OdBuffers b, int iter, int gq) {
   const int p = blockIdx.x, lane = threadIdx.x;
@@ -2291,9 +2151,6 @@ hipError_t od_alloc(OdBuffers& b, int P, int R, int cap_pts, int max_iter) {
   A(&b.part, (size_t)P * b.gq * max_iter * 28 * sizeof(double));  // (k_od_rows_small: per stored iteration)
   A(&b.done, (size_t)P * sizeof(int));
   A(&b.ls_part, (size_t)2 * kOdLsMaxG * 28 * sizeof(double));
-  A(&b.rm_part, (size_t)2 * P * b.gq * 28 * sizeof(double));
-  A(&b.rm_ctr, (size_t)(1 + P * b.gq) * sizeof(int));
-  b.rm_flag = b.rm_ctr + 1;
   A(&b.ls_flag, (size_t)kOdLsMaxG * sizeof(unsigned long long));
   A(&b.ls_epoch, sizeof(unsigned long long));
   A(&b.mono, (size_t)kOdBufs * P * 2 * sizeof(int));
@@ -2324,7 +2181,7 @@ void od_free(OdBuffers& b) {
   void* ptrs[] = {b.state_set[0], b.state_set[1], b.state_set[2], b.istate_set[0], b.istate_set[1], b.istate_set[2], b.lastC, b.lastS, b.fullEnd, b.nlast, b.nfullEnd, b.hC_start,
                   b.hS_start, b.hC_fill, b.hS_fill, b.hC_pts, b.hS_pts, b.hC_T, b.hS_T, b.cC, b.cS,
                   b.ind, b.sel, b.q_cf, b.q_ok, b.mom, b.qa, b.part, b.done, b.mono, b.rstart, b.fC, b.fS,
-                  b.ls_part, b.ls_flag, b.ls_epoch, b.rm_part, b.rm_ctr};
+                  b.ls_part, b.ls_flag, b.ls_epoch};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   b = OdBuffers();
@@ -2428,15 +2285,6 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
       if (lm_round) {  // the round's iterations in one workgroup per problem
         hipLaunchKernelGGL(k_od_lm, dim3(P), dim3(kOdLmThreads), od_lm_lds(b.cap_q), st, b, f, last_buf, it);
         mark("k_od_lm");
-        it += 4;
-        continue;
-      }
-      // batches with the moments: the round's iterations in one launch (k_od_round_mom)
-      if (P > tn.od_small_max && P >= tn.od_moments_min && P <= tn.od_round_max && b.gq <= kOdThreads &&
-          2 * b.gq <= od_round_capacity()) {
-        (void)hipMemsetAsync(b.rm_ctr, 0, (size_t)(1 + P * b.gq) * sizeof(int), st);  // (ticket + words)
-        hipLaunchKernelGGL(k_od_round_mom, dim3(b.gq * P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
-        mark("k_od_rows");
         it += 4;
         continue;
       }

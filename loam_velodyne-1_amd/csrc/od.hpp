@@ -131,11 +131,6 @@ struct OdBuffers {
   double* ls_part = nullptr;              // [2][kOdLsMaxG][28]
   unsigned long long* ls_flag = nullptr;  // [kOdLsMaxG]
   unsigned long long* ls_epoch = nullptr; // [1]
-  // the per-round moments kernel (k_od_round_mom): per iteration parity, problem and workgroup its
-  // partial; the launch's ticket counter followed by the per-(problem, workgroup) publication words
-  double* rm_part = nullptr;  // [2][P][gq][28]
-  int* rm_ctr = nullptr;      // [1 + P * gq]: rm_ctr[0] the ticket counter, rm_flag = rm_ctr + 1
-  int* rm_flag = nullptr;
   int* mono = nullptr;        // [kOdBufs][P][2] Last corner / surf of each buffer ring-monotone (HashJob::mono)
   int* rstart = nullptr;      // [kOdBufs][P][2][kRingTab] their ring start tables (HashJob::rstart)
   Tuning tune;                // host-side launch choices (od_solve)

@@ -148,13 +148,10 @@ def test_config5_batch_parity(loam, oc, sg):
     np.testing.assert_array_equal(aft, aft2)
     e.close()
     # the surf stacks beyond the LDS VoxelGrid kernels through k_vg_big instead of the key-range split
-    # (tuning vg_split, k_vg_split / k_vg_join; auto = 3 here: already the segments beyond the first
-    # kernel split, 2: those beyond the LDS kernels), and the odometry's moments as one launch per
-    # association round instead of one per iteration (od_round_max: k_od_round_mom, not
-    # k_od_rows_mom): the same poses and iterations bit for bit
-    for tune in ({"vg_split": 0}, {"vg_split": 2}, {"od_round_max": P}):
+    # (tuning vg_split, k_vg_split / k_vg_join): the same poses and iterations bit for bit
+    for split in (0, 2):  # (auto = 3 here: already the segments beyond the first kernel split; 2: those beyond the LDS kernels)
         e = loam.Engine(loam.default_config(ring_model=loam.RING_LINEAR, **kw))
-        e.set_tuning(**tune)
+        e.set_tuning(vg_split=split)
         e.batch_upload(prevs, curs)
         e.batch_run()
         od3, aft3, st3 = e.batch_download()

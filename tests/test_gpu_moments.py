@@ -124,14 +124,13 @@ def test_moments_8gpu_share_fused(loam, oc, sg):
     assert np.abs(od - od_o).max() <= TOL and np.abs(aft - aft_o).max() <= TOL
 
 
-@pytest.mark.parametrize("tune", [{"od_round_max": 1024}, {"od_fused_max": 0},
-                                  {"step_pipe": 0, "sr_ahead": 0}, {"graph": 1}, {"od_rows_deep_max": 128}],
+@pytest.mark.parametrize("tune", [{"od_fused_max": 0}, {"step_pipe": 0, "sr_ahead": 0}, {"graph": 1},
+                                  {"od_rows_deep_max": 128}],
                          ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_moments_launch_choices_at_8gpu_share(loam, sg, tune):
-    """the moments' launch choices compute the same sums in the same order: a launch per iteration
-    with the step in the last workgroup (k_od_rows_mom<true>, the default) or as k_od_step, an
-    association round per launch (k_od_round_mom), sequential and pipelined steps, a graph replay give
-    the default's poses bit for bit (the moments run at P >= od_moments_min = 64)"""
+    """the moments' launch choices compute the same sums in the same order: the fused rows kernel
+    (step in the last workgroup) and k_od_rows + k_od_step, sequential and pipelined steps, a graph
+    replay give the default's poses bit for bit (the moments run at P >= od_moments_min = 64)"""
     P, r = 128, 7
     prevs, curs = sg.batch_problems(P, base_seed=1000 + r * P)
 
