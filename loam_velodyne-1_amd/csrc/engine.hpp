@@ -179,6 +179,8 @@ struct SrBuffers {
   int* cnt = nullptr;        // [S][4]: sharp, less_sharp, flat, less_flat
   int* err = nullptr;        // [S]
   int* sel_big = nullptr;    // [S] selection kernel that handles the sweep (0 fast, 1 4096 LDS, 2 global)
+  int* sel_list = nullptr;   // [2 + 2S] the sweeps routed to k_sr_select<4096, 1> / <16, 2>: counts at [0] / [1]
+                             // (zeroed by k_sr_features), sweep indices at [2, 2 + S) / [2 + S, 2 + 2S)
   int* st_loff = nullptr;    // [S][R] offset of each ring's lessFlat in the sweep's st_lflat block
   uint64_t* big_keys = nullptr;  // [kBigSlots][big_stride] ring state of the global-memory selection
   int* big_sidx = nullptr;

@@ -661,6 +661,7 @@ constexpr int kFeatSpan = kFeatTile * kFeatE;
 
 __global__ __launch_bounds__(kFeatTile) void k_sr_features(SrBuffers b, SrParams p) {
   const int s = blockIdx.y, tid = threadIdx.x;
+  if ((blockIdx.x | blockIdx.y) == 0 && tid < 2) b.sel_list[tid] = 0;  // (the selection's routing lists)
   const int n = b.n_full[s];
   const int i0 = blockIdx.x * kFeatSpan;
   if (i0 >= n) return;
@@ -743,8 +744,8 @@ __global__ __launch_bounds__(kFeatTile) void k_sr_features(SrBuffers b, SrParams
     }
     b.curv[gi] = cv;
     b.picked[gi] = (uint8_t)(pk | (gap << 1));
-    b.sortind[gi] = i;
-    b.label[gi] = 0;
+    // (sortInd = identity and labels 0 are implied: the selection's walk of dependent rings, the
+    // one reader of the arrays, initialises them itself, sel_init)
   }
 }
 
@@ -1287,7 +1288,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
     lab = sh.lab;
     for (int k = wlo + tid; k <= whi; k += kSelThreads) {
       pk[k - wlo] = b.picked[(size_t)s * b.cap + k];
-      lab[k - wlo] = SIDX ? b.label[(size_t)s * b.cap + k] : 0;  // labels start at 0 (k_sr_features)
+      lab[k - wlo] = SIDX && seq ? b.label[(size_t)s * b.cap + k] : 0;  // labels start at 0 (sel_init)
     }
   }
   int segb[7];
@@ -1308,7 +1309,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
   for (int t = tid; t < P2; t += kSelThreads) {
     uint64_t key = ~0ull;
     if (t < len) {
-      const int v = SIDX ? b.sortind[(size_t)s * b.cap + lo + t] : lo + t;
+      const int v = SIDX && seq ? b.sortind[(size_t)s * b.cap + lo + t] : lo + t;
       if (SIDX) sidx[t] = v;
       int seg = 0;
 #pragma unroll
@@ -1447,6 +1448,7 @@ LOAM_D void select_ring(const SrBuffers& b, int s, int q, int R, int n, bool seq
 // VoxelGrid runs at full workgroup occupancy.  Other sweeps fall to k_sr_select<4096, 1> / <16, 2>
 // exactly as before (sel_big).
 constexpr int kPickCap = 2048;
+constexpr int kSelListGrid = 32;  // k_sr_select<4096, 1> workgroup rows over its listed sweeps
 // rings (waves) per k_sr_pick workgroup: one, so a workgroup's LDS is freed as soon as its own ring's
 // greedy walk ends (k_sr_select ms/step at batch 1024: 4 -> 1.67-1.69, 2 -> 1.66, 1 -> 1.63-1.65)
 constexpr int kPickWaves = 1;
@@ -1509,7 +1511,10 @@ __global__ __launch_bounds__(64 * kPickWaves) __attribute__((amdgpu_waves_per_eu
   const int route = sweep_route(b, s, R, n, kPickCap, se, order);
   if (tid == 0) {
     sh_route = route;
-    if (blockIdx.x == 0) b.sel_big[s] = route;
+    if (blockIdx.x == 0) {
+      b.sel_big[s] = route;
+      if (route) b.sel_list[2 + atomicAdd(&b.sel_list[0], 1)] = s;  // (k_sr_select<4096, 1>'s sweeps)
+    }
   }
   __syncthreads();
   if (sh_route != 0 || q >= R) return;  // wave-uniform from here on: no workgroup barrier below
@@ -1603,6 +1608,18 @@ __global__ __launch_bounds__(kSelThreads) void k_sr_ringvg(SrBuffers b, SrParams
   if (tid == 0) b.st_cnt[(size_t)(s * R + q) * 4 + 3] = nout;
 }
 
+// sortInd = identity and labels 0 over sweep s (the workgroup), before a walk of dependent rings
+// reads and writes them back ring by ring (k_sr_features leaves them unwritten: the common path,
+// independent rings, never reads them)
+LOAM_D void sel_init(const SrBuffers& b, int s, int n) {
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    b.sortind[(size_t)s * b.cap + k] = k;
+    b.label[(size_t)s * b.cap + k] = 0;
+  }
+  __threadfence_block();
+  __syncthreads();
+}
+
 // Three instantiations, chosen per sweep: CAP = 2048 (34 KB of LDS, four workgroups per CU)
 // takes every sweep whose rings are independent and no longer than 2048 points (VLP-16,
 // HDL-64E) and flags the others (sel_big = 1); CAP = 4096 redoes those whose spans fit it, rings
@@ -1614,7 +1631,12 @@ __global__ __launch_bounds__(kSelThreads) __attribute__((amdgpu_waves_per_eu(MOD
   const int tid = threadIdx.x, R = p.R;
   constexpr bool SIDX = MODE != 0;  // MODE 0 takes independent rings only
   __shared__ SelShared<CAP, SIDX> sh;
-  for (int s = BIG ? blockIdx.x : blockIdx.y; s < b.S; s += BIG ? gridDim.x : b.S) {
+  // MODE 1 / 2: the sweeps k_sr_pick / MODE 1 routed here (sel_list), gridDim.y / gridDim.x workgroups
+  // (of R rings / one) over them; MODE 0: sweep blockIdx.y
+  const int nlist = MODE == 0 ? b.S : b.sel_list[MODE - 1];
+  const int* list = b.sel_list + 2 + (MODE == 2 ? b.S : 0);
+  for (int i = BIG ? blockIdx.x : blockIdx.y; i < nlist; i += BIG ? gridDim.x : gridDim.y) {
+    const int s = MODE == 0 ? i : list[i];
     const int q = BIG ? 0 : blockIdx.x;
     if (MODE != 0 && b.sel_big[s] != MODE) continue;
     const int n = b.n_full[s];
@@ -1650,7 +1672,10 @@ __global__ __launch_bounds__(kSelThreads) __attribute__((amdgpu_waves_per_eu(MOD
       if (MODE == 0 && n > 0 && (!wf || maxspan > CAP)) next = 1;
       if (MODE == 1 && n > 0 && maxspan > CAP) next = 2;
       sh.big = next != MODE;
-      if (q == 0 && MODE != 2) b.sel_big[s] = next;
+      if (q == 0 && MODE != 2) {
+        b.sel_big[s] = next;
+        if (MODE == 1 && next == 2) b.sel_list[2 + b.S + atomicAdd(&b.sel_list[1], 1)] = s;
+      }
     }
     __syncthreads();
     if (!sh.big) {
@@ -1660,12 +1685,14 @@ __global__ __launch_bounds__(kSelThreads) __attribute__((amdgpu_waves_per_eu(MOD
       } else if (sh.wf && !BIG) {
         select_ring<CAP, BIG, SIDX>(b, s, q, R, n, false, sh, 0);
       } else if (q == 0) {
-        if constexpr (SIDX)
+        if constexpr (SIDX) {
+          sel_init(b, s, n);
           for (int r = 0; r < R; ++r) select_ring<CAP, BIG, SIDX>(b, s, r, R, n, true, sh, BIG ? blockIdx.x : 0);
+        }
       }
     }
     __syncthreads();
-    if (!BIG) break;
+    if (MODE == 0) break;
   }
 }
 
@@ -1750,6 +1777,7 @@ hipError_t sr_alloc(SrBuffers& b, int S, int cap, int R) {
   A(&b.cnt, (size_t)S * 4 * sizeof(int));
   A(&b.err, S * sizeof(int));
   A(&b.sel_big, S * sizeof(int));
+  A(&b.sel_list, (2 + 2 * (size_t)S) * sizeof(int));
   A(&b.st_loff, (size_t)S * R * sizeof(int));
   b.big_stride = next_pow2(cap);
   A(&b.big_keys, (size_t)kBigSlots * b.big_stride * sizeof(uint64_t));
@@ -1762,7 +1790,7 @@ hipError_t sr_alloc(SrBuffers& b, int S, int cap, int R) {
 void sr_free(SrBuffers& b) {
   void* ptrs[] = {b.raw, b.raw_n, b.tmp_ori, b.tmp_sid, b.tilecnt, b.tileF, b.ring_sync, b.sweep_ori, b.full, b.n_full, b.curv,
                   b.picked, b.sortind, b.label, b.ring_se, b.st_sharp, b.st_lsharp, b.st_flat,
-                  b.st_lflat, b.st_cnt, b.st_cand, b.st_ncand, b.sharp, b.lsharp, b.flat, b.lflat, b.cnt, b.err, b.sel_big, b.st_loff, b.big_keys, b.big_sidx, b.big_cand};
+                  b.st_lflat, b.st_cnt, b.st_cand, b.st_ncand, b.sharp, b.lsharp, b.flat, b.lflat, b.cnt, b.err, b.sel_big, b.sel_list, b.st_loff, b.big_keys, b.big_sidx, b.big_cand};
   for (void* q : ptrs)
     if (q) HIPCHK(hipFree(q));
   b = SrBuffers();
@@ -1816,7 +1844,9 @@ void sr_launch(const SrBuffers& b, const SrParams& p, hipStream_t st, Prof* prof
   mark("k_sr_features");
   hipLaunchKernelGGL(k_sr_pick, dim3((b.R + kPickWaves - 1) / kPickWaves, b.S), dim3(64 * kPickWaves), 0, st, b, p);
   hipLaunchKernelGGL(k_sr_ringvg, dim3(b.R, b.S), dim3(kSelThreads), LOAM_RINGVG_PAD, st, b, p);
-  hipLaunchKernelGGL((k_sr_select<kRingCap, 1>), dim3(b.R, b.S), dim3(kSelThreads), 0, st, b, p);
+  // (the sweeps k_sr_pick routed on, from its list: a sweep with an empty ring or a ring beyond
+  // kPickCap points; a small grid when there are none)
+  hipLaunchKernelGGL((k_sr_select<kRingCap, 1>), dim3(b.R, std::min(b.S, kSelListGrid)), dim3(kSelThreads), 0, st, b, p);
   hipLaunchKernelGGL((k_sr_select<16, 2>), dim3(kBigSlots), dim3(kSelThreads), 0, st, b, p);
   mark("k_sr_select");
   hipLaunchKernelGGL(k_sr_compact, dim3(b.R, b.S), dim3(256), 0, st, b, p);

@@ -88,6 +88,40 @@ def test_sr_long_rings(loam, oc, sg):
         _cmp_cloud(fg[k], fo[k], k)
 
 
+def test_sr_batch_selection_routes(loam, oc, sg):
+    """A batch whose sweeps take every selection route at once, more of them than the fallback
+    kernels' workgroup rows (sr.hip kSelListGrid): problems with an empty ring (dependent rings,
+    k_sr_select<4096, 1>), two sweeps per message (3600-point rings, the same kernel) and both
+    (a predecessor spanning two long rings, past 4096 points: k_sr_select<16, 2>), between plain
+    ones (k_sr_pick / k_sr_ringvg).  Every problem's poses against the oracle."""
+    P = 48
+    prevs, curs = sg.batch_problems(P + 1, base_seed=3000)
+
+    def drop_ring(a):
+        elev = np.degrees(np.arctan2(a[:, 2], np.hypot(a[:, 0], a[:, 1])))
+        return a[np.abs(elev - 3.0) > 0.5]
+
+    bp, bc = [], []
+    for i in range(P):
+        p, c = prevs[i], curs[i]
+        if i % 4 in (1, 3):  # two sweeps per message
+            p, c = np.concatenate([prevs[i + 1], p]), np.concatenate([p, c])
+        if i % 4 in (0, 3):
+            p, c = drop_ring(p), drop_ring(c)
+        bp.append(p)
+        bc.append(c)
+    kw = dict(max_points=80000)
+    e = loam.Engine(loam.default_config(**kw))
+    e.batch_upload(bp, bc)
+    e.batch_run()
+    od, aft, _ = e.batch_download()
+    e.close()
+    ocfg = oc.default_config(**kw)
+    for i in range(P):
+        od_o, aft_o, _ = oc.problem(bp[i], bc[i], ocfg)
+        assert max(np.abs(od[i] - od_o).max(), np.abs(aft[i] - aft_o).max()) <= POSE_TOL, i
+
+
 @pytest.mark.parametrize("model", ["vlp16", "linear64"])
 def test_sr_ring_boundaries(loam, oc, sg, model):
     """Every third point moved to within 1e-7..3e-3 degrees of a ring boundary: the engine's float
