@@ -6,7 +6,7 @@ R="$(cd "$(dirname "$0")/.." && pwd)"
 S=$R/gpurun_out/prof_$1
 D=$R/profiles/$2
 mkdir -p $D
-cp $S/bench.json $D/bench.json
+[ -f $S/bench.json ] && cp $S/bench.json $D/bench.json
 cp $S/kt/kt_kernel_stats.csv $D/kernel_stats_batch1024.csv
 cp $S/kt128/kt_kernel_stats.csv $D/kernel_stats_share128.csv
 cp $S/dkt/kt_kernel_stats.csv $D/kernel_stats_config5_batch64.csv
