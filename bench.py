@@ -59,7 +59,7 @@ def shard(rank, world, batch, split, global_batch):
 def kernel_bytes(st):
     """Bytes each kernel moves over one step of the whole batch, split by the kernel that moves them
     (DESIGN.md §4).  Streaming kernels: the algorithmic bytes of SURVEY.md §8(d).  Search kernels
-    (k_od_assoc, k_mp_nn): the bytes they actually gather, from the engine's work counters (cells,
+    (k_od_assoc, k_mp_nnfit): the bytes they actually gather, from the engine's work counters (cells,
     candidates, window points, chunk boxes), since their cost is the search, not the algorithmic
     16 B per query."""
     feats = 16 * (st["n_sharp"] + st["n_less_sharp"] + st["n_flat"] + st["n_less_flat"])
@@ -77,12 +77,6 @@ def kernel_bytes(st):
         # st["od_moments"]) the query point (16 B) and its ten fp64 moments read and written (160 B)
         "k_od_rows": (176 * st["od_query_iters"] if st.get("od_moments")
                       else 17 * st["od_row_evals"] + 33 * st["od_query_iters"]),
-        # per query-iteration: stack point read, ordered 5-NN written and last iteration's read
-        # (16 + 32 + 32 B); 8 B per bucket range and 16 B per map point evaluated (seeds included)
-        "k_mp_nn": 80 * st["mp_stack_iters"] + 8 * st["mp_nn_cells"] + 16 * st["mp_nn_candidates"],
-        # per query-iteration: 5-NN read (32 B), stack point (16 B), stored fit (64 B), row
-        # written (17 B); per refit: 5 neighbours (80 B) and the fit written (64 B)
-        "k_mp_fit": 129 * st["mp_stack_iters"] + 144 * st["mp_fits"],
         # per query-iteration: accept flag, stack point and coefficient read back for JtJ
         "k_mp_iter": 33 * st["mp_stack_iters"],
         # the search and the fit in one launch, one 64-B record per query (last 5-NN + its fit): per
@@ -96,21 +90,18 @@ def kernel_bytes(st):
     }
 
 
-SEARCH_KERNELS = ("k_mp_nn", "k_mp_nnfit", "k_od_assoc")
+SEARCH_KERNELS = ("k_mp_nnfit", "k_od_assoc")
 
 
 def algorithmic_bytes(st):
     """SURVEY.md §8(d)'s algorithmic bytes per kernel and step: what the kernel must read and write
     at minimum.  Equal to kernel_bytes for the streaming kernels.  The search and mapping L-M
     kernels are priced by B_MP's / B_OD's per-unit terms, not by the candidates the search visits or
-    the engine's own caches (the MpFit record): k_mp_nn = per query-iteration the stack point and
-    its 5 neighbours (16 + 80 B); k_mp_fit = per accepted row 64 B (the row written and read back,
-    B_MP's 64 r_k); k_mp_nnfit = both (96 B per query-iteration + 64 B per row; the mapping rows'
-    counter mp_rows_sum); k_mp_iter's row reads are part of those 64 B, so it is not priced on its
+    the engine's own caches (the MpFit record): k_mp_nnfit = per query-iteration the stack point and
+    its 5 neighbours (16 + 80 B) and per accepted row 64 B (the row written and read back, B_MP's
+    64 r_k; the mapping rows' counter mp_rows_sum); k_mp_iter's row reads are part of those 64 B, so it is not priced on its
     own; k_od_assoc = per association round every Last point once (16 B (C + S), B_OD)."""
     alg = dict(kernel_bytes(st))
-    alg["k_mp_nn"] = 96 * st["mp_stack_iters"]
-    alg["k_mp_fit"] = 64 * st["mp_rows_sum"]
     alg["k_mp_nnfit"] = 96 * st["mp_stack_iters"] + 64 * st["mp_rows_sum"]
     alg.pop("k_mp_iter")
     alg["k_od_assoc"] = 16 * st["od_assoc_points"]
@@ -136,9 +127,9 @@ def moved_od_bytes(st):
 
 # what bounds each kernel in practice: the roofline is priced against HBM, but the
 # search kernels are limited by dependent gathers, not bandwidth
-LIMITED_BY = {"k_mp_nn": "latency (dependent gathers)", "k_od_assoc": "latency (dependent gathers)",
+LIMITED_BY = {"k_od_assoc": "latency (dependent gathers)",
               "k_mp_nnfit": "latency (dependent gathers, then the fit's VALU)",
-              "k_sr_select": "latency (serial greedy picks)", "k_mp_fit": "latency (gathers + VALU)"}
+              "k_sr_select": "latency (serial greedy picks)"}
 
 
 def load_traffic(traffic_file):

@@ -218,8 +218,7 @@ int loam_batch_lm_info(loam_ctx *ctx, int32_t *od_iters, int32_t *mp_iters, loam
 int loam_set_stream_priority(loam_ctx *ctx, int priority);
 
 /* launch-shape choices of the batch / streaming L-M loops by batch size (no reference equivalent):
- * key = one of od_small_max, od_lm_min, od_lm_max, od_fused_max, mp_small_max, mp_fused_max,
- * nn_lanes, nn_lanes_maxp, od_assoc_wg, od_rows_deep_max, nn_wg, fit_wg, nnfit_max, graph, mp_iter_wide_max,
+ * key = one of od_small_max, od_fused_max, mp_small_max, mp_fused_max, od_assoc_wg, fit_wg, graph,
  * vg_merge, vg_merge_min, vg_split, sr_ahead, sr_ahead_at, step_pipe, batch_streams, pipe_mp_sets, od_sel_min, od_win_mono,
  * od_win_mono_min, od_moments_min, od_persist, mp_persist, stream_defer, od_graph, pipe_sr_sets (loam_velodyne-1_amd/csrc/engine.hpp,
  * struct Tuning).  Every choice computes the same results bit for bit except od_moments_min (the odometry's

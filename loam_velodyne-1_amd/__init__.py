@@ -335,7 +335,7 @@ class Engine:
 
     def set_tuning(self, **kv):
         """launch-shape choices by batch size (include/loam/loam.h loam_set_tuning), e.g.
-        set_tuning(od_lm_max=128); every choice computes the same results"""
+        set_tuning(od_fused_max=0); every choice computes the same results"""
         for k, v in kv.items():
             _check(lib().loam_set_tuning(self.h, k.encode(), int(v)))
 

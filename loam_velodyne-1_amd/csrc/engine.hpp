@@ -36,26 +36,17 @@ constexpr int kSharpPerRing = 12, kLessSharpPerRing = 120, kFlatPerRing = 24;
 // path stays reachable by the parity tests and A/B measurements need no rebuild.
 struct Tuning {
   int od_small_max = 63;   // k_od_rows_small (a workgroup per (queries, stored iteration)) for P <= this
-  int od_lm_min = 1;       // k_od_lm (an association round's 5 iterations in one workgroup per problem)
-  int od_lm_max = 0;       //   for od_lm_min <= P <= od_lm_max
   int od_fused_max = 128;  // k_od_rows<true> (step in the last workgroup) for P <= this, else + k_od_step
                            // (round 4, in the step pipeline: 128 problems 2.19 -> 2.14 ms/step; 1024 slower)
   int mp_small_max = 4;    // k_mp_lm_small (5-NN + fit + rows + step in one launch) for P <= this
-  int mp_fused_max = 1 << 20;  // the fit kernel (k_mp_fit<true> / k_mp_nnfit<true>) adds the rows and runs
+  int mp_fused_max = 1 << 20;  // the fit kernel (k_mp_nnfit<true>) adds the rows and runs
                            // the step in its last workgroup for P <= this, else k_mp_iter (round 4, with
                            // k_mp_nnfit: 128 problems 3.25 -> 3.16 ms/step fused; 1024: 15.73 -> 16.32
                            // with the register reduce-scatter, 15.31 -> 15.23 with the LDS row sums)
-  int nn_lanes = 1;        // lanes per query of the batch 5-NN (1, 2, 4) ...
-  int nn_lanes_maxp = 256; //   for P <= this
   int od_assoc_wg = 0;     // k_od_assoc query waves (workgroups) per problem (batches, P >= 64; 0: the query
                            // capacity / 9, i.e. 64 for VLP-16, 256 for HDL-64E)
-  int od_rows_deep_max = 0;  // k_od_rows with 8 (not 2) stored rows' loads in flight for P <= this
-  int nn_wg = 0;           // k_mp_nn workgroups per problem (0: one pass over a VLP-16 stack)
-  int fit_wg = 0;          // k_mp_fit workgroups per problem (0: likewise)
-  int nnfit_max = 1 << 20; // k_mp_nnfit (5-NN + fit in one launch per iteration) for P <= this (round 4:
-                           // 3.32 -> 3.26-3.27 ms/step at 128, 16.02 -> 15.94 at 1024 with k_mp_iter)
+  int fit_wg = 0;          // k_mp_nnfit workgroups per problem (0: about one pass over a VLP-16 stack; <= 256)
   int graph = 0;           // loam_batch_run replays the step as a captured HIP graph
-  int mp_iter_wide_max = 0;  // k_mp_iter in 1024-thread (not 256) workgroups for P <= this
   int vg_merge = 1;        // the cubes' VoxelGrid merges an old sorted prefix with the appended tail
                            // (k_vg_merge; config 3's big cubes: 95 -> 50 us per mapping frame)
   int vg_merge_min = 12288;  // ... for segments of more than this many points
@@ -117,14 +108,10 @@ struct Tuning {
   }
   bool set(const char* key, long long v, long long* read = nullptr) {
     struct K { const char* n; int* f; long long lo, hi; };
-    const K ks[] = {{"od_small_max", &od_small_max, 0, 1 << 20}, {"stream_defer", &stream_defer, 0, 1}, {"pipe_sr_sets", &pipe_sr_sets, 2, 3}, {"od_graph", &od_graph, 0, 1}, {"od_lm_min", &od_lm_min, 1, 1 << 20},
-                    {"od_lm_max", &od_lm_max, 0, 1 << 20}, {"od_fused_max", &od_fused_max, 0, 1 << 20},
+    const K ks[] = {{"od_small_max", &od_small_max, 0, 1 << 20}, {"stream_defer", &stream_defer, 0, 1}, {"pipe_sr_sets", &pipe_sr_sets, 2, 3}, {"od_graph", &od_graph, 0, 1},
+                    {"od_fused_max", &od_fused_max, 0, 1 << 20},
                     {"mp_small_max", &mp_small_max, 0, 1 << 20}, {"mp_fused_max", &mp_fused_max, 0, 1 << 20},
-                    {"nn_lanes", &nn_lanes, 1, 4}, {"nn_lanes_maxp", &nn_lanes_maxp, 0, 1 << 20},
-                    {"od_assoc_wg", &od_assoc_wg, 0, 1024},
-                    {"od_rows_deep_max", &od_rows_deep_max, 0, 1 << 20}, {"nn_wg", &nn_wg, 0, 4096},
-                    {"fit_wg", &fit_wg, 0, 4096}, {"nnfit_max", &nnfit_max, 0, 1 << 20},
-                    {"graph", &graph, 0, 1}, {"mp_iter_wide_max", &mp_iter_wide_max, 0, 1 << 20},
+                    {"od_assoc_wg", &od_assoc_wg, 0, 1024}, {"fit_wg", &fit_wg, 0, 256}, {"graph", &graph, 0, 1},
                     {"vg_merge", &vg_merge, 0, 1}, {"vg_merge_min", &vg_merge_min, 0, 1 << 20}, {"vg_split", &vg_split, 0, 3},
                     {"sr_ahead", &sr_ahead, 0, 1 << 20}, {"sr_ahead_at", &sr_ahead_at, -1, 2},
                     {"step_pipe", &step_pipe, 0, 1 << 20}, {"batch_streams", &batch_streams, 0, 1},
@@ -139,7 +126,6 @@ struct Tuning {
           return true;
         }
         if (v < k.lo || v > k.hi) return false;
-        if (k.f == &nn_lanes && v == 3) return false;
         *k.f = (int)v;
         return true;
       }

@@ -9,13 +9,14 @@
 //                  by voxel index; equal keys keep input order) for the stacks (:693-701) and the
 //                  valid cubes (:1018-1036)
 //  k_mp_gather     FromMap = valid cubes concatenated (:674-681), then voxel-hashed (k_hash_build)
-//  k_mp_nn         one L-M iteration's 5-NN (:714-719, :821-826) for every instance at once, lane
-//                  per stack point: exact 5-NN through the 1 m hash (any point within the 1 m
-//                  acceptance radius lies in the 27 cells; cells pruned by box distance)
-//  k_mp_fit        corner PCA with the 3x3 Jacobi / surface 5x3 QR plane (reused while the ordered
-//                  5-NN is unchanged), weight -> accepted flag + coefficients (:721-877)
-//  k_mp_iter       per instance: fp64 JᵀJ / Jᵀb of the accepted rows, the 6x6 solve and
-//                  degeneracy projection on one lane, update, convergence (:879-974)
+//  k_mp_nnfit      one L-M iteration for every instance at once, lane per stack point: the exact
+//                  5-NN (:714-719, :821-826) through the 1 m hash (any point within the 1 m acceptance
+//                  radius lies in the 27 cells; cells pruned by box distance), the corner PCA with the
+//                  3x3 Jacobi / surface 5x3 QR plane (reused while the ordered 5-NN is unchanged),
+//                  weight -> accepted row (:721-877), and (fused) the fp64 JᵀJ / Jᵀb partials with
+//                  the 6x6 step in the instance's last workgroup (:879-974)
+//  k_mp_iter       the step as its own launch (tuning mp_fused_max)
+//  k_mp_lm_small / k_mp_lm_stream   the same for a few instances / one (streaming)
 //  k_mp_lm_end     transformUpdate (:199-232)
 //  k_mp_insert     stack -> cubes in stack order (:980-1016)
 //  k_mp_vcopy      per valid cube: old content ++ appended points -> DS input
@@ -1169,22 +1170,16 @@ LOAM_D void knn5(const int* start, const float4* hp, int T, float4 q, Top5& t, i
   }
 }
 
-// batch-size launch choices (k_mp_lm_small, k_mp_fit<true>, lanes per query of k_mp_nn): the
-// context's Tuning (engine.hpp), MpBuffers::tune.  (k_mp_fit<true> measured at batch 128: fit + iter
-// 0.66 -> 0.58 ms/step; at 1024 1.71 -> 2.22.)
+// batch-size launch choices (k_mp_lm_small, k_mp_nnfit<true> or + k_mp_iter): the context's Tuning
+// (engine.hpp), MpBuffers::tune
 constexpr int kMpQueryThreads = 256;
 // lanes per query in k_mp_lm_small (streaming: the per-query search chain is the latency)
 #ifndef LOAM_MP_NN_LANES
 #define LOAM_MP_NN_LANES 8  // (config 3 sequential ms/sweep: 1 -> 0.972, 2 -> 1.009, 4 -> 0.943, 8 -> 0.933)
 #endif
 constexpr int kMpNnLanes = LOAM_MP_NN_LANES;
-// k_mp_nn workgroup size (measured k_mp_nn ms/step at batch 1024: 64 -> 3.83, 128 -> 3.81-3.86,
-// 256 -> 3.92-3.95): a workgroup's LDS is released when its slowest lane is done
-#ifndef LOAM_NN_THREADS
-#define LOAM_NN_THREADS 128  // (round 3: 64 -> 3.00 / 0.648 ms/step at batch 1024 / 128, 128 -> 3.03 / 0.652)
-#endif
-constexpr int kMpNnThreads = LOAM_NN_THREADS;
-// k_mp_fit workgroup size (ms/step at batch 1024: 256 -> 1.27-1.29, 128 -> 1.16-1.20, 64 -> 1.17)
+// k_mp_nnfit workgroup size: one wave (round 3's fit kernel, ms/step at batch 1024: 256 -> 1.27-1.29,
+// 128 -> 1.16-1.20, 64 -> 1.17)
 constexpr int kMpFitThreads = 64;
 
 // The same search with the lane's work flattened: first every cell the lane may need (box
@@ -1201,9 +1196,6 @@ constexpr int kNnInFlight = LOAM_NN_INFLIGHT;
 #define LOAM_NN_LIST 27  // k_mp_nn list entries per lane (non-empty cells beyond it: the unlisted search)
 #endif
 constexpr int kNnListCap = LOAM_NN_LIST;
-#ifndef LOAM_NN_WPE
-#define LOAM_NN_WPE 5  // k_mp_nn waves per SIMD
-#endif
 // cells whose bucket-range loads are in flight together
 #ifndef LOAM_NN_RANGE_GROUP
 #define LOAM_NN_RANGE_GROUP 27  // one-word records: all 27 in flight (ms/step: 9 -> 3.11, 27 -> 3.04; 8-byte pairs: 1 -> 3.83, 9 -> 3.51)
@@ -1358,8 +1350,8 @@ __global__ void k_mp_lm_begin(MpBuffers b) {
 }
 
 // One L-M iteration's correspondences (:714-877), lane per stack point (corner, then surf), in
-// per-query pieces shared by the batch kernels (k_mp_nn, k_mp_fit, k_mp_iter: one launch each) and
-// the small-batch kernel (k_mp_lm_small: all three and the step in one launch).
+// per-query pieces shared by the batch kernel (k_mp_nnfit) and the small-batch / streaming kernels
+// (k_mp_lm_small, k_mp_lm_stream).
 //   mp_nn_query   the point at the current TobeMapped pose and its exact 5-NN (seeded with the
 //                 previous iteration's), stored in q_nn
 //   mp_fit_query  the line (corner PCA, 3x3 Jacobi) or plane (5x3 QR) through the 5 neighbours and
@@ -1681,45 +1673,7 @@ LOAM_D void mp_step(const MpBuffers& b, int p, const double* tot, MpStepScratch&
 }
 }  // namespace
 
-// batch kernels.  k_mp_nn: small and register-light so many waves hide the gather latency; five
-// waves per SIMD (<= 96 VGPRs; the LDS lists allow five workgroups per CU).  COUNT: the profiling
-// variant that also sums its work (candidates, bucket ranges) into the frame's istate
-template <bool COUNT, int L>
-__global__ __launch_bounds__(kMpNnThreads) __attribute__((amdgpu_waves_per_eu(L > 1 ? 4 : LOAM_NN_WPE))) void k_mp_nn(MpBuffers b) {
-  const XcdBlock blk = xcd_block();
-  const int p = blk.y, tid = threadIdx.x;
-  const int* ist = b.istate + (size_t)p * kMpStateInts;
-  if (!ist[kMiLmRan] || ist[kMiStop]) return;
-  const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
-  const int nq = nsc + nss;
-  __shared__ uint32_t lists[kNnListCap * kMpNnThreads];
-  uint32_t* lst = lists + tid;
-  const bool first = ist[kMiIters] == 0;
-  const loampose::MapRot r = rot_load(b, p);
-  const MpNnCtx c = mp_nn_ctx(b, p);
-  int work = 0;  // work counter (loam_stats mp_nn_candidates / mp_nn_cells), packed as in knn5
-  // L lanes per query (aligned groups): the candidates strided over the group, the partial top-5
-  // lists merged (knn5_merge); the group's first lane stores the result
-  constexpr int QPB = kMpNnThreads / L;
-  const int sub = tid % L;
-  for (int q = blk.x * QPB + tid / L; q < nq; q += gridDim.x * QPB) {
-    float4 sel;
-    Top5 t;
-    mp_nn_query<kMpNnThreads, L, kNnListCap>(b, c, q, nsc, first, r, lst, sel, t, work, sub);
-  }
-  if (!COUNT) return;
-  if (sub != 0) work = 0;  // (every lane of a group counted the group's whole list)
-  const int ncand = wave_sum(work & ((1 << kWorkCellShift) - 1)), ncell = wave_sum(work >> kWorkCellShift);
-  if (lane_id() == 0 && ncand) {
-    atomicAdd((int*)&ist[kMiNnCand], ncand);
-    atomicAdd((int*)&ist[kMiNnCells], ncell);
-  }
-}
-
-// FUSED: each lane also adds its accepted row (as k_mp_lm_small does), the workgroup's fp64 partial
-// is stored write-through, and the last workgroup of the instance sums the partials in order and
-// runs the step: no k_mp_iter launch.
-// the fused step of one-wave workgroups (k_mp_fit<true>, k_mp_nnfit<true>): the wave's row sums as
+// the fused step of one-wave workgroups (k_mp_nnfit<true>): the wave's row sums as
 // this workgroup's partial (write-through), and the last workgroup of the instance to arrive sums
 // the G partials in workgroup order and runs the step
 // red: the wave's sums reduce-scattered (wave_reduce_scatter_28: lanes 2v, 2v+1 hold value v)
@@ -1764,63 +1718,12 @@ LOAM_D void mp_store_partial_and_step(const MpBuffers& b, int p, int wg, int G, 
   if (lane == 0) b.done[p] = 0;
   mp_step(b, p, tot, sh);
 }
-LOAM_D void mp_partial_and_step(const MpBuffers& b, int p, int wg, int G, double (&acc)[28]) {
-  wave_reduce_scatter_28(acc);  // lanes 2v, 2v+1: the sum of value v
-  mp_store_partial_and_step(b, p, wg, G, acc[0]);
-}
-
-template <bool FUSED>
-__global__ __launch_bounds__(kMpFitThreads) void k_mp_fit(MpBuffers b) {
-  const XcdBlock blk = xcd_block();
-  const int p = blk.y, tid = threadIdx.x;
-  int* ist = b.istate + (size_t)p * kMpStateInts;
-  if (!ist[kMiLmRan] || ist[kMiStop]) return;
-  const bool first = ist[kMiIters] == 0;  // fits of an earlier frame are stale
-  // per-lane 3x3 Jacobi scratch (27 words; the odd stride keeps lanes on distinct banks): 27 KB,
-  // five workgroups per CU (33-word rows allowed four; measured 1.56 -> 1.40 ms per step)
-  __shared__ float jac[kMpFitThreads][27];
-  const int nsc = b.sseg_cnt[p * 2 + 0], nss = b.sseg_cnt[p * 2 + 1];
-  const int nq = nsc + nss;
-  const float4* stack = b.stack + (size_t)p * b.cap_stack;
-  const int4* qnn = b.q_nn + (size_t)p * b.cap_stack * 2;
-  int8_t* qok = b.q_ok + (size_t)p * b.cap_stack;
-  float4* qcf = b.q_cf + (size_t)p * b.cap_stack;
-  const loampose::MapRot r = rot_load(b, p);
-  float* jw = jac[tid];
-  int nfits = 0;
-  double acc[FUSED ? 28 : 1];
-  const MpTrig tg = mp_trig_of(r);
-  if constexpr (FUSED) {
-#pragma unroll
-    for (int k = 0; k < 28; ++k) acc[k] = 0.0;
-  }
-  for (int q = blk.x * kMpFitThreads + tid; q < nq; q += gridDim.x * kMpFitThreads) {
-    const bool corner = q < nsc;
-    const int4 n0 = qnn[2 * q], n1 = qnn[2 * q + 1];
-    float4 sel = make_float4(0, 0, 0, 0), o = sel;
-    if (n1.x != 0x7fffffff && D(__int_as_float(n1.y)) < 1.0) {  // (a row needs a fit: ok implies this)
-      o = stack[corner ? q : b.capC + (q - nsc)];
-      sel = loampose::point_to_map(r, o);
-    }
-    float4 cf;
-    int ok;
-    mp_fit_query(b, p, q, nsc, first, n0, n1, sel, jw, nfits, cf, ok);
-    qok[q] = (int8_t)ok;
-    qcf[q] = cf;
-    if constexpr (FUSED)
-      if (ok) mp_row_accum(tg, o, cf, acc);
-  }
-  nfits = wave_sum(nfits);
-  if (lane_id() == 0 && nfits) atomicAdd(&ist[kMiFits], nfits);
-  if constexpr (FUSED) mp_partial_and_step(b, p, blk.x, (int)gridDim.x, acc);
-}
-
-// One mapping L-M iteration's correspondences in one launch (small batches): lane per query, the
-// 5-NN search (mp_nn_query, k_mp_nn's) then the fit and row (mp_fit_query, k_mp_fit's) — the fit
-// needs only the lane's own five neighbours — in one-wave workgroups whose 27-entry candidate
-// lists and 27-word Jacobi scratch share one LDS array (the wave's search is over before its fits
-// begin).  Same query -> lane mapping and row order as k_mp_fit, so the sums are k_mp_fit's.
-// FUSED: the partial + last-workgroup step of k_mp_fit<true>.  COUNT: the work counters.
+// One mapping L-M iteration's correspondences in one launch: lane per query, the 5-NN search
+// (knn5_flat, seeded) then the fit and row — the fit needs only the lane's own five neighbours —
+// in one-wave workgroups whose 27-entry candidate lists and 27-word Jacobi scratch share one LDS
+// array (the wave's search is over before its fits begin).  Rows in query order per workgroup.
+// FUSED: the workgroup's partial + the last workgroup's step (mp_store_partial_and_step); else the
+// rows go to q_ok / q_cf for k_mp_iter.  COUNT: the work counters.
 #ifndef LOAM_NNFIT_WPE
 #define LOAM_NNFIT_WPE 4
 #endif
@@ -1845,7 +1748,7 @@ __global__ __launch_bounds__(kMpFitThreads) __attribute__((amdgpu_waves_per_eu(L
   int nfits = 0, work = 0;
   // FUSED: the rows of each pass over the queries are reduce-scattered over the wave at once (no
   // 28 fp64 sums live across the search), the passes' sums added in pass order (one pass per lane
-  // for a VLP-16 stack: the same sums as k_mp_fit<true>)
+  // for a VLP-16 stack)
   double red = 0.0;
   // FUSED: lane 2t's term t of the 28 sums (JᵀJ upper triangle row-major, Jᵀb, rows) as the
   // product of row entries term_x * term_y (mp_row_accum's order; entry 7 = 1 per accepted row)
@@ -3014,48 +2917,19 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
       mark("k_mp_lm_small");
       continue;
     }
-    const int gfit = b.tune.fit_wg > 0 ? std::min(b.tune.fit_wg, kMpFitGridMax) : gq * (kMpQueryThreads / kMpFitThreads);
-    // (round 4: the late iterations, when few instances still run, with 2 / 4 lanes per query
-    // through k_mp_nn<L> measured slower at P = 128: 3.15 -> 3.22 / 3.29 ms/step)
-    if (P <= b.tune.nnfit_max && gfit <= kMpFitGridMax) {  // search + fit (+ step) in one launch
-      const bool fused = P <= b.tune.mp_fused_max;
-      if (fused && prof) hipLaunchKernelGGL((k_mp_nnfit<true, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
-      else if (fused) hipLaunchKernelGGL((k_mp_nnfit<true, false>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
-      else if (prof) hipLaunchKernelGGL((k_mp_nnfit<false, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
-      else hipLaunchKernelGGL((k_mp_nnfit<false, false>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
-      mark("k_mp_nnfit");
-      if (!fused) {
-        if (P <= b.tune.mp_iter_wide_max) hipLaunchKernelGGL(k_mp_iter<1024>, dim3(P), dim3(1024), 0, st, b);
-        else hipLaunchKernelGGL(k_mp_iter<kMpThreads>, dim3(P), dim3(kMpThreads), 0, st, b);
-        mark("k_mp_iter");
-      }
-      continue;
+    const int gfit = std::min(kMpFitGridMax, b.tune.fit_wg > 0 ? b.tune.fit_wg : gq * (kMpQueryThreads / kMpFitThreads));
+    // search + fit (+ step) in one launch (round 3's separate k_mp_nn / k_mp_fit launches, and 2 / 4
+    // lanes per query, measured slower and were removed in round 6)
+    const bool fused = P <= b.tune.mp_fused_max;
+    if (fused && prof) hipLaunchKernelGGL((k_mp_nnfit<true, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+    else if (fused) hipLaunchKernelGGL((k_mp_nnfit<true, false>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+    else if (prof) hipLaunchKernelGGL((k_mp_nnfit<false, true>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+    else hipLaunchKernelGGL((k_mp_nnfit<false, false>), dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
+    mark("k_mp_nnfit");
+    if (!fused) {
+      hipLaunchKernelGGL(k_mp_iter<kMpThreads>, dim3(P), dim3(kMpThreads), 0, st, b);
+      mark("k_mp_iter");
     }
-    const int gnn = b.tune.nn_wg > 0 ? b.tune.nn_wg : gq * (kMpQueryThreads / kMpNnThreads);
-    // L lanes per query for shares of a few hundred problems (the slowest wave is the launch)
-    const int L = P <= b.tune.nn_lanes_maxp ? b.tune.nn_lanes : 1;
-    if (L == 4) {
-      if (prof) hipLaunchKernelGGL((k_mp_nn<true, 4>), dim3(gnn * 4, P), dim3(kMpNnThreads), 0, st, b);
-      else hipLaunchKernelGGL((k_mp_nn<false, 4>), dim3(gnn * 4, P), dim3(kMpNnThreads), 0, st, b);
-    } else if (L == 2) {
-      if (prof) hipLaunchKernelGGL((k_mp_nn<true, 2>), dim3(gnn * 2, P), dim3(kMpNnThreads), 0, st, b);
-      else hipLaunchKernelGGL((k_mp_nn<false, 2>), dim3(gnn * 2, P), dim3(kMpNnThreads), 0, st, b);
-    } else if (prof) {
-      hipLaunchKernelGGL((k_mp_nn<true, 1>), dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
-    } else {
-      hipLaunchKernelGGL((k_mp_nn<false, 1>), dim3(gnn, P), dim3(kMpNnThreads), 0, st, b);
-    }
-    mark("k_mp_nn");
-    if (P <= b.tune.mp_fused_max && gfit <= kMpFitGridMax) {
-      hipLaunchKernelGGL(k_mp_fit<true>, dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
-      mark("k_mp_fit");
-      continue;
-    }
-    hipLaunchKernelGGL(k_mp_fit<false>, dim3(gfit, P), dim3(kMpFitThreads), 0, st, b);
-    mark("k_mp_fit");
-    if (P <= b.tune.mp_iter_wide_max) hipLaunchKernelGGL(k_mp_iter<1024>, dim3(P), dim3(1024), 0, st, b);
-    else hipLaunchKernelGGL(k_mp_iter<kMpThreads>, dim3(P), dim3(kMpThreads), 0, st, b);
-    mark("k_mp_iter");
   }
   hipLaunchKernelGGL(k_mp_lm_end, dim3((P + 255) / 256), dim3(256), 0, st, b);
   // the registration reads only the final pose and the full cloud: beside the insertion with a

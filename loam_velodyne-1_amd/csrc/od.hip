@@ -24,7 +24,7 @@
 
 using namespace loamdev;
 
-// batch-size launch choices (k_od_rows_small / k_od_lm / k_od_rows<true> / k_od_assoc grid): the
+// batch-size launch choices (k_od_rows_small / k_od_rows<true> / k_od_assoc grid): the
 // context's Tuning (engine.hpp), OdBuffers::tune
 // (measured at batch 128: k_od_rows<true> rows + step 0.67 -> 0.62 ms/step, whole step unchanged;
 // 1024 slower)
@@ -1281,8 +1281,8 @@ LOAM_D void od_mom_accum(const OdJf& e, const double (&m)[kOdMom], double (&acc)
 // FUSED: the last workgroup of the problem to finish sums the gq partials (in k_od_step's order)
 // and runs the step itself, instead of a k_od_step launch per iteration.
 constexpr int kOdRowsWpe = 4;  // <= 128 VGPRs with two rows' loads in flight
-// INF: stored rows whose loads are in flight together per lane step (2 for large batches, where
-// occupancy hides the chain; more for small ones, where the lane's chain of iter + 1 loads is the time)
+// INF: stored rows whose loads are in flight together per lane step (2, the one instantiation: 8 for
+// small batches, tuning od_rows_deep_max until round 6, measured no faster and was removed)
 // MOM: the stored rows as the query's fp64 moments (od_mom_add / od_mom_accum; tuning od_moments_min)
 // instead of re-evaluating each (INF unused)
 template <bool FUSED, int INF, bool MOM = false>
@@ -1894,168 +1894,6 @@ __global__ __launch_bounds__(64) void k_od_step(OdBuffers b, int iter, int gq) {
   od_step(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
 }
 
-// One association round's iterations (it0 .. it0 + 4, Q10) of a problem in one workgroup, the 6x6
-// step between them on its first wave: no launch, grid-wide drain or partial hand-off per iteration
-// (at the 8-GPU share the k_od_rows + k_od_step pair cost ~20 us per iteration, mostly latency).
-// Lane q < nq owns query q: its raw point and associated Last points are loaded once per round, and
-// each iteration it stores its new row (:530-583, :653-694).  The Q12 re-evaluation of every stored
-// row at the current transform is spread evenly over the workgroup: lane t sums the rows
-// [t R / NT, (t + 1) R / NT) of R = nq (iter + 1) in (query, iteration) order, recomputing the J
-// factors when its query changes; the fp64 sums are reduced in a fixed order (wave butterflies, then
-// the waves in order).  Needs nq <= NT.
-constexpr int kOdLmThreads = 1024;
-#ifndef LOAM_OD_LM_INFLIGHT
-#define LOAM_OD_LM_INFLIGHT 4
-#endif
-constexpr int kOdLmRowsInFlight = LOAM_OD_LM_INFLIGHT;
-constexpr int kOdJf = 17;  // floats of OdJf
-// dynamic LDS of k_od_lm: per query its raw point and associated Last points (4 float4; t1.w: the
-// association holds) and the J factors at the current transform (17 floats)
-inline size_t od_lm_lds(int cap_q) { return (size_t)cap_q * (4 * sizeof(float4) + kOdJf * sizeof(float)); }
-LOAM_D void od_jf_store(float* d, int s, const OdJf& e) {
-  d[0] = e.e00; d[s] = e.e01; d[2 * s] = e.e02; d[3 * s] = e.e10; d[4 * s] = e.e12; d[5 * s] = e.e20;
-  d[6 * s] = e.e21; d[7 * s] = e.e22; d[8 * s] = e.e30; d[9 * s] = e.e31; d[10 * s] = e.e32; d[11 * s] = e.e40;
-  d[12 * s] = e.e41; d[13 * s] = e.e42; d[14 * s] = e.e50; d[15 * s] = e.e51; d[16 * s] = e.e52;
-}
-LOAM_D OdJf od_jf_load(const float* d, int s) {
-  OdJf e;
-  e.e00 = d[0]; e.e01 = d[s]; e.e02 = d[2 * s]; e.e10 = d[3 * s]; e.e12 = d[4 * s]; e.e20 = d[5 * s];
-  e.e21 = d[6 * s]; e.e22 = d[7 * s]; e.e30 = d[8 * s]; e.e31 = d[9 * s]; e.e32 = d[10 * s]; e.e40 = d[11 * s];
-  e.e41 = d[12 * s]; e.e42 = d[13 * s]; e.e50 = d[14 * s]; e.e51 = d[15 * s]; e.e52 = d[16 * s];
-  return e;
-}
-// the step out of line: its solver's registers are not live beside the row loop's
-__device__ __noinline__ void od_step_call(const OdBuffers& b, int p, int iter, const double* tot, float* AtA, float* AtB,
-                                          float* X, float* lm_ws, int* lm_iws, float* jE, float* jV) {
-  od_step(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
-}
-__global__ __launch_bounds__(kOdLmThreads) void k_od_lm(OdBuffers b, FeatView f, int last_buf, int it0) {
-  const int p = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  int* ist = b.istate + (size_t)p * kOdStateInts;
-  if (!ist[kIsActive] || ist[kIsStop]) return;
-  constexpr int NW = kOdLmThreads / 64;
-  __shared__ double red[NW][28];
-  __shared__ double tot[28];
-  __shared__ float Tsh[6], trig[6];
-  __shared__ int stop_sh;
-  __shared__ float AtA[36], AtB[6], X[6], lm_ws[loamla::kLmWs], jE[6], jV[36];
-  __shared__ int lm_iws[12];
-  extern __shared__ float4 od_lm_dyn[];
-  const int CQ = b.cap_q;
-  float4* qpts = od_lm_dyn;                  // [4][CQ]
-  float* jf = (float*)(od_lm_dyn + 4 * CQ);  // [17][CQ]
-  float* st = b.state + (size_t)p * kOdStateFloats;
-  if (tid < 6) {  // the transform, and the double sin / cos of its angles one per lane
-    Tsh[tid] = st[tid];
-    const float a = st[tid >> 1];
-    trig[tid] = (float)((tid & 1) ? dcos(a) : dsin(a));
-  }
-  const int nc = f.count(p, 0), ns = f.count(p, 2), nq = nc + ns;
-  const size_t lp = (size_t)last_buf * b.P + p;
-  float4* qcf = b.q_cf + (size_t)p * b.max_iter * CQ;
-  int8_t* qok = b.q_ok + (size_t)p * b.max_iter * CQ;
-  if (tid < nq) {
-    float4 t1, t2, t3;
-    const bool has = od_assoc_pts(b, p, tid, nc, lp, t1, t2, t3);
-    t1.w = has ? 1.0f : 0.0f;
-    qpts[tid] = tid < nc ? f.sharp[(size_t)p * f.sharp_stride + tid] : f.flat[(size_t)p * f.flat_stride + (tid - nc)];
-    qpts[CQ + tid] = t1;
-    qpts[2 * CQ + tid] = t2;
-    qpts[3 * CQ + tid] = t3;
-  }
-  __syncthreads();
-  const int it_end = min(it0 + 5, b.max_iter);
-  for (int iter = it0; iter < it_end; ++iter) {
-    LOAM_PH(const unsigned long long pt0 = ph_now();)
-    // lane q: the new row and its query's J factors at the current transform
-    if (tid < nq) {
-      float T[6], tg[6];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        T[k] = Tsh[k];
-        tg[k] = trig[k];
-      }
-      const float4 po = qpts[tid], t1 = qpts[CQ + tid];
-      float4 cf;
-      int ok;
-      od_coeff_from(iter, T, po, tid < nc, t1.w != 0.0f, t1, qpts[2 * CQ + tid], qpts[3 * CQ + tid], cf, ok);
-      qcf[(size_t)iter * CQ + tid] = cf;
-      qok[(size_t)iter * CQ + tid] = (int8_t)ok;
-      const OdJf e = od_jfactors(tg, T, po);
-      od_jf_store(jf + tid, CQ, e);
-    }
-    __syncthreads();
-    LOAM_PH(const unsigned long long pt1 = ph_now();)
-    double acc[28];
-#pragma unroll
-    for (int k = 0; k < 28; ++k) acc[k] = 0.0;
-    const int n_it = iter + 1, R = nq * n_it;
-    int r = (int)((long long)tid * R / kOdLmThreads);
-    const int r1 = (int)((long long)(tid + 1) * R / kOdLmThreads);
-    int qq = r / n_it, it = r - qq * n_it, qe = -1;
-    OdJf e;
-    for (; r < r1; r += kOdLmRowsInFlight) {
-      // the next rows' coefficients, all loads in flight together
-      float4 cv[kOdLmRowsInFlight];
-      int qv[kOdLmRowsInFlight];
-#pragma unroll
-      for (int u = 0; u < kOdLmRowsInFlight; ++u) {
-        qv[u] = qq;
-        cv[u] = r + u < r1 ? qcf[(size_t)it * CQ + qq] : make_float4(0, 0, 0, 0);
-        if (++it == n_it) { it = 0; ++qq; }
-      }
-#pragma unroll
-      for (int u = 0; u < kOdLmRowsInFlight; ++u) {
-        if (r + u < r1) {
-          if (qv[u] != qe) {
-            qe = qv[u];
-            e = od_jf_load(jf + qe, CQ);
-          }
-          od_row_accum(e, cv[u], row_ok(cv[u]), acc);
-        }
-      }
-    }
-    wave_reduce_scatter_28(acc);
-    if ((lane & 1) == 0 && (lane >> 1) < 28) red[w][lane >> 1] = acc[0];
-    __syncthreads();
-    LOAM_PH(const unsigned long long pt2 = ph_now();)
-    if (tid < 28) {
-      double v = red[0][tid];
-#pragma unroll
-      for (int ww = 1; ww < NW; ++ww) v += red[ww][tid];
-      tot[tid] = v;
-    }
-    __syncthreads();
-    LOAM_PH(const unsigned long long pt3 = ph_now();)
-    if (tid < 64) {  // the first wave: the step (od_step writes the state; lane 0 reads its own writes)
-      od_step_call(b, p, iter, tot, AtA, AtB, X, lm_ws, lm_iws, jE, jV);
-      if (tid == 0) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) Tsh[k] = st[k];
-        stop_sh = ist[kIsStop];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (tid < 6) {
-        const float a = Tsh[tid >> 1];
-        trig[tid] = (float)((tid & 1) ? dcos(a) : dsin(a));
-      }
-    }
-    __syncthreads();
-    LOAM_PH(if (tid == 0) {
-      const unsigned long long pt4 = ph_now();
-      atomicAdd(&g_ph_od.sum[1][0], pt1 - pt0);
-      atomicAdd(&g_ph_od.sum[1][1], pt2 - pt1);
-      atomicAdd(&g_ph_od.sum[1][2], pt3 - pt2);
-      atomicAdd(&g_ph_od.sum[1][3], pt4 - pt3);
-      atomicAdd(&g_ph_od.sum[1][4], (unsigned long long)(iter + 1));
-      atomicAdd(&g_ph_od.sum[1][6], 1ull);
-    })
-    if (stop_sh) break;
-  }
-}
-
 // pose accumulation (:830-856) for every problem
 __global__ __launch_bounds__(64) void k_od_fini(OdBuffers b, FeatView f) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2251,10 +2089,7 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
   const int P = b.P;
   auto mark = [&](const char* n) { if (prof) prof->mark(n); };
   hipLaunchKernelGGL(k_od_begin, dim3((P + 255) / 256), dim3(256), 0, st, b, f);
-  // batches of tune.od_lm_min .. od_lm_max problems: each association round's iterations in one k_od_lm
-  // workgroup per problem (the queries must fit its lanes)
   const Tuning& tn = b.tune;
-  const bool lm_round = P >= tn.od_lm_min && P <= tn.od_lm_max && b.cap_q <= kOdLmThreads;
   // one problem (streaming): the whole L-M loop as one persistent launch (tuning od_persist)
   const int gls = P == 1 && tn.od_persist ? od_lm_stream_grid(b.cap_q) : 0;
   if (gls > 0) {
@@ -2282,27 +2117,18 @@ void od_solve(const OdBuffers& b, const FeatView& f, int last_buf, hipStream_t s
         else hipLaunchKernelGGL((k_od_assoc<false, true>), dim3(ga, P), dim3(kAsThreads), 0, st, b, f, last_buf);
       }
       mark("k_od_assoc");
-      if (lm_round) {  // the round's iterations in one workgroup per problem
-        hipLaunchKernelGGL(k_od_lm, dim3(P), dim3(kOdLmThreads), od_lm_lds(b.cap_q), st, b, f, last_buf, it);
-        mark("k_od_lm");
-        it += 4;
-        continue;
-      }
     }
     if (P <= tn.od_small_max) {  // measured: the fused step loses for large batches (its serial tail)
       hipLaunchKernelGGL(k_od_rows_small, dim3(b.gq, P, it + 1), dim3(kOdThreads), 0, st, b, f, last_buf, it);
       mark("k_od_rows");
     } else {
-      const bool deep = P <= tn.od_rows_deep_max;  // more stored rows' loads in flight per lane
       const bool mom = P >= tn.od_moments_min;     // the stored rows as per-query moments (not bit-exact)
       if (P <= tn.od_fused_max) {
         if (mom) hipLaunchKernelGGL((k_od_rows_mom<true>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
-        else if (deep) hipLaunchKernelGGL((k_od_rows<true, 8>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         else hipLaunchKernelGGL((k_od_rows<true, 2>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         mark("k_od_rows");
       } else {
         if (mom) hipLaunchKernelGGL((k_od_rows_mom<false>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
-        else if (deep) hipLaunchKernelGGL((k_od_rows<false, 8>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         else hipLaunchKernelGGL((k_od_rows<false, 2>), dim3(b.gq, P), dim3(kOdThreads), 0, st, b, f, last_buf, it);
         mark("k_od_rows");
         hipLaunchKernelGGL(k_od_step, dim3(P), dim3(64), 0, st, b, it, b.gq);

@@ -45,7 +45,7 @@ class Engine:
         pass
 
     def kernel_times(self):
-        return {"k_mp_nn": (1.0, 10), "k_od_assoc": (0.5, 5)}
+        return {"k_mp_nnfit": (1.0, 10), "k_od_assoc": (0.5, 5)}
 
     def close(self):
         pass

@@ -229,19 +229,12 @@ def _share_run(loam, sg, **tune):
 
 @pytest.mark.parametrize("tune", [
     {"od_fused_max": 0},                     # k_od_rows<false> + k_od_step (the default above 128)
-    {"od_lm_max": 128},                      # k_od_lm: an association round in one workgroup per problem
     {"od_small_max": 128},                   # k_od_rows_small: a workgroup per (queries, stored iteration)
-    {"nnfit_max": 0},                        # k_mp_nn + k_mp_fit<true> (round 3's shapes)
-    {"nnfit_max": 0, "mp_fused_max": 0},     # k_mp_nn + k_mp_fit<false> + k_mp_iter
     {"mp_small_max": 128},                   # k_mp_lm_small: one launch per mapping iteration
-    {"nnfit_max": 0, "nn_lanes": 2},         # k_mp_nn<., L>: L lanes per query, merged 5-lists
-    {"nnfit_max": 0, "nn_lanes": 4},
     {"od_assoc_wg": 16},                     # fewer association waves per problem (queries looped)
-    {"od_rows_deep_max": 128},               # k_od_rows<., 8>: eight stored rows' loads in flight
-    {"od_rows_deep_max": 128, "od_fused_max": 128},
+    {"fit_wg": 7},                           # fewer k_mp_nnfit workgroups per problem (queries looped)
     {"mp_fused_max": 0},                     # k_mp_nnfit<false> + k_mp_iter
     {"graph": 1},                            # the step captured as a HIP graph and replayed
-    {"mp_fused_max": 0, "mp_iter_wide_max": 128},  # k_mp_iter<1024>
     {"vg_merge": 0},                         # the cube VoxelGrid cascade alone (no k_vg_merge)
     {"vg_split": 3},                         # stack segments beyond 2048 points split into key-range buckets
     {"vg_split": 0},                         # ... none split (k_vg_big beyond the LDS kernels)
@@ -278,7 +271,7 @@ def test_tuning_rejects_unknown(loam):
     with pytest.raises(Exception):
         e.set_tuning(no_such_key=1)
     with pytest.raises(Exception):
-        e.set_tuning(nn_lanes=3)
+        e.set_tuning(vg_split=4)
     e.close()
 
 

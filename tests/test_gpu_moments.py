@@ -124,8 +124,7 @@ def test_moments_8gpu_share_fused(loam, oc, sg):
     assert np.abs(od - od_o).max() <= TOL and np.abs(aft - aft_o).max() <= TOL
 
 
-@pytest.mark.parametrize("tune", [{"od_fused_max": 0}, {"step_pipe": 0, "sr_ahead": 0}, {"graph": 1},
-                                  {"od_rows_deep_max": 128}],
+@pytest.mark.parametrize("tune", [{"od_fused_max": 0}, {"step_pipe": 0, "sr_ahead": 0}, {"graph": 1}],
                          ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_moments_launch_choices_at_8gpu_share(loam, sg, tune):
     """the moments' launch choices compute the same sums in the same order: the fused rows kernel

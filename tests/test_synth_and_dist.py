@@ -91,7 +91,7 @@ def test_bench_spawns_two_ranks_gloo(sg, split):
     assert out["gathered"]["sha1"] == _expected_sha(sg, 0, 2 * per)
     other = out["strong" if split == "weak" else "weak"]
     assert other["global_batch"] == 2 * other_per and other["problems_per_gpu"] == other_per
-    assert out["value"] > 0 and out["roofline"]["kernel"] == "k_mp_nn"
+    assert out["value"] > 0 and out["roofline"]["kernel"] == "k_mp_nnfit"
 
 
 def test_bench_single_gpu_share_child(sg):

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of launch choices (loam_set_tuning) at a batch size, one library: for each argument
 # ("key=value,key=value" or "default") a short bench line with the per-kernel ms/step.
-#   BATCH=128 tools/ab_share.sh default od_lm_max=128 od_fused_max=128
+#   BATCH=128 tools/ab_share.sh default od_fused_max=0 mp_fused_max=0
 # Outputs gpurun_out/ab_<BATCH>_<choice>.json; prints one summary line per choice.
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out

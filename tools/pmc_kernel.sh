@@ -5,7 +5,7 @@ R=$GRAFT_REPO_ROOT
 RX=${1:-k_sr_select}
 TAG=${2:-k}
 shift 2 2>/dev/null
-EXTRA=("$@")  # further bench.py arguments (e.g. --tune=nnfit_max=0 --batch 128 --global-batch 128)
+EXTRA=("$@")  # further bench.py arguments (e.g. --tune=mp_fused_max=0 --batch 128 --global-batch 128)
 export TMPDIR=/tmp && cd /tmp && \
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS \
   --kernel-include-regex "$RX" --output-format csv -d $R/gpurun_out/pmc_${TAG}_a -o a -- \

@@ -5,7 +5,7 @@ R=$GRAFT_REPO_ROOT
 RX=${1:-k_mp_nn}
 TAG=${2:-k}
 shift 2 2>/dev/null
-EXTRA=("$@")  # further bench.py arguments (e.g. --tune=nnfit_max=0 --batch 128 --global-batch 128)
+EXTRA=("$@")  # further bench.py arguments (e.g. --tune=mp_fused_max=0 --batch 128 --global-batch 128)
 export TMPDIR=/tmp && cd /tmp && \
 timeout -s KILL 120 rocprofv3 --pmc TA_BUSY_avr TA_TOTAL_WAVEFRONTS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE \
   --kernel-include-regex "$RX" --output-format csv -d $R/gpurun_out/pmc_${TAG}_ta -o ta -- \
