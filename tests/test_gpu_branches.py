@@ -160,6 +160,43 @@ def test_batch_1024_parity(loam, oc, sg):
     np.testing.assert_array_equal(aft[-64:], aft2)
 
 
+def test_batch_size_independence(loam, oc, sg):
+    """a problem's poses do not depend on the batch it runs in: the same problems in batches of 257,
+    129, 65, 64, 63 and 5 — across every launch-shape boundary by batch size (od_small_max 63,
+    od_moments_min / step_pipe / sr_ahead / od_sel_min 64, od_fused_max 128, mp_small_max 4) — with
+    the reference's row accumulation (od_moments_min above the batch) give the same poses bit for
+    bit, and the batch's last problem equals the oracle"""
+    sizes = (257, 129, 65, 64, 63, 5)
+    prevs, curs = sg.batch_problems(sizes[0], base_seed=2100)
+    ref = None
+    for P in sizes:
+        e = loam.Engine()
+        e.set_tuning(od_moments_min=EXACT_ROWS)
+        e.batch_upload(prevs[:P], curs[:P])
+        e.batch_run()
+        od, aft, _ = e.batch_download()
+        e.close()
+        if ref is None:
+            ref = (od, aft)
+        np.testing.assert_array_equal(od, ref[0][:P], err_msg=f"P={P}")
+        np.testing.assert_array_equal(aft, ref[1][:P], err_msg=f"P={P}")
+        od_o, aft_o, _ = oc.problem(prevs[P - 1], curs[P - 1])
+        assert max(np.abs(od[P - 1] - od_o).max(), np.abs(aft[P - 1] - aft_o).max()) <= POSE_TOL, P
+    # the default accumulation of batches >= 64 (per-query moments): per-problem sums as well, so
+    # the same bits at every size that takes it
+    ref = None
+    for P in (257, 129, 65, 64):
+        e = loam.Engine()
+        e.batch_upload(prevs[:P], curs[:P])
+        e.batch_run()
+        od, aft, _ = e.batch_download()
+        e.close()
+        if ref is None:
+            ref = (od, aft)
+        np.testing.assert_array_equal(od, ref[0][:P], err_msg=f"moments P={P}")
+        np.testing.assert_array_equal(aft, ref[1][:P], err_msg=f"moments P={P}")
+
+
 def test_batch_8gpu_share_parity(loam, oc, sg):
     """config 4's strong split on 8 GPUs: the last rank's share (problems 896..1023 of the bench's
     batch, bench.py --split strong) as one 128-problem batch — the fused fit + rows + step mapping
