@@ -363,6 +363,31 @@ def test_capacity_and_empty_errors(loam, sg):
     assert ei.value.code == loam.LOAM_E_INVAL
 
 
+def test_batch_empty_and_tiny_sweeps(loam, oc, sg):
+    """a batch with a sweep of no finite point fails as the node call does (LOAM_E_INVAL at the
+    download) and leaves the context usable; a batch with a 300-point sweep (most rings empty, few or
+    no features) runs through every batch kernel and equals the oracle"""
+    prevs, curs = sg.batch_problems(8, base_seed=4100)
+    bad = list(curs)
+    bad[2] = np.full((100, 4), np.nan, np.float32)
+    e = loam.Engine()
+    e.batch_upload(prevs, bad)
+    e.batch_run()
+    with pytest.raises(loam.LoamError) as ei:
+        e.batch_download()
+    assert ei.value.code == loam.LOAM_E_INVAL
+    tiny = list(prevs)
+    tiny[5] = prevs[5][:300]
+    e.batch_upload(tiny, curs)
+    e.batch_run()
+    od, aft, _ = e.batch_download()
+    e.close()
+    assert np.all(np.isfinite(od)) and np.all(np.isfinite(aft))
+    for i in (0, 5, 7):
+        od_o, aft_o, _ = oc.problem(tiny[i], curs[i])
+        assert max(np.abs(od[i] - od_o).max(), np.abs(aft[i] - aft_o).max()) <= POSE_TOL, i
+
+
 def test_maintenance_chain(loam, oc, sg):
     prev, cur = sg.single_problem(0)
     e = loam.Engine()
