@@ -45,7 +45,7 @@ struct Tuning {
                            // with the register reduce-scatter, 15.31 -> 15.23 with the LDS row sums)
   int od_assoc_wg = 0;     // k_od_assoc query waves (workgroups) per problem (batches, P >= 64; 0: the query
                            // capacity / 9, i.e. 64 for VLP-16, 256 for HDL-64E)
-  int fit_wg = 0;          // k_mp_nnfit workgroups per problem (0: about one pass over a VLP-16 stack; <= 256)
+  int fit_wg = 0;          // k_mp_nnfit workgroups per problem (0: one pass over a VLP-16 stack, two for P >= 512; <= 256)
   int graph = 0;           // loam_batch_run replays the step as a captured HIP graph
   int vg_merge = 1;        // the cubes' VoxelGrid merges an old sorted prefix with the appended tail
                            // (k_vg_merge; config 3's big cubes: 95 -> 50 us per mapping frame)

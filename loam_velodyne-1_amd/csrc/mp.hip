@@ -2917,7 +2917,10 @@ void mp_frame(MpBuffers& b, const MpInput& in, hipStream_t st, Prof* prof, bool 
       mark("k_mp_lm_small");
       continue;
     }
-    const int gfit = std::min(kMpFitGridMax, b.tune.fit_wg > 0 ? b.tune.fit_wg : gq * (kMpQueryThreads / kMpFitThreads));
+    // (P >= 512: 64 workgroups, two passes per lane over a VLP-16 stack; round 6 at 1024 problems:
+    // 12.28-12.32 -> 12.20-12.23 ms/step against 96; at 128 the one-pass 96 stays best)
+    const int gfit_auto = P >= 512 ? 64 : gq * (kMpQueryThreads / kMpFitThreads);
+    const int gfit = std::min(kMpFitGridMax, b.tune.fit_wg > 0 ? b.tune.fit_wg : gfit_auto);
     // search + fit (+ step) in one launch (round 3's separate k_mp_nn / k_mp_fit launches, and 2 / 4
     // lanes per query, measured slower and were removed in round 6)
     const bool fused = P <= b.tune.mp_fused_max;
