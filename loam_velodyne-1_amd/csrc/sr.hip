@@ -771,7 +771,7 @@ struct SelShared {
 #endif
 // member gathers in flight per step of a voxel's mean in ring_vg
 #ifndef LOAM_VG_GATHER
-#define LOAM_VG_GATHER 8
+#define LOAM_VG_GATHER 4  // (round 6: 8 -> 4, k_sr_select 1.34-1.35 -> 1.29 ms/step at 1024, 0.220 -> 0.215 at 128)
 #endif
 constexpr int kVgGather = LOAM_VG_GATHER;
 #ifndef LOAM_RINGVG_HOLD
