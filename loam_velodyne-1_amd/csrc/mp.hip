@@ -2161,7 +2161,7 @@ __global__ __launch_bounds__(kMpQueryThreads) void k_mp_lm_stream(MpBuffers b) {
   const MpNnCtx c = mp_nn_ctx(b, p);
   constexpr int L = kMpNnLanes, QPB = kMpQueryThreads / L;
   const int sub = tid % L;
-  const unsigned long long tag0 = sh_epoch << 8;
+  const unsigned long long tag0 = sh_epoch << 16;  // (iterations + 1 <= 1001 < 2^16: loam_create bounds max_iter)
   int nfits = 0;
   for (int it = 0; it < b.max_iter; ++it) {
     const bool first = S.iters == 0;

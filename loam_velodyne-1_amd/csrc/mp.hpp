@@ -157,7 +157,7 @@ struct MpBuffers {
   double* part = nullptr;     // [P][kMpSmallGrid][28] k_mp_lm_small's per-workgroup JᵀJ | Jᵀb | rows
   int* done = nullptr;        // [P] its workgroups finished (the last one runs the step)
   // the persistent one-instance L-M (k_mp_lm_stream): per workgroup and iteration parity its partial
-  // sums, per workgroup its publication word (epoch << 8 | iteration + 1), the launch epoch
+  // sums, per workgroup its publication word (epoch << 16 | iteration + 1), the launch epoch
   // (advanced by k_mp_lm_begin)
   double* ls_part = nullptr;              // [2][kMpSmallGrid][28]
   unsigned long long* ls_flag = nullptr;  // [kMpSmallGrid]

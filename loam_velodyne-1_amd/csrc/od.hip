@@ -1739,7 +1739,7 @@ __global__ __launch_bounds__(kOdLsThreads) void k_od_lm_stream(OdBuffers b, Feat
   const int Wt = G * NW;                 // association waves: wave (g, w) takes queries g NW + w + k Wt
   const int nloc = nq > g * NW ? ((nq - g * NW - 1) / Wt + 1) * NW : 0;  // (an upper bound; q < nq tested)
   float4* qcf = b.q_cf;
-  const unsigned long long tag0 = sh_epoch << 8;
+  const unsigned long long tag0 = sh_epoch << 16;  // (iterations + 1 <= 1001 < 2^16: loam_create bounds max_iter)
   int wpts = 0, wbox = 0;
   __syncthreads();
   for (int it = 0; it < b.max_iter; ++it) {

@@ -126,7 +126,7 @@ struct OdBuffers {
   double* part = nullptr;     // [P][gq][28] per-workgroup JᵀJ | Jᵀb | rows
   int* done = nullptr;        // [P] workgroups of k_od_rows finished (the last one runs the step)
   // the persistent one-problem L-M (k_od_lm_stream): per workgroup and iteration parity its partial
-  // sums, per workgroup its publication word (epoch << 8 | iteration + 1), and the launch epoch
+  // sums, per workgroup its publication word (epoch << 16 | iteration + 1), and the launch epoch
   // (advanced by k_od_begin, so a replayed graph gets a fresh one)
   double* ls_part = nullptr;              // [2][kOdLsMaxG][28]
   unsigned long long* ls_flag = nullptr;  // [kOdLsMaxG]
