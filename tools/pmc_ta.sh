@@ -2,7 +2,7 @@
 # Texture-address / L1 / L2 counters of one kernel family (diagnostic), one PMC pass over a 1-step
 # bench at batch 1024.   tools/pmc_ta.sh <kernel-regex> <tag>
 R=$GRAFT_REPO_ROOT
-RX=${1:-k_mp_nn}
+RX=${1:-k_mp_nnfit}
 TAG=${2:-k}
 shift 2 2>/dev/null
 EXTRA=("$@")  # further bench.py arguments (e.g. --tune=mp_fused_max=0 --batch 128 --global-batch 128)

@@ -41,7 +41,7 @@ def load(path):
         k = short(r["Kernel_Name"])
         inst[k][0] += float(r["Counter_Value"])
         inst[k][1] += 1
-    # kernels with a profiling (COUNT) variant (k_mp_nn<true>, k_od_assoc<true, ...>): the variant
+    # kernels with a profiling (COUNT) variant (k_mp_nnfit<., true>, k_od_assoc<true, ...>): the variant
     # launches in place of the plain one in the bench's profiling pass, so both are dispatches of
     # the same launch: every dispatch of either counts, averaged together
     counted = {k.split("<")[0] for k in inst if "<true" in k}
